@@ -1,0 +1,93 @@
+// Shared device/host helpers for librgbac_hip.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/rgbac.h"
+
+namespace rgbac {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+// bf16 storage is carried as raw 16-bit words.
+struct bf16_t { uint16_t u; };
+
+__device__ __forceinline__ float bf2f(uint16_t u) {
+  return __uint_as_float(((uint32_t)u) << 16);
+}
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  // round to nearest even (inputs here are finite)
+  uint32_t u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// Element access for the two storage types.
+template <typename T> struct Elem;
+template <> struct Elem<float> {
+  static constexpr int EPV = 4;  // elements per 16-byte chunk
+  __device__ static float ld(const float* p) { return *p; }
+  __device__ static void st(float* p, float v) { *p = v; }
+  __device__ static void ld4(const float* p, float (&v)[4]) {
+    float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  }
+  __device__ static void st4(float* p, const float (&v)[4]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+template <> struct Elem<bf16_t> {
+  static constexpr int EPV = 8;
+  __device__ static float ld(const bf16_t* p) { return bf2f(p->u); }
+  __device__ static void st(bf16_t* p, float v) { p->u = f2bf(v); }
+  __device__ static void ld4(const bf16_t* p, float (&v)[4]) {
+    uint2 t = *reinterpret_cast<const uint2*>(p);
+    v[0] = bf2f(t.x & 0xFFFF); v[1] = bf2f(t.x >> 16);
+    v[2] = bf2f(t.y & 0xFFFF); v[3] = bf2f(t.y >> 16);
+  }
+  __device__ static void st4(bf16_t* p, const float (&v)[4]) {
+    uint2 t;
+    t.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    t.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    *reinterpret_cast<uint2*>(p) = t;
+  }
+};
+
+// ---------------------------------------------------------------- host side
+void set_error(const std::string& msg);
+int check_launch(const char* what);
+
+#define RGBAC_REQUIRE(cond, msg)                                   \
+  do {                                                             \
+    if (!(cond)) {                                                 \
+      ::rgbac::set_error(std::string(__func__) + ": " + (msg));    \
+      return RGBAC_E_ARG;                                          \
+    }                                                              \
+  } while (0)
+
+constexpr int kReduceThreads = 256;
+constexpr int kReduceMaxBlocks = 1024;
+inline int reduce_blocks(int64_t n) {
+  int64_t b = (n + kReduceThreads * 4 - 1) / (kReduceThreads * 4);
+  if (b < 1) b = 1;
+  if (b > kReduceMaxBlocks) b = kReduceMaxBlocks;
+  return (int)b;
+}
+
+// fp64 block reduction of one value per thread (blockDim == kReduceThreads).
+__device__ __forceinline__ double block_sum_f64(double v, double* smem) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) smem[wave] = v;
+  __syncthreads();
+  double r = 0.0;
+  if (threadIdx.x == 0) {
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) r += smem[i];
+  }
+  __syncthreads();
+  return r;  // valid on thread 0
+}
+
+}  // namespace rgbac

@@ -1,0 +1,395 @@
+// Coalesced HBM-bound kernels around the conv/attention engine:
+//   * Gaussian conditional likelihood + quantise + bits (per channel slice),
+//   * factorized-prior (EntropyBottleneck) likelihood + z quantise,
+//   * masked MSE / bpp finalisation (deterministic two-level fp64 sums),
+//   * SupplyMaskToTransform pyramid (+ reconmask round to 1/255),
+//   * NCHW <-> NHWC conversion at the model boundary,
+//   * the library's error plumbing.
+#include <cmath>
+#include <cstdio>
+
+#include "common.h"
+
+namespace rgbac {
+
+static thread_local std::string g_last_error;
+void set_error(const std::string& msg) { g_last_error = msg; }
+int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error(std::string(what) + ": " + hipGetErrorString(e));
+    return RGBAC_E_LAUNCH;
+  }
+  return RGBAC_OK;
+}
+
+// compressai GaussianConditional._standardized_cumulative: 0.5*erfc(-(2^-0.5) * t)
+__device__ __forceinline__ float std_cum(float t) {
+  return 0.5f * erfcf(-0.70710678118654752440f * t);
+}
+__device__ __forceinline__ float bits_of(float lik) {
+  // clamp(-1.0 * log(lik + 1e-10) / log(2.0), 0, 50)   (AutoEncoderRGB_Journal.py:280)
+  float b = (-1.0f * logf(lik + 1e-10f)) / 0.69314718055994530942f;
+  return fminf(fmaxf(b, 0.0f), 50.0f);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+gaussian_slice_kernel(long long n, int nch, const T* __restrict__ y, long long ldy,
+                      const T* __restrict__ mu, long long ldmu, const T* __restrict__ sc,
+                      long long lds, const float* __restrict__ noise, T* __restrict__ hat,
+                      long long ldh, float* __restrict__ likout, double* __restrict__ partial) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+    const long long pix = e / nch;
+    const int ch = (int)(e - pix * nch);
+    const float yv = Elem<T>::ld(y + pix * ldy + ch);
+    const float mv = Elem<T>::ld(mu + pix * ldmu + ch);
+    const float sv = Elem<T>::ld(sc + pix * lds + ch);
+    const float qh = rintf(yv - mv) + mv;              // ste_round(y - mu) + mu (forward value)
+    Elem<T>::st(hat + pix * ldh + ch, qh);
+    const float xin = noise ? yv + noise[e] : qh;      // quantize("noise" | "dequantize")
+    const float v = fabsf(xin - mv);
+    const float s = fmaxf(sv, 0.11f);                  // lower_bound_scale
+    const float up = std_cum((0.5f - v) / s);
+    const float lo = std_cum((-0.5f - v) / s);
+    const float lik = fmaxf(up - lo, 1e-9f);           // likelihood_lower_bound
+    if (likout) likout[e] = lik;
+    acc += (double)bits_of(lik);
+  }
+  const double s = block_sum_f64(acc, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+// EntropyBottleneck param block per channel (fp32, 64 floats):
+//  [0:3) sp(M0) [3:12) sp(M1) [12:21) sp(M2) [21:30) sp(M3) [30:33) sp(M4)
+//  [33:36) b0 [36:39) b1 [39:42) b2 [42:45) b3 [45] b4
+//  [46:49) tanh(f0) [49:52) tanh(f1) [52:55) tanh(f2) [55:58) tanh(f3) [58] median
+constexpr int kEbStride = 64;
+
+__device__ __forceinline__ float eb_logits(const float* P, float x) {
+  float t[3], u[3];
+#pragma unroll
+  for (int o = 0; o < 3; ++o) {
+    float a = P[0 + o] * x;
+    a = a + P[33 + o];
+    t[o] = a + P[46 + o] * tanhf(a);
+  }
+#pragma unroll
+  for (int layer = 0; layer < 3; ++layer) {
+    const float* Mx = P + 3 + 9 * layer;
+    const float* bx = P + 36 + 3 * layer;
+    const float* fx = P + 49 + 3 * layer;
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      float a = Mx[o * 3 + 0] * t[0];
+      a = fmaf(Mx[o * 3 + 1], t[1], a);
+      a = fmaf(Mx[o * 3 + 2], t[2], a);
+      a = a + bx[o];
+      u[o] = a + fx[o] * tanhf(a);
+    }
+#pragma unroll
+    for (int o = 0; o < 3; ++o) t[o] = u[o];
+  }
+  float a = P[30] * t[0];
+  a = fmaf(P[31], t[1], a);
+  a = fmaf(P[32], t[2], a);
+  return a + P[45];
+}
+__device__ __forceinline__ float sigm(float v) { return 1.0f / (1.0f + expf(-v)); }
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+eb_forward_kernel(long long n, int C, const T* __restrict__ z, long long ldz,
+                  const float* __restrict__ params, const float* __restrict__ noise,
+                  T* __restrict__ zhat, long long ldh, float* __restrict__ likout,
+                  double* __restrict__ partial) {
+  __shared__ double red[4];
+  double acc = 0.0;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+    const long long pix = e / C;
+    const int ch = (int)(e - pix * C);
+    const float* P = params + (size_t)ch * kEbStride;
+    const float med = P[58];
+    const float zv = Elem<T>::ld(z + pix * ldz + ch);
+    const float q = rintf(zv - med) + med;
+    Elem<T>::st(zhat + pix * ldh + ch, q);
+    const float xin = noise ? zv + noise[e] : q;
+    const float lo = eb_logits(P, xin - 0.5f);
+    const float up = eb_logits(P, xin + 0.5f);
+    const float lik = fmaxf(sigm(up) - sigm(lo), 1e-9f);
+    if (likout) likout[e] = lik;
+    acc += (double)bits_of(lik);
+  }
+  const double s = block_sum_f64(acc, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+
+// Per-(image, block) partial sums of the reconstruction error.
+//   mode 0: masked (AutoEncoderRGB_Journal.py:36-64): se = sum m*(x-xh)^2 over 3 channels,
+//           cnt = 3 * #(mask > 0)
+//   mode 1: plain (AutoEncoderMask_Journal.py:309): se = sum (xh - x)^2, cnt = #elements
+template <typename T>
+__global__ void __launch_bounds__(256)
+mse_partial_kernel(int mode, int cx, int HW, const float* __restrict__ x, const T* __restrict__ xh,
+                   long long ldh, const float* __restrict__ mask, double* __restrict__ part) {
+  __shared__ double red[4];
+  const int b = blockIdx.y;
+  double se = 0.0, cnt = 0.0;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += gridDim.x * 256) {
+    const long long pix = (long long)b * HW + p;
+    float m = 1.0f;
+    if (mode == 0) m = mask[pix] > 0.0f ? 1.0f : 0.0f;
+    for (int c = 0; c < cx; ++c) {
+      const float xv = x[((long long)b * cx + c) * HW + p];
+      const float hv = Elem<T>::ld(xh + pix * ldh + c);
+      const float dlt = mode == 0 ? (xv * m - hv * m) : (hv - xv);
+      se += (double)(dlt * dlt);
+    }
+    cnt += (double)(m * cx);
+  }
+  const double s0 = block_sum_f64(se, red);
+  const double s1 = block_sum_f64(cnt, red);
+  if (threadIdx.x == 0) {
+    part[((size_t)b * gridDim.x + blockIdx.x) * 2 + 0] = s0;
+    part[((size_t)b * gridDim.x + blockIdx.x) * 2 + 1] = s1;
+  }
+}
+
+__global__ void __launch_bounds__(256)
+finalize_kernel(int mode, int batch, int nblk, double npix, const double* __restrict__ part,
+                const double* __restrict__ yb, int ny, const double* __restrict__ zb, int nz,
+                float* __restrict__ out) {
+  __shared__ double red[4];
+  double ys = 0.0, zs = 0.0;
+  for (int i = threadIdx.x; i < ny; i += 256) ys += yb[i];
+  for (int i = threadIdx.x; i < nz; i += 256) zs += zb[i];
+  ys = block_sum_f64(ys, red);
+  zs = block_sum_f64(zs, red);
+  double mse_acc = 0.0, se_all = 0.0, cnt_all = 0.0;
+  for (int b = 0; b < batch; ++b) {
+    double se = 0.0, cnt = 0.0;
+    for (int i = threadIdx.x; i < nblk; i += 256) {
+      se += part[((size_t)b * nblk + i) * 2 + 0];
+      cnt += part[((size_t)b * nblk + i) * 2 + 1];
+    }
+    se = block_sum_f64(se, red);
+    cnt = block_sum_f64(cnt, red);
+    if (threadIdx.x == 0) {
+      // per-image mean: torch.div(mse, clamp(num_unmasked, min=1)) in fp32
+      const float sef = (float)se, cf = fmaxf((float)cnt, 1.0f);
+      mse_acc += (double)(sef / cf);
+      se_all += se;
+      cnt_all += cnt;
+    }
+  }
+  if (threadIdx.x == 0) {
+    float mse;
+    if (mode == 0)
+      mse = (float)(mse_acc / batch);
+    else
+      mse = (float)(se_all / cnt_all);
+    const float ybits = (float)ys, zbits = (float)zs;
+    const float yb_pp = ybits / (float)npix, zb_pp = zbits / (float)npix;
+    out[0] = mse;
+    out[1] = yb_pp + zb_pp;
+    out[2] = yb_pp;
+    out[3] = zb_pp;
+  }
+}
+
+__global__ void round255_kernel(long long n, const float* __restrict__ in, float* __restrict__ out) {
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    out[i] = rintf(in[i] * 255.0f) / 255.0f;
+  }
+}
+
+// AvgPool2d(3, stride=2, padding=1, count_include_pad=True) on [B,H,W]
+__global__ void avgpool3s2_kernel(int batch, int H, int W, int Ho, int Wo,
+                                  const float* __restrict__ in, float* __restrict__ out) {
+  const long long n = (long long)batch * Ho * Wo;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const int ox = (int)(i % Wo);
+    const long long t = i / Wo;
+    const int oy = (int)(t % Ho);
+    const int b = (int)(t / Ho);
+    float s = 0.f;
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int iy = 2 * oy + dy;
+      if (iy < 0 || iy >= H) continue;
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int ix = 2 * ox + dx;
+        if (ix < 0 || ix >= W) continue;
+        s += in[((long long)b * H + iy) * W + ix];
+      }
+    }
+    out[i] = s / 9.0f;
+  }
+}
+
+template <typename T>
+__global__ void nchw_to_nhwc_kernel(int batch, int C, int HW, const float* __restrict__ src,
+                                    T* __restrict__ dst, long long ldc) {
+  const long long n = (long long)batch * HW * ldc;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const long long pix = i / ldc;
+    const int c = (int)(i - pix * ldc);
+    const int b = (int)(pix / HW);
+    const int p = (int)(pix - (long long)b * HW);
+    const float v = c < C ? src[((long long)b * C + c) * HW + p] : 0.0f;
+    Elem<T>::st(dst + i, v);
+  }
+}
+
+template <typename T>
+__global__ void nhwc_to_nchw_kernel(int batch, int C, int HW, const T* __restrict__ src,
+                                    long long ldc, float* __restrict__ dst) {
+  const long long n = (long long)batch * C * HW;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const int p = (int)(i % HW);
+    const long long t = i / HW;
+    const int c = (int)(t % C);
+    const int b = (int)(t / C);
+    dst[i] = Elem<T>::ld(src + ((long long)b * HW + p) * ldc + c);
+  }
+}
+
+static int grid_for(long long n) {
+  long long g = (n + 255) / 256;
+  if (g > 4096) g = 4096;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace rgbac
+
+using namespace rgbac;
+
+extern "C" int rgbac_abi_version(void) { return RGBAC_ABI_VERSION; }
+extern "C" const char* rgbac_last_error(void) { return g_last_error.c_str(); }
+extern "C" int rgbac_reduce_blocks(int64_t n) { return reduce_blocks(n); }
+
+extern "C" int rgbac_gaussian_slice(int dtype, int64_t npix, int nch, const void* y, int64_t ldy,
+                                    const void* mu, int64_t ldmu, const void* scale, int64_t lds,
+                                    const float* noise, void* out_hat, int64_t ldh, float* lik,
+                                    double* partial, void* stream) {
+  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(npix > 0 && nch > 0, "empty slice");
+  RGBAC_REQUIRE(y && mu && scale && out_hat && partial, "null pointer");
+  const long long n = npix * (long long)nch;
+  const int g = reduce_blocks(n);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == RGBAC_F32)
+    hipLaunchKernelGGL(gaussian_slice_kernel<float>, dim3(g), dim3(256), 0, st, n, nch,
+                       (const float*)y, ldy, (const float*)mu, ldmu, (const float*)scale, lds,
+                       noise, (float*)out_hat, ldh, lik, partial);
+  else
+    hipLaunchKernelGGL(gaussian_slice_kernel<bf16_t>, dim3(g), dim3(256), 0, st, n, nch,
+                       (const bf16_t*)y, ldy, (const bf16_t*)mu, ldmu, (const bf16_t*)scale, lds,
+                       noise, (bf16_t*)out_hat, ldh, lik, partial);
+  return check_launch("gaussian_slice_kernel");
+}
+
+extern "C" int rgbac_eb_forward(int dtype, int64_t npix, int channels, const void* z, int64_t ldz,
+                                const float* params, const float* noise, void* z_hat, int64_t ldh,
+                                float* lik, double* partial, void* stream) {
+  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(npix > 0 && channels > 0, "empty tensor");
+  RGBAC_REQUIRE(z && params && z_hat && partial, "null pointer");
+  const long long n = npix * (long long)channels;
+  const int g = reduce_blocks(n);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == RGBAC_F32)
+    hipLaunchKernelGGL(eb_forward_kernel<float>, dim3(g), dim3(256), 0, st, n, channels,
+                       (const float*)z, ldz, params, noise, (float*)z_hat, ldh, lik, partial);
+  else
+    hipLaunchKernelGGL(eb_forward_kernel<bf16_t>, dim3(g), dim3(256), 0, st, n, channels,
+                       (const bf16_t*)z, ldz, params, noise, (bf16_t*)z_hat, ldh, lik, partial);
+  return check_launch("eb_forward_kernel");
+}
+
+extern "C" int rgbac_finalize(int dtype, int mode, int batch, int cx, int h, int w, const float* x,
+                              const void* x_hat, int64_t ldh, const float* mask,
+                              const double* ybits, int ny, const double* zbits, int nz,
+                              double* scratch, float* out, void* stream) {
+  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(mode == 0 || mode == 1, "mode");
+  RGBAC_REQUIRE(batch > 0 && cx > 0 && h > 0 && w > 0, "shape");
+  RGBAC_REQUIRE(x && x_hat && scratch && out && ybits && zbits, "null pointer");
+  RGBAC_REQUIRE(mode == 1 || mask, "masked mse needs the mask");
+  const int HW = h * w;
+  const int nblk = 64;  // scratch must hold batch * 64 * 2 doubles
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == RGBAC_F32)
+    hipLaunchKernelGGL(mse_partial_kernel<float>, dim3(nblk, batch), dim3(256), 0, st, mode, cx,
+                       HW, x, (const float*)x_hat, ldh, mask, scratch);
+  else
+    hipLaunchKernelGGL(mse_partial_kernel<bf16_t>, dim3(nblk, batch), dim3(256), 0, st, mode, cx,
+                       HW, x, (const bf16_t*)x_hat, ldh, mask, scratch);
+  int rc = check_launch("mse_partial_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, st, mode, batch, nblk,
+                     (double)batch * HW, scratch, ybits, ny, zbits, nz, out);
+  return check_launch("finalize_kernel");
+}
+
+extern "C" int rgbac_mask_pyramid(int batch, int h, int w, const float* alpha, int round255,
+                                  float* rounded, int levels, float* const* outs, void* stream) {
+  RGBAC_REQUIRE(batch > 0 && h > 0 && w > 0 && alpha, "shape");
+  RGBAC_REQUIRE(levels >= 0 && levels <= 8, "levels");
+  RGBAC_REQUIRE(!round255 || rounded, "round255 needs an output buffer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const float* cur = alpha;
+  if (round255) {
+    const long long n = (long long)batch * h * w;
+    hipLaunchKernelGGL(round255_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, alpha, rounded);
+    int rc = check_launch("round255_kernel");
+    if (rc) return rc;
+    cur = rounded;
+  }
+  int H = h, W = w;
+  for (int l = 0; l < levels; ++l) {
+    RGBAC_REQUIRE(outs && outs[l], "null pyramid output");
+    const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+    const long long n = (long long)batch * Ho * Wo;
+    hipLaunchKernelGGL(avgpool3s2_kernel, dim3(grid_for(n)), dim3(256), 0, st, batch, H, W, Ho,
+                       Wo, cur, outs[l]);
+    int rc = check_launch("avgpool3s2_kernel");
+    if (rc) return rc;
+    cur = outs[l];
+    H = Ho;
+    W = Wo;
+  }
+  return RGBAC_OK;
+}
+
+extern "C" int rgbac_nchw_to_nhwc(int dtype, int batch, int c, int h, int w, const float* src,
+                                  void* dst, int64_t ldc, void* stream) {
+  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(batch > 0 && c > 0 && h > 0 && w > 0 && ldc >= c && src && dst, "shape");
+  const long long n = (long long)batch * h * w * ldc;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == RGBAC_F32)
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, batch, c,
+                       h * w, src, (float*)dst, ldc);
+  else
+    hipLaunchKernelGGL(nchw_to_nhwc_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, batch, c,
+                       h * w, src, (bf16_t*)dst, ldc);
+  return check_launch("nchw_to_nhwc_kernel");
+}
+
+extern "C" int rgbac_nhwc_to_nchw(int dtype, int batch, int c, int h, int w, const void* src,
+                                  int64_t ldc, float* dst, void* stream) {
+  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(batch > 0 && c > 0 && h > 0 && w > 0 && ldc >= c && src && dst, "shape");
+  const long long n = (long long)batch * h * w * c;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == RGBAC_F32)
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, batch, c,
+                       h * w, (const float*)src, ldc, dst);
+  else
+    hipLaunchKernelGGL(nhwc_to_nchw_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, batch, c,
+                       h * w, (const bf16_t*)src, ldc, dst);
+  return check_launch("nhwc_to_nchw_kernel");
+}

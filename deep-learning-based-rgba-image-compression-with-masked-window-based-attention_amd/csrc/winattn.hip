@@ -1,0 +1,191 @@
+// Masked shifted-window attention core (per-window softmax(QK^T + B + M) V).
+//
+// The two dense projections of the block (qkv = Linear(C,3C), proj =
+// Linear(C,C)) are per-pixel 1x1 GEMMs and run on the MFMA conv engine: the
+// qkv GEMM produces an NHWC [B,H,W,3C] tensor in the ORIGINAL pixel frame, and
+// the proj GEMM's MASKSEL epilogue adds the result back onto x only for pixels
+// of active windows.  Because roll/partition/reverse are pure index
+// permutations, this kernel folds the cyclic shift, window partition, window
+// drop (remove_zero_windows) and scatter-back into its gather/store index
+// math: no permuted copy of x is ever materialised and no host sync is needed
+// to compact windows (reference: masked_win_attention.py:169-251 does ~8
+// full-tensor copies and two device->host syncs per call).
+//
+// One workgroup = 64 tokens = 64/(ws*ws) windows (1 for ws=8, 4 for ws=4).
+// Heads are processed one after another; q,k,v of a head are staged in LDS as
+// fp32 and the two small products (64 x ws^2 x d) run on the VALU in fp32.
+#include "common.h"
+
+namespace rgbac {
+
+template <typename T, int WS>
+__global__ void __launch_bounds__(256)
+winattn_core_kernel(int batch, int H, int W, int C, int heads, int shift, int masked,
+                    float scale, const T* __restrict__ qkv, long long ldq,
+                    const float* __restrict__ alpha, const float* __restrict__ bias,
+                    T* __restrict__ out, long long ldo, uint8_t* __restrict__ sel) {
+  constexpr int N = WS * WS;
+  constexpr int NWIN = 64 / N;
+  constexpr int DMAX = 24;
+  constexpr int DP = DMAX + 1;
+  __shared__ float qs[64 * DP];
+  __shared__ float ks[64 * DP];
+  __shared__ float vs[64 * DP];
+  __shared__ float S[64 * (N + 1)];
+  __shared__ int pix_s[64];
+  __shared__ int act_s[NWIN];
+
+  const int tid = threadIdx.x;
+  const int nwx = W / WS, nwy = H / WS;
+  const int total = batch * nwx * nwy;
+  const int d = C / heads;
+
+  if (tid < NWIN) act_s[tid] = masked ? 0 : 1;
+  __syncthreads();
+  if (tid < 64) {
+    const int wi = tid / N, lt = tid % N;
+    const int gw = blockIdx.x * NWIN + wi;
+    int pix = -1;
+    if (gw < total) {
+      const int b = gw / (nwx * nwy);
+      const int rem = gw - b * nwx * nwy;
+      const int wy = rem / nwx, wx = rem - (rem / nwx) * nwx;
+      const int r = wy * WS + lt / WS, c = wx * WS + lt % WS;
+      int oy = r + shift; if (oy >= H) oy -= H;
+      int ox = c + shift; if (ox >= W) ox -= W;
+      pix = (b * H + oy) * W + ox;
+      if (masked && alpha[pix] != 0.0f) act_s[wi] = 1;
+    }
+    pix_s[tid] = pix;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int pix = pix_s[tid];
+    if (pix >= 0 && sel) sel[pix] = (uint8_t)act_s[tid / N];
+  }
+  bool any = false;
+#pragma unroll
+  for (int w = 0; w < NWIN; ++w) any |= act_s[w] != 0;
+  if (!any) {
+    // every window of this group is transparent: attention output is 0
+    for (int e = tid; e < 64 * C; e += 256) {
+      const int t = e / C, ch = e - t * C;
+      const int pix = pix_s[t];
+      if (pix >= 0) Elem<T>::st(out + (long long)pix * ldo + ch, 0.0f);
+    }
+    return;
+  }
+
+  for (int h = 0; h < heads; ++h) {
+    // ---- stage q (pre-scaled, as q = q * self.scale), k, v of head h
+    for (int e = tid; e < 64 * d; e += 256) {
+      const int t = e / d, j = e - t * d;
+      const int pix = pix_s[t];
+      float q = 0.f, k = 0.f, v = 0.f;
+      if (pix >= 0) {
+        const T* row = qkv + (long long)pix * ldq + h * d + j;
+        q = Elem<T>::ld(row) * scale;
+        k = Elem<T>::ld(row + C);
+        v = Elem<T>::ld(row + 2 * C);
+      }
+      qs[t * DP + j] = q;
+      ks[t * DP + j] = k;
+      vs[t * DP + j] = v;
+    }
+    __syncthreads();
+    // ---- scores: token i attends keys of its own window
+    const float* bh = bias + (size_t)h * N * N;
+    for (int e = tid; e < 64 * N; e += 256) {
+      const int i = e / N, j = e - i * N;
+      const int wbase = (i / N) * N;
+      const int li = i - wbase;
+      float s = 0.f;
+      for (int q = 0; q < d; ++q) s = fmaf(qs[i * DP + q], ks[(wbase + j) * DP + q], s);
+      s += bh[li * N + j];
+      if (shift > 0) {
+        // region id of each token in the shifted frame (masked_win_attention.py:196-216)
+        const int wi = i / N;
+        const int gw = blockIdx.x * NWIN + wi;
+        const int rem = gw % (nwx * nwy);
+        const int wy = rem / nwx, wx = rem % nwx;
+        const int ri = wy * WS + li / WS, ci = wx * WS + li % WS;
+        const int rj = wy * WS + j / WS, cj = wx * WS + j % WS;
+        const int gi = 3 * (ri < H - WS ? 0 : (ri < H - shift ? 1 : 2)) +
+                       (ci < W - WS ? 0 : (ci < W - shift ? 1 : 2));
+        const int gj = 3 * (rj < H - WS ? 0 : (rj < H - shift ? 1 : 2)) +
+                       (cj < W - WS ? 0 : (cj < W - shift ? 1 : 2));
+        if (gi != gj) s += -100.0f;
+      }
+      S[i * (N + 1) + j] = s;
+    }
+    __syncthreads();
+    // ---- softmax over keys, 4 lanes per query row
+    {
+      const int i = tid >> 2, part = tid & 3;
+      float mx = -INFINITY;
+      for (int j = part; j < N; j += 4) mx = fmaxf(mx, S[i * (N + 1) + j]);
+      mx = fmaxf(mx, __shfl_xor(mx, 1));
+      mx = fmaxf(mx, __shfl_xor(mx, 2));
+      float sum = 0.f;
+      for (int j = part; j < N; j += 4) {
+        const float ex = expf(S[i * (N + 1) + j] - mx);
+        S[i * (N + 1) + j] = ex;
+        sum += ex;
+      }
+      sum += __shfl_xor(sum, 1);
+      sum += __shfl_xor(sum, 2);
+      const float inv = 1.0f / sum;
+      for (int j = part; j < N; j += 4) S[i * (N + 1) + j] *= inv;
+    }
+    __syncthreads();
+    // ---- o = P v, written at the token's original pixel
+    for (int e = tid; e < 64 * d; e += 256) {
+      const int i = e / d, q = e - i * d;
+      const int wbase = (i / N) * N;
+      float o = 0.f;
+#pragma unroll 8
+      for (int j = 0; j < N; ++j) o = fmaf(S[i * (N + 1) + j], vs[(wbase + j) * DP + q], o);
+      const int pix = pix_s[i];
+      if (pix >= 0) {
+        if (!act_s[i / N]) o = 0.f;
+        Elem<T>::st(out + (long long)pix * ldo + h * d + q, o);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+}  // namespace rgbac
+
+using namespace rgbac;
+
+extern "C" int rgbac_winattn_core(int dtype, int batch, int h, int w, int channels, int heads,
+                                  int ws, int shift, int masked, float scale, const void* qkv,
+                                  int64_t ldq, const float* alpha, const float* bias, void* out,
+                                  int64_t ldo, uint8_t* sel, void* stream) {
+  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(ws == 4 || ws == 8, "window size must be 4 or 8");
+  RGBAC_REQUIRE(batch > 0 && h > 0 && w > 0 && h % ws == 0 && w % ws == 0,
+                "H and W must be positive multiples of the window size");
+  RGBAC_REQUIRE(heads > 0 && channels % heads == 0 && channels / heads <= 24,
+                "head dim must divide C and be <= 24");
+  RGBAC_REQUIRE(shift >= 0 && shift < ws, "0 <= shift < window_size");
+  RGBAC_REQUIRE(qkv && out && bias, "null pointer");
+  RGBAC_REQUIRE(!masked || (alpha && sel), "masked attention needs alpha and sel");
+  RGBAC_REQUIRE(ldq >= 3 * channels && ldo >= channels, "strides");
+  const long long windows = (long long)batch * (h / ws) * (w / ws);
+  const int nwin = 64 / (ws * ws);
+  const int blocks = (int)((windows + nwin - 1) / nwin);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define RGBAC_WA(T, WS)                                                                    \
+  hipLaunchKernelGGL((winattn_core_kernel<T, WS>), dim3(blocks), dim3(256), 0, st, batch, h, \
+                     w, channels, heads, shift, masked, scale, (const T*)qkv, ldq, alpha,    \
+                     bias, (T*)out, ldo, sel)
+  if (dtype == RGBAC_F32) {
+    if (ws == 8) RGBAC_WA(float, 8); else RGBAC_WA(float, 4);
+  } else {
+    if (ws == 8) RGBAC_WA(bf16_t, 8); else RGBAC_WA(bf16_t, 4);
+  }
+#undef RGBAC_WA
+  return check_launch("winattn_core_kernel");
+}

@@ -1,0 +1,107 @@
+"""ctypes binding of librgbac_hip.so (the C ABI declared in include/rgbac.h).
+
+The product path has no CPU or eager-PyTorch fallback: if the shared object is
+missing or fails to load, every op raises.  Build it with
+``python -c "import __graft_entry__ as g; g.build()"`` (or ``make -C csrc``).
+"""
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librgbac_hip.so")
+
+F32, BF16 = 0, 1
+ACT = dict(none=0, gelu=1, relu=2, lrelu=3, tanh_half=4, gate=5, gdn=6, igdn=7, masksel=8)
+CONV, CONVT_S2, SUBPEL2 = 0, 1, 2
+
+
+class Src(ctypes.Structure):
+    _fields_ = [("ptr", ctypes.c_void_p), ("ldc", ctypes.c_int64),
+                ("channels", ctypes.c_int32), ("_pad", ctypes.c_int32)]
+
+
+class ConvArgs(ctypes.Structure):
+    _fields_ = [
+        ("dtype", ctypes.c_int32), ("mode", ctypes.c_int32),
+        ("batch", ctypes.c_int32), ("in_h", ctypes.c_int32), ("in_w", ctypes.c_int32),
+        ("ksize", ctypes.c_int32), ("stride", ctypes.c_int32),
+        ("nsrc", ctypes.c_int32), ("src", Src * 3),
+        ("cin_pad", ctypes.c_int32), ("k_pad", ctypes.c_int32),
+        ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p),
+        ("cout", ctypes.c_int32), ("cout_pad", ctypes.c_int32),
+        ("out_h", ctypes.c_int32), ("out_w", ctypes.c_int32),
+        ("out", ctypes.c_void_p), ("out_ldc", ctypes.c_int64),
+        ("out_coff", ctypes.c_int32), ("act", ctypes.c_int32),
+        ("act_param", ctypes.c_float), ("square_input", ctypes.c_int32),
+        ("res0", ctypes.c_void_p), ("res0_ldc", ctypes.c_int64),
+        ("res1", ctypes.c_void_p), ("res1_ldc", ctypes.c_int64),
+        ("res2", ctypes.c_void_p), ("res2_ldc", ctypes.c_int64),
+        ("sel", ctypes.c_void_p),
+    ]
+
+
+_VP, _I32, _I64, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
+# name -> argtypes (restype int unless noted); must match include/rgbac.h
+SIGNATURES = {
+    "rgbac_abi_version": [],
+    "rgbac_last_error": [],
+    "rgbac_conv2d": [ctypes.POINTER(ConvArgs), _VP],
+    "rgbac_winattn_core": [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _F,
+                           _VP, _I64, _VP, _VP, _VP, _I64, _VP, _VP],
+    "rgbac_gaussian_slice": [_I32, _I64, _I32, _VP, _I64, _VP, _I64, _VP, _I64, _VP,
+                             _VP, _I64, _VP, _VP, _VP],
+    "rgbac_eb_forward": [_I32, _I64, _I32, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _VP, _VP],
+    "rgbac_reduce_blocks": [_I64],
+    "rgbac_finalize": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP, _VP, _I32,
+                       _VP, _I32, _VP, _VP, _VP],
+    "rgbac_mask_pyramid": [_I32, _I32, _I32, _VP, _I32, _VP, _I32, _VP, _VP],
+    "rgbac_nchw_to_nhwc": [_I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP],
+    "rgbac_nhwc_to_nchw": [_I32, _I32, _I32, _I32, _I32, _VP, _I64, _VP, _VP],
+}
+
+_lib = None
+
+
+def load(path=LIB_PATH):
+    """Load (once) and return the library; raises if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(
+            f"rgbac: HIP library not found at {path}; build it first "
+            "(make -C <pkg>/csrc or __graft_entry__.build()). There is no fallback path.")
+    lib = ctypes.CDLL(path)
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_char_p if name == "rgbac_last_error" else ctypes.c_int
+    _lib = lib
+    return lib
+
+
+def call(name, *args):
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.rgbac_last_error().decode(errors="replace")
+        raise RuntimeError(f"{name} failed ({rc}): {msg}")
+    return rc
+
+
+def stream_ptr(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def dtype_code(dt):
+    if dt == torch.float32:
+        return F32
+    if dt == torch.bfloat16:
+        return BF16
+    raise ValueError(f"rgbac supports float32 and bfloat16 activations, got {dt}")

@@ -1,0 +1,138 @@
+"""Analysis / synthesis transforms (reference: layers/TransformRGB.py:16-100).
+
+Every conv is one rgbac_conv2d launch; the 5x5 stride-2 ConvTranspose2d layers
+run as four output-parity phases of one launch; GDN/IGDN is one launch each
+(see GDN.py); residual adds are conv epilogues."""
+import torch
+import torch.nn as nn
+
+from .. import runtime as rt
+from .GDN import GDN
+from .Masked_Attention import Win_noShift_Attention
+from ._blocks import conv3x3, subpel_conv3x3  # noqa: F401  (re-exported like the reference)
+
+
+def _act_of(m):
+    if isinstance(m, nn.LeakyReLU):
+        return "lrelu", float(m.negative_slope)
+    if isinstance(m, nn.ReLU):
+        return "relu", 0.0
+    if isinstance(m, nn.GELU):
+        return "gelu", 0.0
+    raise TypeError(f"unsupported activation {type(m)}")
+
+
+def run_conv(m, srcs, **kw):
+    """Run nn.Conv2d / nn.ConvTranspose2d ``m`` over concatenated Feat sources."""
+    dt = srcs[0][0].t.dtype
+    segs = rt.segs_of(*srcs)
+    if isinstance(m, nn.ConvTranspose2d):
+        k, s = m.kernel_size[0], m.stride[0]
+        if k == 1 and s == 1:
+            pk = rt.packed(m, dt, segs, rt.CONV, transposed=True)
+        else:
+            assert k == 5 and s == 2 and m.padding[0] == 2 and m.output_padding[0] == 1
+            pk = rt.packed(m, dt, segs, rt.CONVT_S2)
+    else:
+        assert m.padding[0] == m.kernel_size[0] // 2 and m.dilation[0] == 1 and m.groups == 1
+        pk = rt.packed(m, dt, segs)
+    return rt.conv(pk, srcs, **kw)
+
+
+def run_subpel(seq, srcs, act="none"):
+    """compressai subpel_conv3x3 = Sequential(conv3x3(C, r^2 C), PixelShuffle(r)), r = 2."""
+    assert isinstance(seq[1], nn.PixelShuffle) and seq[1].upscale_factor == 2
+    dt = srcs[0][0].t.dtype
+    pk = rt.packed(seq[0], dt, rt.segs_of(*srcs), rt.SUBPEL2)
+    return rt.conv(pk, srcs, act=act)
+
+
+class EnhancementBlock(nn.Module):
+    def __init__(self, num_filters=32):
+        super().__init__()
+        self.conv1 = nn.Conv2d(num_filters, num_filters, 3, stride=1, padding=1)
+        self.relu = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(num_filters, num_filters, 3, stride=1, padding=1)
+
+    def nhwc(self, x, post=None):
+        act, slope = _act_of(self.relu)
+        t = run_conv(self.conv1, [x.src()], act=act, act_param=slope)
+        return run_conv(self.conv2, [t.src()], res0=x, res2=post)
+
+
+class DSE(nn.Module):
+    def __init__(self, num_filters=32):
+        super().__init__()
+        self.input_conv = nn.Conv2d(3, num_filters, 1, stride=1)
+        self.enh1 = EnhancementBlock(num_filters)
+        self.enh2 = EnhancementBlock(num_filters)
+        self.enh3 = EnhancementBlock(num_filters)
+        self.output_conv = nn.Conv2d(num_filters, 3, 1, stride=1)
+
+    def nhwc(self, x):
+        first = run_conv(self.input_conv, [x.src()])
+        t = self.enh1.nhwc(first)
+        t = self.enh2.nhwc(t)
+        t = self.enh3.nhwc(t, post=first)          # (enh3(t) + x_first)
+        return run_conv(self.output_conv, [t.src()], res0=x)
+
+    def forward(self, input):
+        rt.check_gpu(input)
+        with torch.no_grad():
+            return rt.to_nchw(self.nhwc(rt.to_nhwc(input, torch.float32)))
+
+
+class Analysis_transform(nn.Module):
+    def __init__(self, N=192, M=320):
+        super().__init__()
+        self.x1 = nn.Conv2d(3, N, 5, stride=2, padding=2)
+        self.gdn1 = GDN(N)
+        self.x2 = nn.Conv2d(N, N, 5, stride=2, padding=2)
+        self.gdn2 = GDN(N)
+        self.attention1 = Win_noShift_Attention(dim=N, num_heads=8, window_size=8, shift_size=4)
+        self.x3 = nn.Conv2d(N, N, 5, stride=2, padding=2)
+        self.gdn3 = GDN(N)
+        self.x4 = nn.Conv2d(N, M, 1, stride=1, padding=0)
+        self.attention2 = Win_noShift_Attention(dim=M, num_heads=8, window_size=4, shift_size=2)
+
+    def nhwc(self, x, me2, me3):
+        y = self.gdn1.nhwc(run_conv(self.x1, [x.src()]))
+        y = self.gdn2.nhwc(run_conv(self.x2, [y.src()]))
+        y = self.attention1.nhwc(y, me2)
+        y = self.gdn3.nhwc(run_conv(self.x3, [y.src()]))
+        y = run_conv(self.x4, [y.src()])
+        return self.attention2.nhwc(y, me3)
+
+    def forward(self, input, mask, me1, me2, me3, me4):
+        rt.check_gpu(input, me2, me3)
+        with torch.no_grad():
+            return rt.to_nchw(self.nhwc(rt.to_nhwc(input, torch.float32), me2, me3))
+
+
+class Synthesis_transform(nn.Module):
+    def __init__(self, N=196, M=320):
+        super().__init__()
+        self.attention1 = Win_noShift_Attention(dim=M, num_heads=8, window_size=4, shift_size=2)
+        self.x1 = nn.Conv2d(M, N, 1, stride=1, padding=0)
+        self.igdn1 = GDN(N, inverse=True)
+        self.x2 = nn.ConvTranspose2d(N, N, 5, stride=2, padding=2, output_padding=1)
+        self.igdn2 = GDN(N, inverse=True)
+        self.attention2 = Win_noShift_Attention(N, num_heads=8, window_size=8, shift_size=4)
+        self.x3 = nn.ConvTranspose2d(N, N, 5, stride=2, padding=2, output_padding=1)
+        self.igdn3 = GDN(N, inverse=True)
+        self.x4 = nn.ConvTranspose2d(N, 3, 5, stride=2, padding=2, output_padding=1)
+        self.dse = DSE(32)
+
+    def nhwc(self, y, md2, md3):
+        t = self.attention1.nhwc(y, md3)
+        t = self.igdn1.nhwc(run_conv(self.x1, [t.src()]))
+        t = self.igdn2.nhwc(run_conv(self.x2, [t.src()]))
+        t = self.attention2.nhwc(t, md2)
+        t = self.igdn3.nhwc(run_conv(self.x3, [t.src()]))
+        t = run_conv(self.x4, [t.src()])
+        return self.dse.nhwc(t)
+
+    def forward(self, input, reconmask, md1, md2, md3, md4):
+        rt.check_gpu(input, md2, md3)
+        with torch.no_grad():
+            return rt.to_nchw(self.nhwc(rt.to_nhwc(input, torch.float32), md2, md3))

@@ -1,0 +1,154 @@
+"""Masked shifted-window attention (reference: layers/masked_win_attention.py).
+
+HIP pipeline per WinBasedAttention call (no permuted copies, no host sync):
+  1. qkv  = rgbac_conv2d 1x1 (Linear(C, 3C) per pixel, MFMA)            [B,H,W,3C]
+  2. core = rgbac_winattn_core: shift + partition + window drop + scores +
+            rel-pos bias + region mask + softmax + P.V + reverse + unshift
+  3. out  = rgbac_conv2d 1x1 (proj) with the MASKSEL epilogue:
+            x + proj(o) on pixels of active windows, x elsewhere
+            (result[~window_mask] = 0 then shortcut + x, :235-249).
+"""
+import torch
+import torch.nn as nn
+
+from .. import _lib
+from .. import runtime as rt
+
+
+def _to_2tuple(x):
+    return tuple(x) if isinstance(x, (tuple, list)) else (x, x)
+
+
+def _trunc_normal_(t, std=0.02):
+    # timm.models.layers.trunc_normal_(t, std) == nn.init.trunc_normal_(t, 0, std, -2, 2)
+    return nn.init.trunc_normal_(t, mean=0.0, std=std, a=-2.0, b=2.0)
+
+
+def window_partition(x, window_size=8):
+    """(B,H,W,C) -> (B*nW, ws, ws, C)   (:6-18; index permutation)."""
+    B, H, W, C = x.shape
+    x = x.reshape(B, H // window_size, window_size, W // window_size, window_size, C)
+    return x.permute(0, 1, 3, 2, 4, 5).reshape(-1, window_size, window_size, C)
+
+
+def window_reverse(windows, window_size, H, W):
+    """(B*nW, ws, ws, C) -> (B,H,W,C)   (:20-33)."""
+    B = int(windows.shape[0] / (H * W / window_size / window_size))
+    x = windows.reshape(B, H // window_size, W // window_size, window_size, window_size, -1)
+    return x.permute(0, 1, 3, 2, 4, 5).reshape(B, H, W, -1)
+
+
+def remove_zero_windows(x, alpha):
+    """(:35-47) keep windows whose alpha sums to non-zero.  The fused kernel computes
+    the same decision in-place; this helper is kept for API compatibility."""
+    mask = alpha.sum(dim=(1, 2, 3)) != 0
+    return x[mask], mask
+
+
+class WindowAttention(nn.Module):
+    """W-MSA with relative position bias; parameters as masked_win_attention.py:62-94."""
+
+    def __init__(self, dim=192, window_size=(8, 8), num_heads=8, qkv_bias=True, qk_scale=None,
+                 attn_drop=0., proj_drop=0.):
+        super().__init__()
+        self.dim = dim
+        self.window_size = _to_2tuple(window_size)
+        self.num_heads = num_heads
+        head_dim = dim // num_heads
+        self.scale = qk_scale or head_dim ** -0.5
+        wh, ww = self.window_size
+        assert wh == ww, "square windows only"
+        self.relative_position_bias_table = nn.Parameter(
+            torch.zeros((2 * wh - 1) * (2 * ww - 1), num_heads))
+        ys, xs = torch.meshgrid(torch.arange(wh), torch.arange(ww), indexing="ij")
+        pts = torch.stack([ys.flatten(), xs.flatten()])
+        rel = (pts[:, :, None] - pts[:, None, :]).permute(1, 2, 0).contiguous()
+        rel[:, :, 0] += wh - 1
+        rel[:, :, 1] += ww - 1
+        rel[:, :, 0] *= 2 * ww - 1
+        self.register_buffer("relative_position_index", rel.sum(-1))
+        self.qkv = nn.Linear(dim, dim * 3, bias=qkv_bias)
+        self.attn_drop = nn.Dropout(attn_drop)
+        self.proj = nn.Linear(dim, dim)
+        self.proj_drop = nn.Dropout(proj_drop)
+        _trunc_normal_(self.relative_position_bias_table, std=.02)
+        self.softmax = nn.Softmax(dim=-1)
+
+    def dense_bias(self):
+        """[heads][N][N] fp32 relative position bias (:109-111), cached per version."""
+        t = self.relative_position_bias_table
+        key = (t._version, t.data_ptr())
+        ent = self.__dict__.get("_rgbac_bias")
+        if ent is None or ent[0] != key:
+            N = self.window_size[0] * self.window_size[1]
+            with torch.no_grad():
+                b = t[self.relative_position_index.reshape(-1)].reshape(N, N, -1)
+                b = b.permute(2, 0, 1).contiguous().float()
+            self.__dict__["_rgbac_bias"] = (key, b)
+            ent = self.__dict__["_rgbac_bias"]
+        return ent[1]
+
+    def run_nhwc(self, x, alpha, shift, masked, residual=True):
+        """x: Feat (B,H,W,C), alpha: fp32 (B,1,H,W) or None -> Feat x + attn(x)
+        (or attn(x) alone when ``residual`` is False)."""
+        C, ws = self.dim, self.window_size[0]
+        dt = x.t.dtype
+        qkv = rt.conv(rt.packed(self.qkv, dt, [(C, x.ldc)]), [x.src()])
+        o = rt.new_feat(x.B, x.H, x.W, C, dt, x.t.device)
+        sel = None
+        if masked:
+            sel = torch.empty((x.B, x.H, x.W), dtype=torch.uint8, device=x.t.device)
+            alpha = alpha.contiguous().float()
+        _lib.call("rgbac_winattn_core", _lib.dtype_code(dt), x.B, x.H, x.W, C, self.num_heads,
+                  ws, shift, 1 if masked else 0, float(torch.tensor(self.scale, dtype=torch.float32)),
+                  qkv.ptr(), qkv.ldc, _lib.ptr(alpha) if masked else None,
+                  self.dense_bias().data_ptr(), o.ptr(), o.ldc, _lib.ptr(sel),
+                  _lib.stream_ptr(x.t.device))
+        pk = rt.packed(self.proj, dt, [(C, o.ldc)])
+        if not residual:
+            return rt.conv(pk, [o.src()])
+        if masked:
+            return rt.conv(pk, [o.src()], act="masksel", res1=x, sel=sel)
+        return rt.conv(pk, [o.src()], res0=x)
+
+    def forward(self, x, mask=None):
+        """x: (num_windows*B, N, C) windows; only mask=None is supported standalone
+        (shift masks are generated analytically inside WinBasedAttention)."""
+        rt.check_gpu(x)
+        if mask is not None:
+            raise NotImplementedError("rgbac fuses the shift mask into WinBasedAttention; "
+                                      "standalone WindowAttention supports mask=None only")
+        Bw, N, C = x.shape
+        ws = self.window_size[0]
+        img = x.reshape(Bw, ws, ws, C).permute(0, 3, 1, 2)
+        with torch.no_grad():
+            f = rt.to_nhwc(img, torch.float32)
+            out = rt.to_nchw(self.run_nhwc(f, None, 0, False, residual=False))
+        return out.permute(0, 2, 3, 1).reshape(Bw, N, C)
+
+
+class WinBasedAttention(nn.Module):
+    """Masked Swin block: x + scatter(W-MSA(windows with alpha != 0))  (:134-251)."""
+    masked = True
+
+    def __init__(self, dim=192, num_heads=8, window_size=8, shift_size=0, qkv_bias=True,
+                 qk_scale=None, drop=0., attn_drop=0., drop_path=0.):
+        super().__init__()
+        self.dim = dim
+        self.num_heads = num_heads
+        self.window_size = window_size
+        self.shift_size = shift_size
+        assert 0 <= self.shift_size < self.window_size, "shift_size must in 0-window_size"
+        self.attn = WindowAttention(dim, window_size=_to_2tuple(window_size), num_heads=num_heads,
+                                    qkv_bias=qkv_bias, qk_scale=qk_scale, attn_drop=attn_drop,
+                                    proj_drop=drop)
+        assert drop_path == 0.0, "DropPath is the identity in every reference configuration"
+        self.drop_path = nn.Identity()
+
+    def nhwc(self, x, img_alpha):
+        return self.attn.run_nhwc(x, img_alpha, self.shift_size, self.masked)
+
+    def forward(self, x, img_alpha):
+        rt.check_gpu(x, img_alpha)
+        with torch.no_grad():
+            return rt.to_nchw(self.nhwc(rt.to_nhwc(x, torch.float32), img_alpha))

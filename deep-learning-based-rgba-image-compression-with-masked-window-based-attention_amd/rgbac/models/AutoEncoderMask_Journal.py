@@ -1,0 +1,158 @@
+"""Alpha codec (reference: models/AutoEncoderMask_Journal.py), MI355X hot path.
+
+``AutoEncoder().forward(mask)`` -> ``(x_hat, mse_loss, total_bpp, y_bpp, z_bpp)``
+(:248-316), same module tree / state_dict keys as the reference."""
+import torch
+import torch.nn as nn
+
+from .. import runtime as rt
+from ..entropy import EntropyBottleneck, GaussianConditional
+from ..layers.GDN import GDN
+from ..layers.TransformRGB import _act_of, run_conv
+from ..layers._blocks import conv, conv3x3, deconv, subpel_conv3x3  # noqa: F401
+from ._latent import latent_path
+from .AutoEncoderRGB_Journal import (_CompressionModelMixin, _hyper_analysis, _hyper_synthesis,
+                                     _stack3, finalize, get_scale_table, ste_round)  # noqa: F401
+
+
+class EnhancementBlock(nn.Module):
+    def __init__(self, num_filters=32):
+        super().__init__()
+        self.conv1 = nn.Conv2d(num_filters, num_filters, 3, stride=1, padding=1)
+        self.relu = nn.LeakyReLU(inplace=True)
+        self.conv2 = nn.Conv2d(num_filters, num_filters, 3, stride=1, padding=1)
+
+    def nhwc(self, x, post=None):
+        act, slope = _act_of(self.relu)
+        t = run_conv(self.conv1, [x.src()], act=act, act_param=slope)
+        return run_conv(self.conv2, [t.src()], res0=x, res2=post)
+
+
+class DSE(nn.Module):
+    def __init__(self, in_ch=1, num_filters=32):
+        super().__init__()
+        self.input_conv = nn.Conv2d(in_ch, num_filters, 1, stride=1)
+        self.enh1 = EnhancementBlock(num_filters)
+        self.enh2 = EnhancementBlock(num_filters)
+        self.enh3 = EnhancementBlock(num_filters)
+        self.output_conv = nn.Conv2d(num_filters, in_ch, 1, stride=1)
+
+    def nhwc(self, x):
+        first = run_conv(self.input_conv, [x.src()])
+        t = self.enh1.nhwc(first)
+        t = self.enh2.nhwc(t)
+        t = self.enh3.nhwc(t, post=first)
+        return run_conv(self.output_conv, [t.src()], res0=x)
+
+
+class ResBlock(nn.Module):
+    def __init__(self, num_filters=128):
+        super().__init__()
+        self.conv1 = nn.Conv2d(num_filters, num_filters // 2, 1, stride=1)
+        self.relu1 = nn.ReLU(inplace=True)
+        self.conv2 = nn.Conv2d(num_filters // 2, num_filters // 2, 3, stride=1, padding=1)
+        self.relu2 = nn.ReLU(inplace=True)
+        self.conv3 = nn.Conv2d(num_filters // 2, num_filters, 1, stride=1)
+
+    def nhwc(self, x):
+        t = run_conv(self.conv1, [x.src()], act="relu")
+        t = run_conv(self.conv2, [t.src()], act="relu")
+        return run_conv(self.conv3, [t.src()], res0=x)
+
+
+class SimplifiedAttention(nn.Module):
+    """x + sigmoid(conv1(attention_branch)) * trunk_branch  (:112-136)."""
+
+    def __init__(self, num_filters=128):
+        super().__init__()
+        self.conv1 = nn.Conv2d(num_filters, num_filters, 1, stride=1)
+        self.sigmoid = nn.Sigmoid()
+        self.trunk_ResBlock1 = ResBlock(num_filters)
+        self.trunk_ResBlock2 = ResBlock(num_filters)
+        self.trunk_ResBlock3 = ResBlock(num_filters)
+        self.attention_ResBlock1 = ResBlock(num_filters)
+        self.attention_ResBlock2 = ResBlock(num_filters)
+        self.attention_ResBlock3 = ResBlock(num_filters)
+
+    def nhwc(self, x):
+        tr = self.trunk_ResBlock3.nhwc(self.trunk_ResBlock2.nhwc(self.trunk_ResBlock1.nhwc(x)))
+        at = self.attention_ResBlock3.nhwc(
+            self.attention_ResBlock2.nhwc(self.attention_ResBlock1.nhwc(x)))
+        return run_conv(self.conv1, [at.src()], act="gate", res1=tr, res2=x)
+
+
+def _run_seq(seq, x):
+    t = x
+    for m in seq:
+        if isinstance(m, GDN):
+            t = m.nhwc(t)
+        elif isinstance(m, (SimplifiedAttention, DSE)):
+            t = m.nhwc(t)
+        elif isinstance(m, (nn.Conv2d, nn.ConvTranspose2d)):
+            t = run_conv(m, [t.src()])
+        else:
+            raise TypeError(type(m))
+    return t
+
+
+class AutoEncoder(_CompressionModelMixin, nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.maskN = 192
+        self.maskM = 80
+        N, M = self.maskN, self.maskM
+        self.EncoderMask = nn.Sequential(
+            nn.Conv2d(1, N, 5, stride=2, padding=2), GDN(N),
+            nn.Conv2d(N, N, 5, stride=2, padding=2), GDN(N),
+            SimplifiedAttention(N),
+            nn.Conv2d(N, N, 5, stride=2, padding=2), GDN(N),
+            nn.Conv2d(N, M, 1, stride=1, padding=0),
+            SimplifiedAttention(M))
+        self.DecoderMask = nn.Sequential(
+            SimplifiedAttention(M),
+            nn.ConvTranspose2d(M, N, 1, stride=1, padding=0, output_padding=0),
+            GDN(N, inverse=True),
+            nn.ConvTranspose2d(N, N, 5, stride=2, padding=2, output_padding=1),
+            GDN(N, inverse=True),
+            SimplifiedAttention(N),
+            nn.ConvTranspose2d(N, N, 5, stride=2, padding=2, output_padding=1),
+            GDN(N, inverse=True),
+            nn.ConvTranspose2d(N, 1, 5, stride=2, padding=2, output_padding=1),
+            DSE(in_ch=1, num_filters=32))
+        self.num_slices = 5
+        self.max_support_slices = 5
+        self.h_a = _hyper_analysis(M)
+        self.h_mean_s = _hyper_synthesis(M)
+        self.h_scale_s = _hyper_synthesis(M)
+        ns, cs = self.num_slices, M // self.num_slices
+        self.cc_mean_transforms = nn.ModuleList(
+            _stack3(M + cs * min(i, 5), cs) for i in range(ns))
+        self.cc_scale_transforms = nn.ModuleList(
+            _stack3(M + cs * min(i, 5), cs) for i in range(ns))
+        self.lrp_transforms = nn.ModuleList(
+            _stack3(M + cs * min(i + 1, 6), cs) for i in range(ns))
+        self.entropy_bottleneck = EntropyBottleneck(192)
+        self.gaussian_conditional = GaussianConditional(None)
+        self.compute_dtype = torch.float32
+
+    def set_compute_dtype(self, dtype):
+        assert dtype in (torch.float32, torch.bfloat16)
+        self.compute_dtype = dtype
+        return self
+
+    def forward(self, mask, *, noise_z=None, noise_y=None, debug=None):
+        rt.check_gpu(mask)
+        B, _, H, W = mask.shape
+        if H % 64 or W % 64:
+            raise ValueError("H and W must be multiples of 64")
+        dt = self.compute_dtype
+        with torch.no_grad():
+            m = mask.contiguous().float()
+            y = _run_seq(self.EncoderMask, rt.to_nhwc(m, dt))
+            yh, ypart, zpart = latent_path(self, y, self.training, noise_z, noise_y, debug)
+            xh = _run_seq(self.DecoderMask, yh)
+            out = finalize(1, m, xh, None, ypart, zpart)
+            x_hat = rt.to_nchw(xh)
+        if debug is not None:
+            debug.update(y=y)
+        return x_hat, out[0], out[1], out[2], out[3]

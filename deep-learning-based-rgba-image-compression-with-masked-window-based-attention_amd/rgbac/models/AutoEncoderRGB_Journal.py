@@ -1,0 +1,161 @@
+"""RGB codec (reference: models/AutoEncoderRGB_Journal.py), MI355X hot path.
+
+``AutoEncoder().forward(input, mask, reconmask, me1, me2, me3, me4)`` returns
+``(x_hat, mse_loss, total_bpp, y_bpp, z_bpp)`` like the reference (:203-296).
+Same submodule names / parameter shapes, so reference checkpoints load with
+``load_state_dict`` (compressai CDF buffers are resized like compressai does).
+
+Compute dtype: ``model.compute_dtype`` = torch.float32 (parity mode, fp32
+MFMA) by default; torch.bfloat16 selects the throughput mode (bf16 storage
+and MFMA inputs, fp32 accumulation/epilogues).  Forward only: outputs carry
+no autograd graph in this round.
+"""
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import _lib
+from .. import runtime as rt
+from ..entropy import EntropyBottleneck, GaussianConditional
+from ..layers.SupplyMask import SupplyMaskToTransform, mask_pyramid
+from ..layers.TransformRGB import Analysis_transform, Synthesis_transform
+from ..layers._blocks import conv, conv3x3, deconv, subpel_conv3x3  # noqa: F401
+from ._latent import latent_path
+
+SCALES_MIN = 0.11
+SCALES_MAX = 256
+SCALES_LEVELS = 64
+
+
+def ste_round(x):
+    """:31-32"""
+    return torch.round(x) - x.detach() + x
+
+
+def get_scale_table(min=SCALES_MIN, max=SCALES_MAX, levels=SCALES_LEVELS):
+    return torch.exp(torch.linspace(math.log(min), math.log(max), levels))
+
+
+def reconstruct_error(input, output, input_mask, output_mask=None):
+    """:36-64 (host-side helper kept for API parity; the forward computes it in
+    rgbac_finalize)."""
+    m = (input_mask.expand(-1, 3, -1, -1) > 0.0).float()
+    se = F.mse_loss(input * m, output * m, reduction="none").sum(dim=(1, 2, 3))
+    cnt = torch.clamp(m.sum(dim=(1, 2, 3)), min=1)
+    return torch.mean(se / cnt)
+
+
+class _CompressionModelMixin:
+    """The parts of compressai.models.CompressionModel the reference relies on."""
+
+    def aux_loss(self):
+        return sum(m.loss() for m in self.modules() if isinstance(m, EntropyBottleneck))
+
+    def update(self, scale_table=None, force=False):
+        if scale_table is None:
+            scale_table = get_scale_table()
+        return self.gaussian_conditional.update_scale_table(scale_table, force=force)
+
+    def load_state_dict(self, state_dict, strict=True):
+        # compressai resizes the (initially empty) CDF buffers before loading
+        for name, buf in self.named_buffers():
+            base = name.rsplit(".", 1)[-1]
+            if base in ("_offset", "_quantized_cdf", "_cdf_length", "scale_table") \
+                    and name in state_dict and state_dict[name].shape != buf.shape:
+                mod = self.get_submodule(name.rsplit(".", 1)[0])
+                setattr(mod, base, torch.empty_like(state_dict[name], device=buf.device))
+        return nn.Module.load_state_dict(self, state_dict, strict=strict)
+
+    def compress(self, *args, **kwargs):
+        raise NotImplementedError("rANS bitstream coding is out of scope this round "
+                                  "(SURVEY.md §8f rank 1); forward() estimates bpp")
+
+    def decompress(self, *args, **kwargs):
+        raise NotImplementedError("rANS bitstream coding is out of scope this round")
+
+
+def _stack3(cin, cout=8):
+    return nn.Sequential(conv(cin, 224, stride=1, kernel_size=3), nn.GELU(),
+                         conv(224, 128, stride=1, kernel_size=3), nn.GELU(),
+                         conv(128, cout, stride=1, kernel_size=3))
+
+
+def _hyper_synthesis(M):
+    return nn.Sequential(subpel_conv3x3(192, 192, 2), nn.GELU(), conv3x3(192, 224), nn.GELU(),
+                         subpel_conv3x3(224, 256, 2), nn.GELU(), conv3x3(256, 288), nn.GELU(),
+                         subpel_conv3x3(288, M, 2))
+
+
+def _hyper_analysis(M):
+    return nn.Sequential(conv3x3(M, 320, stride=2), nn.GELU(), conv3x3(320, 288), nn.GELU(),
+                         conv3x3(288, 256, stride=2), nn.GELU(), conv3x3(256, 224), nn.GELU(),
+                         conv3x3(224, 192, stride=2))
+
+
+def finalize(mode, x, x_hat, mask, ypart, zpart):
+    """rgbac_finalize -> fp32 [mse, bpp, y_bpp, z_bpp] on device."""
+    B, cx, H, W = x.shape
+    dev = x.device
+    scratch = torch.empty(B * 64 * 2, dtype=torch.float64, device=dev)
+    out = torch.empty(4, dtype=torch.float32, device=dev)
+    _lib.call("rgbac_finalize", _lib.dtype_code(x_hat.t.dtype), mode, B, cx, H, W,
+              x.data_ptr(), x_hat.ptr(), x_hat.ldc, _lib.ptr(mask), ypart.data_ptr(),
+              ypart.numel(), zpart.data_ptr(), zpart.numel(), scratch.data_ptr(),
+              out.data_ptr(), _lib.stream_ptr(dev))
+    return out
+
+
+class AutoEncoder(_CompressionModelMixin, nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.N = 192
+        self.M = 80
+        self.Encoder = Analysis_transform(self.N, self.M)
+        self.Decoder = Synthesis_transform(self.N, self.M)
+        self.EncMakeMask = SupplyMaskToTransform()
+        self.DecMakeMask = SupplyMaskToTransform()
+        self.num_slices = 10
+        self.max_support_slices = 5
+        self.h_a = _hyper_analysis(self.M)
+        self.h_mean_s = _hyper_synthesis(self.M)
+        self.h_scale_s = _hyper_synthesis(self.M)
+        ns = self.num_slices
+        cs = self.M // ns
+        self.cc_mean_transforms = nn.ModuleList(
+            _stack3(self.M + cs * min(i, 5), cs) for i in range(ns))
+        self.cc_scale_transforms = nn.ModuleList(
+            _stack3(self.M + cs * min(i, 5), cs) for i in range(ns))
+        self.lrp_transforms = nn.ModuleList(
+            _stack3(self.M + cs * min(i + 1, 6), cs) for i in range(ns))
+        self.entropy_bottleneck = EntropyBottleneck(192)
+        self.gaussian_conditional = GaussianConditional(None)
+        self.compute_dtype = torch.float32
+
+    def set_compute_dtype(self, dtype):
+        assert dtype in (torch.float32, torch.bfloat16)
+        self.compute_dtype = dtype
+        return self
+
+    def forward(self, input, mask, reconmask, me1, me2, me3, me4, *, noise_z=None,
+                noise_y=None, debug=None):
+        rt.check_gpu(input, mask, reconmask, me2, me3)
+        B, _, H, W = input.shape
+        if H % 64 or W % 64:
+            raise ValueError("H and W must be multiples of 64 (windows at /4 and /8, "
+                             "hyperprior at /64)")
+        dt = self.compute_dtype
+        with torch.no_grad():
+            x = input.contiguous().float()
+            xf = rt.to_nhwc(x, dt)
+            # reconmask = round(reconmask*255)/255 ; md1..md4 = DecMakeMask(reconmask)  (:212-215)
+            _, md = mask_pyramid(reconmask, 4, round255=True)
+            y = self.Encoder.nhwc(xf, me2, me3)                                  # :217
+            yh, ypart, zpart = latent_path(self, y, self.training, noise_z, noise_y, debug)
+            xh = self.Decoder.nhwc(yh, md[1], md[2])                              # :273
+            out = finalize(0, x, xh, mask.contiguous().float(), ypart, zpart)    # :280-295
+            x_hat = rt.to_nchw(xh)
+        if debug is not None:
+            debug.update(y=y)
+        return x_hat, out[0], out[1], out[2], out[3]

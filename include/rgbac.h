@@ -1,0 +1,183 @@
+/*
+ * rgbac.h -- C ABI of librgbac_hip.so, the MI355X (gfx950) hot path of the
+ * learned RGBA codec (AutoEncoderRGB_Journal / AutoEncoderMask_Journal).
+ *
+ * The reference is pure Python over PyTorch + compressai and has no FFI of its
+ * own: its "operator interface" is the nn.Module forward of the layers listed
+ * below.  Each entry point names the reference code it replaces
+ * (paths relative to the reference repo root).  The Python host side
+ * (rgbac/_lib.py) binds these with ctypes; no torch types cross this boundary.
+ *
+ * Conventions
+ *  - Activations are NHWC with a channel stride ``ldc`` (elements) that is a
+ *    multiple of 8; padding channels hold zeros.  Element type is selected per
+ *    call: RGBAC_F32 (parity mode) or RGBAC_BF16 (throughput mode); MFMA
+ *    accumulation and all epilogue math are fp32 in both.
+ *  - All launches are asynchronous on ``stream`` (a hipStream_t passed as
+ *    void*).  No entry point allocates device memory, synchronises the host or
+ *    keeps state between calls; callers own every buffer (scratch included).
+ *  - Return 0 on success, a negative RGBAC_E* code otherwise (shape checks run
+ *    before any launch); rgbac_last_error() returns a thread-local message.
+ */
+#ifndef RGBAC_H_
+#define RGBAC_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RGBAC_ABI_VERSION 1
+
+enum rgbac_status {
+  RGBAC_OK = 0,
+  RGBAC_E_ARG = -1,      /* bad pointer / shape / unsupported combination */
+  RGBAC_E_DTYPE = -2,    /* unsupported dtype */
+  RGBAC_E_LAUNCH = -3,   /* hipLaunch / hipGetLastError failure */
+};
+
+enum rgbac_dtype { RGBAC_F32 = 0, RGBAC_BF16 = 1 };
+
+/* Fused epilogue of rgbac_conv2d, applied per output element in fp32:
+ *   v = acc + bias[n];  if (res0) v += res0;          (pre-activation add)
+ *   v = act(v, res1);   if (res2) v += res2;          (post-activation add)  */
+enum rgbac_act {
+  RGBAC_ACT_NONE = 0,
+  RGBAC_ACT_GELU = 1,      /* exact erf GELU (nn.GELU())                      */
+  RGBAC_ACT_RELU = 2,
+  RGBAC_ACT_LRELU = 3,     /* LeakyReLU(negative_slope = act_param)            */
+  RGBAC_ACT_TANH_HALF = 4, /* res1 + 0.5*tanh(v)   (lrp update)               */
+  RGBAC_ACT_GATE = 5,      /* res1 * sigmoid(v)    (then + res2)              */
+  RGBAC_ACT_GDN = 6,       /* res1 / sqrt(v)       (use with square_input)     */
+  RGBAC_ACT_IGDN = 7,      /* res1 * sqrt(v)                                    */
+  RGBAC_ACT_MASKSEL = 8,   /* sel[p] ? v + res1 : res1   (window-drop residual) */
+};
+
+enum rgbac_conv_mode {
+  RGBAC_CONV = 0,          /* nn.Conv2d(k, stride, pad = k/2)                  */
+  RGBAC_CONVT_S2 = 1,      /* nn.ConvTranspose2d(k, s=2, p=k/2, op=1), 4 phases */
+  RGBAC_SUBPEL2 = 2,       /* conv3x3 + nn.PixelShuffle(2) folded into store   */
+};
+
+/* One channel-concatenated input source (torch.cat along dim=1 is never
+ * materialised: up to three sources are read in order). */
+typedef struct rgbac_src {
+  const void* ptr;   /* NHWC base, element type = args.dtype                */
+  int64_t ldc;       /* channel stride (elements)                           */
+  int32_t channels;  /* channels taken from this source (multiple of 8)     */
+  int32_t _pad;
+} rgbac_src;
+
+typedef struct rgbac_conv_args {
+  int32_t dtype;               /* rgbac_dtype                                     */
+  int32_t mode;                /* rgbac_conv_mode                                 */
+  int32_t batch, in_h, in_w;   /* input spatial size                              */
+  int32_t ksize, stride;       /* kernel size (1,3,5); stride (1,2)               */
+  int32_t nsrc;                /* 1..3                                            */
+  rgbac_src src[3];
+  int32_t cin_pad;             /* sum(src.channels) (multiple of 8)                */
+  int32_t k_pad;               /* packed K per output row (mult. of 64)            */
+  const void* weight;          /* packed [nphase][cout_pad][k_pad], see rgbac_conv_pack */
+  const float* bias;           /* [cout_pad] fp32 (zero padded) or NULL            */
+  int32_t cout;                /* real output channels (pre-shuffle for SUBPEL2)  */
+  int32_t cout_pad;            /* rows of the packed weight (multiple of 64)      */
+  int32_t out_h, out_w;        /* stored output spatial size                       */
+  void* out; int64_t out_ldc; int32_t out_coff; int32_t act;
+  float act_param; int32_t square_input;   /* square the input (GDN norm pool) */
+  const void* res0; int64_t res0_ldc;      /* same pixel grid as out          */
+  const void* res1; int64_t res1_ldc;
+  const void* res2; int64_t res2_ldc;
+  const uint8_t* sel;                      /* MASKSEL: per output pixel flag   */
+} rgbac_conv_args;
+
+int rgbac_abi_version(void);
+const char* rgbac_last_error(void);
+
+/* Implicit-GEMM convolution on MFMA with fused epilogue.
+ * Replaces nn.Conv2d / nn.ConvTranspose2d / compressai conv3x3 /
+ * subpel_conv3x3 and the elementwise ops that follow them in:
+ *   layers/TransformRGB.py:55-99 (x1..x4, DSE, EnhancementBlock),
+ *   layers/Masked_Attention.py:150-189 (ResidualUnit, conv_a/conv_b, gate),
+ *   layers/GDN.py:64-94 (norm pool as 1x1 conv on x^2 + GDN/IGDN epilogue),
+ *   models/AutoEncoderRGB_Journal.py:135-198,242-264 (h_a, h_*_s, slice stacks,
+ *   lrp tanh update), models/AutoEncoderMask_Journal.py:96-244. */
+int rgbac_conv2d(const rgbac_conv_args* args, void* stream);
+
+/* Attention core of masked shifted-window MSA on a precomputed qkv tensor
+ * (qkv = Linear(C,3C) applied per pixel by rgbac_conv2d).  For every window
+ * of the cyclically shifted frame: activity = any(alpha != 0) over the
+ * window; active windows compute softmax(q*scale k^T + relpos_bias + shift
+ * mask(-100)) v per head and write it back at the un-shifted pixel positions;
+ * inactive windows write zeros.  sel[p] receives the activity of the window
+ * that pixel p belongs to (consumed by the proj conv's MASKSEL epilogue).
+ * Replaces layers/masked_win_attention.py:35-47,96-131,169-251 (masked=1) and
+ * layers/win_attention.py:96-115,153-207 (masked=0).
+ *   qkv:   NHWC [B,H,W,ldq] (channels s*C + h*d + e)
+ *   alpha: fp32 [B,H,W] (ignored when masked == 0)
+ *   bias:  fp32 [heads][ws*ws][ws*ws] dense relative-position bias
+ *   out:   NHWC [B,H,W,ldo], sel: uint8 [B,H,W] (may be NULL when masked==0) */
+int rgbac_winattn_core(int dtype, int batch, int h, int w, int channels,
+                       int heads, int ws, int shift, int masked, float scale,
+                       const void* qkv, int64_t ldq, const float* alpha,
+                       const float* bias, void* out, int64_t ldo, uint8_t* sel,
+                       void* stream);
+
+/* compressai GaussianConditional.forward + ste_round for one channel slice
+ * (models/AutoEncoderRGB_Journal.py:255-257, bits :280):
+ *   out_hat = round(y - mu) + mu   (torch.round: half to even)
+ *   v = |(training ? y + noise : out_hat) - mu|,  s = max(scale, 0.11)
+ *   lik = max(Phi((0.5 - v)/s) - Phi((-0.5 - v)/s), 1e-9)
+ *   partial[block] = sum clamp(-log(lik + 1e-10)/ln2, 0, 50)   (fp64)
+ * y/mu/scale/out_hat: NHWC with their own strides (channel offset folded into
+ * the pointer); noise: fp32 NHWC [npix][nch] or NULL; lik: fp32 NHWC or NULL.
+ * ``partial`` must hold rgbac_reduce_blocks(npix*nch) doubles. */
+int rgbac_gaussian_slice(int dtype, int64_t npix, int nch,
+                         const void* y, int64_t ldy, const void* mu, int64_t ldmu,
+                         const void* scale, int64_t lds, const float* noise,
+                         void* out_hat, int64_t ldh, float* lik, double* partial,
+                         void* stream);
+
+/* compressai EntropyBottleneck.forward (factorized prior, filters (3,3,3,3))
+ * fused with z_hat = ste_round(z - med) + med
+ * (models/AutoEncoderRGB_Journal.py:225-229).  params: fp32 [C][61] packed as
+ * softplus(M0..M4) (3,9,9,9,3), b0..b4 (3,3,3,3,1), tanh(f0..f3) (3x4),
+ * median -- see rgbac/entropy.py.  z: NHWC [npix][ldz]; z_hat written NHWC. */
+int rgbac_eb_forward(int dtype, int64_t npix, int channels, const void* z,
+                     int64_t ldz, const float* params, const float* noise,
+                     void* z_hat, int64_t ldh, float* lik, double* partial,
+                     void* stream);
+
+/* Number of fp64 partial sums written by a reduction over n elements. */
+int rgbac_reduce_blocks(int64_t n);
+
+/* Final scalars of AutoEncoder.forward: reconstruct_error (masked MSE,
+ * models/AutoEncoderRGB_Journal.py:36-64; or plain MSE when mode==1,
+ * AutoEncoderMask_Journal.py:309) and bpp = bits/(B*H*W) (:290-295).
+ * x: fp32 NCHW [B,cx,H,W]; x_hat: NHWC [B,H,W,ldh]; mask: fp32 [B,H,W].
+ * out[0..3] = mse, bpp, y_bpp, z_bpp.  Single-block finalize, deterministic. */
+int rgbac_finalize(int dtype, int mode, int batch, int cx, int h, int w,
+                   const float* x, const void* x_hat, int64_t ldh,
+                   const float* mask, const double* ybits, int ny,
+                   const double* zbits, int nz, double* scratch, float* out,
+                   void* stream);
+
+/* SupplyMaskToTransform (layers/SupplyMask.py:11-18): ``levels`` successive
+ * AvgPool2d(3, s2, p1, count_include_pad) of fp32 [B,H,W]; if round255, the
+ * input is first replaced by round(x*255)/255 (AutoEncoderRGB_Journal.py:212-214)
+ * and written to ``rounded``.  outs[i] receives level i+1. */
+int rgbac_mask_pyramid(int batch, int h, int w, const float* alpha, int round255,
+                       float* rounded, int levels, float* const* outs,
+                       void* stream);
+
+/* Layout conversions at the model boundary: fp32 NCHW <-> NHWC (ldc >= C,
+ * padding channels zeroed on the way in). */
+int rgbac_nchw_to_nhwc(int dtype, int batch, int c, int h, int w,
+                       const float* src, void* dst, int64_t ldc, void* stream);
+int rgbac_nhwc_to_nchw(int dtype, int batch, int c, int h, int w,
+                       const void* src, int64_t ldc, float* dst, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RGBAC_H_ */

@@ -1,0 +1,94 @@
+"""End-to-end GPU parity of both codecs against the CPU oracle (fp32 parity mode),
+plus stage-wise (teacher-forced) checks that isolate quantisation flips."""
+import pytest
+import torch
+
+from oracle import ref_model as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def cpu_sd(net):
+    return {k: v.detach().cpu() for k, v in net.state_dict().items()}
+
+
+def rel(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+
+
+def _inputs(B, H, W, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.round(torch.rand((B, 3, H, W), generator=g) * 255) / 255
+    a = torch.ones((B, 1, H, W))
+    kinds = ["ones", "half", "blob", "zero"]
+    for b in range(B):
+        k = kinds[b % 4]
+        if k == "half":
+            a[b, :, :, : W // 2] = 0
+        elif k == "blob":
+            yy, xx = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+            r = ((yy - H / 2) ** 2 + (xx - W / 2) ** 2).float().sqrt()
+            a[b, 0] = torch.clamp((H / 3 - r) / 8, 0, 1)
+            a[b, 0] = torch.round(a[b, 0] * 255) / 255
+        elif k == "zero":
+            a[b].zero_()
+    xm = torch.where(a > 0, x, a)
+    return xm, a
+
+
+@pytest.fixture(scope="module")
+def rgb_net():
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    torch.manual_seed(234)
+    return AutoEncoder().eval()
+
+
+def test_rgb_forward_fp32(device, rgb_net):
+    x, a = _inputs(4, 64, 128)
+    me = ref.supply_mask(a)
+    sd = cpu_sd(rgb_net)
+    with torch.no_grad():
+        want = ref.rgb_forward(sd, x, a, a, *me[:4])
+    net = rgb_net.to(device)
+    dbg = {}
+    got = net(x.to(device), a.to(device), a.to(device), *[m.to(device) for m in me[:4]], debug=dbg)
+    with torch.no_grad():
+        y_ref = ref.analysis(x, sd, "Encoder", me[1], me[2])
+    from rgbac import runtime as rt
+    assert rel(rt.to_nchw(dbg["y"]), y_ref) < 1e-4
+    assert got[0].shape == want[0].shape
+    print("x_hat rel", rel(got[0], want[0]), "bpp", got[2].item(), want[2].item())
+    assert rel(got[0], want[0]) < 1e-3
+    for i in (1, 2, 3, 4):
+        assert abs(got[i].item() - want[i].item()) <= 1e-4 * max(abs(want[i].item()), 1e-6)
+
+
+def test_rgb_forward_bf16(device, rgb_net):
+    x, a = _inputs(2, 64, 64, seed=1)
+    me = ref.supply_mask(a)
+    with torch.no_grad():
+        want = ref.rgb_forward(cpu_sd(rgb_net), x, a, a, *me[:4])
+    net = rgb_net.to(device).set_compute_dtype(torch.bfloat16)
+    try:
+        got = net(x.to(device), a.to(device), a.to(device), *[m.to(device) for m in me[:4]])
+    finally:
+        net.set_compute_dtype(torch.float32)
+    assert torch.isfinite(got[0]).all()
+    # bf16 storage: reconstruction within 5e-2 of the fp32 oracle's range, bpp within 5 %
+    assert rel(got[0], want[0]) < 5e-2
+    assert abs(got[2].item() - want[2].item()) < 0.05 * want[2].item()
+
+
+def test_mask_forward_fp32(device):
+    from rgbac.models.AutoEncoderMask_Journal import AutoEncoder
+    torch.manual_seed(234)
+    net = AutoEncoder().eval()
+    _, a = _inputs(2, 64, 64, seed=3)
+    with torch.no_grad():
+        want = ref.mask_forward(cpu_sd(net), a)
+    got = net.to(device)(a.to(device))
+    print("alpha x_hat rel", rel(got[0], want[0]))
+    assert rel(got[0], want[0]) < 1e-3
+    for i in (1, 2, 3, 4):
+        assert abs(got[i].item() - want[i].item()) <= 1e-4 * max(abs(want[i].item()), 1e-6)

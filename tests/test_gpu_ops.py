@@ -1,0 +1,212 @@
+"""GPU parity of each HIP op against the CPU oracle / PyTorch-CPU fp32 reference.
+
+fp32 (parity) mode: every result is compared with the CPU fp32 restatement
+(oracle/ref_model.py) on identical seeded inputs.  Tolerances are relative to
+the reference's max magnitude and state summation-order noise of fp32 MFMA
+(exact f32 FMA chains, different order): 2e-5 for single ops, looser for deep
+stacks as stated per test.  bf16 mode is checked with a stated looser bound.
+"""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from oracle import ref_model as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+
+
+def _rt():
+    from rgbac import runtime as rt
+    return rt
+
+
+def _gen(seed):
+    return torch.Generator().manual_seed(seed)
+
+
+# ------------------------------------------------------------------ convs
+CONV_CASES = [
+    # cin, cout, k, stride, H
+    (3, 192, 5, 2, 32), (192, 192, 5, 2, 16), (192, 80, 1, 1, 8), (96, 96, 3, 1, 16),
+    (80, 224, 3, 1, 8), (128, 8, 3, 1, 8), (320, 288, 3, 1, 4), (80, 320, 3, 2, 8),
+    (32, 32, 3, 1, 32), (32, 3, 1, 1, 16), (1, 192, 5, 2, 16), (40, 40, 3, 1, 8),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cin,cout,k,s,H", CONV_CASES)
+def test_conv2d(device, dtype, cin, cout, k, s, H):
+    rt = _rt()
+    from rgbac.layers.TransformRGB import run_conv
+    g = _gen(cin * 1000 + cout)
+    m = nn.Conv2d(cin, cout, k, stride=s, padding=k // 2)
+    x = torch.randn((2, cin, H, H + 8), generator=g)
+    want = m(x)
+    with torch.no_grad():
+        got = rt.to_nchw(run_conv(m.to(device), [rt.to_nhwc(x.to(device), dtype).src()]))
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    assert got.shape == want.shape
+    assert rel(got, want) < tol
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cin,cout,H", [(192, 192, 8), (192, 3, 16), (80, 192, 4), (16, 1, 8)])
+def test_conv_transpose(device, dtype, cin, cout, H):
+    rt = _rt()
+    from rgbac.layers.TransformRGB import run_conv
+    g = _gen(cin + cout)
+    m = nn.ConvTranspose2d(cin, cout, 5, stride=2, padding=2, output_padding=1)
+    x = torch.randn((2, cin, H, H + 4), generator=g)
+    want = m(x)
+    with torch.no_grad():
+        got = rt.to_nchw(run_conv(m.to(device), [rt.to_nhwc(x.to(device), dtype).src()]))
+    assert got.shape == want.shape
+    assert rel(got, want) < (2e-5 if dtype == torch.float32 else 2e-2)
+
+
+def test_conv_transpose_1x1(device):
+    rt = _rt()
+    from rgbac.layers.TransformRGB import run_conv
+    m = nn.ConvTranspose2d(80, 192, 1, stride=1, padding=0, output_padding=0)
+    x = torch.randn((2, 80, 8, 8), generator=_gen(5))
+    want = m(x)
+    with torch.no_grad():
+        got = rt.to_nchw(run_conv(m.to(device), [rt.to_nhwc(x.to(device), torch.float32).src()]))
+    assert rel(got, want) < 2e-5
+
+
+@pytest.mark.parametrize("cin,cout", [(192, 192), (288, 80), (224, 256)])
+def test_subpel(device, cin, cout):
+    rt = _rt()
+    from rgbac.layers.TransformRGB import run_subpel
+    from rgbac.layers._blocks import subpel_conv3x3
+    m = subpel_conv3x3(cin, cout, 2)
+    x = torch.randn((2, cin, 4, 4), generator=_gen(cin))
+    want = F.gelu(m(x))
+    with torch.no_grad():
+        got = rt.to_nchw(run_subpel(m.to(device), [rt.to_nhwc(x.to(device), torch.float32).src()],
+                                    act="gelu"))
+    assert rel(got, want) < 2e-5
+
+
+def test_concat_sources_and_epilogues(device):
+    """Three channel sources (torch.cat never materialised) + tanh_half epilogue."""
+    rt = _rt()
+    from rgbac.layers.TransformRGB import run_conv
+    g = _gen(7)
+    a, b, c = (torch.randn((2, n, 8, 8), generator=g) for n in (80, 40, 8))
+    pre = torch.randn((2, 8, 8, 8), generator=g)
+    m = nn.Conv2d(128, 8, 3, padding=1)
+    want = pre + 0.5 * torch.tanh(m(torch.cat([a, b, c], 1)))
+    with torch.no_grad():
+        fa, fb, fc = (rt.to_nhwc(t.to(device), torch.float32) for t in (a, b, c))
+        fp = rt.to_nhwc(pre.to(device), torch.float32)
+        got = run_conv(m.to(device), [fa.src(), fb.src(), fc.src()], act="tanh_half", res1=fp)
+    assert rel(rt.to_nchw(got), want) < 2e-5
+
+
+def test_gate_and_residual_epilogues(device):
+    rt = _rt()
+    from rgbac.layers.TransformRGB import run_conv
+    g = _gen(8)
+    x, a, r = (torch.randn((1, 64, 8, 8), generator=g) for _ in range(3))
+    m = nn.Conv2d(64, 64, 1)
+    want_gate = a * torch.sigmoid(m(x)) + r
+    want_gelu = F.gelu(m(x) + r)
+    with torch.no_grad():
+        fx, fa, fr = (rt.to_nhwc(t.to(device), torch.float32) for t in (x, a, r))
+        m = m.to(device)
+        gate = rt.to_nchw(run_conv(m, [fx.src()], act="gate", res1=fa, res2=fr))
+        gel = rt.to_nchw(run_conv(m, [fx.src()], act="gelu", res0=fr))
+    assert rel(gate, want_gate) < 2e-5
+    assert rel(gel, want_gelu) < 2e-5
+
+
+# ------------------------------------------------------------------ GDN
+@pytest.mark.parametrize("inverse", [False, True])
+def test_gdn(device, inverse):
+    from rgbac.layers.GDN import GDN
+    g = _gen(11)
+    m = GDN(192, inverse=inverse)
+    with torch.no_grad():
+        m.gamma.add_(0.05 * torch.rand(m.gamma.shape, generator=g))
+        m.beta.add_(0.1 * torch.rand(m.beta.shape, generator=g))
+    x = torch.randn((2, 192, 16, 16), generator=g)
+    want = ref.gdn(x, {"m." + k: v for k, v in m.state_dict().items()}, "m", inverse)
+    got = m.to(device)(x.to(device))
+    assert rel(got, want) < 2e-5
+
+
+# ------------------------------------------------------------------ attention
+def _alpha(kind, B, H, W, g):
+    a = torch.ones((B, 1, H, W))
+    if kind == "zero":
+        a.zero_()
+    elif kind == "half":
+        a[..., :, : W // 2] = 0
+    elif kind == "blob":
+        yy, xx = torch.meshgrid(torch.arange(H), torch.arange(W), indexing="ij")
+        r = ((yy - H / 3) ** 2 + (xx - W / 2) ** 2).float().sqrt()
+        a = (r < H / 4).float().expand(B, 1, H, W).clone()
+    elif kind == "rand":
+        a = (torch.rand((B, 1, H, W), generator=g) > 0.97).float()
+    return a
+
+
+@pytest.mark.parametrize("dim,ws,H", [(192, 8, 32), (80, 4, 16)])
+@pytest.mark.parametrize("kind", ["ones", "zero", "half", "blob", "rand"])
+def test_win_based_attention_masked(device, dim, ws, H, kind):
+    from rgbac.layers.masked_win_attention import WinBasedAttention
+    g = _gen(dim + H)
+    m = WinBasedAttention(dim=dim, num_heads=8, window_size=ws, shift_size=ws // 2)
+    x = torch.randn((2, dim, H, H + 2 * ws), generator=g)
+    a = _alpha(kind, 2, H, H + 2 * ws, g)
+    sd = {"blk." + k: v for k, v in m.state_dict().items()}
+    want = ref.win_based_attention(x, a, sd, "blk", ws, ws // 2)
+    got = m.to(device)(x.to(device), a.to(device))
+    assert rel(got, want) < 2e-5
+
+
+@pytest.mark.parametrize("dim,ws,shift", [(192, 8, 4), (80, 4, 2), (192, 8, 0)])
+def test_win_based_attention_unmasked(device, dim, ws, shift):
+    from rgbac.layers.win_attention import WinBasedAttention
+    g = _gen(dim)
+    m = WinBasedAttention(dim=dim, num_heads=8, window_size=ws, shift_size=shift)
+    x = torch.randn((2, dim, 4 * ws, 4 * ws), generator=g)
+    sd = {"blk." + k: v for k, v in m.state_dict().items()}
+    want = ref.win_based_attention(x, None, sd, "blk", ws, shift, masked=False)
+    got = m.to(device)(x.to(device))
+    assert rel(got, want) < 2e-5
+
+
+@pytest.mark.parametrize("dim,ws,H", [(192, 8, 32), (80, 4, 16)])
+def test_win_noshift_attention_block(device, dim, ws, H):
+    from rgbac.layers.Masked_Attention import Win_noShift_Attention
+    g = _gen(3 * dim)
+    m = Win_noShift_Attention(dim=dim, num_heads=8, window_size=ws, shift_size=ws // 2)
+    x = torch.randn((2, dim, H, H), generator=g)
+    a = _alpha("half", 2, H, H, g)
+    sd = {"blk." + k: v for k, v in m.state_dict().items()}
+    want = ref.win_noshift_attention(x, a, sd, "blk", ws, ws // 2)
+    got = m.to(device)(x.to(device), a.to(device))
+    assert rel(got, want) < 1e-4   # 7 chained convs + attention
+
+
+# ------------------------------------------------------------------ masks / entropy
+def test_mask_pyramid(device):
+    from rgbac.layers.SupplyMask import SupplyMaskToTransform, mask_pyramid
+    g = _gen(2)
+    a = torch.round(torch.rand((2, 1, 64, 96), generator=g) * 255) / 255
+    want = ref.supply_mask(a)
+    got = SupplyMaskToTransform()(a.to(device))
+    for w_, g_ in zip(want, got):
+        assert w_.shape == g_.shape
+        assert rel(g_, w_) < 1e-6
+    r, lv = mask_pyramid(a.to(device) * 0.999, 2, round255=True)
+    assert torch.equal(r.cpu(), torch.round(a * 0.999 * 255) / 255)
