@@ -1,0 +1,200 @@
+#!/usr/bin/env python
+"""Throughput of AutoEncoderRGB_Journal encode+decode on MI355X (BASELINE.json metric).
+
+One "step" = one full forward (encoder, hyperprior, 10-slice entropy model,
+decoder, bpp + masked MSE) of a synthetic 256x256 RGBA batch of 8 per GPU
+(BASELINE config 2), inputs resident in HBM, replayed from a HIP graph.
+N > 1: one process per GPU (torchrun), independent replicas (inference has no
+exchange step), barrier + synchronize around the timed region, MAX over ranks.
+
+Rank 0 also prints, in the same JSON line:
+  roofline      -- the dominant kernel's algorithmic FLOP/s (HIP events on the
+                   launching stream, eager attribution pass) vs its peak;
+  cpu_baseline  -- the CPU oracle (fp32 PyTorch restatement of the reference)
+                   on a bounded sample of the same workload, on this host.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "deep-learning-based-rgba-image-compression-with-masked-window-based-attention_amd")
+for _p in (ROOT, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "MPixels/sec encode+decode, 256×256 RGBA batch; bpp & PSNR parity vs reference"
+PEAK = {"bf16": {"mfma": 2500.0, "hbm": 8000.0}, "f32": {"mfma": 157.3, "hbm": 8000.0}}
+
+
+def synth_inputs(B, H, W, seed=0):
+    """RGB k/255; alpha cycles ones / left-half-zero / ellipse with an
+    8-px linear ramp (k/255) / zero; masked_input = where(alpha > 0, rgb, alpha)."""
+    g = torch.Generator().manual_seed(seed)
+    rgb = torch.round(torch.rand((B, 3, H, W), generator=g) * 255) / 255
+    a = torch.ones((B, 1, H, W))
+    yy, xx = torch.meshgrid(torch.arange(H).float(), torch.arange(W).float(), indexing="ij")
+    for b in range(B):
+        k = b % 4
+        if k == 1:
+            a[b, :, :, : W // 2] = 0
+        elif k == 2:
+            r = (((yy - H / 2) / (0.35 * H)) ** 2 + ((xx - W / 2) / (0.45 * W)) ** 2).sqrt()
+            ramp = torch.clamp((1.0 - r) * (0.4 * min(H, W)) / 8.0, 0, 1)
+            a[b, 0] = torch.round(ramp * 255) / 255
+        elif k == 3:
+            a[b].zero_()
+    return torch.where(a > 0, rgb, a), a
+
+
+def cpu_baseline(budget_s):
+    """Oracle (CPU fp32 restatement) on 1 image of the same workload, this host's cores."""
+    from oracle import ref_model as ref
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    torch.manual_seed(234)
+    sd = {k: v.detach().cpu() for k, v in AutoEncoder().eval().state_dict().items()}
+    x, a = synth_inputs(2, 256, 256, seed=0)
+    x, a = x[1:2], a[1:2]          # the half-transparent pattern
+    me = ref.supply_mask(a)
+    with torch.no_grad():
+        ref.rgb_forward(sd, x, a, a, *me[:4])          # warm-up
+        n, t0 = 0, time.perf_counter()
+        while True:
+            ref.rgb_forward(sd, x, a, a, *me[:4])
+            n += 1
+            if time.perf_counter() - t0 >= budget_s or n >= 20:
+                break
+        dt = time.perf_counter() - t0
+    return {"value": round(n * 256 * 256 / dt / 1e6, 4), "unit": "MPix/s",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle rgb_forward fp32, 1 image 256x256 (half-transparent alpha), "
+                      f"{n} timed iterations after 1 warm-up, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--size", type=int, default=256)
+    ap.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--kernels", action="store_true", help="add the per-kernel time table")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+
+    from rgbac import runtime as rt
+    from rgbac.layers.SupplyMask import mask_pyramid
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    torch.manual_seed(234)
+    net = AutoEncoder().eval().to(dev).set_compute_dtype(dt)
+    B, S = args.batch, args.size
+    x, a = synth_inputs(B, S, S, seed=rank)
+    x, a = x.to(dev), a.to(dev)
+    _, me = mask_pyramid(a, 4)
+
+    def step():
+        return net(x, a, a, *me)
+
+    out = step()                                       # packs weights, warms caches
+    torch.cuda.synchronize()
+    graph = None
+    if not args.no_graph:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                step()
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = step()
+        run = graph.replay
+    else:
+        run = step
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    ms = elapsed / args.steps * 1e3
+    value = world * B * S * S * args.steps / elapsed / 1e6
+
+    if rank == 0:
+        # ---- roofline attribution: eager replay with HIP events around every launch
+        prof = rt.LaunchProfiler()
+        rt.PROFILER = prof
+        for _ in range(3):
+            step()
+        rt.PROFILER = None
+        summ = prof.summary()
+        total_ms = sum(d["ms"] for d in summ.values())
+        dom_name, dom = max(summ.items(), key=lambda kv: kv[1]["ms"])
+        per_ms = dom["ms"] / dom["launches"]
+        per_fl = dom["flops"] / dom["launches"]
+        achieved = per_fl / (per_ms * 1e-3) / 1e12
+        peak = PEAK[args.dtype]["mfma"]
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "traffic": None, "kernel": dom_name,
+                "avg_launch_us": round(per_ms * 1e3, 2),
+                "algorithmic_gflop_per_launch": round(per_fl / 1e9, 4),
+                "share_of_forward": round(dom["ms"] / total_ms, 3)}
+        fwd_flops = sum(d["flops"] for d in summ.values()) / 3
+        rec = {"metric": METRIC, "value": round(value, 2), "unit": "MPix/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+               "dtype": args.dtype, "data": "synthetic (seeded RGB k/255 + 4 alpha patterns; "
+                                             "random-init weights, torch seed 234)",
+               "config": {"workload": "AutoEncoderRGB_Journal forward encode+decode "
+                                      f"(BASELINE config 2), {S}x{S} RGBA",
+                          "global_batch": B * world, "per_gpu_batch": B, "height": S, "width": S,
+                          "parallelism": f"replicas{world}", "hip_graph": graph is not None},
+               "roofline": roof,
+               "achieved_model_tflops": round(fwd_flops / (ms * 1e-3) / 1e12, 2)}
+        if args.kernels:
+            rec["kernels"] = {k: {"launches": v["launches"] // 3, "ms": round(v["ms"] / 3, 4),
+                                  "share": round(v["ms"] / total_ms, 4),
+                                  "tflops": round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 2)}
+                              for k, v in sorted(summ.items(), key=lambda kv: -kv[1]["ms"])}
+        rec["cpu_baseline"] = None
+        if world == 1 and not args.no_cpu_baseline:
+            rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        print(json.dumps(rec), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

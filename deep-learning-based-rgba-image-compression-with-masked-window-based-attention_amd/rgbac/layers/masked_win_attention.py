@@ -99,11 +99,15 @@ class WindowAttention(nn.Module):
         if masked:
             sel = torch.empty((x.B, x.H, x.W), dtype=torch.uint8, device=x.t.device)
             alpha = alpha.contiguous().float()
-        _lib.call("rgbac_winattn_core", _lib.dtype_code(dt), x.B, x.H, x.W, C, self.num_heads,
-                  ws, shift, 1 if masked else 0, float(torch.tensor(self.scale, dtype=torch.float32)),
-                  qkv.ptr(), qkv.ldc, _lib.ptr(alpha) if masked else None,
-                  self.dense_bias().data_ptr(), o.ptr(), o.ldc, _lib.ptr(sel),
-                  _lib.stream_ptr(x.t.device))
+        npix = x.B * x.H * x.W
+        rt.launch(f"winattn_core_kernel<{'f32' if dt == torch.float32 else 'bf16'},{ws}>",
+                  4.0 * npix * ws * ws * C, qkv.t.element_size() * npix * 4 * C,
+                  lambda: _lib.call(
+                      "rgbac_winattn_core", _lib.dtype_code(dt), x.B, x.H, x.W, C, self.num_heads,
+                      ws, shift, 1 if masked else 0,
+                      float(torch.tensor(self.scale, dtype=torch.float32)), qkv.ptr(), qkv.ldc,
+                      _lib.ptr(alpha) if masked else None, self.dense_bias().data_ptr(), o.ptr(),
+                      o.ldc, _lib.ptr(sel), _lib.stream_ptr(x.t.device)))
         pk = rt.packed(self.proj, dt, [(C, o.ldc)])
         if not residual:
             return rt.conv(pk, [o.src()])

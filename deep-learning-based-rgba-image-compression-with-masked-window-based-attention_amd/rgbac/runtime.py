@@ -18,6 +18,43 @@ from . import _lib
 from ._lib import ACT, CONV, CONVT_S2, SUBPEL2
 
 
+# Optional launch profiler (bench.py's roofline attribution): when set to a
+# LaunchProfiler, every launch made through ``launch`` is bracketed by HIP events
+# recorded on the launching stream, together with its algorithmic FLOPs/bytes.
+PROFILER = None
+
+
+class LaunchProfiler:
+    def __init__(self):
+        self.records = []   # (kernel name, flops, bytes, start event, end event)
+
+    def wrap(self, name, flops, nbytes, fn):
+        s = torch.cuda.Event(enable_timing=True)
+        e = torch.cuda.Event(enable_timing=True)
+        s.record()
+        fn()
+        e.record()
+        self.records.append((name, flops, nbytes, s, e))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for name, fl, nb, s, e in self.records:
+            d = out.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
+            d["launches"] += 1
+            d["ms"] += s.elapsed_time(e)
+            d["flops"] += fl
+            d["bytes"] += nb
+        return out
+
+
+def launch(name, flops, nbytes, fn):
+    if PROFILER is None:
+        fn()
+    else:
+        PROFILER.wrap(name, flops, nbytes, fn)
+
+
 def round_up(x, m):
     return (x + m - 1) // m * m
 
@@ -194,7 +231,18 @@ def conv(pk, srcs, out=None, out_coff=0, act="none", act_param=0.0, res0=None, r
             setattr(a, name, r.ptr())
             setattr(a, name + "_ldc", r.ldc)
     a.sel = None if sel is None else sel.data_ptr()
-    _lib.call("rgbac_conv2d", a, _lib.stream_ptr(f0.t.device))
+    if PROFILER is None:
+        _lib.call("rgbac_conv2d", a, _lib.stream_ptr(f0.t.device))
+    else:
+        taps = 25 if pk.mode == CONVT_S2 else pk.ksize * pk.ksize
+        mgrid = B * (H * W if pk.mode != CONV else Ho * Wo)
+        flops = 2.0 * mgrid * pk.cout * pk.cin * taps
+        es = f0.t.element_size()
+        nbytes = es * (B * H * W * pk.cin + B * Ho * Wo * cstore) + pk.w.numel() * es
+        wn = 4 if pk.cout_pad % 64 == 0 else (2 if pk.cout_pad % 32 == 0 else 1)
+        name = f"conv_kernel<{'f32' if dtype == torch.float32 else 'bf16'},{wn}>"
+        PROFILER.wrap(name, flops, nbytes,
+                      lambda: _lib.call("rgbac_conv2d", a, _lib.stream_ptr(f0.t.device)))
     return out
 
 
