@@ -87,6 +87,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--kernels", action="store_true", help="add the per-kernel time table")
+    ap.add_argument("--layers", default=None, help="write a per-layer time table to this file")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -159,6 +160,14 @@ def main():
             step()
         rt.PROFILER = None
         summ = prof.summary()
+        if args.layers:
+            lay = prof.layers()
+            tot = sum(v[1] for v in lay.values())
+            with open(args.layers, "w") as fh:
+                for k, v in sorted(lay.items(), key=lambda kv: -kv[1][1]):
+                    fh.write(f"{v[1] / 3:9.4f} ms {100 * v[1] / tot:5.1f}% n={v[0] // 3:3d} "
+                             f"{v[2] / max(v[1], 1e-9) / 1e9:8.1f} TF/s  "
+                             f"{v[3] / max(v[1], 1e-9) / 1e6:7.0f} GB/s  {k}\n")
         total_ms = sum(d["ms"] for d in summ.values())
         dom_name, dom = max(summ.items(), key=lambda kv: kv[1]["ms"])
         per_ms = dom["ms"] / dom["launches"]

@@ -2,52 +2,82 @@
 //
 // GEMM view (output-stationary, NHWC):   D[n][m] = sum_k W[n][k] * X[m][k]
 //   n = output channel, m = output pixel of the "M grid", k = (tap, cin).
-// A operand = packed weights [cout_pad][k_pad] (K contiguous), B operand =
-// im2col rows gathered on the fly from up to three NHWC sources (fused
-// channel concat).  Putting the channel on the MFMA row axis makes every lane
-// own 4 consecutive channels of one pixel in the accumulator, so epilogue
-// loads/stores are 16-byte (f32) / 8-byte (bf16) channel vectors.
+// A operand = packed weights [rows][k_pad] (K contiguous); B operand = im2col
+// rows gathered on the fly from up to three NHWC sources (fused channel
+// concat).  Putting channels on the MFMA row axis gives every lane 4
+// consecutive channels of one pixel in the accumulator, so epilogue
+// loads/stores are channel vectors.
 //
-// Tile: 256 threads = 4 waves, BM = 128 pixels (32 per wave), BN = 16*WN
-// channels, K staged 128 bytes per row per step (64 bf16 / 32 f32) through a
-// double-buffered, XOR-swizzled LDS image (chunk c of row r at c ^ (r & 7):
-// conflict-free ds_read_b128 for the 16-lane fragment groups).
-//   bf16: v_mfma_f32_16x16x32_bf16, one per 16x16 tile per 32-deep k-step.
-//   f32 : v_mfma_f32_16x16x4_f32 x4 per 16-deep k-step (exact f32 FMA chain;
-//         parity mode).  Lane l feeds k = 4*(l>>4)+e to MFMA e for both
-//         operands, which is a permutation of k and so the same sum.
+// Staging: both operands go HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4,
+// one 1-KiB piece = 8 rows x 128 B per wave-instruction) into an NBUF-deep ring
+// of K stages (128 bytes of K per row per stage: 64 bf16 / 32 f32).  The
+// 16-byte chunk c of row r lives at slot c ^ (r & 7) (conflict-free
+// ds_read_b128 for the 16-lane fragment groups); because the DMA destination
+// is lane-linear, the XOR is applied to the per-lane SOURCE chunk.  Padding
+// taps / out-of-image pixels read a zero page.  Stage s+NBUF-1 is issued while
+// stage s is consumed; a counted s_waitcnt vmcnt + raw s_barrier retires one
+// stage per iteration (no vmcnt(0) drain in the loop).
+//   bf16: v_mfma_f32_16x16x32_bf16 per 16x16 tile per 32-deep k-step.
+//   f32 : v_mfma_f32_16x16x4_f32 x4 per 16-deep k-step (exact f32 FMA chains,
+//         parity mode); lane l feeds k = 4*(l>>4)+e to MFMA e for both
+//         operands (a permutation of k: the same sum).
 //
 // Modes (rgbac_conv_mode): plain conv (stride 1/2), ConvTranspose2d(5, s2,
-// p2, op1) split into 4 output-parity phases (blockIdx.z) each of which is a
-// stride-1 conv with 3x3/3x2/2x3/2x2 taps, and subpel conv3x3 + PixelShuffle(2)
-// folded into the store.
+// p2, op1) as four output-parity phases (stride-1 convs with 3x3/3x2/2x3/2x2
+// taps) in one launch, and subpel conv3x3 + PixelShuffle(2) folded into the
+// store.  Split-K (ksplit > 1) writes fp32 partial slabs that
+// conv_splitk_epilogue sums in a fixed order (deterministic).
+//
+// Groups: one launch runs up to kMaxGroups independent convs that share the
+// geometry (mode, input/output size, kernel, stride, tile, split, activation)
+// but have their own weights, sources, outputs and residuals (blockIdx.z =
+// group, split, phase).  The model uses it for the cc_mean/cc_scale stacks,
+// the conv_a/conv_b residual units and h_mean_s/h_scale_s, which are
+// independent chains of identical shape.
 #include "common.h"
 
 namespace rgbac {
 
-struct ConvParams {
-  int mode, batch, in_h, in_w, Hm, Wm, out_h, out_w, M, sy;
-  int ksize, pad;
-  int nsrc;
+constexpr int kMaxGroups = 10;
+
+struct ConvGroup {                  // per-group operands
   const void* sp0; const void* sp1; const void* sp2;
   long long sld0, sld1, sld2;
-  int send0, send1, send2;          // cumulative channel ends
-  int cin_pad, k_pad;
-  int cout, cout_pad;
   const void* w;
   const float* bias;
-  void* out; long long out_ldc; int out_coff;
-  int act; float act_param; int square;
-  const void* res0; long long ld0;
-  const void* res1; long long ld1;
-  const void* res2; long long ld2;
+  void* out;
+  const void* res0; const void* res1; const void* res2;
+  long long ld0, ld1, ld2, out_ldc;
   const uint8_t* sel;
+  float* ws;                        // split-K slabs [ksplit][nphase][M][cout16]
+  const float* aux0;                // GAUSS: noise [M][cout/2] or NULL
+  float* aux1;                      // GAUSS: likelihood out [M][cout/2] or NULL
+  double* partial;                  // GAUSS: bits per M-tile block
+  int send0, send1, send2;          // cumulative channel ends
+  int cin_pad, k_pad, cout, rows, cout16, out_coff;
 };
+
+struct ConvShared {
+  int mode, batch, in_h, in_w, Hm, Wm, out_h, out_w, M, sy;
+  int ksize, pad;
+  int act; float act_param; int square;
+  int ksplit, nphase, ngroups;
+};
+
+struct ConvArgsDev {
+  ConvShared s;
+  ConvGroup g[kMaxGroups];
+};
+
+__device__ uint4 g_zero_page[64];   // zero source for padding taps (static, never written)
 
 __device__ __forceinline__ float gelu_f(float v) {
   return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f));
 }
 __device__ __forceinline__ float sigmoid_f(float v) { return 1.0f / (1.0f + expf(-v)); }
+__device__ __forceinline__ float std_cum_f(float t) {
+  return 0.5f * erfcf(-0.70710678118654752440f * t);
+}
 
 template <typename T>
 __device__ __forceinline__ uint4 square_chunk(uint4 v);
@@ -83,22 +113,9 @@ __device__ __forceinline__ void mma_step<float>(f32x4& acc, uint4 a, uint4 b) {
 }
 
 template <typename T>
-__device__ __forceinline__ void epi_store(const ConvParams& p, int opix, int n, float (&v)[4]) {
-  T* out = reinterpret_cast<T*>(p.out);
-  const long long base = (long long)opix * p.out_ldc + p.out_coff + n;
-  if (n + 3 < p.cout) {
-    Elem<T>::st4(out + base, v);
-  } else {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (n + r < p.cout) Elem<T>::st(out + base + r, v[r]);
-  }
-}
-
-template <typename T>
-__device__ __forceinline__ void load_res(const void* ptr, long long ld, int opix, int n,
+__device__ __forceinline__ void load_res(const void* ptr, long long ld, long long opix, int n,
                                          int cout, float (&v)[4]) {
-  const T* r = reinterpret_cast<const T*>(ptr) + (long long)opix * ld + n;
+  const T* r = reinterpret_cast<const T*>(ptr) + opix * ld + n;
   if (n + 3 < cout) {
     Elem<T>::ld4(r, v);
   } else {
@@ -107,270 +124,418 @@ __device__ __forceinline__ void load_res(const void* ptr, long long ld, int opix
   }
 }
 
-template <typename T, int WN>
-__global__ void __launch_bounds__(256) conv_kernel(const ConvParams p) {
-  constexpr int EPV = Elem<T>::EPV;
-  constexpr int KB = 8 * EPV;       // elements of K per stage (128 bytes/row)
-  constexpr int BN = 16 * WN;
-  constexpr int BM = 128;
-  constexpr int WM = 2;
-  constexpr int A_ITERS = (BN * 8 + 255) / 256;
-  __shared__ uint4 As[2][BN * 8];
-  __shared__ uint4 Bs[2][BM * 8];
+// Bias + fused epilogue + store of channels n..n+3 of M-grid pixel m (phase ph).
+template <typename T>
+__device__ __forceinline__ void epilogue4(const ConvShared& s, const ConvGroup& g, int ph, int m,
+                                          int n, float (&v)[4]) {
+  const int mx = m % s.Wm;
+  const int t = m / s.Wm;
+  const int my = t % s.Hm;
+  const int b = t / s.Hm;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] += (g.bias ? g.bias[n + r] : 0.0f);
+  T* out = reinterpret_cast<T*>(g.out);
+  if (s.mode == RGBAC_SUBPEL2) {
+    // conv channel n+r = 4*cc + 2*ii + jj -> pixel (2my+ii, 2mx+jj), channel cc
+    const int cc = n >> 2;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float x = v[r];
+      if (s.act == RGBAC_ACT_GELU) x = gelu_f(x);
+      const int oy = 2 * my + (r >> 1), ox = 2 * mx + (r & 1);
+      const long long o = ((long long)(b * s.out_h + oy) * s.out_w + ox) * g.out_ldc + g.out_coff + cc;
+      Elem<T>::st(out + o, x);
+    }
+    return;
+  }
+  long long opix;
+  if (s.mode == RGBAC_CONVT_S2)
+    opix = (long long)(b * s.out_h + 2 * my + (ph >> 1)) * s.out_w + 2 * mx + (ph & 1);
+  else
+    opix = (long long)(b * s.out_h + my) * s.out_w + mx;
+  if (g.res0) {
+    float r0[4];
+    load_res<T>(g.res0, g.ld0, opix, n, g.cout, r0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += r0[r];
+  }
+  float r1[4] = {0.f, 0.f, 0.f, 0.f};
+  if (g.res1) load_res<T>(g.res1, g.ld1, opix, n, g.cout, r1);
+  switch (s.act) {
+    case RGBAC_ACT_GELU:
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = gelu_f(v[r]);
+      break;
+    case RGBAC_ACT_RELU:
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+      break;
+    case RGBAC_ACT_LRELU:
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * s.act_param;
+      break;
+    case RGBAC_ACT_TANH_HALF:
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = r1[r] + 0.5f * tanhf(v[r]);
+      break;
+    case RGBAC_ACT_GATE:
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = r1[r] * sigmoid_f(v[r]);
+      break;
+    case RGBAC_ACT_GDN:
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = r1[r] / sqrtf(v[r]);
+      break;
+    case RGBAC_ACT_IGDN:
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = r1[r] * sqrtf(v[r]);
+      break;
+    case RGBAC_ACT_MASKSEL: {
+      const bool on = g.sel[opix] != 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = on ? r1[r] + v[r] : r1[r];
+      break;
+    }
+    default:
+      break;
+  }
+  if (g.res2) {
+    float r2[4];
+    load_res<T>(g.res2, g.ld2, opix, n, g.cout, r2);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += r2[r];
+  }
+  const long long base = opix * g.out_ldc + g.out_coff + n;
+  if (n + 3 < g.cout) {
+    Elem<T>::st4(out + base, v);
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (n + r < g.cout) Elem<T>::st(out + base + r, v[r]);
+  }
+}
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int phase = blockIdx.z;
+// GaussianConditional + ste_round on a (mu | sigma) conv output (ACT_GAUSS):
+//   hat = round(y - mu) + mu -> out;  v = |(train ? y + noise : hat) - mu|;
+//   lik = max(Phi((.5-v)/s) - Phi((-.5-v)/s), 1e-9), s = max(sigma, .11);
+//   returns clamp(-log(lik + 1e-10)/ln2, 0, 50)   (AutoEncoderRGB_Journal.py:255-257,280)
+template <typename T>
+__device__ __forceinline__ float gauss_elem(const ConvGroup& g, int m, int c, int nch, float mu,
+                                            float sg) {
+  const float yv = Elem<T>::ld(reinterpret_cast<const T*>(g.res1) + (long long)m * g.ld1 + c);
+  const float hat = rintf(yv - mu) + mu;
+  Elem<T>::st(reinterpret_cast<T*>(g.out) + (long long)m * g.out_ldc + g.out_coff + c, hat);
+  const float xin = g.aux0 ? yv + g.aux0[(long long)m * nch + c] : hat;
+  const float v = fabsf(xin - mu);
+  const float sc = fmaxf(sg, 0.11f);
+  const float lik = fmaxf(std_cum_f((0.5f - v) / sc) - std_cum_f((-0.5f - v) / sc), 1e-9f);
+  if (g.aux1) g.aux1[(long long)m * nch + c] = lik;
+  const float bits = (-1.0f * logf(lik + 1e-10f)) / 0.69314718055994530942f;
+  return fminf(fmaxf(bits, 0.0f), 50.0f);
+}
+
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+// One LDS-DMA piece: each lane moves 16 bytes from its own global address to
+// lds_block + 16*lane.  Issued from inline asm so hipcc neither counts it nor
+// inserts its own vmcnt(0) before later ds_reads; every wait on it is the
+// kernel's explicit counted s_waitcnt (M0 saved/restored inside the statement).
+__device__ __forceinline__ void dma16(const void* src, uint4* lds_block) {
+  const uint32_t lds = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lptr_t)lds_block);
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// BM x BN tile, 4 waves laid out WGM (along m) x WGN (along n), NBUF-stage ring.
+template <typename T, int BM, int BN, int WGM, int WGN, int NBUF>
+__global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
+  constexpr int EPV = Elem<T>::EPV;
+  constexpr int KS = 8 * EPV;                 // K elements per stage (128 B per row)
+  constexpr int TM = BM / WGM / 16;           // 16-pixel tiles per wave
+  constexpr int TN = BN / WGN / 16;           // 16-channel tiles per wave
+  constexpr int IA = BN / 8, IB = BM / 8;     // DMA pieces per stage
+  constexpr int LW = (IA + IB + 3) / 4;       // pieces per wave per stage (uniform)
+  constexpr int STAGE = (BN + BM) * 8;        // uint4 per stage
+  static_assert(WGM * WGN == 4, "4 waves");
+  static_assert(TM >= 1 && TN >= 1, "tile");
+  static_assert(NBUF * STAGE * 4 >= BM * BN, "GAUSS epilogue reuses the ring as a [BM][BN] fp32 tile");
+  __shared__ __attribute__((aligned(16))) uint4 smem[NBUF * STAGE];
+  __shared__ double red[4];
+
+  const ConvShared& s = args.s;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int zz = blockIdx.z;
+  const int phase = zz % s.nphase;
+  const int split = (zz / s.nphase) % s.ksplit;
+  const int gi = zz / (s.nphase * s.ksplit);
+  const ConvGroup& g = args.g[gi];
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  if (n0 >= g.cout) return;                    // groups may differ in cout
   const int py = phase >> 1, px = phase & 1;
-  int ntaps, tw;  // taps and taps per row for this phase
-  if (p.mode == RGBAC_CONVT_S2) {
+  int ntaps, tw;
+  if (s.mode == RGBAC_CONVT_S2) {
     tw = 3 - px;
     ntaps = (3 - py) * tw;
   } else {
-    tw = p.ksize;
-    ntaps = p.ksize * p.ksize;
+    tw = s.ksize;
+    ntaps = s.ksize * s.ksize;
   }
-  const int ktot = ntaps * p.cin_pad;
-  const int nk = (ktot + KB - 1) / KB;
-  const T* wbase = reinterpret_cast<const T*>(p.w) + (size_t)phase * p.cout_pad * p.k_pad;
+  const int ktot = ntaps * g.cin_pad;
+  const int nst = (ktot + KS - 1) / KS;
+  const int s_beg = (int)((long long)nst * split / s.ksplit);
+  const int s_end = (int)((long long)nst * (split + 1) / s.ksplit);
+  const int ns = s_end - s_beg;
 
-  // ---- per-thread im2col row state (rows fixed across the K loop)
-  const int c = tid & 7;
-  int rb[4], riy[4], rix[4];
-  bool rv[4];
+  // ---- per-lane DMA assignment: piece j = wave + 4*i; lane -> row (lane>>3),
+  //      source chunk c = (lane&7) ^ (lane>>3) so LDS slot (lane&7) holds chunk c.
+  const int lrow = lane >> 3;
+  const int c = (lane & 7) ^ lrow;
+  const T* wrow[LW];
+  int bb[LW], biy[LW], bix[LW];
+  bool isA[LW], bval[LW];
+  int lofs[LW];                                 // uint4 offset of the piece in a stage
+  const T* wbase = reinterpret_cast<const T*>(g.w) + (size_t)phase * g.rows * g.k_pad;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = m0 + (tid >> 3) + 32 * i;
-    rv[i] = m < p.M;
-    const int mm = rv[i] ? m : 0;
-    const int mx = mm % p.Wm;
-    const int t = mm / p.Wm;
-    const int my = t % p.Hm;
-    rb[i] = t / p.Hm;
-    riy[i] = my * p.sy;
-    rix[i] = mx * p.sy;
+  for (int i = 0; i < LW; ++i) {
+    int j = wave + 4 * i;
+    if (j >= IA + IB) j = IA + IB - 1;          // surplus slot re-issues the last piece
+    isA[i] = j < IA;
+    lofs[i] = j * 64;
+    const int arow = 8 * j + lrow;
+    wrow[i] = wbase + (size_t)(n0 + (isA[i] ? arow : 0)) * g.k_pad + c * EPV;
+    const int m = m0 + 8 * (j - IA) + lrow;
+    bval[i] = !isA[i] && m < s.M;
+    const int mm = bval[i] ? m : 0;
+    const int mx = mm % s.Wm;
+    const int t = mm / s.Wm;
+    bb[i] = t / s.Hm;
+    biy[i] = (t % s.Hm) * s.sy;
+    bix[i] = mx * s.sy;
   }
 
-  uint4 ra[A_ITERS], rbv[4];
+  // ---- incremental k -> (tap, ci) decode for this lane's chunk
+  const int k0 = s_beg * KS + c * EPV;
+  int tap = k0 / g.cin_pad;
+  int ci = k0 - tap * g.cin_pad;
+  int ty = tap / tw, tx = tap - (tap / tw) * tw;
 
-  auto load_stage = [&](int kb) {
-    // weights
-#pragma unroll
-    for (int i = 0; i < A_ITERS; ++i) {
-      const int q = tid + 256 * i;
-      if (q < BN * 8) {
-        const int row = q >> 3;
-        ra[i] = *reinterpret_cast<const uint4*>(wbase + (size_t)(n0 + row) * p.k_pad + kb * KB +
-                                                (q & 7) * EPV);
-      }
-    }
-    // activations (im2col gather)
-    const int k = kb * KB + c * EPV;
-    const int tap = k / p.cin_pad;
-    const int ci = k - tap * p.cin_pad;
-    bool kval = tap < ntaps;
+  auto issue = [&](int st_local, int buf) {
     int dy, dx;
-    {
-      const int ty = tap / tw, tx = tap - ty * tw;
-      if (p.mode == RGBAC_CONVT_S2) {
-        dy = 1 - ty;
-        dx = 1 - tx;
-      } else {
-        dy = ty - p.pad;
-        dx = tx - p.pad;
-      }
+    if (s.mode == RGBAC_CONVT_S2) {
+      dy = 1 - ty; dx = 1 - tx;
+    } else {
+      dy = ty - s.pad; dx = tx - s.pad;
     }
     const void* sp;
     long long sld;
     int cs;
-    if (ci < p.send0) {
-      sp = p.sp0; sld = p.sld0; cs = ci;
-    } else if (ci < p.send1) {
-      sp = p.sp1; sld = p.sld1; cs = ci - p.send0;
+    bool kval = tap < ntaps;
+    if (ci < g.send0) {
+      sp = g.sp0; sld = g.sld0; cs = ci;
+    } else if (ci < g.send1) {
+      sp = g.sp1; sld = g.sld1; cs = ci - g.send0;
     } else {
-      sp = p.sp2; sld = p.sld2; cs = ci - p.send1;
-      kval = kval && (ci < p.send2);
+      sp = g.sp2; sld = g.sld2; cs = ci - g.send1;
+      kval = kval && ci < g.send2;
     }
     const T* src = reinterpret_cast<const T*>(sp);
+    const int kk = (s_beg + st_local) * KS;
+    uint4* stage = smem + buf * STAGE;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int iy = riy[i] + dy, ix = rix[i] + dx;
-      const bool ok = kval && rv[i] && iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (ok) {
-        const long long off = ((long long)(rb[i] * p.in_h + iy) * p.in_w + ix) * sld + cs;
-        v = *reinterpret_cast<const uint4*>(src + off);
-        if (p.square) v = square_chunk<T>(v);
+    for (int i = 0; i < LW; ++i) {
+      const void* gp;
+      if (isA[i]) {
+        gp = wrow[i] + kk;
+      } else {
+        const int iy = biy[i] + dy, ix = bix[i] + dx;
+        const bool ok = kval && bval[i] && iy >= 0 && iy < s.in_h && ix >= 0 && ix < s.in_w;
+        gp = ok ? (const void*)(src + ((long long)(bb[i] * s.in_h + iy) * s.in_w + ix) * sld + cs)
+                : (const void*)g_zero_page;
       }
-      rbv[i] = v;
+      dma16(gp, stage + lofs[i]);
     }
-  };
-  auto store_stage = [&](int buf) {
-#pragma unroll
-    for (int i = 0; i < A_ITERS; ++i) {
-      const int q = tid + 256 * i;
-      if (q < BN * 8) {
-        const int row = q >> 3;
-        As[buf][row * 8 + ((q & 7) ^ (row & 7))] = ra[i];
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int row = (tid >> 3) + 32 * i;
-      Bs[buf][row * 8 + (c ^ (row & 7))] = rbv[i];
+    // advance this lane's decode to the next stage
+    ci += KS;
+    while (ci >= g.cin_pad) {
+      ci -= g.cin_pad;
+      ++tap;
+      if (++tx == tw) { tx = 0; ++ty; }
     }
   };
 
-  f32x4 acc[WN][WM];
+  f32x4 acc[TN][TM];
 #pragma unroll
-  for (int j = 0; j < WN; ++j)
+  for (int j = 0; j < TN; ++j)
 #pragma unroll
-    for (int i = 0; i < WM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load_stage(0);
-  store_stage(0);
-  __syncthreads();
-
+  const int wm = wave % WGM, wn = wave / WGM;
   const int fr = lane & 15, fq = lane >> 4, sw = lane & 7;
-  for (int kb = 0; kb < nk; ++kb) {
-    const int cur = kb & 1;
-    if (kb + 1 < nk) load_stage(kb + 1);
+
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int chunk = (4 * s + fq) ^ sw;
-      uint4 a[WN], b[WM];
-#pragma unroll
-      for (int j = 0; j < WN; ++j) a[j] = As[cur][(j * 16 + fr) * 8 + chunk];
-#pragma unroll
-      for (int i = 0; i < WM; ++i) b[i] = Bs[cur][(wave * 32 + i * 16 + fr) * 8 + chunk];
-#pragma unroll
-      for (int j = 0; j < WN; ++j)
-#pragma unroll
-        for (int i = 0; i < WM; ++i) mma_step<T>(acc[j][i], a[j], b[i]);
+  for (int st = 0; st < NBUF - 1; ++st)
+    if (st < ns) issue(st, st);
+
+  for (int it = 0; it < ns; ++it) {
+    // retire stage `it`: leave the stages issued after it in flight
+    if constexpr (NBUF >= 3) {
+      if (it + 1 < ns) wait_vm<LW * (NBUF - 2)>(); else wait_vm<0>();
+    } else {
+      wait_vm<0>();
     }
-    if (kb + 1 < nk) store_stage(cur ^ 1);
-    __syncthreads();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (it + NBUF - 1 < ns) issue(it + NBUF - 1, (it + NBUF - 1) % NBUF);
+    const uint4* As = smem + (it % NBUF) * STAGE;
+    const uint4* Bs = As + BN * 8;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = (4 * ks + fq) ^ sw;
+      uint4 a[TN], b[TM];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) a[j] = As[(wn * TN * 16 + j * 16 + fr) * 8 + chunk];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        b[i] = Bs[(wm * TM * 16 + i * 16 + fr) * 8 + chunk];
+        if (s.square) b[i] = square_chunk<T>(b[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) mma_step<T>(acc[j][i], a[j], b[i]);
+    }
   }
 
-  // ---- fused epilogue: lane owns channels n..n+3 of pixel m per tile
+  if (s.act == RGBAC_ACT_GAUSS) {
+    // (mu | sigma) tile -> LDS [BM][BN] fp32, then one (pixel, channel) per thread
+    float* tilef = reinterpret_cast<float*>(smem);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
 #pragma unroll
-  for (int i = 0; i < WM; ++i) {
-    const int m = m0 + wave * 32 + i * 16 + fr;
-    if (m >= p.M) continue;
-    const int mx = m % p.Wm;
-    const int t = m / p.Wm;
-    const int my = t % p.Hm;
-    const int b = t / p.Hm;
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < WN; ++j) {
-      const int n = n0 + j * 16 + fq * 4;
-      if (n >= p.cout) continue;
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = acc[j][i][r] + (p.bias ? p.bias[n + r] : 0.0f);
-      if (p.mode == RGBAC_SUBPEL2) {
-        // conv channel n+r = 4*cc + 2*ii + jj -> pixel (2my+ii, 2mx+jj), channel cc
-        const int cc = n >> 2;
-        T* out = reinterpret_cast<T*>(p.out);
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          float x = v[r];
-          if (p.act == RGBAC_ACT_GELU) x = gelu_f(x);
-          const int oy = 2 * my + (r >> 1), ox = 2 * mx + (r & 1);
-          const long long o = ((long long)(b * p.out_h + oy) * p.out_w + ox) * p.out_ldc + p.out_coff + cc;
-          Elem<T>::st(out + o, x);
+          const int ml = wm * TM * 16 + i * 16 + fr;
+          const int nl = wn * TN * 16 + j * 16 + fq * 4 + r;
+          tilef[ml * BN + nl] = acc[j][i][r] + (g.bias ? g.bias[nl] : 0.0f);
         }
-        continue;
+    __syncthreads();
+    const int nch = g.cout >> 1;
+    double bits = 0.0;
+    for (int e = tid; e < BM * nch; e += 256) {
+      const int ml = e / nch, ch = e - ml * nch;
+      const int m = m0 + ml;
+      if (m < s.M) bits += (double)gauss_elem<T>(g, m, ch, nch, tilef[ml * BN + ch],
+                                                 tilef[ml * BN + nch + ch]);
+    }
+    const double tot = block_sum_f64(bits, red);
+    if (tid == 0) g.partial[blockIdx.x] = tot;
+    return;
+  }
+
+  // ---- epilogue: lane owns channels n..n+3 of pixel m for every (j, i) tile
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * TM * 16 + i * 16 + fr;
+    if (m >= s.M) continue;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * TN * 16 + j * 16 + fq * 4;
+      if (n >= g.cout) continue;
+      float v[4] = {acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]};
+      if (s.ksplit > 1) {
+        float* w = g.ws + (((size_t)split * s.nphase + phase) * s.M + m) * g.cout16 + n;
+        *reinterpret_cast<float4*>(w) = make_float4(v[0], v[1], v[2], v[3]);
+      } else {
+        epilogue4<T>(s, g, phase, m, n, v);
       }
-      int opix;
-      if (p.mode == RGBAC_CONVT_S2)
-        opix = (b * p.out_h + 2 * my + py) * p.out_w + 2 * mx + px;
-      else
-        opix = (b * p.out_h + my) * p.out_w + mx;
-      if (p.res0) {
-        float r0[4];
-        load_res<T>(p.res0, p.ld0, opix, n, p.cout, r0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += r0[r];
-      }
-      float r1[4] = {0.f, 0.f, 0.f, 0.f};
-      if (p.res1) load_res<T>(p.res1, p.ld1, opix, n, p.cout, r1);
-      switch (p.act) {
-        case RGBAC_ACT_GELU:
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = gelu_f(v[r]);
-          break;
-        case RGBAC_ACT_RELU:
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
-          break;
-        case RGBAC_ACT_LRELU:
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * p.act_param;
-          break;
-        case RGBAC_ACT_TANH_HALF:
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = r1[r] + 0.5f * tanhf(v[r]);
-          break;
-        case RGBAC_ACT_GATE:
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = r1[r] * sigmoid_f(v[r]);
-          break;
-        case RGBAC_ACT_GDN:
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = r1[r] / sqrtf(v[r]);
-          break;
-        case RGBAC_ACT_IGDN:
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = r1[r] * sqrtf(v[r]);
-          break;
-        case RGBAC_ACT_MASKSEL: {
-          const bool on = p.sel[opix] != 0;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = on ? r1[r] + v[r] : r1[r];
-          break;
-        }
-        default:
-          break;
-      }
-      if (p.res2) {
-        float r2[4];
-        load_res<T>(p.res2, p.ld2, opix, n, p.cout, r2);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += r2[r];
-      }
-      epi_store<T>(p, opix, n, v);
     }
   }
 }
 
 template <typename T>
-static int launch_conv(const ConvParams& p, int nphase, hipStream_t st) {
-  const int wn = (p.cout_pad % 64 == 0) ? 4 : (p.cout_pad % 32 == 0) ? 2 : 1;
-  dim3 grid((p.M + 127) / 128, p.cout_pad / (16 * wn), nphase);
-  if (wn == 4)
-    hipLaunchKernelGGL((conv_kernel<T, 4>), grid, dim3(256), 0, st, p);
-  else if (wn == 2)
-    hipLaunchKernelGGL((conv_kernel<T, 2>), grid, dim3(256), 0, st, p);
-  else
-    hipLaunchKernelGGL((conv_kernel<T, 1>), grid, dim3(256), 0, st, p);
-  return check_launch("conv_kernel");
+__global__ void __launch_bounds__(256) conv_splitk_epilogue(const ConvArgsDev args, int gi) {
+  const ConvShared& s = args.s;
+  const ConvGroup& g = args.g[gi];
+  const int nq = g.cout16 / 4;
+  const long long total = (long long)s.nphase * s.M * nq;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    const int q = (int)(e % nq);
+    const long long pm = e / nq;
+    const int m = (int)(pm % s.M);
+    const int ph = (int)(pm / s.M);
+    const int n = 4 * q;
+    if (n >= g.cout) continue;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int sp = 0; sp < s.ksplit; ++sp) {
+      const float4 t = *reinterpret_cast<const float4*>(
+          g.ws + (((size_t)sp * s.nphase + ph) * s.M + m) * g.cout16 + n);
+      v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
+    }
+    epilogue4<T>(s, g, ph, m, n, v);
+  }
 }
 
-}  // namespace rgbac
+struct TileCfg { int bm, bn; };
+static const TileCfg kTiles[] = {
+    {128, 128}, {128, 64}, {64, 64}, {128, 32}, {64, 32}, {128, 16}, {64, 16}};
+constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 
-using namespace rgbac;
+template <typename T>
+static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t st) {
+  const ConvShared& s = d.s;
+  const TileCfg tc = kTiles[tile];
+  dim3 grid((s.M + tc.bm - 1) / tc.bm, (max_cout + tc.bn - 1) / tc.bn,
+            s.nphase * s.ksplit * s.ngroups);
+  switch (tile) {
+    case 0: hipLaunchKernelGGL((conv_kernel<T, 128, 128, 2, 2, 2>), grid, dim3(256), 0, st, d); break;
+    case 1: hipLaunchKernelGGL((conv_kernel<T, 128, 64, 4, 1, 3>), grid, dim3(256), 0, st, d); break;
+    case 2: hipLaunchKernelGGL((conv_kernel<T, 64, 64, 2, 2, 3>), grid, dim3(256), 0, st, d); break;
+    case 3: hipLaunchKernelGGL((conv_kernel<T, 128, 32, 4, 1, 3>), grid, dim3(256), 0, st, d); break;
+    case 4: hipLaunchKernelGGL((conv_kernel<T, 64, 32, 2, 2, 3>), grid, dim3(256), 0, st, d); break;
+    case 5: hipLaunchKernelGGL((conv_kernel<T, 128, 16, 4, 1, 3>), grid, dim3(256), 0, st, d); break;
+    default: hipLaunchKernelGGL((conv_kernel<T, 64, 16, 4, 1, 3>), grid, dim3(256), 0, st, d); break;
+  }
+  int rc = check_launch("conv_kernel");
+  if (rc || s.ksplit == 1) return rc;
+  for (int gi = 0; gi < s.ngroups; ++gi) {
+    const long long total = (long long)s.nphase * s.M * (d.g[gi].cout16 / 4);
+    long long gsz = (total + 255) / 256;
+    if (gsz > 8192) gsz = 8192;
+    hipLaunchKernelGGL((conv_splitk_epilogue<T>), dim3((int)gsz), dim3(256), 0, st, d, gi);
+    rc = check_launch("conv_splitk_epilogue");
+    if (rc) return rc;
+  }
+  return RGBAC_OK;
+}
 
-extern "C" int rgbac_conv2d(const rgbac_conv_args* a, void* stream) {
-  RGBAC_REQUIRE(a != nullptr, "null args");
-  RGBAC_REQUIRE(a->dtype == RGBAC_F32 || a->dtype == RGBAC_BF16, "dtype");
+static int fill_group(const rgbac_conv_args* a, int ntaps_max, ConvGroup& g) {
   RGBAC_REQUIRE(a->nsrc >= 1 && a->nsrc <= 3, "nsrc must be 1..3");
-  RGBAC_REQUIRE(a->batch > 0 && a->in_h > 0 && a->in_w > 0, "bad input shape");
   RGBAC_REQUIRE(a->weight && a->out, "null weight/out");
-  RGBAC_REQUIRE(a->cout > 0 && a->cout_pad >= a->cout && a->cout_pad % 16 == 0,
-                "cout_pad must be >= cout and a multiple of 16");
+  RGBAC_REQUIRE(a->ksplit == 1 || a->workspace, "split-K needs a workspace");
+  RGBAC_REQUIRE(a->cout > 0 && a->cout_pad % 128 == 0 && a->cout_pad >= a->cout,
+                "cout_pad (packed weight rows) must be a multiple of 128 and >= cout");
   RGBAC_REQUIRE(a->cin_pad % 8 == 0 && a->cin_pad > 0, "cin_pad must be a multiple of 8");
   RGBAC_REQUIRE(a->k_pad % 64 == 0, "k_pad must be a multiple of 64");
+  RGBAC_REQUIRE(ntaps_max * a->cin_pad <= a->k_pad, "k_pad too small for the taps");
   int csum = 0;
   for (int i = 0; i < a->nsrc; ++i) {
     RGBAC_REQUIRE(a->src[i].ptr != nullptr, "null source");
@@ -378,22 +543,77 @@ extern "C" int rgbac_conv2d(const rgbac_conv_args* a, void* stream) {
                   "source channels must be a positive multiple of 8");
     RGBAC_REQUIRE(a->src[i].ldc % 8 == 0 && a->src[i].ldc >= a->src[i].channels,
                   "source ldc must be a multiple of 8 and >= channels");
+    RGBAC_REQUIRE(((uintptr_t)a->src[i].ptr) % 16 == 0, "source pointers must be 16-byte aligned");
     csum += a->src[i].channels;
   }
-  RGBAC_REQUIRE(csum <= a->cin_pad, "sum of source channels exceeds cin_pad");
+  RGBAC_REQUIRE(csum == a->cin_pad, "sum of source channels must equal cin_pad");
   RGBAC_REQUIRE(a->out_ldc % 4 == 0 && a->out_coff % 4 == 0, "out_ldc/out_coff must be multiples of 4");
-  RGBAC_REQUIRE(a->act >= RGBAC_ACT_NONE && a->act <= RGBAC_ACT_MASKSEL, "act");
   RGBAC_REQUIRE(a->act != RGBAC_ACT_MASKSEL || (a->sel && a->res1), "MASKSEL needs sel and res1");
   RGBAC_REQUIRE(!(a->act == RGBAC_ACT_TANH_HALF || a->act == RGBAC_ACT_GATE ||
-                  a->act == RGBAC_ACT_GDN || a->act == RGBAC_ACT_IGDN) || a->res1,
+                  a->act == RGBAC_ACT_GDN || a->act == RGBAC_ACT_IGDN ||
+                  a->act == RGBAC_ACT_GAUSS) || a->res1,
                 "act needs res1");
+  g.sp0 = a->src[0].ptr; g.sld0 = a->src[0].ldc; g.send0 = a->src[0].channels;
+  g.sp1 = a->nsrc > 1 ? a->src[1].ptr : a->src[0].ptr;
+  g.sld1 = a->nsrc > 1 ? a->src[1].ldc : a->src[0].ldc;
+  g.send1 = g.send0 + (a->nsrc > 1 ? a->src[1].channels : 0);
+  g.sp2 = a->nsrc > 2 ? a->src[2].ptr : g.sp1;
+  g.sld2 = a->nsrc > 2 ? a->src[2].ldc : g.sld1;
+  g.send2 = g.send1 + (a->nsrc > 2 ? a->src[2].channels : 0);
+  g.cin_pad = a->cin_pad;
+  g.k_pad = a->k_pad;
+  g.cout = a->cout;
+  g.rows = a->cout_pad;
+  g.cout16 = (a->cout + 15) / 16 * 16;
+  g.w = a->weight;
+  g.bias = a->bias;
+  g.out = a->out;
+  g.out_ldc = a->out_ldc;
+  g.out_coff = a->out_coff;
+  g.res0 = a->res0; g.ld0 = a->res0_ldc;
+  g.res1 = a->res1; g.ld1 = a->res1_ldc;
+  g.res2 = a->res2; g.ld2 = a->res2_ldc;
+  g.sel = a->sel;
+  g.ws = reinterpret_cast<float*>(a->workspace);
+  g.aux0 = a->aux0;
+  g.aux1 = a->aux1;
+  g.partial = a->partial;
+  return RGBAC_OK;
+}
 
-  ConvParams p{};
-  p.mode = a->mode;
-  p.batch = a->batch;
-  p.in_h = a->in_h;
-  p.in_w = a->in_w;
-  int nphase = 1;
+}  // namespace rgbac
+
+using namespace rgbac;
+
+extern "C" int rgbac_conv_num_tiles(void) { return kNumTiles; }
+extern "C" int rgbac_conv_max_groups(void) { return kMaxGroups; }
+
+extern "C" int rgbac_conv2d_grouped(const rgbac_conv_args* args, int ngroups, void* stream) {
+  RGBAC_REQUIRE(args != nullptr, "null args");
+  RGBAC_REQUIRE(ngroups >= 1 && ngroups <= kMaxGroups, "ngroups must be 1..10");
+  const rgbac_conv_args* a = &args[0];
+  RGBAC_REQUIRE(a->dtype == RGBAC_F32 || a->dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(a->batch > 0 && a->in_h > 0 && a->in_w > 0, "bad input shape");
+  RGBAC_REQUIRE(a->tile >= 0 && a->tile < kNumTiles, "tile index out of range");
+  RGBAC_REQUIRE(a->ksplit >= 1 && a->ksplit <= 64, "ksplit must be 1..64");
+  RGBAC_REQUIRE(a->act >= RGBAC_ACT_NONE && a->act <= RGBAC_ACT_GAUSS, "act");
+  for (int i = 1; i < ngroups; ++i) {
+    const rgbac_conv_args* b = &args[i];
+    RGBAC_REQUIRE(b->dtype == a->dtype && b->mode == a->mode && b->batch == a->batch &&
+                      b->in_h == a->in_h && b->in_w == a->in_w && b->ksize == a->ksize &&
+                      b->stride == a->stride && b->out_h == a->out_h && b->out_w == a->out_w &&
+                      b->tile == a->tile && b->ksplit == a->ksplit && b->act == a->act &&
+                      b->act_param == a->act_param && b->square_input == a->square_input,
+                  "grouped convs must share geometry, tile, split and activation");
+  }
+  ConvArgsDev d{};
+  ConvShared& s = d.s;
+  s.mode = a->mode;
+  s.batch = a->batch;
+  s.in_h = a->in_h;
+  s.in_w = a->in_w;
+  s.nphase = 1;
+  int ntaps_max;
   if (a->mode == RGBAC_CONV) {
     RGBAC_REQUIRE(a->ksize == 1 || a->ksize == 3 || a->ksize == 5, "ksize must be 1/3/5");
     RGBAC_REQUIRE(a->stride == 1 || a->stride == 2, "stride must be 1/2");
@@ -401,55 +621,55 @@ extern "C" int rgbac_conv2d(const rgbac_conv_args* a, void* stream) {
     const int oh = (a->in_h + 2 * pad - a->ksize) / a->stride + 1;
     const int ow = (a->in_w + 2 * pad - a->ksize) / a->stride + 1;
     RGBAC_REQUIRE(a->out_h == oh && a->out_w == ow, "out size mismatch for conv");
-    p.Hm = oh; p.Wm = ow; p.sy = a->stride; p.ksize = a->ksize; p.pad = pad;
-    RGBAC_REQUIRE(a->ksize * a->ksize * a->cin_pad <= a->k_pad, "k_pad too small");
+    s.Hm = oh; s.Wm = ow; s.sy = a->stride; s.ksize = a->ksize; s.pad = pad;
+    ntaps_max = a->ksize * a->ksize;
   } else if (a->mode == RGBAC_CONVT_S2) {
     RGBAC_REQUIRE(a->ksize == 5 && a->stride == 2, "CONVT_S2 supports k=5, s=2, p=2, op=1 only");
     RGBAC_REQUIRE(a->out_h == 2 * a->in_h && a->out_w == 2 * a->in_w, "out size mismatch for convT");
-    RGBAC_REQUIRE(9 * a->cin_pad <= a->k_pad, "k_pad too small");
-    p.Hm = a->in_h; p.Wm = a->in_w; p.sy = 1; p.ksize = 5; p.pad = 2;
-    nphase = 4;
+    s.Hm = a->in_h; s.Wm = a->in_w; s.sy = 1; s.ksize = 5; s.pad = 2;
+    s.nphase = 4;
+    ntaps_max = 9;
   } else if (a->mode == RGBAC_SUBPEL2) {
     RGBAC_REQUIRE(a->ksize == 3 && a->stride == 1, "SUBPEL2 is conv3x3 s1");
     RGBAC_REQUIRE(a->out_h == 2 * a->in_h && a->out_w == 2 * a->in_w, "out size mismatch for subpel");
-    RGBAC_REQUIRE(a->cout % 4 == 0, "subpel cout must be a multiple of 4");
     RGBAC_REQUIRE(a->act == RGBAC_ACT_NONE || a->act == RGBAC_ACT_GELU, "subpel supports NONE/GELU");
-    RGBAC_REQUIRE(!a->res0 && !a->res1 && !a->res2, "subpel has no residual epilogue");
-    RGBAC_REQUIRE(9 * a->cin_pad <= a->k_pad, "k_pad too small");
-    p.Hm = a->in_h; p.Wm = a->in_w; p.sy = 1; p.ksize = 3; p.pad = 1;
+    s.Hm = a->in_h; s.Wm = a->in_w; s.sy = 1; s.ksize = 3; s.pad = 1;
+    ntaps_max = 9;
   } else {
     RGBAC_REQUIRE(false, "unknown conv mode");
   }
-  const long long M = (long long)a->batch * p.Hm * p.Wm;
+  const long long M = (long long)a->batch * s.Hm * s.Wm;
   RGBAC_REQUIRE(M < (1ll << 31), "too many output pixels");
-  p.M = (int)M;
-  p.out_h = a->out_h;
-  p.out_w = a->out_w;
-  p.nsrc = a->nsrc;
-  p.sp0 = a->src[0].ptr; p.sld0 = a->src[0].ldc; p.send0 = a->src[0].channels;
-  p.sp1 = a->nsrc > 1 ? a->src[1].ptr : a->src[0].ptr;
-  p.sld1 = a->nsrc > 1 ? a->src[1].ldc : a->src[0].ldc;
-  p.send1 = p.send0 + (a->nsrc > 1 ? a->src[1].channels : 0);
-  p.sp2 = a->nsrc > 2 ? a->src[2].ptr : p.sp1;
-  p.sld2 = a->nsrc > 2 ? a->src[2].ldc : p.sld1;
-  p.send2 = p.send1 + (a->nsrc > 2 ? a->src[2].channels : 0);
-  p.cin_pad = a->cin_pad;
-  p.k_pad = a->k_pad;
-  p.cout = a->cout;
-  p.cout_pad = a->cout_pad;
-  p.w = a->weight;
-  p.bias = a->bias;
-  p.out = a->out;
-  p.out_ldc = a->out_ldc;
-  p.out_coff = a->out_coff;
-  p.act = a->act;
-  p.act_param = a->act_param;
-  p.square = a->square_input;
-  p.res0 = a->res0; p.ld0 = a->res0_ldc;
-  p.res1 = a->res1; p.ld1 = a->res1_ldc;
-  p.res2 = a->res2; p.ld2 = a->res2_ldc;
-  p.sel = a->sel;
+  s.M = (int)M;
+  s.out_h = a->out_h;
+  s.out_w = a->out_w;
+  s.act = a->act;
+  s.act_param = a->act_param;
+  s.square = a->square_input;
+  s.ksplit = a->ksplit;
+  s.ngroups = ngroups;
+  int max_cout = 0;
+  for (int i = 0; i < ngroups; ++i) {
+    const rgbac_conv_args* b = &args[i];
+    if (a->mode == RGBAC_SUBPEL2) {
+      RGBAC_REQUIRE(b->cout % 4 == 0, "subpel cout must be a multiple of 4");
+      RGBAC_REQUIRE(!b->res0 && !b->res1 && !b->res2, "subpel has no residual epilogue");
+    }
+    if (a->act == RGBAC_ACT_GAUSS) {
+      RGBAC_REQUIRE(a->mode == RGBAC_CONV && a->ksplit == 1, "GAUSS needs a plain conv, ksplit 1");
+      RGBAC_REQUIRE(b->cout % 2 == 0 && b->cout <= kTiles[a->tile].bn,
+                    "GAUSS needs (mu|sigma) channels in one N tile");
+      RGBAC_REQUIRE(b->partial, "GAUSS needs a partial-sum buffer");
+    }
+    int rc = fill_group(b, ntaps_max, d.g[i]);
+    if (rc) return rc;
+    if (b->cout > max_cout) max_cout = b->cout;
+  }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (a->dtype == RGBAC_F32) return launch_conv<float>(p, nphase, st);
-  return launch_conv<bf16_t>(p, nphase, st);
+  if (a->dtype == RGBAC_F32) return launch_conv<float>(d, a->tile, max_cout, st);
+  return launch_conv<bf16_t>(d, a->tile, max_cout, st);
+}
+
+extern "C" int rgbac_conv2d(const rgbac_conv_args* a, void* stream) {
+  return rgbac_conv2d_grouped(a, 1, stream);
 }

@@ -13,7 +13,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "librgbac_hip.so")
 
 F32, BF16 = 0, 1
-ACT = dict(none=0, gelu=1, relu=2, lrelu=3, tanh_half=4, gate=5, gdn=6, igdn=7, masksel=8)
+ACT = dict(none=0, gelu=1, relu=2, lrelu=3, tanh_half=4, gate=5, gdn=6, igdn=7, masksel=8,
+           gauss=9)
 CONV, CONVT_S2, SUBPEL2 = 0, 1, 2
 
 
@@ -39,6 +40,9 @@ class ConvArgs(ctypes.Structure):
         ("res1", ctypes.c_void_p), ("res1_ldc", ctypes.c_int64),
         ("res2", ctypes.c_void_p), ("res2_ldc", ctypes.c_int64),
         ("sel", ctypes.c_void_p),
+        ("tile", ctypes.c_int32), ("ksplit", ctypes.c_int32),
+        ("workspace", ctypes.c_void_p),
+        ("aux0", ctypes.c_void_p), ("aux1", ctypes.c_void_p), ("partial", ctypes.c_void_p),
     ]
 
 
@@ -48,6 +52,9 @@ SIGNATURES = {
     "rgbac_abi_version": [],
     "rgbac_last_error": [],
     "rgbac_conv2d": [ctypes.POINTER(ConvArgs), _VP],
+    "rgbac_conv_num_tiles": [],
+    "rgbac_conv2d_grouped": [ctypes.c_void_p, _I32, _VP],
+    "rgbac_conv_max_groups": [],
     "rgbac_winattn_core": [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _F,
                            _VP, _I64, _VP, _VP, _VP, _I64, _VP, _VP],
     "rgbac_gaussian_slice": [_I32, _I64, _I32, _VP, _I64, _VP, _I64, _VP, _I64, _VP,

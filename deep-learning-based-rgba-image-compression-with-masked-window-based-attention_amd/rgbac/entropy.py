@@ -145,7 +145,7 @@ class GaussianConditional(_EntropyModel):
 def eb_forward_hip(eb, z, z_hat, params, noise, partial, lik=None):
     """z, z_hat: Feat; params: packed_params(); partial: fp64 scratch."""
     npix = z.B * z.H * z.W
-    rt.launch("eb_forward_kernel", 0.0, 2.0 * npix * z.C * z.t.element_size(),
+    rt.timed("eb_forward_kernel", 0.0, 2.0 * npix * z.C * z.t.element_size(),
               lambda: _lib.call("rgbac_eb_forward", _lib.dtype_code(z.t.dtype), npix, z.C,
                                 z.ptr(), z.ldc, params.data_ptr(), _lib.ptr(noise), z_hat.ptr(),
                                 z_hat.ldc, _lib.ptr(lik), partial.data_ptr(),
@@ -155,7 +155,7 @@ def eb_forward_hip(eb, z, z_hat, params, noise, partial, lik=None):
 def gaussian_slice_hip(y, ycoff, nch, mu, sc, hat, noise, partial, lik=None):
     """One slice of GaussianConditional.forward + ste_round, all Feats (NHWC)."""
     npix = y.B * y.H * y.W
-    rt.launch("gaussian_slice_kernel", 0.0, 4.0 * npix * nch * y.t.element_size(),
+    rt.timed("gaussian_slice_kernel", 0.0, 4.0 * npix * nch * y.t.element_size(),
               lambda: _lib.call("rgbac_gaussian_slice", _lib.dtype_code(y.t.dtype), npix, nch,
                                 y.ptr(ycoff), y.ldc, mu.ptr(), mu.ldc, sc.ptr(), sc.ldc,
                                 _lib.ptr(noise), hat.ptr(), hat.ldc, _lib.ptr(lik),

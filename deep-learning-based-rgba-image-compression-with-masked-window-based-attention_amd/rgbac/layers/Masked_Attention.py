@@ -23,16 +23,22 @@ class ResidualUnit(nn.Module):
         self.relu = nn.GELU()
 
     def nhwc(self, x):
-        dt = x.t.dtype
-        c0, c2, c4 = self.conv[0], self.conv[2], self.conv[4]
-        t = rt.conv(rt.packed(c0, dt, rt.segs_of(x.src())), [x.src()], act="gelu")
-        t = rt.conv(rt.packed(c2, dt, rt.segs_of(t.src())), [t.src()], act="gelu")
-        return rt.conv(rt.packed(c4, dt, rt.segs_of(t.src())), [t.src()], act="gelu", res0=x)
+        return run_residual_units([(self, x)])[0]
 
     def forward(self, x):
         rt.check_gpu(x)
         with torch.no_grad():
             return rt.to_nchw(self.nhwc(rt.to_nhwc(x, torch.float32)))
+
+
+def run_residual_units(pairs):
+    """Independent ResidualUnits [(unit, x), ...] of equal shape as grouped launches:
+    1x1+GELU, 3x3+GELU, 1x1 (+identity, GELU) -- three launches for all units."""
+    from .TransformRGB import prep_conv
+    ts = rt.launch([prep_conv(u.conv[0], [x.src()], act="gelu") for u, x in pairs])
+    ts = rt.launch([prep_conv(u.conv[2], [t.src()], act="gelu") for (u, _), t in zip(pairs, ts)])
+    return rt.launch([prep_conv(u.conv[4], [t.src()], act="gelu", res0=x)
+                      for (u, x), t in zip(pairs, ts)])
 
 
 class Win_noShift_Attention(nn.Module):
@@ -48,12 +54,12 @@ class Win_noShift_Attention(nn.Module):
                                     conv1x1(N, N))
 
     def nhwc(self, x, mask):
-        a = x
-        for ru in self.conv_a:
-            a = ru.nhwc(a)
+        # the trunk (conv_a) and the attention branch (attn -> conv_b) are independent
+        # until the gate: their residual units run pairwise as 2-group launches
         b = self.attn.nhwc(x, mask)
-        for ru in list(self.conv_b)[:3]:
-            b = ru.nhwc(b)
+        a = x
+        for k in range(3):
+            a, b = run_residual_units([(self.conv_a[k], a), (self.conv_b[k], b)])
         pk = rt.packed(self.conv_b[3], x.t.dtype, rt.segs_of(b.src()))
         return rt.conv(pk, [b.src()], act="gate", res1=a, res2=x)
 

@@ -24,6 +24,11 @@ def _act_of(m):
 
 def run_conv(m, srcs, **kw):
     """Run nn.Conv2d / nn.ConvTranspose2d ``m`` over concatenated Feat sources."""
+    return rt.launch([prep_conv(m, srcs, **kw)])[0]
+
+
+def prep_conv(m, srcs, **kw):
+    """rt.Prepared record of ``m`` over ``srcs`` (for grouped launches)."""
     dt = srcs[0][0].t.dtype
     segs = rt.segs_of(*srcs)
     if isinstance(m, nn.ConvTranspose2d):
@@ -36,15 +41,19 @@ def run_conv(m, srcs, **kw):
     else:
         assert m.padding[0] == m.kernel_size[0] // 2 and m.dilation[0] == 1 and m.groups == 1
         pk = rt.packed(m, dt, segs)
-    return rt.conv(pk, srcs, **kw)
+    return rt.prepare(pk, srcs, **kw)
 
 
-def run_subpel(seq, srcs, act="none"):
+def prep_subpel(seq, srcs, act="none"):
     """compressai subpel_conv3x3 = Sequential(conv3x3(C, r^2 C), PixelShuffle(r)), r = 2."""
     assert isinstance(seq[1], nn.PixelShuffle) and seq[1].upscale_factor == 2
     dt = srcs[0][0].t.dtype
     pk = rt.packed(seq[0], dt, rt.segs_of(*srcs), rt.SUBPEL2)
-    return rt.conv(pk, srcs, act=act)
+    return rt.prepare(pk, srcs, act=act)
+
+
+def run_subpel(seq, srcs, act="none"):
+    return rt.launch([prep_subpel(seq, srcs, act)])[0]
 
 
 class EnhancementBlock(nn.Module):

@@ -8,7 +8,7 @@ import torch.nn as nn
 from .. import runtime as rt
 from ..entropy import EntropyBottleneck, GaussianConditional
 from ..layers.GDN import GDN
-from ..layers.TransformRGB import _act_of, run_conv
+from ..layers.TransformRGB import _act_of, prep_conv, run_conv
 from ..layers._blocks import conv, conv3x3, deconv, subpel_conv3x3  # noqa: F401
 from ._latent import latent_path
 from .AutoEncoderRGB_Journal import (_CompressionModelMixin, _hyper_analysis, _hyper_synthesis,
@@ -55,9 +55,14 @@ class ResBlock(nn.Module):
         self.conv3 = nn.Conv2d(num_filters // 2, num_filters, 1, stride=1)
 
     def nhwc(self, x):
-        t = run_conv(self.conv1, [x.src()], act="relu")
-        t = run_conv(self.conv2, [t.src()], act="relu")
-        return run_conv(self.conv3, [t.src()], res0=x)
+        return run_resblocks([(self, x)])[0]
+
+
+def run_resblocks(pairs):
+    """Independent ResBlocks [(block, x), ...] of equal shape as grouped launches."""
+    ts = rt.launch([prep_conv(b.conv1, [x.src()], act="relu") for b, x in pairs])
+    ts = rt.launch([prep_conv(b.conv2, [t.src()], act="relu") for (b, _), t in zip(pairs, ts)])
+    return rt.launch([prep_conv(b.conv3, [t.src()], res0=x) for (b, x), t in zip(pairs, ts)])
 
 
 class SimplifiedAttention(nn.Module):
@@ -75,9 +80,11 @@ class SimplifiedAttention(nn.Module):
         self.attention_ResBlock3 = ResBlock(num_filters)
 
     def nhwc(self, x):
-        tr = self.trunk_ResBlock3.nhwc(self.trunk_ResBlock2.nhwc(self.trunk_ResBlock1.nhwc(x)))
-        at = self.attention_ResBlock3.nhwc(
-            self.attention_ResBlock2.nhwc(self.attention_ResBlock1.nhwc(x)))
+        # trunk and attention branches are independent: ResBlock pairs as 2-group launches
+        tr, at = x, x
+        for k in (1, 2, 3):
+            tr, at = run_resblocks([(getattr(self, f"trunk_ResBlock{k}"), tr),
+                                    (getattr(self, f"attention_ResBlock{k}"), at)])
         return run_conv(self.conv1, [at.src()], act="gate", res1=tr, res2=x)
 
 

@@ -2,17 +2,26 @@
 (reference: models/AutoEncoderRGB_Journal.py:222-271,
 models/AutoEncoderMask_Journal.py:251-298), on the HIP path.
 
-Concatenations are never materialised: the slice stacks read up to three
-channel sources (latent means/scales, the y_hat prefix, the current
-pre-lrp slice) directly.  y_hat slices are written into one NHWC buffer YH
-that is the decoder input.  The lrp update ``y_hat += 0.5*tanh(lrp)`` is the
-last lrp conv's epilogue."""
+Restructured for the GPU without changing the arithmetic:
+  * concatenations are never materialised: the slice stacks read up to three
+    channel sources (latent means/scales, the y_hat prefix, the pre-lrp
+    slice) directly, and y_hat slices land in one NHWC buffer YH (the
+    decoder input); ``y_hat += 0.5*tanh(lrp)`` is the last lrp conv's epilogue;
+  * cc_mean and cc_scale stacks of a slice (and h_mean_s / h_scale_s) are
+    independent and run as 2-group launches;
+  * the last mean and scale convs form one block-diagonal conv producing
+    (mu | sigma) whose epilogue is the Gaussian conditional + quantiser + bits
+    (ACT_GAUSS): no mu/sigma round trip through HBM;
+  * slices i >= max_support_slices all see the same support
+    [latent, y_hat_0 .. y_hat_{msup-1}] (:241), so they are mutually
+    independent and run together as one wave of grouped launches.
+"""
 import torch
 import torch.nn as nn
 
 from .. import runtime as rt
-from ..entropy import eb_forward_hip, gaussian_slice_hip, reduce_blocks
-from ..layers.TransformRGB import run_conv, run_subpel
+from ..entropy import eb_forward_hip, reduce_blocks
+from ..layers.TransformRGB import prep_conv, prep_subpel, run_conv
 
 
 def _hyper_a(h_a, y):
@@ -22,21 +31,37 @@ def _hyper_a(h_a, y):
     return t
 
 
-def _hyper_s(h_s, z_hat):
-    t = z_hat
+def _hyper_s_pair(hs, z_hat):
+    """h_scale_s and h_mean_s (identical shapes, same input) as 2-group launches."""
+    ts = [z_hat] * len(hs)
     for idx in (0, 2, 4, 6, 8):
         act = "gelu" if idx != 8 else "none"
-        if isinstance(h_s[idx], nn.Sequential):
-            t = run_subpel(h_s[idx], [t.src()], act=act)
-        else:
-            t = run_conv(h_s[idx], [t.src()], act=act)
-    return t
+        preps = []
+        for h, t in zip(hs, ts):
+            if isinstance(h[idx], nn.Sequential):
+                preps.append(prep_subpel(h[idx], [t.src()], act=act))
+            else:
+                preps.append(prep_conv(h[idx], [t.src()], act=act))
+        ts = rt.launch(preps)
+    return ts
 
 
-def _stack(seq, srcs, out=None, out_coff=0, **last_kw):
-    t = run_conv(seq[0], srcs, act="gelu")
-    t = run_conv(seq[2], [t.src()], act="gelu")
-    return run_conv(seq[4], [t.src()], out=out, out_coff=out_coff, **last_kw)
+def _musigma_pack(mconv, sconv, dtype, cin):
+    """Block-diagonal (mu | sigma) conv from the last cc_mean / cc_scale convs."""
+    key = (dtype, cin) + tuple((p._version, p.data_ptr()) for p in
+                               (mconv.weight, mconv.bias, sconv.weight, sconv.bias))
+    ent = mconv.__dict__.get("_rgbac_musigma")
+    if ent is None or ent[0] != key:
+        with torch.no_grad():
+            cs, k = mconv.out_channels, mconv.kernel_size[0]
+            w = torch.zeros((2 * cs, 2 * cin, k, k), device=mconv.weight.device)
+            w[:cs, :cin] = mconv.weight.float()
+            w[cs:, cin:] = sconv.weight.float()
+            b = torch.cat([mconv.bias.float(), sconv.bias.float()])
+            pk = rt.PackedConv(w, b, rt.CONV, [(cin, cin), (cin, cin)], dtype)
+        mconv.__dict__["_rgbac_musigma"] = (key, pk)
+        ent = mconv.__dict__["_rgbac_musigma"]
+    return ent[1]
 
 
 def latent_path(model, y, training=False, noise_z=None, noise_y=None, debug=None):
@@ -56,36 +81,56 @@ def latent_path(model, y, training=False, noise_z=None, noise_y=None, debug=None
     if training:
         nz = noise_z if noise_z is not None else torch.rand((z.B, z.H, z.W, z.C), device=dev) - 0.5
     eb_forward_hip(eb, z, z_hat, eb.packed_params_cached(), nz, zpart, zlik)
-    scales = _hyper_s(model.h_scale_s, z_hat)
-    means = _hyper_s(model.h_mean_s, z_hat)
+    scales, means = _hyper_s_pair((model.h_scale_s, model.h_mean_s), z_hat)
 
     B, h, w = y.B, y.H, y.W
     npix = B * h * w
     YH = rt.new_feat(B, h, w, M, dt, dev)
-    pre = rt.new_feat(B, h, w, cs, dt, dev)
-    nb = reduce_blocks(npix * cs)
-    ypart = torch.empty((ns, nb), dtype=torch.float64, device=dev)
-    liks, mus, sigmas = [], [], []
-    for i in range(ns):
-        nsup = cs * min(i, msup)
-        msrc = [means.src(), YH.src(0, nsup)]
-        ssrc = [scales.src(), YH.src(0, nsup)]
-        mu = _stack(model.cc_mean_transforms[i], msrc)
-        sc = _stack(model.cc_scale_transforms[i], ssrc)
-        lik = None
-        if debug is not None:
-            lik = torch.empty((B, h, w, cs), dtype=torch.float32, device=dev)
-            liks.append(lik)
-            mus.append(mu)
-            sigmas.append(sc)
-        ny = None
-        if training:
-            ny = (noise_y[..., i * cs:(i + 1) * cs].contiguous() if noise_y is not None
-                  else torch.rand((B, h, w, cs), device=dev) - 0.5)
-        gaussian_slice_hip(y, i * cs, cs, mu, sc, pre, ny, ypart[i], lik)
-        _stack(model.lrp_transforms[i], msrc + [pre.src()], out=YH, out_coff=i * cs,
-               act="tanh_half", res1=pre)
+    ypart = torch.zeros((ns, -(-npix // 64)), dtype=torch.float64, device=dev)
+    liks = [None] * ns
+    waves = [[i] for i in range(min(msup, ns))]
+    if ns > msup:
+        waves.append(list(range(msup, ns)))
+    for wave in waves:
+        sup = [cs * min(i, msup) for i in wave]
+        # cc_mean / cc_scale stacks of every slice in the wave, as one grouped launch per layer
+        t1 = rt.launch(
+            [prep_conv(model.cc_mean_transforms[i][0], [means.src(), YH.src(0, n)], act="gelu")
+             for i, n in zip(wave, sup)] +
+            [prep_conv(model.cc_scale_transforms[i][0], [scales.src(), YH.src(0, n)], act="gelu")
+             for i, n in zip(wave, sup)])
+        k = len(wave)
+        t2 = rt.launch(
+            [prep_conv(model.cc_mean_transforms[i][2], [t1[j].src()], act="gelu")
+             for j, i in enumerate(wave)] +
+            [prep_conv(model.cc_scale_transforms[i][2], [t1[k + j].src()], act="gelu")
+             for j, i in enumerate(wave)])
+        # (mu | sigma) conv + GaussianConditional + ste_round + bits (one launch)
+        pres, preps = [], []
+        for j, i in enumerate(wave):
+            pre = rt.new_feat(B, h, w, cs, dt, dev)
+            pres.append(pre)
+            pk = _musigma_pack(model.cc_mean_transforms[i][4], model.cc_scale_transforms[i][4],
+                               dt, t2[j].ldc)
+            nyi = None
+            if training:
+                nyi = (noise_y[..., i * cs:(i + 1) * cs].contiguous() if noise_y is not None
+                       else torch.rand((B, h, w, cs), device=dev) - 0.5)
+            if debug is not None:
+                liks[i] = torch.empty((B, h, w, cs), dtype=torch.float32, device=dev)
+            preps.append(rt.prepare(pk, [t2[j].src(), t2[k + j].src()], out=pre, act="gauss",
+                                    res1=(y, i * cs), aux0=nyi, aux1=liks[i], partial=ypart[i]))
+        rt.launch(preps)
+        # lrp stacks: y_hat_i = pre_i + 0.5 * tanh(lrp([means, y_hat_<i, pre_i]))
+        l1 = rt.launch([prep_conv(model.lrp_transforms[i][0],
+                                  [means.src(), YH.src(0, n), pres[j].src()], act="gelu")
+                        for j, (i, n) in enumerate(zip(wave, sup))])
+        l2 = rt.launch([prep_conv(model.lrp_transforms[i][2], [l1[j].src()], act="gelu")
+                        for j, i in enumerate(wave)])
+        rt.launch([prep_conv(model.lrp_transforms[i][4], [l2[j].src()], out=YH,
+                             out_coff=i * cs, act="tanh_half", res1=pres[j])
+                   for j, i in enumerate(wave)])
     if debug is not None:
-        debug.update(z=z, z_hat=z_hat, z_lik=zlik, y_lik=liks, mu=mus, sigma=sigmas,
-                     latent_means=means, latent_scales=scales, y_hat=YH)
+        debug.update(z=z, z_hat=z_hat, z_lik=zlik, y_lik=liks, latent_means=means,
+                     latent_scales=scales, y_hat=YH)
     return YH, ypart, zpart

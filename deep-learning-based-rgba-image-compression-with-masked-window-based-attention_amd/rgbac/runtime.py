@@ -10,7 +10,9 @@ Data layout in HBM:
 torch is used here only for device allocation and the (cached) weight
 repack; every arithmetic op of the forward runs in librgbac_hip.so.
 """
-import math
+import ctypes
+import json
+import os
 
 import torch
 
@@ -28,18 +30,18 @@ class LaunchProfiler:
     def __init__(self):
         self.records = []   # (kernel name, flops, bytes, start event, end event)
 
-    def wrap(self, name, flops, nbytes, fn):
+    def wrap(self, name, flops, nbytes, fn, desc=None):
         s = torch.cuda.Event(enable_timing=True)
         e = torch.cuda.Event(enable_timing=True)
         s.record()
         fn()
         e.record()
-        self.records.append((name, flops, nbytes, s, e))
+        self.records.append((name, flops, nbytes, s, e, desc or name))
 
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for name, fl, nb, s, e in self.records:
+        for name, fl, nb, s, e, _ in self.records:
             d = out.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
             d["launches"] += 1
             d["ms"] += s.elapsed_time(e)
@@ -48,7 +50,21 @@ class LaunchProfiler:
         return out
 
 
-def launch(name, flops, nbytes, fn):
+    def layers(self):
+        """Per-descriptor totals: {desc: [launches, ms, flops, bytes]}."""
+        torch.cuda.synchronize()
+        out = {}
+        for name, fl, nb, s, e, desc in self.records:
+            d = out.setdefault(desc, [0, 0.0, 0.0, 0.0])
+            d[0] += 1
+            d[1] += s.elapsed_time(e)
+            d[2] += fl
+            d[3] += nb
+        return out
+
+
+def timed(name, flops, nbytes, fn):
+    """Run ``fn`` (one non-conv launch), attributed to ``name`` when profiling."""
     if PROFILER is None:
         fn()
     else:
@@ -59,14 +75,65 @@ def round_up(x, m):
     return (x + m - 1) // m * m
 
 
+# conv tile shapes of csrc/conv.hip (pixels x channels); index = rgbac_conv_args.tile
+TILES = [(128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 16)]
+KSPLITS = (1, 2, 4, 8)
+TUNE = os.environ.get("RGBAC_TUNE", "1") != "0"
+_tune_cache = {}          # shape key -> (tile, ksplit)
+FORCE = None              # (tile, ksplit) override, used by the tile/split-K tests
+
+
 def pick_cout_pad(cout):
-    """Smallest padded row count, preferring the widest N tile (64/32/16)."""
-    r16, r32, r64 = round_up(cout, 16), round_up(cout, 32), round_up(cout, 64)
-    if r64 == r16:
-        return r64
-    if r32 == r16:
-        return r32
-    return r16
+    """Packed weight rows per phase: every tile's N blocks stay inside the buffer."""
+    return round_up(cout, 128)
+
+
+def _candidates(M, cout, nst):
+    """(tile, ksplit) pairs worth timing for an M-pixel, cout-channel, nst-stage conv."""
+    out = []
+    n16 = round_up(cout, 16)
+    for t, (bm, bn) in enumerate(TILES):
+        if bn > 16 and bn > 2 * n16:
+            continue
+        blocks = -(-M // bm) * -(-cout // bn)
+        for ks in KSPLITS:
+            if ks > 1 and (nst // ks < 2 or blocks * ks > 4096 or blocks >= 512):
+                continue
+            out.append((t, ks))
+    return out
+
+
+def _heuristic(M, cout, nst):
+    n16 = round_up(cout, 16)
+    if n16 % 128 == 0:
+        t = 0
+    elif n16 >= 64:
+        t = 1
+    elif n16 > 16:
+        t = 3
+    else:
+        t = 5
+    bm, bn = TILES[t]
+    blocks = -(-M // bm) * -(-cout // bn)
+    ks = 1
+    while ks < 8 and blocks * ks < 256 and nst // (2 * ks) >= 4:
+        ks *= 2
+    return t, ks
+
+
+def tune_cache():
+    return dict(_tune_cache)
+
+
+def load_tune_cache(path):
+    with open(path) as fh:
+        for k, v in json.load(fh).items():
+            _tune_cache[k] = tuple(v)
+
+
+def save_tune_cache(path):
+    with open(path, "w") as fh:
+        json.dump({k: list(v) for k, v in sorted(_tune_cache.items())}, fh, indent=0)
 
 
 class Feat:
@@ -184,9 +251,16 @@ class PackedConv:
         self.segs = list(segs)
 
 
-def conv(pk, srcs, out=None, out_coff=0, act="none", act_param=0.0, res0=None, res1=None,
-         res2=None, sel=None, square=False, bias=True):
-    """Run a PackedConv over concatenated sources [(Feat, coff, nch), ...] -> Feat."""
+class Prepared:
+    """One conv's ABI record plus what the launcher needs (output, tuning key)."""
+    __slots__ = ("a", "out", "key", "mgrid", "nphase", "nst", "pk", "desc", "flops", "nbytes")
+
+
+def prepare(pk, srcs, out=None, out_coff=0, act="none", act_param=0.0, res0=None, res1=None,
+            res2=None, sel=None, square=False, bias=True, aux0=None, aux1=None, partial=None):
+    """Build the rgbac_conv_args record of one conv over sources [(Feat, coff, nch), ...].
+
+    ``res*`` are Feats on the output grid or (Feat, coff) channel slices."""
     f0 = srcs[0][0]
     B, H, W = f0.B, f0.H, f0.W
     dtype = f0.t.dtype
@@ -199,6 +273,8 @@ def conv(pk, srcs, out=None, out_coff=0, act="none", act_param=0.0, res0=None, r
         Ho, Wo, cstore = 2 * H, 2 * W, pk.cout
     else:
         Ho, Wo, cstore = 2 * H, 2 * W, pk.cout // 4
+    if act == "gauss":
+        cstore = pk.cout // 2
     if out is None:
         out = new_feat(B, Ho, Wo, cstore, dtype, f0.t.device)
     a = _lib.ConvArgs()
@@ -206,14 +282,14 @@ def conv(pk, srcs, out=None, out_coff=0, act="none", act_param=0.0, res0=None, r
     a.mode = pk.mode
     a.batch, a.in_h, a.in_w = B, H, W
     a.ksize, a.stride = pk.ksize, pk.stride
-    srcs = [s for s in srcs if s[2] > 0]
+    srcs = [sr for sr in srcs if sr[2] > 0]
     a.nsrc = len(srcs)
     for i, (f, coff, nch) in enumerate(srcs):
         assert f.B == B and f.H == H and f.W == W and f.t.dtype == dtype
         a.src[i].ptr = f.ptr(coff)
         a.src[i].ldc = f.ldc
         a.src[i].channels = nch
-    assert sum(s[2] for s in srcs) == pk.cin_pad, (sum(s[2] for s in srcs), pk.cin_pad)
+    assert sum(sr[2] for sr in srcs) == pk.cin_pad, (sum(sr[2] for sr in srcs), pk.cin_pad)
     a.cin_pad, a.k_pad = pk.cin_pad, pk.k_pad
     a.weight = pk.w.data_ptr()
     a.bias = pk.bias.data_ptr() if bias else None
@@ -227,23 +303,106 @@ def conv(pk, srcs, out=None, out_coff=0, act="none", act_param=0.0, res0=None, r
     a.square_input = 1 if square else 0
     for name, r in (("res0", res0), ("res1", res1), ("res2", res2)):
         if r is not None:
-            assert r.H == Ho and r.W == Wo and r.t.dtype == dtype
-            setattr(a, name, r.ptr())
-            setattr(a, name + "_ldc", r.ldc)
+            rf, rc = (r, 0) if isinstance(r, Feat) else r
+            assert rf.H == Ho and rf.W == Wo and rf.t.dtype == dtype
+            setattr(a, name, rf.ptr(rc))
+            setattr(a, name + "_ldc", rf.ldc)
     a.sel = None if sel is None else sel.data_ptr()
+    a.aux0 = None if aux0 is None else aux0.data_ptr()
+    a.aux1 = None if aux1 is None else aux1.data_ptr()
+    a.partial = None if partial is None else partial.data_ptr()
+    pr = Prepared()
+    pr.a, pr.out, pr.pk = a, out, pk
+    taps = 9 if pk.mode == CONVT_S2 else pk.ksize * pk.ksize
+    pr.mgrid = B * (H * W if pk.mode != CONV else Ho * Wo)
+    pr.nphase = 4 if pk.mode == CONVT_S2 else 1
+    pr.nst = -(-taps * pk.cin_pad // (32 if dtype == torch.float32 else 64))
+    pr.key = f"{a.dtype}/{pk.mode}/{pk.ksize}/{pk.stride}/{B}x{H}x{W}/{pk.cin_pad}/{pk.cout}/{act == 'gauss'}"
+    pr.flops = 2.0 * pr.mgrid * pk.cout * pk.cin * (25 if pk.mode == CONVT_S2 else taps)
+    es = f0.t.element_size()
+    pr.nbytes = es * (B * H * W * pk.cin + B * Ho * Wo * cstore) + pk.w.numel() * es
+    pr.desc = (f"m{pk.mode} k{pk.ksize}s{pk.stride} {pk.cin}->{pk.cout} {H}x{W}->{Ho}x{Wo} "
+               f"B{B} act={act}{' sq' if square else ''}")
+    return pr
+
+
+def _gauss_ok(t, cout):
+    return TILES[t][1] >= cout
+
+
+def launch(preps):
+    """Launch prepared convs (same geometry) as ONE grouped kernel; returns their outputs."""
+    n = len(preps)
+    p0 = preps[0]
+    dev = p0.out.t.device
+    gauss = p0.a.act == ACT["gauss"]
+    key = f"{p0.key}/g{n}"
+    keep = []
+    arr = (_lib.ConvArgs * n)()
+    for i, pr in enumerate(preps):
+        arr[i] = pr.a
+
+    def set_choice(t, ks):
+        for i, pr in enumerate(preps):
+            arr[i].tile, arr[i].ksplit = t, ks
+            arr[i].workspace = None
+            if ks > 1:
+                ws = torch.empty(ks * pr.nphase * pr.mgrid * round_up(pr.pk.cout, 16),
+                                 dtype=torch.float32, device=dev)
+                keep.append(ws)
+                arr[i].workspace = ws.data_ptr()
+
+    def run():
+        _lib.call("rgbac_conv2d_grouped", ctypes.addressof(arr), n, _lib.stream_ptr(dev))
+
+    choice = FORCE if (FORCE and not gauss) else _tune_cache.get(key)
+    if choice is None:
+        mtot = p0.mgrid * p0.nphase * n
+        cout = max(pr.pk.cout for pr in preps)
+        nst = max(pr.nst for pr in preps)
+        if gauss:
+            cands = [(t, 1) for t in range(len(TILES)) if _gauss_ok(t, cout)]
+        else:
+            cands = _candidates(mtot, cout, nst)
+        if TUNE and not torch.cuda.is_current_stream_capturing():
+            best = None
+            for cand in cands:
+                set_choice(*cand)
+                run()                                           # warm-up
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev0.record()
+                for _ in range(3):
+                    run()
+                ev1.record()
+                ev1.synchronize()
+                ms = ev0.elapsed_time(ev1)
+                if best is None or ms < best[0]:
+                    best = (ms, cand)
+            choice = best[1]
+        elif gauss:
+            choice = min(cands, key=lambda c: TILES[c[0]][1])
+        else:
+            choice = _heuristic(mtot, cout, nst)
+        _tune_cache[key] = choice
+    if gauss and not _gauss_ok(choice[0], max(pr.pk.cout for pr in preps)):
+        choice = (min((t for t in range(len(TILES)) if _gauss_ok(t, p0.pk.cout)),
+                      key=lambda t: TILES[t][1]), 1)
+    set_choice(*choice)
     if PROFILER is None:
-        _lib.call("rgbac_conv2d", a, _lib.stream_ptr(f0.t.device))
+        run()
     else:
-        taps = 25 if pk.mode == CONVT_S2 else pk.ksize * pk.ksize
-        mgrid = B * (H * W if pk.mode != CONV else Ho * Wo)
-        flops = 2.0 * mgrid * pk.cout * pk.cin * taps
-        es = f0.t.element_size()
-        nbytes = es * (B * H * W * pk.cin + B * Ho * Wo * cstore) + pk.w.numel() * es
-        wn = 4 if pk.cout_pad % 64 == 0 else (2 if pk.cout_pad % 32 == 0 else 1)
-        name = f"conv_kernel<{'f32' if dtype == torch.float32 else 'bf16'},{wn}>"
-        PROFILER.wrap(name, flops, nbytes,
-                      lambda: _lib.call("rgbac_conv2d", a, _lib.stream_ptr(f0.t.device)))
-    return out
+        bm, bn = TILES[choice[0]]
+        name = f"conv_kernel<{'f32' if p0.a.dtype == 0 else 'bf16'},{bm}x{bn}>"
+        desc = f"{name} ks{choice[1]} g{n} {p0.desc}"
+        PROFILER.wrap(name, sum(pr.flops for pr in preps), sum(pr.nbytes for pr in preps),
+                      run, desc)
+    return [pr.out for pr in preps]
+
+
+def conv(pk, srcs, **kw):
+    """Run one PackedConv over concatenated sources [(Feat, coff, nch), ...] -> Feat."""
+    return launch([prepare(pk, srcs, **kw)])[0]
 
 
 def feat_srcs(f):

@@ -52,6 +52,11 @@ enum rgbac_act {
   RGBAC_ACT_GDN = 6,       /* res1 / sqrt(v)       (use with square_input)     */
   RGBAC_ACT_IGDN = 7,      /* res1 * sqrt(v)                                    */
   RGBAC_ACT_MASKSEL = 8,   /* sel[p] ? v + res1 : res1   (window-drop residual) */
+  RGBAC_ACT_GAUSS = 9,     /* output channels are (mu | sigma) of a latent slice:
+                              GaussianConditional.forward + ste_round of res1 (= y
+                              slice) -> out = round(y-mu)+mu, aux1 = likelihood,
+                              partial[m-block] = sum of clamped bits; aux0 = noise
+                              (training) or NULL.  One N tile, ksplit 1.          */
 };
 
 enum rgbac_conv_mode {
@@ -81,7 +86,7 @@ typedef struct rgbac_conv_args {
   const void* weight;          /* packed [nphase][cout_pad][k_pad], see rgbac_conv_pack */
   const float* bias;           /* [cout_pad] fp32 (zero padded) or NULL            */
   int32_t cout;                /* real output channels (pre-shuffle for SUBPEL2)  */
-  int32_t cout_pad;            /* rows of the packed weight (multiple of 64)      */
+  int32_t cout_pad;            /* rows of the packed weight per phase (mult. of 128) */
   int32_t out_h, out_w;        /* stored output spatial size                       */
   void* out; int64_t out_ldc; int32_t out_coff; int32_t act;
   float act_param; int32_t square_input;   /* square the input (GDN norm pool) */
@@ -89,6 +94,14 @@ typedef struct rgbac_conv_args {
   const void* res1; int64_t res1_ldc;
   const void* res2; int64_t res2_ldc;
   const uint8_t* sel;                      /* MASKSEL: per output pixel flag   */
+  int32_t tile;                /* tile shape index, 0..rgbac_conv_num_tiles()-1:
+                                  0:128x128 1:128x64 2:64x64 3:128x32 4:64x32
+                                  5:128x16 6:64x16 (pixels x channels)          */
+  int32_t ksplit;              /* split-K factor (1 = fused epilogue in-kernel)   */
+  void* workspace;             /* ksplit>1: fp32 [ksplit][nphase][M][round16(cout)] */
+  const float* aux0;           /* GAUSS: fp32 noise [M][cout/2] or NULL            */
+  float* aux1;                 /* GAUSS: fp32 likelihood out [M][cout/2] or NULL   */
+  double* partial;             /* GAUSS: fp64 bits per M-tile block                */
 } rgbac_conv_args;
 
 int rgbac_abi_version(void);
@@ -103,6 +116,17 @@ const char* rgbac_last_error(void);
  *   models/AutoEncoderRGB_Journal.py:135-198,242-264 (h_a, h_*_s, slice stacks,
  *   lrp tanh update), models/AutoEncoderMask_Journal.py:96-244. */
 int rgbac_conv2d(const rgbac_conv_args* args, void* stream);
+int rgbac_conv_num_tiles(void);
+
+/* ngroups (1..rgbac_conv_max_groups()) independent convs in one launch.  All
+ * groups share dtype, mode, batch, input/output size, ksize, stride, tile,
+ * ksplit, act/act_param and square_input; weights, sources (cin may differ),
+ * cout, outputs, residuals and workspaces are per group.  Used for the
+ * cc_mean/cc_scale stacks (AutoEncoderRGB_Journal.py:240-252), the conv_a /
+ * conv_b residual units (Masked_Attention.py:182-189) and h_mean_s/h_scale_s
+ * (AutoEncoderRGB_Journal.py:231-232). */
+int rgbac_conv2d_grouped(const rgbac_conv_args* args, int ngroups, void* stream);
+int rgbac_conv_max_groups(void);
 
 /* Attention core of masked shifted-window MSA on a precomputed qkv tensor
  * (qkv = Linear(C,3C) applied per pixel by rgbac_conv2d).  For every window

@@ -210,3 +210,28 @@ def test_mask_pyramid(device):
         assert rel(g_, w_) < 1e-6
     r, lv = mask_pyramid(a.to(device) * 0.999, 2, round255=True)
     assert torch.equal(r.cpu(), torch.round(a * 0.999 * 255) / 255)
+
+
+# ------------------------------------------------------------------ every tile x split-K
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("tile", range(7))
+@pytest.mark.parametrize("ksplit", [1, 3])
+def test_conv_tiles_and_splitk(device, dtype, tile, ksplit):
+    """Every tile shape and split-K path against PyTorch, on conv / convT / 3 sources."""
+    rt = _rt()
+    from rgbac.layers.TransformRGB import run_conv
+    g = _gen(100 + tile)
+    cases = [(nn.Conv2d(96, 40, 3, padding=1), (96,)),
+             (nn.ConvTranspose2d(64, 24, 5, stride=2, padding=2, output_padding=1), (64,)),
+             (nn.Conv2d(56, 136, 5, stride=2, padding=2), (32, 16, 8))]
+    rt.FORCE = (tile, ksplit)
+    try:
+        for m, parts in cases:
+            xs = [torch.randn((2, c, 12, 20), generator=g) for c in parts]
+            want = m(torch.cat(xs, 1))
+            with torch.no_grad():
+                fs = [rt.to_nhwc(t.to(device), dtype) for t in xs]
+                got = rt.to_nchw(run_conv(m.to(device), [f.src() for f in fs]))
+            assert rel(got, want) < (2e-5 if dtype == torch.float32 else 2e-2), (tile, ksplit, m)
+    finally:
+        rt.FORCE = None
