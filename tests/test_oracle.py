@@ -1,0 +1,174 @@
+"""CPU: analytic known-answer tests pinning the oracle (oracle/ref_model.py).
+
+The reference ships no tests or vectors and cannot be imported here (SURVEY.md
+§8c), so these KATs are derived from first principles for each restated op.
+"""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import ref_model as ref
+
+
+def _sd_prefix(module, prefix):
+    return {f"{prefix}.{k}": v for k, v in module.state_dict().items()}
+
+
+def test_window_partition_roundtrip():
+    g = torch.Generator().manual_seed(0)
+    for ws, H, W in ((8, 16, 24), (4, 8, 12)):
+        x = torch.randn((2, H, W, 5), generator=g)
+        w = ref.window_partition(x, ws)
+        assert w.shape == (2 * (H // ws) * (W // ws), ws, ws, 5)
+        # window (b, wy, wx) holds x[b, wy*ws:(wy+1)*ws, wx*ws:(wx+1)*ws]
+        assert torch.equal(w[1], x[0, 0:ws, ws:2 * ws])
+        assert torch.equal(ref.window_reverse(w, ws, H, W), x)
+
+
+@pytest.mark.parametrize("ws", [4, 8])
+def test_relative_position_index(ws):
+    idx = ref.relative_position_index(ws)
+    N = ws * ws
+    assert idx.shape == (N, N) and idx.dtype == torch.int64
+    assert idx.min() == 0 and idx.max() == (2 * ws - 1) ** 2 - 1
+    center = (ws - 1) * (2 * ws - 1) + (ws - 1)
+    assert torch.all(idx.diagonal() == center)
+    assert torch.all(idx + idx.T == 2 * center)          # d(i,j) = -d(j,i)
+    i, j = 1 * ws + 2, 3 * ws + 0                          # (1,2) vs (3,0): dy=-2, dx=+2
+    assert idx[i, j] == (-2 + ws - 1) * (2 * ws - 1) + (2 + ws - 1)
+
+
+def test_shift_region_ids():
+    reg = ref._region_ids(1, 16, 16, 8, 4)[0, :, :, 0]
+    # rows [0,8) -> 0, [8,12) -> 1, [12,16) -> 2; same for columns; id = 3*r + c
+    assert reg[0, 0] == 0 and reg[0, 9] == 1 and reg[0, 13] == 2
+    assert reg[9, 0] == 3 and reg[13, 13] == 8 and reg[10, 14] == 5
+    assert torch.unique(reg).numel() == 9
+
+
+def test_gdn_known_answer():
+    """gamma <= bound -> gamma' = 2^-36 - 2^-36 = 0, so y = x / sqrt(beta^2 - 2^-36)."""
+    C = 6
+    beta = torch.linspace(0.5, 2.0, C)
+    sd = {"g.beta": beta, "g.gamma": torch.zeros(C, C)}
+    x = torch.randn((2, C, 3, 4), generator=torch.Generator().manual_seed(1))
+    ped = (2.0 ** -18) ** 2
+    b_eff = (torch.max(beta, torch.full_like(beta, (1e-6 + ped) ** 0.5)) ** 2 - ped)
+    want = x / torch.sqrt(b_eff).view(1, C, 1, 1)
+    assert torch.allclose(ref.gdn(x, sd, "g"), want, rtol=1e-6, atol=0)
+    assert torch.allclose(ref.gdn(x, sd, "g", inverse=True),
+                          x * torch.sqrt(b_eff).view(1, C, 1, 1), rtol=1e-6, atol=0)
+
+
+@pytest.mark.parametrize("sigma", [0.05, 0.11, 0.5, 1.0, 3.0, 40.0])
+def test_gaussian_likelihood_closed_form(sigma):
+    """y == mu -> symbol 0, p = erf(0.5 / (s*sqrt2)) with s = max(sigma, 0.11)."""
+    y = torch.full((1, 1, 2, 2), 0.25)
+    _, lik = ref.gc_forward(y, torch.full_like(y, sigma), y.clone())
+    s = max(sigma, float(np.float32(0.11)))
+    want = max(math.erf(0.5 / (s * math.sqrt(2.0))), 1e-9)
+    assert abs(lik[0, 0, 0, 0].item() - want) < 2e-6 * max(want, 1e-3)
+    bits = ref._bits(lik) / 4
+    assert abs(bits.item() - min(max(-math.log2(want + 1e-10), 0), 50)) < 1e-4
+
+
+def test_quantiser_half_to_even():
+    y = torch.tensor([0.5, 1.5, 2.5, -0.5, -1.5, 0.4999, 2.5001])
+    mu = torch.zeros_like(y)
+    out, _ = ref.gc_forward(y.view(1, 1, 1, -1), torch.ones(1, 1, 1, 7), mu.view(1, 1, 1, -1))
+    assert out.flatten().tolist() == [0.0, 2.0, 2.0, -0.0, -2.0, 0.0, 3.0]
+    assert torch.equal(ref.ste_round(y), torch.round(y))
+
+
+def test_entropy_bottleneck_init_is_affine():
+    """At compressai init (factors 0) the density model is affine: every layer is
+    softplus(M) @ t + b with softplus(M) = 1/scale/f_out; re-derived in numpy."""
+    import sys
+    from rgbac.entropy import EntropyBottleneck
+    torch.manual_seed(3)
+    eb = EntropyBottleneck(4)
+    sd = _sd_prefix(eb, "eb")
+    x = torch.linspace(-3, 3, 7).repeat(4, 1, 1)                  # (C,1,L)
+    got = ref.eb_logits_cumulative(sd, "eb", x).numpy()
+    scale = 10.0 ** (1 / 5)
+    f = (1, 3, 3, 3, 3, 1)
+    t = x.numpy().astype(np.float64)
+    for i in range(5):
+        m = np.full((f[i + 1], f[i]), 1.0 / scale / f[i + 1])
+        b = eb.state_dict()[f"_bias{i}"].numpy().astype(np.float64)    # (C, f_out, 1)
+        t = np.einsum("oi,cil->col", m, t) + b
+    np.testing.assert_allclose(got, t, rtol=1e-5, atol=1e-5)
+    # medians are quantiles[:, :, 1] = 0 at init
+    assert torch.all(ref.eb_medians(sd, "eb") == 0)
+
+
+def test_masked_attention_special_alphas():
+    from rgbac.layers.masked_win_attention import WinBasedAttention
+    torch.manual_seed(5)
+    m = WinBasedAttention(dim=16, num_heads=8, window_size=4, shift_size=2)
+    sd = _sd_prefix(m, "blk")
+    x = torch.randn((2, 16, 8, 12))
+    zero = torch.zeros((2, 1, 8, 12))
+    # all-transparent alpha: every window dropped -> block is the identity (x + 0)
+    assert torch.equal(ref.win_based_attention(x, zero, sd, "blk", 4, 2), x)
+    # all-opaque alpha == the unmasked variant (win_attention.py)
+    ones = torch.ones_like(zero)
+    a = ref.win_based_attention(x, ones, sd, "blk", 4, 2)
+    b = ref.win_based_attention(x, None, sd, "blk", 4, 2, masked=False)
+    assert torch.allclose(a, b, rtol=0, atol=1e-6)
+
+
+def test_reconstruct_error_cases():
+    g = torch.Generator().manual_seed(2)
+    x, y = torch.rand((2, 3, 8, 8), generator=g), torch.rand((2, 3, 8, 8), generator=g)
+    ones = torch.ones((2, 1, 8, 8))
+    assert torch.allclose(ref.reconstruct_error(x, y, ones), F.mse_loss(x, y), rtol=1e-6)
+    assert ref.reconstruct_error(x, y, torch.zeros_like(ones)).item() == 0.0
+    half = ones.clone()
+    half[..., :4] = 0
+    want = ((x - y)[..., 4:] ** 2).sum(dim=(1, 2, 3)) / (3 * 8 * 4)
+    assert torch.allclose(ref.reconstruct_error(x, y, half), want.mean(), rtol=1e-6)
+
+
+def test_supply_mask_pyramid():
+    a = torch.zeros((1, 1, 256, 256))
+    a[..., 100:110, 40:41] = 0.2
+    lv = ref.supply_mask(a)
+    assert [t.shape[-1] for t in lv] == [128, 64, 32, 16, 8, 4]
+    # with alpha >= 0 the non-zero pattern equals a 3x3/s2/p1 OR-pool chain
+    nz = (a > 0).float()
+    for t in lv:
+        nz = (F.max_pool2d(nz, 3, stride=2, padding=1) > 0).float()
+        assert torch.equal((t > 0).float(), nz)
+    assert abs(lv[0].max().item() - 0.2 * 3 / 9) < 1e-7
+
+
+def test_constraint_rgb():
+    t = torch.ones((1, 1, 5, 5))
+    t[0, 0, 2, 2] = 0                  # isolated zero -> 1
+    u = torch.zeros((1, 1, 5, 5))
+    u[0, 0, 1, 1] = 0.5                # isolated non-zero -> 0
+    assert torch.equal(ref.constraint_rgb(t), torch.ones_like(t))
+    assert torch.equal(ref.constraint_rgb(u), torch.zeros_like(u))
+
+
+@pytest.mark.slow
+def test_models_run_small():
+    from rgbac.models.AutoEncoderMask_Journal import AutoEncoder as MaskAE
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    torch.manual_seed(234)
+    net = AutoEncoder().eval()
+    x = torch.rand((1, 3, 64, 64))
+    a = torch.ones((1, 1, 64, 64))
+    me = ref.supply_mask(a)
+    with torch.no_grad():
+        out = ref.rgb_forward(net.state_dict(), x, a, a, *me[:4])
+    assert out[0].shape == x.shape and torch.isfinite(out[0]).all()
+    assert out[2] > 0 and abs(out[2] - out[3] - out[4]) < 1e-6
+    m = MaskAE().eval()
+    with torch.no_grad():
+        o2 = ref.mask_forward(m.state_dict(), a)
+    assert o2[0].shape == a.shape and torch.isfinite(o2[0]).all()
