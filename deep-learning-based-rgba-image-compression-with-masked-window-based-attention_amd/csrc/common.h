@@ -55,6 +55,26 @@ template <> struct Elem<bf16_t> {
   }
 };
 
+// One MFMA k-step on 16-byte operand chunks held per lane (lane l: row l&15,
+// chunk l>>4 of the 64-byte k-step):  acc[n][m] += sum_k A[n][k] * B[m][k].
+//   bf16: v_mfma_f32_16x16x32_bf16 (k-step = 32 elements)
+//   f32 : v_mfma_f32_16x16x4_f32 x4 (k-step = 16 elements; element e of every
+//         lane's chunk feeds MFMA e, a permutation of k applied to both operands)
+template <typename T>
+__device__ __forceinline__ void mma_step(f32x4& acc, uint4 a, uint4 b);
+template <>
+__device__ __forceinline__ void mma_step<bf16_t>(f32x4& acc, uint4 a, uint4 b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
+                                                __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
+}
+template <>
+__device__ __forceinline__ void mma_step<float>(f32x4& acc, uint4 a, uint4 b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
+}
+
 // ---------------------------------------------------------------- host side
 void set_error(const std::string& msg);
 int check_launch(const char* what);

@@ -98,21 +98,6 @@ __device__ __forceinline__ uint4 square_chunk<bf16_t>(uint4 v) {
 }
 
 template <typename T>
-__device__ __forceinline__ void mma_step(f32x4& acc, uint4 a, uint4 b);
-template <>
-__device__ __forceinline__ void mma_step<bf16_t>(f32x4& acc, uint4 a, uint4 b) {
-  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a),
-                                                __builtin_bit_cast(bf16x8, b), acc, 0, 0, 0);
-}
-template <>
-__device__ __forceinline__ void mma_step<float>(f32x4& acc, uint4 a, uint4 b) {
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.x), __uint_as_float(b.x), acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.y), __uint_as_float(b.y), acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.z), __uint_as_float(b.z), acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
-}
-
-template <typename T>
 __device__ __forceinline__ void load_res(const void* ptr, long long ld, long long opix, int n,
                                          int cout, float (&v)[4]) {
   const T* r = reinterpret_cast<const T*>(ptr) + opix * ld + n;

@@ -155,6 +155,216 @@ winattn_core_kernel(int batch, int H, int W, int C, int heads, int shift, int ma
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// MFMA variant for the model's two shapes: (ws 8, head dim 24, C 192) and
+// (ws 4, head dim 10, C 80).  Per head h, in LDS:
+//   Qs[64][DP] = q_h * scale, Ks[64][DP] = k_h     (DP = head dim padded to a k-step, zeros)
+//   Vt[16*CT][64] = v_h^T                          (key index contiguous)
+//   Ps[64][64]   = softmax probabilities          (zero outside a token's window)
+// S^T = K Q^T on MFMA puts one query per lane column, its keys in the lane's
+// accumulator registers + 3 partner lanes (l^16, l^32, l^48): the softmax row
+// reductions are two xor-shuffles.  O = P V on MFMA leaves 4 consecutive
+// channels of one query per lane -> channel-vector stores.
+template <typename T, int WS, int DH>
+__global__ void __launch_bounds__(256)
+winattn_mfma_kernel(int batch, int H, int W, int C, int heads, int shift, int masked,
+                    float scale, const T* __restrict__ qkv, long long ldq,
+                    const float* __restrict__ alpha, const float* __restrict__ bias,
+                    T* __restrict__ out, long long ldo, uint8_t* __restrict__ sel) {
+  constexpr int N = WS * WS;
+  constexpr int NWIN = 64 / N;
+  constexpr int EPV = Elem<T>::EPV;
+  constexpr int KSTEP = 4 * EPV;
+  constexpr int DP = (DH + KSTEP - 1) / KSTEP * KSTEP;
+  constexpr int QRS = DP / EPV + 1;            // Q/K row stride in 16-B chunks (+1 pad)
+  constexpr int PRS = 64 / EPV + 1;            // P / V^T row stride in chunks
+  constexpr int CT = (DH + 15) / 16;           // 16-channel output tiles
+  constexpr int ROWB = DH * (int)sizeof(T);
+  constexpr int VEC = (ROWB % 16 == 0) ? 16 : (ROWB % 8 == 0 ? 8 : 4);
+  constexpr int NP = ROWB / VEC;
+  constexpr int KT = (WS == 8) ? 4 : 1;        // key tiles per query tile
+  __shared__ __attribute__((aligned(16))) uint4 Qs[64 * QRS];
+  __shared__ __attribute__((aligned(16))) uint4 Ks[64 * QRS];
+  __shared__ __attribute__((aligned(16))) uint4 Vt[CT * 16 * PRS];
+  __shared__ __attribute__((aligned(16))) uint4 Ps[64 * PRS];
+  __shared__ int pix_s[64];
+  __shared__ int rid_s[64];
+  __shared__ int act_s[NWIN];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nwx = W / WS, nwy = H / WS;
+  const int total = batch * nwx * nwy;
+
+  // zero the LDS images (pad columns/rows and off-window P entries stay zero)
+  for (int e = tid; e < 64 * QRS; e += 256) Qs[e] = Ks[e] = make_uint4(0, 0, 0, 0);
+  for (int e = tid; e < CT * 16 * PRS; e += 256) Vt[e] = make_uint4(0, 0, 0, 0);
+  for (int e = tid; e < 64 * PRS; e += 256) Ps[e] = make_uint4(0, 0, 0, 0);
+  if (tid < NWIN) act_s[tid] = masked ? 0 : 1;
+  __syncthreads();
+  if (tid < 64) {
+    const int wi = tid / N, lt = tid % N;
+    const int gw = blockIdx.x * NWIN + wi;
+    int pix = -1, rid = 0;
+    if (gw < total) {
+      const int b = gw / (nwx * nwy);
+      const int rem = gw - b * nwx * nwy;
+      const int wy = rem / nwx, wx = rem - (rem / nwx) * nwx;
+      const int r = wy * WS + lt / WS, c = wx * WS + lt % WS;
+      int oy = r + shift; if (oy >= H) oy -= H;
+      int ox = c + shift; if (ox >= W) ox -= W;
+      pix = (b * H + oy) * W + ox;
+      if (masked && alpha[pix] != 0.0f) act_s[wi] = 1;
+      // region id in the shifted frame (masked_win_attention.py:196-207)
+      rid = 3 * (r < H - WS ? 0 : (r < H - shift ? 1 : 2)) + (c < W - WS ? 0 : (c < W - shift ? 1 : 2));
+    }
+    pix_s[tid] = pix;
+    rid_s[tid] = rid;
+  }
+  __syncthreads();
+  if (tid < 64 && pix_s[tid] >= 0 && sel) sel[pix_s[tid]] = (uint8_t)act_s[tid / N];
+  bool any = false;
+#pragma unroll
+  for (int w = 0; w < NWIN; ++w) any |= act_s[w] != 0;
+  if (!any) {
+    for (int e = tid; e < 64 * C; e += 256) {
+      const int t = e / C, ch = e - t * C;
+      if (pix_s[t] >= 0) Elem<T>::st(out + (long long)pix_s[t] * ldo + ch, 0.0f);
+    }
+    return;
+  }
+
+  const int qi = wave * 16 + fr;                 // this lane's query (row of S^T cols)
+  const int qwin = qi / N, qloc = qi % N;
+  const bool qact = act_s[qwin] != 0;
+  const int qpix = pix_s[qi];
+  const int qrid = rid_s[qi];
+
+  for (int h = 0; h < heads; ++h) {
+    // ---- stage q*scale, k (rows) and v^T (transposed) with VEC-byte loads
+    for (int e = tid; e < 3 * 64 * NP; e += 256) {
+      const int which = e / (64 * NP);
+      const int rem = e - which * 64 * NP;
+      const int t = rem / NP, pc = rem - t * NP;
+      const int pix = pix_s[t];
+      constexpr int EV = VEC / (int)sizeof(T);
+      float v[EV];
+      if (pix >= 0) {
+        const T* src = qkv + (long long)pix * ldq + which * C + h * DH + pc * EV;
+        if constexpr (VEC == 16) {
+          const uint4 raw = *reinterpret_cast<const uint4*>(src);
+          const T* el = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+          for (int q = 0; q < EV; ++q) v[q] = Elem<T>::ld(el + q);
+        } else if constexpr (VEC == 8) {
+          const uint2 raw = *reinterpret_cast<const uint2*>(src);
+          const T* el = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+          for (int q = 0; q < EV; ++q) v[q] = Elem<T>::ld(el + q);
+        } else {
+          const uint32_t raw = *reinterpret_cast<const uint32_t*>(src);
+          const T* el = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+          for (int q = 0; q < EV; ++q) v[q] = Elem<T>::ld(el + q);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < EV; ++q) v[q] = 0.f;
+      }
+      if (which == 2) {
+        T* vt = reinterpret_cast<T*>(Vt);
+#pragma unroll
+        for (int q = 0; q < EV; ++q) Elem<T>::st(vt + (pc * EV + q) * (PRS * EPV) + t, v[q]);
+      } else {
+        T* row = reinterpret_cast<T*>(which == 0 ? Qs : Ks) + t * (QRS * EPV) + pc * EV;
+#pragma unroll
+        for (int q = 0; q < EV; ++q) Elem<T>::st(row + q, which == 0 ? v[q] * scale : v[q]);
+      }
+    }
+    __syncthreads();
+
+    // ---- S^T tile(s): keys on the MFMA row axis, this wave's 16 queries on columns
+    f32x4 s[KT];
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      const int ktile = (WS == 8) ? kt : wave;   // ws 4: the query tile IS its window
+      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < DP / KSTEP; ++ks) {
+        const uint4 a = Ks[(ktile * 16 + fr) * QRS + 4 * ks + fq];
+        const uint4 b = Qs[(wave * 16 + fr) * QRS + 4 * ks + fq];
+        mma_step<T>(s[kt], a, b);
+      }
+    }
+    // ---- + relative position bias + shift mask, softmax over the window's keys
+    const float* bh = bias + (size_t)h * N * N;
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      const int ktile = (WS == 8) ? kt : wave;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kj = ktile * 16 + fq * 4 + r;
+        const int kloc = kj % N;
+        float v = s[kt][r] + bh[qloc * N + kloc];
+        if (shift > 0 && rid_s[kj] != qrid) v += -100.0f;
+        s[kt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float ex = expf(s[kt][r] - mx);
+        s[kt][r] = ex;
+        sum += ex;
+      }
+    sum += __shfl_xor(sum, 16);
+    sum += __shfl_xor(sum, 32);
+    const float inv = 1.0f / sum;
+    T* prow = reinterpret_cast<T*>(Ps) + qi * (PRS * EPV);
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      const int ktile = (WS == 8) ? kt : wave;
+      float pv[4] = {s[kt][0] * inv, s[kt][1] * inv, s[kt][2] * inv, s[kt][3] * inv};
+      Elem<T>::st4(prow + ktile * 16 + fq * 4, pv);
+    }
+    __syncthreads();
+
+    // ---- O^T = V^T P^T: channels on rows, this wave's queries on columns
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 64 / KSTEP; ++ks) {
+        const uint4 a = Vt[(ct * 16 + fr) * PRS + 4 * ks + fq];
+        const uint4 b = Ps[(wave * 16 + fr) * PRS + 4 * ks + fq];
+        mma_step<T>(o, a, b);
+      }
+      const int c0 = ct * 16 + fq * 4;
+      if (qpix >= 0 && c0 < DH) {
+        float ov[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) ov[r] = qact ? o[r] : 0.0f;
+        T* dst = out + (long long)qpix * ldo + h * DH + c0;
+        if constexpr (DH % 4 == 0) {
+          Elem<T>::st4(dst, ov);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (c0 + r < DH) Elem<T>::st(dst + r, ov[r]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace rgbac
 
 using namespace rgbac;
@@ -181,11 +391,22 @@ extern "C" int rgbac_winattn_core(int dtype, int batch, int h, int w, int channe
   hipLaunchKernelGGL((winattn_core_kernel<T, WS>), dim3(blocks), dim3(256), 0, st, batch, h, \
                      w, channels, heads, shift, masked, scale, (const T*)qkv, ldq, alpha,    \
                      bias, (T*)out, ldo, sel)
-  if (dtype == RGBAC_F32) {
+#define RGBAC_WM(T, WS, DH)                                                                \
+  hipLaunchKernelGGL((winattn_mfma_kernel<T, WS, DH>), dim3(blocks), dim3(256), 0, st, batch, h, \
+                     w, channels, heads, shift, masked, scale, (const T*)qkv, ldq, alpha,      \
+                     bias, (T*)out, ldo, sel)
+  const int dh = channels / heads;
+  const bool mfma_shape = (ws == 8 && dh == 24) || (ws == 4 && dh == 10);
+  if (mfma_shape && dtype == RGBAC_F32) {
+    if (ws == 8) RGBAC_WM(float, 8, 24); else RGBAC_WM(float, 4, 10);
+  } else if (mfma_shape) {
+    if (ws == 8) RGBAC_WM(bf16_t, 8, 24); else RGBAC_WM(bf16_t, 4, 10);
+  } else if (dtype == RGBAC_F32) {
     if (ws == 8) RGBAC_WA(float, 8); else RGBAC_WA(float, 4);
   } else {
     if (ws == 8) RGBAC_WA(bf16_t, 8); else RGBAC_WA(bf16_t, 4);
   }
 #undef RGBAC_WA
-  return check_launch("winattn_core_kernel");
+#undef RGBAC_WM
+  return check_launch("winattn_core");
 }

@@ -35,6 +35,10 @@ def prep_conv(m, srcs, **kw):
         k, s = m.kernel_size[0], m.stride[0]
         if k == 1 and s == 1:
             pk = rt.packed(m, dt, segs, rt.CONV, transposed=True)
+        elif m.out_channels <= 4:
+            # tiny Cout: one conv3x3 with 4*Cout rows + PixelShuffle store beats 4 phases
+            assert k == 5 and s == 2 and m.padding[0] == 2 and m.output_padding[0] == 1
+            pk = rt.packed(m, dt, segs, rt.SUBPEL2, transposed=True)
         else:
             assert k == 5 and s == 2 and m.padding[0] == 2 and m.output_padding[0] == 1
             pk = rt.packed(m, dt, segs, rt.CONVT_S2)

@@ -218,6 +218,23 @@ class PackedConv:
         if transposed and mode == CONV:
             # ConvTranspose2d(k=1, s=1, p=0): a 1x1 conv with W^T
             w = w.transpose(0, 1)
+        if transposed and mode == SUBPEL2:
+            # ConvTranspose2d(5, s=2, p=2, op=1) == conv3x3(4*Cout) + PixelShuffle(2):
+            # output parity (py, px) of channel c is conv channel 4c + 2py + px, and its
+            # 3x3 tap (a, b) (input offset a-1, b-1) is ConvT tap (py + 4 - 2a, px + 4 - 2b).
+            cin_t, cout_t = w.shape[0], w.shape[1]
+            ws = torch.zeros((4 * cout_t, cin_t, 3, 3), device=dev)
+            for py in (0, 1):
+                for px in (0, 1):
+                    for ta in range(3):
+                        for tb in range(3):
+                            ky, kx = py + 4 - 2 * ta, px + 4 - 2 * tb
+                            if ky <= 4 and kx <= 4:
+                                ws[2 * py + px::4, :, ta, tb] = w[:, :, ky, kx].t()
+            w = ws
+            if bias is not None:
+                bias = bias.detach().float().repeat_interleave(4)
+            stride = 1
         if mode == CONVT_S2:
             cin, cout, k, _ = w.shape
             assert k == 5 and stride == 2

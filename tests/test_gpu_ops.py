@@ -235,3 +235,17 @@ def test_conv_tiles_and_splitk(device, dtype, tile, ksplit):
             assert rel(got, want) < (2e-5 if dtype == torch.float32 else 2e-2), (tile, ksplit, m)
     finally:
         rt.FORCE = None
+
+
+@pytest.mark.parametrize("dim,ws", [(96, 8), (64, 4)])
+def test_win_attention_generic_head_dims(device, dim, ws):
+    """Head dims other than the model's (24 / 10) take the generic VALU core."""
+    from rgbac.layers.masked_win_attention import WinBasedAttention
+    g = _gen(dim * ws)
+    m = WinBasedAttention(dim=dim, num_heads=8, window_size=ws, shift_size=ws // 2)
+    x = torch.randn((1, dim, 2 * ws, 3 * ws), generator=g)
+    a = _alpha("half", 1, 2 * ws, 3 * ws, g)
+    sd = {"blk." + k: v for k, v in m.state_dict().items()}
+    want = ref.win_based_attention(x, a, sd, "blk", ws, ws // 2)
+    got = m.to(device)(x.to(device), a.to(device))
+    assert rel(got, want) < 2e-5

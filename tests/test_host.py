@@ -194,3 +194,16 @@ def test_cpu_tensors_fail_loudly():
     from rgbac.layers.GDN import GDN
     with pytest.raises(RuntimeError, match="GPU"):
         GDN(8)(torch.randn(1, 8, 4, 4))
+
+
+@pytest.mark.parametrize("cout", [1, 3, 4])
+def test_convtranspose_small_cout_as_subpel(cout):
+    """ConvTranspose2d(5, s2, p2, op1) repacked as conv3x3(4*Cout) + PixelShuffle(2)."""
+    from rgbac import runtime as rt
+    g = torch.Generator().manual_seed(cout)
+    m = torch.nn.ConvTranspose2d(16, cout, 5, stride=2, padding=2, output_padding=1)
+    x = torch.randn((2, 16, 5, 6), generator=g)
+    pk = rt.PackedConv(m.weight, m.bias, rt.SUBPEL2, [(16, 16)], torch.float32, stride=2,
+                       transposed=True)
+    assert pk.mode == rt.SUBPEL2 and pk.ksize == 3 and pk.stride == 1 and pk.cout == 4 * cout
+    assert torch.allclose(_emulate(pk, [x], 5, 6), m(x), atol=1e-5)
