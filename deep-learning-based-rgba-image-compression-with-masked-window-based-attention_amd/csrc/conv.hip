@@ -58,6 +58,7 @@ struct ConvGroup {                  // per-group operands
 };
 
 struct ConvShared {
+  double rWm, rHm;                  // 1/Wm, 1/Hm for divide-free pixel decode
   int mode, batch, in_h, in_w, Hm, Wm, out_h, out_w, M, sy;
   int ksize, pad;
   int act; float act_param; int square;
@@ -70,6 +71,16 @@ struct ConvArgsDev {
 };
 
 __device__ uint4 g_zero_page[64];   // zero source for padding taps (static, never written)
+
+// n / d for 0 <= n < 2^31 via a double reciprocal and one correction step
+// (|n*rd - n/d| < 2^-21, so the truncated quotient is off by at most one).
+__device__ __forceinline__ int udiv(int n, int d, double rd) {
+  int q = (int)((double)n * rd);
+  const int r = n - q * d;
+  if (r < 0) --q;
+  else if (r >= d) ++q;
+  return q;
+}
 
 __device__ __forceinline__ float gelu_f(float v) {
   return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f));
@@ -200,6 +211,86 @@ __device__ __forceinline__ void epilogue4(const ConvShared& s, const ConvGroup& 
   }
 }
 
+// Epilogue of one pixel row held by a lane: channels nn[j]..nn[j]+3 for j < TN.
+// The pixel index is decoded once and every residual load of the row is issued
+// before any store (stores could alias later loads in program order otherwise,
+// which serialises one memory latency per 16x16 tile).
+template <typename T, int TN>
+__device__ __forceinline__ void epilogue_row(const ConvShared& s, const ConvGroup& g, int ph, int m,
+                                             const int (&nn)[TN], float (&v)[TN][4]) {
+  const int t = udiv(m, s.Wm, s.rWm);
+  const int mx = m - t * s.Wm;
+  const int b = udiv(t, s.Hm, s.rHm);
+  const int my = t - b * s.Hm;
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+    if (nn[j] < g.cout)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[j][r] += (g.bias ? g.bias[nn[j] + r] : 0.0f);
+  T* out = reinterpret_cast<T*>(g.out);
+  if (s.mode == RGBAC_SUBPEL2) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (nn[j] >= g.cout) continue;
+      const int cc = nn[j] >> 2;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float x = v[j][r];
+        if (s.act == RGBAC_ACT_GELU) x = gelu_f(x);
+        const int oy = 2 * my + (r >> 1), ox = 2 * mx + (r & 1);
+        const long long o = ((long long)(b * s.out_h + oy) * s.out_w + ox) * g.out_ldc + g.out_coff + cc;
+        Elem<T>::st(out + o, x);
+      }
+    }
+    return;
+  }
+  long long opix;
+  if (s.mode == RGBAC_CONVT_S2)
+    opix = (long long)(b * s.out_h + 2 * my + (ph >> 1)) * s.out_w + 2 * mx + (ph & 1);
+  else
+    opix = (long long)(b * s.out_h + my) * s.out_w + mx;
+  float r0[TN][4], r1[TN][4], r2[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) r0[j][r] = r1[j][r] = r2[j][r] = 0.0f;
+    if (nn[j] >= g.cout) continue;
+    if (g.res0) load_res<T>(g.res0, g.ld0, opix, nn[j], g.cout, r0[j]);
+    if (g.res1) load_res<T>(g.res1, g.ld1, opix, nn[j], g.cout, r1[j]);
+    if (g.res2) load_res<T>(g.res2, g.ld2, opix, nn[j], g.cout, r2[j]);
+  }
+  const bool on = s.act != RGBAC_ACT_MASKSEL || g.sel[opix] != 0;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    if (nn[j] >= g.cout) continue;
+    float* vv = v[j];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float x = vv[r] + r0[j][r];
+      switch (s.act) {
+        case RGBAC_ACT_GELU: x = gelu_f(x); break;
+        case RGBAC_ACT_RELU: x = x > 0.f ? x : 0.f; break;
+        case RGBAC_ACT_LRELU: x = x > 0.f ? x : x * s.act_param; break;
+        case RGBAC_ACT_TANH_HALF: x = r1[j][r] + 0.5f * tanhf(x); break;
+        case RGBAC_ACT_GATE: x = r1[j][r] * sigmoid_f(x); break;
+        case RGBAC_ACT_GDN: x = r1[j][r] / sqrtf(x); break;
+        case RGBAC_ACT_IGDN: x = r1[j][r] * sqrtf(x); break;
+        case RGBAC_ACT_MASKSEL: x = on ? r1[j][r] + x : r1[j][r]; break;
+        default: break;
+      }
+      vv[r] = x + r2[j][r];
+    }
+    const long long base = opix * g.out_ldc + g.out_coff + nn[j];
+    if (nn[j] + 3 < g.cout) {
+      Elem<T>::st4(out + base, v[j]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (nn[j] + r < g.cout) Elem<T>::st(out + base + r, vv[r]);
+    }
+  }
+}
+
 // GaussianConditional + ste_round on a (mu | sigma) conv output (ACT_GAUSS):
 //   hat = round(y - mu) + mu -> out;  v = |(train ? y + noise : hat) - mu|;
 //   lik = max(Phi((.5-v)/s) - Phi((-.5-v)/s), 1e-9), s = max(sigma, .11);
@@ -306,10 +397,10 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
     const int m = m0 + 8 * (j - IA) + lrow;
     bval[i] = !isA[i] && m < s.M;
     const int mm = bval[i] ? m : 0;
-    const int mx = mm % s.Wm;
-    const int t = mm / s.Wm;
-    bb[i] = t / s.Hm;
-    biy[i] = (t % s.Hm) * s.sy;
+    const int t = udiv(mm, s.Wm, s.rWm);
+    const int mx = mm - t * s.Wm;
+    bb[i] = udiv(t, s.Hm, s.rHm);
+    biy[i] = (t - bb[i] * s.Hm) * s.sy;
     bix[i] = mx * s.sy;
   }
 
@@ -437,22 +528,29 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
   }
 
   // ---- epilogue: lane owns channels n..n+3 of pixel m for every (j, i) tile
+  int nn[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) nn[j] = n0 + wn * TN * 16 + j * 16 + fq * 4;
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = m0 + wm * TM * 16 + i * 16 + fr;
     if (m >= s.M) continue;
+    if (s.ksplit > 1) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * TN * 16 + j * 16 + fq * 4;
-      if (n >= g.cout) continue;
-      float v[4] = {acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]};
-      if (s.ksplit > 1) {
-        float* w = g.ws + (((size_t)split * s.nphase + phase) * s.M + m) * g.cout16 + n;
-        *reinterpret_cast<float4*>(w) = make_float4(v[0], v[1], v[2], v[3]);
-      } else {
-        epilogue4<T>(s, g, phase, m, n, v);
+      for (int j = 0; j < TN; ++j) {
+        if (nn[j] >= g.cout) continue;
+        float* w = g.ws + (((size_t)split * s.nphase + phase) * s.M + m) * g.cout16 + nn[j];
+        *reinterpret_cast<float4*>(w) =
+            make_float4(acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]);
       }
+      continue;
     }
+    float v[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[j][r] = acc[j][i][r];
+    epilogue_row<T, TN>(s, g, phase, m, nn, v);
   }
 }
 
@@ -479,15 +577,336 @@ __global__ void __launch_bounds__(256) conv_splitk_epilogue(const ConvArgsDev ar
   }
 }
 
+// ---------------------------------------------------------------------------
+// Weight-resident persistent variant (small K: 1x1 convs, GDN, qkv/proj,
+// DSE 3x3 at 32 channels, ...).  Each workgroup DMAs its BN x K weight panel
+// into LDS ONCE, then streams pixel tiles t = blockIdx.x + i*gridDim.x through
+// a 3-deep B ring.  Stages are numbered by one flat counter across tiles, so
+// the next tile's loads are in flight while the current tile's epilogue runs.
+// Requires nst <= NSA stages of K, ksplit == 1, no GAUSS epilogue.
+template <typename T, int BM, int BN, int WGM, int WGN, int NSA>
+__global__ void __launch_bounds__(256) conv_wres_kernel(const ConvArgsDev args) {
+  constexpr int EPV = Elem<T>::EPV;
+  constexpr int KS = 8 * EPV;
+  constexpr int TM = BM / WGM / 16;
+  constexpr int TN = BN / WGN / 16;
+  constexpr int IA = BN / 8, IB = BM / 8;
+  constexpr int LWA = (IA + 3) / 4, LWB = (IB + 3) / 4;
+  constexpr int NB = 3;
+  static_assert(WGM * WGN == 4 && TM >= 1 && TN >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) uint4 smem[NSA * BN * 8 + NB * BM * 8];
+  uint4* const Ares = smem;
+  uint4* const Bring = smem + NSA * BN * 8;
+
+  const ConvShared& s = args.s;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int phase = blockIdx.z % s.nphase;
+  const int gi = blockIdx.z / s.nphase;
+  const ConvGroup& g = args.g[gi];
+  const int n0 = blockIdx.y * BN;
+  if (n0 >= g.cout) return;
+  const int py = phase >> 1, px = phase & 1;
+  int ntaps, tw;
+  if (s.mode == RGBAC_CONVT_S2) {
+    tw = 3 - px;
+    ntaps = (3 - py) * tw;
+  } else {
+    tw = s.ksize;
+    ntaps = s.ksize * s.ksize;
+  }
+  const int nst = (ntaps * g.cin_pad + KS - 1) / KS;
+  const int mtiles = (s.M + BM - 1) / BM;
+  const int mine = blockIdx.x < mtiles ? (mtiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  const int Q = mine * nst;
+  const int lrow = lane >> 3;
+  const int c = (lane & 7) ^ lrow;
+
+  // ---- resident weight panel: all nst stages of rows n0..n0+BN-1
+  const T* wbase = reinterpret_cast<const T*>(g.w) + (size_t)phase * g.rows * g.k_pad;
+  for (int st = 0; st < nst; ++st) {
+#pragma unroll
+    for (int i = 0; i < LWA; ++i) {
+      int j = wave + 4 * i;
+      if (j >= IA) j = IA - 1;
+      dma16(wbase + (size_t)(n0 + 8 * j + lrow) * g.k_pad + st * KS + c * EPV,
+            Ares + st * BN * 8 + j * 64);
+    }
+  }
+
+  auto issueB = [&](int q) {
+    const int tl = q / nst;
+    const int st = q - tl * nst;
+    const int m0 = (blockIdx.x + tl * gridDim.x) * BM;
+    const int k = st * KS + c * EPV;
+    const int tap = k / g.cin_pad;
+    const int ci = k - tap * g.cin_pad;
+    const int ty = tap / tw, tx = tap - ty * tw;
+    int dy, dx;
+    if (s.mode == RGBAC_CONVT_S2) {
+      dy = 1 - ty; dx = 1 - tx;
+    } else {
+      dy = ty - s.pad; dx = tx - s.pad;
+    }
+    const void* sp;
+    long long sld;
+    int cs;
+    bool kval = tap < ntaps;
+    if (ci < g.send0) {
+      sp = g.sp0; sld = g.sld0; cs = ci;
+    } else if (ci < g.send1) {
+      sp = g.sp1; sld = g.sld1; cs = ci - g.send0;
+    } else {
+      sp = g.sp2; sld = g.sld2; cs = ci - g.send1;
+      kval = kval && ci < g.send2;
+    }
+    const T* src = reinterpret_cast<const T*>(sp);
+    uint4* buf = Bring + (q % NB) * BM * 8;
+#pragma unroll
+    for (int i = 0; i < LWB; ++i) {
+      int j = wave + 4 * i;
+      if (j >= IB) j = IB - 1;
+      const int m = m0 + 8 * j + lrow;
+      const void* gp = (const void*)g_zero_page;
+      if (kval && m < s.M) {
+        const int t = udiv(m, s.Wm, s.rWm);
+        const int mx = m - t * s.Wm;
+        const int b = udiv(t, s.Hm, s.rHm);
+        const int iy = (t - b * s.Hm) * s.sy + dy, ix = mx * s.sy + dx;
+        if (iy >= 0 && iy < s.in_h && ix >= 0 && ix < s.in_w)
+          gp = (const void*)(src + ((long long)(b * s.in_h + iy) * s.in_w + ix) * sld + cs);
+      }
+      dma16(gp, buf + j * 64);
+    }
+  };
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wm = wave % WGM, wn = wave / WGM;
+  const int fr = lane & 15, fq = lane >> 4, sw = lane & 7;
+  int nn[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) nn[j] = n0 + wn * TN * 16 + j * 16 + fq * 4;
+
+  if (Q > 0) issueB(0);
+  if (Q > 1) issueB(1);
+  for (int q = 0; q < Q; ++q) {
+    if (q + 1 < Q) wait_vm<LWB>(); else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (q + 2 < Q) issueB(q + 2);
+    const int tl = q / nst;
+    const int st = q - tl * nst;
+    const uint4* As = Ares + st * BN * 8;
+    const uint4* Bs = Bring + (q % NB) * BM * 8;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = (4 * ks + fq) ^ sw;
+      uint4 a[TN], b[TM];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) a[j] = As[(wn * TN * 16 + j * 16 + fr) * 8 + chunk];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        b[i] = Bs[(wm * TM * 16 + i * 16 + fr) * 8 + chunk];
+        if (s.square) b[i] = square_chunk<T>(b[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) mma_step<T>(acc[j][i], a[j], b[i]);
+    }
+    if (st == nst - 1) {
+      const int m0 = (blockIdx.x + tl * gridDim.x) * BM;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm * TM * 16 + i * 16 + fr;
+        float v[TN][4];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[j][r] = acc[j][i][r];
+          acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        if (m < s.M) epilogue_row<T, TN>(s, g, phase, m, nn, v);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Direct small-K variant (CONV mode, K <= NKS k-steps).  The workgroup's weight
+// panel (16*NT rows x K) is loaded into LDS once; then every WAVE walks its own
+// 16-pixel tiles (tile = (blockIdx.x*4 + wave) + i*gridDim.x*4): the im2col row
+// of pixel (lane&15), chunk (lane>>4) of every k-step, is loaded straight into
+// VGPRs (one 16-byte load per k-step; zero for padding), the NT x nks MFMAs run
+// from LDS weight fragments, and the fused epilogue stores the tile.  No
+// barrier after the weight load: latency is hidden by the other resident waves.
+template <typename T, int NT, int NKS>
+__global__ void __launch_bounds__(256) conv_direct_kernel(const ConvArgsDev args, int rs) {
+  constexpr int EPV = Elem<T>::EPV;
+  constexpr int KSTEP = 4 * EPV;
+  constexpr int BN = 16 * NT;
+  extern __shared__ __attribute__((aligned(16))) uint4 Wl[];   // [BN][rs] chunks
+  __shared__ int ktab[NKS * 4];   // per (k-step, chunk): valid | src | dx | dy | channel
+
+  const ConvShared& s = args.s;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const ConvGroup& g = args.g[blockIdx.z];
+  const int n0 = blockIdx.y * BN;
+  if (n0 >= g.cout) return;
+  const int ntaps = s.ksize * s.ksize;
+  const int nks = (ntaps * g.cin_pad + KSTEP - 1) / KSTEP;
+  const T* wbase = reinterpret_cast<const T*>(g.w);
+  for (int e = tid; e < BN * nks * 4; e += 256) {
+    const int row = e / (nks * 4), ch = e - row * (nks * 4);
+    Wl[row * rs + ch] = *reinterpret_cast<const uint4*>(wbase + (size_t)(n0 + row) * g.k_pad + ch * EPV);
+  }
+  if (tid < NKS * 4) {
+    const int st = tid >> 2, q = tid & 3;
+    const int k = st * KSTEP + q * EPV;
+    const int tap = k / g.cin_pad;
+    const int ci = k - tap * g.cin_pad;
+    const int ty = tap / s.ksize, tx = tap - ty * s.ksize;
+    int src, cs;
+    bool ok = st < nks && tap < ntaps;
+    if (ci < g.send0) { src = 0; cs = ci; }
+    else if (ci < g.send1) { src = 1; cs = ci - g.send0; }
+    else { src = 2; cs = ci - g.send1; ok = ok && ci < g.send2; }
+    ktab[tid] = cs | ((ty - s.pad + 4) << 12) | ((tx - s.pad + 4) << 15) | (src << 18) | ((int)ok << 20);
+  }
+  __syncthreads();
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ntile = (s.M + 15) / 16;
+  for (int tile = blockIdx.x * 4 + wave; tile < ntile; tile += gridDim.x * 4) {
+    const int m = tile * 16 + fr;
+    const int mm = m < s.M ? m : s.M - 1;
+    const int t = udiv(mm, s.Wm, s.rWm);
+    const int x = mm - t * s.Wm;
+    const int b = udiv(t, s.Hm, s.rHm);
+    const int y = t - b * s.Hm;
+    uint4 bv[NKS];
+#pragma unroll
+    for (int st = 0; st < NKS; ++st) {
+      bv[st] = make_uint4(0, 0, 0, 0);
+      if (st < nks) {
+        const int e = ktab[st * 4 + fq];
+        const int iy = y * s.sy + ((e >> 12) & 7) - 4, ix = x * s.sy + ((e >> 15) & 7) - 4;
+        const int src = (e >> 18) & 3;
+        if ((e >> 20) && iy >= 0 && iy < s.in_h && ix >= 0 && ix < s.in_w) {
+          const T* base = reinterpret_cast<const T*>(src == 0 ? g.sp0 : (src == 1 ? g.sp1 : g.sp2));
+          const long long ld = src == 0 ? g.sld0 : (src == 1 ? g.sld1 : g.sld2);
+          bv[st] = *reinterpret_cast<const uint4*>(
+              base + ((long long)(b * s.in_h + iy) * s.in_w + ix) * ld + (e & 0xFFF));
+        }
+        if (s.square) bv[st] = square_chunk<T>(bv[st]);
+      }
+    }
+    f32x4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int st = 0; st < NKS; ++st) {
+      if (st < nks) {
+#pragma unroll
+        for (int j = 0; j < NT; ++j) mma_step<T>(acc[j], Wl[(j * 16 + fr) * rs + st * 4 + fq], bv[st]);
+      }
+    }
+    if (m < s.M) {
+      constexpr int CH = NT < 4 ? NT : 4;          // epilogue in chunks of <= 4 tiles
+#pragma unroll
+      for (int j0 = 0; j0 < NT; j0 += CH) {
+        int nn[CH];
+        float v[CH][4];
+#pragma unroll
+        for (int j = 0; j < CH; ++j) {
+          nn[j] = n0 + (j0 + j) * 16 + fq * 4;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[j][r] = acc[j0 + j][r];
+        }
+        epilogue_row<T, CH>(s, g, 0, m, nn, v);
+      }
+    }
+  }
+}
+
+template <typename T, int NT>
+static void launch_direct(const ConvArgsDev& d, dim3 grid, int rs, int nks_max, hipStream_t st) {
+  constexpr int NKS = 12;
+  const size_t lds = (size_t)16 * NT * rs * 16;
+  (void)nks_max;
+  hipLaunchKernelGGL((conv_direct_kernel<T, NT, NKS>), grid, dim3(256), lds, st, d, rs);
+}
+
 struct TileCfg { int bm, bn; };
+// 0..6: streaming K-ring kernel; 7..12: weight-resident persistent kernel (kWresStages)
 static const TileCfg kTiles[] = {
-    {128, 128}, {128, 64}, {64, 64}, {128, 32}, {64, 32}, {128, 16}, {64, 16}};
+    {128, 128}, {128, 64}, {64, 64}, {128, 32}, {64, 32}, {128, 16}, {64, 16},
+    {128, 64}, {64, 64}, {128, 32}, {64, 32}, {128, 128}, {128, 16},
+    {16, 16}, {16, 32}, {16, 48}, {16, 64}, {16, 96}, {16, 192}};
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
+constexpr int kFirstWres = 7;
+constexpr int kWresStages = 6;
+constexpr int kFirstDirect = 13;   // 13..18: direct kernel with NT = bn/16
+constexpr int kDirectSteps = 12;
 
 template <typename T>
 static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t st) {
   const ConvShared& s = d.s;
   const TileCfg tc = kTiles[tile];
+  if (tile >= kFirstDirect) {
+    const int ny = (max_cout + tc.bn - 1) / tc.bn;
+    const int nz = s.ngroups;
+    const int ntile = (s.M + 15) / 16;
+    int gx = (512 + ny * nz - 1) / (ny * nz);
+    if (gx > (ntile + 3) / 4) gx = (ntile + 3) / 4;
+    if (gx < 1) gx = 1;
+    int nks_max = 0;
+    const int kstep = sizeof(T) == 4 ? 16 : 32;
+    for (int i = 0; i < s.ngroups; ++i) {
+      const int nk = (s.ksize * s.ksize * d.g[i].cin_pad + kstep - 1) / kstep;
+      if (nk > nks_max) nks_max = nk;
+    }
+    const int rs = nks_max * 4 + 1;
+    if ((size_t)tc.bn * rs * 16 > 65536) {
+      set_error("direct tile weight panel exceeds 64 KiB of LDS");
+      return RGBAC_E_ARG;
+    }
+    dim3 grid(gx, ny, nz);
+    switch (tc.bn / 16) {
+      case 1: launch_direct<T, 1>(d, grid, rs, nks_max, st); break;
+      case 2: launch_direct<T, 2>(d, grid, rs, nks_max, st); break;
+      case 3: launch_direct<T, 3>(d, grid, rs, nks_max, st); break;
+      case 4: launch_direct<T, 4>(d, grid, rs, nks_max, st); break;
+      case 6: launch_direct<T, 6>(d, grid, rs, nks_max, st); break;
+      default: launch_direct<T, 12>(d, grid, rs, nks_max, st); break;
+    }
+    return check_launch("conv_direct_kernel");
+  }
+  if (tile >= kFirstWres) {
+    const int mtiles = (s.M + tc.bm - 1) / tc.bm;
+    const int ny = (max_cout + tc.bn - 1) / tc.bn;
+    const int nz = s.nphase * s.ngroups;
+    int gx = (512 + ny * nz - 1) / (ny * nz);
+    if (gx > mtiles) gx = mtiles;
+    if (gx < 1) gx = 1;
+    dim3 grid(gx, ny, nz);
+    constexpr int NS = kWresStages;
+    switch (tile) {
+      case 7: hipLaunchKernelGGL((conv_wres_kernel<T, 128, 64, 2, 2, NS>), grid, dim3(256), 0, st, d); break;
+      case 8: hipLaunchKernelGGL((conv_wres_kernel<T, 64, 64, 2, 2, NS>), grid, dim3(256), 0, st, d); break;
+      case 9: hipLaunchKernelGGL((conv_wres_kernel<T, 128, 32, 4, 1, NS>), grid, dim3(256), 0, st, d); break;
+      case 10: hipLaunchKernelGGL((conv_wres_kernel<T, 64, 32, 2, 2, NS>), grid, dim3(256), 0, st, d); break;
+      case 11: hipLaunchKernelGGL((conv_wres_kernel<T, 128, 128, 2, 2, NS>), grid, dim3(256), 0, st, d); break;
+      default: hipLaunchKernelGGL((conv_wres_kernel<T, 128, 16, 4, 1, NS>), grid, dim3(256), 0, st, d); break;
+    }
+    return check_launch("conv_wres_kernel");
+  }
   dim3 grid((s.M + tc.bm - 1) / tc.bm, (max_cout + tc.bn - 1) / tc.bn,
             s.nphase * s.ksplit * s.ngroups);
   switch (tile) {
@@ -623,6 +1042,8 @@ extern "C" int rgbac_conv2d_grouped(const rgbac_conv_args* args, int ngroups, vo
   } else {
     RGBAC_REQUIRE(false, "unknown conv mode");
   }
+  s.rWm = 1.0 / s.Wm;
+  s.rHm = 1.0 / s.Hm;
   const long long M = (long long)a->batch * s.Hm * s.Wm;
   RGBAC_REQUIRE(M < (1ll << 31), "too many output pixels");
   s.M = (int)M;
@@ -633,6 +1054,21 @@ extern "C" int rgbac_conv2d_grouped(const rgbac_conv_args* args, int ngroups, vo
   s.square = a->square_input;
   s.ksplit = a->ksplit;
   s.ngroups = ngroups;
+  if (a->tile >= kFirstDirect) {
+    RGBAC_REQUIRE(a->mode == RGBAC_CONV && a->ksplit == 1 && a->act != RGBAC_ACT_GAUSS,
+                  "direct tiles need a plain conv, ksplit 1 and no GAUSS epilogue");
+    const int ks_elems = a->dtype == RGBAC_F32 ? 16 : 32;
+    for (int i = 0; i < ngroups; ++i)
+      RGBAC_REQUIRE((ntaps_max * args[i].cin_pad + ks_elems - 1) / ks_elems <= kDirectSteps,
+                    "K too large for a direct tile");
+  } else if (a->tile >= kFirstWres) {
+    RGBAC_REQUIRE(a->ksplit == 1 && a->act != RGBAC_ACT_GAUSS,
+                  "weight-resident tiles need ksplit 1 and no GAUSS epilogue");
+    const int ks_elems = a->dtype == RGBAC_F32 ? 32 : 64;
+    for (int i = 0; i < ngroups; ++i)
+      RGBAC_REQUIRE((ntaps_max * args[i].cin_pad + ks_elems - 1) / ks_elems <= kWresStages,
+                    "K too large for a weight-resident tile");
+  }
   int max_cout = 0;
   for (int i = 0; i < ngroups; ++i) {
     const rgbac_conv_args* b = &args[i];

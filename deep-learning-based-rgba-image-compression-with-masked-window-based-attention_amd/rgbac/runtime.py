@@ -75,8 +75,17 @@ def round_up(x, m):
     return (x + m - 1) // m * m
 
 
-# conv tile shapes of csrc/conv.hip (pixels x channels); index = rgbac_conv_args.tile
-TILES = [(128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 16)]
+# conv tile shapes of csrc/conv.hip (pixels x channels); index = rgbac_conv_args.tile.
+# 0..6: streaming K-ring kernel; 7..12: weight-resident persistent kernel (K <= WRES_STAGES
+# stages of 64 bf16 / 32 f32 elements, ksplit 1).
+TILES = [(128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 16),
+         (128, 64), (64, 64), (128, 32), (64, 32), (128, 128), (128, 16),
+         (16, 16), (16, 32), (16, 48), (16, 64), (16, 96), (16, 192)]
+FIRST_WRES = 7
+WRES_STAGES = 6
+FIRST_DIRECT = 13        # 13..18: direct kernel (plain conv, K <= DIRECT_STEPS MFMA k-steps)
+DIRECT_STEPS = 12
+DIRECT_LDS = 65536       # weight panel bytes of a direct tile (dynamic LDS limit)
 KSPLITS = (1, 2, 4, 8)
 TUNE = os.environ.get("RGBAC_TUNE", "1") != "0"
 _tune_cache = {}          # shape key -> (tile, ksplit)
@@ -88,12 +97,22 @@ def pick_cout_pad(cout):
     return round_up(cout, 128)
 
 
-def _candidates(M, cout, nst):
-    """(tile, ksplit) pairs worth timing for an M-pixel, cout-channel, nst-stage conv."""
+def _candidates(M, cout, nst, nks=None, plain=True):
+    """(tile, ksplit) pairs worth timing for an M-pixel, cout-channel conv with nst K-stages
+    (nks MFMA k-steps; ``plain`` = CONV mode)."""
     out = []
     n16 = round_up(cout, 16)
     for t, (bm, bn) in enumerate(TILES):
+        if t >= FIRST_DIRECT:
+            if plain and nks is not None and nks <= DIRECT_STEPS and bn >= n16 / 4 \
+                    and bn < 2 * n16 + 16 and bn * (4 * nks + 1) * 16 <= DIRECT_LDS:
+                out.append((t, 1))
+            continue
         if bn > 16 and bn > 2 * n16:
+            continue
+        if t >= FIRST_WRES:
+            if nst <= WRES_STAGES:
+                out.append((t, 1))
             continue
         blocks = -(-M // bm) * -(-cout // bn)
         for ks in KSPLITS:
@@ -270,7 +289,8 @@ class PackedConv:
 
 class Prepared:
     """One conv's ABI record plus what the launcher needs (output, tuning key)."""
-    __slots__ = ("a", "out", "key", "mgrid", "nphase", "nst", "pk", "desc", "flops", "nbytes")
+    __slots__ = ("a", "out", "key", "mgrid", "nphase", "nst", "nks", "pk", "desc", "flops",
+                 "nbytes")
 
 
 def prepare(pk, srcs, out=None, out_coff=0, act="none", act_param=0.0, res0=None, res1=None,
@@ -334,6 +354,7 @@ def prepare(pk, srcs, out=None, out_coff=0, act="none", act_param=0.0, res0=None
     pr.mgrid = B * (H * W if pk.mode != CONV else Ho * Wo)
     pr.nphase = 4 if pk.mode == CONVT_S2 else 1
     pr.nst = -(-taps * pk.cin_pad // (32 if dtype == torch.float32 else 64))
+    pr.nks = -(-taps * pk.cin_pad // (16 if dtype == torch.float32 else 32))
     pr.key = f"{a.dtype}/{pk.mode}/{pk.ksize}/{pk.stride}/{B}x{H}x{W}/{pk.cin_pad}/{pk.cout}/{act == 'gauss'}"
     pr.flops = 2.0 * pr.mgrid * pk.cout * pk.cin * (25 if pk.mode == CONVT_S2 else taps)
     es = f0.t.element_size()
@@ -378,9 +399,10 @@ def launch(preps):
         cout = max(pr.pk.cout for pr in preps)
         nst = max(pr.nst for pr in preps)
         if gauss:
-            cands = [(t, 1) for t in range(len(TILES)) if _gauss_ok(t, cout)]
+            cands = [(t, 1) for t in range(FIRST_WRES) if _gauss_ok(t, cout)]
         else:
-            cands = _candidates(mtot, cout, nst)
+            cands = _candidates(mtot, cout, nst, max(pr.nks for pr in preps),
+                                p0.pk.mode == CONV)
         if TUNE and not torch.cuda.is_current_stream_capturing():
             best = None
             for cand in cands:
@@ -403,14 +425,16 @@ def launch(preps):
             choice = _heuristic(mtot, cout, nst)
         _tune_cache[key] = choice
     if gauss and not _gauss_ok(choice[0], max(pr.pk.cout for pr in preps)):
-        choice = (min((t for t in range(len(TILES)) if _gauss_ok(t, p0.pk.cout)),
+        choice = (min((t for t in range(FIRST_WRES) if _gauss_ok(t, p0.pk.cout)),
                       key=lambda t: TILES[t][1]), 1)
     set_choice(*choice)
     if PROFILER is None:
         run()
     else:
         bm, bn = TILES[choice[0]]
-        name = f"conv_kernel<{'f32' if p0.a.dtype == 0 else 'bf16'},{bm}x{bn}>"
+        kname = ("conv_direct_kernel" if choice[0] >= FIRST_DIRECT else
+                 "conv_wres_kernel" if choice[0] >= FIRST_WRES else "conv_kernel")
+        name = f"{kname}<{'f32' if p0.a.dtype == 0 else 'bf16'},{bm}x{bn}>"
         desc = f"{name} ks{choice[1]} g{n} {p0.desc}"
         PROFILER.wrap(name, sum(pr.flops for pr in preps), sum(pr.nbytes for pr in preps),
                       run, desc)

@@ -249,3 +249,40 @@ def test_win_attention_generic_head_dims(device, dim, ws):
     want = ref.win_based_attention(x, a, sd, "blk", ws, ws // 2)
     got = m.to(device)(x.to(device), a.to(device))
     assert rel(got, want) < 2e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("tile", range(7, 19))
+def test_conv_small_k_tiles(device, dtype, tile):
+    """Weight-resident persistent tiles on small-K convs (1x1, 3x3 @ 16 ch, convT 1x1,
+    grouped, residual/gate epilogues), several pixel tiles per workgroup."""
+    rt = _rt()
+    from rgbac.layers.TransformRGB import prep_conv, run_conv
+    g = _gen(200 + tile)
+    rt.FORCE = (tile, 1)
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    try:
+        m1 = nn.Conv2d(96, 72, 1)
+        x = torch.randn((3, 96, 40, 56), generator=g)
+        r = torch.randn((3, 72, 40, 56), generator=g)
+        want = F.gelu(m1(x) + r)
+        with torch.no_grad():
+            fx, fr = rt.to_nhwc(x.to(device), dtype), rt.to_nhwc(r.to(device), dtype)
+            got = rt.to_nchw(run_conv(m1.to(device), [fx.src()], act="gelu", res0=fr))
+        assert rel(got, want) < tol
+        m3 = nn.Conv2d(16, 24, 3, padding=1)
+        x3 = torch.randn((2, 16, 33, 20), generator=g)
+        want3 = m3(x3)
+        with torch.no_grad():
+            got = rt.to_nchw(run_conv(m3.to(device), [rt.to_nhwc(x3.to(device), dtype).src()]))
+        assert rel(got, want3) < tol
+        ms = [nn.Conv2d(64, 40, 1) for _ in range(2)]
+        xs = [torch.randn((2, 64, 16, 16), generator=g) for _ in range(2)]
+        wants = [m(t) for m, t in zip(ms, xs)]
+        with torch.no_grad():
+            fs = [rt.to_nhwc(t.to(device), dtype) for t in xs]
+            outs = rt.launch([prep_conv(m.to(device), [f.src()]) for m, f in zip(ms, fs)])
+        for w_, o in zip(wants, outs):
+            assert rel(rt.to_nchw(o), w_) < tol
+    finally:
+        rt.FORCE = None

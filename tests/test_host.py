@@ -31,7 +31,8 @@ def test_library_exports_every_header_symbol():
         assert hasattr(lib, n), n
     assert set(names) == set(_lib.SIGNATURES), set(names) ^ set(_lib.SIGNATURES)
     assert lib.rgbac_abi_version() == 1
-    assert lib.rgbac_conv_num_tiles() == 7
+    from rgbac import runtime as rt
+    assert lib.rgbac_conv_num_tiles() == len(rt.TILES)
     assert lib.rgbac_conv_max_groups() == 10
 
 
