@@ -764,7 +764,9 @@ __global__ void __launch_bounds__(256) conv_direct_kernel(const ConvArgsDev args
   const T* wbase = reinterpret_cast<const T*>(g.w);
   for (int e = tid; e < BN * nks * 4; e += 256) {
     const int row = e / (nks * 4), ch = e - row * (nks * 4);
-    Wl[row * rs + ch] = *reinterpret_cast<const uint4*>(wbase + (size_t)(n0 + row) * g.k_pad + ch * EPV);
+    Wl[row * rs + ch] = n0 + row < g.rows
+        ? *reinterpret_cast<const uint4*>(wbase + (size_t)(n0 + row) * g.k_pad + ch * EPV)
+        : make_uint4(0, 0, 0, 0);   // panel rows past the packed cout_pad
   }
   if (tid < NKS * 4) {
     const int st = tid >> 2, q = tid & 3;
