@@ -53,6 +53,8 @@ struct ConvGroup {                  // per-group operands
   const float* aux0;                // GAUSS: noise [M][cout/2] or NULL
   float* aux1;                      // GAUSS: likelihood out [M][cout/2] or NULL
   double* partial;                  // GAUSS: bits per M-tile block
+  void* zout;                       // training: pre-activation store (or NULL)
+  long long zld;
   int send0, send1, send2;          // cumulative channel ends
   int cin_pad, k_pad, cout, rows, cout16, out_coff;
 };
@@ -137,10 +139,11 @@ __device__ __forceinline__ void epilogue4(const ConvShared& s, const ConvGroup& 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float x = v[r];
-      if (s.act == RGBAC_ACT_GELU) x = gelu_f(x);
       const int oy = 2 * my + (r >> 1), ox = 2 * mx + (r & 1);
-      const long long o = ((long long)(b * s.out_h + oy) * s.out_w + ox) * g.out_ldc + g.out_coff + cc;
-      Elem<T>::st(out + o, x);
+      const long long op = (long long)(b * s.out_h + oy) * s.out_w + ox;
+      if (g.zout) Elem<T>::st(reinterpret_cast<T*>(g.zout) + op * g.zld + g.out_coff + cc, x);
+      if (s.act == RGBAC_ACT_GELU) x = gelu_f(x);
+      Elem<T>::st(out + op * g.out_ldc + g.out_coff + cc, x);
     }
     return;
   }
@@ -149,14 +152,23 @@ __device__ __forceinline__ void epilogue4(const ConvShared& s, const ConvGroup& 
     opix = (long long)(b * s.out_h + 2 * my + (ph >> 1)) * s.out_w + 2 * mx + (ph & 1);
   else
     opix = (long long)(b * s.out_h + my) * s.out_w + mx;
-  if (g.res0) {
-    float r0[4];
-    load_res<T>(g.res0, g.ld0, opix, n, g.cout, r0);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] += r0[r];
-  }
+  float r0[4] = {0.f, 0.f, 0.f, 0.f};
+  if (g.res0) load_res<T>(g.res0, g.ld0, opix, n, g.cout, r0);
   float r1[4] = {0.f, 0.f, 0.f, 0.f};
   if (g.res1) load_res<T>(g.res1, g.ld1, opix, n, g.cout, r1);
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    v[r] = s.act == RGBAC_ACT_SQBWD ? r0[r] + 2.0f * r1[r] * v[r] : v[r] + r0[r];
+  if (g.zout) {
+    T* z = reinterpret_cast<T*>(g.zout) + opix * g.zld + g.out_coff + n;
+    if (n + 3 < g.cout) {
+      Elem<T>::st4(z, v);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (n + r < g.cout) Elem<T>::st(z + r, v[r]);
+    }
+  }
   switch (s.act) {
     case RGBAC_ACT_GELU:
 #pragma unroll
@@ -236,10 +248,11 @@ __device__ __forceinline__ void epilogue_row(const ConvShared& s, const ConvGrou
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float x = v[j][r];
-        if (s.act == RGBAC_ACT_GELU) x = gelu_f(x);
         const int oy = 2 * my + (r >> 1), ox = 2 * mx + (r & 1);
-        const long long o = ((long long)(b * s.out_h + oy) * s.out_w + ox) * g.out_ldc + g.out_coff + cc;
-        Elem<T>::st(out + o, x);
+        const long long op = (long long)(b * s.out_h + oy) * s.out_w + ox;
+        if (g.zout) Elem<T>::st(reinterpret_cast<T*>(g.zout) + op * g.zld + g.out_coff + cc, x);
+        if (s.act == RGBAC_ACT_GELU) x = gelu_f(x);
+        Elem<T>::st(out + op * g.out_ldc + g.out_coff + cc, x);
       }
     }
     return;
@@ -264,9 +277,23 @@ __device__ __forceinline__ void epilogue_row(const ConvShared& s, const ConvGrou
   for (int j = 0; j < TN; ++j) {
     if (nn[j] >= g.cout) continue;
     float* vv = v[j];
+    if (g.zout) {
+      float zv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        zv[r] = s.act == RGBAC_ACT_SQBWD ? r0[j][r] + 2.0f * r1[j][r] * vv[r] : vv[r] + r0[j][r];
+      T* z = reinterpret_cast<T*>(g.zout) + opix * g.zld + g.out_coff + nn[j];
+      if (nn[j] + 3 < g.cout) {
+        Elem<T>::st4(z, zv);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (nn[j] + r < g.cout) Elem<T>::st(z + r, zv[r]);
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float x = vv[r] + r0[j][r];
+      float x = s.act == RGBAC_ACT_SQBWD ? r0[j][r] + 2.0f * r1[j][r] * vv[r] : vv[r] + r0[j][r];
       switch (s.act) {
         case RGBAC_ACT_GELU: x = gelu_f(x); break;
         case RGBAC_ACT_RELU: x = x > 0.f ? x : 0.f; break;
@@ -966,6 +993,12 @@ static int fill_group(const rgbac_conv_args* a, int ntaps_max, ConvGroup& g) {
   g.sp2 = a->nsrc > 2 ? a->src[2].ptr : g.sp1;
   g.sld2 = a->nsrc > 2 ? a->src[2].ldc : g.sld1;
   g.send2 = g.send1 + (a->nsrc > 2 ? a->src[2].channels : 0);
+  RGBAC_REQUIRE(!a->zout || (a->zout_ldc % 4 == 0 && a->act != RGBAC_ACT_GAUSS),
+                "zout needs zout_ldc % 4 == 0 and no GAUSS epilogue");
+  RGBAC_REQUIRE(a->act != RGBAC_ACT_SQBWD || (a->res0 && a->res1 && !a->bias),
+                "SQBWD needs res0 (direct gradient), res1 (x) and no bias");
+  g.zout = a->zout;
+  g.zld = a->zout_ldc;
   g.cin_pad = a->cin_pad;
   g.k_pad = a->k_pad;
   g.cout = a->cout;
@@ -1002,7 +1035,7 @@ extern "C" int rgbac_conv2d_grouped(const rgbac_conv_args* args, int ngroups, vo
   RGBAC_REQUIRE(a->batch > 0 && a->in_h > 0 && a->in_w > 0, "bad input shape");
   RGBAC_REQUIRE(a->tile >= 0 && a->tile < kNumTiles, "tile index out of range");
   RGBAC_REQUIRE(a->ksplit >= 1 && a->ksplit <= 64, "ksplit must be 1..64");
-  RGBAC_REQUIRE(a->act >= RGBAC_ACT_NONE && a->act <= RGBAC_ACT_GAUSS, "act");
+  RGBAC_REQUIRE(a->act >= RGBAC_ACT_NONE && a->act <= RGBAC_ACT_SQBWD, "act");
   for (int i = 1; i < ngroups; ++i) {
     const rgbac_conv_args* b = &args[i];
     RGBAC_REQUIRE(b->dtype == a->dtype && b->mode == a->mode && b->batch == a->batch &&

@@ -1,0 +1,1141 @@
+// Backward kernels of the training step (reference: trainRGB.py:178-198 --
+// rd_loss.backward(), grad.clamp_(-5, 5), Adam).  The forward convs save their
+// pre-activation value through rgbac_conv_args.zout; the input gradient of a
+// conv is the same MFMA conv engine run over a repacked (transposed / flipped /
+// phase-split) weight; this file holds what has no forward twin:
+//
+//   act_bwd_kernel       dL/dv of every fused epilogue (GELU, ReLU, LeakyReLU,
+//                        tanh-half, sigmoid gate, GDN/IGDN, window-drop select)
+//   wgrad_kernel         dW[n][k] = sum_m G[m][n] * Col(S)[m][k] on MFMA: the
+//                        reduction runs over PIXELS, so both operands are read
+//                        from pixel-major LDS tiles with ds_read_b64_tr_b16
+//                        (bf16) -- split over M with deterministic fp32 slabs
+//   wgrad_reduce_kernel  slab sum + scatter into the PyTorch weight layout, bias
+//   winattn_bwd_kernel   softmax(QK^T+B+M)V backward per (window group, head),
+//                        relative-position-bias gradient as per-block partials
+//   gaussian_bwd_kernel  GaussianConditional likelihood + bits + STE backward
+//   eb_bwd_kernel        EntropyBottleneck factorized density backward (per channel)
+//   mse_bwd_kernel       reconstruct_error backward
+//   adam_clamp_kernel    grad.clamp_(-c, c) + torch.optim.Adam step (fp32)
+//   pixel_shuffle_kernel / channel_copy_kernel   layout helpers (subpel, concat)
+#include <cmath>
+
+#include "common.h"
+
+namespace rgbac {
+
+__device__ __forceinline__ float t_sigmoid(float v) { return 1.0f / (1.0f + expf(-v)); }
+__device__ __forceinline__ float t_phi(float t) {       // standard normal pdf
+  return 0.39894228040143267794f * expf(-0.5f * t * t);
+}
+__device__ __forceinline__ float t_cdf(float t) {       // 0.5 * erfc(-t / sqrt 2)
+  return 0.5f * erfcf(-0.70710678118654752440f * t);
+}
+
+// ------------------------------------------------------------------ act_bwd
+// dz = dL/dv for y = act(v [, r1]); dr1 = dL/dr1 where r1 enters the activation
+// (GATE: y = r1*sigmoid(v); GDN: y = r1/sqrt(v); IGDN: y = r1*sqrt(v)).
+// Channels [C, ld) of the outputs are written as zeros.
+template <typename T>
+__global__ void __launch_bounds__(256)
+act_bwd_kernel(int act, float slope, long long npix, int C, const T* __restrict__ dy, long long ldy,
+               const T* __restrict__ z, long long ldz, const T* __restrict__ r1, long long ld1,
+               const uint8_t* __restrict__ sel, T* __restrict__ dz, long long lddz,
+               T* __restrict__ dr1, long long lddr1) {
+  const long long n = npix * lddz;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+    const long long p = e / lddz;
+    const int c = (int)(e - p * lddz);
+    if (c >= C) {
+      Elem<T>::st(dz + e, 0.0f);
+      if (dr1 && c < lddr1) Elem<T>::st(dr1 + p * lddr1 + c, 0.0f);
+      continue;
+    }
+    const float g = Elem<T>::ld(dy + p * ldy + c);
+    const float v = z ? Elem<T>::ld(z + p * ldz + c) : 0.0f;
+    float gz = g, gr = 0.0f;
+    switch (act) {
+      case RGBAC_ACT_GELU:
+        gz = g * (t_cdf(v) + v * t_phi(v));
+        break;
+      case RGBAC_ACT_RELU:
+        gz = v > 0.0f ? g : 0.0f;
+        break;
+      case RGBAC_ACT_LRELU:
+        gz = v > 0.0f ? g : g * slope;
+        break;
+      case RGBAC_ACT_TANH_HALF: {
+        const float t = tanhf(v);
+        gz = g * 0.5f * (1.0f - t * t);
+        gr = g;
+        break;
+      }
+      case RGBAC_ACT_GATE: {
+        const float s = t_sigmoid(v);
+        const float a = Elem<T>::ld(r1 + p * ld1 + c);
+        gz = g * a * (s * (1.0f - s));
+        gr = g * s;
+        break;
+      }
+      case RGBAC_ACT_GDN: {
+        const float a = Elem<T>::ld(r1 + p * ld1 + c);
+        const float rs = 1.0f / sqrtf(v);
+        gz = g * a * (-0.5f) * rs / v;
+        gr = g * rs;
+        break;
+      }
+      case RGBAC_ACT_IGDN: {
+        const float a = Elem<T>::ld(r1 + p * ld1 + c);
+        const float sq = sqrtf(v);
+        gz = g * a * 0.5f / sq;
+        gr = g * sq;
+        break;
+      }
+      case RGBAC_ACT_MASKSEL:
+        gz = sel[p] ? g : 0.0f;
+        gr = g;
+        break;
+      default:
+        break;
+    }
+    Elem<T>::st(dz + e, gz);
+    if (dr1) Elem<T>::st(dr1 + p * lddr1 + c, gr);
+  }
+}
+
+// ------------------------------------------------------------------ wgrad
+struct WgradDev {
+  const void* g; long long ldg; int gch;
+  const void* sp0; const void* sp1; const void* sp2;
+  long long sld0, sld1, sld2;
+  int send0, send1, send2;
+  int cin_pad, K, k_pad, n_pad;
+  int M, Hg, Wg;
+  int in_h, in_w, ksize, stride, pad, square;
+  int m_chunk;
+  float* part;
+  float* bpart;
+};
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s* lds_v4s_ptr;
+
+// D[n][k] = sum_m G[m][n] * Col(S)[m][k]; 64(n) x 64(k) per workgroup, 64 pixels
+// per stage, register-staged double-buffered LDS tiles (row = pixel).
+//   bf16: LDS rows of 128 B, 16-B chunk c of row r stored at slot c ^ swz(r),
+//         swz(r) = 2*((r>>1)&1) + 4*((r>>3)&1) -- the ds_read_b64_tr_b16 reads
+//         of a 32-lane half (rows 8q..8q+3 of two groups, 32 B each) then hit
+//         64 distinct banks.  Operand of lane l (row l&15 of the 16-row tile,
+//         pixels 8q..8q+7, q = l>>4) = two transposed reads.
+//   f32 : rows padded to 272 B; operands are 4 scalar reads per lane.
+template <typename T>
+__global__ void __launch_bounds__(256) wgrad_kernel(const WgradDev a) {
+  constexpr int EPV = Elem<T>::EPV;
+  constexpr int CPR = 64 / EPV;                   // 16-B chunks per 64-element row
+  constexpr int NL = 64 * CPR / 256;              // chunks per thread per tile
+  constexpr int RSB = sizeof(T) == 2 ? 128 : 272; // LDS row stride (bytes)
+  constexpr int TILE = 64 * RSB;
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2][2][TILE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int k0 = blockIdx.x * 64, n0 = blockIdx.y * 64, split = blockIdx.z;
+  const int mbeg = split * a.m_chunk;
+  int mend = mbeg + a.m_chunk;
+  if (mend > a.M) mend = a.M;
+  const bool do_bias = a.bpart && blockIdx.x == 0;
+
+  // per-thread chunk geometry (fixed over stages)
+  int crow[NL], ccol[NL];
+  int s_src[NL], s_cs[NL], s_dy[NL], s_dx[NL];
+  bool s_ok[NL], g_ok[NL];
+#pragma unroll
+  for (int j = 0; j < NL; ++j) {
+    const int c = tid + 256 * j;
+    crow[j] = c / CPR;
+    ccol[j] = c % CPR;
+    g_ok[j] = n0 + ccol[j] * EPV < a.gch;
+    const int k = k0 + ccol[j] * EPV;
+    const int tap = k / a.cin_pad;
+    const int ci = k - tap * a.cin_pad;
+    s_ok[j] = k < a.K;
+    s_dy[j] = tap / a.ksize - a.pad;
+    s_dx[j] = tap % a.ksize - a.pad;
+    if (ci < a.send0) { s_src[j] = 0; s_cs[j] = ci; }
+    else if (ci < a.send1) { s_src[j] = 1; s_cs[j] = ci - a.send0; }
+    else { s_src[j] = 2; s_cs[j] = ci - a.send1; s_ok[j] = s_ok[j] && ci < a.send2; }
+  }
+
+  uint4 rg[NL], rs[NL];
+  auto load_stage = [&](int mb) {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      const int m = mb + crow[j];
+      rg[j] = make_uint4(0, 0, 0, 0);
+      rs[j] = make_uint4(0, 0, 0, 0);
+      if (m < mend) {
+        if (g_ok[j])
+          rg[j] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.g) +
+                                                  (long long)m * a.ldg + n0 + ccol[j] * EPV);
+        if (s_ok[j]) {
+          const int x = m % a.Wg;
+          const int t = m / a.Wg;
+          const int y = t % a.Hg;
+          const int b = t / a.Hg;
+          const int iy = y * a.stride + s_dy[j], ix = x * a.stride + s_dx[j];
+          if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
+            const int sj = s_src[j];
+            const T* base = reinterpret_cast<const T*>(sj == 0 ? a.sp0 : (sj == 1 ? a.sp1 : a.sp2));
+            const long long ld = sj == 0 ? a.sld0 : (sj == 1 ? a.sld1 : a.sld2);
+            rs[j] = *reinterpret_cast<const uint4*>(
+                base + ((long long)(b * a.in_h + iy) * a.in_w + ix) * ld + s_cs[j]);
+          }
+        }
+      }
+    }
+  };
+  auto slot = [&](int r, int c) -> int {     // byte offset of chunk c of row r
+    if constexpr (sizeof(T) == 2) return r * RSB + 16 * (c ^ (2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1)));
+    else return r * RSB + 16 * c;
+  };
+  auto store_stage = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      uint4 sv = rs[j];
+      if (a.square) {
+        if constexpr (sizeof(T) == 2) {
+          uint32_t w[4] = {sv.x, sv.y, sv.z, sv.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float lo = bf2f(w[q] & 0xFFFF), hi = bf2f(w[q] >> 16);
+            w[q] = (uint32_t)f2bf(lo * lo) | ((uint32_t)f2bf(hi * hi) << 16);
+          }
+          sv = make_uint4(w[0], w[1], w[2], w[3]);
+        } else {
+          const float p0 = __uint_as_float(sv.x), p1 = __uint_as_float(sv.y);
+          const float p2 = __uint_as_float(sv.z), p3 = __uint_as_float(sv.w);
+          sv = make_uint4(__float_as_uint(p0 * p0), __float_as_uint(p1 * p1),
+                          __float_as_uint(p2 * p2), __float_as_uint(p3 * p3));
+        }
+      }
+      *reinterpret_cast<uint4*>(&lds[buf][0][slot(crow[j], ccol[j])]) = rg[j];
+      *reinterpret_cast<uint4*>(&lds[buf][1][slot(crow[j], ccol[j])]) = sv;
+    }
+  };
+
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc = 0.0f;
+
+  const int wn = wave >> 1, wk = wave & 1;
+  const int fi = lane & 15, fq = lane >> 4;
+  const int nst = mend > mbeg ? (mend - mbeg + 63) / 64 : 0;
+  if (nst > 0) {
+    load_stage(mbeg);
+    store_stage(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < nst; ++it) {
+    const int buf = it & 1;
+    if (it + 1 < nst) load_stage(mbeg + (it + 1) * 64);
+    const unsigned char* Gs = lds[buf][0];
+    const unsigned char* Ss = lds[buf][1];
+    if (do_bias && tid < 64) {
+      // column sums of G (bias gradient) over this stage's 64 pixels
+#pragma unroll 4
+      for (int r = 0; r < 64; ++r) {
+        const int off = slot(r, tid / EPV) + (tid % EPV) * (int)sizeof(T);
+        if constexpr (sizeof(T) == 2) bacc += bf2f(*reinterpret_cast<const uint16_t*>(Gs + off));
+        else bacc += *reinterpret_cast<const float*>(Gs + off);
+      }
+    }
+    if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        uint4 A[2], B[2];
+        const int ra = kk * 32 + 8 * fq + (fi >> 2);     // block row of this lane's address
+        const int cq = (fi & 3);                         // 4-column quad within the 16 columns
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int ncol = wn * 32 + t * 16 + 4 * cq;    // element column
+          const int kcol = wk * 32 + t * 16 + 4 * cq;
+          const int offa0 = slot(ra, ncol >> 3) + (ncol & 7) * 2;
+          const int offa1 = slot(ra + 4, ncol >> 3) + (ncol & 7) * 2;
+          const int offb0 = slot(ra, kcol >> 3) + (kcol & 7) * 2;
+          const int offb1 = slot(ra + 4, kcol >> 3) + (kcol & 7) * 2;
+          const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)(Gs + offa0));
+          const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)(Gs + offa1));
+          const v4s b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)(Ss + offb0));
+          const v4s b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)(Ss + offb1));
+          const uint2 ua0 = __builtin_bit_cast(uint2, a0), ua1 = __builtin_bit_cast(uint2, a1);
+          const uint2 ub0 = __builtin_bit_cast(uint2, b0), ub1 = __builtin_bit_cast(uint2, b1);
+          A[t] = make_uint4(ua0.x, ua0.y, ua1.x, ua1.y);
+          B[t] = make_uint4(ub0.x, ub0.y, ub1.x, ub1.y);
+        }
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+          for (int tk = 0; tk < 2; ++tk) mma_step<bf16_t>(acc[tn][tk], A[tn], B[tk]);
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        uint4 A[2], B[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int ncol = wn * 32 + t * 16 + fi;
+          const int kcol = wk * 32 + t * 16 + fi;
+          uint32_t av[4], bv[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int r = ks * 16 + 4 * fq + e;
+            av[e] = *reinterpret_cast<const uint32_t*>(Gs + r * RSB + ncol * 4);
+            bv[e] = *reinterpret_cast<const uint32_t*>(Ss + r * RSB + kcol * 4);
+          }
+          A[t] = make_uint4(av[0], av[1], av[2], av[3]);
+          B[t] = make_uint4(bv[0], bv[1], bv[2], bv[3]);
+        }
+#pragma unroll
+        for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+          for (int tk = 0; tk < 2; ++tk) mma_step<float>(acc[tn][tk], A[tn], B[tk]);
+      }
+    }
+    if (it + 1 < nst) store_stage(buf ^ 1);
+    __syncthreads();
+  }
+  // partial slab [split][n_pad][k_pad]: lane holds D[n = 4*fq + r][k = fi] per 16x16 tile
+  float* P = a.part + (size_t)split * a.n_pad * a.k_pad;
+#pragma unroll
+  for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+    for (int tk = 0; tk < 2; ++tk)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * 32 + tn * 16 + 4 * fq + r;
+        const int k = k0 + wk * 32 + tk * 16 + fi;
+        P[(size_t)n * a.k_pad + k] = acc[tn][tk][r];
+      }
+  if (do_bias && tid < 64) a.bpart[(size_t)split * a.n_pad + n0 + tid] = bacc;
+}
+
+// dw[i] = sum_s part[s][map[i]] (map < 0 -> 0); db[j] = sum_s bpart[s][j]   (fixed order)
+__global__ void __launch_bounds__(256)
+wgrad_reduce_kernel(long long numel, const int* __restrict__ map, const float* __restrict__ part,
+                    int nsplit, long long slab, float* __restrict__ dw, int nbias,
+                    const float* __restrict__ bpart, int n_pad, float* __restrict__ db) {
+  const long long total = numel + nbias;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    if (e < numel) {
+      const int p = map[e];
+      float s = 0.0f;
+      if (p >= 0)
+        for (int q = 0; q < nsplit; ++q) s += part[q * slab + p];
+      dw[e] = s;
+    } else {
+      const int j = (int)(e - numel);
+      float s = 0.0f;
+      for (int q = 0; q < nsplit; ++q) s += bpart[(size_t)q * n_pad + j];
+      db[j] = s;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ attention core backward
+// Recomputes P = softmax(q k^T * scale + B + M) per window (fp32, same op order
+// as the VALU forward), then dV = P^T dO, dP = dO V^T, dS = P (dP - rowsum(P dP)),
+// dQ = scale dS K, dK = dS^T (scale Q).  Grid (blocks, heads): block b, head h
+// walks window groups g = b, b + gridDim.x, ... accumulating its dS sum (the
+// dense bias gradient of head h) in registers -> bpart[b][h][N][N].
+template <typename T, int WS>
+__global__ void __launch_bounds__(256)
+winattn_bwd_kernel(int batch, int H, int W, int C, int heads, int shift, int masked, float scale,
+                   const T* __restrict__ qkv, long long ldq, const float* __restrict__ alpha,
+                   const float* __restrict__ bias, const T* __restrict__ dout, long long ldo,
+                   T* __restrict__ dqkv, long long lddq, float* __restrict__ bpart) {
+  constexpr int N = WS * WS;
+  constexpr int NWIN = 64 / N;
+  constexpr int DP = 25;
+  constexpr int NR = (N == 64) ? 16 : 1;        // dense-bias entries per thread
+  __shared__ float qs[64 * DP], ks[64 * DP], vs[64 * DP], gs[64 * DP];
+  __shared__ float P[64 * (N + 1)], G[64 * (N + 1)];
+  __shared__ float Dsum[64];
+  __shared__ int pix_s[64];
+  __shared__ int act_s[NWIN];
+
+  const int tid = threadIdx.x;
+  const int h = blockIdx.y;
+  const int nwx = W / WS, nwy = H / WS;
+  const int total = batch * nwx * nwy;
+  const int ngroups = (total + NWIN - 1) / NWIN;
+  const int d = C / heads;
+  float bacc[NR];
+#pragma unroll
+  for (int r = 0; r < NR; ++r) bacc[r] = 0.0f;
+
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    if (tid < NWIN) act_s[tid] = masked ? 0 : 1;
+    __syncthreads();
+    if (tid < 64) {
+      const int wi = tid / N, lt = tid % N;
+      const int gw = grp * NWIN + wi;
+      int pix = -1;
+      if (gw < total) {
+        const int b = gw / (nwx * nwy);
+        const int rem = gw - b * nwx * nwy;
+        const int wy = rem / nwx, wx = rem - (rem / nwx) * nwx;
+        const int r = wy * WS + lt / WS, c = wx * WS + lt % WS;
+        int oy = r + shift; if (oy >= H) oy -= H;
+        int ox = c + shift; if (ox >= W) ox -= W;
+        pix = (b * H + oy) * W + ox;
+        if (masked && alpha[pix] != 0.0f) act_s[wi] = 1;
+      }
+      pix_s[tid] = pix;
+    }
+    __syncthreads();
+    // ---- stage q*scale, k, v, dO of head h (zeros for inactive windows / padding)
+    for (int e = tid; e < 64 * d; e += 256) {
+      const int t = e / d, j = e - t * d;
+      const int pix = pix_s[t];
+      float q = 0.f, k = 0.f, v = 0.f, g = 0.f;
+      if (pix >= 0 && act_s[t / N]) {
+        const T* row = qkv + (long long)pix * ldq + h * d + j;
+        q = Elem<T>::ld(row) * scale;
+        k = Elem<T>::ld(row + C);
+        v = Elem<T>::ld(row + 2 * C);
+        g = Elem<T>::ld(dout + (long long)pix * ldo + h * d + j);
+      }
+      qs[t * DP + j] = q;
+      ks[t * DP + j] = k;
+      vs[t * DP + j] = v;
+      gs[t * DP + j] = g;
+    }
+    __syncthreads();
+    // ---- scores (same arithmetic as the forward) and dP = dO V^T
+    const float* bh = bias + (size_t)h * N * N;
+    for (int e = tid; e < 64 * N; e += 256) {
+      const int i = e / N, j = e - i * N;
+      const int wbase = (i / N) * N;
+      const int li = i - wbase;
+      float s = 0.f, dp = 0.f;
+      for (int q = 0; q < d; ++q) {
+        s = fmaf(qs[i * DP + q], ks[(wbase + j) * DP + q], s);
+        dp = fmaf(gs[i * DP + q], vs[(wbase + j) * DP + q], dp);
+      }
+      s += bh[li * N + j];
+      if (shift > 0) {
+        const int wi = i / N;
+        const int gw = grp * NWIN + wi;
+        const int rem = gw % (nwx * nwy);
+        const int wy = rem / nwx, wx = rem % nwx;
+        const int ri = wy * WS + li / WS, ci = wx * WS + li % WS;
+        const int rj = wy * WS + j / WS, cj = wx * WS + j % WS;
+        const int gi = 3 * (ri < H - WS ? 0 : (ri < H - shift ? 1 : 2)) +
+                       (ci < W - WS ? 0 : (ci < W - shift ? 1 : 2));
+        const int gj = 3 * (rj < H - WS ? 0 : (rj < H - shift ? 1 : 2)) +
+                       (cj < W - WS ? 0 : (cj < W - shift ? 1 : 2));
+        if (gi != gj) s += -100.0f;
+      }
+      P[i * (N + 1) + j] = s;
+      G[i * (N + 1) + j] = dp;
+    }
+    __syncthreads();
+    // ---- softmax rows and D_i = sum_j P dP (4 lanes per row)
+    {
+      const int i = tid >> 2, part = tid & 3;
+      float mx = -INFINITY;
+      for (int j = part; j < N; j += 4) mx = fmaxf(mx, P[i * (N + 1) + j]);
+      mx = fmaxf(mx, __shfl_xor(mx, 1));
+      mx = fmaxf(mx, __shfl_xor(mx, 2));
+      float sum = 0.f;
+      for (int j = part; j < N; j += 4) {
+        const float ex = expf(P[i * (N + 1) + j] - mx);
+        P[i * (N + 1) + j] = ex;
+        sum += ex;
+      }
+      sum += __shfl_xor(sum, 1);
+      sum += __shfl_xor(sum, 2);
+      const float inv = 1.0f / sum;
+      float dd = 0.f;
+      for (int j = part; j < N; j += 4) {
+        const float pv = P[i * (N + 1) + j] * inv;
+        P[i * (N + 1) + j] = pv;
+        dd = fmaf(pv, G[i * (N + 1) + j], dd);
+      }
+      dd += __shfl_xor(dd, 1);
+      dd += __shfl_xor(dd, 2);
+      if (part == 0) Dsum[i] = dd;
+    }
+    __syncthreads();
+    // ---- dS = P (dP - D) in place of dP; dense-bias gradient accumulation
+    for (int e = tid; e < 64 * N; e += 256) {
+      const int i = e / N, j = e - i * N;
+      const float ds = P[i * (N + 1) + j] * (G[i * (N + 1) + j] - Dsum[i]);
+      G[i * (N + 1) + j] = act_s[i / N] ? ds : 0.0f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < NR; ++r) {
+      if (N == 64) {
+        const int e = tid + 256 * r;               // (i, j), one window of 64 tokens
+        bacc[r] += G[(e / N) * (N + 1) + (e % N)];
+      } else {
+        // ws 4: entry (li, j) = tid, summed over the group's NWIN windows
+        const int li = tid / N, j = tid % N;
+#pragma unroll
+        for (int w = 0; w < NWIN; ++w) bacc[r] += G[(w * N + li) * (N + 1) + j];
+      }
+    }
+    // ---- dq, dk, dv at the tokens' original pixels
+    for (int e = tid; e < 64 * d; e += 256) {
+      const int i = e / d, c = e - i * d;
+      const int wbase = (i / N) * N;
+      const int li = i - wbase;
+      float dq = 0.f, dk = 0.f, dv = 0.f;
+      for (int j = 0; j < N; ++j) {
+        dq = fmaf(G[i * (N + 1) + j], ks[(wbase + j) * DP + c], dq);
+        dk = fmaf(G[(wbase + j) * (N + 1) + li], qs[(wbase + j) * DP + c], dk);
+        dv = fmaf(P[(wbase + j) * (N + 1) + li], gs[(wbase + j) * DP + c], dv);
+      }
+      const int pix = pix_s[i];
+      if (pix >= 0) {
+        const bool on = act_s[i / N] != 0;
+        T* row = dqkv + (long long)pix * lddq + h * d + c;
+        Elem<T>::st(row, on ? dq * scale : 0.0f);
+        Elem<T>::st(row + C, on ? dk : 0.0f);
+        Elem<T>::st(row + 2 * C, on ? dv : 0.0f);
+      }
+    }
+    __syncthreads();
+  }
+  float* bp = bpart + ((size_t)blockIdx.x * heads + h) * N * N;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) bp[N == 64 ? tid + 256 * r : tid] = bacc[r];
+}
+
+// dtable[e][h] = sum over blocks and (i, j) with index[i][j] == e of bpart[blk][h][i][j]
+__global__ void __launch_bounds__(256)
+relpos_reduce_kernel(int nblk, int heads, int N, const float* __restrict__ bpart,
+                     float* __restrict__ dense) {
+  const int total = heads * N * N;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
+    float s = 0.0f;
+    for (int b = 0; b < nblk; ++b) s += bpart[(size_t)b * total + e];
+    dense[e] = s;
+  }
+}
+__global__ void __launch_bounds__(256)
+relpos_scatter_kernel(int ntab, int heads, int N, const int64_t* __restrict__ index,
+                      const float* __restrict__ dense, float* __restrict__ dtable) {
+  const int total = ntab * heads;
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
+    const int t = e / heads, h = e - t * heads;
+    float s = 0.0f;
+    for (int ij = 0; ij < N * N; ++ij)
+      if (index[ij] == t) s += dense[(size_t)h * N * N + ij];
+    dtable[e] = s;
+  }
+}
+
+// ------------------------------------------------------------------ Gaussian conditional
+// Forward (per element): x = y + noise (training) | round(y-mu)+mu; v = |x - mu|;
+// s = LB(sigma, .11); lik = LB(Phi((.5-v)/s) - Phi((-.5-v)/s), 1e-9);
+// bits = clamp(-log(lik+1e-10)/ln2, 0, 50); hat = ste_round(y - mu) + mu.
+// Backward with g = dL/dbits (device scalar) and dhat = dL/dhat:
+//   dy = dhat + g * dbits/dy (training only), dmu = -g * dbits/dv sign(x-mu)
+//   (training only; dhat/dmu = 0), dsigma through compressai's LowerBound rule.
+template <typename T>
+__global__ void __launch_bounds__(256)
+gaussian_bwd_kernel(long long n, int nch, const T* __restrict__ y, long long ldy,
+                    const T* __restrict__ mu, long long ldmu, const T* __restrict__ sc,
+                    long long lds, const float* __restrict__ noise, const float* __restrict__ gbits,
+                    const T* __restrict__ dhat, long long lddh, T* __restrict__ dy, long long lddy,
+                    T* __restrict__ dmu, long long lddmu, T* __restrict__ dsc, long long lddsc) {
+  const float gb = *gbits;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+    const long long pix = e / nch;
+    const int ch = (int)(e - pix * nch);
+    const float yv = Elem<T>::ld(y + pix * ldy + ch);
+    const float mv = Elem<T>::ld(mu + pix * ldmu + ch);
+    const float sv = Elem<T>::ld(sc + pix * lds + ch);
+    const float xin = noise ? yv + noise[e] : rintf(yv - mv) + mv;
+    const float val = xin - mv;
+    const float v = fabsf(val);
+    const float s = fmaxf(sv, 0.11f);
+    const float ta = (0.5f - v) / s, tb = (-0.5f - v) / s;
+    const float lraw = t_cdf(ta) - t_cdf(tb);
+    const float lik = fmaxf(lraw, 1e-9f);
+    const float braw = (-1.0f * logf(lik + 1e-10f)) / 0.69314718055994530942f;
+    float gl = (braw >= 0.0f && braw <= 50.0f) ? gb * (-1.0f / ((lik + 1e-10f) * 0.69314718055994530942f)) : 0.0f;
+    if (!(lraw >= 1e-9f || gl < 0.0f)) gl = 0.0f;                // likelihood LowerBound
+    const float pa = t_phi(ta), pb = t_phi(tb);
+    const float gv = gl * (pb - pa) / s;
+    float gs = gl * (tb * pb - ta * pa) / s;
+    if (!(sv >= 0.11f || gs < 0.0f)) gs = 0.0f;                  // scale LowerBound
+    const float sg = val > 0.0f ? 1.0f : (val < 0.0f ? -1.0f : 0.0f);
+    const float gval = noise ? gv * sg : 0.0f;
+    const float dh = dhat ? Elem<T>::ld(dhat + pix * lddh + ch) : 0.0f;
+    Elem<T>::st(dy + pix * lddy + ch, gval + dh);
+    Elem<T>::st(dmu + pix * lddmu + ch, -gval);
+    Elem<T>::st(dsc + pix * lddsc + ch, gs);
+  }
+}
+
+// ------------------------------------------------------------------ EntropyBottleneck
+// One block per channel.  Per element: x = z + noise (training) | round(z-med)+med;
+// lik = LB(sigmoid(l(x+.5)) - sigmoid(l(x-.5)), 1e-9), l = the factorized MLP
+// over the packed param block (entropy.hip layout); bits as above.  Gradients are
+// w.r.t. the PACKED values (softplus(matrix), bias, tanh(factor)) in the same
+// [C][64] positions (the host chains them to the raw parameters); [58] = median
+// (quantiles[:, 0, 1]) in eval mode.
+struct EbCache { float x; float a[4][3]; float t[4][3]; };
+
+__device__ __forceinline__ float eb_fwd_cache(const float* P, float x, EbCache& c) {
+  c.x = x;
+#pragma unroll
+  for (int o = 0; o < 3; ++o) {
+    float a = P[0 + o] * x;
+    a = a + P[33 + o];
+    c.a[0][o] = a;
+    c.t[0][o] = a + P[46 + o] * tanhf(a);
+  }
+#pragma unroll
+  for (int layer = 1; layer < 4; ++layer) {
+    const float* Mx = P + 3 + 9 * (layer - 1);
+    const float* bx = P + 36 + 3 * (layer - 1);
+    const float* fx = P + 49 + 3 * (layer - 1);
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      float a = Mx[o * 3 + 0] * c.t[layer - 1][0];
+      a = fmaf(Mx[o * 3 + 1], c.t[layer - 1][1], a);
+      a = fmaf(Mx[o * 3 + 2], c.t[layer - 1][2], a);
+      a = a + bx[o];
+      c.a[layer][o] = a;
+      c.t[layer][o] = a + fx[o] * tanhf(a);
+    }
+  }
+  float a = P[30] * c.t[3][0];
+  a = fmaf(P[31], c.t[3][1], a);
+  a = fmaf(P[32], c.t[3][2], a);
+  return a + P[45];
+}
+
+// accumulate d(params) (packed positions, w.r.t. sp(M), b, tanh(f)) for dL/dlogit = g; returns dL/dx
+__device__ __forceinline__ float eb_bwd_acc(const float* P, const EbCache& c, float g, float* gp) {
+  float dt[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    gp[30 + i] += g * c.t[3][i];
+    dt[i] = g * P[30 + i];
+  }
+  gp[45] += g;
+#pragma unroll
+  for (int layer = 3; layer >= 1; --layer) {
+    const float* Mx = P + 3 + 9 * (layer - 1);
+    const float* fx = P + 49 + 3 * (layer - 1);
+    float da[3];
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      const float th = tanhf(c.a[layer][o]);
+      gp[49 + 3 * (layer - 1) + o] += dt[o] * th;
+      da[o] = dt[o] * (1.0f + fx[o] * (1.0f - th * th));
+      gp[36 + 3 * (layer - 1) + o] += da[o];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) gp[3 + 9 * (layer - 1) + o * 3 + i] += da[o] * c.t[layer - 1][i];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) dt[i] = da[0] * Mx[0 * 3 + i] + da[1] * Mx[1 * 3 + i] + da[2] * Mx[2 * 3 + i];
+  }
+  float dx = 0.0f;
+#pragma unroll
+  for (int o = 0; o < 3; ++o) {
+    const float th = tanhf(c.a[0][o]);
+    gp[46 + o] += dt[o] * th;
+    const float da = dt[o] * (1.0f + P[46 + o] * (1.0f - th * th));
+    gp[33 + o] += da;
+    gp[0 + o] += da * c.x;
+    dx += da * P[0 + o];
+  }
+  return dx;
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256)
+eb_bwd_kernel(long long npix, int C, const T* __restrict__ z, long long ldz,
+              const float* __restrict__ params, const float* __restrict__ noise,
+              const float* __restrict__ gbits, const T* __restrict__ dzhat, long long lddh,
+              T* __restrict__ dz, long long lddz, float* __restrict__ dparams) {
+  __shared__ float red[4][60];
+  const int ch = blockIdx.x;
+  const float* P = params + (size_t)ch * 64;
+  const float gb = *gbits;
+  float gp[59];
+#pragma unroll
+  for (int i = 0; i < 59; ++i) gp[i] = 0.0f;
+  for (long long pix = threadIdx.x; pix < npix; pix += 256) {
+    const long long e = pix * C + ch;
+    const float med = P[58];
+    const float zv = Elem<T>::ld(z + pix * ldz + ch);
+    const float xin = noise ? zv + noise[e] : rintf(zv - med) + med;
+    EbCache cl, cu;
+    const float lo = eb_fwd_cache(P, xin - 0.5f, cl);
+    const float up = eb_fwd_cache(P, xin + 0.5f, cu);
+    const float su = t_sigmoid(up), sl = t_sigmoid(lo);
+    const float lraw = su - sl;
+    const float lik = fmaxf(lraw, 1e-9f);
+    const float braw = (-1.0f * logf(lik + 1e-10f)) / 0.69314718055994530942f;
+    float gl = (braw >= 0.0f && braw <= 50.0f) ? gb * (-1.0f / ((lik + 1e-10f) * 0.69314718055994530942f)) : 0.0f;
+    if (!(lraw >= 1e-9f || gl < 0.0f)) gl = 0.0f;
+    const float gu = gl * su * (1.0f - su);
+    const float glo = -gl * sl * (1.0f - sl);
+    float dx = eb_bwd_acc(P, cu, gu, gp);
+    dx += eb_bwd_acc(P, cl, glo, gp);
+    float dzv = dzhat ? Elem<T>::ld(dzhat + pix * lddh + ch) : 0.0f;
+    if (noise) dzv += dx;
+    else gp[58] += dx;                        // dequantize: d x / d median = 1
+    Elem<T>::st(dz + pix * lddz + ch, dzv);
+  }
+  // block reduction of the 59 parameter gradients
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < 59; ++i) {
+    float v = gp[i];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if (lane == 0) red[wave][i] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int i = threadIdx.x;
+    float v = 0.0f;
+    if (i < 59) v = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    dparams[(size_t)ch * 64 + i] = v;
+  }
+}
+
+// ------------------------------------------------------------------ reconstruct_error backward
+// mode 0 (AutoEncoderRGB_Journal.py:36-64): mse = mean_b sum_c,p (m x - m xh)^2 / max(cnt_b, 1)
+//   -> dxh = g * 2 m (m xh - m x) / (B max(cnt_b, 1)); cnt_b from the forward's partials.
+// mode 1 (AutoEncoderMask_Journal.py:309): mse = mean (xh - x)^2 -> dxh = g * 2 (xh - x) / count.
+template <typename T>
+__global__ void __launch_bounds__(256)
+mse_bwd_kernel(int mode, int batch, int cx, int HW, int nblk, const float* __restrict__ x,
+               const T* __restrict__ xh, long long ldh, const float* __restrict__ mask,
+               const double* __restrict__ part, const float* __restrict__ gmse, T* __restrict__ dxh,
+               long long lddx) {
+  const int b = blockIdx.y;
+  __shared__ float scale_s;
+  if (threadIdx.x == 0) {
+    double cnt = 0.0;
+    if (mode == 0) {
+      for (int i = 0; i < nblk; ++i) cnt += part[((size_t)b * nblk + i) * 2 + 1];
+      scale_s = *gmse * 2.0f / ((float)batch * fmaxf((float)cnt, 1.0f));
+    } else {
+      scale_s = *gmse * 2.0f / ((float)batch * (float)cx * (float)HW);
+    }
+  }
+  __syncthreads();
+  const float sc = scale_s;
+  for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += gridDim.x * 256) {
+    const long long pix = (long long)b * HW + p;
+    const float m = mode == 0 ? (mask[pix] > 0.0f ? 1.0f : 0.0f) : 1.0f;
+    for (int c = 0; c < (int)lddx; ++c) {
+      float g = 0.0f;
+      if (c < cx) {
+        const float xv = x[((long long)b * cx + c) * HW + p];
+        const float hv = Elem<T>::ld(xh + pix * ldh + c);
+        g = mode == 0 ? sc * m * (hv * m - xv * m) : sc * (hv - xv);
+      }
+      Elem<T>::st(dxh + pix * lddx + c, g);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ optimizer
+// trainRGB.py:190-198: grad.clamp_(-clip, clip) then torch.optim.Adam (no weight
+// decay, no amsgrad): m = lerp(m, g, 1-b1); v = b2 v + (1-b2) g^2;
+// p -= step_size * m / (sqrt(v) / sqrt(bc2) + eps), step_size = lr / bc1.
+__global__ void __launch_bounds__(256)
+adam_clamp_kernel(long long n, float* __restrict__ p, float* __restrict__ g, float* __restrict__ m,
+                  float* __restrict__ v, float w1, float b2, float w2, float bc2_sqrt, float eps,
+                  float step_size, float clip, float gscale) {
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+    float gv = g[e];
+    if (gscale != 1.0f) gv *= gscale;             // data-parallel mean (after the all-reduce sum)
+    if (clip > 0.0f) gv = fminf(fmaxf(gv, -clip), clip);
+    g[e] = gv;
+    const float mv = m[e] + w1 * (gv - m[e]);
+    const float vv = v[e] * b2 + w2 * (gv * gv);
+    m[e] = mv;
+    v[e] = vv;
+    const float denom = sqrtf(vv) / bc2_sqrt + eps;
+    p[e] = p[e] + (-step_size) * (mv / denom);
+  }
+}
+
+// ------------------------------------------------------------------ layout helpers
+// dir 0: shuffle   in (B,H,W,4C) -> out (B,2H,2W,C), out[2y+i][2x+j][c] = in[y][x][4c+2i+j]
+// dir 1: unshuffle in (B,2H,2W,C) -> out (B,H,W,4C)
+template <typename T>
+__global__ void __launch_bounds__(256)
+pixel_shuffle_kernel(int dir, int batch, int H, int W, int C, const T* __restrict__ in,
+                     long long ldi, T* __restrict__ out, long long ldo) {
+  const long long n = (long long)batch * H * W * 4 * C;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+    const int cc = (int)(e % (4 * C));
+    const long long pix = e / (4 * C);
+    const int x = (int)(pix % W);
+    const long long t = pix / W;
+    const int y = (int)(t % H);
+    const int b = (int)(t / H);
+    const int c = cc >> 2, i = (cc >> 1) & 1, j = cc & 1;
+    const long long lo = pix * (dir == 0 ? ldi : ldo) + cc;
+    const long long hi = ((long long)(b * 2 * H + 2 * y + i) * (2 * W) + 2 * x + j) * (dir == 0 ? ldo : ldi) + c;
+    if (dir == 0) Elem<T>::st(out + hi, Elem<T>::ld(in + lo));
+    else Elem<T>::st(out + lo, Elem<T>::ld(in + hi));
+  }
+}
+
+// dst[p][dcoff + c] = src[p][scoff + c] for c < C   (channel concat / split)
+template <typename T>
+__global__ void __launch_bounds__(256)
+channel_copy_kernel(long long npix, int C, const T* __restrict__ src, long long lds, int scoff,
+                    T* __restrict__ dst, long long ldd, int dcoff) {
+  const long long n = npix * C;
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+    const long long p = e / C;
+    const int c = (int)(e - p * C);
+    dst[p * ldd + dcoff + c] = src[p * lds + scoff + c];
+  }
+}
+
+// ------------------------------------------------------------------ small helpers
+// packed[i] = idx[i] >= 0 ? (T) src[idx[i]] : 0   (weight repack through a cached map)
+template <typename T>
+__global__ void __launch_bounds__(256)
+gather_kernel(long long n, const float* __restrict__ src, const int* __restrict__ idx,
+              T* __restrict__ dst) {
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+    const int j = idx[e];
+    Elem<T>::st(dst + e, j >= 0 ? src[j] : 0.0f);
+  }
+}
+
+// partial[blk][c] = sum over the block's pixels of x[p][c]   (bias gradients)
+template <typename T>
+__global__ void __launch_bounds__(256)
+colsum_kernel(long long npix, int C, const T* __restrict__ x, long long ldx, long long chunk,
+              float* __restrict__ partial) {
+  const long long p0 = blockIdx.x * chunk;
+  long long p1 = p0 + chunk;
+  if (p1 > npix) p1 = npix;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.0f;
+    for (long long p = p0; p < p1; ++p) s += Elem<T>::ld(x + p * ldx + c);
+    partial[(size_t)blockIdx.x * C + c] = s;
+  }
+}
+
+// out[i] = (float) sum_j part[i][j] over n fp64 partials per row (fixed order)
+__global__ void __launch_bounds__(256)
+sum_rows_kernel(int rows, int n, const double* __restrict__ part, float* __restrict__ out) {
+  __shared__ double red[4];
+  for (int r = 0; r < rows; ++r) {
+    double s = 0.0;
+    for (int j = threadIdx.x; j < n; j += 256) s += part[(size_t)r * n + j];
+    s = block_sum_f64(s, red);
+    if (threadIdx.x == 0) out[r] = (float)s;
+  }
+}
+
+static int grid_for(long long n) {
+  long long g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  if (g < 1) g = 1;
+  return (int)g;
+}
+
+}  // namespace rgbac
+
+using namespace rgbac;
+
+#define RGBAC_DT_DISPATCH(dtype, KERNEL, ...)                                    \
+  do {                                                                           \
+    if ((dtype) == RGBAC_F32) { KERNEL(float, __VA_ARGS__); }                    \
+    else { KERNEL(bf16_t, __VA_ARGS__); }                                        \
+  } while (0)
+
+extern "C" int rgbac_act_bwd(int dtype, int act, float act_param, int64_t npix, int channels,
+                             const void* dy, int64_t ldy, const void* z, int64_t ldz,
+                             const void* res1, int64_t ld1, const uint8_t* sel, void* dz,
+                             int64_t lddz, void* dres1, int64_t lddr1, void* stream) {
+  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(act >= RGBAC_ACT_NONE && act <= RGBAC_ACT_MASKSEL, "act has no backward here");
+  RGBAC_REQUIRE(npix >= 0 && channels > 0 && lddz >= channels && ldy >= channels, "shape");
+  RGBAC_REQUIRE(dy && dz, "null pointer");
+  RGBAC_REQUIRE(act == RGBAC_ACT_NONE || act == RGBAC_ACT_MASKSEL || z, "act needs z");
+  RGBAC_REQUIRE(!(act == RGBAC_ACT_GATE || act == RGBAC_ACT_GDN || act == RGBAC_ACT_IGDN) || res1,
+                "act needs res1");
+  RGBAC_REQUIRE(act != RGBAC_ACT_MASKSEL || sel, "MASKSEL needs sel");
+  if (npix == 0) return RGBAC_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int g = grid_for(npix * lddz);
+#define K_(T, ...)                                                                            \
+  hipLaunchKernelGGL(act_bwd_kernel<T>, dim3(g), dim3(256), 0, st, act, act_param, npix,        \
+                     channels, (const T*)dy, ldy, (const T*)z, ldz, (const T*)res1, ld1, sel,   \
+                     (T*)dz, lddz, (T*)dres1, lddr1)
+  RGBAC_DT_DISPATCH(dtype, K_, 0);
+#undef K_
+  return check_launch("act_bwd_kernel");
+}
+
+extern "C" int rgbac_conv_wgrad(const rgbac_wgrad_args* a, void* stream) {
+  RGBAC_REQUIRE(a != nullptr, "null args");
+  RGBAC_REQUIRE(a->dtype == RGBAC_F32 || a->dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(a->batch > 0 && a->grid_h > 0 && a->grid_w > 0, "grid");
+  RGBAC_REQUIRE(a->g && a->partial, "null pointer");
+  RGBAC_REQUIRE(a->g_ldc % 8 == 0 && a->g_channels > 0 && a->g_channels <= a->g_ldc &&
+                    a->g_channels % 8 == 0, "g channels must be a multiple of 8 within g_ldc");
+  RGBAC_REQUIRE(a->ksize >= 1 && a->ksize <= 5 && a->stride >= 1 && a->stride <= 2 &&
+                    a->pad >= 0 && a->pad < a->ksize, "kernel geometry");
+  RGBAC_REQUIRE(a->nsrc >= 1 && a->nsrc <= 3, "nsrc must be 1..3");
+  RGBAC_REQUIRE(a->n_pad % 64 == 0 && a->n_pad >= a->g_channels, "n_pad");
+  int csum = 0;
+  for (int i = 0; i < a->nsrc; ++i) {
+    RGBAC_REQUIRE(a->src[i].ptr && a->src[i].channels % 8 == 0 && a->src[i].channels > 0 &&
+                      a->src[i].ldc % 8 == 0 && a->src[i].ldc >= a->src[i].channels,
+                  "bad source");
+    RGBAC_REQUIRE(((uintptr_t)a->src[i].ptr) % 16 == 0, "source pointers must be 16-byte aligned");
+    csum += a->src[i].channels;
+  }
+  RGBAC_REQUIRE(csum == a->cin_pad, "sum of source channels must equal cin_pad");
+  const int K = a->ksize * a->ksize * a->cin_pad;
+  RGBAC_REQUIRE(a->k_pad % 64 == 0 && a->k_pad >= K, "k_pad");
+  RGBAC_REQUIRE(a->nsplit >= 1 && a->nsplit <= 4096, "nsplit");
+  const long long M = (long long)a->batch * a->grid_h * a->grid_w;
+  RGBAC_REQUIRE(M < (1ll << 31), "too many pixels");
+  WgradDev d{};
+  d.g = a->g; d.ldg = a->g_ldc; d.gch = a->g_channels;
+  d.sp0 = a->src[0].ptr; d.sld0 = a->src[0].ldc; d.send0 = a->src[0].channels;
+  d.sp1 = a->nsrc > 1 ? a->src[1].ptr : d.sp0;
+  d.sld1 = a->nsrc > 1 ? a->src[1].ldc : d.sld0;
+  d.send1 = d.send0 + (a->nsrc > 1 ? a->src[1].channels : 0);
+  d.sp2 = a->nsrc > 2 ? a->src[2].ptr : d.sp1;
+  d.sld2 = a->nsrc > 2 ? a->src[2].ldc : d.sld1;
+  d.send2 = d.send1 + (a->nsrc > 2 ? a->src[2].channels : 0);
+  d.cin_pad = a->cin_pad; d.K = K; d.k_pad = a->k_pad; d.n_pad = a->n_pad;
+  d.M = (int)M; d.Hg = a->grid_h; d.Wg = a->grid_w;
+  d.in_h = a->in_h; d.in_w = a->in_w; d.ksize = a->ksize; d.stride = a->stride; d.pad = a->pad;
+  d.square = a->square_input;
+  d.m_chunk = (int)(((M + a->nsplit - 1) / a->nsplit + 63) / 64 * 64);
+  d.part = a->partial;
+  d.bpart = a->bias_partial;
+  dim3 grid(a->k_pad / 64, a->n_pad / 64, a->nsplit);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (a->dtype == RGBAC_F32)
+    hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, d);
+  else
+    hipLaunchKernelGGL(wgrad_kernel<bf16_t>, grid, dim3(256), 0, st, d);
+  return check_launch("wgrad_kernel");
+}
+
+extern "C" int rgbac_wgrad_reduce(int64_t numel, const int32_t* map, const float* partial,
+                                  int nsplit, int64_t slab, float* dw, int nbias,
+                                  const float* bias_partial, int n_pad, float* db, void* stream) {
+  RGBAC_REQUIRE(numel >= 0 && nsplit >= 1 && slab > 0, "shape");
+  RGBAC_REQUIRE((numel == 0 || (map && partial && dw)) && (nbias == 0 || (bias_partial && db)),
+                "null pointer");
+  RGBAC_REQUIRE(nbias <= n_pad, "nbias > n_pad");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(numel + nbias)), dim3(256), 0, st, numel,
+                     map, partial, nsplit, slab, dw, nbias, bias_partial, n_pad, db);
+  return check_launch("wgrad_reduce_kernel");
+}
+
+extern "C" int rgbac_winattn_core_bwd(int dtype, int batch, int h, int w, int channels, int heads,
+                                      int ws, int shift, int masked, float scale, const void* qkv,
+                                      int64_t ldq, const float* alpha, const float* bias,
+                                      const void* dout, int64_t ldo, void* dqkv, int64_t lddq,
+                                      int nblk, float* bias_partial, void* stream) {
+  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(ws == 4 || ws == 8, "window size must be 4 or 8");
+  RGBAC_REQUIRE(batch > 0 && h > 0 && w > 0 && h % ws == 0 && w % ws == 0, "shape");
+  RGBAC_REQUIRE(heads > 0 && channels % heads == 0 && channels / heads <= 24, "head dim");
+  RGBAC_REQUIRE(shift >= 0 && shift < ws, "shift");
+  RGBAC_REQUIRE(qkv && dout && dqkv && bias && bias_partial, "null pointer");
+  RGBAC_REQUIRE(!masked || alpha, "masked attention needs alpha");
+  RGBAC_REQUIRE(nblk >= 1 && nblk <= 65535, "nblk");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid(nblk, heads);
+#define K_(T, WS_)                                                                              \
+  hipLaunchKernelGGL((winattn_bwd_kernel<T, WS_>), grid, dim3(256), 0, st, batch, h, w, channels, \
+                     heads, shift, masked, scale, (const T*)qkv, ldq, alpha, bias,                \
+                     (const T*)dout, ldo, (T*)dqkv, lddq, bias_partial)
+  if (ws == 8) { RGBAC_DT_DISPATCH(dtype, K_, 8); }
+  else { RGBAC_DT_DISPATCH(dtype, K_, 4); }
+#undef K_
+  return check_launch("winattn_bwd_kernel");
+}
+
+extern "C" int rgbac_relpos_bwd(int nblk, int heads, int ws, const float* bias_partial,
+                                const int64_t* index, float* dense, float* dtable, void* stream) {
+  RGBAC_REQUIRE(ws == 4 || ws == 8, "window size");
+  RGBAC_REQUIRE(nblk >= 1 && heads > 0 && bias_partial && index && dense && dtable, "args");
+  const int N = ws * ws;
+  const int ntab = (2 * ws - 1) * (2 * ws - 1);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(relpos_reduce_kernel, dim3(grid_for((long long)heads * N * N)), dim3(256), 0,
+                     st, nblk, heads, N, bias_partial, dense);
+  int rc = check_launch("relpos_reduce_kernel");
+  if (rc) return rc;
+  hipLaunchKernelGGL(relpos_scatter_kernel, dim3(grid_for((long long)ntab * heads)), dim3(256), 0,
+                     st, ntab, heads, N, index, dense, dtable);
+  return check_launch("relpos_scatter_kernel");
+}
+
+extern "C" int rgbac_gaussian_bwd(int dtype, int64_t npix, int nch, const void* y, int64_t ldy,
+                                  const void* mu, int64_t ldmu, const void* scale, int64_t lds,
+                                  const float* noise, const float* gbits, const void* dhat,
+                                  int64_t lddh, void* dy, int64_t lddy, void* dmu, int64_t lddmu,
+                                  void* dscale, int64_t lddsc, void* stream) {
+  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(npix > 0 && nch > 0, "empty slice");
+  RGBAC_REQUIRE(y && mu && scale && gbits && dy && dmu && dscale, "null pointer");
+  const long long n = npix * (long long)nch;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define K_(T, ...)                                                                              \
+  hipLaunchKernelGGL(gaussian_bwd_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, n, nch,      \
+                     (const T*)y, ldy, (const T*)mu, ldmu, (const T*)scale, lds, noise, gbits,  \
+                     (const T*)dhat, lddh, (T*)dy, lddy, (T*)dmu, lddmu, (T*)dscale, lddsc)
+  RGBAC_DT_DISPATCH(dtype, K_, 0);
+#undef K_
+  return check_launch("gaussian_bwd_kernel");
+}
+
+extern "C" int rgbac_eb_bwd(int dtype, int64_t npix, int channels, const void* z, int64_t ldz,
+                            const float* params, const float* noise, const float* gbits,
+                            const void* dzhat, int64_t lddh, void* dz, int64_t lddz,
+                            float* dparams, void* stream) {
+  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(npix > 0 && channels > 0, "empty tensor");
+  RGBAC_REQUIRE(z && params && gbits && dz && dparams, "null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define K_(T, ...)                                                                              \
+  hipLaunchKernelGGL(eb_bwd_kernel<T>, dim3(channels), dim3(256), 0, st, npix, channels,        \
+                     (const T*)z, ldz, params, noise, gbits, (const T*)dzhat, lddh, (T*)dz, lddz, \
+                     dparams)
+  RGBAC_DT_DISPATCH(dtype, K_, 0);
+#undef K_
+  return check_launch("eb_bwd_kernel");
+}
+
+extern "C" int rgbac_mse_bwd(int dtype, int mode, int batch, int cx, int h, int w, const float* x,
+                             const void* x_hat, int64_t ldh, const float* mask,
+                             const double* scratch, const float* gmse, void* dx_hat, int64_t lddx,
+                             void* stream) {
+  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(mode == 0 || mode == 1, "mode");
+  RGBAC_REQUIRE(batch > 0 && cx > 0 && h > 0 && w > 0 && lddx >= cx, "shape");
+  RGBAC_REQUIRE(x && x_hat && gmse && dx_hat && (mode == 1 || (mask && scratch)), "null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  dim3 grid(64, batch);
+#define K_(T, ...)                                                                              \
+  hipLaunchKernelGGL(mse_bwd_kernel<T>, grid, dim3(256), 0, st, mode, batch, cx, h * w, 64, x,   \
+                     (const T*)x_hat, ldh, mask, scratch, gmse, (T*)dx_hat, lddx)
+  RGBAC_DT_DISPATCH(dtype, K_, 0);
+#undef K_
+  return check_launch("mse_bwd_kernel");
+}
+
+extern "C" int rgbac_adam_clamp(int64_t n, float* param, float* grad, float* exp_avg,
+                                float* exp_avg_sq, double lr, double beta1, double beta2,
+                                double eps, int64_t step, float clip, float grad_scale,
+                                void* stream) {
+  RGBAC_REQUIRE(n >= 0 && step >= 1, "shape/step");
+  RGBAC_REQUIRE(n == 0 || (param && grad && exp_avg && exp_avg_sq), "null pointer");
+  if (n == 0) return RGBAC_OK;
+  // scalars exactly as torch.optim.Adam forms them (python doubles, applied in fp32)
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(adam_clamp_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, param, grad,
+                     exp_avg, exp_avg_sq, (float)(1.0 - beta1), (float)beta2,
+                     (float)(1.0 - beta2), (float)std::sqrt(bc2), (float)eps,
+                     (float)(lr / bc1), clip, grad_scale);
+  return check_launch("adam_clamp_kernel");
+}
+
+extern "C" int rgbac_pixel_shuffle(int dtype, int dir, int batch, int h, int w, int c,
+                                   const void* in, int64_t ldi, void* out, int64_t ldo,
+                                   void* stream) {
+  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(dir == 0 || dir == 1, "dir");
+  RGBAC_REQUIRE(batch > 0 && h > 0 && w > 0 && c > 0 && in && out, "shape");
+  RGBAC_REQUIRE(dir == 0 ? (ldi >= 4 * c && ldo >= c) : (ldi >= c && ldo >= 4 * c), "strides");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const long long n = (long long)batch * h * w * 4 * c;
+#define K_(T, ...)                                                                              \
+  hipLaunchKernelGGL(pixel_shuffle_kernel<T>, dim3(grid_for(n)), dim3(256), 0, st, dir, batch, h, \
+                     w, c, (const T*)in, ldi, (T*)out, ldo)
+  RGBAC_DT_DISPATCH(dtype, K_, 0);
+#undef K_
+  return check_launch("pixel_shuffle_kernel");
+}
+
+extern "C" int rgbac_channel_copy(int dtype, int64_t npix, int channels, const void* src,
+                                  int64_t lds, int scoff, void* dst, int64_t ldd, int dcoff,
+                                  void* stream) {
+  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(npix >= 0 && channels > 0 && src && dst, "shape");
+  RGBAC_REQUIRE(scoff + channels <= lds && dcoff + channels <= ldd, "channel range");
+  if (npix == 0) return RGBAC_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const long long n = npix * channels;
+  if (dtype == RGBAC_F32)
+    hipLaunchKernelGGL(channel_copy_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, npix,
+                       channels, (const float*)src, lds, scoff, (float*)dst, ldd, dcoff);
+  else
+    hipLaunchKernelGGL(channel_copy_kernel<uint16_t>, dim3(grid_for(n)), dim3(256), 0, st, npix,
+                       channels, (const uint16_t*)src, lds, scoff, (uint16_t*)dst, ldd, dcoff);
+  return check_launch("channel_copy_kernel");
+}
+
+extern "C" int rgbac_weight_gather(int dtype, int64_t n, const float* src, const int32_t* idx,
+                                   void* dst, void* stream) {
+  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(n >= 0 && (n == 0 || (src && idx && dst)), "args");
+  if (n == 0) return RGBAC_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == RGBAC_F32)
+    hipLaunchKernelGGL(gather_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, n, src, idx,
+                       (float*)dst);
+  else
+    hipLaunchKernelGGL(gather_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, n, src, idx,
+                       (bf16_t*)dst);
+  return check_launch("gather_kernel");
+}
+
+extern "C" int rgbac_colsum(int dtype, int64_t npix, int channels, const void* x, int64_t ldx,
+                            int nsplit, float* partial, void* stream) {
+  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(npix > 0 && channels > 0 && ldx >= channels && x && partial, "args");
+  RGBAC_REQUIRE(nsplit >= 1 && nsplit <= 65535, "nsplit");
+  const long long chunk = (npix + nsplit - 1) / nsplit;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == RGBAC_F32)
+    hipLaunchKernelGGL(colsum_kernel<float>, dim3(nsplit), dim3(256), 0, st, npix, channels,
+                       (const float*)x, ldx, chunk, partial);
+  else
+    hipLaunchKernelGGL(colsum_kernel<bf16_t>, dim3(nsplit), dim3(256), 0, st, npix, channels,
+                       (const bf16_t*)x, ldx, chunk, partial);
+  return check_launch("colsum_kernel");
+}
+
+extern "C" int rgbac_sum_partials(int rows, int n, const double* partial, float* out,
+                                  void* stream) {
+  RGBAC_REQUIRE(rows >= 1 && n >= 1 && partial && out, "args");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(256), 0, st, rows, n, partial, out);
+  return check_launch("sum_rows_kernel");
+}

@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(_HERE, "librgbac_hip.so")
 
 F32, BF16 = 0, 1
 ACT = dict(none=0, gelu=1, relu=2, lrelu=3, tanh_half=4, gate=5, gdn=6, igdn=7, masksel=8,
-           gauss=9)
+           gauss=9, sqbwd=10)
 CONV, CONVT_S2, SUBPEL2 = 0, 1, 2
 
 
@@ -43,10 +43,28 @@ class ConvArgs(ctypes.Structure):
         ("tile", ctypes.c_int32), ("ksplit", ctypes.c_int32),
         ("workspace", ctypes.c_void_p),
         ("aux0", ctypes.c_void_p), ("aux1", ctypes.c_void_p), ("partial", ctypes.c_void_p),
+        ("zout", ctypes.c_void_p), ("zout_ldc", ctypes.c_int64),
+    ]
+
+
+class WgradArgs(ctypes.Structure):
+    _fields_ = [
+        ("dtype", ctypes.c_int32),
+        ("batch", ctypes.c_int32), ("grid_h", ctypes.c_int32), ("grid_w", ctypes.c_int32),
+        ("g", ctypes.c_void_p), ("g_ldc", ctypes.c_int64), ("g_channels", ctypes.c_int32),
+        ("in_h", ctypes.c_int32), ("in_w", ctypes.c_int32), ("ksize", ctypes.c_int32),
+        ("stride", ctypes.c_int32), ("pad", ctypes.c_int32),
+        ("nsrc", ctypes.c_int32), ("cin_pad", ctypes.c_int32),
+        ("src", Src * 3),
+        ("square_input", ctypes.c_int32),
+        ("n_pad", ctypes.c_int32), ("k_pad", ctypes.c_int32),
+        ("nsplit", ctypes.c_int32),
+        ("partial", ctypes.c_void_p), ("bias_partial", ctypes.c_void_p),
     ]
 
 
 _VP, _I32, _I64, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
+_D = ctypes.c_double
 # name -> argtypes (restype int unless noted); must match include/rgbac.h
 SIGNATURES = {
     "rgbac_abi_version": [],
@@ -66,6 +84,25 @@ SIGNATURES = {
     "rgbac_mask_pyramid": [_I32, _I32, _I32, _VP, _I32, _VP, _I32, _VP, _VP],
     "rgbac_nchw_to_nhwc": [_I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP],
     "rgbac_nhwc_to_nchw": [_I32, _I32, _I32, _I32, _I32, _VP, _I64, _VP, _VP],
+    # training step
+    "rgbac_act_bwd": [_I32, _I32, _F, _I64, _I32, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP,
+                      _I64, _VP, _I64, _VP],
+    "rgbac_conv_wgrad": [ctypes.POINTER(WgradArgs), _VP],
+    "rgbac_wgrad_reduce": [_I64, _VP, _VP, _I32, _I64, _VP, _I32, _VP, _I32, _VP, _VP],
+    "rgbac_winattn_core_bwd": [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _F, _VP,
+                               _I64, _VP, _VP, _VP, _I64, _VP, _I64, _I32, _VP, _VP],
+    "rgbac_relpos_bwd": [_I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP],
+    "rgbac_gaussian_bwd": [_I32, _I64, _I32, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP, _VP,
+                           _I64, _VP, _I64, _VP, _I64, _VP, _I64, _VP],
+    "rgbac_eb_bwd": [_I32, _I64, _I32, _VP, _I64, _VP, _VP, _VP, _VP, _I64, _VP, _I64, _VP, _VP],
+    "rgbac_mse_bwd": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP, _VP, _VP, _VP,
+                      _I64, _VP],
+    "rgbac_adam_clamp": [_I64, _VP, _VP, _VP, _VP, _D, _D, _D, _D, _I64, _F, _F, _VP],
+    "rgbac_pixel_shuffle": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _I64, _VP, _I64, _VP],
+    "rgbac_channel_copy": [_I32, _I64, _I32, _VP, _I64, _I32, _VP, _I64, _I32, _VP],
+    "rgbac_weight_gather": [_I32, _I64, _VP, _VP, _VP, _VP],
+    "rgbac_colsum": [_I32, _I64, _I32, _VP, _I64, _I32, _VP, _VP],
+    "rgbac_sum_partials": [_I32, _I32, _VP, _VP, _VP],
 }
 
 _lib = None

@@ -1,0 +1,683 @@
+"""Training path: torch.autograd.Function wrappers over the HIP kernels.
+
+SURVEY.md §8b: "The Python torch.autograd.Function wrappers call *_fwd/*_bwd".
+Every Function's forward is the same HIP launch the inference path uses (with
+the pre-activation saved through ``zout``); its backward is HIP too:
+
+  ConvFn      conv / convT / subpel / Linear / GDN with fused epilogue
+              backward = rgbac_act_bwd -> input-gradient conv on the MFMA conv
+              engine over a repacked weight (+ SQBWD epilogue for GDN) ->
+              rgbac_conv_wgrad + rgbac_wgrad_reduce (weight, bias)
+  WinAttnFn   rgbac_winattn_core / rgbac_winattn_core_bwd + rgbac_relpos_bwd
+  GaussFn     rgbac_gaussian_slice / rgbac_gaussian_bwd
+  EBFn        rgbac_eb_forward / rgbac_eb_bwd
+  MSEFn       rgbac_finalize / rgbac_mse_bwd
+  CatFn, ToNCHW   channel concat / layout change (rgbac_channel_copy, layout kernels)
+
+Tensors crossing Function boundaries are NHWC (B, H, W, ldc) with zero padding
+channels (runtime.Feat).  Weights are repacked each step by ONE gather launch
+through an index map computed once per layer (``PackMap``); the map's inverse
+scatters the weight-gradient slabs straight into the PyTorch parameter layout.
+Parameter-side reparametrisations (GDN beta'/gamma', EntropyBottleneck
+softplus/tanh) stay torch autograd on O(#params) tensors.
+"""
+import ctypes
+
+import torch
+from torch.autograd import Function
+
+from . import _lib
+from . import runtime as rt
+from .runtime import CONV, CONVT_S2, SUBPEL2, Feat, new_feat, round_up
+
+_F32 = torch.float32
+
+
+def _stream(t):
+    return _lib.stream_ptr(t.device)
+
+
+# --------------------------------------------------------------------------
+# index-map weight packing
+# --------------------------------------------------------------------------
+def _pack_map(idx_w, mode, segs, stride=1, transposed=False):
+    """Run runtime.PackedConv over a weight of (flat index + 1) values: the packed
+    buffer then holds, per slot, 1 + the source element it takes (0 = zero pad)."""
+    pk = rt.PackedConv(idx_w, None, mode, segs, _F32, stride=stride, transposed=transposed)
+    idx = (pk.w.round().to(torch.int32) - 1).contiguous()
+    return pk, idx
+
+
+def _inverse(idx, numel, k_pad):
+    """param element -> slab position n * k_pad + k of a phase-0 packed map."""
+    inv = torch.full((numel,), -1, dtype=torch.int32, device=idx.device)
+    flat = idx[0].reshape(-1) if idx.dim() == 3 else idx.reshape(-1)
+    pos = torch.nonzero(flat >= 0).squeeze(1)
+    inv[flat[pos].long()] = pos.to(torch.int32)
+    return inv
+
+
+class TPack:
+    """A packed weight (same fields runtime.prepare reads from a PackedConv),
+    refilled from the fp32 parameter by rgbac_weight_gather."""
+
+    def __init__(self, pk, idx, dtype, bias_idx=None):
+        self.mode, self.ksize, self.stride = pk.mode, pk.ksize, pk.stride
+        self.cin, self.cin_pad, self.cout = pk.cin, pk.cin_pad, pk.cout
+        self.cout_pad, self.k_pad = pk.cout_pad, pk.k_pad
+        self.idx = idx
+        self.bias_idx = bias_idx
+        self.w = torch.empty(idx.shape, dtype=dtype, device=idx.device)
+        self.bias = torch.zeros(pk.cout_pad, dtype=_F32, device=idx.device)
+
+    def refresh(self, weight, bias=None):
+        # always re-gathered: the optimizer kernel updates parameters in place
+        # through raw pointers (no autograd version bump), and one gather per
+        # layer per step is cheap next to the conv it feeds
+        w = weight.detach()
+        assert w.dtype == _F32 and w.is_contiguous()
+        dev = w.device
+        _lib.call("rgbac_weight_gather", _lib.dtype_code(self.w.dtype), self.w.numel(),
+                  w.data_ptr(), self.idx.data_ptr(), self.w.data_ptr(), _lib.stream_ptr(dev))
+        if bias is not None:
+            b = bias.detach()
+            _lib.call("rgbac_weight_gather", _lib.F32, self.bias.numel(), b.data_ptr(),
+                      self.bias_idx.data_ptr(), self.bias.data_ptr(), _lib.stream_ptr(dev))
+        return self
+
+
+class TrainConv:
+    """Packing maps of one layer for the training path.
+
+    kind: 'conv' (Conv2d / Linear as 1x1), 'convt' (ConvTranspose2d k5 s2 p2 op1 or
+    k1), 'subpel' (compressai subpel_conv3x3's conv, PixelShuffle(2) in the store),
+    'gdn' (the 1x1 gamma' conv of GDN on x^2).  ``segs``: [(real, padded)] channel
+    segments of the sources (conv-like kinds) or of the convT input."""
+
+    def __init__(self, kind, wshape, stride, segs, device):
+        self.kind, self.stride, self.segs = kind, stride, list(segs)
+        self.wshape = tuple(wshape)
+        numel = 1
+        for d in wshape:
+            numel *= d
+        self.numel = numel
+        w4 = self.wshape if len(wshape) == 4 else (wshape[0], wshape[1], 1, 1)
+        k = w4[2]
+        self.ksize = k
+        base = (torch.arange(numel, device=device, dtype=_F32) + 1).reshape(w4)
+        if kind == "convt":
+            cin_t, cout_t = w4[0], w4[1]
+            out_segs = [(cout_t, round_up(cout_t, 8))]
+            if k == 1:
+                self.fwd = _pack_map(base, CONV, segs, transposed=True)
+            else:
+                assert k == 5 and stride == 2
+                self.fwd = _pack_map(base, CONVT_S2, segs, stride=2)
+            # input gradient: conv of dY with W_t viewed as (cout = cin_t, cin = cout_t)
+            self.bwd = [_pack_map(base, CONV, out_segs, stride=1 if k == 1 else 2)]
+            wg = self.bwd[0]
+            self.cout = cout_t
+            self.rows = cin_t
+        else:
+            cout, cin = w4[0], w4[1]
+            mode = SUBPEL2 if kind == "subpel" else CONV
+            self.fwd = _pack_map(base, mode, segs, stride=stride)
+            g_segs = [(cout, round_up(cout, 8))]
+            self.bwd = []
+            col = 0
+            for real, padded in segs:
+                sub = base[:, col:col + real]
+                col += real
+                if stride == 1:
+                    t = sub.transpose(0, 1).flip(2, 3).contiguous()
+                    self.bwd.append(_pack_map(t, CONV, g_segs))
+                else:
+                    # stride-2 conv: input gradient = ConvTranspose(k5, s2, p2, op1); a 3x3
+                    # (pad 1) kernel is embedded in the 5x5 frame (same output geometry)
+                    if k == 3:
+                        t = torch.zeros((cout, real, 5, 5), device=device)
+                        t[:, :, 1:4, 1:4] = sub
+                        sub = t
+                    assert sub.shape[2] == 5
+                    self.bwd.append(_pack_map(sub.contiguous(), CONVT_S2, g_segs, stride=2))
+            wg = self.fwd
+            self.cout = cout
+            self.rows = cout
+        pkw, idxw = wg
+        self.wg_kpad = pkw.k_pad
+        self.wg_map = _inverse(idxw, numel, pkw.k_pad)
+        self.bias_idx = {}
+        self._fw = {}
+        self._bw = {}
+
+    def _bidx(self, pk, nreal):
+        key = (pk.cout_pad, nreal)
+        if key not in self.bias_idx:
+            b = torch.full((pk.cout_pad,), -1, dtype=torch.int32, device=self.wg_map.device)
+            b[:nreal] = torch.arange(nreal, dtype=torch.int32, device=b.device)
+            self.bias_idx[key] = b
+        return self.bias_idx[key]
+
+    def fwd_pack(self, dtype, weight, bias):
+        tp = self._fw.get(dtype)
+        if tp is None:
+            pk, idx = self.fwd
+            nb = self.cout if self.kind != "subpel" else pk.cout
+            tp = TPack(pk, idx, dtype, self._bidx(pk, nb))
+            self._fw[dtype] = tp
+        return tp.refresh(weight, bias)
+
+    def bwd_pack(self, i, dtype, weight):
+        tp = self._bw.get((i, dtype))
+        if tp is None:
+            pk, idx = self.bwd[i]
+            tp = TPack(pk, idx, dtype)
+            self._bw[(i, dtype)] = tp
+        return tp.refresh(weight, None)
+
+
+def train_conv_of(m, kind, wshape, stride, segs, device):
+    key = (kind, tuple(segs), tuple(wshape))
+    cache = m.__dict__.setdefault("_rgbac_train", {})
+    tc = cache.get(key)
+    if tc is None:
+        tc = TrainConv(kind, wshape, stride, segs, device)
+        cache[key] = tc
+    return tc
+
+
+# --------------------------------------------------------------------------
+# weight gradient (rgbac_conv_wgrad + rgbac_wgrad_reduce)
+# --------------------------------------------------------------------------
+def _nsplit(tiles, M):
+    want = max(1, -(-2048 // tiles))
+    return int(max(1, min(want, -(-M // 512), 1024)))
+
+
+def wgrad(G, S, ksize, stride, pad, square, k_pad, inv_map, numel, nbias=0, bias_from_g=True):
+    """dW (fp32, flat param layout) and optional db from G (Feat on the M grid) and
+    sources S [Feat] sampled with (ksize, stride, pad)."""
+    dev = G.t.device
+    n_pad = round_up(G.ldc, 64)
+    M = G.B * G.H * G.W
+    tiles = (k_pad // 64) * (n_pad // 64)
+    ns = _nsplit(tiles, M)
+    part = torch.empty(ns * n_pad * k_pad, dtype=_F32, device=dev)
+    bpart = None
+    if nbias and bias_from_g:
+        bpart = torch.empty(ns * n_pad, dtype=_F32, device=dev)
+    a = _lib.WgradArgs()
+    a.dtype = _lib.dtype_code(G.t.dtype)
+    a.batch, a.grid_h, a.grid_w = G.B, G.H, G.W
+    a.g, a.g_ldc, a.g_channels = G.ptr(), G.ldc, G.ldc
+    s0 = S[0]
+    a.in_h, a.in_w, a.ksize, a.stride, a.pad = s0.H, s0.W, ksize, stride, pad
+    a.nsrc = len(S)
+    cin = 0
+    for i, f in enumerate(S):
+        assert f.t.dtype == G.t.dtype and f.B == G.B
+        a.src[i].ptr, a.src[i].ldc, a.src[i].channels = f.ptr(), f.ldc, f.ldc
+        cin += f.ldc
+    a.cin_pad = cin
+    a.square_input = 1 if square else 0
+    a.n_pad, a.k_pad, a.nsplit = n_pad, k_pad, ns
+    a.partial = part.data_ptr()
+    a.bias_partial = None if bpart is None else bpart.data_ptr()
+    st = _stream(G.t)
+    rt.timed("wgrad_kernel", 2.0 * M * G.ldc * ksize * ksize * cin,
+             G.t.element_size() * M * (G.ldc + cin * ksize * ksize // max(1, stride * stride)),
+             lambda: _lib.call("rgbac_conv_wgrad", ctypes.byref(a), st))
+    dw = torch.empty(numel, dtype=_F32, device=dev)
+    db = torch.empty(nbias, dtype=_F32, device=dev) if nbias else None
+    if nbias and not bias_from_g:
+        raise ValueError("use colsum for biases not on G")
+    _lib.call("rgbac_wgrad_reduce", numel, inv_map.data_ptr(), part.data_ptr(), ns,
+              n_pad * k_pad, dw.data_ptr(), nbias if bpart is not None else 0,
+              None if bpart is None else bpart.data_ptr(), n_pad,
+              None if db is None else db.data_ptr(), st)
+    return dw, db
+
+
+def colsum(f, C):
+    """Per-channel sum over pixels of Feat ``f`` (first C channels) -> fp32 (C,)."""
+    dev = f.t.device
+    npix = f.B * f.H * f.W
+    ns = int(max(1, min(1024, -(-npix // 256))))
+    part = torch.empty(ns * C, dtype=_F32, device=dev)
+    st = _stream(f.t)
+    _lib.call("rgbac_colsum", _lib.dtype_code(f.t.dtype), npix, C, f.ptr(), f.ldc, ns,
+              part.data_ptr(), st)
+    db = torch.empty(C, dtype=_F32, device=dev)
+    _lib.call("rgbac_wgrad_reduce", 0, None, None, ns, 1, None, C, part.data_ptr(), C,
+              db.data_ptr(), st)
+    return db
+
+
+# --------------------------------------------------------------------------
+# ConvFn
+# --------------------------------------------------------------------------
+_NEEDS_Z = {"gelu", "relu", "lrelu", "tanh_half", "gate", "gdn", "igdn"}
+
+
+class ConvCall:
+    """Non-tensor description of one training conv (ctx of ConvFn)."""
+    __slots__ = ("tc", "src_C", "act", "act_param", "square")
+
+    def __init__(self, tc, src_C, act, act_param, square=False):
+        self.tc, self.src_C, self.act, self.act_param = tc, list(src_C), act, act_param
+        self.square = square
+
+
+def _act_bwd(act, slope, dy, z, r1, sel, C, want_r1):
+    dev = dy.t.device
+    dz = Feat(torch.empty_like(dy.t), C)
+    dr1 = Feat(torch.empty_like(dy.t), C) if want_r1 else None
+    npix = dy.B * dy.H * dy.W
+    _lib.call("rgbac_act_bwd", _lib.dtype_code(dy.t.dtype), _lib.ACT[act], slope, npix, C,
+              dy.ptr(), dy.ldc, None if z is None else z.ptr(), 0 if z is None else z.ldc,
+              None if r1 is None else r1.ptr(), 0 if r1 is None else r1.ldc,
+              _lib.ptr(sel), dz.ptr(), dz.ldc, None if dr1 is None else dr1.ptr(),
+              0 if dr1 is None else dr1.ldc, _lib.stream_ptr(dev))
+    return dz, dr1
+
+
+class ConvFn(Function):
+    @staticmethod
+    def forward(ctx, call, weight, bias, res0, res1, res2, sel, *srcs):
+        tc = call.tc
+        dt = srcs[0].dtype
+        feats = [Feat(t, c) for t, c in zip(srcs, call.src_C)]
+        pk = tc.fwd_pack(dt, weight.contiguous(), bias)
+        f0 = feats[0]
+        if tc.kind == "convt" and tc.ksize == 5:
+            Ho, Wo, Cs = 2 * f0.H, 2 * f0.W, tc.cout
+        elif tc.kind == "subpel":
+            Ho, Wo, Cs = 2 * f0.H, 2 * f0.W, tc.cout // 4
+        else:
+            s = tc.stride
+            p = tc.ksize // 2
+            Ho = (f0.H + 2 * p - tc.ksize) // s + 1
+            Wo = (f0.W + 2 * p - tc.ksize) // s + 1
+            Cs = tc.cout
+        out = new_feat(f0.B, Ho, Wo, Cs, dt, f0.t.device)
+        z = new_feat(f0.B, Ho, Wo, Cs, dt, f0.t.device) if call.act in _NEEDS_Z else None
+
+        def rf(r):
+            return None if r is None else Feat(r, Cs)
+        pr = rt.prepare(pk, [f.src() for f in feats], out=out, act=call.act,
+                        act_param=call.act_param, res0=rf(res0), res1=rf(res1), res2=rf(res2),
+                        sel=sel, square=call.square, bias=bias is not None, zout=z)
+        rt.launch([pr])
+        ctx.call = call
+        ctx.has = (bias is not None, res0 is not None, res1 is not None, res2 is not None)
+        ctx.shape = (f0.B, Ho, Wo, Cs)
+        keep_r1 = res1 if call.act in ("gate", "gdn", "igdn") else None
+        ctx.save_for_backward(weight, None if z is None else z.t, keep_r1, sel, *srcs)
+        if sel is not None:
+            ctx.mark_non_differentiable(sel)
+        return out.t
+
+    @staticmethod
+    def backward(ctx, dy_t):
+        call = ctx.call
+        tc = call.tc
+        weight, z_t, r1_t, sel, *srcs = ctx.saved_tensors
+        has_b, has0, has1, has2 = ctx.has
+        B, Ho, Wo, Cs = ctx.shape
+        dy = Feat(dy_t.contiguous(), Cs)
+        dt = dy.t.dtype
+        act = call.act
+        z = None if z_t is None else Feat(z_t, Cs)
+        r1 = None if r1_t is None else Feat(r1_t, Cs)
+        if act == "none":
+            dz, dr1 = dy, None
+        else:
+            dz, dr1 = _act_bwd(act, call.act_param, dy, z, r1, sel, Cs,
+                               act in ("gate", "gdn", "igdn"))
+        g_res0 = dz.t if has0 else None
+        g_res1 = None
+        if has1:
+            if act in ("tanh_half", "masksel"):
+                g_res1 = dy.t
+            elif act in ("gate", "igdn", "gdn") and not call.square:
+                g_res1 = dr1.t
+        g_res2 = dy.t if has2 else None
+        feats = [Feat(t, c) for t, c in zip(srcs, call.src_C)]
+        # the conv's own output-gradient grid
+        if tc.kind == "subpel":
+            f0 = feats[0]
+            G = new_feat(B, f0.H, f0.W, tc.cout, dt, dy.t.device)
+            _lib.call("rgbac_pixel_shuffle", _lib.dtype_code(dt), 1, B, f0.H, f0.W, Cs,
+                      dz.ptr(), dz.ldc, G.ptr(), G.ldc, _lib.stream_ptr(dy.t.device))
+        else:
+            G = dz
+        need = ctx.needs_input_grad
+        # ---- input gradients (one grouped launch over the sources)
+        g_srcs = [None] * len(srcs)
+        preps = []
+        idxs = []
+        for i, f in enumerate(feats):
+            if not need[7 + i]:
+                continue
+            pk = tc.bwd_pack(i, dt, weight.detach().contiguous())
+            o = new_feat(f.B, f.H, f.W, f.C, dt, f.t.device, zero=True)
+            if call.square:
+                preps.append(rt.prepare(pk, [G.src()], out=o, act="sqbwd", res0=dr1,
+                                        res1=f, bias=False))
+            else:
+                preps.append(rt.prepare(pk, [G.src()], out=o, bias=False))
+            idxs.append(i)
+        if preps:
+            outs = rt.launch(preps)
+            for i, o in zip(idxs, outs):
+                g_srcs[i] = o.t
+        # ---- weight / bias gradients
+        g_w = g_b = None
+        if need[1] or (has_b and need[2]):
+            nb = tc.rows if (has_b and tc.kind != "convt") else 0
+            if tc.kind == "convt":
+                # G = the convT input, S = dL/dv on the output grid
+                dw, _ = wgrad(feats[0], [dz], tc.ksize, tc.stride if tc.ksize == 5 else 1,
+                              tc.ksize // 2, False, tc.wg_kpad, tc.wg_map, tc.numel)
+                db = colsum(dz, tc.cout) if has_b else None
+            else:
+                p = tc.ksize // 2
+                dw, db = wgrad(G, feats, tc.ksize, tc.stride, p, call.square, tc.wg_kpad,
+                               tc.wg_map, tc.numel, nbias=nb)
+            g_w = dw.view(weight.shape)
+            g_b = db
+        return (None, g_w, g_b, g_res0, g_res1, g_res2, None, *g_srcs)
+
+
+def conv_t(m, srcs, act="none", act_param=0.0, res0=None, res1=None, res2=None, sel=None,
+           kind=None, weight=None, bias=None, square=False):
+    """Training conv of module ``m`` over Feat sources -> Feat (autograd-tracked)."""
+    import torch.nn as nn
+    dev = srcs[0].t.device
+    segs = [(f.C, f.ldc) for f in srcs]
+    w = m.weight if weight is None else weight
+    b = getattr(m, "bias", None) if bias is None else bias
+    if kind is None:
+        if isinstance(m, nn.ConvTranspose2d):
+            kind = "convt"
+        else:
+            kind = "conv"
+    stride = m.stride[0] if hasattr(m, "stride") else 1
+    if kind == "convt":
+        stride = m.stride[0]
+    wshape = tuple(w.shape) if w.dim() == 4 else (w.shape[0], w.shape[1], 1, 1)
+    tc = train_conv_of(m, kind, wshape, stride, segs, dev)
+    call = ConvCall(tc, [f.C for f in srcs], act, act_param, square)
+    w4 = w if w.dim() == 4 else w.reshape(wshape)
+    out = ConvFn.apply(call, w4, b, None if res0 is None else res0.t,
+                       None if res1 is None else res1.t, None if res2 is None else res2.t,
+                       sel, *[f.t for f in srcs])
+    if kind == "subpel":
+        return Feat(out, tc.cout // 4)
+    return Feat(out, tc.cout)
+
+
+# --------------------------------------------------------------------------
+# window attention core
+# --------------------------------------------------------------------------
+class WinAttnFn(Function):
+    @staticmethod
+    def forward(ctx, spec, qkv_t, table, alpha):
+        C, heads, ws, shift, masked, scale, index = spec
+        B, H, W, ldq = qkv_t.shape
+        dt = qkv_t.dtype
+        dev = qkv_t.device
+        with torch.no_grad():
+            N = ws * ws
+            dense = table.detach()[index.reshape(-1)].reshape(N, N, -1).permute(2, 0, 1)
+            dense = dense.contiguous().float()
+        o = new_feat(B, H, W, C, dt, dev)
+        sel = torch.empty((B, H, W), dtype=torch.uint8, device=dev) if masked else None
+        al = alpha.contiguous().float() if masked else None
+        _lib.call("rgbac_winattn_core", _lib.dtype_code(dt), B, H, W, C, heads, ws, shift,
+                  1 if masked else 0, scale, qkv_t.data_ptr(), ldq, _lib.ptr(al),
+                  dense.data_ptr(), o.ptr(), o.ldc, _lib.ptr(sel), _lib.stream_ptr(dev))
+        ctx.spec = spec
+        ctx.save_for_backward(qkv_t, dense, al, table)
+        if sel is None:
+            sel = torch.empty(0, dtype=torch.uint8, device=dev)
+        ctx.mark_non_differentiable(sel)
+        return o.t, sel
+
+    @staticmethod
+    def backward(ctx, do_t, _dsel):
+        C, heads, ws, shift, masked, scale, index = ctx.spec
+        qkv_t, dense, al, table = ctx.saved_tensors
+        B, H, W, ldq = qkv_t.shape
+        dt = qkv_t.dtype
+        dev = qkv_t.device
+        do_t = do_t.contiguous()
+        dqkv = torch.zeros_like(qkv_t)
+        N = ws * ws
+        groups = -(-(B * (H // ws) * (W // ws)) // (64 // N))
+        nblk = int(min(groups, 64))
+        part = torch.empty(nblk * heads * N * N, dtype=_F32, device=dev)
+        st = _lib.stream_ptr(dev)
+        rt.timed(f"winattn_bwd_kernel<{'f32' if dt == _F32 else 'bf16'},{ws}>",
+                 8.0 * B * H * W * N * C, qkv_t.element_size() * B * H * W * 8 * C,
+                 lambda: _lib.call("rgbac_winattn_core_bwd", _lib.dtype_code(dt), B, H, W, C,
+                                   heads, ws, shift, 1 if masked else 0, scale, qkv_t.data_ptr(),
+                                   ldq, _lib.ptr(al), dense.data_ptr(), do_t.data_ptr(),
+                                   do_t.shape[3], dqkv.data_ptr(), ldq, nblk, part.data_ptr(),
+                                   st))
+        dtab = None
+        if ctx.needs_input_grad[2]:
+            dense_g = torch.empty(heads * N * N, dtype=_F32, device=dev)
+            dtab = torch.empty(table.shape, dtype=_F32, device=dev)
+            _lib.call("rgbac_relpos_bwd", nblk, heads, ws, part.data_ptr(), index.data_ptr(),
+                      dense_g.data_ptr(), dtab.data_ptr(), st)
+        return None, dqkv, dtab, None
+
+
+# --------------------------------------------------------------------------
+# channel concat / layout
+# --------------------------------------------------------------------------
+def _copy(dst, dcoff, src, scoff, C):
+    _lib.call("rgbac_channel_copy", _lib.dtype_code(src.t.dtype), src.B * src.H * src.W, C,
+              src.ptr(), src.ldc, scoff, dst.ptr(), dst.ldc, dcoff, _lib.stream_ptr(src.t.device))
+
+
+class CatFn(Function):
+    @staticmethod
+    def forward(ctx, Cs, *ts):
+        fs = [Feat(t, c) for t, c in zip(ts, Cs)]
+        f0 = fs[0]
+        out = new_feat(f0.B, f0.H, f0.W, sum(Cs), f0.t.dtype, f0.t.device)
+        off = 0
+        for f in fs:
+            _copy(out, off, f, 0, f.C)
+            off += f.C
+        ctx.Cs = Cs
+        ctx.shapes = [t.shape for t in ts]
+        return out.t
+
+    @staticmethod
+    def backward(ctx, g):
+        g = Feat(g.contiguous(), sum(ctx.Cs))
+        outs = []
+        off = 0
+        for c, shp in zip(ctx.Cs, ctx.shapes):
+            o = Feat(torch.zeros(shp, dtype=g.t.dtype, device=g.t.device), c)
+            _copy(o, 0, g, off, c)
+            off += c
+            outs.append(o.t)
+        return (None, *outs)
+
+
+def cat_t(feats):
+    if len(feats) == 1:
+        return feats[0]
+    Cs = [f.C for f in feats]
+    return Feat(CatFn.apply(Cs, *[f.t for f in feats]), sum(Cs))
+
+
+class SliceFn(Function):
+    """Channels [coff, coff + C) of a Feat as a new Feat."""
+
+    @staticmethod
+    def forward(ctx, t, Cin, coff, C):
+        f = Feat(t, Cin)
+        out = new_feat(f.B, f.H, f.W, C, t.dtype, t.device)
+        _copy(out, 0, f, coff, C)
+        ctx.meta = (t.shape, Cin, coff, C)
+        return out.t
+
+    @staticmethod
+    def backward(ctx, g):
+        shp, Cin, coff, C = ctx.meta
+        o = Feat(torch.zeros(shp, dtype=g.dtype, device=g.device), Cin)
+        _copy(o, coff, Feat(g.contiguous(), C), 0, C)
+        return o.t, None, None, None
+
+
+def slice_t(f, coff, C):
+    return Feat(SliceFn.apply(f.t, f.C, coff, C), C)
+
+
+class ToNCHWFn(Function):
+    @staticmethod
+    def forward(ctx, t, C):
+        ctx.meta = (t.shape, t.dtype, C)
+        return rt.to_nchw(Feat(t, C))
+
+    @staticmethod
+    def backward(ctx, g):
+        shp, dt, C = ctx.meta
+        g = g.contiguous().float()
+        B, _, H, W = g.shape
+        out = torch.empty(shp, dtype=dt, device=g.device)
+        _lib.call("rgbac_nchw_to_nhwc", _lib.dtype_code(dt), B, C, H, W, g.data_ptr(),
+                  out.data_ptr(), shp[3], _lib.stream_ptr(g.device))
+        return out, None
+
+
+def to_nchw_t(f):
+    return ToNCHWFn.apply(f.t, f.C)
+
+
+# --------------------------------------------------------------------------
+# entropy models and loss
+# --------------------------------------------------------------------------
+class GaussFn(Function):
+    """One latent slice: (hat = ste_round(y - mu) + mu, sum of clamped bits)."""
+
+    @staticmethod
+    def forward(ctx, y_t, Cy, coff, cs, mu_t, sc_t, noise):
+        y = Feat(y_t, Cy)
+        mu, sc = Feat(mu_t, cs), Feat(sc_t, cs)
+        dev = y_t.device
+        npix = y.B * y.H * y.W
+        hat = new_feat(y.B, y.H, y.W, cs, y_t.dtype, dev)
+        nb = _lib.load().rgbac_reduce_blocks(npix * cs)
+        part = torch.empty(nb, dtype=torch.float64, device=dev)
+        _lib.call("rgbac_gaussian_slice", _lib.dtype_code(y_t.dtype), npix, cs, y.ptr(coff), y.ldc,
+                  mu.ptr(), mu.ldc, sc.ptr(), sc.ldc, _lib.ptr(noise), hat.ptr(), hat.ldc, None,
+                  part.data_ptr(), _lib.stream_ptr(dev))
+        bits = torch.empty(1, dtype=_F32, device=dev)
+        _lib.call("rgbac_sum_partials", 1, nb, part.data_ptr(), bits.data_ptr(),
+                  _lib.stream_ptr(dev))
+        ctx.meta = (Cy, coff, cs)
+        ctx.save_for_backward(y_t, mu_t, sc_t, noise)
+        return hat.t, bits.reshape(())
+
+    @staticmethod
+    def backward(ctx, dhat, dbits):
+        Cy, coff, cs = ctx.meta
+        y_t, mu_t, sc_t, noise = ctx.saved_tensors
+        y = Feat(y_t, Cy)
+        mu, sc = Feat(mu_t, cs), Feat(sc_t, cs)
+        dev = y_t.device
+        npix = y.B * y.H * y.W
+        dy = Feat(torch.zeros_like(y_t), Cy)
+        dmu = Feat(torch.zeros_like(mu_t), cs)
+        dsc = Feat(torch.zeros_like(sc_t), cs)
+        gb = (dbits if dbits is not None else torch.zeros((), device=dev)).float().reshape(1)
+        dh = None if dhat is None else Feat(dhat.contiguous(), cs)
+        _lib.call("rgbac_gaussian_bwd", _lib.dtype_code(y_t.dtype), npix, cs, y.ptr(coff), y.ldc,
+                  mu.ptr(), mu.ldc, sc.ptr(), sc.ldc, _lib.ptr(noise), gb.data_ptr(),
+                  None if dh is None else dh.ptr(), 0 if dh is None else dh.ldc, dy.ptr(coff),
+                  dy.ldc, dmu.ptr(), dmu.ldc, dsc.ptr(), dsc.ldc, _lib.stream_ptr(dev))
+        return dy.t, None, None, None, dmu.t, dsc.t, None
+
+
+def gauss_t(y, coff, mu, sc, noise):
+    """GaussianConditional + ste_round of y[..., coff:coff+cs] -> (hat Feat, bits scalar)."""
+    hat, bits = GaussFn.apply(y.t, y.C, coff, mu.C, mu.t, sc.t, noise)
+    return Feat(hat, mu.C), bits
+
+
+class EBFn(Function):
+    """EntropyBottleneck forward (noise / dequantize) + z_hat STE + bits."""
+
+    @staticmethod
+    def forward(ctx, z_t, C, params, noise):
+        z = Feat(z_t, C)
+        dev = z_t.device
+        npix = z.B * z.H * z.W
+        zh = new_feat(z.B, z.H, z.W, C, z_t.dtype, dev)
+        nb = _lib.load().rgbac_reduce_blocks(npix * C)
+        part = torch.empty(nb, dtype=torch.float64, device=dev)
+        p = params.detach().contiguous()
+        _lib.call("rgbac_eb_forward", _lib.dtype_code(z_t.dtype), npix, C, z.ptr(), z.ldc,
+                  p.data_ptr(), _lib.ptr(noise), zh.ptr(), zh.ldc, None, part.data_ptr(),
+                  _lib.stream_ptr(dev))
+        bits = torch.empty(1, dtype=_F32, device=dev)
+        _lib.call("rgbac_sum_partials", 1, nb, part.data_ptr(), bits.data_ptr(),
+                  _lib.stream_ptr(dev))
+        ctx.C = C
+        ctx.save_for_backward(z_t, p, noise)
+        return zh.t, bits.reshape(())
+
+    @staticmethod
+    def backward(ctx, dzh, dbits):
+        C = ctx.C
+        z_t, p, noise = ctx.saved_tensors
+        z = Feat(z_t, C)
+        dev = z_t.device
+        npix = z.B * z.H * z.W
+        dz = Feat(torch.zeros_like(z_t), C)
+        dp = torch.zeros_like(p)
+        gb = (dbits if dbits is not None else torch.zeros((), device=dev)).float().reshape(1)
+        dh = None if dzh is None else Feat(dzh.contiguous(), C)
+        _lib.call("rgbac_eb_bwd", _lib.dtype_code(z_t.dtype), npix, C, z.ptr(), z.ldc,
+                  p.data_ptr(), _lib.ptr(noise), gb.data_ptr(), None if dh is None else dh.ptr(),
+                  0 if dh is None else dh.ldc, dz.ptr(), dz.ldc, dp.data_ptr(),
+                  _lib.stream_ptr(dev))
+        return dz.t, None, dp, None
+
+
+class MSEFn(Function):
+    """reconstruct_error (mode 0) / plain MSE (mode 1) of NHWC x_hat vs NCHW x."""
+
+    @staticmethod
+    def forward(ctx, xh_t, C, x, mask, mode):
+        xh = Feat(xh_t, C)
+        dev = xh_t.device
+        B, cx, H, W = x.shape
+        scratch = torch.empty(B * 64 * 2, dtype=torch.float64, device=dev)
+        zero = torch.zeros(1, dtype=torch.float64, device=dev)
+        out = torch.empty(4, dtype=_F32, device=dev)
+        _lib.call("rgbac_finalize", _lib.dtype_code(xh_t.dtype), mode, B, cx, H, W, x.data_ptr(),
+                  xh.ptr(), xh.ldc, _lib.ptr(mask), zero.data_ptr(), 1, zero.data_ptr(), 1,
+                  scratch.data_ptr(), out.data_ptr(), _lib.stream_ptr(dev))
+        ctx.meta = (C, mode)
+        ctx.save_for_backward(xh_t, x, mask, scratch)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        C, mode = ctx.meta
+        xh_t, x, mask, scratch = ctx.saved_tensors
+        B, cx, H, W = x.shape
+        dev = xh_t.device
+        dxh = torch.empty_like(xh_t)
+        gm = g.float().reshape(1).contiguous()
+        _lib.call("rgbac_mse_bwd", _lib.dtype_code(xh_t.dtype), mode, B, cx, H, W, x.data_ptr(),
+                  xh_t.data_ptr(), xh_t.shape[3], _lib.ptr(mask), scratch.data_ptr(),
+                  gm.data_ptr(), dxh.data_ptr(), dxh.shape[3], _lib.stream_ptr(dev))
+        return dxh, None, None, None, None

@@ -86,7 +86,7 @@ class EntropyBottleneck(_EntropyModel):
 
     def packed_params_cached(self):
         ps = [getattr(self, n) for n in sorted(self._parameters)]
-        key = tuple((q._version, q.data_ptr()) for q in ps)
+        key = (rt.PARAM_GEN,) + tuple((q._version, q.data_ptr()) for q in ps)
         ent = self.__dict__.get("_rgbac_eb")
         if ent is None or ent[0] != key:
             with torch.no_grad():

@@ -55,7 +55,7 @@ class GDN(nn.Module):
         return beta, gamma
 
     def _pack(self, dtype, C):
-        key = (dtype, self.beta._version, self.gamma._version, self.beta.data_ptr(),
+        key = (dtype, rt.PARAM_GEN, self.beta._version, self.gamma._version, self.beta.data_ptr(),
                self.gamma.data_ptr())
         ent = self.__dict__.get("_rgbac_gdn")
         if ent is None or ent[0] != key:

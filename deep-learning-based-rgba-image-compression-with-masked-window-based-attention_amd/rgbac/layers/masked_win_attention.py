@@ -77,7 +77,7 @@ class WindowAttention(nn.Module):
     def dense_bias(self):
         """[heads][N][N] fp32 relative position bias (:109-111), cached per version."""
         t = self.relative_position_bias_table
-        key = (t._version, t.data_ptr())
+        key = (rt.PARAM_GEN, t._version, t.data_ptr())
         ent = self.__dict__.get("_rgbac_bias")
         if ent is None or ent[0] != key:
             N = self.window_size[0] * self.window_size[1]

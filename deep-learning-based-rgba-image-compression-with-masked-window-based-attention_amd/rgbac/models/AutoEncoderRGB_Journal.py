@@ -7,8 +7,9 @@ Same submodule names / parameter shapes, so reference checkpoints load with
 
 Compute dtype: ``model.compute_dtype`` = torch.float32 (parity mode, fp32
 MFMA) by default; torch.bfloat16 selects the throughput mode (bf16 storage
-and MFMA inputs, fp32 accumulation/epilogues).  Forward only: outputs carry
-no autograd graph in this round.
+and MFMA inputs, fp32 accumulation/epilogues).  With grad enabled (training),
+forward builds an autograd graph whose backward is HIP (rgbac/train_forward.py);
+under torch.no_grad() it runs the fused, grouped inference path.
 """
 import math
 
@@ -145,6 +146,10 @@ class AutoEncoder(_CompressionModelMixin, nn.Module):
         if H % 64 or W % 64:
             raise ValueError("H and W must be multiples of 64 (windows at /4 and /8, "
                              "hyperprior at /64)")
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            # training step (trainRGB.py:178-198): autograd graph over the HIP kernels
+            from ..train_forward import rgb_forward_train
+            return rgb_forward_train(self, input, mask, reconmask, me2, me3, noise_z, noise_y)
         dt = self.compute_dtype
         with torch.no_grad():
             x = input.contiguous().float()

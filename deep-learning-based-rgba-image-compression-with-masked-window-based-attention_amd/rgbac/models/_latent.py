@@ -48,7 +48,7 @@ def _hyper_s_pair(hs, z_hat):
 
 def _musigma_pack(mconv, sconv, dtype, cin):
     """Block-diagonal (mu | sigma) conv from the last cc_mean / cc_scale convs."""
-    key = (dtype, cin) + tuple((p._version, p.data_ptr()) for p in
+    key = (dtype, cin, rt.PARAM_GEN) + tuple((p._version, p.data_ptr()) for p in
                                (mconv.weight, mconv.bias, sconv.weight, sconv.bias))
     ent = mconv.__dict__.get("_rgbac_musigma")
     if ent is None or ent[0] != key:

@@ -25,6 +25,10 @@ from ._lib import ACT, CONV, CONVT_S2, SUBPEL2
 # recorded on the launching stream, together with its algorithmic FLOPs/bytes.
 PROFILER = None
 
+# Bumped by rgbac.optim after every in-place parameter update it makes through raw
+# pointers (no autograd version bump): part of every cached weight-pack key.
+PARAM_GEN = 0
+
 
 class LaunchProfiler:
     def __init__(self):
@@ -294,7 +298,8 @@ class Prepared:
 
 
 def prepare(pk, srcs, out=None, out_coff=0, act="none", act_param=0.0, res0=None, res1=None,
-            res2=None, sel=None, square=False, bias=True, aux0=None, aux1=None, partial=None):
+            res2=None, sel=None, square=False, bias=True, aux0=None, aux1=None, partial=None,
+            zout=None):
     """Build the rgbac_conv_args record of one conv over sources [(Feat, coff, nch), ...].
 
     ``res*`` are Feats on the output grid or (Feat, coff) channel slices."""
@@ -348,6 +353,9 @@ def prepare(pk, srcs, out=None, out_coff=0, act="none", act_param=0.0, res0=None
     a.aux0 = None if aux0 is None else aux0.data_ptr()
     a.aux1 = None if aux1 is None else aux1.data_ptr()
     a.partial = None if partial is None else partial.data_ptr()
+    if zout is not None:
+        assert zout.H == Ho and zout.W == Wo and zout.t.dtype == dtype
+        a.zout, a.zout_ldc = zout.ptr(), zout.ldc
     pr = Prepared()
     pr.a, pr.out, pr.pk = a, out, pk
     taps = 9 if pk.mode == CONVT_S2 else pk.ksize * pk.ksize
@@ -456,7 +464,8 @@ def packed(m, dtype, segs, mode=CONV, transposed=False, weight=None, bias=None):
     w = m.weight if weight is None else weight
     b = getattr(m, "bias", None) if bias is None else bias
     key = (dtype, tuple(segs), mode, transposed)
-    ver = (w._version, w.data_ptr(), None if b is None else (b._version, b.data_ptr()))
+    ver = (PARAM_GEN, w._version, w.data_ptr(),
+           None if b is None else (b._version, b.data_ptr()))
     cache = m.__dict__.setdefault("_rgbac_pack", {})
     ent = cache.get(key)
     if ent is None or ent[0] != ver:

@@ -1,0 +1,185 @@
+"""Autograd-tracked forward of the RGB codec for the training step
+(reference: trainRGB.py:178-198 -> models/AutoEncoderRGB_Journal.py:203-296).
+
+Same arithmetic and op order as the inference path (runtime/_latent), expressed
+with the Functions of ``autograd.py`` so ``rd_loss.backward()`` runs the HIP
+backward kernels.  Differences from the inference path are structural only:
+  * one launch per conv (no grouping), concatenations materialised by
+    rgbac_channel_copy (CatFn) so every conv input is one autograd tensor;
+  * the (mu | sigma) heads are two convs + rgbac_gaussian_slice (no fused
+    GAUSS epilogue), so mu and sigma exist as tensors for their gradients;
+  * ConvTranspose2d(192 -> 3) runs as 4 output phases (CONVT_S2) rather than the
+    inference-only conv3x3 + PixelShuffle form.
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import autograd as ag
+from . import runtime as rt
+from .layers.SupplyMask import mask_pyramid
+from .layers.TransformRGB import _act_of
+from .runtime import Feat
+
+conv_t = ag.conv_t
+
+
+def gdn_t(g, x):
+    """GDN.py:64-94: beta'/gamma' through the reference's LowerBound (torch autograd on
+    the O(C^2) parameters), the norm pool + division as one ConvFn (square input)."""
+    beta, gamma = g.effective_params()
+    C = x.C
+    return conv_t(g, [x], act="igdn" if g.inverse else "gdn", res1=x, kind="gdn",
+                  weight=gamma.reshape(C, C, 1, 1), bias=beta, square=True)
+
+
+def residual_unit_t(u, x):
+    """Masked_Attention.py:150-169."""
+    t = conv_t(u.conv[0], [x], act="gelu")
+    t = conv_t(u.conv[2], [t], act="gelu")
+    return conv_t(u.conv[4], [t], act="gelu", res0=x)
+
+
+def win_attention_t(blk, x, alpha):
+    """masked_win_attention.py:169-251 (or win_attention.py:153-207 when unmasked)."""
+    wa = blk.attn
+    C, ws = wa.dim, wa.window_size[0]
+    masked = type(blk).masked
+    qkv = conv_t(wa.qkv, [x])
+    scale = float(torch.tensor(wa.scale, dtype=torch.float32))
+    spec = (C, wa.num_heads, ws, blk.shift_size, masked, scale, wa.relative_position_index)
+    o_t, sel = ag.WinAttnFn.apply(spec, qkv.t, wa.relative_position_bias_table,
+                                  alpha if masked else None)
+    o = Feat(o_t, C)
+    if masked:
+        return conv_t(wa.proj, [o], act="masksel", res1=x, sel=sel)
+    return conv_t(wa.proj, [o], res0=x)
+
+
+def attention_block_t(blk, x, mask):
+    """Win_noShift_Attention.forward (Masked_Attention.py:182-189)."""
+    b = win_attention_t(blk.attn, x, mask)
+    a = x
+    for k in range(3):
+        a = residual_unit_t(blk.conv_a[k], a)
+        b = residual_unit_t(blk.conv_b[k], b)
+    return conv_t(blk.conv_b[3], [b], act="gate", res1=a, res2=x)
+
+
+def enhancement_t(e, x, post=None):
+    act, slope = _act_of(e.relu)
+    t = conv_t(e.conv1, [x], act=act, act_param=slope)
+    return conv_t(e.conv2, [t], res0=x, res2=post)
+
+
+def dse_t(d, x):
+    first = conv_t(d.input_conv, [x])
+    t = enhancement_t(d.enh1, first)
+    t = enhancement_t(d.enh2, t)
+    t = enhancement_t(d.enh3, t, post=first)
+    return conv_t(d.output_conv, [t], res0=x)
+
+
+def analysis_t(E, x, me2, me3):
+    """TransformRGB.py:65-75."""
+    y = gdn_t(E.gdn1, conv_t(E.x1, [x]))
+    y = gdn_t(E.gdn2, conv_t(E.x2, [y]))
+    y = attention_block_t(E.attention1, y, me2)
+    y = gdn_t(E.gdn3, conv_t(E.x3, [y]))
+    y = conv_t(E.x4, [y])
+    return attention_block_t(E.attention2, y, me3)
+
+
+def synthesis_t(D, y, md2, md3):
+    """TransformRGB.py:90-100."""
+    t = attention_block_t(D.attention1, y, md3)
+    t = gdn_t(D.igdn1, conv_t(D.x1, [t]))
+    t = gdn_t(D.igdn2, conv_t(D.x2, [t]))
+    t = attention_block_t(D.attention2, t, md2)
+    t = gdn_t(D.igdn3, conv_t(D.x3, [t]))
+    t = conv_t(D.x4, [t])
+    return dse_t(D.dse, t)
+
+
+def _seq_t(seq, x):
+    """conv / GELU / ... / conv (the hyper transforms and slice stacks)."""
+    mods = list(seq)
+    t = x
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        act = "none"
+        if i + 1 < len(mods) and isinstance(mods[i + 1], nn.GELU):
+            act = "gelu"
+        if isinstance(m, nn.Sequential):            # compressai subpel_conv3x3
+            assert isinstance(m[1], nn.PixelShuffle) and m[1].upscale_factor == 2
+            t = conv_t(m[0], [t], act=act, kind="subpel")
+        else:
+            t = conv_t(m, [t], act=act)
+        i += 2 if act != "none" else 1
+    return t
+
+
+def eb_params_t(eb):
+    """The [C][64] param block of rgbac_eb_forward with autograd to the raw parameters
+    (softplus / tanh chained by torch on O(C) tensors)."""
+    C = eb.channels
+    parts = [F.softplus(getattr(eb, f"_matrix{i}")).reshape(C, -1) for i in range(5)]
+    parts += [getattr(eb, f"_bias{i}").reshape(C, -1) for i in range(5)]
+    parts += [torch.tanh(getattr(eb, f"_factor{i}")).reshape(C, -1) for i in range(4)]
+    parts.append(eb._get_medians().reshape(C, 1))
+    return F.pad(torch.cat(parts, dim=1), (0, 64 - 59)).contiguous()
+
+
+def latent_t(model, y, training, noise_z=None, noise_y=None):
+    """Hyperprior + 10-slice channel-conditional model (AutoEncoderRGB_Journal.py:222-271)
+    -> (y_hat Feat, sum of y bits, sum of z bits)."""
+    dev = y.t.device
+    ns, msup = model.num_slices, model.max_support_slices
+    cs = y.C // ns
+    z = _seq_t(model.h_a, y)
+    nz = None
+    if training:
+        nz = (noise_z.contiguous().float() if noise_z is not None else
+              torch.rand((z.B, z.H, z.W, z.C), device=dev) - 0.5)
+    zh_t, zbits = ag.EBFn.apply(z.t, z.C, eb_params_t(model.entropy_bottleneck), nz)
+    z_hat = Feat(zh_t, z.C)
+    scales = _seq_t(model.h_scale_s, z_hat)
+    means = _seq_t(model.h_mean_s, z_hat)
+    yh, ybits = [], None
+    for i in range(ns):
+        sup = yh if msup < 0 else yh[:msup]
+        ms = ag.cat_t([means] + sup)
+        ss = ag.cat_t([scales] + sup)
+        mu = _seq_t(model.cc_mean_transforms[i], ms)
+        sc = _seq_t(model.cc_scale_transforms[i], ss)
+        nyi = None
+        if training:
+            nyi = (noise_y[..., i * cs:(i + 1) * cs].contiguous().float() if noise_y is not None
+                   else torch.rand((y.B, y.H, y.W, cs), device=dev) - 0.5)
+        hat, bits = ag.gauss_t(y, i * cs, mu, sc, nyi)
+        lrp = model.lrp_transforms[i]
+        lsup = ag.cat_t([ms, hat])
+        t = conv_t(lrp[0], [lsup], act="gelu")
+        t = conv_t(lrp[2], [t], act="gelu")
+        yh.append(conv_t(lrp[4], [t], act="tanh_half", res1=hat))
+        ybits = bits if ybits is None else ybits + bits
+    return ag.cat_t(yh), ybits, zbits
+
+
+def rgb_forward_train(model, input, mask, reconmask, me2, me3, noise_z=None, noise_y=None):
+    """AutoEncoderRGB_Journal.forward with autograd -> (x_hat, mse, bpp, y_bpp, z_bpp)."""
+    B, _, H, W = input.shape
+    dt = model.compute_dtype
+    x = input.contiguous().float()
+    with torch.no_grad():
+        xf = rt.to_nhwc(x, dt)
+        _, md = mask_pyramid(reconmask, 4, round255=True)                      # :212-215
+    y = analysis_t(model.Encoder, xf, me2, me3)                                 # :217
+    yh, ybits, zbits = latent_t(model, y, model.training, noise_z, noise_y)
+    xh = synthesis_t(model.Decoder, yh, md[1], md[2])                          # :273
+    mse = ag.MSEFn.apply(xh.t, xh.C, x, mask.contiguous().float(), 0)          # :285
+    npix = float(B * H * W)
+    y_bpp = ybits / npix                                                       # :290-295
+    z_bpp = zbits / npix
+    return ag.to_nchw_t(xh), mse, y_bpp + z_bpp, y_bpp, z_bpp

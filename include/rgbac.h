@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define RGBAC_ABI_VERSION 1
+#define RGBAC_ABI_VERSION 2
 
 enum rgbac_status {
   RGBAC_OK = 0,
@@ -57,6 +57,8 @@ enum rgbac_act {
                               slice) -> out = round(y-mu)+mu, aux1 = likelihood,
                               partial[m-block] = sum of clamped bits; aux0 = noise
                               (training) or NULL.  One N tile, ksplit 1.          */
+  RGBAC_ACT_SQBWD = 10,    /* res0 + 2*res1*acc  (GDN input gradient: dL/dx =
+                              dL/dy-direct + 2 x * (gamma'^T dL/dnorm); no bias)  */
 };
 
 enum rgbac_conv_mode {
@@ -102,6 +104,9 @@ typedef struct rgbac_conv_args {
   const float* aux0;           /* GAUSS: fp32 noise [M][cout/2] or NULL            */
   float* aux1;                 /* GAUSS: fp32 likelihood out [M][cout/2] or NULL   */
   double* partial;             /* GAUSS: fp64 bits per M-tile block                */
+  void* zout;                  /* training: pre-activation value v (after bias and
+                                  res0) stored on the output grid, or NULL         */
+  int64_t zout_ldc;            /* channel stride of zout (same coff as out)        */
 } rgbac_conv_args;
 
 int rgbac_abi_version(void);
@@ -200,6 +205,114 @@ int rgbac_nchw_to_nhwc(int dtype, int batch, int c, int h, int w,
                        const float* src, void* dst, int64_t ldc, void* stream);
 int rgbac_nhwc_to_nchw(int dtype, int batch, int c, int h, int w,
                        const void* src, int64_t ldc, float* dst, void* stream);
+
+
+/* ====================================================================== *
+ * Training step (trainRGB.py:178-198): backward kernels, optimizer.       *
+ * The input gradient of a conv is rgbac_conv2d over a repacked weight      *
+ * (transposed + flipped taps; a stride-2 conv's is the CONVT_S2 mode and   *
+ * vice versa); the forward saves its pre-activation through args.zout.    *
+ * ====================================================================== */
+
+/* dL/dv of a fused epilogue y = act(v [, res1]) (v = the saved zout), and
+ * dL/dres1 for the activations res1 enters (GATE, GDN, IGDN); channels
+ * [channels, ldd*) of the outputs are zeroed.  NONE/MASKSEL need no z.
+ * Replaces autograd of nn.GELU/ReLU/LeakyReLU, torch.sigmoid gate
+ * (Masked_Attention.py:189), 0.5*tanh (AutoEncoderRGB_Journal.py:263),
+ * GDN/IGDN (GDN.py:88-94) and the window scatter (masked_win_attention.py:235). */
+int rgbac_act_bwd(int dtype, int act, float act_param, int64_t npix, int channels,
+                  const void* dy, int64_t ldy, const void* z, int64_t ldz, const void* res1,
+                  int64_t ld1, const uint8_t* sel, void* dz, int64_t lddz, void* dres1,
+                  int64_t lddr1, void* stream);
+
+/* Weight gradient of a conv as an MFMA GEMM reducing over pixels:
+ *   D[n][k] = sum_m G[m][n] * Col(S)[m][k],  k = tap * cin_pad + cin,
+ * m over the (batch, grid_h, grid_w) grid of G; S sampled at
+ * (y*stride + ty - pad, x*stride + tx - pad) of the in_h x in_w sources.
+ * Conv layers: G = dL/dv (output grid), S = the forward input.
+ * ConvTranspose layers: G = the forward input, S = dL/dv (k5, s2, p2).
+ * Output: fp32 slabs partial[nsplit][n_pad][k_pad] (+ column sums of G in
+ * bias_partial[nsplit][n_pad] if non-NULL), summed by rgbac_wgrad_reduce.   */
+typedef struct rgbac_wgrad_args {
+  int32_t dtype;
+  int32_t batch, grid_h, grid_w;
+  const void* g; int64_t g_ldc; int32_t g_channels;   /* multiple of 8          */
+  int32_t in_h, in_w, ksize, stride, pad;
+  int32_t nsrc; int32_t cin_pad;
+  rgbac_src src[3];
+  int32_t square_input;        /* S = x^2 (GDN gamma gradient)                 */
+  int32_t n_pad, k_pad;        /* slab dims: multiples of 64                   */
+  int32_t nsplit;              /* pixel splits (deterministic fixed-order sum) */
+  float* partial;
+  float* bias_partial;
+} rgbac_wgrad_args;
+int rgbac_conv_wgrad(const rgbac_wgrad_args* args, void* stream);
+
+/* dw[i] = sum_s partial[s*slab + map[i]] (map[i] < 0 -> 0) in the PyTorch
+ * parameter layout; db[j] = sum_s bias_partial[s*n_pad + j], j < nbias.     */
+int rgbac_wgrad_reduce(int64_t numel, const int32_t* map, const float* partial, int nsplit,
+                       int64_t slab, float* dw, int nbias, const float* bias_partial, int n_pad,
+                       float* db, void* stream);
+
+/* Backward of rgbac_winattn_core: dqkv [B,H,W,>=3C] (dq, dk, dv; zero for
+ * dropped windows) and per-block dense bias gradients bias_partial
+ * [nblk][heads][N][N] (N = ws*ws), reduced by rgbac_relpos_bwd into the
+ * relative_position_bias_table gradient [(2ws-1)^2][heads]
+ * (masked_win_attention.py:96-131 autograd).                               */
+int rgbac_winattn_core_bwd(int dtype, int batch, int h, int w, int channels, int heads, int ws,
+                           int shift, int masked, float scale, const void* qkv, int64_t ldq,
+                           const float* alpha, const float* bias, const void* dout, int64_t ldo,
+                           void* dqkv, int64_t lddq, int nblk, float* bias_partial,
+                           void* stream);
+int rgbac_relpos_bwd(int nblk, int heads, int ws, const float* bias_partial,
+                     const int64_t* index, float* dense, float* dtable, void* stream);
+
+/* GaussianConditional + bits + ste_round backward of one latent slice
+ * (AutoEncoderRGB_Journal.py:255-257,280): gbits = device dL/d(sum bits),
+ * dhat = dL/d y_hat (STE: passes to y), noise = training noise or NULL.     */
+int rgbac_gaussian_bwd(int dtype, int64_t npix, int nch, const void* y, int64_t ldy,
+                       const void* mu, int64_t ldmu, const void* scale, int64_t lds,
+                       const float* noise, const float* gbits, const void* dhat, int64_t lddh,
+                       void* dy, int64_t lddy, void* dmu, int64_t lddmu, void* dscale,
+                       int64_t lddsc, void* stream);
+
+/* EntropyBottleneck likelihood/bits backward (compressai >= 1.2, :225-229):
+ * dz (plus dL/dz_hat through the STE), dparams [C][64] w.r.t. the packed
+ * values of rgbac_eb_forward's block (softplus(M), b, tanh(f), median).     */
+int rgbac_eb_bwd(int dtype, int64_t npix, int channels, const void* z, int64_t ldz,
+                 const float* params, const float* noise, const float* gbits, const void* dzhat,
+                 int64_t lddh, void* dz, int64_t lddz, float* dparams, void* stream);
+
+/* reconstruct_error backward (AutoEncoderRGB_Journal.py:36-64 / mask :309);
+ * scratch = the forward rgbac_finalize's scratch (per-image counts).        */
+int rgbac_mse_bwd(int dtype, int mode, int batch, int cx, int h, int w, const float* x,
+                  const void* x_hat, int64_t ldh, const float* mask, const double* scratch,
+                  const float* gmse, void* dx_hat, int64_t lddx, void* stream);
+
+/* grad = clamp(grad * grad_scale, -clip, clip) (clip <= 0: no clamp; the
+ * result is written back like grad.clamp_) + torch.optim.Adam step over a flat
+ * fp32 parameter buffer (trainRGB.py:190-198).  grad_scale = 1/world after a
+ * data-parallel all-reduce sum.                                             */
+int rgbac_adam_clamp(int64_t n, float* param, float* grad, float* exp_avg, float* exp_avg_sq,
+                     double lr, double beta1, double beta2, double eps, int64_t step,
+                     float clip, float grad_scale, void* stream);
+
+/* PixelShuffle(2) (dir 0) / PixelUnshuffle(2) (dir 1) on NHWC; c = channels
+ * after shuffling.  Channel copy for concatenation / split.                 */
+int rgbac_pixel_shuffle(int dtype, int dir, int batch, int h, int w, int c, const void* in,
+                        int64_t ldi, void* out, int64_t ldo, void* stream);
+int rgbac_channel_copy(int dtype, int64_t npix, int channels, const void* src, int64_t lds,
+                       int scoff, void* dst, int64_t ldd, int dcoff, void* stream);
+
+/* Weight repack through a cached index map: dst[i] = idx[i] >= 0 ? src[idx[i]] : 0
+ * (src = fp32 PyTorch parameter, dst = packed [nphase][cout_pad][k_pad]).   */
+int rgbac_weight_gather(int dtype, int64_t n, const float* src, const int32_t* idx, void* dst,
+                        void* stream);
+/* Per-channel sums over pixels into partial[nsplit][channels] (bias grads). */
+int rgbac_colsum(int dtype, int64_t npix, int channels, const void* x, int64_t ldx, int nsplit,
+                 float* partial, void* stream);
+/* out[r] = (float) sum_j partial[r][j]  (fixed order; bits sums -> loss scalars). */
+int rgbac_sum_partials(int rows, int n, const double* partial, float* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -63,9 +63,25 @@ def ste_round(x):
     return torch.round(x) - x.detach() + x
 
 
+class _LowerBoundFn(torch.autograd.Function):
+    """GDN.py:9-23 (and compressai's LowerBoundFunction, same rule): forward
+    max(x, bound); backward passes the gradient where x >= bound or grad < 0."""
+
+    @staticmethod
+    def forward(ctx, x, bound):
+        b = torch.ones_like(x) * bound
+        ctx.save_for_backward(x, b)
+        return torch.max(x, b)
+
+    @staticmethod
+    def backward(ctx, g):
+        x, b = ctx.saved_tensors
+        return ((x >= b) | (g < 0)).type(g.dtype) * g, None
+
+
 def _lower_bound(x, bound):
-    """GDN.py:9-23 / compressai LowerBound forward: max(x, bound)."""
-    return torch.max(x, torch.ones_like(x) * bound)
+    """GDN.py:9-23 / compressai LowerBound: max(x, bound) with the reference's gradient."""
+    return _LowerBoundFn.apply(x, bound)
 
 
 # --------------------------------------------------------------------------

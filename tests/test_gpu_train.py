@@ -1,0 +1,366 @@
+"""GPU parity of the training path (backward kernels) against autograd of the
+CPU references: plain torch fp32 for single convs, the oracle
+(oracle/ref_model.py, with the reference's LowerBound gradient rule) for GDN,
+attention, entropy models and the whole RGB codec.
+
+Tolerances (relative to the reference gradient's max magnitude unless stated):
+fp32 single ops 1e-4 (exact-f32 MFMA, different summation order); bf16 single
+convs 4e-2; whole-model parameter gradients 2e-2 norm-wise (||g - g_ref|| /
+||g_ref||; 60-layer chains and rare round(y - mu) flips of the STE path).
+"""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from oracle import ref_model as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+
+
+def nrel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _gen(seed):
+    return torch.Generator().manual_seed(seed)
+
+
+def _rt():
+    from rgbac import runtime as rt
+    return rt
+
+
+def _leaf(x, dtype):
+    """fp32 NCHW CPU tensor -> NHWC Feat on the GPU whose tensor is an autograd leaf."""
+    rt = _rt()
+    f = rt.to_nhwc(x.cuda(), dtype)
+    f.t.requires_grad_(True)
+    return f
+
+
+def _nchw_grad(f):
+    rt = _rt()
+    return rt.to_nchw(rt.Feat(f.t.grad, f.C)).cpu()
+
+
+ACTS = [("none", 0.0), ("gelu", 0.0), ("relu", 0.0), ("lrelu", 0.01), ("tanh_half", 0.0),
+        ("gate", 0.0), ("masksel", 0.0)]
+
+
+def _ref_act(act, slope, v, r0, r1, r2, sel):
+    if r0 is not None:
+        v = v + r0
+    if act == "gelu":
+        v = F.gelu(v)
+    elif act == "relu":
+        v = F.relu(v)
+    elif act == "lrelu":
+        v = F.leaky_relu(v, slope)
+    elif act == "tanh_half":
+        v = r1 + 0.5 * torch.tanh(v)
+    elif act == "gate":
+        v = r1 * torch.sigmoid(v)
+    elif act == "masksel":
+        v = torch.where(sel[:, None].bool(), r1 + v, r1)
+    if r2 is not None:
+        v = v + r2
+    return v
+
+
+LAYERS = ["conv3_2src", "conv5s2", "conv3s2", "conv1", "convt5", "convt5_c3", "convt1",
+          "subpel", "linear"]
+
+
+def _make(name, g):
+    if name == "conv3_2src":
+        return nn.Conv2d(40, 24, 3, padding=1), [16, 24], 1
+    if name == "conv5s2":
+        return nn.Conv2d(3, 16, 5, stride=2, padding=2), [3], 2
+    if name == "conv3s2":
+        return nn.Conv2d(24, 16, 3, stride=2, padding=1), [24], 2
+    if name == "conv1":
+        return nn.Conv2d(20, 12, 1), [20], 1
+    if name == "convt5":
+        return nn.ConvTranspose2d(16, 8, 5, stride=2, padding=2, output_padding=1), [16], 0.5
+    if name == "convt5_c3":
+        return nn.ConvTranspose2d(16, 3, 5, stride=2, padding=2, output_padding=1), [16], 0.5
+    if name == "convt1":
+        return nn.ConvTranspose2d(8, 16, 1), [8], 1
+    if name == "subpel":
+        return nn.Sequential(nn.Conv2d(8, 16, 3, padding=1), nn.PixelShuffle(2)), [8], 0.5
+    if name == "linear":
+        return nn.Linear(24, 40), [24], 1
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("act,slope", ACTS)
+@pytest.mark.parametrize("name", LAYERS)
+def test_conv_fn_grads(name, act, slope, dtype):
+    if name in ("subpel",) and act not in ("none", "gelu"):
+        pytest.skip("subpel epilogue supports NONE/GELU")
+    rt = _rt()
+    from rgbac import autograd as ag
+    g = _gen(hash((name, act)) % 1000)
+    m, segs, scale = _make(name, g)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(torch.randn(p.shape, generator=g) * 0.2)
+    B, H, W = 2, 8, 12
+    xs = [torch.randn((B, c, H, W), generator=g, requires_grad=True) for c in segs]
+    x = torch.cat(xs, 1)
+    if name == "linear":
+        v = F.linear(x.permute(0, 2, 3, 1), m.weight, m.bias).permute(0, 3, 1, 2)
+    else:
+        v = m(x)
+    Cout, Ho, Wo = v.shape[1], v.shape[2], v.shape[3]
+    use0 = act in ("none", "gelu", "relu", "lrelu")
+    use1 = act in ("tanh_half", "gate", "masksel")
+    use2 = act in ("none", "gate")
+    if name == "subpel":
+        use0 = use1 = use2 = False
+    r0 = torch.randn((B, Cout, Ho, Wo), generator=g, requires_grad=True) if use0 else None
+    r1 = torch.randn((B, Cout, Ho, Wo), generator=g, requires_grad=True) if use1 else None
+    r2 = torch.randn((B, Cout, Ho, Wo), generator=g, requires_grad=True) if use2 else None
+    sel = (torch.rand((B, Ho, Wo), generator=g) > 0.4).to(torch.uint8) if act == "masksel" else None
+    want = _ref_act(act, slope, v, r0, r1, r2, sel)
+    gy = torch.randn(want.shape, generator=g)
+    want.backward(gy)
+
+    mg = _make(name, g)[0].cuda()
+    mg.load_state_dict(m.state_dict())
+    fx = [_leaf(t.detach(), dtype) for t in xs]
+    fr = [None if r is None else _leaf(r.detach(), dtype) for r in (r0, r1, r2)]
+    kw = dict(act=act, act_param=slope, res0=fr[0], res1=fr[1], res2=fr[2],
+              sel=None if sel is None else sel.cuda())
+    if name == "subpel":
+        out = ag.conv_t(mg[0], fx, kind="subpel", **kw)
+    else:
+        out = ag.conv_t(mg, fx, **kw)
+    got = rt.to_nchw(rt.Feat(out.t.detach(), out.C)).cpu()
+    # fp32: max-abs relative; bf16: norm-wise (a ReLU/LeakyReLU kink flips where the
+    # bf16 pre-activation and the fp32 reference straddle 0 -- O(1) per flipped element)
+    tol, err = (1e-4, rel) if dtype == torch.float32 else (3e-2, nrel)
+    assert got.shape == want.shape
+    assert err(got, want) < tol
+    out.t.backward(rt.to_nhwc(gy.cuda(), dtype).t)
+    for f, t in zip(fx, xs):
+        assert err(_nchw_grad(f), t.grad) < tol
+    for f, r in zip(fr, (r0, r1, r2)):
+        if r is not None:
+            assert err(_nchw_grad(f), r.grad) < tol
+    pg = dict(mg.named_parameters())
+    for k, p in m.named_parameters():
+        assert err(pg[k].grad, p.grad) < tol, k
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("inverse", [False, True])
+def test_gdn_grads(inverse, dtype):
+    from rgbac.layers.GDN import GDN
+    from rgbac.train_forward import gdn_t
+    g = _gen(21 + inverse)
+    m = GDN(32, inverse=inverse)
+    with torch.no_grad():
+        m.gamma.add_(0.05 * torch.rand(m.gamma.shape, generator=g))
+        m.beta.add_(0.1 * torch.rand(m.beta.shape, generator=g))
+        m.beta[:3] = 1e-4                  # below beta_bound: LowerBound gradient rule
+    x = torch.randn((2, 32, 8, 8), generator=g, requires_grad=True)
+    sd = {"m." + k: v.detach().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    want = ref.gdn(x, sd, "m", inverse)
+    gy = torch.randn(want.shape, generator=g)
+    want.backward(gy)
+    mg = GDN(32, inverse=inverse).cuda()
+    mg.load_state_dict(m.state_dict())
+    fx = _leaf(x.detach(), dtype)
+    out = gdn_t(mg, fx)
+    rt = _rt()
+    tol = 1e-4 if dtype == torch.float32 else 4e-2
+    assert rel(rt.to_nchw(rt.Feat(out.t.detach(), 32)).cpu(), want) < tol
+    out.t.backward(rt.to_nhwc(gy.cuda(), dtype).t)
+    assert rel(_nchw_grad(fx), x.grad) < tol
+    assert rel(mg.beta.grad, sd["m.beta"].grad) < tol
+    assert rel(mg.gamma.grad, sd["m.gamma"].grad) < tol
+
+
+def _alpha(kind, B, H, W, g):
+    a = torch.ones((B, 1, H, W))
+    if kind == "zero":
+        a.zero_()
+    elif kind == "half":
+        a[..., :, : W // 2] = 0
+    elif kind == "rand":
+        a = (torch.rand((B, 1, H, W), generator=g) > 0.97).float()
+    return a
+
+
+@pytest.mark.parametrize("dim,ws,H", [(192, 8, 16), (80, 4, 16)])
+@pytest.mark.parametrize("kind", ["ones", "half", "rand", "zero"])
+def test_attention_block_grads(dim, ws, H, kind):
+    """Win_noShift_Attention (Masked_Attention.py:182-189) incl. the masked window
+    attention core backward and the relative-position-bias table gradient."""
+    from rgbac.layers.Masked_Attention import Win_noShift_Attention
+    from rgbac.train_forward import attention_block_t
+    g = _gen(dim + ws + len(kind))
+    m = Win_noShift_Attention(dim=dim, num_heads=8, window_size=ws, shift_size=ws // 2)
+    with torch.no_grad():
+        m.attn.attn.relative_position_bias_table.normal_(0, 0.5, generator=g)
+    W = H + 2 * ws
+    x = torch.randn((2, dim, H, W), generator=g, requires_grad=True)
+    a = _alpha(kind, 2, H, W, g)
+    sd = {"blk." + k: v.detach().clone().requires_grad_(v.is_floating_point())
+          for k, v in m.state_dict().items()}
+    want = ref.win_noshift_attention(x, a, sd, "blk", ws, ws // 2)
+    gy = torch.randn(want.shape, generator=g)
+    want.backward(gy)
+    mg = Win_noShift_Attention(dim=dim, num_heads=8, window_size=ws, shift_size=ws // 2).cuda()
+    mg.load_state_dict(m.state_dict())
+    fx = _leaf(x.detach(), torch.float32)
+    out = attention_block_t(mg, fx, a.cuda())
+    rt = _rt()
+    assert rel(rt.to_nchw(rt.Feat(out.t.detach(), dim)).cpu(), want) < 2e-4
+    out.t.backward(rt.to_nhwc(gy.cuda(), torch.float32).t)
+    assert rel(_nchw_grad(fx), x.grad) < 5e-4
+    pg = dict(mg.named_parameters())
+    for k, p in pg.items():
+        r = sd["blk." + k].grad
+        if r is None or r.abs().max() == 0:
+            assert p.grad is None or p.grad.abs().max() < 1e-6, k
+            continue
+        assert nrel(p.grad, r) < 1e-3, k
+
+
+def test_gaussian_slice_grads():
+    from rgbac import autograd as ag
+    rt = _rt()
+    g = _gen(31)
+    B, H, W, M, cs = 2, 8, 8, 16, 8
+    y = torch.randn((B, M, H, W), generator=g, requires_grad=True)
+    mu = (torch.randn((B, cs, H, W), generator=g) * 0.5).requires_grad_(True)
+    sc = (torch.rand((B, cs, H, W), generator=g) * 2).requires_grad_(True)   # some < 0.11
+    noise = torch.rand((B, cs, H, W), generator=g) - 0.5
+    a = torch.randn((B, cs, H, W), generator=g)
+    ysl = y[:, cs:2 * cs]
+    _, lik = ref.gc_forward(ysl, sc, mu, True, noise)
+    hat = ref.ste_round(ysl - mu) + mu
+    loss = ref._bits(lik) * 0.01 + (hat * a).sum()
+    loss.backward()
+    fy = _leaf(y.detach(), torch.float32)
+    fmu, fsc = _leaf(mu.detach(), torch.float32), _leaf(sc.detach(), torch.float32)
+    nz = noise.permute(0, 2, 3, 1).contiguous().cuda()
+    h, bits = ag.gauss_t(fy, cs, fmu, fsc, nz)
+    assert abs(bits.item() - ref._bits(lik).item()) < 1e-4 * ref._bits(lik).item()
+    ga = rt.to_nhwc(a.cuda(), torch.float32)
+    l2 = bits * 0.01 + (h.t * ga.t).sum()
+    l2.backward()
+    assert rel(_nchw_grad(fy), y.grad) < 1e-4
+    assert rel(_nchw_grad(fmu), mu.grad) < 1e-4
+    assert rel(_nchw_grad(fsc), sc.grad) < 1e-4
+
+
+def test_entropy_bottleneck_grads():
+    from rgbac import autograd as ag
+    from rgbac.entropy import EntropyBottleneck
+    from rgbac.train_forward import eb_params_t
+    rt = _rt()
+    g = _gen(41)
+    C = 16
+    eb = EntropyBottleneck(C)
+    with torch.no_grad():
+        for n, p in eb.named_parameters():
+            if n.startswith("_factor"):
+                p.copy_(torch.randn(p.shape, generator=g) * 0.3)
+            elif n.startswith("_matrix"):
+                p.add_(torch.randn(p.shape, generator=g) * 0.3)
+    z = (torch.randn((2, C, 4, 4), generator=g) * 3).requires_grad_(True)
+    noise = torch.rand((2, C, 4, 4), generator=g) - 0.5
+    a = torch.randn((2, C, 4, 4), generator=g)
+    sd = {"eb." + k: v.detach().clone().requires_grad_(v.is_floating_point())
+          for k, v in eb.state_dict().items()}
+    _, lik = ref.eb_forward(z, sd, "eb", True, noise)
+    med = ref.eb_medians(sd, "eb")
+    zh = ref.ste_round(z - med.reshape(1, C, 1, 1)) + med.reshape(1, C, 1, 1)
+    loss = ref._bits(lik) * 0.01 + (zh * a).sum()
+    loss.backward()
+    ebg = EntropyBottleneck(C).cuda()
+    ebg.load_state_dict(eb.state_dict())
+    fz = _leaf(z.detach(), torch.float32)
+    nz = noise.permute(0, 2, 3, 1).contiguous().cuda()
+    zh_t, bits = ag.EBFn.apply(fz.t, C, eb_params_t(ebg), nz)
+    assert abs(bits.item() - ref._bits(lik).item()) < 1e-4 * ref._bits(lik).item()
+    ga = rt.to_nhwc(a.cuda(), torch.float32)
+    (bits * 0.01 + (zh_t * ga.t).sum()).backward()
+    assert rel(_nchw_grad(fz), z.grad) < 1e-4
+    for n, p in ebg.named_parameters():
+        r = sd["eb." + n].grad
+        if n == "quantiles":
+            assert p.grad is None or p.grad.abs().max() < 1e-6
+            continue
+        assert rel(p.grad, r) < 2e-4, n
+
+
+def test_adam_clamp_matches_torch():
+    from rgbac.optim import AdamClamp
+    g = _gen(51)
+    ps = [torch.randn(s, generator=g).cuda().requires_grad_(True) for s in ((7, 5), (13,), (3, 3, 2))]
+    qs = [p.detach().clone().requires_grad_(True) for p in ps]
+    opt = AdamClamp(ps, lr=1e-3, clip=0.5)
+    topt = torch.optim.Adam(qs, lr=1e-3)
+    for step in range(3):
+        grads = [torch.randn(p.shape, generator=g).cuda() * 2 for p in ps]
+        opt.zero_grad()
+        topt.zero_grad()
+        for p, q, gr in zip(ps, qs, grads):
+            (p * gr).sum().backward()
+            (q * gr).sum().backward()
+            q.grad.clamp_(-0.5, 0.5)
+        opt.step()
+        topt.step()
+    for p, q in zip(ps, qs):
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32])
+def test_rgb_train_step_grads(dtype):
+    """rd_loss = 4096*mse + bpp (trainRGB.py:178-186) backward: every parameter gradient
+    of the HIP path against the oracle's autograd, same noise, B=2, 64x64, fp32."""
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    torch.manual_seed(234)
+    net = AutoEncoder().train()
+    g = _gen(61)
+    B, H, W = 2, 64, 64
+    x = (torch.randint(0, 256, (B, 3, H, W), generator=g).float() / 255)
+    a = torch.ones((B, 1, H, W))
+    a[1, :, :, : W // 2] = 0
+    me = ref.supply_mask(a)
+    nz = torch.rand((B, 192, 1, 1), generator=g) - 0.5
+    ny = torch.rand((B, 80, 8, 8), generator=g) - 0.5
+    sd = {k: v.detach().clone().requires_grad_(v.is_floating_point())
+          for k, v in net.state_dict().items()}
+    out = ref.rgb_forward(sd, x * (a > 0), a, a, *me[:4], training=True, noise_z=nz, noise_y=ny)
+    (4096 * out[1] + out[2]).backward()
+    netg = AutoEncoder().cuda().train()
+    netg.load_state_dict(net.state_dict())
+    xg = (x * (a > 0)).cuda()
+    ag_ = a.cuda()
+    meg = [t.cuda() for t in me]
+    o = netg(xg, ag_, ag_, *meg[:4], noise_z=nz.permute(0, 2, 3, 1).cuda(),
+             noise_y=ny.permute(0, 2, 3, 1).cuda())
+    assert abs(o[1].item() - out[1].item()) < 1e-3 * out[1].item()
+    assert abs(o[2].item() - out[2].item()) < 1e-3 * out[2].item()
+    (4096 * o[1] + o[2]).backward()
+    bad = []
+    for n, p in netg.named_parameters():
+        r = sd[n].grad
+        if r is None or r.abs().max() == 0:
+            continue
+        e = nrel(p.grad, r)
+        if e > 2e-2:
+            bad.append((n, e))
+    assert not bad, bad[:10]

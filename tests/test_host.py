@@ -30,7 +30,7 @@ def test_library_exports_every_header_symbol():
     for n in names:
         assert hasattr(lib, n), n
     assert set(names) == set(_lib.SIGNATURES), set(names) ^ set(_lib.SIGNATURES)
-    assert lib.rgbac_abi_version() == 1
+    assert lib.rgbac_abi_version() == 2
     from rgbac import runtime as rt
     assert lib.rgbac_conv_num_tiles() == len(rt.TILES)
     assert lib.rgbac_conv_max_groups() == 10
@@ -46,23 +46,26 @@ def test_argument_errors_are_reported_without_launching():
                   None, 16, None, None)
 
 
-def test_conv_args_struct_layout_matches_c(tmp_path):
+@pytest.mark.parametrize("pyname,cname", [("ConvArgs", "rgbac_conv_args"),
+                                           ("WgradArgs", "rgbac_wgrad_args")])
+def test_args_struct_layout_matches_c(tmp_path, pyname, cname):
     """Compile a probe against include/rgbac.h with gcc and compare offsets with ctypes."""
     from rgbac import _lib
-    fields = [f for f, _ in _lib.ConvArgs._fields_]
+    cls = getattr(_lib, pyname)
+    fields = [f for f, _ in cls._fields_]
     src = tmp_path / "probe.c"
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"',
-             'int main(void){', 'printf("%zu\\n", sizeof(rgbac_conv_args));']
-    lines += [f'printf("%zu\\n", offsetof(rgbac_conv_args, {f}));' for f in fields]
+             'int main(void){', f'printf("%zu\\n", sizeof({cname}));']
+    lines += [f'printf("%zu\\n", offsetof({cname}, {f}));' for f in fields]
     lines += ['printf("%zu\\n", sizeof(rgbac_src)); return 0;}']
     src.write_text("\n".join(lines))
     exe = tmp_path / "probe"
     subprocess.run(["gcc", "-O0", str(src), "-o", str(exe)], check=True)
     vals = [int(v) for v in subprocess.run([str(exe)], check=True, capture_output=True,
                                            text=True).stdout.split()]
-    assert vals[0] == ctypes.sizeof(_lib.ConvArgs)
+    assert vals[0] == ctypes.sizeof(cls)
     for f, off in zip(fields, vals[1:-1]):
-        assert getattr(_lib.ConvArgs, f).offset == off, f
+        assert getattr(cls, f).offset == off, f
     assert vals[-1] == ctypes.sizeof(_lib.Src)
 
 
