@@ -28,6 +28,7 @@ for _p in (ROOT, PKG):
         sys.path.insert(0, _p)
 
 METRIC = "MPixels/sec encode+decode, 256×256 RGBA batch; bpp & PSNR parity vs reference"
+TRAIN_METRIC = "MPixels/sec training step (fwd+bwd+clamp+Adam), 256×256 RGBA batch"
 PEAK = {"bf16": {"mfma": 2500.0, "hbm": 8000.0}, "f32": {"mfma": 157.3, "hbm": 8000.0}}
 
 
@@ -75,6 +76,143 @@ def cpu_baseline(budget_s):
                       f"{n} timed iterations after 1 warm-up, {dt:.1f} s"}
 
 
+def cpu_baseline_train(budget_s):
+    """Oracle training step (fp32 autograd on CPU: forward + backward of
+    4096*mse + bpp) on 1 image of the same workload, this host's cores."""
+    from oracle import ref_model as ref
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    torch.manual_seed(234)
+    sd = {k: v.detach().cpu().clone().requires_grad_(v.is_floating_point())
+          for k, v in AutoEncoder().train().state_dict().items()}
+    x, a = synth_inputs(2, 256, 256, seed=0)
+    x, a = x[1:2], a[1:2]
+    me = ref.supply_mask(a)
+    g = torch.Generator().manual_seed(1)
+
+    def one():
+        nz = torch.rand((1, 192, 4, 4), generator=g) - 0.5
+        ny = torch.rand((1, 80, 32, 32), generator=g) - 0.5
+        out = ref.rgb_forward(sd, x, a, a, *me[:4], training=True, noise_z=nz, noise_y=ny)
+        (4096 * out[1] + out[2]).backward()
+    one()
+    n, t0 = 0, time.perf_counter()
+    while True:
+        one()
+        n += 1
+        if time.perf_counter() - t0 >= budget_s or n >= 10:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n * 256 * 256 / dt / 1e6, 4), "unit": "MPix/s",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle rgb_forward(training) + autograd backward fp32, 1 image 256x256 "
+                      f"(half-transparent alpha), {n} timed iterations after 1 warm-up, {dt:.1f} s"}
+
+
+def roofline_of(summ, dtype, nrep):
+    total_ms = sum(d["ms"] for d in summ.values())
+    dom_name, dom = max(summ.items(), key=lambda kv: kv[1]["ms"])
+    per_ms = dom["ms"] / dom["launches"]
+    per_fl = dom["flops"] / dom["launches"]
+    achieved = per_fl / (per_ms * 1e-3) / 1e12
+    peak = PEAK[dtype]["mfma"]
+    return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+            "frac": round(achieved / peak, 4), "traffic": None, "kernel": dom_name,
+            "avg_launch_us": round(per_ms * 1e3, 2),
+            "algorithmic_gflop_per_launch": round(per_fl / 1e9, 4),
+            "share_of_step": round(dom["ms"] / total_ms, 3)}, total_ms
+
+
+def write_layers(prof, path, nrep):
+    lay = prof.layers()
+    tot = sum(v[1] for v in lay.values())
+    with open(path, "w") as fh:
+        for k, v in sorted(lay.items(), key=lambda kv: -kv[1][1]):
+            fh.write(f"{v[1] / nrep:9.4f} ms {100 * v[1] / tot:5.1f}% n={v[0] // nrep:3d} "
+                     f"{v[2] / max(v[1], 1e-9) / 1e9:8.1f} TF/s  "
+                     f"{v[3] / max(v[1], 1e-9) / 1e6:7.0f} GB/s  {k}\n")
+
+
+def main_train(args, world, rank, dev, dist):
+    """BASELINE config 3 (1 GPU, batch 16) / config 5 (torchrun, 16 per GPU, RCCL)."""
+    from rgbac import runtime as rt
+    from rgbac.layers.SupplyMask import mask_pyramid
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    from rgbac.optim import AdamClamp
+    from rgbac.parallel import DataParallelTrainer
+
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    torch.manual_seed(234)
+    net = AutoEncoder().train().to(dev).set_compute_dtype(dt)
+    opt = AdamClamp(net.parameters(), lr=1e-4, clip=5.0)
+    trainer = DataParallelTrainer(net, opt)
+    B, S = args.batch, args.size
+    x, a = synth_inputs(B, S, S, seed=rank)
+    x, a = x.to(dev), a.to(dev)
+    _, me = mask_pyramid(a, 4)
+
+    def step():
+        out = net(x, a, a, *me)
+        trainer.step(4096.0 * out[1] + out[2])        # trainRGB.py:183-198 (lambda 4096)
+        return out
+
+    step()
+    torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    ms = elapsed / args.steps * 1e3
+    value = world * B * S * S * args.steps / elapsed / 1e6
+    if rank == 0:
+        prof = rt.LaunchProfiler()
+        rt.PROFILER = prof
+        for _ in range(2):
+            step()
+        rt.PROFILER = None
+        summ = prof.summary()
+        if args.layers:
+            write_layers(prof, args.layers, 2)
+        roof, total_ms = roofline_of(summ, args.dtype, 2)
+        rec = {"metric": TRAIN_METRIC, "value": round(value, 2), "unit": "MPix/s",
+               "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": args.dtype,
+               "data": "synthetic (seeded RGB k/255 + 4 alpha patterns; random-init weights, "
+                       "torch seed 234)",
+               "config": {"workload": "trainRGB.py step: AutoEncoderRGB_Journal forward + "
+                                      "backward of 4096*mse+bpp + clamp(+-5) + Adam "
+                                      f"(BASELINE config {3 if world == 1 else 5}), {S}x{S} RGBA",
+                          "global_batch": B * world, "per_gpu_batch": B, "height": S,
+                          "width": S, "parallelism": f"dp{world}",
+                          "loss": round(4096.0 * out[1].item() + out[2].item(), 4)},
+               "roofline": roof}
+        if args.kernels:
+            rec["kernels"] = {k: {"launches": v["launches"] // 2, "ms": round(v["ms"] / 2, 4),
+                                  "share": round(v["ms"] / total_ms, 4),
+                                  "tflops": round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 2)}
+                              for k, v in sorted(summ.items(), key=lambda kv: -kv[1]["ms"])}
+        rec["cpu_baseline"] = None
+        if world == 1 and not args.no_cpu_baseline:
+            rec["cpu_baseline"] = cpu_baseline_train(args.cpu_seconds)
+        print(json.dumps(rec), flush=True)
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -88,7 +226,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--kernels", action="store_true", help="add the per-kernel time table")
     ap.add_argument("--layers", default=None, help="write a per-layer time table to this file")
+    ap.add_argument("--train", action="store_true",
+                    help="time the training step (BASELINE config 3 / 5) instead of the forward")
     args = ap.parse_args()
+    if args.train and args.batch == 8 and "--batch" not in sys.argv:
+        args.batch = 16
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -100,6 +242,9 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
+
+    if args.train:
+        return main_train(args, world, rank, dev, dist)
 
     from rgbac import runtime as rt
     from rgbac.layers.SupplyMask import mask_pyramid
@@ -114,7 +259,8 @@ def main():
     _, me = mask_pyramid(a, 4)
 
     def step():
-        return net(x, a, a, *me)
+        with torch.no_grad():                          # inference: the fused, grouped path
+            return net(x, a, a, *me)
 
     out = step()                                       # packs weights, warms caches
     torch.cuda.synchronize()

@@ -146,7 +146,8 @@ class AutoEncoder(_CompressionModelMixin, nn.Module):
         if H % 64 or W % 64:
             raise ValueError("H and W must be multiples of 64 (windows at /4 and /8, "
                              "hyperprior at /64)")
-        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+        if debug is None and torch.is_grad_enabled() and \
+                any(p.requires_grad for p in self.parameters()):
             # training step (trainRGB.py:178-198): autograd graph over the HIP kernels
             from ..train_forward import rgb_forward_train
             return rgb_forward_train(self, input, mask, reconmask, me2, me3, noise_z, noise_y)

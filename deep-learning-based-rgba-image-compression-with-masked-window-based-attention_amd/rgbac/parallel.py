@@ -1,0 +1,103 @@
+"""Data-parallel training (trainRGB.py:178-198 across ranks).
+
+One process per GPU (torchrun); every rank runs the full model on its shard of
+the global batch.  The only exchange is the gradient all-reduce: the flat fp32
+gradient buffer of rgbac.optim.AdamClamp is cut into ~25 MB buckets in REVERSE
+parameter order (the order backward produces them), and each bucket's
+all-reduce (backend "nccl" = RCCL over xGMI) is launched from the parameters'
+post-accumulate-grad hooks as soon as its last gradient lands -- overlapped with
+the rest of backward on RCCL's own stream.  ``finish()`` waits for all buckets
+and hands the 1/world mean to the optimizer kernel, which applies it before the
+per-element clamp (the reference clamps the global-batch gradient).
+"""
+import torch
+import torch.distributed as dist
+
+
+class GradBuckets:
+    def __init__(self, params, flat_grad, bucket_bytes=25 << 20, group=None):
+        self.params = list(params)
+        self.flat = flat_grad
+        self.group = group
+        self.world = dist.get_world_size(group)
+        # param i occupies [off_i, off_i + n_i) of the flat buffer (AdamClamp layout)
+        offs, off = [], 0
+        for p in self.params:
+            offs.append((off, p.numel()))
+            off += p.numel()
+        assert off == flat_grad.numel()
+        per = max(1, bucket_bytes // flat_grad.element_size())
+        self.buckets = []                  # [lo, hi, [param idx]]
+        cur, hi = [], off
+        for i in range(len(self.params) - 1, -1, -1):
+            cur.append(i)
+            lo = offs[i][0]
+            if hi - lo >= per or i == 0:
+                self.buckets.append([lo, hi, cur])
+                cur, hi = [], lo
+        self.owner = {}
+        for b, (_, _, idx) in enumerate(self.buckets):
+            for i in idx:
+                self.owner[i] = b
+        self.pending = [0] * len(self.buckets)
+        self.works = [None] * len(self.buckets)
+        self.active = False
+        self.hooks = [p.register_post_accumulate_grad_hook(self._hook(i))
+                      for i, p in enumerate(self.params)]
+
+    def _hook(self, i):
+        def fn(_p):
+            if not self.active:
+                return
+            b = self.owner[i]
+            self.pending[b] -= 1
+            if self.pending[b] == 0:
+                self._launch(b)
+        return fn
+
+    def _launch(self, b):
+        lo, hi, _ = self.buckets[b]
+        self.works[b] = dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM,
+                                        group=self.group, async_op=True)
+
+    def begin(self):
+        """Call before loss.backward()."""
+        for b, (_, _, idx) in enumerate(self.buckets):
+            self.pending[b] = len(idx)
+            self.works[b] = None
+        self.active = True
+
+    def finish(self):
+        """Call after loss.backward(): all-reduce what backward did not launch (parameters
+        without a gradient this step), wait for every bucket; returns 1/world."""
+        self.active = False
+        for b in range(len(self.buckets)):
+            if self.works[b] is None:
+                self._launch(b)
+        for w in self.works:
+            w.wait()
+        return 1.0 / self.world
+
+    def remove(self):
+        for h in self.hooks:
+            h.remove()
+
+
+class DataParallelTrainer:
+    """net + AdamClamp + GradBuckets: ``step(loss)`` = backward with overlapped all-reduce,
+    clamp, Adam (one launch)."""
+
+    def __init__(self, net, optimizer, bucket_bytes=25 << 20):
+        self.net, self.opt = net, optimizer
+        self.buckets = None
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            self.buckets = GradBuckets(optimizer.params, optimizer.flat_grad, bucket_bytes)
+
+    def step(self, loss):
+        self.opt.zero_grad()
+        if self.buckets is not None:
+            self.buckets.begin()
+        loss.backward()
+        if self.buckets is not None:
+            self.opt.grad_scale = self.buckets.finish()
+        self.opt.step()

@@ -92,6 +92,8 @@ DIRECT_STEPS = 12
 DIRECT_LDS = 65536       # weight panel bytes of a direct tile (dynamic LDS limit)
 KSPLITS = (1, 2, 4, 8)
 TUNE = os.environ.get("RGBAC_TUNE", "1") != "0"
+# RGBAC_TILE_SET: "all" (default) | "stream" (streaming K-ring tiles only, for A/B runs)
+TILE_SET = os.environ.get("RGBAC_TILE_SET", "all")
 _tune_cache = {}          # shape key -> (tile, ksplit)
 FORCE = None              # (tile, ksplit) override, used by the tile/split-K tests
 
@@ -107,6 +109,8 @@ def _candidates(M, cout, nst, nks=None, plain=True):
     out = []
     n16 = round_up(cout, 16)
     for t, (bm, bn) in enumerate(TILES):
+        if TILE_SET == "stream" and t >= FIRST_WRES:
+            continue
         if t >= FIRST_DIRECT:
             if plain and nks is not None and nks <= DIRECT_STEPS and bn >= n16 / 4 \
                     and bn < 2 * n16 + 16 and bn * (4 * nks + 1) * 16 <= DIRECT_LDS:

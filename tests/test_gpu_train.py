@@ -8,6 +8,8 @@ fp32 single ops 1e-4 (exact-f32 MFMA, different summation order); bf16 single
 convs 4e-2; whole-model parameter gradients 2e-2 norm-wise (||g - g_ref|| /
 ||g_ref||; 60-layer chains and rare round(y - mu) flips of the STE path).
 """
+import zlib
+
 import pytest
 import torch
 import torch.nn as nn
@@ -107,13 +109,16 @@ def test_conv_fn_grads(name, act, slope, dtype):
         pytest.skip("subpel epilogue supports NONE/GELU")
     rt = _rt()
     from rgbac import autograd as ag
-    g = _gen(hash((name, act)) % 1000)
+    g = _gen(zlib.crc32(f"{name}/{act}".encode()) % 100000)
     m, segs, scale = _make(name, g)
+    # bf16 mode: the reference sees the same bf16-representable inputs and weights the
+    # kernels see (fp32 math on them), so ReLU kinks are decided on equal pre-activations
+    rnd = (lambda t: t.to(torch.bfloat16).float()) if dtype == torch.bfloat16 else (lambda t: t)
     with torch.no_grad():
         for p in m.parameters():
-            p.copy_(torch.randn(p.shape, generator=g) * 0.2)
+            p.copy_(rnd(torch.randn(p.shape, generator=g) * 0.2))
     B, H, W = 2, 8, 12
-    xs = [torch.randn((B, c, H, W), generator=g, requires_grad=True) for c in segs]
+    xs = [rnd(torch.randn((B, c, H, W), generator=g)).requires_grad_(True) for c in segs]
     x = torch.cat(xs, 1)
     if name == "linear":
         v = F.linear(x.permute(0, 2, 3, 1), m.weight, m.bias).permute(0, 3, 1, 2)
@@ -125,9 +130,9 @@ def test_conv_fn_grads(name, act, slope, dtype):
     use2 = act in ("none", "gate")
     if name == "subpel":
         use0 = use1 = use2 = False
-    r0 = torch.randn((B, Cout, Ho, Wo), generator=g, requires_grad=True) if use0 else None
-    r1 = torch.randn((B, Cout, Ho, Wo), generator=g, requires_grad=True) if use1 else None
-    r2 = torch.randn((B, Cout, Ho, Wo), generator=g, requires_grad=True) if use2 else None
+    def leaf(on):
+        return rnd(torch.randn((B, Cout, Ho, Wo), generator=g)).requires_grad_(True) if on else None
+    r0, r1, r2 = leaf(use0), leaf(use1), leaf(use2)
     sel = (torch.rand((B, Ho, Wo), generator=g) > 0.4).to(torch.uint8) if act == "masksel" else None
     want = _ref_act(act, slope, v, r0, r1, r2, sel)
     gy = torch.randn(want.shape, generator=g)
