@@ -126,10 +126,10 @@ __device__ __forceinline__ void load_res(const void* ptr, long long ld, long lon
 template <typename T>
 __device__ __forceinline__ void epilogue4(const ConvShared& s, const ConvGroup& g, int ph, int m,
                                           int n, float (&v)[4]) {
-  const int mx = m % s.Wm;
-  const int t = m / s.Wm;
-  const int my = t % s.Hm;
-  const int b = t / s.Hm;
+  const int t = udiv(m, s.Wm, s.rWm);
+  const int mx = m - t * s.Wm;
+  const int b = udiv(t, s.Hm, s.rHm);
+  const int my = t - b * s.Hm;
 #pragma unroll
   for (int r = 0; r < 4; ++r) v[r] += (g.bias ? g.bias[n + r] : 0.0f);
   T* out = reinterpret_cast<T*>(g.out);
@@ -572,12 +572,14 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
       }
       continue;
     }
-    float v[TN][4];
+    // per 16x16 tile (a row-batched epilogue holding every residual of the row
+    // costs ~50 VGPRs and one wave/SIMD of occupancy in the K loop: measured slower)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[j][r] = acc[j][i][r];
-    epilogue_row<T, TN>(s, g, phase, m, nn, v);
+    for (int j = 0; j < TN; ++j) {
+      if (nn[j] >= g.cout) continue;
+      float v[4] = {acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]};
+      epilogue4<T>(s, g, phase, m, nn[j], v);
+    }
   }
 }
 

@@ -35,71 +35,92 @@ __device__ __forceinline__ float t_cdf(float t) {       // 0.5 * erfc(-t / sqrt 
 // ------------------------------------------------------------------ act_bwd
 // dz = dL/dv for y = act(v [, r1]); dr1 = dL/dr1 where r1 enters the activation
 // (GATE: y = r1*sigmoid(v); GDN: y = r1/sqrt(v); IGDN: y = r1*sqrt(v)).
-// Channels [C, ld) of the outputs are written as zeros.
+// Channels [C, ld) of the outputs are written as zeros.  One thread per group of
+// 4 channels of a pixel (vector loads/stores; all leading dims are multiples of 4).
+__device__ __forceinline__ void act_bwd1(int act, float slope, float g, float v, float a,
+                                         bool on, float& gz, float& gr) {
+  gz = g;
+  gr = 0.0f;
+  switch (act) {
+    case RGBAC_ACT_GELU:
+      gz = g * (t_cdf(v) + v * t_phi(v));
+      break;
+    case RGBAC_ACT_RELU:
+      gz = v > 0.0f ? g : 0.0f;
+      break;
+    case RGBAC_ACT_LRELU:
+      gz = v > 0.0f ? g : g * slope;
+      break;
+    case RGBAC_ACT_TANH_HALF: {
+      const float t = tanhf(v);
+      gz = g * 0.5f * (1.0f - t * t);
+      gr = g;
+      break;
+    }
+    case RGBAC_ACT_GATE: {
+      const float s = t_sigmoid(v);
+      gz = g * a * (s * (1.0f - s));
+      gr = g * s;
+      break;
+    }
+    case RGBAC_ACT_GDN: {
+      const float rs = 1.0f / sqrtf(v);
+      gz = g * a * (-0.5f) * rs / v;
+      gr = g * rs;
+      break;
+    }
+    case RGBAC_ACT_IGDN: {
+      const float sq = sqrtf(v);
+      gz = g * a * 0.5f / sq;
+      gr = g * sq;
+      break;
+    }
+    case RGBAC_ACT_MASKSEL:
+      gz = on ? g : 0.0f;
+      gr = g;
+      break;
+    default:
+      break;
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256)
 act_bwd_kernel(int act, float slope, long long npix, int C, const T* __restrict__ dy, long long ldy,
                const T* __restrict__ z, long long ldz, const T* __restrict__ r1, long long ld1,
                const uint8_t* __restrict__ sel, T* __restrict__ dz, long long lddz,
                T* __restrict__ dr1, long long lddr1) {
-  const long long n = npix * lddz;
+  const int q4 = (int)(lddz / 4);
+  const long long n = npix * q4;
   for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
-    const long long p = e / lddz;
-    const int c = (int)(e - p * lddz);
-    if (c >= C) {
-      Elem<T>::st(dz + e, 0.0f);
-      if (dr1 && c < lddr1) Elem<T>::st(dr1 + p * lddr1 + c, 0.0f);
-      continue;
+    const long long p = e / q4;
+    const int c0 = (int)(e - p * q4) * 4;
+    float gz[4] = {0.f, 0.f, 0.f, 0.f}, gr[4] = {0.f, 0.f, 0.f, 0.f};
+    if (c0 + 3 < C) {
+      float g[4], v[4] = {0.f, 0.f, 0.f, 0.f}, a[4] = {0.f, 0.f, 0.f, 0.f};
+      Elem<T>::ld4(dy + p * ldy + c0, g);
+      if (z) Elem<T>::ld4(z + p * ldz + c0, v);
+      if (r1 && (act == RGBAC_ACT_GATE || act == RGBAC_ACT_GDN || act == RGBAC_ACT_IGDN))
+        Elem<T>::ld4(r1 + p * ld1 + c0, a);
+      const bool on = sel ? sel[p] != 0 : true;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) act_bwd1(act, slope, g[r], v[r], a[r], on, gz[r], gr[r]);
+    } else {
+      const bool on = sel ? sel[p] != 0 : true;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = c0 + r;
+        if (c < C) {
+          const float g = Elem<T>::ld(dy + p * ldy + c);
+          const float v = z ? Elem<T>::ld(z + p * ldz + c) : 0.0f;
+          const float a = (r1 && (act == RGBAC_ACT_GATE || act == RGBAC_ACT_GDN ||
+                                  act == RGBAC_ACT_IGDN)) ? Elem<T>::ld(r1 + p * ld1 + c) : 0.0f;
+          act_bwd1(act, slope, g, v, a, on, gz[r], gr[r]);
+        }
+      }
     }
-    const float g = Elem<T>::ld(dy + p * ldy + c);
-    const float v = z ? Elem<T>::ld(z + p * ldz + c) : 0.0f;
-    float gz = g, gr = 0.0f;
-    switch (act) {
-      case RGBAC_ACT_GELU:
-        gz = g * (t_cdf(v) + v * t_phi(v));
-        break;
-      case RGBAC_ACT_RELU:
-        gz = v > 0.0f ? g : 0.0f;
-        break;
-      case RGBAC_ACT_LRELU:
-        gz = v > 0.0f ? g : g * slope;
-        break;
-      case RGBAC_ACT_TANH_HALF: {
-        const float t = tanhf(v);
-        gz = g * 0.5f * (1.0f - t * t);
-        gr = g;
-        break;
-      }
-      case RGBAC_ACT_GATE: {
-        const float s = t_sigmoid(v);
-        const float a = Elem<T>::ld(r1 + p * ld1 + c);
-        gz = g * a * (s * (1.0f - s));
-        gr = g * s;
-        break;
-      }
-      case RGBAC_ACT_GDN: {
-        const float a = Elem<T>::ld(r1 + p * ld1 + c);
-        const float rs = 1.0f / sqrtf(v);
-        gz = g * a * (-0.5f) * rs / v;
-        gr = g * rs;
-        break;
-      }
-      case RGBAC_ACT_IGDN: {
-        const float a = Elem<T>::ld(r1 + p * ld1 + c);
-        const float sq = sqrtf(v);
-        gz = g * a * 0.5f / sq;
-        gr = g * sq;
-        break;
-      }
-      case RGBAC_ACT_MASKSEL:
-        gz = sel[p] ? g : 0.0f;
-        gr = g;
-        break;
-      default:
-        break;
-    }
-    Elem<T>::st(dz + e, gz);
-    if (dr1) Elem<T>::st(dr1 + p * lddr1 + c, gr);
+    Elem<T>::st4(dz + p * lddz + c0, gz);
+    if (dr1 && c0 < lddr1) Elem<T>::st4(dr1 + p * lddr1 + c0, gr);
   }
 }
 
@@ -111,6 +132,7 @@ struct WgradDev {
   int send0, send1, send2;
   int cin_pad, K, k_pad, n_pad;
   int M, Hg, Wg;
+  double rWg, rHg;
   int in_h, in_w, ksize, stride, pad, square;
   int m_chunk;
   float* part;
@@ -120,41 +142,77 @@ struct WgradDev {
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s* lds_v4s_ptr;
 
-// D[n][k] = sum_m G[m][n] * Col(S)[m][k]; 64(n) x 64(k) per workgroup, 64 pixels
-// per stage, register-staged double-buffered LDS tiles (row = pixel).
-//   bf16: LDS rows of 128 B, 16-B chunk c of row r stored at slot c ^ swz(r),
-//         swz(r) = 2*((r>>1)&1) + 4*((r>>3)&1) -- the ds_read_b64_tr_b16 reads
-//         of a 32-lane half (rows 8q..8q+3 of two groups, 32 B each) then hit
-//         64 distinct banks.  Operand of lane l (row l&15 of the 16-row tile,
-//         pixels 8q..8q+7, q = l>>4) = two transposed reads.
-//   f32 : rows padded to 272 B; operands are 4 scalar reads per lane.
-template <typename T>
+__device__ __forceinline__ int wdiv(int n, int d, double rd) {   // n / d, 0 <= n < 2^31
+  int q = (int)((double)n * rd);
+  const int r = n - q * d;
+  if (r < 0) --q;
+  else if (r >= d) ++q;
+  return q;
+}
+
+// D[n][k] = sum_m G[m][n] * Col(S)[m][k]; a 64(n) x BK(k) tile per workgroup
+// (BK = 32*KT), 4 waves as 2(n) x 2(k), each 32 x 16*KT; 64 pixels per stage,
+// register-staged, double-buffered LDS tiles whose rows are pixels.
+//   bf16: the 16-B chunk c of LDS row r lives at slot c ^ swz(r) so that the
+//         ds_read_b64_tr_b16 reads of a 32-lane half (rows 8q..8q+3 of two
+//         16-lane groups, 32 B each) hit 64 distinct banks:
+//           128-B rows (64 elements): swz = 2*((r>>1)&1) + 4*((r>>3)&1)
+//           256-B rows (128 elements): swz = 2*((r&3) + 4*((r>>3)&1))
+//         The MFMA operand of lane l (row l&15 of a 16-row tile, pixels
+//         8q..8q+7 of the 32-deep k-step, q = l>>4) = two transposed reads.
+//   f32 : KT = 2, rows padded to 272 B, operands are 4 scalar LDS reads per lane.
+template <typename T, int KT>
 __global__ void __launch_bounds__(256) wgrad_kernel(const WgradDev a) {
   constexpr int EPV = Elem<T>::EPV;
-  constexpr int CPR = 64 / EPV;                   // 16-B chunks per 64-element row
-  constexpr int NL = 64 * CPR / 256;              // chunks per thread per tile
-  constexpr int RSB = sizeof(T) == 2 ? 128 : 272; // LDS row stride (bytes)
-  constexpr int TILE = 64 * RSB;
-  __shared__ __attribute__((aligned(16))) unsigned char lds[2][2][TILE];
+  constexpr int BK = 32 * KT;
+  constexpr int CPRG = 64 / EPV;                  // 16-B chunks per G row (64 channels)
+  constexpr int CPRS = BK / EPV;                  // chunks per S row
+  constexpr int NLG = 64 * CPRG / 256;            // chunks per thread per tile
+  constexpr int NLS = 64 * CPRS / 256;
+  constexpr int RSG = sizeof(T) == 2 ? 128 : 272; // LDS row strides (bytes)
+  constexpr int RSS = sizeof(T) == 2 ? BK * 2 : BK * 4 + 16;
+  static_assert(sizeof(T) == 2 || KT == 2, "f32 wgrad uses KT = 2");
+  __shared__ __attribute__((aligned(16))) unsigned char ldsG[2][64 * RSG];
+  __shared__ __attribute__((aligned(16))) unsigned char ldsS[2][64 * RSS];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int k0 = blockIdx.x * 64, n0 = blockIdx.y * 64, split = blockIdx.z;
+  const int k0 = blockIdx.x * BK, n0 = blockIdx.y * 64, split = blockIdx.z;
   const int mbeg = split * a.m_chunk;
   int mend = mbeg + a.m_chunk;
   if (mend > a.M) mend = a.M;
   const bool do_bias = a.bpart && blockIdx.x == 0;
 
+  auto slotG = [&](int r, int c) -> int {
+    if constexpr (sizeof(T) == 2) return r * RSG + 16 * (c ^ (2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1)));
+    else return r * RSG + 16 * c;
+  };
+  auto slotS = [&](int r, int c) -> int {
+    if constexpr (sizeof(T) == 2) {
+      if constexpr (BK == 64) return r * RSS + 16 * (c ^ (2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1)));
+      else return r * RSS + 16 * (c ^ (2 * ((r & 3) + 4 * ((r >> 3) & 1))));
+    } else {
+      return r * RSS + 16 * c;
+    }
+  };
+
   // per-thread chunk geometry (fixed over stages)
-  int crow[NL], ccol[NL];
-  int s_src[NL], s_cs[NL], s_dy[NL], s_dx[NL];
-  bool s_ok[NL], g_ok[NL];
+  int grow[NLG], gcol[NLG];
+  bool g_ok[NLG];
 #pragma unroll
-  for (int j = 0; j < NL; ++j) {
+  for (int j = 0; j < NLG; ++j) {
     const int c = tid + 256 * j;
-    crow[j] = c / CPR;
-    ccol[j] = c % CPR;
-    g_ok[j] = n0 + ccol[j] * EPV < a.gch;
-    const int k = k0 + ccol[j] * EPV;
+    grow[j] = c / CPRG;
+    gcol[j] = c % CPRG;
+    g_ok[j] = n0 + gcol[j] * EPV < a.gch;
+  }
+  int srow[NLS], scol[NLS], s_src[NLS], s_cs[NLS], s_dy[NLS], s_dx[NLS];
+  bool s_ok[NLS];
+#pragma unroll
+  for (int j = 0; j < NLS; ++j) {
+    const int c = tid + 256 * j;
+    srow[j] = c / CPRS;
+    scol[j] = c % CPRS;
+    const int k = k0 + scol[j] * EPV;
     const int tap = k / a.cin_pad;
     const int ci = k - tap * a.cin_pad;
     s_ok[j] = k < a.K;
@@ -165,41 +223,42 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WgradDev a) {
     else { s_src[j] = 2; s_cs[j] = ci - a.send1; s_ok[j] = s_ok[j] && ci < a.send2; }
   }
 
-  uint4 rg[NL], rs[NL];
+  uint4 rg[NLG], rs[NLS];
   auto load_stage = [&](int mb) {
 #pragma unroll
-    for (int j = 0; j < NL; ++j) {
-      const int m = mb + crow[j];
+    for (int j = 0; j < NLG; ++j) {
+      const int m = mb + grow[j];
       rg[j] = make_uint4(0, 0, 0, 0);
+      if (m < mend && g_ok[j])
+        rg[j] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.g) +
+                                                (long long)m * a.ldg + n0 + gcol[j] * EPV);
+    }
+#pragma unroll
+    for (int j = 0; j < NLS; ++j) {
+      const int m = mb + srow[j];
       rs[j] = make_uint4(0, 0, 0, 0);
-      if (m < mend) {
-        if (g_ok[j])
-          rg[j] = *reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.g) +
-                                                  (long long)m * a.ldg + n0 + ccol[j] * EPV);
-        if (s_ok[j]) {
-          const int x = m % a.Wg;
-          const int t = m / a.Wg;
-          const int y = t % a.Hg;
-          const int b = t / a.Hg;
-          const int iy = y * a.stride + s_dy[j], ix = x * a.stride + s_dx[j];
-          if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
-            const int sj = s_src[j];
-            const T* base = reinterpret_cast<const T*>(sj == 0 ? a.sp0 : (sj == 1 ? a.sp1 : a.sp2));
-            const long long ld = sj == 0 ? a.sld0 : (sj == 1 ? a.sld1 : a.sld2);
-            rs[j] = *reinterpret_cast<const uint4*>(
-                base + ((long long)(b * a.in_h + iy) * a.in_w + ix) * ld + s_cs[j]);
-          }
+      if (m < mend && s_ok[j]) {
+        const int t = wdiv(m, a.Wg, a.rWg);
+        const int x = m - t * a.Wg;
+        const int b = wdiv(t, a.Hg, a.rHg);
+        const int y = t - b * a.Hg;
+        const int iy = y * a.stride + s_dy[j], ix = x * a.stride + s_dx[j];
+        if (iy >= 0 && iy < a.in_h && ix >= 0 && ix < a.in_w) {
+          const int sj = s_src[j];
+          const T* base = reinterpret_cast<const T*>(sj == 0 ? a.sp0 : (sj == 1 ? a.sp1 : a.sp2));
+          const long long ld = sj == 0 ? a.sld0 : (sj == 1 ? a.sld1 : a.sld2);
+          rs[j] = *reinterpret_cast<const uint4*>(
+              base + ((long long)(b * a.in_h + iy) * a.in_w + ix) * ld + s_cs[j]);
         }
       }
     }
   };
-  auto slot = [&](int r, int c) -> int {     // byte offset of chunk c of row r
-    if constexpr (sizeof(T) == 2) return r * RSB + 16 * (c ^ (2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1)));
-    else return r * RSB + 16 * c;
-  };
   auto store_stage = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < NL; ++j) {
+    for (int j = 0; j < NLG; ++j)
+      *reinterpret_cast<uint4*>(&ldsG[buf][slotG(grow[j], gcol[j])]) = rg[j];
+#pragma unroll
+    for (int j = 0; j < NLS; ++j) {
       uint4 sv = rs[j];
       if (a.square) {
         if constexpr (sizeof(T) == 2) {
@@ -217,16 +276,15 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WgradDev a) {
                           __float_as_uint(p2 * p2), __float_as_uint(p3 * p3));
         }
       }
-      *reinterpret_cast<uint4*>(&lds[buf][0][slot(crow[j], ccol[j])]) = rg[j];
-      *reinterpret_cast<uint4*>(&lds[buf][1][slot(crow[j], ccol[j])]) = sv;
+      *reinterpret_cast<uint4*>(&ldsS[buf][slotS(srow[j], scol[j])]) = sv;
     }
   };
 
-  f32x4 acc[2][2];
+  f32x4 acc[2][KT];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < KT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bacc = 0.0f;
 
   const int wn = wave >> 1, wk = wave & 1;
@@ -240,13 +298,13 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WgradDev a) {
   for (int it = 0; it < nst; ++it) {
     const int buf = it & 1;
     if (it + 1 < nst) load_stage(mbeg + (it + 1) * 64);
-    const unsigned char* Gs = lds[buf][0];
-    const unsigned char* Ss = lds[buf][1];
+    const unsigned char* Gs = ldsG[buf];
+    const unsigned char* Ss = ldsS[buf];
     if (do_bias && tid < 64) {
       // column sums of G (bias gradient) over this stage's 64 pixels
 #pragma unroll 4
       for (int r = 0; r < 64; ++r) {
-        const int off = slot(r, tid / EPV) + (tid % EPV) * (int)sizeof(T);
+        const int off = slotG(r, tid / EPV) + (tid % EPV) * (int)sizeof(T);
         if constexpr (sizeof(T) == 2) bacc += bf2f(*reinterpret_cast<const uint16_t*>(Gs + off));
         else bacc += *reinterpret_cast<const float*>(Gs + off);
       }
@@ -254,53 +312,60 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WgradDev a) {
     if constexpr (sizeof(T) == 2) {
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
-        uint4 A[2], B[2];
+        uint4 A[2], B[KT];
         const int ra = kk * 32 + 8 * fq + (fi >> 2);     // block row of this lane's address
-        const int cq = (fi & 3);                         // 4-column quad within the 16 columns
+        const int cq = (fi & 3);                         // 4-column quad within 16 columns
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
-          const int ncol = wn * 32 + t * 16 + 4 * cq;    // element column
-          const int kcol = wk * 32 + t * 16 + 4 * cq;
-          const int offa0 = slot(ra, ncol >> 3) + (ncol & 7) * 2;
-          const int offa1 = slot(ra + 4, ncol >> 3) + (ncol & 7) * 2;
-          const int offb0 = slot(ra, kcol >> 3) + (kcol & 7) * 2;
-          const int offb1 = slot(ra + 4, kcol >> 3) + (kcol & 7) * 2;
-          const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)(Gs + offa0));
-          const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)(Gs + offa1));
-          const v4s b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)(Ss + offb0));
-          const v4s b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)(Ss + offb1));
+          const int ncol = wn * 32 + t * 16 + 4 * cq;
+          const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4s_ptr)(Gs + slotG(ra, ncol >> 3) + (ncol & 7) * 2));
+          const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4s_ptr)(Gs + slotG(ra + 4, ncol >> 3) + (ncol & 7) * 2));
           const uint2 ua0 = __builtin_bit_cast(uint2, a0), ua1 = __builtin_bit_cast(uint2, a1);
-          const uint2 ub0 = __builtin_bit_cast(uint2, b0), ub1 = __builtin_bit_cast(uint2, b1);
           A[t] = make_uint4(ua0.x, ua0.y, ua1.x, ua1.y);
+        }
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+          const int kcol = wk * 16 * KT + t * 16 + 4 * cq;
+          const v4s b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4s_ptr)(Ss + slotS(ra, kcol >> 3) + (kcol & 7) * 2));
+          const v4s b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4s_ptr)(Ss + slotS(ra + 4, kcol >> 3) + (kcol & 7) * 2));
+          const uint2 ub0 = __builtin_bit_cast(uint2, b0), ub1 = __builtin_bit_cast(uint2, b1);
           B[t] = make_uint4(ub0.x, ub0.y, ub1.x, ub1.y);
         }
 #pragma unroll
         for (int tn = 0; tn < 2; ++tn)
 #pragma unroll
-          for (int tk = 0; tk < 2; ++tk) mma_step<bf16_t>(acc[tn][tk], A[tn], B[tk]);
+          for (int tk = 0; tk < KT; ++tk) mma_step<bf16_t>(acc[tn][tk], A[tn], B[tk]);
       }
     } else {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        uint4 A[2], B[2];
+        uint4 A[2], B[KT];
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           const int ncol = wn * 32 + t * 16 + fi;
-          const int kcol = wk * 32 + t * 16 + fi;
-          uint32_t av[4], bv[4];
+          uint32_t av[4];
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int r = ks * 16 + 4 * fq + e;
-            av[e] = *reinterpret_cast<const uint32_t*>(Gs + r * RSB + ncol * 4);
-            bv[e] = *reinterpret_cast<const uint32_t*>(Ss + r * RSB + kcol * 4);
-          }
+          for (int e = 0; e < 4; ++e)
+            av[e] = *reinterpret_cast<const uint32_t*>(Gs + (ks * 16 + 4 * fq + e) * RSG + ncol * 4);
           A[t] = make_uint4(av[0], av[1], av[2], av[3]);
+        }
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+          const int kcol = wk * 16 * KT + t * 16 + fi;
+          uint32_t bv[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            bv[e] = *reinterpret_cast<const uint32_t*>(Ss + (ks * 16 + 4 * fq + e) * RSS + kcol * 4);
           B[t] = make_uint4(bv[0], bv[1], bv[2], bv[3]);
         }
 #pragma unroll
         for (int tn = 0; tn < 2; ++tn)
 #pragma unroll
-          for (int tk = 0; tk < 2; ++tk) mma_step<float>(acc[tn][tk], A[tn], B[tk]);
+          for (int tk = 0; tk < KT; ++tk) mma_step<float>(acc[tn][tk], A[tn], B[tk]);
       }
     }
     if (it + 1 < nst) store_stage(buf ^ 1);
@@ -311,31 +376,34 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WgradDev a) {
 #pragma unroll
   for (int tn = 0; tn < 2; ++tn)
 #pragma unroll
-    for (int tk = 0; tk < 2; ++tk)
+    for (int tk = 0; tk < KT; ++tk)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int n = n0 + wn * 32 + tn * 16 + 4 * fq + r;
-        const int k = k0 + wk * 32 + tk * 16 + fi;
-        P[(size_t)n * a.k_pad + k] = acc[tn][tk][r];
+        const int k = k0 + wk * 16 * KT + tk * 16 + fi;
+        if (k < a.k_pad) P[(size_t)n * a.k_pad + k] = acc[tn][tk][r];
       }
   if (do_bias && tid < 64) a.bpart[(size_t)split * a.n_pad + n0 + tid] = bacc;
 }
 
-// dw[i] = sum_s part[s][map[i]] (map < 0 -> 0); db[j] = sum_s bpart[s][j]   (fixed order)
+// Slab reduction in the slab's own (coalesced) order: for slab position e (row n,
+// column k of the packed layout), dw[fmap[e]] = sum_s part[s][e] (fmap < 0: a pad
+// slot, skipped; every parameter element owns exactly one slot);
+// db[j] = sum_s bpart[s][j].  Fixed summation order: deterministic.
 __global__ void __launch_bounds__(256)
-wgrad_reduce_kernel(long long numel, const int* __restrict__ map, const float* __restrict__ part,
+wgrad_reduce_kernel(long long nslot, const int* __restrict__ fmap, const float* __restrict__ part,
                     int nsplit, long long slab, float* __restrict__ dw, int nbias,
                     const float* __restrict__ bpart, int n_pad, float* __restrict__ db) {
-  const long long total = numel + nbias;
+  const long long total = nslot + nbias;
   for (long long e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
-    if (e < numel) {
-      const int p = map[e];
+    if (e < nslot) {
+      const int i = fmap[e];
+      if (i < 0) continue;
       float s = 0.0f;
-      if (p >= 0)
-        for (int q = 0; q < nsplit; ++q) s += part[q * slab + p];
-      dw[e] = s;
+      for (int q = 0; q < nsplit; ++q) s += part[q * slab + e];
+      dw[i] = s;
     } else {
-      const int j = (int)(e - numel);
+      const int j = (int)(e - nslot);
       float s = 0.0f;
       for (int q = 0; q < nsplit; ++q) s += bpart[(size_t)q * n_pad + j];
       db[j] = s;
@@ -527,14 +595,14 @@ relpos_reduce_kernel(int nblk, int heads, int N, const float* __restrict__ bpart
   }
 }
 __global__ void __launch_bounds__(256)
-relpos_scatter_kernel(int ntab, int heads, int N, const int64_t* __restrict__ index,
-                      const float* __restrict__ dense, float* __restrict__ dtable) {
+relpos_scatter_kernel(int ntab, int heads, int N, const int* __restrict__ csr_off,
+                      const int* __restrict__ csr_ij, const float* __restrict__ dense,
+                      float* __restrict__ dtable) {
   const int total = ntab * heads;
   for (int e = blockIdx.x * 256 + threadIdx.x; e < total; e += gridDim.x * 256) {
     const int t = e / heads, h = e - t * heads;
     float s = 0.0f;
-    for (int ij = 0; ij < N * N; ++ij)
-      if (index[ij] == t) s += dense[(size_t)h * N * N + ij];
+    for (int q = csr_off[t]; q < csr_off[t + 1]; ++q) s += dense[(size_t)h * N * N + csr_ij[q]];
     dtable[e] = s;
   }
 }
@@ -873,6 +941,8 @@ extern "C" int rgbac_act_bwd(int dtype, int act, float act_param, int64_t npix, 
   RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
   RGBAC_REQUIRE(act >= RGBAC_ACT_NONE && act <= RGBAC_ACT_MASKSEL, "act has no backward here");
   RGBAC_REQUIRE(npix >= 0 && channels > 0 && lddz >= channels && ldy >= channels, "shape");
+  RGBAC_REQUIRE(lddz % 4 == 0 && ldy % 4 == 0 && (!z || ldz % 4 == 0) && (!res1 || ld1 % 4 == 0) &&
+                    (!dres1 || (lddr1 % 4 == 0 && lddr1 == lddz)), "leading dims must be multiples of 4");
   RGBAC_REQUIRE(dy && dz, "null pointer");
   RGBAC_REQUIRE(act == RGBAC_ACT_NONE || act == RGBAC_ACT_MASKSEL || z, "act needs z");
   RGBAC_REQUIRE(!(act == RGBAC_ACT_GATE || act == RGBAC_ACT_GDN || act == RGBAC_ACT_IGDN) || res1,
@@ -880,7 +950,7 @@ extern "C" int rgbac_act_bwd(int dtype, int act, float act_param, int64_t npix, 
   RGBAC_REQUIRE(act != RGBAC_ACT_MASKSEL || sel, "MASKSEL needs sel");
   if (npix == 0) return RGBAC_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  const int g = grid_for(npix * lddz);
+  const int g = grid_for(npix * lddz / 4);
 #define K_(T, ...)                                                                            \
   hipLaunchKernelGGL(act_bwd_kernel<T>, dim3(g), dim3(256), 0, st, act, act_param, npix,        \
                      channels, (const T*)dy, ldy, (const T*)z, ldz, (const T*)res1, ld1, sel,   \
@@ -929,27 +999,33 @@ extern "C" int rgbac_conv_wgrad(const rgbac_wgrad_args* a, void* stream) {
   d.in_h = a->in_h; d.in_w = a->in_w; d.ksize = a->ksize; d.stride = a->stride; d.pad = a->pad;
   d.square = a->square_input;
   d.m_chunk = (int)(((M + a->nsplit - 1) / a->nsplit + 63) / 64 * 64);
+  d.rWg = 1.0 / a->grid_w;
+  d.rHg = 1.0 / a->grid_h;
   d.part = a->partial;
   d.bpart = a->bias_partial;
-  dim3 grid(a->k_pad / 64, a->n_pad / 64, a->nsplit);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // 64 x 128 tiles when K is wide (8 MFMAs per k-step per wave on 12 transposed reads)
+  const bool wide = a->dtype == RGBAC_BF16 && a->k_pad >= 512;
+  dim3 grid(wide ? (a->k_pad + 127) / 128 : a->k_pad / 64, a->n_pad / 64, a->nsplit);
   if (a->dtype == RGBAC_F32)
-    hipLaunchKernelGGL(wgrad_kernel<float>, grid, dim3(256), 0, st, d);
+    hipLaunchKernelGGL((wgrad_kernel<float, 2>), grid, dim3(256), 0, st, d);
+  else if (wide)
+    hipLaunchKernelGGL((wgrad_kernel<bf16_t, 4>), grid, dim3(256), 0, st, d);
   else
-    hipLaunchKernelGGL(wgrad_kernel<bf16_t>, grid, dim3(256), 0, st, d);
+    hipLaunchKernelGGL((wgrad_kernel<bf16_t, 2>), grid, dim3(256), 0, st, d);
   return check_launch("wgrad_kernel");
 }
 
-extern "C" int rgbac_wgrad_reduce(int64_t numel, const int32_t* map, const float* partial,
+extern "C" int rgbac_wgrad_reduce(int64_t nslot, const int32_t* fmap, const float* partial,
                                   int nsplit, int64_t slab, float* dw, int nbias,
                                   const float* bias_partial, int n_pad, float* db, void* stream) {
-  RGBAC_REQUIRE(numel >= 0 && nsplit >= 1 && slab > 0, "shape");
-  RGBAC_REQUIRE((numel == 0 || (map && partial && dw)) && (nbias == 0 || (bias_partial && db)),
+  RGBAC_REQUIRE(nslot >= 0 && nsplit >= 1 && slab > 0 && nslot <= slab, "shape");
+  RGBAC_REQUIRE((nslot == 0 || (fmap && partial && dw)) && (nbias == 0 || (bias_partial && db)),
                 "null pointer");
   RGBAC_REQUIRE(nbias <= n_pad, "nbias > n_pad");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(numel + nbias)), dim3(256), 0, st, numel,
-                     map, partial, nsplit, slab, dw, nbias, bias_partial, n_pad, db);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(nslot + nbias)), dim3(256), 0, st, nslot,
+                     fmap, partial, nsplit, slab, dw, nbias, bias_partial, n_pad, db);
   return check_launch("wgrad_reduce_kernel");
 }
 
@@ -979,9 +1055,11 @@ extern "C" int rgbac_winattn_core_bwd(int dtype, int batch, int h, int w, int ch
 }
 
 extern "C" int rgbac_relpos_bwd(int nblk, int heads, int ws, const float* bias_partial,
-                                const int64_t* index, float* dense, float* dtable, void* stream) {
+                                const int32_t* csr_off, const int32_t* csr_ij, float* dense,
+                                float* dtable, void* stream) {
   RGBAC_REQUIRE(ws == 4 || ws == 8, "window size");
-  RGBAC_REQUIRE(nblk >= 1 && heads > 0 && bias_partial && index && dense && dtable, "args");
+  RGBAC_REQUIRE(nblk >= 1 && heads > 0 && bias_partial && csr_off && csr_ij && dense && dtable,
+                "args");
   const int N = ws * ws;
   const int ntab = (2 * ws - 1) * (2 * ws - 1);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -990,7 +1068,7 @@ extern "C" int rgbac_relpos_bwd(int nblk, int heads, int ws, const float* bias_p
   int rc = check_launch("relpos_reduce_kernel");
   if (rc) return rc;
   hipLaunchKernelGGL(relpos_scatter_kernel, dim3(grid_for((long long)ntab * heads)), dim3(256), 0,
-                     st, ntab, heads, N, index, dense, dtable);
+                     st, ntab, heads, N, csr_off, csr_ij, dense, dtable);
   return check_launch("relpos_scatter_kernel");
 }
 

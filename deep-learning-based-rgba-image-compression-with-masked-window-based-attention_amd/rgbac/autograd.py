@@ -145,7 +145,8 @@ class TrainConv:
             self.rows = cout
         pkw, idxw = wg
         self.wg_kpad = pkw.k_pad
-        self.wg_map = _inverse(idxw, numel, pkw.k_pad)
+        self.wg_map = _inverse(idxw, numel, pkw.k_pad)      # param element -> slab slot
+        self.wg_fmap = idxw[0].contiguous()                  # slab slot -> param element
         self.bias_idx = {}
         self._fw = {}
         self._bw = {}
@@ -189,19 +190,25 @@ def train_conv_of(m, kind, wshape, stride, segs, device):
 # --------------------------------------------------------------------------
 # weight gradient (rgbac_conv_wgrad + rgbac_wgrad_reduce)
 # --------------------------------------------------------------------------
-def _nsplit(tiles, M):
-    want = max(1, -(-2048 // tiles))
-    return int(max(1, min(want, -(-M // 512), 1024)))
+_SLAB_FLOATS = 16 << 20         # cap of nsplit * n_pad * k_pad (64 MiB of fp32 partials)
 
 
-def wgrad(G, S, ksize, stride, pad, square, k_pad, inv_map, numel, nbias=0, bias_from_g=True):
+def _nsplit(tiles, M, slab):
+    """Pixel splits: enough workgroups to fill the chip (~1024), each split >= 512 pixels,
+    and the fp32 partial slabs bounded (their write + reduce read is pure overhead)."""
+    want = max(1, -(-1024 // tiles))
+    cap = max(1, _SLAB_FLOATS // slab)
+    return int(max(1, min(want, -(-M // 512), cap, 1024)))
+
+
+def wgrad(G, S, ksize, stride, pad, square, k_pad, fmap, numel, nbias=0, bias_from_g=True):
     """dW (fp32, flat param layout) and optional db from G (Feat on the M grid) and
     sources S [Feat] sampled with (ksize, stride, pad)."""
     dev = G.t.device
     n_pad = round_up(G.ldc, 64)
     M = G.B * G.H * G.W
     tiles = (k_pad // 64) * (n_pad // 64)
-    ns = _nsplit(tiles, M)
+    ns = _nsplit(tiles, M, n_pad * k_pad)
     part = torch.empty(ns * n_pad * k_pad, dtype=_F32, device=dev)
     bpart = None
     if nbias and bias_from_g:
@@ -226,12 +233,15 @@ def wgrad(G, S, ksize, stride, pad, square, k_pad, inv_map, numel, nbias=0, bias
     st = _stream(G.t)
     rt.timed("wgrad_kernel", 2.0 * M * G.ldc * ksize * ksize * cin,
              G.t.element_size() * M * (G.ldc + cin * ksize * ksize // max(1, stride * stride)),
-             lambda: _lib.call("rgbac_conv_wgrad", ctypes.byref(a), st))
+             lambda: _lib.call("rgbac_conv_wgrad", ctypes.byref(a), st),
+             f"wgrad_kernel k{ksize}s{stride} G{G.ldc}@{G.H}x{G.W} S{cin}@{s0.H}x{s0.W} "
+             f"B{G.B} split{ns}{' sq' if square else ''}")
     dw = torch.empty(numel, dtype=_F32, device=dev)
     db = torch.empty(nbias, dtype=_F32, device=dev) if nbias else None
     if nbias and not bias_from_g:
         raise ValueError("use colsum for biases not on G")
-    _lib.call("rgbac_wgrad_reduce", numel, inv_map.data_ptr(), part.data_ptr(), ns,
+    nslot = min(fmap.shape[0], n_pad) * k_pad
+    _lib.call("rgbac_wgrad_reduce", nslot, fmap.data_ptr(), part.data_ptr(), ns,
               n_pad * k_pad, dw.data_ptr(), nbias if bpart is not None else 0,
               None if bpart is None else bpart.data_ptr(), n_pad,
               None if db is None else db.data_ptr(), st)
@@ -360,7 +370,7 @@ class ConvFn(Function):
             if not need[7 + i]:
                 continue
             pk = tc.bwd_pack(i, dt, weight.detach().contiguous())
-            o = new_feat(f.B, f.H, f.W, f.C, dt, f.t.device, zero=True)
+            o = new_feat(f.B, f.H, f.W, f.C, dt, f.t.device)   # zero-filled iff padded
             if call.square:
                 preps.append(rt.prepare(pk, [G.src()], out=o, act="sqbwd", res0=dr1,
                                         res1=f, bias=False))
@@ -378,12 +388,12 @@ class ConvFn(Function):
             if tc.kind == "convt":
                 # G = the convT input, S = dL/dv on the output grid
                 dw, _ = wgrad(feats[0], [dz], tc.ksize, tc.stride if tc.ksize == 5 else 1,
-                              tc.ksize // 2, False, tc.wg_kpad, tc.wg_map, tc.numel)
+                              tc.ksize // 2, False, tc.wg_kpad, tc.wg_fmap, tc.numel)
                 db = colsum(dz, tc.cout) if has_b else None
             else:
                 p = tc.ksize // 2
                 dw, db = wgrad(G, feats, tc.ksize, tc.stride, p, call.square, tc.wg_kpad,
-                               tc.wg_map, tc.numel, nbias=nb)
+                               tc.wg_fmap, tc.numel, nbias=nb)
             g_w = dw.view(weight.shape)
             g_b = db
         return (None, g_w, g_b, g_res0, g_res1, g_res2, None, *g_srcs)
@@ -420,6 +430,22 @@ def conv_t(m, srcs, act="none", act_param=0.0, res0=None, res1=None, res2=None, 
 # --------------------------------------------------------------------------
 # window attention core
 # --------------------------------------------------------------------------
+_CSR = {}
+
+
+def _relpos_csr(index, ntab):
+    """(offsets, flat (i, j) list) grouping relative_position_index by table row."""
+    key = (index.data_ptr(), ntab)
+    if key not in _CSR:
+        flat = index.reshape(-1).long()
+        order = torch.argsort(flat, stable=True)
+        counts = torch.bincount(flat, minlength=ntab)
+        off = torch.zeros(ntab + 1, dtype=torch.int64, device=index.device)
+        off[1:] = torch.cumsum(counts, 0)
+        _CSR[key] = (off.to(torch.int32).contiguous(), order.to(torch.int32).contiguous())
+    return _CSR[key]
+
+
 class WinAttnFn(Function):
     @staticmethod
     def forward(ctx, spec, qkv_t, table, alpha):
@@ -467,10 +493,11 @@ class WinAttnFn(Function):
                                    st))
         dtab = None
         if ctx.needs_input_grad[2]:
+            off, ij = _relpos_csr(index, table.shape[0])
             dense_g = torch.empty(heads * N * N, dtype=_F32, device=dev)
             dtab = torch.empty(table.shape, dtype=_F32, device=dev)
-            _lib.call("rgbac_relpos_bwd", nblk, heads, ws, part.data_ptr(), index.data_ptr(),
-                      dense_g.data_ptr(), dtab.data_ptr(), st)
+            _lib.call("rgbac_relpos_bwd", nblk, heads, ws, part.data_ptr(), off.data_ptr(),
+                      ij.data_ptr(), dense_g.data_ptr(), dtab.data_ptr(), st)
         return None, dqkv, dtab, None
 
 

@@ -67,12 +67,12 @@ class LaunchProfiler:
         return out
 
 
-def timed(name, flops, nbytes, fn):
+def timed(name, flops, nbytes, fn, desc=None):
     """Run ``fn`` (one non-conv launch), attributed to ``name`` when profiling."""
     if PROFILER is None:
         fn()
     else:
-        PROFILER.wrap(name, flops, nbytes, fn)
+        PROFILER.wrap(name, flops, nbytes, fn, desc)
 
 
 def round_up(x, m):
@@ -92,8 +92,9 @@ DIRECT_STEPS = 12
 DIRECT_LDS = 65536       # weight panel bytes of a direct tile (dynamic LDS limit)
 KSPLITS = (1, 2, 4, 8)
 TUNE = os.environ.get("RGBAC_TUNE", "1") != "0"
-# RGBAC_TILE_SET: "all" (default) | "stream" (streaming K-ring tiles only, for A/B runs)
-TILE_SET = os.environ.get("RGBAC_TILE_SET", "all")
+# RGBAC_TILE_SET: "stream" (default: streaming K-ring tiles; the weight-resident and
+# direct small-K tiles measured slower under graph replay) | "all"
+TILE_SET = os.environ.get("RGBAC_TILE_SET", "stream")
 _tune_cache = {}          # shape key -> (tile, ksplit)
 FORCE = None              # (tile, ksplit) override, used by the tile/split-K tests
 

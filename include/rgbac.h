@@ -248,9 +248,11 @@ typedef struct rgbac_wgrad_args {
 } rgbac_wgrad_args;
 int rgbac_conv_wgrad(const rgbac_wgrad_args* args, void* stream);
 
-/* dw[i] = sum_s partial[s*slab + map[i]] (map[i] < 0 -> 0) in the PyTorch
- * parameter layout; db[j] = sum_s bias_partial[s*n_pad + j], j < nbias.     */
-int rgbac_wgrad_reduce(int64_t numel, const int32_t* map, const float* partial, int nsplit,
+/* Fixed-order sum of the slabs, scattered into the PyTorch parameter layout:
+ * dw[fmap[e]] = sum_s partial[s*slab + e] for slab slots e < nslot with
+ * fmap[e] >= 0 (fmap = the packed layout's slot -> parameter element map);
+ * db[j] = sum_s bias_partial[s*n_pad + j], j < nbias.                       */
+int rgbac_wgrad_reduce(int64_t nslot, const int32_t* fmap, const float* partial, int nsplit,
                        int64_t slab, float* dw, int nbias, const float* bias_partial, int n_pad,
                        float* db, void* stream);
 
@@ -264,8 +266,11 @@ int rgbac_winattn_core_bwd(int dtype, int batch, int h, int w, int channels, int
                            const float* alpha, const float* bias, const void* dout, int64_t ldo,
                            void* dqkv, int64_t lddq, int nblk, float* bias_partial,
                            void* stream);
+/* csr_off[(2ws-1)^2 + 1] / csr_ij[N*N]: for table row t, the flattened (i, j)
+ * positions with relative_position_index[i][j] == t (fixed order).          */
 int rgbac_relpos_bwd(int nblk, int heads, int ws, const float* bias_partial,
-                     const int64_t* index, float* dense, float* dtable, void* stream);
+                     const int32_t* csr_off, const int32_t* csr_ij, float* dense, float* dtable,
+                     void* stream);
 
 /* GaussianConditional + bits + ste_round backward of one latent slice
  * (AutoEncoderRGB_Journal.py:255-257,280): gbits = device dL/d(sum bits),

@@ -76,13 +76,15 @@ def _ref_act(act, slope, v, r0, r1, r2, sel):
     return v
 
 
-LAYERS = ["conv3_2src", "conv5s2", "conv3s2", "conv1", "convt5", "convt5_c3", "convt1",
+LAYERS = ["conv3_2src", "conv3_wide", "conv5s2", "conv3s2", "conv1", "convt5", "convt5_c3", "convt1",
           "subpel", "linear"]
 
 
 def _make(name, g):
     if name == "conv3_2src":
         return nn.Conv2d(40, 24, 3, padding=1), [16, 24], 1
+    if name == "conv3_wide":                  # K = 864 >= 512: the 64x128 wgrad tile
+        return nn.Conv2d(96, 40, 3, padding=1), [96], 1
     if name == "conv5s2":
         return nn.Conv2d(3, 16, 5, stride=2, padding=2), [3], 2
     if name == "conv3s2":
