@@ -75,6 +75,22 @@ __device__ __forceinline__ void mma_step<float>(f32x4& acc, uint4 a, uint4 b) {
   acc = __builtin_amdgcn_mfma_f32_16x16x4f32(__uint_as_float(a.w), __uint_as_float(b.w), acc, 0, 0, 0);
 }
 
+// GELU(x) = 0.5 x (1 + erf(x / sqrt 2)) with a branch-free erf (Abramowitz &
+// Stegun 7.1.26, |erf error| <= 1.5e-7; 1 + erf is formed as q = 1 - erf(|z|)
+// for x < 0, so no cancellation): ~16 instructions instead of erff's ~40
+// divergent ones.  Used where results are stored as bf16 (3 significant
+// digits); the fp32 parity mode keeps erff.
+__device__ __forceinline__ float gelu_fast(float x) {
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float q = p * t * __expf(-z * z);         // 1 - erf(|z|)
+  return 0.5f * x * (x >= 0.0f ? 2.0f - q : q);
+}
+
 // ---------------------------------------------------------------- host side
 void set_error(const std::string& msg);
 int check_launch(const char* what);

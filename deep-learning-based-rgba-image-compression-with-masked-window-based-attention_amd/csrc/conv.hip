@@ -87,6 +87,10 @@ __device__ __forceinline__ int udiv(int n, int d, double rd) {
 __device__ __forceinline__ float gelu_f(float v) {
   return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f));
 }
+// exact erf GELU for fp32 (parity mode), the branch-free form for bf16 outputs
+template <typename T> __device__ __forceinline__ float gelu_t(float v);
+template <> __device__ __forceinline__ float gelu_t<float>(float v) { return gelu_f(v); }
+template <> __device__ __forceinline__ float gelu_t<bf16_t>(float v) { return gelu_fast(v); }
 __device__ __forceinline__ float sigmoid_f(float v) { return 1.0f / (1.0f + expf(-v)); }
 __device__ __forceinline__ float std_cum_f(float t) {
   return 0.5f * erfcf(-0.70710678118654752440f * t);
@@ -142,7 +146,7 @@ __device__ __forceinline__ void epilogue4(const ConvShared& s, const ConvGroup& 
       const int oy = 2 * my + (r >> 1), ox = 2 * mx + (r & 1);
       const long long op = (long long)(b * s.out_h + oy) * s.out_w + ox;
       if (g.zout) Elem<T>::st(reinterpret_cast<T*>(g.zout) + op * g.zld + g.out_coff + cc, x);
-      if (s.act == RGBAC_ACT_GELU) x = gelu_f(x);
+      if (s.act == RGBAC_ACT_GELU) x = gelu_t<T>(x);
       Elem<T>::st(out + op * g.out_ldc + g.out_coff + cc, x);
     }
     return;
@@ -172,7 +176,7 @@ __device__ __forceinline__ void epilogue4(const ConvShared& s, const ConvGroup& 
   switch (s.act) {
     case RGBAC_ACT_GELU:
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = gelu_f(v[r]);
+      for (int r = 0; r < 4; ++r) v[r] = gelu_t<T>(v[r]);
       break;
     case RGBAC_ACT_RELU:
 #pragma unroll
@@ -251,7 +255,7 @@ __device__ __forceinline__ void epilogue_row(const ConvShared& s, const ConvGrou
         const int oy = 2 * my + (r >> 1), ox = 2 * mx + (r & 1);
         const long long op = (long long)(b * s.out_h + oy) * s.out_w + ox;
         if (g.zout) Elem<T>::st(reinterpret_cast<T*>(g.zout) + op * g.zld + g.out_coff + cc, x);
-        if (s.act == RGBAC_ACT_GELU) x = gelu_f(x);
+        if (s.act == RGBAC_ACT_GELU) x = gelu_t<T>(x);
         Elem<T>::st(out + op * g.out_ldc + g.out_coff + cc, x);
       }
     }
@@ -295,7 +299,7 @@ __device__ __forceinline__ void epilogue_row(const ConvShared& s, const ConvGrou
     for (int r = 0; r < 4; ++r) {
       float x = s.act == RGBAC_ACT_SQBWD ? r0[j][r] + 2.0f * r1[j][r] * vv[r] : vv[r] + r0[j][r];
       switch (s.act) {
-        case RGBAC_ACT_GELU: x = gelu_f(x); break;
+        case RGBAC_ACT_GELU: x = gelu_t<T>(x); break;
         case RGBAC_ACT_RELU: x = x > 0.f ? x : 0.f; break;
         case RGBAC_ACT_LRELU: x = x > 0.f ? x : x * s.act_param; break;
         case RGBAC_ACT_TANH_HALF: x = r1[j][r] + 0.5f * tanhf(x); break;

@@ -1,0 +1,350 @@
+// Fused ResidualUnit (reference: layers/Masked_Attention.py:150-169)
+//
+//   y = GELU( W3 * GELU( W2 (*)3x3 GELU( W1 * x + b1 ) + b2 ) + b3 + x )
+//
+// for C = 192 (CH = 96) on bf16 NHWC activations.  One workgroup computes an
+// 8x8 output tile: stage 1 evaluates the first 1x1 conv on the 10x10 halo
+// (zero outside the image, as the 3x3's zero padding requires) into LDS (T1),
+// stage 2 the 3x3 conv from T1 into LDS (T2), stage 3 the last 1x1 conv with
+// bias, residual and GELU straight to HBM.  The three packed weight matrices
+// ([rows][k_pad], k = tap*cin + c, the conv engine's layout) stream through one
+// double-buffered LDS ring in 12-15 KB chunks shared by the four waves.
+// Versus three conv launches this removes two HBM round trips of the
+// intermediates and two launch/latency tails per unit; two units of identical
+// shape (the conv_a / conv_b chains of Win_noShift_Attention) run as one
+// launch (blockIdx.z = group).
+//
+// MFMA: v_mfma_f32_16x16x32_bf16, D[n][m] = sum_k W[n][k] X[m][k]: channels on
+// the row axis (each lane ends with 4 consecutive channels of one pixel).
+//   stage 1: M = 128 halo rows (100 real; waves own 32 rows), N = 96, K = 192
+//   stage 2: M = 64, N = 96, K = 864    (waves: 2 channel halves x 2 pixel halves)
+//   stage 3: M = 64, N = 192, K = 96    (same split)
+// LDS: T1 100 x 192 B, T2 (64 x 192 B) aliased onto T1 once
+// stage 2 has consumed it, ring 2 x 15 KB -> 51 KB: three workgroups per CU.
+// Weight chunks are prefetched PF = 4 chunks ahead in registers (the chunk
+// loops are fully unrolled so the register ring is statically indexed).
+#include "common.h"
+
+namespace rgbac {
+
+constexpr int kRuMaxGroups = 4;
+
+struct RuGroup {
+  const bf16_t* x; long long ldx;
+  const bf16_t* w1; const bf16_t* w2; const bf16_t* w3;
+  int kp1, kp2, kp3;
+  const float* b1; const float* b2; const float* b3;
+  bf16_t* out; long long ldo;
+};
+struct RuArgsDev {
+  int batch, H, W, ngroups;
+  RuGroup g[kRuMaxGroups];
+};
+
+__device__ __forceinline__ float ru_gelu(float v) { return gelu_fast(v); }   // bf16 outputs
+
+template <int C, int CH>
+__global__ void __launch_bounds__(256, 3) ru_fused_kernel(const RuArgsDev args) {
+  constexpr int TS = 8, HS = TS + 2, NH = HS * HS;     // 8x8 tile, 10x10 halo
+  constexpr int NT1 = CH / 16;                         // n tiles of stages 1 / 2
+  constexpr int NT3 = C / 16;                          // n tiles of stage 3
+  constexpr int TROW = CH * 2;    // T1 / T2 row bytes: unpadded rows give at most 2-way
+                                  // conflicts for the ds_read_b128 lane groups (208 B: 3-way)
+  constexpr int KC1 = C / 64;                          // stage-1 chunks (64 k each)
+  constexpr int K2 = 9 * CH;
+  constexpr int KC2 = (K2 + 63) / 64;                  // stage-2 chunks (64 k each)
+  constexpr int KC3 = CH / 32;                         // stage-3 chunks (32 k each)
+  constexpr int NCH = KC1 + KC2 + KC3;
+  constexpr int RING = (CH * 128 > C * 80 ? CH * 128 : C * 80);   // bytes per ring slot
+  constexpr int PIECES = 768;                          // 16-B pieces per chunk (12 KB)
+  static_assert(CH * 128 == PIECES * 16 && C * 64 == PIECES * 16, "chunk geometry");
+  static_assert(C % 64 == 0 && CH % 32 == 0, "channel geometry");
+  constexpr int PF = 4;                                // chunks in flight ahead
+  __shared__ __attribute__((aligned(16))) unsigned char T1[NH * TROW];
+  unsigned char* const T2 = T1;                        // stage-3 input, after stage 2
+  __shared__ __attribute__((aligned(16))) unsigned char ring[2][RING];
+
+  const RuGroup& g = args.g[blockIdx.z];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int tx_n = args.W / TS, ty_n = args.H / TS;
+  int t = blockIdx.x;
+  const int tx = t % tx_n; t /= tx_n;
+  const int ty = t % ty_n;
+  const int b = t / ty_n;
+  const int y0 = ty * TS, x0 = tx * TS;
+
+  // ---- weight ring: chunk c -> 3 pieces of 16 B per thread, staged in registers
+  // set c % 5 of five named register sets (selects fold after full unrolling;
+  // an indexed array here is not promoted to registers), stored to LDS slot c & 1
+  static_assert(PF == 4, "five register sets");
+  uint4 wa[3], wb[3], wc[3], wd[3], we[3];
+  auto load_w = [&](int c) {
+    if (c >= NCH) return;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int p = tid + 256 * j;
+      const bf16_t* src;
+      if (c < KC1) {
+        const int r = p >> 3, q = p & 7;
+        src = g.w1 + (size_t)r * g.kp1 + c * 64 + q * 8;
+      } else if (c < KC1 + KC2) {
+        const int r = p >> 3, q = p & 7;
+        src = g.w2 + (size_t)r * g.kp2 + (c - KC1) * 64 + q * 8;
+      } else {
+        const int r = p >> 2, q = p & 3;
+        src = g.w3 + (size_t)r * g.kp3 + (c - KC1 - KC2) * 32 + q * 8;
+      }
+      const uint4 v = *reinterpret_cast<const uint4*>(src);
+      const int set = c % 5;
+      if (set == 0) wa[j] = v;
+      else if (set == 1) wb[j] = v;
+      else if (set == 2) wc[j] = v;
+      else if (set == 3) wd[j] = v;
+      else we[j] = v;
+    }
+  };
+  auto store_w = [&](int c, int buf) {
+    if (c >= NCH) return;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int p = tid + 256 * j;
+      int off;
+      if (c < KC1 + KC2) {
+        const int r = p >> 3, q = p & 7;
+        off = r * 128 + 16 * (q ^ (r & 7));
+      } else {
+        const int r = p >> 2, q = p & 3;
+        off = r * 80 + 16 * q;
+      }
+      const int set = c % 5;
+      *reinterpret_cast<uint4*>(&ring[buf][off]) =
+          set == 0 ? wa[j] : set == 1 ? wb[j] : set == 2 ? wc[j] : set == 3 ? wd[j] : we[j];
+    }
+  };
+  // A fragment of n tile j, k-step kk of a 64-k chunk (stages 1 / 2)
+  auto wfrag64 = [&](int buf, int j, int kk) -> uint4 {
+    const int r = j * 16 + fr, q = kk * 4 + fq;
+    return *reinterpret_cast<const uint4*>(&ring[buf][r * 128 + 16 * (q ^ (r & 7))]);
+  };
+  auto wfrag32 = [&](int buf, int j) -> uint4 {          // stage 3 (32-k chunks)
+    const int r = j * 16 + fr;
+    return *reinterpret_cast<const uint4*>(&ring[buf][r * 80 + 16 * fq]);
+  };
+
+#pragma unroll
+  for (int c = 0; c <= PF; ++c) load_w(c);
+  store_w(0, 0);
+  __syncthreads();
+
+  // ======================= stage 1: T1 = GELU(W1 x + b1) on the 10x10 halo
+  {
+    f32x4 acc[NT1][2];
+#pragma unroll
+    for (int j = 0; j < NT1; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bf16_t* xrow[2];
+    bool xin[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int hp = wave * 32 + i * 16 + fr;
+      const int hy = hp / HS, hx = hp - (hp / HS) * HS;
+      const int iy = y0 + hy - 1, ix = x0 + hx - 1;
+      xin[i] = hp < NH && iy >= 0 && iy < args.H && ix >= 0 && ix < args.W;
+      xrow[i] = g.x + ((long long)(b * args.H + (xin[i] ? iy : 0)) * args.W + (xin[i] ? ix : 0)) * g.ldx;
+    }
+#pragma unroll
+    for (int c = 0; c < KC1; ++c) {
+      uint4 xb[2][2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          xb[kk][i] = xin[i] ? *reinterpret_cast<const uint4*>(xrow[i] + c * 64 + kk * 32 + fq * 8)
+                             : make_uint4(0, 0, 0, 0);
+      const int buf = c & 1;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int j = 0; j < NT1; ++j) {
+          const uint4 a = wfrag64(buf, j, kk);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) mma_step<bf16_t>(acc[j][i], a, xb[kk][i]);
+        }
+      store_w(c + 1, buf ^ 1);
+      load_w(c + PF + 1);
+      __syncthreads();
+    }
+    // epilogue -> T1 (zero outside the image: the 3x3's zero padding)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int hp = wave * 32 + i * 16 + fr;
+      if (hp >= NH) continue;
+#pragma unroll
+      for (int j = 0; j < NT1; ++j) {
+        const int n = j * 16 + fq * 4;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = xin[i] ? ru_gelu(acc[j][i][r] + g.b1[n + r]) : 0.0f;
+        Elem<bf16_t>::st4(reinterpret_cast<bf16_t*>(&T1[hp * TROW + n * 2]), v);
+      }
+    }
+  }
+  __syncthreads();
+
+  // stages 2 / 3: waves as 2 (channel halves) x 2 (pixel halves): per k-step a wave
+  // reads NT/2 weight fragments and 2 pixel fragments for NT/2 x 2 MFMAs
+  const int wn = wave >> 1, wm = wave & 1;
+
+  // ======================= stage 2: T2 = GELU(W2 (*) T1 + b2), 3x3 over the halo
+  {
+    constexpr int NJ = NT1 / 2;                       // 3 channel tiles per wave
+    f32x4 acc[NJ][2];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int py[2], px[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int p = wm * 32 + i * 16 + fr;            // this lane's pixel of m tile i
+      py[i] = p >> 3;
+      px[i] = p & 7;
+    }
+#pragma unroll
+    for (int c2 = 0; c2 < KC2; ++c2) {
+      const int c = KC1 + c2;
+      const int buf = c & 1;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int k = c2 * 64 + kk * 32;              // a 32-k step never straddles taps
+        const int tap = k / CH, ch = k - tap * CH + fq * 8;
+        uint4 bv[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          bv[i] = make_uint4(0, 0, 0, 0);
+          if (tap < 9) {
+            const int hr = (py[i] + tap / 3) * HS + px[i] + tap % 3;
+            bv[i] = *reinterpret_cast<const uint4*>(&T1[hr * TROW + ch * 2]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          const uint4 a = wfrag64(buf, wn * NJ + j, kk);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) mma_step<bf16_t>(acc[j][i], a, bv[i]);
+        }
+      }
+      store_w(c + 1, buf ^ 1);
+      load_w(c + PF + 1);
+      __syncthreads();                  // (last one: every wave is done reading T1)
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int p = wm * 32 + i * 16 + fr;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = (wn * NJ + j) * 16 + fq * 4;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = ru_gelu(acc[j][i][r] + g.b2[n + r]);
+        Elem<bf16_t>::st4(reinterpret_cast<bf16_t*>(&T2[p * TROW + n * 2]), v);
+      }
+    }
+  }
+  __syncthreads();
+
+  // ======================= stage 3: y = GELU(W3 T2 + b3 + x)
+  {
+    constexpr int NJ = NT3 / 2;                       // 6 channel tiles per wave
+    f32x4 acc[NJ][2];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c3 = 0; c3 < KC3; ++c3) {
+      const int c = KC1 + KC2 + c3;
+      const int buf = c & 1;
+      uint4 bv[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int p = wm * 32 + i * 16 + fr;
+        bv[i] = *reinterpret_cast<const uint4*>(&T2[p * TROW + (c3 * 32 + fq * 8) * 2]);
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const uint4 a = wfrag32(buf, wn * NJ + j);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) mma_step<bf16_t>(acc[j][i], a, bv[i]);
+      }
+      store_w(c + 1, buf ^ 1);
+      load_w(c + PF + 1);
+      __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int p = wm * 32 + i * 16 + fr;
+      const int py = p >> 3, px = p & 7;
+      const long long pix = (long long)(b * args.H + y0 + py) * args.W + x0 + px;
+      const bf16_t* xr = g.x + pix * g.ldx;
+      bf16_t* orow = g.out + pix * g.ldo;
+      float res[NJ][4];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) Elem<bf16_t>::ld4(xr + (wn * NJ + j) * 16 + fq * 4, res[j]);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int n = (wn * NJ + j) * 16 + fq * 4;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = ru_gelu(acc[j][i][r] + g.b3[n + r] + res[j][r]);
+        Elem<bf16_t>::st4(orow + n, v);
+      }
+    }
+  }
+}
+
+}  // namespace rgbac
+
+using namespace rgbac;
+
+extern "C" int rgbac_residual_unit(const rgbac_ru_args* args, int ngroups, void* stream) {
+  RGBAC_REQUIRE(args != nullptr && ngroups >= 1 && ngroups <= kRuMaxGroups, "groups");
+  const rgbac_ru_args* a = args;
+  RGBAC_REQUIRE(a->dtype == RGBAC_BF16, "the fused residual unit is bf16 only");
+  RGBAC_REQUIRE(a->channels == 192, "fused residual unit supports C = 192");
+  RGBAC_REQUIRE(a->batch > 0 && a->h > 0 && a->w > 0 && a->h % 8 == 0 && a->w % 8 == 0,
+                "H and W must be positive multiples of 8");
+  RuArgsDev d{};
+  d.batch = a->batch; d.H = a->h; d.W = a->w; d.ngroups = ngroups;
+  for (int i = 0; i < ngroups; ++i) {
+    const rgbac_ru_args* q = &args[i];
+    RGBAC_REQUIRE(q->dtype == a->dtype && q->channels == a->channels && q->batch == a->batch &&
+                      q->h == a->h && q->w == a->w, "grouped units must share the geometry");
+    RGBAC_REQUIRE(q->x && q->out && q->w1 && q->w2 && q->w3 && q->b1 && q->b2 && q->b3,
+                  "null pointer");
+    RGBAC_REQUIRE(q->x != q->out, "out must not alias x (the halo is read by other tiles)");
+    RGBAC_REQUIRE(q->x_ldc >= 192 && q->x_ldc % 8 == 0 && q->out_ldc >= 192 && q->out_ldc % 4 == 0,
+                  "strides");
+    RGBAC_REQUIRE(q->w1_kpad >= 192 && q->w2_kpad >= 896 && q->w3_kpad >= 96 &&
+                      q->w1_kpad % 8 == 0 && q->w2_kpad % 8 == 0 && q->w3_kpad % 8 == 0,
+                  "packed weight k_pad (w1 >= 192, w2 >= 896 zero-padded, w3 >= 96)");
+    RGBAC_REQUIRE(((uintptr_t)q->x % 16) == 0 && ((uintptr_t)q->w1 % 16) == 0 &&
+                      ((uintptr_t)q->w2 % 16) == 0 && ((uintptr_t)q->w3 % 16) == 0,
+                  "16-byte alignment");
+    RuGroup& g = d.g[i];
+    g.x = (const bf16_t*)q->x; g.ldx = q->x_ldc;
+    g.w1 = (const bf16_t*)q->w1; g.w2 = (const bf16_t*)q->w2; g.w3 = (const bf16_t*)q->w3;
+    g.kp1 = q->w1_kpad; g.kp2 = q->w2_kpad; g.kp3 = q->w3_kpad;
+    g.b1 = q->b1; g.b2 = q->b2; g.b3 = q->b3;
+    g.out = (bf16_t*)q->out; g.ldo = q->out_ldc;
+  }
+  const long long tiles = (long long)a->batch * (a->h / 8) * (a->w / 8);
+  RGBAC_REQUIRE(tiles < (1ll << 31), "too many tiles");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL((ru_fused_kernel<192, 96>), dim3((unsigned)tiles, 1, ngroups), dim3(256), 0,
+                     st, d);
+  return check_launch("ru_fused_kernel");
+}

@@ -63,6 +63,19 @@ class WgradArgs(ctypes.Structure):
     ]
 
 
+class RuArgs(ctypes.Structure):
+    _fields_ = [
+        ("dtype", ctypes.c_int32), ("channels", ctypes.c_int32), ("batch", ctypes.c_int32),
+        ("h", ctypes.c_int32), ("w", ctypes.c_int32), ("_pad0", ctypes.c_int32),
+        ("x", ctypes.c_void_p), ("x_ldc", ctypes.c_int64),
+        ("w1", ctypes.c_void_p), ("w2", ctypes.c_void_p), ("w3", ctypes.c_void_p),
+        ("w1_kpad", ctypes.c_int32), ("w2_kpad", ctypes.c_int32), ("w3_kpad", ctypes.c_int32),
+        ("_pad1", ctypes.c_int32),
+        ("b1", ctypes.c_void_p), ("b2", ctypes.c_void_p), ("b3", ctypes.c_void_p),
+        ("out", ctypes.c_void_p), ("out_ldc", ctypes.c_int64),
+    ]
+
+
 _VP, _I32, _I64, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
 _D = ctypes.c_double
 # name -> argtypes (restype int unless noted); must match include/rgbac.h
@@ -84,6 +97,7 @@ SIGNATURES = {
     "rgbac_mask_pyramid": [_I32, _I32, _I32, _VP, _I32, _VP, _I32, _VP, _VP],
     "rgbac_nchw_to_nhwc": [_I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP],
     "rgbac_nhwc_to_nchw": [_I32, _I32, _I32, _I32, _I32, _VP, _I64, _VP, _VP],
+    "rgbac_residual_unit": [_VP, _I32, _VP],
     # training step
     "rgbac_act_bwd": [_I32, _I32, _F, _I64, _I32, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP,
                       _I64, _VP, _I64, _VP],

@@ -207,6 +207,22 @@ int rgbac_nhwc_to_nchw(int dtype, int batch, int c, int h, int w,
                        const void* src, int64_t ldc, float* dst, void* stream);
 
 
+/* Fused ResidualUnit (layers/Masked_Attention.py:150-169), bf16, C = 192:
+ *   out = GELU(W3 * GELU(W2 (*)3x3 GELU(W1 * x + b1) + b2) + b3 + x)
+ * W1/W2/W3 are rgbac_conv2d packed weights ([rows][k_pad], k = tap*cin + c;
+ * w2_kpad >= 896 zero-padded), biases fp32.  One 8x8 output tile per
+ * workgroup with both intermediates in LDS; up to 4 units of identical
+ * geometry per launch.  out must not alias x.                               */
+typedef struct rgbac_ru_args {
+  int32_t dtype, channels, batch, h, w, _pad0;
+  const void* x; int64_t x_ldc;
+  const void* w1; const void* w2; const void* w3;
+  int32_t w1_kpad, w2_kpad, w3_kpad, _pad1;
+  const float* b1; const float* b2; const float* b3;
+  void* out; int64_t out_ldc;
+} rgbac_ru_args;
+int rgbac_residual_unit(const rgbac_ru_args* args, int ngroups, void* stream);
+
 /* ====================================================================== *
  * Training step (trainRGB.py:178-198): backward kernels, optimizer.       *
  * The input gradient of a conv is rgbac_conv2d over a repacked weight      *

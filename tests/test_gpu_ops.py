@@ -298,3 +298,26 @@ def test_conv_small_k_tiles(device, dtype, tile):
             assert rel(rt.to_nchw(o), w_) < tol
     finally:
         rt.FORCE = None
+
+
+@pytest.mark.parametrize("H,W", [(16, 24), (64, 64)])
+def test_fused_residual_units(device, H, W):
+    """csrc/fused.hip (bf16, C=192): two ResidualUnits in one launch vs the three-launch
+    path and vs the oracle (masked_attention.py:150-169), incl. image-border halos."""
+    rt = _rt()
+    from rgbac.layers.Masked_Attention import (ResidualUnit, run_residual_units_fused,
+                                               run_residual_units_unfused)
+    g = _gen(300 + H)
+    us = [ResidualUnit(192) for _ in range(2)]
+    xs = [torch.randn((2, 192, H, W), generator=g) for _ in range(2)]
+    wants = [ref.residual_unit(x, {"u." + k: v for k, v in u.state_dict().items()}, "u")
+             for u, x in zip(us, xs)]
+    us = [u.to(device) for u in us]
+    with torch.no_grad():
+        fx = [rt.to_nhwc(x.to(device), torch.bfloat16) for x in xs]
+        fused = run_residual_units_fused(list(zip(us, fx)))
+        plain = run_residual_units_unfused(list(zip(us, fx)))
+    for f, p, w in zip(fused, plain, wants):
+        a, b = rt.to_nchw(f).cpu(), rt.to_nchw(p).cpu()
+        assert rel(a, b) < 2e-2
+        assert rel(a, w) < 3e-2

@@ -1,0 +1,39 @@
+"""Time the fused ResidualUnit kernel (csrc/fused.hip) on one shape (bench helper)."""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "deep-learning-based-rgba-image-compression-with-masked-window-based-attention_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--hw", type=int, default=64)
+    ap.add_argument("--groups", type=int, default=2)
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    from rgbac import runtime as rt
+    from rgbac.layers.Masked_Attention import ResidualUnit, run_residual_units_fused
+    dev = torch.device("cuda:0")
+    us = [ResidualUnit(192).to(dev) for _ in range(a.groups)]
+    xs = [rt.to_nhwc(torch.randn((a.batch, 192, a.hw, a.hw), device=dev), torch.bfloat16)
+          for _ in range(a.groups)]
+    with torch.no_grad():
+        run_residual_units_fused(list(zip(us, xs)))
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            run_residual_units_fused(list(zip(us, xs)))
+        e1.record()
+        e1.synchronize()
+    us_per = e0.elapsed_time(e1) / a.iters * 1e3
+    print(f"ru_fused g{a.groups} B{a.batch} {a.hw}x{a.hw}: {us_per:.1f} us")
+
+
+if __name__ == "__main__":
+    main()
