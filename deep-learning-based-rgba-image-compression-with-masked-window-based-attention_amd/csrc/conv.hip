@@ -870,6 +870,83 @@ __global__ void __launch_bounds__(256) conv_direct_kernel(const ConvArgsDev args
   }
 }
 
+// ---------------------------------------------------------------------------
+// Spatial-tile variant for 3x3 stride-1 convs with Cin = 32 and Cout <= 32
+// (the DSE EnhancementBlocks at full resolution): one workgroup per 16x16 output
+// tile stages its 18x18x32 input halo (20.7 KB) and the whole 32 x 288 weight
+// panel (18.4 KB) in LDS once, then each wave runs 4 rows x 2 channel tiles x
+// 9 taps = 72 MFMAs straight from LDS (the k-step of 32 channels is one tap).
+// Both LDS images use slot = chunk ^ ((row >> 1) & 3), conflict-free for the
+// ds_read_b128 lane groups of the fragment reads.  bf16 only.
+template <typename T>
+__global__ void __launch_bounds__(256) conv3x3_c32_kernel(const ConvArgsDev args) {
+  constexpr int TS = 16, HS = TS + 2, NH = HS * HS;
+  __shared__ __attribute__((aligned(16))) uint4 Xs[NH * 4];
+  __shared__ __attribute__((aligned(16))) uint4 Ws[32 * 36];
+  const ConvShared& s = args.s;
+  const ConvGroup& g = args.g[blockIdx.z];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int tx_n = s.Wm / TS, ty_n = s.Hm / TS;
+  int t = blockIdx.x;
+  const int tx = t % tx_n; t /= tx_n;
+  const int ty = t % ty_n;
+  const int b = t / ty_n;
+  const int y0 = ty * TS, x0 = tx * TS;
+  const T* wsrc = reinterpret_cast<const T*>(g.w);
+  for (int e = tid; e < 32 * 36; e += 256) {
+    const int r = e / 36, c = e - r * 36;
+    Ws[r * 36 + (c ^ ((r >> 1) & 3))] =
+        *reinterpret_cast<const uint4*>(wsrc + (size_t)r * g.k_pad + c * 8);
+  }
+  const T* xsrc = reinterpret_cast<const T*>(g.sp0);
+  for (int e = tid; e < NH * 4; e += 256) {
+    const int hr = e >> 2, c = e & 3;
+    const int hy = hr / HS, hx = hr - hy * HS;
+    const int iy = y0 + hy - 1, ix = x0 + hx - 1;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (iy >= 0 && iy < s.in_h && ix >= 0 && ix < s.in_w)
+      v = *reinterpret_cast<const uint4*>(xsrc + ((long long)(b * s.in_h + iy) * s.in_w + ix) * g.sld0 + c * 8);
+    if (s.square) v = square_chunk<T>(v);
+    Xs[hr * 4 + (c ^ ((hr >> 1) & 3))] = v;
+  }
+  __syncthreads();
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int dy = tap / 3, dx = tap % 3;
+    uint4 A[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = 16 * j + fr;
+      A[j] = Ws[r * 36 + ((4 * tap + fq) ^ ((r >> 1) & 3))];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int hr = (wave * 4 + i + dy) * HS + fr + dx;
+      const uint4 B = Xs[hr * 4 + (fq ^ ((hr >> 1) & 3))];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) mma_step<T>(acc[j][i], A[j], B);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = (b * s.Hm + y0 + wave * 4 + i) * s.Wm + x0 + fr;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = 16 * j + fq * 4;
+      if (n >= g.cout) continue;
+      float v[4] = {acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]};
+      epilogue4<T>(s, g, 0, m, n, v);
+    }
+  }
+}
+
 template <typename T, int NT>
 static void launch_direct(const ConvArgsDev& d, dim3 grid, int rs, int nks_max, hipStream_t st) {
   constexpr int NKS = 12;
@@ -883,17 +960,29 @@ struct TileCfg { int bm, bn; };
 static const TileCfg kTiles[] = {
     {128, 128}, {128, 64}, {64, 64}, {128, 32}, {64, 32}, {128, 16}, {64, 16},
     {128, 64}, {64, 64}, {128, 32}, {64, 32}, {128, 128}, {128, 16},
-    {16, 16}, {16, 32}, {16, 48}, {16, 64}, {16, 96}, {16, 192}};
+    {16, 16}, {16, 32}, {16, 48}, {16, 64}, {16, 96}, {16, 192},
+    {256, 32}};
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 constexpr int kFirstWres = 7;
 constexpr int kWresStages = 6;
 constexpr int kFirstDirect = 13;   // 13..18: direct kernel with NT = bn/16
 constexpr int kDirectSteps = 12;
+constexpr int kTileSpatial = 19;   // conv3x3_c32_kernel (16x16 pixels x 32 channels)
 
 template <typename T>
 static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t st) {
   const ConvShared& s = d.s;
   const TileCfg tc = kTiles[tile];
+  if (tile == kTileSpatial) {
+    if constexpr (sizeof(T) == 2) {
+      dim3 grid((unsigned)((long long)s.batch * (s.Hm / 16) * (s.Wm / 16)), 1, s.ngroups);
+      hipLaunchKernelGGL(conv3x3_c32_kernel<T>, grid, dim3(256), 0, st, d);
+      return check_launch("conv3x3_c32_kernel");
+    } else {
+      set_error("the spatial 3x3 tile is bf16 only");
+      return RGBAC_E_ARG;
+    }
+  }
   if (tile >= kFirstDirect) {
     const int ny = (max_cout + tc.bn - 1) / tc.bn;
     const int nz = s.ngroups;
@@ -1095,7 +1184,16 @@ extern "C" int rgbac_conv2d_grouped(const rgbac_conv_args* args, int ngroups, vo
   s.square = a->square_input;
   s.ksplit = a->ksplit;
   s.ngroups = ngroups;
-  if (a->tile >= kFirstDirect) {
+  if (a->tile == kTileSpatial) {
+    RGBAC_REQUIRE(a->dtype == RGBAC_BF16 && a->mode == RGBAC_CONV && a->ksize == 3 &&
+                      a->stride == 1 && a->ksplit == 1 && a->act != RGBAC_ACT_GAUSS &&
+                      s.Hm % 16 == 0 && s.Wm % 16 == 0,
+                  "the spatial 3x3 tile needs bf16, 3x3 stride 1, H/W multiples of 16, ksplit 1");
+    for (int i = 0; i < ngroups; ++i)
+      RGBAC_REQUIRE(args[i].nsrc == 1 && args[i].cin_pad == 32 && args[i].src[0].channels == 32 &&
+                        args[i].cout <= 32 && args[i].k_pad >= 288,
+                    "the spatial 3x3 tile needs one 32-channel source and cout <= 32");
+  } else if (a->tile >= kFirstDirect) {
     RGBAC_REQUIRE(a->mode == RGBAC_CONV && a->ksplit == 1 && a->act != RGBAC_ACT_GAUSS,
                   "direct tiles need a plain conv, ksplit 1 and no GAUSS epilogue");
     const int ks_elems = a->dtype == RGBAC_F32 ? 16 : 32;

@@ -84,12 +84,14 @@ def round_up(x, m):
 # stages of 64 bf16 / 32 f32 elements, ksplit 1).
 TILES = [(128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 16),
          (128, 64), (64, 64), (128, 32), (64, 32), (128, 128), (128, 16),
-         (16, 16), (16, 32), (16, 48), (16, 64), (16, 96), (16, 192)]
+         (16, 16), (16, 32), (16, 48), (16, 64), (16, 96), (16, 192),
+         (256, 32)]
 FIRST_WRES = 7
 WRES_STAGES = 6
 FIRST_DIRECT = 13        # 13..18: direct kernel (plain conv, K <= DIRECT_STEPS MFMA k-steps)
 DIRECT_STEPS = 12
 DIRECT_LDS = 65536       # weight panel bytes of a direct tile (dynamic LDS limit)
+TILE_SPATIAL = 19        # conv3x3_c32_kernel: 16x16-pixel tiles, 3x3 s1, Cin 32, Cout <= 32, bf16
 KSPLITS = (1, 2, 4, 8)
 TUNE = os.environ.get("RGBAC_TUNE", "1") != "0"
 # RGBAC_TILE_SET: "stream" (default: streaming K-ring tiles; the weight-resident and
@@ -104,12 +106,16 @@ def pick_cout_pad(cout):
     return round_up(cout, 128)
 
 
-def _candidates(M, cout, nst, nks=None, plain=True):
+def _candidates(M, cout, nst, nks=None, plain=True, spatial=False):
     """(tile, ksplit) pairs worth timing for an M-pixel, cout-channel conv with nst K-stages
-    (nks MFMA k-steps; ``plain`` = CONV mode)."""
+    (nks MFMA k-steps; ``plain`` = CONV mode; ``spatial`` = the 3x3/Cin-32 tile applies)."""
     out = []
     n16 = round_up(cout, 16)
     for t, (bm, bn) in enumerate(TILES):
+        if t == TILE_SPATIAL:
+            if spatial:
+                out.append((t, 1))
+            continue
         if TILE_SET == "stream" and t >= FIRST_WRES:
             continue
         if t >= FIRST_DIRECT:
@@ -377,6 +383,14 @@ def prepare(pk, srcs, out=None, out_coff=0, act="none", act_param=0.0, res0=None
     return pr
 
 
+def _spatial_ok(preps):
+    a = preps[0].a
+    return (a.dtype == _lib.BF16 and a.mode == CONV and a.ksize == 3 and a.stride == 1 and
+            a.in_h % 16 == 0 and a.in_w % 16 == 0 and a.act != ACT["gauss"] and
+            all(p.a.nsrc == 1 and p.a.cin_pad == 32 and p.a.src[0].channels == 32 and
+                p.a.cout <= 32 for p in preps))
+
+
 def _gauss_ok(t, cout):
     return TILES[t][1] >= cout
 
@@ -415,7 +429,7 @@ def launch(preps):
             cands = [(t, 1) for t in range(FIRST_WRES) if _gauss_ok(t, cout)]
         else:
             cands = _candidates(mtot, cout, nst, max(pr.nks for pr in preps),
-                                p0.pk.mode == CONV)
+                                p0.pk.mode == CONV, _spatial_ok(preps))
         if TUNE and not torch.cuda.is_current_stream_capturing():
             best = None
             for cand in cands:
@@ -445,7 +459,8 @@ def launch(preps):
         run()
     else:
         bm, bn = TILES[choice[0]]
-        kname = ("conv_direct_kernel" if choice[0] >= FIRST_DIRECT else
+        kname = ("conv3x3_c32_kernel" if choice[0] == TILE_SPATIAL else
+                 "conv_direct_kernel" if choice[0] >= FIRST_DIRECT else
                  "conv_wres_kernel" if choice[0] >= FIRST_WRES else "conv_kernel")
         name = f"{kname}<{'f32' if p0.a.dtype == 0 else 'bf16'},{bm}x{bn}>"
         desc = f"{name} ks{choice[1]} g{n} {p0.desc}"

@@ -321,3 +321,28 @@ def test_fused_residual_units(device, H, W):
         a, b = rt.to_nchw(f).cpu(), rt.to_nchw(p).cpu()
         assert rel(a, b) < 2e-2
         assert rel(a, w) < 3e-2
+
+
+@pytest.mark.parametrize("cout,act", [(32, "relu"), (32, "none"), (24, "gelu")])
+def test_conv_spatial_tile(device, cout, act):
+    """conv3x3_c32_kernel (rt.TILE_SPATIAL): 16x16-pixel tiles with the input halo and the
+    weight panel in LDS; bf16; with pre/post residual epilogues like the DSE blocks."""
+    rt = _rt()
+    from rgbac.layers.TransformRGB import run_conv
+    g = _gen(400 + cout)
+    m = nn.Conv2d(32, cout, 3, padding=1)
+    x = torch.randn((2, 32, 32, 48), generator=g)
+    r0 = torch.randn((2, cout, 32, 48), generator=g)
+    r2 = torch.randn((2, cout, 32, 48), generator=g)
+    v = m(x) + r0
+    want = {"relu": F.relu, "gelu": F.gelu, "none": lambda t: t}[act](v) + r2
+    rt.FORCE = (rt.TILE_SPATIAL, 1)
+    try:
+        with torch.no_grad():
+            fx = rt.to_nhwc(x.to(device), torch.bfloat16)
+            f0 = rt.to_nhwc(r0.to(device), torch.bfloat16)
+            f2 = rt.to_nhwc(r2.to(device), torch.bfloat16)
+            got = rt.to_nchw(run_conv(m.to(device), [fx.src()], act=act, res0=f0, res2=f2))
+    finally:
+        rt.FORCE = None
+    assert rel(got, want) < 2e-2
