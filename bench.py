@@ -52,6 +52,13 @@ def synth_inputs(B, H, W, seed=0):
     return torch.where(a > 0, rgb, a), a
 
 
+# Attribution runs enqueue one eager step behind a GPU spin (torch.cuda._sleep, in clock
+# cycles) long enough for the host to queue every launch first, so the per-launch HIP-event
+# intervals measure back-to-back GPU execution as in the graph replay, not host launch gaps.
+SPIN_FWD = 150_000_000
+SPIN_TRAIN = 600_000_000
+
+
 def cpu_baseline(budget_s):
     """Oracle (CPU fp32 restatement) on 1 image of the same workload, this host's cores."""
     from oracle import ref_model as ref
@@ -180,6 +187,7 @@ def main_train(args, world, rank, dev, dist):
         prof = rt.LaunchProfiler()
         rt.PROFILER = prof
         for _ in range(2):
+            torch.cuda._sleep(SPIN_TRAIN)   # queue the whole step behind a spin: GPU-side times
             step()
         rt.PROFILER = None
         summ = prof.summary()
@@ -303,7 +311,9 @@ def main():
         prof = rt.LaunchProfiler()
         rt.PROFILER = prof
         for _ in range(3):
+            torch.cuda._sleep(SPIN_FWD)     # queue the whole step behind a spin: GPU-side times
             step()
+            torch.cuda.synchronize()
         rt.PROFILER = None
         summ = prof.summary()
         if args.layers:

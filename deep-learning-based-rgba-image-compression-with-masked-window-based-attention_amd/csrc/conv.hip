@@ -34,6 +34,8 @@
 // group, split, phase).  The model uses it for the cc_mean/cc_scale stacks,
 // the conv_a/conv_b residual units and h_mean_s/h_scale_s, which are
 // independent chains of identical shape.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace rgbac {
@@ -65,6 +67,7 @@ struct ConvShared {
   int ksize, pad;
   int act; float act_param; int square;
   int ksplit, nphase, ngroups;
+  int remap;                        // 1: XCD-aware block order (env RGBAC_XCD_REMAP=0 disables)
 };
 
 struct ConvArgsDev {
@@ -367,6 +370,20 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+struct KDec { int ci, tap, ty, tx; };      // a lane's (channel, tap) position in K
+
+// Retire the oldest ring stage when `after` stages (LW DMA pieces each) were issued
+// behind it: vmcnt(LW * min(after, D)), D = the ring's steady-state look-ahead.
+template <int LW, int D>
+__device__ __forceinline__ void wait_ring(int after) {
+  if constexpr (D <= 0) {
+    wait_vm<0>();
+  } else {
+    if (after >= D) wait_vm<LW * D>();
+    else wait_ring<LW, D - 1>(after);
+  }
+}
+
 // BM x BN tile, 4 waves laid out WGM (along m) x WGN (along n), NBUF-stage ring.
 template <typename T, int BM, int BN, int WGM, int WGN, int NBUF>
 __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
@@ -386,12 +403,33 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
   const ConvShared& s = args.s;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int zz = blockIdx.z;
-  const int phase = zz % s.nphase;
-  const int split = (zz / s.nphase) % s.ksplit;
-  const int gi = zz / (s.nphase * s.ksplit);
+  // Block order.  The dispatcher deals consecutive workgroup ids round-robin to the
+  // 8 XCDs (each with its own 4 MiB L2); with remap, XCD x gets one contiguous run of
+  // (group, split, M-tile, phase, N-tile) ids, N fastest, so the N-tiles and phases
+  // sharing an M-tile's im2col rows -- and neighbouring M-tiles sharing halo rows --
+  // run on the same L2 (bijective for any grid size).
+  int mblk, nblk, phase, split, gi;
+  {
+    const int Mb = gridDim.x, Nb = gridDim.y;
+    const int lin = blockIdx.x + Mb * (blockIdx.y + Nb * blockIdx.z);
+    int t;
+    if (s.remap) {
+      const int nwg = Mb * Nb * gridDim.z;
+      const int xcd = lin & 7, q = nwg >> 3, r = nwg & 7;
+      t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (lin >> 3);
+      nblk = t % Nb; t /= Nb;
+      phase = t % s.nphase; t /= s.nphase;
+      mblk = t % Mb; t /= Mb;
+    } else {
+      mblk = blockIdx.x; nblk = blockIdx.y;
+      t = blockIdx.z;
+      phase = t % s.nphase; t /= s.nphase;
+    }
+    split = t % s.ksplit;
+    gi = t / s.ksplit;
+  }
   const ConvGroup& g = args.g[gi];
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const int m0 = mblk * BM, n0 = nblk * BN;
   if (n0 >= g.cout) return;                    // groups may differ in cout
   const int py = phase >> 1, px = phase & 1;
   int ntaps, tw;
@@ -408,12 +446,24 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
   const int s_end = (int)((long long)nst * (split + 1) / s.ksplit);
   const int ns = s_end - s_beg;
 
+  // Kernel arguments the K loop reads, held in registers: the DMA statement clobbers
+  // "memory", which would otherwise force a scalar reload of every field per stage.
+  const int in_h = s.in_h, in_w = s.in_w, cin_pad = g.cin_pad, Mtot = s.M;
+  const int send0 = g.send0, send1 = g.send1, send2 = g.send2;
+  const char* const sp0 = reinterpret_cast<const char*>(g.sp0);
+  const char* const sp1 = reinterpret_cast<const char*>(g.sp1);
+  const char* const sp2 = reinterpret_cast<const char*>(g.sp2);
+  const int sld0 = (int)g.sld0, sld1 = (int)g.sld1, sld2 = (int)g.sld2;
+  const bool convt = s.mode == RGBAC_CONVT_S2;
+  const int pad = s.pad;
+  const bool sq_in = s.square != 0;
+
   // ---- per-lane DMA assignment: piece j = wave + 4*i; lane -> row (lane>>3),
   //      source chunk c = (lane&7) ^ (lane>>3) so LDS slot (lane&7) holds chunk c.
   const int lrow = lane >> 3;
   const int c = (lane & 7) ^ lrow;
   const T* wrow[LW];
-  int bb[LW], biy[LW], bix[LW];
+  int pbase[LW], biy[LW], bix[LW];
   bool isA[LW], bval[LW];
   int lofs[LW];                                 // uint4 offset of the piece in a stage
   const T* wbase = reinterpret_cast<const T*>(g.w) + (size_t)phase * g.rows * g.k_pad;
@@ -426,64 +476,23 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
     const int arow = 8 * j + lrow;
     wrow[i] = wbase + (size_t)(n0 + (isA[i] ? arow : 0)) * g.k_pad + c * EPV;
     const int m = m0 + 8 * (j - IA) + lrow;
-    bval[i] = !isA[i] && m < s.M;
+    bval[i] = !isA[i] && m < Mtot;
     const int mm = bval[i] ? m : 0;
     const int t = udiv(mm, s.Wm, s.rWm);
     const int mx = mm - t * s.Wm;
-    bb[i] = udiv(t, s.Hm, s.rHm);
-    biy[i] = (t - bb[i] * s.Hm) * s.sy;
+    const int b = udiv(t, s.Hm, s.rHm);
+    biy[i] = (t - b * s.Hm) * s.sy;
     bix[i] = mx * s.sy;
+    pbase[i] = (b * in_h + biy[i]) * in_w + bix[i];   // input pixel of tap offset (0, 0)
   }
 
   // ---- incremental k -> (tap, ci) decode for this lane's chunk
   const int k0 = s_beg * KS + c * EPV;
-  int tap = k0 / g.cin_pad;
-  int ci = k0 - tap * g.cin_pad;
-  int ty = tap / tw, tx = tap - (tap / tw) * tw;
-
-  auto issue = [&](int st_local, int buf) {
-    int dy, dx;
-    if (s.mode == RGBAC_CONVT_S2) {
-      dy = 1 - ty; dx = 1 - tx;
-    } else {
-      dy = ty - s.pad; dx = tx - s.pad;
-    }
-    const void* sp;
-    long long sld;
-    int cs;
-    bool kval = tap < ntaps;
-    if (ci < g.send0) {
-      sp = g.sp0; sld = g.sld0; cs = ci;
-    } else if (ci < g.send1) {
-      sp = g.sp1; sld = g.sld1; cs = ci - g.send0;
-    } else {
-      sp = g.sp2; sld = g.sld2; cs = ci - g.send1;
-      kval = kval && ci < g.send2;
-    }
-    const T* src = reinterpret_cast<const T*>(sp);
-    const int kk = (s_beg + st_local) * KS;
-    uint4* stage = smem + buf * STAGE;
-#pragma unroll
-    for (int i = 0; i < LW; ++i) {
-      const void* gp;
-      if (isA[i]) {
-        gp = wrow[i] + kk;
-      } else {
-        const int iy = biy[i] + dy, ix = bix[i] + dx;
-        const bool ok = kval && bval[i] && iy >= 0 && iy < s.in_h && ix >= 0 && ix < s.in_w;
-        gp = ok ? (const void*)(src + ((long long)(bb[i] * s.in_h + iy) * s.in_w + ix) * sld + cs)
-                : (const void*)g_zero_page;
-      }
-      dma16(gp, stage + lofs[i]);
-    }
-    // advance this lane's decode to the next stage
-    ci += KS;
-    while (ci >= g.cin_pad) {
-      ci -= g.cin_pad;
-      ++tap;
-      if (++tx == tw) { tx = 0; ++ty; }
-    }
-  };
+  KDec dec;
+  dec.tap = k0 / cin_pad;
+  dec.ci = k0 - dec.tap * cin_pad;
+  dec.ty = dec.tap / tw;
+  dec.tx = dec.tap - dec.ty * tw;
 
   f32x4 acc[TN][TM];
 #pragma unroll
@@ -494,21 +503,60 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
   const int wm = wave % WGM, wn = wave / WGM;
   const int fr = lane & 15, fq = lane >> 4, sw = lane & 7;
 
+  // Staging code for stage `st_issue` (used by the prologue and the steady-state loop).
+  // A macro, not a lambda: captured locals would be address-taken, and the DMA
+  // statement's "memory" clobber then pins them -- and the source-pointer select --
+  // to scratch; and a merged prologue/steady-state loop makes the accumulators a
+  // loop-carried VGPR/AGPR copy pair.
+#define CONV_ISSUE_STAGE(st_issue)                                                            \
+  do {                                                                                        \
+    /* branch-free per-lane addressing: source select, bounds and zero page by */             \
+    /* v_cndmask; 32-bit element offsets (the host bounds every source below 2 GiB) */        \
+    const int dy = convt ? 1 - dec.ty : dec.ty - pad;                                         \
+    const int dx = convt ? 1 - dec.tx : dec.tx - pad;                                         \
+    const int ci = dec.ci;                                                                    \
+    const bool in0 = ci < send0, in1 = ci < send1;                                            \
+    const char* src = in0 ? sp0 : (in1 ? sp1 : sp2);                                          \
+    const int sld = in0 ? sld0 : (in1 ? sld1 : sld2);                                         \
+    const int cs = ci - (in0 ? 0 : (in1 ? send0 : send1));                                    \
+    const bool kval = (dec.tap < ntaps) & (ci < send2);                                       \
+    const int doff = dy * in_w + dx;                                                          \
+    const int kk = (s_beg + (st_issue)) * KS;                                                 \
+    uint4* stage = smem + ((st_issue) % NBUF) * STAGE;                                        \
+_Pragma("unroll")                                                                             \
+    for (int i = 0; i < LW; ++i) {                                                            \
+      const void* gp;                                                                         \
+      if (isA[i]) {                                                                           \
+        gp = wrow[i] + kk;                                                                    \
+      } else {                                                                                \
+        const int iy = biy[i] + dy, ix = bix[i] + dx;                                         \
+        const bool ok = kval & bval[i] & ((unsigned)iy < (unsigned)in_h) &                    \
+                        ((unsigned)ix < (unsigned)in_w);                                      \
+        const unsigned off = ((unsigned)((pbase[i] + doff) * sld + cs)) * (unsigned)sizeof(T); \
+        gp = ok ? (const void*)(src + off) : (const void*)g_zero_page;                        \
+      }                                                                                       \
+      dma16(gp, stage + lofs[i]);                                                             \
+    }                                                                                         \
+    /* advance this lane's decode to the next stage */                                        \
+    dec.ci += KS;                                                                             \
+    while (dec.ci >= cin_pad) {                                                               \
+      dec.ci -= cin_pad;                                                                      \
+      ++dec.tap;                                                                              \
+      if (++dec.tx == tw) { dec.tx = 0; ++dec.ty; }                                           \
+    }                                                                                         \
+  } while (0)
+
 #pragma unroll
   for (int st = 0; st < NBUF - 1; ++st)
-    if (st < ns) issue(st, st);
+    if (st < ns) CONV_ISSUE_STAGE(st);
 
   for (int it = 0; it < ns; ++it) {
     // retire stage `it`: leave the stages issued after it in flight
-    if constexpr (NBUF >= 3) {
-      if (it + 1 < ns) wait_vm<LW * (NBUF - 2)>(); else wait_vm<0>();
-    } else {
-      wait_vm<0>();
-    }
+    wait_ring<LW, NBUF - 2>(ns - 1 - it);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (it + NBUF - 1 < ns) issue(it + NBUF - 1, (it + NBUF - 1) % NBUF);
+    if (it + NBUF - 1 < ns) CONV_ISSUE_STAGE(it + NBUF - 1);
     const uint4* As = smem + (it % NBUF) * STAGE;
     const uint4* Bs = As + BN * 8;
 #pragma unroll
@@ -520,7 +568,7 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         b[i] = Bs[(wm * TM * 16 + i * 16 + fr) * 8 + chunk];
-        if (s.square) b[i] = square_chunk<T>(b[i]);
+        if (sq_in) b[i] = square_chunk<T>(b[i]);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j)
@@ -528,6 +576,8 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
         for (int i = 0; i < TM; ++i) mma_step<T>(acc[j][i], a[j], b[i]);
     }
   }
+
+#undef CONV_ISSUE_STAGE
 
   if (s.act == RGBAC_ACT_GAUSS) {
     // (mu | sigma) tile -> LDS [BM][BN] fp32, then one (pixel, channel) per thread
@@ -554,7 +604,7 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
                                                  tilef[ml * BN + nch + ch]);
     }
     const double tot = block_sum_f64(bits, red);
-    if (tid == 0) g.partial[blockIdx.x] = tot;
+    if (tid == 0) g.partial[mblk] = tot;
     return;
   }
 
@@ -961,13 +1011,16 @@ static const TileCfg kTiles[] = {
     {128, 128}, {128, 64}, {64, 64}, {128, 32}, {64, 32}, {128, 16}, {64, 16},
     {128, 64}, {64, 64}, {128, 32}, {64, 32}, {128, 128}, {128, 16},
     {16, 16}, {16, 32}, {16, 48}, {16, 64}, {16, 96}, {16, 192},
-    {256, 32}};
+    {256, 32},
+    // 20..26: the streaming shapes of 0..6 with a deeper LDS ring (more K stages in flight)
+    {128, 128}, {128, 64}, {64, 64}, {128, 32}, {64, 32}, {128, 16}, {64, 16}};
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 constexpr int kFirstWres = 7;
 constexpr int kWresStages = 6;
 constexpr int kFirstDirect = 13;   // 13..18: direct kernel with NT = bn/16
 constexpr int kDirectSteps = 12;
 constexpr int kTileSpatial = 19;   // conv3x3_c32_kernel (16x16 pixels x 32 channels)
+constexpr int kFirstDeep = 20;     // 20..26: deep-ring streaming tiles
 
 template <typename T>
 static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t st) {
@@ -983,7 +1036,7 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
       return RGBAC_E_ARG;
     }
   }
-  if (tile >= kFirstDirect) {
+  if (tile >= kFirstDirect && tile < kFirstDeep) {
     const int ny = (max_cout + tc.bn - 1) / tc.bn;
     const int nz = s.ngroups;
     const int ntile = (s.M + 15) / 16;
@@ -1012,7 +1065,7 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
     }
     return check_launch("conv_direct_kernel");
   }
-  if (tile >= kFirstWres) {
+  if (tile >= kFirstWres && tile < kFirstDeep) {
     const int mtiles = (s.M + tc.bm - 1) / tc.bm;
     const int ny = (max_cout + tc.bn - 1) / tc.bn;
     const int nz = s.nphase * s.ngroups;
@@ -1040,7 +1093,14 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
     case 3: hipLaunchKernelGGL((conv_kernel<T, 128, 32, 4, 1, 3>), grid, dim3(256), 0, st, d); break;
     case 4: hipLaunchKernelGGL((conv_kernel<T, 64, 32, 2, 2, 3>), grid, dim3(256), 0, st, d); break;
     case 5: hipLaunchKernelGGL((conv_kernel<T, 128, 16, 4, 1, 3>), grid, dim3(256), 0, st, d); break;
-    default: hipLaunchKernelGGL((conv_kernel<T, 64, 16, 4, 1, 3>), grid, dim3(256), 0, st, d); break;
+    case 6: hipLaunchKernelGGL((conv_kernel<T, 64, 16, 4, 1, 3>), grid, dim3(256), 0, st, d); break;
+    case 20: hipLaunchKernelGGL((conv_kernel<T, 128, 128, 2, 2, 4>), grid, dim3(256), 0, st, d); break;
+    case 21: hipLaunchKernelGGL((conv_kernel<T, 128, 64, 4, 1, 5>), grid, dim3(256), 0, st, d); break;
+    case 22: hipLaunchKernelGGL((conv_kernel<T, 64, 64, 2, 2, 6>), grid, dim3(256), 0, st, d); break;
+    case 23: hipLaunchKernelGGL((conv_kernel<T, 128, 32, 4, 1, 6>), grid, dim3(256), 0, st, d); break;
+    case 24: hipLaunchKernelGGL((conv_kernel<T, 64, 32, 2, 2, 8>), grid, dim3(256), 0, st, d); break;
+    case 25: hipLaunchKernelGGL((conv_kernel<T, 128, 16, 4, 1, 6>), grid, dim3(256), 0, st, d); break;
+    default: hipLaunchKernelGGL((conv_kernel<T, 64, 16, 4, 1, 8>), grid, dim3(256), 0, st, d); break;
   }
   int rc = check_launch("conv_kernel");
   if (rc || s.ksplit == 1) return rc;
@@ -1184,6 +1244,11 @@ extern "C" int rgbac_conv2d_grouped(const rgbac_conv_args* args, int ngroups, vo
   s.square = a->square_input;
   s.ksplit = a->ksplit;
   s.ngroups = ngroups;
+  static const int remap_env = [] {
+    const char* e = getenv("RGBAC_XCD_REMAP");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  s.remap = remap_env;
   if (a->tile == kTileSpatial) {
     RGBAC_REQUIRE(a->dtype == RGBAC_BF16 && a->mode == RGBAC_CONV && a->ksize == 3 &&
                       a->stride == 1 && a->ksplit == 1 && a->act != RGBAC_ACT_GAUSS &&
@@ -1193,14 +1258,14 @@ extern "C" int rgbac_conv2d_grouped(const rgbac_conv_args* args, int ngroups, vo
       RGBAC_REQUIRE(args[i].nsrc == 1 && args[i].cin_pad == 32 && args[i].src[0].channels == 32 &&
                         args[i].cout <= 32 && args[i].k_pad >= 288,
                     "the spatial 3x3 tile needs one 32-channel source and cout <= 32");
-  } else if (a->tile >= kFirstDirect) {
+  } else if (a->tile >= kFirstDirect && a->tile < kFirstDeep) {
     RGBAC_REQUIRE(a->mode == RGBAC_CONV && a->ksplit == 1 && a->act != RGBAC_ACT_GAUSS,
                   "direct tiles need a plain conv, ksplit 1 and no GAUSS epilogue");
     const int ks_elems = a->dtype == RGBAC_F32 ? 16 : 32;
     for (int i = 0; i < ngroups; ++i)
       RGBAC_REQUIRE((ntaps_max * args[i].cin_pad + ks_elems - 1) / ks_elems <= kDirectSteps,
                     "K too large for a direct tile");
-  } else if (a->tile >= kFirstWres) {
+  } else if (a->tile >= kFirstWres && a->tile < kFirstDeep) {
     RGBAC_REQUIRE(a->ksplit == 1 && a->act != RGBAC_ACT_GAUSS,
                   "weight-resident tiles need ksplit 1 and no GAUSS epilogue");
     const int ks_elems = a->dtype == RGBAC_F32 ? 32 : 64;
@@ -1221,6 +1286,10 @@ extern "C" int rgbac_conv2d_grouped(const rgbac_conv_args* args, int ngroups, vo
                     "GAUSS needs (mu|sigma) channels in one N tile");
       RGBAC_REQUIRE(b->partial, "GAUSS needs a partial-sum buffer");
     }
+    for (int j = 0; j < b->nsrc; ++j)
+      RGBAC_REQUIRE((long long)a->batch * a->in_h * a->in_w * b->src[j].ldc *
+                            (a->dtype == RGBAC_F32 ? 4 : 2) < (1ll << 31),
+                    "each conv source must span < 2 GiB (32-bit gather offsets)");
     int rc = fill_group(b, ntaps_max, d.g[i]);
     if (rc) return rc;
     if (b->cout > max_cout) max_cout = b->cout;

@@ -85,13 +85,16 @@ def round_up(x, m):
 TILES = [(128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 16),
          (128, 64), (64, 64), (128, 32), (64, 32), (128, 128), (128, 16),
          (16, 16), (16, 32), (16, 48), (16, 64), (16, 96), (16, 192),
-         (256, 32)]
+         (256, 32),
+         (128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 16)]
 FIRST_WRES = 7
 WRES_STAGES = 6
 FIRST_DIRECT = 13        # 13..18: direct kernel (plain conv, K <= DIRECT_STEPS MFMA k-steps)
 DIRECT_STEPS = 12
 DIRECT_LDS = 65536       # weight panel bytes of a direct tile (dynamic LDS limit)
 TILE_SPATIAL = 19        # conv3x3_c32_kernel: 16x16-pixel tiles, 3x3 s1, Cin 32, Cout <= 32, bf16
+FIRST_DEEP = 20          # 20..26: tiles 0..6 with a deeper LDS ring (4..8 K stages)
+STREAM_TILES = tuple(range(FIRST_WRES)) + tuple(range(FIRST_DEEP, FIRST_DEEP + 7))
 KSPLITS = (1, 2, 4, 8)
 TUNE = os.environ.get("RGBAC_TUNE", "1") != "0"
 # RGBAC_TILE_SET: "stream" (default: streaming K-ring tiles; the weight-resident and
@@ -116,16 +119,16 @@ def _candidates(M, cout, nst, nks=None, plain=True, spatial=False):
             if spatial:
                 out.append((t, 1))
             continue
-        if TILE_SET == "stream" and t >= FIRST_WRES:
+        if TILE_SET == "stream" and t not in STREAM_TILES:
             continue
-        if t >= FIRST_DIRECT:
+        if FIRST_DIRECT <= t < FIRST_DEEP:
             if plain and nks is not None and nks <= DIRECT_STEPS and bn >= n16 / 4 \
                     and bn < 2 * n16 + 16 and bn * (4 * nks + 1) * 16 <= DIRECT_LDS:
                 out.append((t, 1))
             continue
         if bn > 16 and bn > 2 * n16:
             continue
-        if t >= FIRST_WRES:
+        if FIRST_WRES <= t < FIRST_DIRECT:
             if nst <= WRES_STAGES:
                 out.append((t, 1))
             continue
@@ -426,7 +429,7 @@ def launch(preps):
         cout = max(pr.pk.cout for pr in preps)
         nst = max(pr.nst for pr in preps)
         if gauss:
-            cands = [(t, 1) for t in range(FIRST_WRES) if _gauss_ok(t, cout)]
+            cands = [(t, 1) for t in STREAM_TILES if _gauss_ok(t, cout)]
         else:
             cands = _candidates(mtot, cout, nst, max(pr.nks for pr in preps),
                                 p0.pk.mode == CONV, _spatial_ok(preps))
@@ -452,7 +455,7 @@ def launch(preps):
             choice = _heuristic(mtot, cout, nst)
         _tune_cache[key] = choice
     if gauss and not _gauss_ok(choice[0], max(pr.pk.cout for pr in preps)):
-        choice = (min((t for t in range(FIRST_WRES) if _gauss_ok(t, p0.pk.cout)),
+        choice = (min((t for t in STREAM_TILES if _gauss_ok(t, p0.pk.cout)),
                       key=lambda t: TILES[t][1]), 1)
     set_choice(*choice)
     if PROFILER is None:
@@ -460,8 +463,8 @@ def launch(preps):
     else:
         bm, bn = TILES[choice[0]]
         kname = ("conv3x3_c32_kernel" if choice[0] == TILE_SPATIAL else
-                 "conv_direct_kernel" if choice[0] >= FIRST_DIRECT else
-                 "conv_wres_kernel" if choice[0] >= FIRST_WRES else "conv_kernel")
+                 "conv_direct_kernel" if FIRST_DIRECT <= choice[0] < FIRST_DEEP else
+                 "conv_wres_kernel" if FIRST_WRES <= choice[0] < FIRST_DIRECT else "conv_kernel")
         name = f"{kname}<{'f32' if p0.a.dtype == 0 else 'bf16'},{bm}x{bn}>"
         desc = f"{name} ks{choice[1]} g{n} {p0.desc}"
         PROFILER.wrap(name, sum(pr.flops for pr in preps), sum(pr.nbytes for pr in preps),

@@ -214,7 +214,7 @@ def test_mask_pyramid(device):
 
 # ------------------------------------------------------------------ every tile x split-K
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("tile", range(7))
+@pytest.mark.parametrize("tile", list(range(7)) + list(range(20, 27)))
 @pytest.mark.parametrize("ksplit", [1, 3])
 def test_conv_tiles_and_splitk(device, dtype, tile, ksplit):
     """Every tile shape and split-K path against PyTorch, on conv / convT / 3 sources."""
