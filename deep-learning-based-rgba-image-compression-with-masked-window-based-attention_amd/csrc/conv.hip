@@ -129,6 +129,10 @@ __device__ __forceinline__ void load_res(const void* ptr, long long ld, long lon
   }
 }
 
+template <typename T>
+__device__ __forceinline__ void epilogue4_body(const ConvShared& s, const ConvGroup& g,
+                                               long long opix, int n, float (&v)[4]);
+
 // Bias + fused epilogue + store of channels n..n+3 of M-grid pixel m (phase ph).
 template <typename T>
 __device__ __forceinline__ void epilogue4(const ConvShared& s, const ConvGroup& g, int ph, int m,
@@ -137,10 +141,10 @@ __device__ __forceinline__ void epilogue4(const ConvShared& s, const ConvGroup& 
   const int mx = m - t * s.Wm;
   const int b = udiv(t, s.Hm, s.rHm);
   const int my = t - b * s.Hm;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] += (g.bias ? g.bias[n + r] : 0.0f);
   T* out = reinterpret_cast<T*>(g.out);
   if (s.mode == RGBAC_SUBPEL2) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += (g.bias ? g.bias[n + r] : 0.0f);
     // conv channel n+r = 4*cc + 2*ii + jj -> pixel (2my+ii, 2mx+jj), channel cc
     const int cc = n >> 2;
 #pragma unroll
@@ -159,10 +163,57 @@ __device__ __forceinline__ void epilogue4(const ConvShared& s, const ConvGroup& 
     opix = (long long)(b * s.out_h + 2 * my + (ph >> 1)) * s.out_w + 2 * mx + (ph & 1);
   else
     opix = (long long)(b * s.out_h + my) * s.out_w + mx;
-  float r0[4] = {0.f, 0.f, 0.f, 0.f};
-  if (g.res0) load_res<T>(g.res0, g.ld0, opix, n, g.cout, r0);
-  float r1[4] = {0.f, 0.f, 0.f, 0.f};
-  if (g.res1) load_res<T>(g.res1, g.ld1, opix, n, g.cout, r1);
+  epilogue4_body<T>(s, g, opix, n, v);
+}
+
+// Same for a stride-1 CONV whose output grid is the M grid (output pixel = m).
+template <typename T>
+__device__ __forceinline__ void epilogue4_at(const ConvShared& s, const ConvGroup& g, int m, int n,
+                                             float (&v)[4]) {
+  epilogue4_body<T>(s, g, (long long)m, n, v);
+}
+
+// Operands the epilogue reads from memory, loaded ahead of the math so several quads'
+// loads can be in flight together (EpiIn::load, then epilogue4_fin).
+struct EpiIn {
+  float r0[4], r1[4], r2[4];
+  bool on;
+  template <typename T>
+  __device__ __forceinline__ void load(const ConvGroup& g, int act, long long opix, int n) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { r0[r] = 0.f; r1[r] = 0.f; r2[r] = 0.f; }
+    if (g.res0) load_res<T>(g.res0, g.ld0, opix, n, g.cout, r0);
+    if (g.res1) load_res<T>(g.res1, g.ld1, opix, n, g.cout, r1);
+    if (g.res2) load_res<T>(g.res2, g.ld2, opix, n, g.cout, r2);
+    on = act == RGBAC_ACT_MASKSEL ? g.sel[opix] != 0 : true;
+  }
+};
+
+template <typename T>
+__device__ __forceinline__ void epilogue4_fin(const ConvShared& s, const ConvGroup& g,
+                                              long long opix, int n, float (&v)[4],
+                                              const float (&bias)[4], const EpiIn& in);
+
+template <typename T>
+__device__ __forceinline__ void epilogue4_body(const ConvShared& s, const ConvGroup& g,
+                                               long long opix, int n, float (&v)[4]) {
+  EpiIn in;
+  in.template load<T>(g, s.act, opix, n);
+  float bias[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) bias[r] = g.bias ? g.bias[n + r] : 0.0f;
+  epilogue4_fin<T>(s, g, opix, n, v, bias, in);
+}
+
+template <typename T>
+__device__ __forceinline__ void epilogue4_fin(const ConvShared& s, const ConvGroup& g,
+                                              long long opix, int n, float (&v)[4],
+                                              const float (&bias)[4], const EpiIn& in) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] += bias[r];
+  T* out = reinterpret_cast<T*>(g.out);
+  const float (&r0)[4] = in.r0;
+  const float (&r1)[4] = in.r1;
 #pragma unroll
   for (int r = 0; r < 4; ++r)
     v[r] = s.act == RGBAC_ACT_SQBWD ? r0[r] + 2.0f * r1[r] * v[r] : v[r] + r0[r];
@@ -206,19 +257,16 @@ __device__ __forceinline__ void epilogue4(const ConvShared& s, const ConvGroup& 
       for (int r = 0; r < 4; ++r) v[r] = r1[r] * sqrtf(v[r]);
       break;
     case RGBAC_ACT_MASKSEL: {
-      const bool on = g.sel[opix] != 0;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = on ? r1[r] + v[r] : r1[r];
+      for (int r = 0; r < 4; ++r) v[r] = in.on ? r1[r] + v[r] : r1[r];
       break;
     }
     default:
       break;
   }
   if (g.res2) {
-    float r2[4];
-    load_res<T>(g.res2, g.ld2, opix, n, g.cout, r2);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] += r2[r];
+    for (int r = 0; r < 4; ++r) v[r] += in.r2[r];
   }
   const long long base = opix * g.out_ldc + g.out_coff + n;
   if (n + 3 < g.cout) {
@@ -227,6 +275,46 @@ __device__ __forceinline__ void epilogue4(const ConvShared& s, const ConvGroup& 
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       if (n + r < g.cout) Elem<T>::st(out + base + r, v[r]);
+  }
+}
+
+// conv_kernel epilogue of accumulator row i (pixel m, channels nn[j]..+3 for j < TN):
+// every residual load of the row is issued before any math/store.
+template <typename T, int TN, int TM>
+__device__ __forceinline__ void epilogue_tile_row(const ConvShared& s, const ConvGroup& g, int ph,
+                                                  int m, const int (&nn)[TN],
+                                                  const f32x4 (&acc)[TN][TM], int i) {
+  if (s.mode == RGBAC_SUBPEL2) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      if (nn[j] >= g.cout) continue;
+      float v[4] = {acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]};
+      epilogue4<T>(s, g, ph, m, nn[j], v);
+    }
+    return;
+  }
+  const int t = udiv(m, s.Wm, s.rWm);
+  const int mx = m - t * s.Wm;
+  const int b = udiv(t, s.Hm, s.rHm);
+  const int my = t - b * s.Hm;
+  long long opix;
+  if (s.mode == RGBAC_CONVT_S2)
+    opix = (long long)(b * s.out_h + 2 * my + (ph >> 1)) * s.out_w + 2 * mx + (ph & 1);
+  else
+    opix = (long long)(b * s.out_h + my) * s.out_w + mx;
+  EpiIn in[TN];
+  float bias[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    if (nn[j] < g.cout) in[j].template load<T>(g, s.act, opix, nn[j]);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[j][r] = (g.bias && nn[j] < g.cout) ? g.bias[nn[j] + r] : 0.0f;
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    if (nn[j] >= g.cout) continue;
+    float v[4] = {acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]};
+    epilogue4_fin<T>(s, g, opix, nn[j], v, bias[j], in[j]);
   }
 }
 
@@ -626,15 +714,229 @@ _Pragma("unroll")                                                               
       }
       continue;
     }
-    // per 16x16 tile (a row-batched epilogue holding every residual of the row
-    // costs ~50 VGPRs and one wave/SIMD of occupancy in the K loop: measured slower)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      if (nn[j] >= g.cout) continue;
-      float v[4] = {acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]};
-      epilogue4<T>(s, g, phase, m, nn[j], v);
-    }
+    // the row's residual loads are issued together, then the math and stores (one
+    // memory latency per 16-pixel row instead of one per 16x16 tile)
+    epilogue_tile_row<T, TN>(s, g, phase, m, nn, acc, i);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Persistent variant of conv_kernel (no GAUSS epilogue).  grid = (G, 1, Z): block x of
+// z-slice (group, split, phase) walks the slice's output tiles f = x, x + G, ...
+// (N-tile fastest) and streams ONE flattened sequence of (tile, K-stage) pieces through
+// the NBUF ring, so the next tile's first stages load while the current tile's last
+// stages compute and its epilogue stores -- the prologue/epilogue latency of short-K
+// convs (1x1, GDN, qkv/proj, x1, DSE) is hidden instead of paid once per tile.
+template <typename T, int BM, int BN, int WGM, int WGN, int NBUF>
+__global__ void __launch_bounds__(256) conv_pers_kernel(const ConvArgsDev args) {
+  constexpr int EPV = Elem<T>::EPV;
+  constexpr int KS = 8 * EPV;
+  constexpr int TM = BM / WGM / 16;
+  constexpr int TN = BN / WGN / 16;
+  constexpr int IA = BN / 8, IB = BM / 8;
+  constexpr int LW = (IA + IB + 3) / 4;
+  constexpr int STAGE = (BN + BM) * 8;
+  static_assert(WGM * WGN == 4, "4 waves");
+  static_assert(TM >= 1 && TN >= 1, "tile");
+  __shared__ __attribute__((aligned(16))) uint4 smem[NBUF * STAGE];
+
+  const ConvShared& s = args.s;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int t = blockIdx.z;
+  const int phase = t % s.nphase; t /= s.nphase;
+  const int split = t % s.ksplit;
+  const int gi = t / s.ksplit;
+  const ConvGroup& g = args.g[gi];
+  const int Mb = (s.M + BM - 1) / BM;
+  const int Nb = (g.cout + BN - 1) / BN;
+  const int ntile = Mb * Nb;
+  const int G = gridDim.x;
+  if ((int)blockIdx.x >= ntile) return;
+  const int mytiles = (ntile - 1 - (int)blockIdx.x) / G + 1;
+
+  const int py = phase >> 1, px = phase & 1;
+  int ntaps, tw;
+  if (s.mode == RGBAC_CONVT_S2) {
+    tw = 3 - px;
+    ntaps = (3 - py) * tw;
+  } else {
+    tw = s.ksize;
+    ntaps = s.ksize * s.ksize;
+  }
+  const int ktot = ntaps * g.cin_pad;
+  const int nst = (ktot + KS - 1) / KS;
+  const int s_beg = (int)((long long)nst * split / s.ksplit);
+  const int s_end = (int)((long long)nst * (split + 1) / s.ksplit);
+  const int ns = s_end - s_beg;
+  const int nq = mytiles * ns;
+
+  const int in_h = s.in_h, in_w = s.in_w, cin_pad = g.cin_pad, Mtot = s.M;
+  const int Wm = s.Wm, Hm = s.Hm, sy = s.sy;
+  const double rWm = s.rWm, rHm = s.rHm;
+  const int send0 = g.send0, send1 = g.send1, send2 = g.send2;
+  const char* const sp0 = reinterpret_cast<const char*>(g.sp0);
+  const char* const sp1 = reinterpret_cast<const char*>(g.sp1);
+  const char* const sp2 = reinterpret_cast<const char*>(g.sp2);
+  const int sld0 = (int)g.sld0, sld1 = (int)g.sld1, sld2 = (int)g.sld2;
+  const bool convt = s.mode == RGBAC_CONVT_S2;
+  const int pad = s.pad;
+  const bool sq_in = s.square != 0;
+  const int kpad = g.k_pad;
+
+  const int lrow = lane >> 3;
+  const int c = (lane & 7) ^ lrow;
+  int jpc[LW];
+  bool isA[LW];
+  int lofs[LW];
+#pragma unroll
+  for (int i = 0; i < LW; ++i) {
+    int j = wave + 4 * i;
+    if (j >= IA + IB) j = IA + IB - 1;
+    jpc[i] = j;
+    isA[i] = j < IA;
+    lofs[i] = j * 64;
+  }
+  const T* wbase = reinterpret_cast<const T*>(g.w) + (size_t)phase * g.rows * kpad + c * EPV;
+  // per-piece state of the tile currently being ISSUED
+  const T* wrow[LW];
+  int pbase[LW], biy[LW], bix[LW];
+  bool bval[LW];
+  KDec dec;
+  const int k0 = s_beg * KS + c * EPV;
+
+#define PERS_SETUP_TILE(ti)                                                                   \
+  do {                                                                                        \
+    const int f_ = (int)blockIdx.x + (ti) * G;                                                \
+    const int n0_ = (f_ % Nb) * BN, m0_ = (f_ / Nb) * BM;                                     \
+    _Pragma("unroll")                                                                         \
+    for (int i = 0; i < LW; ++i) {                                                            \
+      wrow[i] = wbase + (size_t)(n0_ + (isA[i] ? 8 * jpc[i] + lrow : 0)) * kpad;              \
+      const int m = m0_ + 8 * (jpc[i] - IA) + lrow;                                           \
+      bval[i] = !isA[i] && m < Mtot;                                                          \
+      const int mm = bval[i] ? m : 0;                                                         \
+      const int t_ = udiv(mm, Wm, rWm);                                                       \
+      const int mx = mm - t_ * Wm;                                                            \
+      const int b_ = udiv(t_, Hm, rHm);                                                       \
+      biy[i] = (t_ - b_ * Hm) * sy;                                                           \
+      bix[i] = mx * sy;                                                                       \
+      pbase[i] = (b_ * in_h + biy[i]) * in_w + bix[i];                                        \
+    }                                                                                         \
+    dec.tap = k0 / cin_pad;                                                                   \
+    dec.ci = k0 - dec.tap * cin_pad;                                                          \
+    dec.ty = dec.tap / tw;                                                                    \
+    dec.tx = dec.tap - dec.ty * tw;                                                           \
+  } while (0)
+
+#define PERS_ISSUE(q_)                                                                        \
+  do {                                                                                        \
+    const int qq_ = (q_);                                                                     \
+    const int sti_ = qq_ % ns;                                                                \
+    if (sti_ == 0) PERS_SETUP_TILE(qq_ / ns);                                                 \
+    const int dy = convt ? 1 - dec.ty : dec.ty - pad;                                         \
+    const int dx = convt ? 1 - dec.tx : dec.tx - pad;                                         \
+    const int ci = dec.ci;                                                                    \
+    const bool in0 = ci < send0, in1 = ci < send1;                                            \
+    const char* src = in0 ? sp0 : (in1 ? sp1 : sp2);                                          \
+    const int sld = in0 ? sld0 : (in1 ? sld1 : sld2);                                         \
+    const int cs = ci - (in0 ? 0 : (in1 ? send0 : send1));                                    \
+    const bool kval = (dec.tap < ntaps) & (ci < send2);                                       \
+    const int doff = dy * in_w + dx;                                                          \
+    const int kk = (s_beg + sti_) * KS;                                                       \
+    uint4* stage = smem + (qq_ % NBUF) * STAGE;                                               \
+    _Pragma("unroll")                                                                         \
+    for (int i = 0; i < LW; ++i) {                                                            \
+      const void* gp;                                                                         \
+      if (isA[i]) {                                                                           \
+        gp = wrow[i] + kk;                                                                    \
+      } else {                                                                                \
+        const int iy = biy[i] + dy, ix = bix[i] + dx;                                         \
+        const bool ok = kval & bval[i] & ((unsigned)iy < (unsigned)in_h) &                    \
+                        ((unsigned)ix < (unsigned)in_w);                                      \
+        const unsigned off = ((unsigned)((pbase[i] + doff) * sld + cs)) * (unsigned)sizeof(T); \
+        gp = ok ? (const void*)(src + off) : (const void*)g_zero_page;                        \
+      }                                                                                       \
+      dma16(gp, stage + lofs[i]);                                                             \
+    }                                                                                         \
+    dec.ci += KS;                                                                             \
+    while (dec.ci >= cin_pad) {                                                               \
+      dec.ci -= cin_pad;                                                                      \
+      ++dec.tap;                                                                              \
+      if (++dec.tx == tw) { dec.tx = 0; ++dec.ty; }                                           \
+    }                                                                                         \
+  } while (0)
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int wm = wave % WGM, wn = wave / WGM;
+  const int fr = lane & 15, fq = lane >> 4, sw = lane & 7;
+
+#pragma unroll
+  for (int st = 0; st < NBUF - 1; ++st)
+    if (st < nq) PERS_ISSUE(st);
+
+  int ktile = 0, kst = 0;                      // tile / stage being consumed
+  for (int q = 0; q < nq; ++q) {
+    wait_ring<LW, NBUF - 2>(nq - 1 - q);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (q + NBUF - 1 < nq) PERS_ISSUE(q + NBUF - 1);
+    const uint4* As = smem + (q % NBUF) * STAGE;
+    const uint4* Bs = As + BN * 8;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int chunk = (4 * ks + fq) ^ sw;
+      uint4 a[TN], b[TM];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) a[j] = As[(wn * TN * 16 + j * 16 + fr) * 8 + chunk];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        b[i] = Bs[(wm * TM * 16 + i * 16 + fr) * 8 + chunk];
+        if (sq_in) b[i] = square_chunk<T>(b[i]);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) mma_step<T>(acc[j][i], a[j], b[i]);
+    }
+    if (++kst < ns) continue;
+    // ---- tile `ktile` complete: fused epilogue, then reset the accumulators
+    {
+      const int f = (int)blockIdx.x + ktile * G;
+      const int n0 = (f % Nb) * BN, m0 = (f / Nb) * BM;
+      int nn[TN];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) nn[j] = n0 + wn * TN * 16 + j * 16 + fq * 4;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = m0 + wm * TM * 16 + i * 16 + fr;
+        if (m < Mtot) {
+          if (s.ksplit > 1) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              if (nn[j] >= g.cout) continue;
+              float* w = g.ws + (((size_t)split * s.nphase + phase) * s.M + m) * g.cout16 + nn[j];
+              *reinterpret_cast<float4*>(w) =
+                  make_float4(acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]);
+            }
+          } else {
+            epilogue_tile_row<T, TN>(s, g, phase, m, nn, acc, i);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    kst = 0;
+    ++ktile;
+  }
+#undef PERS_ISSUE
+#undef PERS_SETUP_TILE
 }
 
 template <typename T>
@@ -1013,7 +1315,11 @@ static const TileCfg kTiles[] = {
     {16, 16}, {16, 32}, {16, 48}, {16, 64}, {16, 96}, {16, 192},
     {256, 32},
     // 20..26: the streaming shapes of 0..6 with a deeper LDS ring (more K stages in flight)
-    {128, 128}, {128, 64}, {64, 64}, {128, 32}, {64, 32}, {128, 16}, {64, 16}};
+    {128, 128}, {128, 64}, {64, 64}, {128, 32}, {64, 32}, {128, 16}, {64, 16},
+    // 27..33: the streaming shapes of 0..6, persistent over output tiles (conv_pers_kernel)
+    {128, 128}, {128, 64}, {64, 64}, {128, 32}, {64, 32}, {128, 16}, {64, 16},
+    // 34: small-K wave-streaming kernel (32-pixel wave tiles x up to 192 channels)
+    {32, 96}};
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 constexpr int kFirstWres = 7;
 constexpr int kWresStages = 6;
@@ -1021,6 +1327,191 @@ constexpr int kFirstDirect = 13;   // 13..18: direct kernel with NT = bn/16
 constexpr int kDirectSteps = 12;
 constexpr int kTileSpatial = 19;   // conv3x3_c32_kernel (16x16 pixels x 32 channels)
 constexpr int kFirstDeep = 20;     // 20..26: deep-ring streaming tiles
+constexpr int kFirstPers = 27;     // 27..33: persistent streaming tiles
+constexpr int kTileSmallK = 34;    // conv_smallk_kernel (bf16, plain conv, K <= 256)
+constexpr int kSmallKMax = 256;
+
+// ---------------------------------------------------------------------------
+// Pointwise (1x1, stride 1, one source, K = cin_pad <= 16 * NKS) wave-streaming kernel,
+// bf16: the HBM-bound 1x1 convs at full resolution -- GDN/IGDN norm pools, qkv/proj,
+// gates, the DSE in/out projections.  The block's weight panel (BN = 32*NT rows x K) is
+// staged in LDS once; then each WAVE streams 32-pixel tiles on its own (no barrier):
+// per 16-deep k-step ONE 16-byte load per lane (pixel lane&31, channels 8*(lane>>5)..+7,
+// straight into VGPRs at an immediate offset from the pixel's row) feeds NT
+// v_mfma_f32_32x32x16_bf16 whose A fragments come from the LDS panel.  Each k-step's
+// fragment is reloaded for the wave's NEXT tile right after its MFMAs issue (a register
+// ring), so the next tile's HBM reads overlap this tile's MFMAs and epilogue.
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+template <int NT, int NKS>
+__global__ void __launch_bounds__(256, 2) conv_smallk_kernel(const ConvArgsDev args) {
+  constexpr int BN = 32 * NT;
+  constexpr int RS = 2 * NKS + 1;               // uint4 per panel row (odd: spreads banks)
+  __shared__ __attribute__((aligned(16))) uint4 Wl[BN * RS];
+  __shared__ float bl[BN];
+
+  const ConvShared& s = args.s;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const ConvGroup& g = args.g[blockIdx.z];
+  const int n0 = blockIdx.y * BN;
+  if (n0 >= g.cout) return;
+  const int act = s.act;
+  for (int e = tid; e < BN; e += 256) bl[e] = (g.bias && n0 + e < g.rows) ? g.bias[n0 + e] : 0.0f;
+  const int nchunk = g.cin_pad / 8;              // 8-channel chunks of K
+  {
+    const bf16_t* wbase = reinterpret_cast<const bf16_t*>(g.w);
+    for (int e = tid; e < BN * 2 * NKS; e += 256) {
+      const int row = e / (2 * NKS), ch = e - row * (2 * NKS);
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (n0 + row < g.rows && ch < nchunk)
+        v = *reinterpret_cast<const uint4*>(wbase + (size_t)(n0 + row) * g.k_pad + ch * 8);
+      Wl[row * RS + ch] = v;
+    }
+  }
+  __syncthreads();
+
+  const int Mtot = s.M;
+  const int ld = (int)g.sld0;
+  const bool sq_in = s.square != 0;
+  const int r32 = lane & 31, h = lane >> 5;
+  const char* const src = reinterpret_cast<const char*>(g.sp0) + 16 * h;
+  // chunk 2*st+h of a pixel exists iff 16*st + 8*h < cin_pad
+  const int ntile = (Mtot + 31) / 32;
+  const int tstride = gridDim.x * 4;
+  int tile = blockIdx.x * 4 + wave;
+  if (tile >= ntile) return;
+
+#define PW_LOAD(dst, st, rowp_, valid_)                                                       \
+  do {                                                                                        \
+    const bool ok_ = (valid_) & (2 * (st) + h < nchunk);                                      \
+    const uint4* p_ = ok_ ? reinterpret_cast<const uint4*>((rowp_) + 32 * (st)) : g_zero_page; \
+    dst = *p_;                                                                                \
+  } while (0)
+
+  uint4 bv[NKS];
+  {
+    const int m = tile * 32 + r32;
+    const bool valid = m < Mtot;
+    const char* rowp = src + (size_t)(valid ? m : 0) * ld * 2;
+#pragma unroll
+    for (int st = 0; st < NKS; ++st) PW_LOAD(bv[st], st, rowp, valid);
+  }
+  for (; tile < ntile; tile += tstride) {
+    const int mn = (tile + tstride) * 32 + r32;
+    const bool nvalid = mn < Mtot;
+    const char* nrowp = src + (size_t)(nvalid ? mn : 0) * ld * 2;
+    f32x16 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+    // (NKS is the launch's exact k-step count: no runtime guard between k-steps, so the
+    // compiler can run the LDS fragment reads ahead of the MFMAs)
+#pragma unroll
+    for (int st = 0; st < NKS; ++st) {
+      uint4 b = bv[st];
+      if (sq_in) b = square_chunk<bf16_t>(b);
+      const bf16x8 bb = __builtin_bit_cast(bf16x8, b);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const uint4 a = Wl[(j * 32 + r32) * RS + 2 * st + h];
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), bb,
+                                                         acc[j], 0, 0, 0);
+      }
+      PW_LOAD(bv[st], st, nrowp, nvalid);
+    }
+    const int m = tile * 32 + r32;
+    if (m < Mtot) {
+      // per 32-channel column: the 4 quads' residual loads are issued together, then
+      // the math and stores (one memory latency per column, not per quad)
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        EpiIn in[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int n = n0 + j * 32 + 8 * q + 4 * h;
+          if (n < g.cout) in[q].load<bf16_t>(g, act, (long long)m, n);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int nl = j * 32 + 8 * q + 4 * h;
+          if (n0 + nl < g.cout) {
+            float v[4] = {acc[j][4 * q], acc[j][4 * q + 1], acc[j][4 * q + 2], acc[j][4 * q + 3]};
+            const float bias[4] = {bl[nl], bl[nl + 1], bl[nl + 2], bl[nl + 3]};
+            epilogue4_fin<bf16_t>(s, g, (long long)m, n0 + nl, v, bias, in[q]);
+          }
+        }
+      }
+    }
+  }
+#undef PW_LOAD
+}
+
+template <int NT, int NKS>
+static void launch_smallk_nt(const ConvArgsDev& d, int ny, int nz, hipStream_t st) {
+  static int per_cu = -1, ncu = 0;
+  auto kern = conv_smallk_kernel<NT, NKS>;
+  if (per_cu < 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    if (ncu < 1) ncu = 256;
+  }
+  const int ntile = (d.s.M + 31) / 32;
+  int gx = (ncu * per_cu + ny * nz - 1) / (ny * nz);
+  const int need = (ntile + 3) / 4;
+  if (gx > need) gx = need;
+  if (gx < 1) gx = 1;
+  hipLaunchKernelGGL(kern, dim3(gx, ny, nz), dim3(256), 0, st, d);
+}
+
+template <int NKS>
+static void launch_smallk_k(const ConvArgsDev& d, int max_cout, hipStream_t st) {
+  const int nz = d.s.ngroups;
+  if (max_cout <= 32) launch_smallk_nt<1, NKS>(d, 1, nz, st);
+  else if (max_cout <= 64) launch_smallk_nt<2, NKS>(d, 1, nz, st);
+  else launch_smallk_nt<3, NKS>(d, (max_cout + 95) / 96, nz, st);
+}
+
+static void launch_smallk(const ConvArgsDev& d, int nks16, int max_cout, hipStream_t st) {
+  switch (nks16) {
+    case 1: launch_smallk_k<1>(d, max_cout, st); break;
+    case 2: launch_smallk_k<2>(d, max_cout, st); break;
+    case 3: launch_smallk_k<3>(d, max_cout, st); break;
+    case 4: launch_smallk_k<4>(d, max_cout, st); break;
+    case 5: launch_smallk_k<5>(d, max_cout, st); break;
+    case 6: launch_smallk_k<6>(d, max_cout, st); break;
+    case 7: case 8: launch_smallk_k<8>(d, max_cout, st); break;
+    case 9: case 10: case 11: case 12: launch_smallk_k<12>(d, max_cout, st); break;
+    default: launch_smallk_k<16>(d, max_cout, st); break;
+  }
+}
+
+// Persistent grid: as many blocks per z-slice as fit on the chip at once (occupancy query,
+// cached per kernel), evened out so every block gets the same number of tiles (+-1).
+template <typename T, int BM, int BN, int WGM, int WGN, int NBUF>
+static void launch_pers(const ConvArgsDev& d, int ntile, int nz, hipStream_t st) {
+  static int per_cu = -1, ncu = 0;
+  auto kern = conv_pers_kernel<T, BM, BN, WGM, WGN, NBUF>;
+  if (per_cu < 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess ||
+        per_cu < 1)
+      per_cu = 1;
+    if (ncu < 1) ncu = 256;
+  }
+  int cap = (ncu * per_cu + nz - 1) / nz;
+  if (cap < 1) cap = 1;
+  const int rounds = (ntile + cap - 1) / cap;
+  const int G = (ntile + rounds - 1) / rounds;
+  hipLaunchKernelGGL(kern, dim3(G, 1, nz), dim3(256), 0, st, d);
+}
 
 template <typename T>
 static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t st) {
@@ -1084,6 +1575,33 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
     }
     return check_launch("conv_wres_kernel");
   }
+  if (tile == kTileSmallK) {
+    if constexpr (sizeof(T) == 2) {
+      int nks16 = 0;
+      for (int i = 0; i < s.ngroups; ++i) {
+        const int k = (s.ksize * s.ksize * d.g[i].cin_pad + 15) / 16;
+        if (k > nks16) nks16 = k;
+      }
+      launch_smallk(d, nks16, max_cout, st);
+      return check_launch("conv_smallk_kernel");
+    } else {
+      set_error("the small-K tile is bf16 only");
+      return RGBAC_E_ARG;
+    }
+  }
+  if (tile >= kFirstPers) {
+    const int ntile = ((s.M + tc.bm - 1) / tc.bm) * ((max_cout + tc.bn - 1) / tc.bn);
+    const int nz = s.nphase * s.ksplit * s.ngroups;
+    switch (tile) {
+      case 27: launch_pers<T, 128, 128, 2, 2, 2>(d, ntile, nz, st); break;
+      case 28: launch_pers<T, 128, 64, 4, 1, 3>(d, ntile, nz, st); break;
+      case 29: launch_pers<T, 64, 64, 2, 2, 3>(d, ntile, nz, st); break;
+      case 30: launch_pers<T, 128, 32, 4, 1, 3>(d, ntile, nz, st); break;
+      case 31: launch_pers<T, 64, 32, 2, 2, 3>(d, ntile, nz, st); break;
+      case 32: launch_pers<T, 128, 16, 4, 1, 3>(d, ntile, nz, st); break;
+      default: launch_pers<T, 64, 16, 4, 1, 3>(d, ntile, nz, st); break;
+    }
+  } else {
   dim3 grid((s.M + tc.bm - 1) / tc.bm, (max_cout + tc.bn - 1) / tc.bn,
             s.nphase * s.ksplit * s.ngroups);
   switch (tile) {
@@ -1101,6 +1619,7 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
     case 24: hipLaunchKernelGGL((conv_kernel<T, 64, 32, 2, 2, 8>), grid, dim3(256), 0, st, d); break;
     case 25: hipLaunchKernelGGL((conv_kernel<T, 128, 16, 4, 1, 6>), grid, dim3(256), 0, st, d); break;
     default: hipLaunchKernelGGL((conv_kernel<T, 64, 16, 4, 1, 8>), grid, dim3(256), 0, st, d); break;
+  }
   }
   int rc = check_launch("conv_kernel");
   if (rc || s.ksplit == 1) return rc;
@@ -1258,6 +1777,14 @@ extern "C" int rgbac_conv2d_grouped(const rgbac_conv_args* args, int ngroups, vo
       RGBAC_REQUIRE(args[i].nsrc == 1 && args[i].cin_pad == 32 && args[i].src[0].channels == 32 &&
                         args[i].cout <= 32 && args[i].k_pad >= 288,
                     "the spatial 3x3 tile needs one 32-channel source and cout <= 32");
+  } else if (a->tile == kTileSmallK) {
+    RGBAC_REQUIRE(a->dtype == RGBAC_BF16 && a->mode == RGBAC_CONV && a->ksplit == 1 &&
+                      a->act != RGBAC_ACT_GAUSS,
+                  "the small-K tile needs bf16, a plain conv, ksplit 1 and no GAUSS epilogue");
+    RGBAC_REQUIRE(a->ksize == 1 && a->stride == 1, "the small-K tile is a 1x1 stride-1 conv");
+    for (int i = 0; i < ngroups; ++i)
+      RGBAC_REQUIRE(args[i].cin_pad <= kSmallKMax && args[i].nsrc == 1,
+                    "the small-K tile needs one source with cin_pad <= 256");
   } else if (a->tile >= kFirstDirect && a->tile < kFirstDeep) {
     RGBAC_REQUIRE(a->mode == RGBAC_CONV && a->ksplit == 1 && a->act != RGBAC_ACT_GAUSS,
                   "direct tiles need a plain conv, ksplit 1 and no GAUSS epilogue");
@@ -1282,6 +1809,7 @@ extern "C" int rgbac_conv2d_grouped(const rgbac_conv_args* args, int ngroups, vo
     }
     if (a->act == RGBAC_ACT_GAUSS) {
       RGBAC_REQUIRE(a->mode == RGBAC_CONV && a->ksplit == 1, "GAUSS needs a plain conv, ksplit 1");
+      RGBAC_REQUIRE(a->tile < kFirstPers, "GAUSS needs a non-persistent tile");
       RGBAC_REQUIRE(b->cout % 2 == 0 && b->cout <= kTiles[a->tile].bn,
                     "GAUSS needs (mu|sigma) channels in one N tile");
       RGBAC_REQUIRE(b->partial, "GAUSS needs a partial-sum buffer");

@@ -86,7 +86,9 @@ TILES = [(128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 1
          (128, 64), (64, 64), (128, 32), (64, 32), (128, 128), (128, 16),
          (16, 16), (16, 32), (16, 48), (16, 64), (16, 96), (16, 192),
          (256, 32),
-         (128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 16)]
+         (128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 16),
+         (128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 16),
+         (32, 96)]
 FIRST_WRES = 7
 WRES_STAGES = 6
 FIRST_DIRECT = 13        # 13..18: direct kernel (plain conv, K <= DIRECT_STEPS MFMA k-steps)
@@ -94,7 +96,12 @@ DIRECT_STEPS = 12
 DIRECT_LDS = 65536       # weight panel bytes of a direct tile (dynamic LDS limit)
 TILE_SPATIAL = 19        # conv3x3_c32_kernel: 16x16-pixel tiles, 3x3 s1, Cin 32, Cout <= 32, bf16
 FIRST_DEEP = 20          # 20..26: tiles 0..6 with a deeper LDS ring (4..8 K stages)
-STREAM_TILES = tuple(range(FIRST_WRES)) + tuple(range(FIRST_DEEP, FIRST_DEEP + 7))
+FIRST_PERS = 27          # 27..33: tiles 0..6, persistent over output tiles (no GAUSS epilogue)
+STREAM_TILES = (tuple(range(FIRST_WRES)) + tuple(range(FIRST_DEEP, FIRST_DEEP + 7)) +
+                tuple(range(FIRST_PERS, FIRST_PERS + 7)))
+GAUSS_TILES = tuple(range(FIRST_WRES)) + tuple(range(FIRST_DEEP, FIRST_DEEP + 7))
+TILE_SMALLK = 34         # conv_smallk_kernel: bf16 1x1 stride-1 conv, one source, cin_pad <= 256
+SMALLK_MAX = 256
 KSPLITS = (1, 2, 4, 8)
 TUNE = os.environ.get("RGBAC_TUNE", "1") != "0"
 # RGBAC_TILE_SET: "stream" (default: streaming K-ring tiles; the weight-resident and
@@ -109,12 +116,15 @@ def pick_cout_pad(cout):
     return round_up(cout, 128)
 
 
-def _candidates(M, cout, nst, nks=None, plain=True, spatial=False):
+def _candidates(M, cout, nst, nks=None, plain=True, spatial=False, smallk=False):
     """(tile, ksplit) pairs worth timing for an M-pixel, cout-channel conv with nst K-stages
-    (nks MFMA k-steps; ``plain`` = CONV mode; ``spatial`` = the 3x3/Cin-32 tile applies)."""
-    out = []
+    (nks MFMA k-steps; ``plain`` = CONV mode; ``spatial`` = the 3x3/Cin-32 tile applies;
+    ``smallk`` = the small-K wave-streaming tile applies)."""
+    out = [(TILE_SMALLK, 1)] if smallk else []
     n16 = round_up(cout, 16)
     for t, (bm, bn) in enumerate(TILES):
+        if t == TILE_SMALLK:
+            continue
         if t == TILE_SPATIAL:
             if spatial:
                 out.append((t, 1))
@@ -394,6 +404,13 @@ def _spatial_ok(preps):
                 p.a.cout <= 32 for p in preps))
 
 
+def _smallk_ok(preps):
+    a = preps[0].a
+    return (a.dtype == _lib.BF16 and a.mode == CONV and a.act != ACT["gauss"] and
+            a.ksize == 1 and a.stride == 1 and
+            all(p.a.nsrc == 1 and p.a.cin_pad <= SMALLK_MAX for p in preps))
+
+
 def _gauss_ok(t, cout):
     return TILES[t][1] >= cout
 
@@ -429,10 +446,10 @@ def launch(preps):
         cout = max(pr.pk.cout for pr in preps)
         nst = max(pr.nst for pr in preps)
         if gauss:
-            cands = [(t, 1) for t in STREAM_TILES if _gauss_ok(t, cout)]
+            cands = [(t, 1) for t in GAUSS_TILES if _gauss_ok(t, cout)]
         else:
             cands = _candidates(mtot, cout, nst, max(pr.nks for pr in preps),
-                                p0.pk.mode == CONV, _spatial_ok(preps))
+                                p0.pk.mode == CONV, _spatial_ok(preps), _smallk_ok(preps))
         if TUNE and not torch.cuda.is_current_stream_capturing():
             best = None
             for cand in cands:
@@ -454,8 +471,9 @@ def launch(preps):
         else:
             choice = _heuristic(mtot, cout, nst)
         _tune_cache[key] = choice
-    if gauss and not _gauss_ok(choice[0], max(pr.pk.cout for pr in preps)):
-        choice = (min((t for t in STREAM_TILES if _gauss_ok(t, p0.pk.cout)),
+    if gauss and (choice[0] not in GAUSS_TILES or
+                  not _gauss_ok(choice[0], max(pr.pk.cout for pr in preps))):
+        choice = (min((t for t in GAUSS_TILES if _gauss_ok(t, p0.pk.cout)),
                       key=lambda t: TILES[t][1]), 1)
     set_choice(*choice)
     if PROFILER is None:
@@ -463,8 +481,10 @@ def launch(preps):
     else:
         bm, bn = TILES[choice[0]]
         kname = ("conv3x3_c32_kernel" if choice[0] == TILE_SPATIAL else
+                 "conv_smallk_kernel" if choice[0] == TILE_SMALLK else
                  "conv_direct_kernel" if FIRST_DIRECT <= choice[0] < FIRST_DEEP else
-                 "conv_wres_kernel" if FIRST_WRES <= choice[0] < FIRST_DIRECT else "conv_kernel")
+                 "conv_wres_kernel" if FIRST_WRES <= choice[0] < FIRST_DIRECT else
+                 "conv_pers_kernel" if choice[0] >= FIRST_PERS else "conv_kernel")
         name = f"{kname}<{'f32' if p0.a.dtype == 0 else 'bf16'},{bm}x{bn}>"
         desc = f"{name} ks{choice[1]} g{n} {p0.desc}"
         PROFILER.wrap(name, sum(pr.flops for pr in preps), sum(pr.nbytes for pr in preps),

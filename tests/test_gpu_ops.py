@@ -214,7 +214,7 @@ def test_mask_pyramid(device):
 
 # ------------------------------------------------------------------ every tile x split-K
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("tile", list(range(7)) + list(range(20, 27)))
+@pytest.mark.parametrize("tile", list(range(7)) + list(range(20, 34)))
 @pytest.mark.parametrize("ksplit", [1, 3])
 def test_conv_tiles_and_splitk(device, dtype, tile, ksplit):
     """Every tile shape and split-K path against PyTorch, on conv / convT / 3 sources."""
@@ -346,3 +346,68 @@ def test_conv_spatial_tile(device, cout, act):
     finally:
         rt.FORCE = None
     assert rel(got, want) < 2e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("tile", range(27, 34))
+def test_conv_persistent_many_tiles(device, dtype, tile):
+    """Persistent tiles with several output tiles per workgroup (the flattened
+    (tile, K-stage) ring crossing tile boundaries), residual epilogue, split-K and convT."""
+    rt = _rt()
+    from rgbac.layers.TransformRGB import run_conv
+    g = _gen(300 + tile)
+    tol = 2e-5 if dtype == torch.float32 else 2e-2
+    try:
+        rt.FORCE = (tile, 1)
+        m1 = nn.Conv2d(96, 72, 1)
+        x = torch.randn((4, 96, 96, 128), generator=g)
+        r = torch.randn((4, 72, 96, 128), generator=g)
+        want = F.gelu(m1(x) + r)
+        with torch.no_grad():
+            fx, fr = rt.to_nhwc(x.to(device), dtype), rt.to_nhwc(r.to(device), dtype)
+            got = rt.to_nchw(run_conv(m1.to(device), [fx.src()], act="gelu", res0=fr))
+        assert rel(got, want) < tol
+        for ks in (1, 2):
+            rt.FORCE = (tile, ks)
+            m3 = nn.Conv2d(40, 24, 3, padding=1)
+            x3 = torch.randn((3, 40, 100, 90), generator=g)
+            want3 = m3(x3)
+            with torch.no_grad():
+                got = rt.to_nchw(run_conv(m3.to(device), [rt.to_nhwc(x3.to(device), dtype).src()]))
+            assert rel(got, want3) < tol, ks
+        rt.FORCE = (tile, 1)
+        mt = nn.ConvTranspose2d(32, 40, 5, stride=2, padding=2, output_padding=1)
+        xt = torch.randn((2, 32, 64, 48), generator=g)
+        wantt = mt(xt)
+        with torch.no_grad():
+            got = rt.to_nchw(run_conv(mt.to(device), [rt.to_nhwc(xt.to(device), dtype).src()]))
+        assert rel(got, wantt) < tol
+    finally:
+        rt.FORCE = None
+
+
+@pytest.mark.parametrize("cin,cout,k,s,act", [(192, 192, 1, 1, "gelu"), (3, 32, 1, 1, "none"),
+                                              (32, 3, 1, 1, "none"), (192, 576, 1, 1, "none"),
+                                              (80, 40, 1, 1, "gelu"), (256, 100, 1, 1, "relu"),
+                                              (16, 24, 1, 1, "relu"), (96, 80, 1, 1, "none")])
+def test_conv_smallk_tile(device, cin, cout, k, s, act):
+    """The pointwise wave-streaming tile (bf16): 1x1 convs over ragged pixel counts (several
+    tiles per wave), every panel width, K up to 256, residual epilogue."""
+    rt = _rt()
+    from rgbac.layers.TransformRGB import run_conv
+    g = _gen(400 + cin + cout + k)
+    m = nn.Conv2d(cin, cout, k, stride=s, padding=k // 2)
+    x = torch.randn((3, cin, 70, 94), generator=g)
+    y = m(x)
+    r = torch.randn(y.shape, generator=g)
+    f = {"gelu": F.gelu, "relu": F.relu, "none": lambda t: t}[act]
+    want = f(y + r)
+    rt.FORCE = (rt.TILE_SMALLK, 1)
+    try:
+        with torch.no_grad():
+            fx = rt.to_nhwc(x.to(device), torch.bfloat16)
+            fr = rt.to_nhwc(r.to(device), torch.bfloat16)
+            got = rt.to_nchw(run_conv(m.to(device), [fx.src()], act=act, res0=fr))
+        assert rel(got, want) < 2e-2
+    finally:
+        rt.FORCE = None
