@@ -115,7 +115,28 @@ def cpu_baseline_train(budget_s):
                       f"(half-transparent alpha), {n} timed iterations after 1 warm-up, {dt:.1f} s"}
 
 
-def roofline_of(summ, dtype, nrep):
+def pmc_traffic(kernel, path):
+    """HBM bytes per dispatch of ``kernel`` from a committed rocprofv3 PMC summary
+    (tools/pmc_bench.sh + tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE), or None."""
+    if not path or not os.path.exists(path):
+        return None
+    with open(path) as fh:
+        ent = json.load(fh).get("kernels", {}).get(kernel)
+    return None if ent is None else ent["hbm_bytes_per_dispatch"]
+
+
+def tune_cache_setup(args, default):
+    """Load the committed per-shape tile choices (so the timed run and a rocprofv3 trace of
+    it contain no autotuning dispatches); --save-tune writes the cache after warm-up."""
+    from rgbac import runtime as rt
+    path = args.tune_cache if args.tune_cache is not None else default
+    if path and os.path.exists(path):
+        rt.load_tune_cache(path)
+        return path
+    return None
+
+
+def roofline_of(summ, dtype, nrep, traffic_file=None):
     total_ms = sum(d["ms"] for d in summ.values())
     dom_name, dom = max(summ.items(), key=lambda kv: kv[1]["ms"])
     per_ms = dom["ms"] / dom["launches"]
@@ -123,7 +144,8 @@ def roofline_of(summ, dtype, nrep):
     achieved = per_fl / (per_ms * 1e-3) / 1e12
     peak = PEAK[dtype]["mfma"]
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": None, "kernel": dom_name,
+            "frac": round(achieved / peak, 4), "traffic": pmc_traffic(dom_name, traffic_file),
+            "kernel": dom_name,
             "avg_launch_us": round(per_ms * 1e3, 2),
             "algorithmic_gflop_per_launch": round(per_fl / 1e9, 4),
             "share_of_step": round(dom["ms"] / total_ms, 3)}, total_ms
@@ -162,8 +184,11 @@ def main_train(args, world, rank, dev, dist):
         trainer.step(4096.0 * out[1] + out[2])        # trainRGB.py:183-198 (lambda 4096)
         return out
 
+    tuned = tune_cache_setup(args, os.path.join(ROOT, "profiles", f"tune_train_{args.dtype}_b{B}_{S}.json"))
     step()
     torch.cuda.synchronize()
+    if args.save_tune and rank == 0:
+        rt.save_tune_cache(args.save_tune)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
@@ -193,7 +218,9 @@ def main_train(args, world, rank, dev, dist):
         summ = prof.summary()
         if args.layers:
             write_layers(prof, args.layers, 2)
-        roof, total_ms = roofline_of(summ, args.dtype, 2)
+        traffic_file = args.traffic_file if args.traffic_file is not None else \
+            os.path.join(ROOT, "profiles", "r01_pmc_traffic_train.json")
+        roof, total_ms = roofline_of(summ, args.dtype, 2, traffic_file)
         rec = {"metric": TRAIN_METRIC, "value": round(value, 2), "unit": "MPix/s",
                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
@@ -205,6 +232,7 @@ def main_train(args, world, rank, dev, dist):
                                       f"(BASELINE config {3 if world == 1 else 5}), {S}x{S} RGBA",
                           "global_batch": B * world, "per_gpu_batch": B, "height": S,
                           "width": S, "parallelism": f"dp{world}",
+                          "tile_cache": tuned and os.path.relpath(tuned, ROOT),
                           "loss": round(4096.0 * out[1].item() + out[2].item(), 4)},
                "roofline": roof}
         if args.kernels:
@@ -236,6 +264,12 @@ def main():
     ap.add_argument("--layers", default=None, help="write a per-layer time table to this file")
     ap.add_argument("--train", action="store_true",
                     help="time the training step (BASELINE config 3 / 5) instead of the forward")
+    ap.add_argument("--tune-cache", default=None,
+                    help="tile-choice cache to load (default: the committed profiles/ one for "
+                         "the forward config); '' disables")
+    ap.add_argument("--save-tune", default=None, help="write the tile-choice cache here")
+    ap.add_argument("--traffic-file", default=None,
+                    help="PMC traffic summary (default: the committed profiles/ one)")
     args = ap.parse_args()
     if args.train and args.batch == 8 and "--batch" not in sys.argv:
         args.batch = 16
@@ -270,8 +304,11 @@ def main():
         with torch.no_grad():                          # inference: the fused, grouped path
             return net(x, a, a, *me)
 
-    out = step()                                       # packs weights, warms caches
+    tuned = tune_cache_setup(args, os.path.join(ROOT, "profiles", f"tune_fwd_{args.dtype}_b{B}_{S}.json"))
+    out = step()                                       # packs weights, warms caches (and tunes)
     torch.cuda.synchronize()
+    if args.save_tune and rank == 0:
+        rt.save_tune_cache(args.save_tune)
     graph = None
     if not args.no_graph:
         s = torch.cuda.Stream()
@@ -307,35 +344,28 @@ def main():
     value = world * B * S * S * args.steps / elapsed / 1e6
 
     if rank == 0:
-        # ---- roofline attribution: eager replay with HIP events around every launch
+        # ---- roofline attribution: eager steps, each queued behind a GPU spin so the host has
+        # enqueued every launch before the GPU reaches them (back-to-back execution as in the
+        # graph replay), with a fence-free HIP event (rgbac_timer_*: no cache writeback /
+        # invalidate per record) on the launching stream around every launch.
         prof = rt.LaunchProfiler()
+        nrep = 3
         rt.PROFILER = prof
-        for _ in range(3):
-            torch.cuda._sleep(SPIN_FWD)     # queue the whole step behind a spin: GPU-side times
+        for _ in range(nrep):
+            torch.cuda._sleep(SPIN_FWD)
             step()
             torch.cuda.synchronize()
         rt.PROFILER = None
         summ = prof.summary()
         if args.layers:
-            lay = prof.layers()
-            tot = sum(v[1] for v in lay.values())
-            with open(args.layers, "w") as fh:
-                for k, v in sorted(lay.items(), key=lambda kv: -kv[1][1]):
-                    fh.write(f"{v[1] / 3:9.4f} ms {100 * v[1] / tot:5.1f}% n={v[0] // 3:3d} "
-                             f"{v[2] / max(v[1], 1e-9) / 1e9:8.1f} TF/s  "
-                             f"{v[3] / max(v[1], 1e-9) / 1e6:7.0f} GB/s  {k}\n")
-        total_ms = sum(d["ms"] for d in summ.values())
-        dom_name, dom = max(summ.items(), key=lambda kv: kv[1]["ms"])
-        per_ms = dom["ms"] / dom["launches"]
-        per_fl = dom["flops"] / dom["launches"]
-        achieved = per_fl / (per_ms * 1e-3) / 1e12
-        peak = PEAK[args.dtype]["mfma"]
-        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(achieved / peak, 4), "traffic": None, "kernel": dom_name,
-                "avg_launch_us": round(per_ms * 1e3, 2),
-                "algorithmic_gflop_per_launch": round(per_fl / 1e9, 4),
-                "share_of_forward": round(dom["ms"] / total_ms, 3)}
-        fwd_flops = sum(d["flops"] for d in summ.values()) / 3
+            write_layers(prof, args.layers, nrep)
+        traffic_file = args.traffic_file if args.traffic_file is not None else \
+            os.path.join(ROOT, "profiles", "r01_pmc_traffic_fwd.json")
+        roof, total_ms = roofline_of(summ, args.dtype, nrep, traffic_file)
+        roof["timing"] = "eager steps behind a GPU spin, fence-free HIP events per launch"
+        if roof["traffic"] is not None:
+            roof["traffic_source"] = os.path.relpath(traffic_file, ROOT)
+        fwd_flops = sum(d["flops"] for d in summ.values()) / nrep
         rec = {"metric": METRIC, "value": round(value, 2), "unit": "MPix/s", "n_gpus": world,
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -344,11 +374,12 @@ def main():
                "config": {"workload": "AutoEncoderRGB_Journal forward encode+decode "
                                       f"(BASELINE config 2), {S}x{S} RGBA",
                           "global_batch": B * world, "per_gpu_batch": B, "height": S, "width": S,
-                          "parallelism": f"replicas{world}", "hip_graph": graph is not None},
+                          "parallelism": f"replicas{world}", "hip_graph": graph is not None,
+                          "tile_cache": tuned and os.path.relpath(tuned, ROOT)},
                "roofline": roof,
                "achieved_model_tflops": round(fwd_flops / (ms * 1e-3) / 1e12, 2)}
         if args.kernels:
-            rec["kernels"] = {k: {"launches": v["launches"] // 3, "ms": round(v["ms"] / 3, 4),
+            rec["kernels"] = {k: {"launches": v["launches"] // nrep, "ms": round(v["ms"] / nrep, 4),
                                   "share": round(v["ms"] / total_ms, 4),
                                   "tflops": round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 2)}
                               for k, v in sorted(summ.items(), key=lambda kv: -kv[1]["ms"])}

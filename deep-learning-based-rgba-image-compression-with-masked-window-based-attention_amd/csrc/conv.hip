@@ -1514,9 +1514,15 @@ static void launch_pers(const ConvArgsDev& d, int ntile, int nz, hipStream_t st)
 }
 
 template <typename T>
-static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t st) {
+static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t st, int part) {
   const ConvShared& s = d.s;
   const TileCfg tc = kTiles[tile];
+  if (part == 2) {                         // split-K reduce + epilogue kernels only
+    if (s.ksplit == 1 || tile == kTileSpatial || tile == kTileSmallK ||
+        (tile >= kFirstWres && tile < kFirstDeep))
+      return RGBAC_OK;
+    goto splitk_epilogue;
+  }
   if (tile == kTileSpatial) {
     if constexpr (sizeof(T) == 2) {
       dim3 grid((unsigned)((long long)s.batch * (s.Hm / 16) * (s.Wm / 16)), 1, s.ngroups);
@@ -1621,14 +1627,17 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
     default: hipLaunchKernelGGL((conv_kernel<T, 64, 16, 4, 1, 8>), grid, dim3(256), 0, st, d); break;
   }
   }
-  int rc = check_launch("conv_kernel");
-  if (rc || s.ksplit == 1) return rc;
+  {
+    int rc = check_launch("conv_kernel");
+    if (rc || s.ksplit == 1 || part == 1) return rc;
+  }
+splitk_epilogue:
   for (int gi = 0; gi < s.ngroups; ++gi) {
     const long long total = (long long)s.nphase * s.M * (d.g[gi].cout16 / 4);
     long long gsz = (total + 255) / 256;
     if (gsz > 8192) gsz = 8192;
     hipLaunchKernelGGL((conv_splitk_epilogue<T>), dim3((int)gsz), dim3(256), 0, st, d, gi);
-    rc = check_launch("conv_splitk_epilogue");
+    const int rc = check_launch("conv_splitk_epilogue");
     if (rc) return rc;
   }
   return RGBAC_OK;
@@ -1702,6 +1711,12 @@ extern "C" int rgbac_conv_num_tiles(void) { return kNumTiles; }
 extern "C" int rgbac_conv_max_groups(void) { return kMaxGroups; }
 
 extern "C" int rgbac_conv2d_grouped(const rgbac_conv_args* args, int ngroups, void* stream) {
+  return rgbac_conv2d_grouped_part(args, ngroups, 0, stream);
+}
+
+extern "C" int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroups, int part,
+                                         void* stream) {
+  RGBAC_REQUIRE(part >= 0 && part <= 2, "part must be 0 (all), 1 (main) or 2 (split-K epilogue)");
   RGBAC_REQUIRE(args != nullptr, "null args");
   RGBAC_REQUIRE(ngroups >= 1 && ngroups <= kMaxGroups, "ngroups must be 1..10");
   const rgbac_conv_args* a = &args[0];
@@ -1823,8 +1838,8 @@ extern "C" int rgbac_conv2d_grouped(const rgbac_conv_args* args, int ngroups, vo
     if (b->cout > max_cout) max_cout = b->cout;
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (a->dtype == RGBAC_F32) return launch_conv<float>(d, a->tile, max_cout, st);
-  return launch_conv<bf16_t>(d, a->tile, max_cout, st);
+  if (a->dtype == RGBAC_F32) return launch_conv<float>(d, a->tile, max_cout, st, part);
+  return launch_conv<bf16_t>(d, a->tile, max_cout, st, part);
 }
 
 extern "C" int rgbac_conv2d(const rgbac_conv_args* a, void* stream) {

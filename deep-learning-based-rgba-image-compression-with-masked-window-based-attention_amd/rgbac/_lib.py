@@ -85,7 +85,12 @@ SIGNATURES = {
     "rgbac_conv2d": [ctypes.POINTER(ConvArgs), _VP],
     "rgbac_conv_num_tiles": [],
     "rgbac_conv2d_grouped": [ctypes.c_void_p, _I32, _VP],
+    "rgbac_conv2d_grouped_part": [ctypes.c_void_p, _I32, _I32, _VP],
     "rgbac_conv_max_groups": [],
+    "rgbac_timer_create": [ctypes.POINTER(ctypes.c_void_p)],
+    "rgbac_timer_record": [_VP, _VP],
+    "rgbac_timer_elapsed_ms": [_VP, _VP, ctypes.POINTER(ctypes.c_float)],
+    "rgbac_timer_destroy": [_VP],
     "rgbac_winattn_core": [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _F,
                            _VP, _I64, _VP, _VP, _VP, _I64, _VP, _VP],
     "rgbac_gaussian_slice": [_I32, _I64, _I32, _VP, _I64, _VP, _I64, _VP, _I64, _VP,

@@ -68,7 +68,7 @@ def run_residual_units_fused(pairs):
     npix = x0.B * x0.H * x0.W
     C = x0.C
     flops = 2.0 * npix * len(pairs) * (C * C // 2 * 2 + 9 * (C // 2) ** 2)
-    rt.timed("ru_fused_kernel<bf16,192>", flops, 2 * npix * len(pairs) * 2 * C,
+    rt.timed(f"ru_fused_kernel<{C}, {C // 2}>", flops, 2 * npix * len(pairs) * 2 * C,
              lambda: _lib.call("rgbac_residual_unit", ctypes.addressof(arr), len(pairs),
                                _lib.stream_ptr(x0.t.device)),
              f"ru_fused_kernel g{len(pairs)} C{C} {x0.H}x{x0.W} B{x0.B}")

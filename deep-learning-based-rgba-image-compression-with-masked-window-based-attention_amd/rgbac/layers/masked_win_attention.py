@@ -100,7 +100,11 @@ class WindowAttention(nn.Module):
             sel = torch.empty((x.B, x.H, x.W), dtype=torch.uint8, device=x.t.device)
             alpha = alpha.contiguous().float()
         npix = x.B * x.H * x.W
-        rt.timed(f"winattn_core_kernel<{'f32' if dt == torch.float32 else 'bf16'},{ws}>",
+        dh = C // self.num_heads
+        tname = "float" if dt == torch.float32 else "bf16_t"
+        kname = (f"winattn_mfma_kernel<{tname}, {ws}, {dh}>" if (ws, dh) in ((8, 24), (4, 10))
+                 else f"winattn_core_kernel<{tname}, {ws}>")    # rocprofv3's kernel names
+        rt.timed(kname,
                   4.0 * npix * ws * ws * C, qkv.t.element_size() * npix * 4 * C,
                   lambda: _lib.call(
                       "rgbac_winattn_core", _lib.dtype_code(dt), x.B, x.H, x.W, C, self.num_heads,

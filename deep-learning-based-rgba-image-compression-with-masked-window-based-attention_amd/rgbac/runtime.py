@@ -30,13 +30,41 @@ PROFILER = None
 PARAM_GEN = 0
 
 
-class LaunchProfiler:
+class _Timer:
+    """A fence-free HIP event (rgbac_timer_*): recording it does not write back / invalidate
+    the caches, and on a capturing stream it becomes an event node of the HIP graph."""
+    __slots__ = ("h",)
+
     def __init__(self):
-        self.records = []   # (kernel name, flops, bytes, start event, end event)
+        h = ctypes.c_void_p()
+        _lib.call("rgbac_timer_create", ctypes.byref(h))
+        self.h = h
+
+    def record(self):
+        _lib.call("rgbac_timer_record", self.h, _lib.stream_ptr())
+
+    def elapsed_ms(self, end):
+        ms = ctypes.c_float()
+        _lib.call("rgbac_timer_elapsed_ms", self.h, end.h, ctypes.byref(ms))
+        return ms.value
+
+    def __del__(self):
+        try:
+            _lib.load().rgbac_timer_destroy(self.h)
+        except Exception:
+            pass
+
+
+class LaunchProfiler:
+    """Per-launch GPU times from fence-free HIP events recorded on the launching stream
+    around every launch (works eagerly and inside a HIP-graph capture: read the times after
+    a replay of the captured graph)."""
+
+    def __init__(self):
+        self.records = []   # (kernel name, flops, bytes, start timer, end timer, desc)
 
     def wrap(self, name, flops, nbytes, fn, desc=None):
-        s = torch.cuda.Event(enable_timing=True)
-        e = torch.cuda.Event(enable_timing=True)
+        s, e = _Timer(), _Timer()
         s.record()
         fn()
         e.record()
@@ -48,11 +76,10 @@ class LaunchProfiler:
         for name, fl, nb, s, e, _ in self.records:
             d = out.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0, "bytes": 0.0})
             d["launches"] += 1
-            d["ms"] += s.elapsed_time(e)
+            d["ms"] += s.elapsed_ms(e)
             d["flops"] += fl
             d["bytes"] += nb
         return out
-
 
     def layers(self):
         """Per-descriptor totals: {desc: [launches, ms, flops, bytes]}."""
@@ -61,7 +88,7 @@ class LaunchProfiler:
         for name, fl, nb, s, e, desc in self.records:
             d = out.setdefault(desc, [0, 0.0, 0.0, 0.0])
             d[0] += 1
-            d[1] += s.elapsed_time(e)
+            d[1] += s.elapsed_ms(e)
             d[2] += fl
             d[3] += nb
         return out
@@ -404,6 +431,36 @@ def _spatial_ok(preps):
                 p.a.cout <= 32 for p in preps))
 
 
+# C++ template arguments (BM, BN, WGM, WGN, NBUF) of the streaming/persistent tiles, so the
+# profiler's kernel names are exactly rocprofv3's (csrc/conv.hip launch_conv).
+_TILE_SIG = {0: "128, 128, 2, 2, 2", 1: "128, 64, 4, 1, 3", 2: "64, 64, 2, 2, 3",
+             3: "128, 32, 4, 1, 3", 4: "64, 32, 2, 2, 3", 5: "128, 16, 4, 1, 3",
+             6: "64, 16, 4, 1, 3", 20: "128, 128, 2, 2, 4", 21: "128, 64, 4, 1, 5",
+             22: "64, 64, 2, 2, 6", 23: "128, 32, 4, 1, 6", 24: "64, 32, 2, 2, 8",
+             25: "128, 16, 4, 1, 6", 26: "64, 16, 4, 1, 8"}
+_SMALLK_NKS = {1: 1, 2: 2, 3: 3, 4: 4, 5: 5, 6: 6, 7: 8, 8: 8, 9: 12, 10: 12, 11: 12, 12: 12}
+
+
+def kernel_name(tile, preps):
+    """rocprofv3-style name (namespace and argument list stripped) of a conv launch."""
+    dt = "float" if preps[0].a.dtype == 0 else "bf16_t"
+    if tile == TILE_SPATIAL:
+        return f"conv3x3_c32_kernel<{dt}>"
+    if tile == TILE_SMALLK:
+        cout = max(p.pk.cout for p in preps)
+        nt = 1 if cout <= 32 else (2 if cout <= 64 else 3)
+        nks = -(-max(p.a.cin_pad for p in preps) // 16)
+        return f"conv_smallk_kernel<{nt}, {_SMALLK_NKS.get(nks, 16)}>"
+    if FIRST_DIRECT <= tile < FIRST_DEEP:
+        return f"conv_direct_kernel<{dt},{TILES[tile][1] // 16}>"
+    if FIRST_WRES <= tile < FIRST_DIRECT:
+        bm, bn = TILES[tile]
+        return f"conv_wres_kernel<{dt},{bm}x{bn}>"
+    if tile >= FIRST_PERS:
+        return f"conv_pers_kernel<{dt}, {_TILE_SIG[tile - FIRST_PERS]}>"
+    return f"conv_kernel<{dt}, {_TILE_SIG[tile]}>"
+
+
 def _smallk_ok(preps):
     a = preps[0].a
     return (a.dtype == _lib.BF16 and a.mode == CONV and a.act != ACT["gauss"] and
@@ -479,16 +536,19 @@ def launch(preps):
     if PROFILER is None:
         run()
     else:
-        bm, bn = TILES[choice[0]]
-        kname = ("conv3x3_c32_kernel" if choice[0] == TILE_SPATIAL else
-                 "conv_smallk_kernel" if choice[0] == TILE_SMALLK else
-                 "conv_direct_kernel" if FIRST_DIRECT <= choice[0] < FIRST_DEEP else
-                 "conv_wres_kernel" if FIRST_WRES <= choice[0] < FIRST_DIRECT else
-                 "conv_pers_kernel" if choice[0] >= FIRST_PERS else "conv_kernel")
-        name = f"{kname}<{'f32' if p0.a.dtype == 0 else 'bf16'},{bm}x{bn}>"
+        name = kernel_name(choice[0], preps)
         desc = f"{name} ks{choice[1]} g{n} {p0.desc}"
+        # main kernel and split-K reduce timed separately (rocprofv3 lists them apart)
         PROFILER.wrap(name, sum(pr.flops for pr in preps), sum(pr.nbytes for pr in preps),
-                      run, desc)
+                      lambda: _lib.call("rgbac_conv2d_grouped_part", ctypes.addressof(arr), n, 1,
+                                        _lib.stream_ptr(dev)), desc)
+        if choice[1] > 1:
+            dts = "float" if p0.a.dtype == 0 else "bf16_t"
+            PROFILER.wrap(f"conv_splitk_epilogue<{dts}>", 0.0,
+                          sum(4.0 * choice[1] * pr.mgrid * pr.nphase * pr.pk.cout for pr in preps),
+                          lambda: _lib.call("rgbac_conv2d_grouped_part", ctypes.addressof(arr), n,
+                                            2, _lib.stream_ptr(dev)),
+                          f"conv_splitk_epilogue ks{choice[1]} g{n} {p0.desc}")
     return [pr.out for pr in preps]
 
 

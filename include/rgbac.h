@@ -133,6 +133,11 @@ int rgbac_conv_num_tiles(void);
 int rgbac_conv2d_grouped(const rgbac_conv_args* args, int ngroups, void* stream);
 int rgbac_conv_max_groups(void);
 
+/* rgbac_conv2d_grouped split into its two launches, for per-kernel timing (bench.py's
+ * launch profiler): part 1 = the main conv kernel only, part 2 = the split-K reduce +
+ * epilogue kernels only (a no-op when ksplit == 1), part 0 = both (== grouped). */
+int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroups, int part, void* stream);
+
 /* Attention core of masked shifted-window MSA on a precomputed qkv tensor
  * (qkv = Linear(C,3C) applied per pixel by rgbac_conv2d).  For every window
  * of the cyclically shifted frame: activity = any(alpha != 0) over the
@@ -334,6 +339,15 @@ int rgbac_colsum(int dtype, int64_t npix, int channels, const void* x, int64_t l
                  float* partial, void* stream);
 /* out[r] = (float) sum_j partial[r][j]  (fixed order; bits sums -> loss scalars). */
 int rgbac_sum_partials(int rows, int n, const double* partial, float* out, void* stream);
+
+/* Kernel timing (bench.py's launch profiler; no reference counterpart).  Events are created
+ * with hipEventDisableSystemFence (no cache writeback/invalidate per record); recorded on a
+ * capturing stream they become external event nodes of the HIP graph, so per-launch times
+ * can be read from a graph replay.  rgbac_timer_elapsed_ms needs both events completed. */
+int rgbac_timer_create(void** event);
+int rgbac_timer_record(void* event, void* stream);
+int rgbac_timer_elapsed_ms(void* start, void* stop, float* ms);
+int rgbac_timer_destroy(void* event);
 
 #ifdef __cplusplus
 }
