@@ -95,6 +95,18 @@ template <typename T> __device__ __forceinline__ float gelu_t(float v);
 template <> __device__ __forceinline__ float gelu_t<float>(float v) { return gelu_f(v); }
 template <> __device__ __forceinline__ float gelu_t<bf16_t>(float v) { return gelu_fast(v); }
 __device__ __forceinline__ float sigmoid_f(float v) { return 1.0f / (1.0f + expf(-v)); }
+// GDN / IGDN output x / sqrt(n), x * sqrt(n): IEEE sqrt + divide in the fp32 parity mode,
+// the hardware rsq / sqrt (~1 ulp fp32) where the result is stored as bf16
+template <typename T> __device__ __forceinline__ float gdn_t(float x, float n);
+template <> __device__ __forceinline__ float gdn_t<float>(float x, float n) { return x / sqrtf(n); }
+template <> __device__ __forceinline__ float gdn_t<bf16_t>(float x, float n) {
+  return x * __builtin_amdgcn_rsqf(n);
+}
+template <typename T> __device__ __forceinline__ float igdn_t(float x, float n);
+template <> __device__ __forceinline__ float igdn_t<float>(float x, float n) { return x * sqrtf(n); }
+template <> __device__ __forceinline__ float igdn_t<bf16_t>(float x, float n) {
+  return x * __builtin_amdgcn_sqrtf(n);
+}
 __device__ __forceinline__ float std_cum_f(float t) {
   return 0.5f * erfcf(-0.70710678118654752440f * t);
 }
@@ -250,11 +262,11 @@ __device__ __forceinline__ void epilogue4_fin(const ConvShared& s, const ConvGro
       break;
     case RGBAC_ACT_GDN:
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = r1[r] / sqrtf(v[r]);
+      for (int r = 0; r < 4; ++r) v[r] = gdn_t<T>(r1[r], v[r]);
       break;
     case RGBAC_ACT_IGDN:
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = r1[r] * sqrtf(v[r]);
+      for (int r = 0; r < 4; ++r) v[r] = igdn_t<T>(r1[r], v[r]);
       break;
     case RGBAC_ACT_MASKSEL: {
 #pragma unroll
@@ -395,8 +407,8 @@ __device__ __forceinline__ void epilogue_row(const ConvShared& s, const ConvGrou
         case RGBAC_ACT_LRELU: x = x > 0.f ? x : x * s.act_param; break;
         case RGBAC_ACT_TANH_HALF: x = r1[j][r] + 0.5f * tanhf(x); break;
         case RGBAC_ACT_GATE: x = r1[j][r] * sigmoid_f(x); break;
-        case RGBAC_ACT_GDN: x = r1[j][r] / sqrtf(x); break;
-        case RGBAC_ACT_IGDN: x = r1[j][r] * sqrtf(x); break;
+        case RGBAC_ACT_GDN: x = gdn_t<T>(r1[j][r], x); break;
+        case RGBAC_ACT_IGDN: x = igdn_t<T>(r1[j][r], x); break;
         case RGBAC_ACT_MASKSEL: x = on ? r1[j][r] + x : r1[j][r]; break;
         default: break;
       }

@@ -103,6 +103,8 @@ SIGNATURES = {
     "rgbac_nchw_to_nhwc": [_I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP],
     "rgbac_nhwc_to_nchw": [_I32, _I32, _I32, _I32, _I32, _VP, _I64, _VP, _VP],
     "rgbac_residual_unit": [_VP, _I32, _VP],
+    "rgbac_stem_gdn": [_I32, _I32, _I32, _VP, _I64, _VP, _I32, _VP, _VP, _I32, _VP, _I32, _VP,
+                       _I64, _VP],
     # training step
     "rgbac_act_bwd": [_I32, _I32, _F, _I64, _I32, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP,
                       _I64, _VP, _I64, _VP],

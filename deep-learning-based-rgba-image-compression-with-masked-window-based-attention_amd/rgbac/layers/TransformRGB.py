@@ -108,8 +108,28 @@ class Analysis_transform(nn.Module):
         self.x4 = nn.Conv2d(N, M, 1, stride=1, padding=0)
         self.attention2 = Win_noShift_Attention(dim=M, num_heads=8, window_size=4, shift_size=2)
 
+    def _stem(self, x):
+        """x1 -> gdn1 (TransformRGB.py:66).  bf16 with the reference's 5x5/s2 3 -> 192 stem:
+        one fused launch (rgbac_stem_gdn) that never writes the stem output to HBM."""
+        m = self.x1
+        if (x.t.dtype == torch.bfloat16 and x.ldc == 8 and m.out_channels == 192 and
+                m.kernel_size == (5, 5) and m.stride == (2, 2) and m.padding == (2, 2) and
+                not self.gdn1.inverse and rt.STEM_FUSED):
+            pk1 = rt.packed(m, x.t.dtype, rt.segs_of(x.src()))
+            pk2 = self.gdn1._pack(x.t.dtype, 192)
+            out = rt.new_feat(x.B, (x.H + 1) // 2, (x.W + 1) // 2, 192, x.t.dtype, x.t.device)
+            rt.timed("stem_gdn_kernel", 2.0 * out.B * out.H * out.W * 192 * (75 + 192),
+                     2.0 * (x.B * x.H * x.W * 8 + out.B * out.H * out.W * 192),
+                     lambda: rt._lib.call("rgbac_stem_gdn", x.B, x.H, x.W, x.ptr(), x.ldc,
+                                          pk1.w.data_ptr(), pk1.k_pad, pk1.bias.data_ptr(),
+                                          pk2.w.data_ptr(), pk2.k_pad, pk2.bias.data_ptr(), 0,
+                                          out.ptr(), out.ldc, rt._lib.stream_ptr(x.t.device)),
+                     f"stem_gdn_kernel 3->192 {x.H}x{x.W} B{x.B}")
+            return out
+        return self.gdn1.nhwc(run_conv(m, [x.src()]))
+
     def nhwc(self, x, me2, me3):
-        y = self.gdn1.nhwc(run_conv(self.x1, [x.src()]))
+        y = self._stem(x)
         y = self.gdn2.nhwc(run_conv(self.x2, [y.src()]))
         y = self.attention1.nhwc(y, me2)
         y = self.gdn3.nhwc(run_conv(self.x3, [y.src()]))

@@ -136,6 +136,7 @@ TUNE = os.environ.get("RGBAC_TUNE", "1") != "0"
 TILE_SET = os.environ.get("RGBAC_TILE_SET", "stream")
 _tune_cache = {}          # shape key -> (tile, ksplit)
 FORCE = None              # (tile, ksplit) override, used by the tile/split-K tests
+STEM_FUSED = os.environ.get("RGBAC_STEM_FUSED", "1") != "0"   # x1 + gdn1 as one launch (bf16)
 
 
 def pick_cout_pad(cout):

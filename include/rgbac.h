@@ -340,6 +340,16 @@ int rgbac_colsum(int dtype, int64_t npix, int channels, const void* x, int64_t l
 /* out[r] = (float) sum_j partial[r][j]  (fixed order; bits sums -> loss scalars). */
 int rgbac_sum_partials(int rows, int n, const double* partial, float* out, void* stream);
 
+/* Fused analysis stem (bf16): conv5x5/s2/p2 of an NHWC input with 8 (zero-padded) channels
+ * to 192 channels, then GDN (inverse=0) or IGDN (1), writing only the GDN output.
+ * Replaces layers/TransformRGB.py:55-56,66 (self.x1 -> self.gdn1) with layers/GDN.py:64-94.
+ * w1: packed conv weights [>=192 rows][w1_kpad], k = tap*8 + c (rgbac_conv2d's layout),
+ * b1: its bias (or NULL); w2: gamma' packed [>=192][w2_kpad]; beta: beta' [192];
+ * out: NHWC bf16 [batch][ceil(h/2)][ceil(w/2)][out_ldc]. */
+int rgbac_stem_gdn(int batch, int in_h, int in_w, const void* x, int64_t x_ldc, const void* w1,
+                   int w1_kpad, const float* b1, const void* w2, int w2_kpad, const float* beta,
+                   int inverse, void* out, int64_t out_ldc, void* stream);
+
 /* Kernel timing (bench.py's launch profiler; no reference counterpart).  Events are created
  * with hipEventDisableSystemFence (no cache writeback/invalidate per record); recorded on a
  * capturing stream they become external event nodes of the HIP graph, so per-launch times

@@ -411,3 +411,32 @@ def test_conv_smallk_tile(device, cin, cout, k, s, act):
         assert rel(got, want) < 2e-2
     finally:
         rt.FORCE = None
+
+
+@pytest.mark.parametrize("H,W", [(64, 96), (256, 256), (40, 72)])
+def test_stem_gdn_fused(device, H, W):
+    """Fused x1 (conv5x5/s2 3->192) + gdn1 (bf16) against the unfused bf16 kernels and the
+    fp32 torch formula of TransformRGB.py:66 / GDN.py:64-94."""
+    rt = _rt()
+    from rgbac.layers.TransformRGB import Analysis_transform, run_conv
+    torch.manual_seed(7)
+    enc = Analysis_transform(192, 80)
+    with torch.no_grad():
+        enc.gdn1.gamma.add_(0.05 * torch.rand_like(enc.gdn1.gamma))   # non-diagonal gamma'
+    g = _gen(H * W)
+    x = torch.rand((2, 3, H, W), generator=g)
+    with torch.no_grad():
+        y = enc.x1(x)
+        beta, gamma = enc.gdn1.effective_params()
+        want = y / torch.sqrt(F.conv2d(y * y, gamma.reshape(192, 192, 1, 1), beta))
+    enc = enc.to(device)
+    with torch.no_grad():
+        fx = rt.to_nhwc(x.to(device), torch.bfloat16)
+        fused = rt.to_nchw(enc._stem(fx))
+        rt.STEM_FUSED = False
+        try:
+            unfused = rt.to_nchw(enc._stem(fx))
+        finally:
+            rt.STEM_FUSED = True
+    assert rel(fused, unfused) < 1e-2
+    assert rel(fused, want) < 2e-2
