@@ -23,6 +23,8 @@
 // stage 2 has consumed it, ring 2 x 15 KB -> 51 KB: three workgroups per CU.
 // Weight chunks are prefetched PF = 4 chunks ahead in registers (the chunk
 // loops are fully unrolled so the register ring is statically indexed).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace rgbac {
@@ -43,9 +45,15 @@ struct RuArgsDev {
 
 __device__ __forceinline__ float ru_gelu(float v) { return gelu_fast(v); }   // bf16 outputs
 
-template <int C, int CH>
-__global__ void __launch_bounds__(256, 3) ru_fused_kernel(const RuArgsDev args) {
-  constexpr int TS = 8, HS = TS + 2, NH = HS * HS;     // 8x8 tile, 10x10 halo
+template <int C, int CH, int TY, int TX, int OCC>
+__global__ void __launch_bounds__(256, OCC) ru_fused_kernel(const RuArgsDev args) {
+  // TY x TX output tile, (TY+2) x (TX+2) halo; 8x16 halves the weight traffic per pixel
+  // (every tile streams all three weight matrices once) at 2 workgroups per CU
+  constexpr int HY = TY + 2, HX = TX + 2, NH = HY * HX;
+  constexpr int MT1 = (NH + 63) / 64;                  // stage-1 m tiles per wave
+  constexpr int NPX = TY * TX;                         // output pixels per tile
+  constexpr int MT2 = NPX / 32;                        // stage-2/3 m tiles per wave
+  static_assert(NPX % 32 == 0 && NH >= NPX, "tile geometry");
   constexpr int NT1 = CH / 16;                         // n tiles of stages 1 / 2
   constexpr int NT3 = C / 16;                          // n tiles of stage 3
   constexpr int TROW = CH * 2;    // T1 / T2 row bytes: unpadded rows give at most 2-way
@@ -68,12 +76,12 @@ __global__ void __launch_bounds__(256, 3) ru_fused_kernel(const RuArgsDev args) 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
-  const int tx_n = args.W / TS, ty_n = args.H / TS;
+  const int tx_n = args.W / TX, ty_n = args.H / TY;
   int t = blockIdx.x;
   const int tx = t % tx_n; t /= tx_n;
   const int ty = t % ty_n;
   const int b = t / ty_n;
-  const int y0 = ty * TS, x0 = tx * TS;
+  const int y0 = ty * TY, x0 = tx * TX;
 
   // ---- weight ring: chunk c -> 3 pieces of 16 B per thread, staged in registers
   // set c % 5 of five named register sets (selects fold after full unrolling;
@@ -140,28 +148,28 @@ __global__ void __launch_bounds__(256, 3) ru_fused_kernel(const RuArgsDev args) 
 
   // ======================= stage 1: T1 = GELU(W1 x + b1) on the 10x10 halo
   {
-    f32x4 acc[NT1][2];
+    f32x4 acc[NT1][MT1];
 #pragma unroll
     for (int j = 0; j < NT1; ++j)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const bf16_t* xrow[2];
-    bool xin[2];
+      for (int i = 0; i < MT1; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bf16_t* xrow[MT1];
+    bool xin[MT1];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int hp = wave * 32 + i * 16 + fr;
-      const int hy = hp / HS, hx = hp - (hp / HS) * HS;
+    for (int i = 0; i < MT1; ++i) {
+      const int hp = wave * (16 * MT1) + i * 16 + fr;
+      const int hy = hp / HX, hx = hp - (hp / HX) * HX;
       const int iy = y0 + hy - 1, ix = x0 + hx - 1;
       xin[i] = hp < NH && iy >= 0 && iy < args.H && ix >= 0 && ix < args.W;
       xrow[i] = g.x + ((long long)(b * args.H + (xin[i] ? iy : 0)) * args.W + (xin[i] ? ix : 0)) * g.ldx;
     }
 #pragma unroll
     for (int c = 0; c < KC1; ++c) {
-      uint4 xb[2][2];
+      uint4 xb[2][MT1];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < MT1; ++i)
           xb[kk][i] = xin[i] ? *reinterpret_cast<const uint4*>(xrow[i] + c * 64 + kk * 32 + fq * 8)
                              : make_uint4(0, 0, 0, 0);
       const int buf = c & 1;
@@ -171,7 +179,7 @@ __global__ void __launch_bounds__(256, 3) ru_fused_kernel(const RuArgsDev args) 
         for (int j = 0; j < NT1; ++j) {
           const uint4 a = wfrag64(buf, j, kk);
 #pragma unroll
-          for (int i = 0; i < 2; ++i) mma_step<bf16_t>(acc[j][i], a, xb[kk][i]);
+          for (int i = 0; i < MT1; ++i) mma_step<bf16_t>(acc[j][i], a, xb[kk][i]);
         }
       store_w(c + 1, buf ^ 1);
       load_w(c + PF + 1);
@@ -179,8 +187,8 @@ __global__ void __launch_bounds__(256, 3) ru_fused_kernel(const RuArgsDev args) 
     }
     // epilogue -> T1 (zero outside the image: the 3x3's zero padding)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int hp = wave * 32 + i * 16 + fr;
+    for (int i = 0; i < MT1; ++i) {
+      const int hp = wave * (16 * MT1) + i * 16 + fr;
       if (hp >= NH) continue;
 #pragma unroll
       for (int j = 0; j < NT1; ++j) {
@@ -201,17 +209,17 @@ __global__ void __launch_bounds__(256, 3) ru_fused_kernel(const RuArgsDev args) 
   // ======================= stage 2: T2 = GELU(W2 (*) T1 + b2), 3x3 over the halo
   {
     constexpr int NJ = NT1 / 2;                       // 3 channel tiles per wave
-    f32x4 acc[NJ][2];
+    f32x4 acc[NJ][MT2];
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-    int py[2], px[2];
+      for (int i = 0; i < MT2; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    int py[MT2], px[MT2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int p = wm * 32 + i * 16 + fr;            // this lane's pixel of m tile i
-      py[i] = p >> 3;
-      px[i] = p & 7;
+    for (int i = 0; i < MT2; ++i) {
+      const int p = wm * (NPX / 2) + i * 16 + fr;     // this lane's pixel of m tile i
+      py[i] = p / TX;
+      px[i] = p % TX;
     }
 #pragma unroll
     for (int c2 = 0; c2 < KC2; ++c2) {
@@ -221,12 +229,12 @@ __global__ void __launch_bounds__(256, 3) ru_fused_kernel(const RuArgsDev args) 
       for (int kk = 0; kk < 2; ++kk) {
         const int k = c2 * 64 + kk * 32;              // a 32-k step never straddles taps
         const int tap = k / CH, ch = k - tap * CH + fq * 8;
-        uint4 bv[2];
+        uint4 bv[MT2];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < MT2; ++i) {
           bv[i] = make_uint4(0, 0, 0, 0);
           if (tap < 9) {
-            const int hr = (py[i] + tap / 3) * HS + px[i] + tap % 3;
+            const int hr = (py[i] + tap / 3) * HX + px[i] + tap % 3;
             bv[i] = *reinterpret_cast<const uint4*>(&T1[hr * TROW + ch * 2]);
           }
         }
@@ -234,7 +242,7 @@ __global__ void __launch_bounds__(256, 3) ru_fused_kernel(const RuArgsDev args) 
         for (int j = 0; j < NJ; ++j) {
           const uint4 a = wfrag64(buf, wn * NJ + j, kk);
 #pragma unroll
-          for (int i = 0; i < 2; ++i) mma_step<bf16_t>(acc[j][i], a, bv[i]);
+          for (int i = 0; i < MT2; ++i) mma_step<bf16_t>(acc[j][i], a, bv[i]);
         }
       }
       store_w(c + 1, buf ^ 1);
@@ -242,8 +250,8 @@ __global__ void __launch_bounds__(256, 3) ru_fused_kernel(const RuArgsDev args) 
       __syncthreads();                  // (last one: every wave is done reading T1)
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int p = wm * 32 + i * 16 + fr;
+    for (int i = 0; i < MT2; ++i) {
+      const int p = wm * (NPX / 2) + i * 16 + fr;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int n = (wn * NJ + j) * 16 + fq * 4;
@@ -259,35 +267,35 @@ __global__ void __launch_bounds__(256, 3) ru_fused_kernel(const RuArgsDev args) 
   // ======================= stage 3: y = GELU(W3 T2 + b3 + x)
   {
     constexpr int NJ = NT3 / 2;                       // 6 channel tiles per wave
-    f32x4 acc[NJ][2];
+    f32x4 acc[NJ][MT2];
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int i = 0; i < MT2; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int c3 = 0; c3 < KC3; ++c3) {
       const int c = KC1 + KC2 + c3;
       const int buf = c & 1;
-      uint4 bv[2];
+      uint4 bv[MT2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int p = wm * 32 + i * 16 + fr;
+      for (int i = 0; i < MT2; ++i) {
+        const int p = wm * (NPX / 2) + i * 16 + fr;
         bv[i] = *reinterpret_cast<const uint4*>(&T2[p * TROW + (c3 * 32 + fq * 8) * 2]);
       }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const uint4 a = wfrag32(buf, wn * NJ + j);
 #pragma unroll
-        for (int i = 0; i < 2; ++i) mma_step<bf16_t>(acc[j][i], a, bv[i]);
+        for (int i = 0; i < MT2; ++i) mma_step<bf16_t>(acc[j][i], a, bv[i]);
       }
       store_w(c + 1, buf ^ 1);
       load_w(c + PF + 1);
       __syncthreads();
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int p = wm * 32 + i * 16 + fr;
-      const int py = p >> 3, px = p & 7;
+    for (int i = 0; i < MT2; ++i) {
+      const int p = wm * (NPX / 2) + i * 16 + fr;
+      const int py = p / TX, px = p % TX;
       const long long pix = (long long)(b * args.H + y0 + py) * args.W + x0 + px;
       const bf16_t* xr = g.x + pix * g.ldx;
       bf16_t* orow = g.out + pix * g.ldo;
@@ -341,10 +349,21 @@ extern "C" int rgbac_residual_unit(const rgbac_ru_args* args, int ngroups, void*
     g.b1 = q->b1; g.b2 = q->b2; g.b3 = q->b3;
     g.out = (bf16_t*)q->out; g.ldo = q->out_ldc;
   }
-  const long long tiles = (long long)a->batch * (a->h / 8) * (a->w / 8);
-  RGBAC_REQUIRE(tiles < (1ll << 31), "too many tiles");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL((ru_fused_kernel<192, 96>), dim3((unsigned)tiles, 1, ngroups), dim3(256), 0,
-                     st, d);
+  static const int wide_env = [] {
+    const char* e = getenv("RGBAC_RU_TILE");
+    return (e && e[0] == '8') ? 0 : 1;              // RGBAC_RU_TILE=8: the 8x8 tile
+  }();
+  if (wide_env && a->w % 16 == 0) {
+    const long long tiles = (long long)a->batch * (a->h / 8) * (a->w / 16);
+    RGBAC_REQUIRE(tiles < (1ll << 31), "too many tiles");
+    hipLaunchKernelGGL((ru_fused_kernel<192, 96, 8, 16, 2>), dim3((unsigned)tiles, 1, ngroups),
+                       dim3(256), 0, st, d);
+  } else {
+    const long long tiles = (long long)a->batch * (a->h / 8) * (a->w / 8);
+    RGBAC_REQUIRE(tiles < (1ll << 31), "too many tiles");
+    hipLaunchKernelGGL((ru_fused_kernel<192, 96, 8, 8, 3>), dim3((unsigned)tiles, 1, ngroups),
+                       dim3(256), 0, st, d);
+  }
   return check_launch("ru_fused_kernel");
 }
