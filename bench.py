@@ -115,13 +115,17 @@ def cpu_baseline_train(budget_s):
                       f"(half-transparent alpha), {n} timed iterations after 1 warm-up, {dt:.1f} s"}
 
 
-def pmc_traffic(kernel, path):
+def pmc_traffic(kernel, path, config=None):
     """HBM bytes per dispatch of ``kernel`` from a committed rocprofv3 PMC summary
-    (tools/pmc_bench.sh + tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE), or None."""
+    (tools/profile_round.sh + tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE) taken on the
+    same workload (``config``: batch / size / dtype), or None."""
     if not path or not os.path.exists(path):
         return None
     with open(path) as fh:
-        ent = json.load(fh).get("kernels", {}).get(kernel)
+        d = json.load(fh)
+    if config is not None and d.get("config") not in (None, config):
+        return None
+    ent = d.get("kernels", {}).get(kernel)
     return None if ent is None else ent["hbm_bytes_per_dispatch"]
 
 
@@ -136,7 +140,7 @@ def tune_cache_setup(args, default):
     return None
 
 
-def roofline_of(summ, dtype, nrep, traffic_file=None):
+def roofline_of(summ, dtype, nrep, traffic_file=None, config=None):
     total_ms = sum(d["ms"] for d in summ.values())
     dom_name, dom = max(summ.items(), key=lambda kv: kv[1]["ms"])
     per_ms = dom["ms"] / dom["launches"]
@@ -144,7 +148,8 @@ def roofline_of(summ, dtype, nrep, traffic_file=None):
     achieved = per_fl / (per_ms * 1e-3) / 1e12
     peak = PEAK[dtype]["mfma"]
     return {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-            "frac": round(achieved / peak, 4), "traffic": pmc_traffic(dom_name, traffic_file),
+            "frac": round(achieved / peak, 4),
+            "traffic": pmc_traffic(dom_name, traffic_file, config),
             "kernel": dom_name,
             "avg_launch_us": round(per_ms * 1e3, 2),
             "algorithmic_gflop_per_launch": round(per_fl / 1e9, 4),
@@ -361,7 +366,8 @@ def main():
             write_layers(prof, args.layers, nrep)
         traffic_file = args.traffic_file if args.traffic_file is not None else \
             os.path.join(ROOT, "profiles", "r01_pmc_traffic_fwd.json")
-        roof, total_ms = roofline_of(summ, args.dtype, nrep, traffic_file)
+        roof, total_ms = roofline_of(summ, args.dtype, nrep, traffic_file,
+                                     {"batch": B, "size": S, "dtype": args.dtype})
         roof["timing"] = "eager steps behind a GPU spin, fence-free HIP events per launch"
         if roof["traffic"] is not None:
             roof["traffic_source"] = os.path.relpath(traffic_file, ROOT)

@@ -57,6 +57,7 @@ def main(fetch_csv, write_csv, out):
     with open(out, "w") as fh:
         json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over "
                              "tools/graph_trace.py forward graph replays; FETCH_SIZE x2 (gfx950)",
+                   "config": {"batch": 8, "size": 256, "dtype": "bf16"},
                    "kernels": res}, fh, indent=1)
     for k, v in sorted(res.items(), key=lambda kv: -kv[1]["hbm_bytes_per_dispatch"]):
         print(f"{v['hbm_bytes_per_dispatch'] / 1e6:9.2f} MB/dispatch  {k}")
