@@ -106,7 +106,9 @@ int check_launch(const char* what);
 constexpr int kReduceThreads = 256;
 constexpr int kReduceMaxBlocks = 1024;
 inline int reduce_blocks(int64_t n) {
-  int64_t b = (n + kReduceThreads * 4 - 1) / (kReduceThreads * 4);
+  // one element per thread up to the block cap: the per-element entropy math (factorized
+  // density MLP, erfc) is latency-bound, so spreading it wide beats per-thread loops
+  int64_t b = (n + kReduceThreads - 1) / kReduceThreads;
   if (b < 1) b = 1;
   if (b > kReduceMaxBlocks) b = kReduceMaxBlocks;
   return (int)b;

@@ -57,6 +57,7 @@ struct ConvGroup {                  // per-group operands
   double* partial;                  // GAUSS: bits per M-tile block
   void* zout;                       // training: pre-activation store (or NULL)
   long long zld;
+  int* cnt;                         // split-K tickets (in-launch reduction) or NULL
   int send0, send1, send2;          // cumulative channel ends
   int cin_pad, k_pad, cout, rows, cout16, out_coff;
 };
@@ -712,6 +713,80 @@ _Pragma("unroll")                                                               
   int nn[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) nn[j] = n0 + wn * TN * 16 + j * 16 + fq * 4;
+  if (s.ksplit > 1 && g.cnt) {
+    // split-K slab, then an in-launch reduction by the tile's last-arriving split block
+    // (agent-scope release / relaxed ticket / agent-scope acquire; cdna_hip_programming.md
+    // "In-launch split-K reduction"), so no separate reduce launch is needed
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + wm * TM * 16 + i * 16 + fr;
+      if (m >= s.M) continue;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        if (nn[j] >= g.cout) continue;
+        float* w = g.ws + (((size_t)split * s.nphase + phase) * s.M + m) * g.cout16 + nn[j];
+        *reinterpret_cast<float4*>(w) =
+            make_float4(acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(red);
+    if (tid == 0) {
+      const int tix = ((gi * s.nphase + phase) * (int)gridDim.x + mblk) * (int)gridDim.y + nblk;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int old = __hip_atomic_fetch_add(&g.cnt[tix], 1, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == s.ksplit - 1;
+      if (last) {
+        __hip_atomic_store(&g.cnt[tix], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    // R quads per thread per pass; every slab and residual load of a pass is issued before
+    // any math (the reducer pays ~one memory latency per pass, not one per load)
+    constexpr int NQ = BN / 4;
+    constexpr int R = (BM * NQ / 256) < 4 ? (BM * NQ / 256) : 4;
+    static_assert(R >= 1 && (BM * NQ) % (256 * R) == 0, "reducer geometry");
+    const size_t sstride = (size_t)s.nphase * s.M * g.cout16;
+    for (int e0 = tid; e0 < BM * NQ; e0 += 256 * R) {
+      int mq[R], nq4[R];
+      bool ok[R];
+      float v[R][4];
+#pragma unroll
+      for (int q = 0; q < R; ++q) {
+        const int e = e0 + 256 * q;
+        const int ml = e / NQ;
+        mq[q] = m0 + ml;
+        nq4[q] = n0 + 4 * (e - ml * NQ);
+        ok[q] = mq[q] < s.M && nq4[q] < g.cout;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[q][r] = 0.f;
+      }
+      const float* base = g.ws + (size_t)phase * s.M * g.cout16;
+      for (int sp = 0; sp < s.ksplit; ++sp) {
+        float4 t[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q)
+          t[q] = ok[q] ? *reinterpret_cast<const float4*>(base + sp * sstride +
+                                                          (size_t)mq[q] * g.cout16 + nq4[q])
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+          v[q][0] += t[q].x; v[q][1] += t[q].y; v[q][2] += t[q].z; v[q][3] += t[q].w;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < R; ++q)
+        if (ok[q]) epilogue4<T>(s, g, phase, mq[q], nq4[q], v[q]);
+    }
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int m = m0 + wm * TM * 16 + i * 16 + fr;
@@ -1529,8 +1604,10 @@ template <typename T>
 static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t st, int part) {
   const ConvShared& s = d.s;
   const TileCfg tc = kTiles[tile];
+  const bool inlaunch = s.ksplit > 1 && d.g[0].cnt != nullptr &&
+                        (tile < kFirstWres || (tile >= kFirstDeep && tile < kFirstPers));
   if (part == 2) {                         // split-K reduce + epilogue kernels only
-    if (s.ksplit == 1 || tile == kTileSpatial || tile == kTileSmallK ||
+    if (s.ksplit == 1 || inlaunch || tile == kTileSpatial || tile == kTileSmallK ||
         (tile >= kFirstWres && tile < kFirstDeep))
       return RGBAC_OK;
     goto splitk_epilogue;
@@ -1641,7 +1718,7 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
   }
   {
     int rc = check_launch("conv_kernel");
-    if (rc || s.ksplit == 1 || part == 1) return rc;
+    if (rc || s.ksplit == 1 || part == 1 || inlaunch) return rc;
   }
 splitk_epilogue:
   for (int gi = 0; gi < s.ngroups; ++gi) {
@@ -1694,6 +1771,7 @@ static int fill_group(const rgbac_conv_args* a, int ntaps_max, ConvGroup& g) {
                 "SQBWD needs res0 (direct gradient), res1 (x) and no bias");
   g.zout = a->zout;
   g.zld = a->zout_ldc;
+  g.cnt = a->tile_counters;
   g.cin_pad = a->cin_pad;
   g.k_pad = a->k_pad;
   g.cout = a->cout;

@@ -44,6 +44,7 @@ class ConvArgs(ctypes.Structure):
         ("workspace", ctypes.c_void_p),
         ("aux0", ctypes.c_void_p), ("aux1", ctypes.c_void_p), ("partial", ctypes.c_void_p),
         ("zout", ctypes.c_void_p), ("zout_ldc", ctypes.c_int64),
+        ("tile_counters", ctypes.c_void_p),
     ]
 
 

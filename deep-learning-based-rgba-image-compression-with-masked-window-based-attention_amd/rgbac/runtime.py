@@ -473,6 +473,27 @@ def _gauss_ok(t, cout):
     return TILES[t][1] >= cout
 
 
+# Split-K tickets for the in-launch reduction (rgbac_conv_args.tile_counters): one zeroed
+# int32 buffer per device shared by every launch -- launches on a stream run one after the
+# other and the last split block of each tile resets its ticket, so it is zero again between
+# launches.  Allocated outside graph capture (the first, eager launch of a shape).
+_COUNTERS = {}
+_COUNTERS_MIN = 1 << 20
+# Off by default: measured slower end-to-end (165.6 -> 157 MPix/s) -- each split block's
+# agent-scope release writes back its XCD's L2 -- than the separate reduce launch.
+INLAUNCH_SPLITK = os.environ.get("RGBAC_INLAUNCH_SPLITK", "0") == "1"
+
+
+def _tile_counters(dev, n):
+    buf = _COUNTERS.get(dev)
+    if buf is None or buf.numel() < n:
+        if torch.cuda.is_current_stream_capturing():
+            return None                   # never allocate (and zero-fill) inside a capture
+        buf = torch.zeros(max(n, _COUNTERS_MIN), dtype=torch.int32, device=dev)
+        _COUNTERS[dev] = buf
+    return buf
+
+
 def launch(preps):
     """Launch prepared convs (same geometry) as ONE grouped kernel; returns their outputs."""
     n = len(preps)
@@ -486,8 +507,17 @@ def launch(preps):
         arr[i] = pr.a
 
     def set_choice(t, ks):
+        cnt = None
+        if ks > 1 and INLAUNCH_SPLITK and (t < FIRST_WRES or FIRST_DEEP <= t < FIRST_PERS):
+            bm, bn = TILES[t]
+            need = n * p0.nphase * (-(-p0.mgrid // bm)) * (-(-max(pr.pk.cout for pr in preps) // bn))
+            buf = _tile_counters(dev, need)
+            if buf is not None:
+                keep.append(buf)
+                cnt = buf.data_ptr()
         for i, pr in enumerate(preps):
             arr[i].tile, arr[i].ksplit = t, ks
+            arr[i].tile_counters = cnt
             arr[i].workspace = None
             if ks > 1:
                 ws = torch.empty(ks * pr.nphase * pr.mgrid * round_up(pr.pk.cout, 16),
@@ -543,7 +573,7 @@ def launch(preps):
         PROFILER.wrap(name, sum(pr.flops for pr in preps), sum(pr.nbytes for pr in preps),
                       lambda: _lib.call("rgbac_conv2d_grouped_part", ctypes.addressof(arr), n, 1,
                                         _lib.stream_ptr(dev)), desc)
-        if choice[1] > 1:
+        if choice[1] > 1 and not arr[0].tile_counters:
             dts = "float" if p0.a.dtype == 0 else "bf16_t"
             PROFILER.wrap(f"conv_splitk_epilogue<{dts}>", 0.0,
                           sum(4.0 * choice[1] * pr.mgrid * pr.nphase * pr.pk.cout for pr in preps),

@@ -107,6 +107,11 @@ typedef struct rgbac_conv_args {
   void* zout;                  /* training: pre-activation value v (after bias and
                                   res0) stored on the output grid, or NULL         */
   int64_t zout_ldc;            /* channel stride of zout (same coff as out)        */
+  int32_t* tile_counters;      /* ksplit>1 on a streaming tile (0..6, 20..26): zero-
+                                  initialised int32 tickets, one per (group, phase,
+                                  M-tile, N-tile); the last split block of a tile sums
+                                  the slabs and runs the epilogue inside the launch and
+                                  resets its ticket to 0.  NULL: separate reduce kernels */
 } rgbac_conv_args;
 
 int rgbac_abi_version(void);

@@ -440,3 +440,25 @@ def test_stem_gdn_fused(device, H, W):
             rt.STEM_FUSED = True
     assert rel(fused, unfused) < 1e-2
     assert rel(fused, want) < 2e-2
+
+
+@pytest.mark.parametrize("tile", [0, 2, 22])
+def test_conv_inlaunch_splitk(device, tile):
+    """The in-launch split-K reduction (last-arriving split block reduces; off by default)."""
+    rt = _rt()
+    from rgbac.layers.TransformRGB import run_conv
+    g = _gen(500 + tile)
+    m = nn.Conv2d(96, 80, 3, padding=1)
+    x = torch.randn((2, 96, 40, 36), generator=g)
+    r = torch.randn((2, 80, 40, 36), generator=g)
+    want = F.gelu(m(x) + r)
+    rt.FORCE, rt.INLAUNCH_SPLITK = (tile, 3), True
+    try:
+        for dt, tol in ((torch.float32, 2e-5), (torch.bfloat16, 2e-2)):
+            with torch.no_grad():
+                fx, fr = rt.to_nhwc(x.to(device), dt), rt.to_nhwc(r.to(device), dt)
+                for _ in range(2):        # second launch reuses the reset tickets
+                    got = rt.to_nchw(run_conv(m.to(device), [fx.src()], act="gelu", res0=fr))
+                    assert rel(got, want) < tol
+    finally:
+        rt.FORCE, rt.INLAUNCH_SPLITK = None, False
