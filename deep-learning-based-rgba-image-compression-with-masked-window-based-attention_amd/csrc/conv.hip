@@ -1406,7 +1406,9 @@ static const TileCfg kTiles[] = {
     // 27..33: the streaming shapes of 0..6, persistent over output tiles (conv_pers_kernel)
     {128, 128}, {128, 64}, {64, 64}, {128, 32}, {64, 32}, {128, 16}, {64, 16},
     // 34: small-K wave-streaming kernel (32-pixel wave tiles x up to 192 channels)
-    {32, 96}};
+    {32, 96},
+    // 35: narrow-output wave-streaming kernel (32-pixel wave tiles x <= 32 channels, full K)
+    {32, 32}};
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 constexpr int kFirstWres = 7;
 constexpr int kWresStages = 6;
@@ -1416,6 +1418,7 @@ constexpr int kTileSpatial = 19;   // conv3x3_c32_kernel (16x16 pixels x 32 chan
 constexpr int kFirstDeep = 20;     // 20..26: deep-ring streaming tiles
 constexpr int kFirstPers = 27;     // 27..33: persistent streaming tiles
 constexpr int kTileSmallK = 34;    // conv_smallk_kernel (bf16, plain conv, K <= 256)
+constexpr int kTileWStream = 35;   // conv_wstream_kernel (bf16, stride 1, k 1/3, cout <= 32)
 constexpr int kSmallKMax = 256;
 
 // ---------------------------------------------------------------------------
@@ -1578,6 +1581,162 @@ static void launch_smallk(const ConvArgsDev& d, int nks16, int max_cout, hipStre
   }
 }
 
+// ---------------------------------------------------------------------------
+// Narrow-output K-split kernel (bf16, plain conv, stride 1, k = 1 or 3, up to three
+// concatenated sources, cout <= 32, K = taps * cin_pad <= 16 * kWsMaxSteps): the slice
+// chain's (mu | sigma) + GaussianConditional convs (256 -> 16, K = 2304) and lrp output
+// convs (128 -> 8, tanh update).  In the LDS-ring kernel they are a 36-stage serial K loop
+// over only 128 workgroups.  Here one workgroup owns a 32-pixel tile and its 4 waves split
+// K four ways: per 16-deep k-step each lane loads one 16-byte weight fragment (row lane&31)
+// and one 16-byte im2col fragment (pixel lane&31; tap / channel from a per-chunk LDS table)
+// straight into an R-deep register ring -- no LDS staging of either operand -- for one
+// v_mfma_f32_32x32x16_bf16.  The four partial tiles are summed through LDS and wave 0 runs
+// the epilogue; the GAUSS epilogue works in the accumulator layout (mu channel c and sigma
+// channel c + nch of a pixel sit in the same lane) and writes one fp64 bits partial per tile.
+constexpr int kWsMaxSteps = 146;
+
+template <int R>
+__global__ void __launch_bounds__(256) conv_wstream_kernel(const ConvArgsDev args) {
+  __shared__ int ktab[2 * kWsMaxSteps];
+  __shared__ float bl[32];
+  __shared__ __attribute__((aligned(16))) float part[3][16][64];
+  const ConvShared& s = args.s;
+  const ConvGroup& g = args.g[blockIdx.z];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ntaps = s.ksize * s.ksize;
+  const int kused = ntaps * g.cin_pad;
+  const int nks = (kused + 15) / 16;
+  for (int kc = tid; kc < 2 * nks; kc += 256) {
+    const int k = kc * 8;
+    const int tap = k / g.cin_pad;
+    const int ci = k - tap * g.cin_pad;
+    const int ty = tap / s.ksize, tx = tap - ty * s.ksize;
+    int src, cs;
+    bool ok = k < kused && tap < ntaps;
+    if (ci < g.send0) { src = 0; cs = ci; }
+    else if (ci < g.send1) { src = 1; cs = ci - g.send0; }
+    else { src = 2; cs = ci - g.send1; ok = ok && ci < g.send2; }
+    ktab[kc] = cs | ((ty - s.pad + 4) << 12) | ((tx - s.pad + 4) << 15) | (src << 18) |
+               ((int)ok << 20);
+  }
+  if (tid < 32) bl[tid] = (g.bias && tid < g.rows) ? g.bias[tid] : 0.0f;
+  __syncthreads();
+
+  const int in_h = s.in_h, in_w = s.in_w, Mtot = s.M;
+  const char* const sp0 = reinterpret_cast<const char*>(g.sp0);
+  const char* const sp1 = reinterpret_cast<const char*>(g.sp1);
+  const char* const sp2 = reinterpret_cast<const char*>(g.sp2);
+  const int sld0 = (int)g.sld0, sld1 = (int)g.sld1, sld2 = (int)g.sld2;
+  const int r32 = lane & 31, h = lane >> 5;
+  const int tile = blockIdx.x;
+  const int m = tile * 32 + r32;
+  const bool valid = m < Mtot;
+  const int mm = valid ? m : 0;
+  const int t_ = udiv(mm, s.Wm, s.rWm);
+  const int px = mm - t_ * s.Wm;
+  const int pb = udiv(t_, s.Hm, s.rHm);
+  const int py = t_ - pb * s.Hm;
+  // this wave's k-steps [k0, k1)
+  const int k0 = (nks * wave) >> 2, k1 = (nks * (wave + 1)) >> 2;
+  const bf16_t* wrow = reinterpret_cast<const bf16_t*>(g.w) + (size_t)r32 * g.k_pad + 8 * h;
+
+#define WS_LOAD(da, db, ks_)                                                                  \
+  do {                                                                                        \
+    const int e_ = ktab[2 * (ks_) + h];                                                       \
+    const int iy_ = py + ((e_ >> 12) & 7) - 4, ix_ = px + ((e_ >> 15) & 7) - 4;              \
+    const int sr_ = (e_ >> 18) & 3;                                                           \
+    const bool ok_ = valid & ((e_ >> 20) != 0) & ((unsigned)iy_ < (unsigned)in_h) &           \
+                     ((unsigned)ix_ < (unsigned)in_w);                                        \
+    const char* base_ = sr_ == 0 ? sp0 : (sr_ == 1 ? sp1 : sp2);                              \
+    const int ld_ = sr_ == 0 ? sld0 : (sr_ == 1 ? sld1 : sld2);                               \
+    const unsigned off_ =                                                                     \
+        ((unsigned)(((pb * in_h + iy_) * in_w + ix_) * ld_ + (e_ & 0xFFF))) * 2u;             \
+    const uint4* p_ = ok_ ? reinterpret_cast<const uint4*>(base_ + off_) : g_zero_page;       \
+    db = *p_;                                                                                 \
+    da = *reinterpret_cast<const uint4*>(wrow + 16 * (ks_));                                  \
+  } while (0)
+
+  uint4 av[R], bv[R];
+#pragma unroll
+  for (int u = 0; u < R; ++u) {
+    av[u] = make_uint4(0, 0, 0, 0);
+    bv[u] = make_uint4(0, 0, 0, 0);
+    if (k0 + u < k1) WS_LOAD(av[u], bv[u], k0 + u);
+  }
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  for (int c = k0; c < k1; c += R) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int ks = c + u;
+      if (ks < k1) {
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, av[u]),
+                                                      __builtin_bit_cast(bf16x8, bv[u]), acc,
+                                                      0, 0, 0);
+        if (ks + R < k1) WS_LOAD(av[u], bv[u], ks + R);
+      }
+    }
+  }
+#undef WS_LOAD
+  // ---- sum the four waves' partial tiles (waves 1..3 -> LDS -> wave 0)
+  if (wave > 0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) part[wave - 1][r][lane] = acc[r];
+  }
+  __syncthreads();
+  if (wave > 0) return;
+#pragma unroll
+  for (int w = 0; w < 3; ++w)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] += part[w][r][lane];
+
+  // accumulator layout: lane (pixel r32, half h) holds channel 8q + 4h + r in acc[4q + r]
+  if (s.act == RGBAC_ACT_GAUSS) {
+    const int nch = g.cout >> 1;                   // 8 or 16
+    double bits = 0.0;
+    if (valid) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = 8 * q + 4 * h + r;
+          if (c < nch) {
+            // sigma channel c + nch sits in accumulator quad q + nch/8 (static indices)
+            const float mu = acc[4 * q + r] + bl[c];
+            const float sg = (nch == 8 ? acc[4 * (q + 1) + r] : acc[4 * ((q + 2) & 3) + r]) +
+                             bl[c + nch];
+            bits += (double)gauss_elem<bf16_t>(g, m, c, nch, mu, sg);
+          }
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) bits += __shfl_xor(bits, o);
+    if (lane == 0) g.partial[tile] = bits;
+  } else if (valid) {
+    EpiIn in[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n = 8 * q + 4 * h;
+      if (n < g.cout) in[q].template load<bf16_t>(g, s.act, (long long)m, n);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n = 8 * q + 4 * h;
+      if (n < g.cout) {
+        float v[4] = {acc[4 * q], acc[4 * q + 1], acc[4 * q + 2], acc[4 * q + 3]};
+        const float bias[4] = {bl[n], bl[n + 1], bl[n + 2], bl[n + 3]};
+        epilogue4_fin<bf16_t>(s, g, (long long)m, n, v, bias, in[q]);
+      }
+    }
+  }
+}
+
+static void launch_wstream(const ConvArgsDev& d, hipStream_t st) {
+  const int ntile = (d.s.M + 31) / 32;
+  hipLaunchKernelGGL(conv_wstream_kernel<8>, dim3(ntile, 1, d.s.ngroups), dim3(256), 0, st, d);
+}
+
 // Persistent grid: as many blocks per z-slice as fit on the chip at once (occupancy query,
 // cached per kernel), evened out so every block gets the same number of tiles (+-1).
 template <typename T, int BM, int BN, int WGM, int WGN, int NBUF>
@@ -1608,6 +1767,7 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
                         (tile < kFirstWres || (tile >= kFirstDeep && tile < kFirstPers));
   if (part == 2) {                         // split-K reduce + epilogue kernels only
     if (s.ksplit == 1 || inlaunch || tile == kTileSpatial || tile == kTileSmallK ||
+        tile == kTileWStream ||
         (tile >= kFirstWres && tile < kFirstDeep))
       return RGBAC_OK;
     goto splitk_epilogue;
@@ -1669,6 +1829,15 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
       default: hipLaunchKernelGGL((conv_wres_kernel<T, 128, 16, 4, 1, NS>), grid, dim3(256), 0, st, d); break;
     }
     return check_launch("conv_wres_kernel");
+  }
+  if (tile == kTileWStream) {
+    if constexpr (sizeof(T) == 2) {
+      launch_wstream(d, st);
+      return check_launch("conv_wstream_kernel");
+    } else {
+      set_error("the narrow wave-streaming tile is bf16 only");
+      return RGBAC_E_ARG;
+    }
   }
   if (tile == kTileSmallK) {
     if constexpr (sizeof(T) == 2) {
@@ -1882,6 +2051,18 @@ extern "C" int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroup
       RGBAC_REQUIRE(args[i].nsrc == 1 && args[i].cin_pad == 32 && args[i].src[0].channels == 32 &&
                         args[i].cout <= 32 && args[i].k_pad >= 288,
                     "the spatial 3x3 tile needs one 32-channel source and cout <= 32");
+  } else if (a->tile == kTileWStream) {
+    RGBAC_REQUIRE(a->dtype == RGBAC_BF16 && a->mode == RGBAC_CONV && a->ksplit == 1 &&
+                      a->stride == 1 && (a->ksize == 1 || a->ksize == 3),
+                  "the narrow wave-streaming tile needs bf16, a stride-1 1x1/3x3 conv, ksplit 1");
+    for (int i = 0; i < ngroups; ++i) {
+      RGBAC_REQUIRE(args[i].cout <= 32 && args[i].cin_pad < 4096 &&
+                        (ntaps_max * args[i].cin_pad + 15) / 16 <= kWsMaxSteps,
+                    "the narrow wave-streaming tile needs cout <= 32 and K <= 2336");
+      RGBAC_REQUIRE(a->act != RGBAC_ACT_GAUSS ||
+                        (args[i].cout % 16 == 0 && args[i].cout <= 32),
+                    "GAUSS on the narrow tile needs (mu|sigma) halves of 8 or 16 channels");
+    }
   } else if (a->tile == kTileSmallK) {
     RGBAC_REQUIRE(a->dtype == RGBAC_BF16 && a->mode == RGBAC_CONV && a->ksplit == 1 &&
                       a->act != RGBAC_ACT_GAUSS,
@@ -1914,7 +2095,8 @@ extern "C" int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroup
     }
     if (a->act == RGBAC_ACT_GAUSS) {
       RGBAC_REQUIRE(a->mode == RGBAC_CONV && a->ksplit == 1, "GAUSS needs a plain conv, ksplit 1");
-      RGBAC_REQUIRE(a->tile < kFirstPers, "GAUSS needs a non-persistent tile");
+      RGBAC_REQUIRE(a->tile < kFirstPers || a->tile == kTileWStream,
+                    "GAUSS needs a non-persistent tile");
       RGBAC_REQUIRE(b->cout % 2 == 0 && b->cout <= kTiles[a->tile].bn,
                     "GAUSS needs (mu|sigma) channels in one N tile");
       RGBAC_REQUIRE(b->partial, "GAUSS needs a partial-sum buffer");

@@ -86,7 +86,9 @@ def latent_path(model, y, training=False, noise_z=None, noise_y=None, debug=None
     B, h, w = y.B, y.H, y.W
     npix = B * h * w
     YH = rt.new_feat(B, h, w, M, dt, dev)
-    ypart = torch.zeros((ns, -(-npix // 64)), dtype=torch.float64, device=dev)
+    # one fp64 bits partial per M block of the GAUSS conv (64-pixel LDS-ring tiles or
+    # 32-pixel wave tiles); unused slots stay zero
+    ypart = torch.zeros((ns, -(-npix // 32)), dtype=torch.float64, device=dev)
     liks = [None] * ns
     waves = [[i] for i in range(min(msup, ns))]
     if ns > msup:

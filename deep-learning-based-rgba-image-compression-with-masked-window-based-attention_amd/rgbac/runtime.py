@@ -115,7 +115,7 @@ TILES = [(128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 1
          (256, 32),
          (128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 16),
          (128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 16),
-         (32, 96)]
+         (32, 96), (32, 32)]
 FIRST_WRES = 7
 WRES_STAGES = 6
 FIRST_DIRECT = 13        # 13..18: direct kernel (plain conv, K <= DIRECT_STEPS MFMA k-steps)
@@ -128,6 +128,8 @@ STREAM_TILES = (tuple(range(FIRST_WRES)) + tuple(range(FIRST_DEEP, FIRST_DEEP + 
                 tuple(range(FIRST_PERS, FIRST_PERS + 7)))
 GAUSS_TILES = tuple(range(FIRST_WRES)) + tuple(range(FIRST_DEEP, FIRST_DEEP + 7))
 TILE_SMALLK = 34         # conv_smallk_kernel: bf16 1x1 stride-1 conv, one source, cin_pad <= 256
+TILE_WSTREAM = 35        # conv_wstream_kernel: bf16 stride-1 1x1/3x3, cout <= 32, K <= 2336
+WSTREAM_MAX_STEPS = 146
 SMALLK_MAX = 256
 KSPLITS = (1, 2, 4, 8)
 TUNE = os.environ.get("RGBAC_TUNE", "1") != "0"
@@ -144,14 +146,28 @@ def pick_cout_pad(cout):
     return round_up(cout, 128)
 
 
-def _candidates(M, cout, nst, nks=None, plain=True, spatial=False, smallk=False):
+def _wstream_ok(preps):
+    a = preps[0].a
+    if not (a.dtype == _lib.BF16 and a.mode == CONV and a.stride == 1 and a.ksize in (1, 3)):
+        return False
+    for p in preps:
+        if p.pk.cout > 32 or -(-a.ksize * a.ksize * p.a.cin_pad // 16) > WSTREAM_MAX_STEPS:
+            return False
+        if a.act == ACT["gauss"] and p.pk.cout % 16:
+            return False
+    return True
+
+
+def _candidates(M, cout, nst, nks=None, plain=True, spatial=False, smallk=False, wstream=False):
     """(tile, ksplit) pairs worth timing for an M-pixel, cout-channel conv with nst K-stages
     (nks MFMA k-steps; ``plain`` = CONV mode; ``spatial`` = the 3x3/Cin-32 tile applies;
     ``smallk`` = the small-K wave-streaming tile applies)."""
     out = [(TILE_SMALLK, 1)] if smallk else []
+    if wstream:
+        out.append((TILE_WSTREAM, 1))
     n16 = round_up(cout, 16)
     for t, (bm, bn) in enumerate(TILES):
-        if t == TILE_SMALLK:
+        if t in (TILE_SMALLK, TILE_WSTREAM):
             continue
         if t == TILE_SPATIAL:
             if spatial:
@@ -447,6 +463,8 @@ def kernel_name(tile, preps):
     dt = "float" if preps[0].a.dtype == 0 else "bf16_t"
     if tile == TILE_SPATIAL:
         return f"conv3x3_c32_kernel<{dt}>"
+    if tile == TILE_WSTREAM:
+        return "conv_wstream_kernel<8>"
     if tile == TILE_SMALLK:
         cout = max(p.pk.cout for p in preps)
         nt = 1 if cout <= 32 else (2 if cout <= 64 else 3)
@@ -535,9 +553,12 @@ def launch(preps):
         nst = max(pr.nst for pr in preps)
         if gauss:
             cands = [(t, 1) for t in GAUSS_TILES if _gauss_ok(t, cout)]
+            if _wstream_ok(preps):
+                cands.append((TILE_WSTREAM, 1))
         else:
             cands = _candidates(mtot, cout, nst, max(pr.nks for pr in preps),
-                                p0.pk.mode == CONV, _spatial_ok(preps), _smallk_ok(preps))
+                                p0.pk.mode == CONV, _spatial_ok(preps), _smallk_ok(preps),
+                                _wstream_ok(preps))
         if TUNE and not torch.cuda.is_current_stream_capturing():
             best = None
             for cand in cands:
@@ -559,8 +580,9 @@ def launch(preps):
         else:
             choice = _heuristic(mtot, cout, nst)
         _tune_cache[key] = choice
-    if gauss and (choice[0] not in GAUSS_TILES or
-                  not _gauss_ok(choice[0], max(pr.pk.cout for pr in preps))):
+    if gauss and not (choice[0] == TILE_WSTREAM and _wstream_ok(preps)) and (
+            choice[0] not in GAUSS_TILES or
+            not _gauss_ok(choice[0], max(pr.pk.cout for pr in preps))):
         choice = (min((t for t in GAUSS_TILES if _gauss_ok(t, p0.pk.cout)),
                       key=lambda t: TILES[t][1]), 1)
     set_choice(*choice)

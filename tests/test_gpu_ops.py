@@ -6,6 +6,8 @@ the reference's max magnitude and state summation-order noise of fp32 MFMA
 (exact f32 FMA chains, different order): 2e-5 for single ops, looser for deep
 stacks as stated per test.  bf16 mode is checked with a stated looser bound.
 """
+import ctypes
+
 import pytest
 import torch
 import torch.nn as nn
@@ -462,3 +464,74 @@ def test_conv_inlaunch_splitk(device, tile):
                     assert rel(got, want) < tol
     finally:
         rt.FORCE, rt.INLAUNCH_SPLITK = None, False
+
+
+@pytest.mark.parametrize("cin,cout,k,act,nsrc", [(128, 8, 3, "tanh_half", 3), (256, 16, 3, "none", 2),
+                                                 (64, 24, 3, "gelu", 1), (96, 32, 1, "relu", 1)])
+def test_conv_wstream_tile(device, cin, cout, k, act, nsrc):
+    """The narrow-output wave-streaming tile (bf16): 3x3 / 1x1 convs with concatenated sources
+    and residual / tanh-update epilogues against PyTorch."""
+    rt = _rt()
+    from rgbac.layers.TransformRGB import run_conv
+    g = _gen(600 + cin + cout)
+    m = nn.Conv2d(cin, cout, k, padding=k // 2)
+    parts = [cin // nsrc] * (nsrc - 1) + [cin - (cin // nsrc) * (nsrc - 1)]
+    xs = [torch.randn((2, c, 20, 36), generator=g) for c in parts]
+    y = m(torch.cat(xs, 1))
+    r = torch.randn(y.shape, generator=g)
+    if act == "tanh_half":
+        want = r + 0.5 * torch.tanh(y)
+        kw = dict(act=act, res1=None)
+    else:
+        f = {"gelu": F.gelu, "relu": F.relu, "none": lambda t: t}[act]
+        want = f(y + r)
+        kw = dict(act=act)
+    rt.FORCE = (rt.TILE_WSTREAM, 1)
+    try:
+        with torch.no_grad():
+            fs = [rt.to_nhwc(t.to(device), torch.bfloat16) for t in xs]
+            fr = rt.to_nhwc(r.to(device), torch.bfloat16)
+            if act == "tanh_half":
+                kw["res1"] = fr
+            else:
+                kw["res0"] = fr
+            got = rt.to_nchw(run_conv(m.to(device), [f.src() for f in fs], **kw))
+        assert rel(got, want) < 2e-2
+    finally:
+        rt.FORCE = None
+
+
+def test_gauss_wstream_matches_ring_tile(device):
+    """GaussianConditional epilogue on the narrow wave-streaming tile == on the LDS-ring tile
+    (same bf16 inputs): y_hat, likelihoods and the bits sum."""
+    rt = _rt()
+    g = _gen(77)
+    B, H, W, cs = 2, 16, 20, 8
+    dt = torch.bfloat16
+    mconv = nn.Conv2d(128, cs, 3, padding=1)
+    sconv = nn.Conv2d(128, cs, 3, padding=1)
+    t_mean = torch.randn((B, 128, H, W), generator=g)
+    t_scale = torch.randn((B, 128, H, W), generator=g)
+    y = torch.randn((B, cs, H, W), generator=g) * 3
+    from rgbac.models._latent import _musigma_pack
+    mconv, sconv = mconv.to(device), sconv.to(device)
+    fm, fsc = rt.to_nhwc(t_mean.to(device), dt), rt.to_nhwc(t_scale.to(device), dt)
+    fy = rt.to_nhwc(y.to(device), dt)
+    pk = _musigma_pack(mconv, sconv, dt, fm.ldc)
+    res = {}
+    for tile in (6, rt.TILE_WSTREAM):
+        out = rt.new_feat(B, H, W, cs, dt, device)
+        lik = torch.empty((B, H, W, cs), dtype=torch.float32, device=device)
+        part = torch.zeros(-(-B * H * W // 32), dtype=torch.float64, device=device)
+        pr = rt.prepare(pk, [fm.src(), fsc.src()], out=out, act="gauss", res1=(fy, 0),
+                        aux1=lik, partial=part)
+        arr = (rt._lib.ConvArgs * 1)()
+        arr[0] = pr.a
+        arr[0].tile, arr[0].ksplit = tile, 1
+        rt._lib.call("rgbac_conv2d_grouped", ctypes.addressof(arr), 1, rt._lib.stream_ptr(device))
+        torch.cuda.synchronize()
+        res[tile] = (rt.to_nchw(out), lik.clone(), part.sum().item())
+    a, b = res[6], res[rt.TILE_WSTREAM]
+    assert (a[0] - b[0]).abs().max().item() <= 1.0 + 1e-6     # a rare .5-boundary symbol flip
+    assert (a[0] != b[0]).float().mean().item() < 0.01
+    assert abs(a[2] - b[2]) / abs(a[2]) < 1e-2
