@@ -92,3 +92,30 @@ def test_mask_forward_fp32(device):
     assert rel(got[0], want[0]) < 1e-3
     for i in (1, 2, 3, 4):
         assert abs(got[i].item() - want[i].item()) <= 1e-4 * max(abs(want[i].item()), 1e-6)
+
+
+def test_rgb_bf16_slice_precompute_matches(device, rgb_net):
+    """bf16 inference with the side-stream precompute of the slice convs' latent-means/scales
+    half (rgbac.models._latent.PRECOMPUTE) and with the single-conv path: both within the
+    bf16 bar of the fp32 oracle, and the same bpp within bf16 noise."""
+    from rgbac.models import _latent
+    x, a = _inputs(4, 64, 64, seed=3)
+    me = ref.supply_mask(a)
+    with torch.no_grad():
+        want = ref.rgb_forward(cpu_sd(rgb_net), x, a, a, *me[:4])
+    net = rgb_net.to(device).set_compute_dtype(torch.bfloat16)
+    outs, saved = {}, _latent.PRECOMPUTE
+    try:
+        for flag in (False, True):
+            _latent.PRECOMPUTE = flag
+            with torch.no_grad():
+                outs[flag] = net(x.to(device), a.to(device), a.to(device),
+                                 *[m.to(device) for m in me[:4]])
+    finally:
+        _latent.PRECOMPUTE = saved
+        net.set_compute_dtype(torch.float32)
+    for got in outs.values():
+        assert rel(got[0], want[0]) < 5e-2
+        assert abs(got[2].item() - want[2].item()) < 0.05 * want[2].item()
+    b0, b1 = outs[False][2].item(), outs[True][2].item()
+    assert abs(b0 - b1) < 0.02 * b0
