@@ -9,12 +9,15 @@
 // loads/stores are channel vectors.
 //
 // Staging: both operands go HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4,
-// one 1-KiB piece = 8 rows x 128 B per wave-instruction) into an NBUF-deep ring
-// of K stages (128 bytes of K per row per stage: 64 bf16 / 32 f32).  The
-// 16-byte chunk c of row r lives at slot c ^ (r & 7) (conflict-free
-// ds_read_b128 for the 16-lane fragment groups); because the DMA destination
-// is lane-linear, the XOR is applied to the per-lane SOURCE chunk.  Padding
-// taps / out-of-image pixels read a zero page.  Stage s+NBUF-1 is issued while
+// one 1-KiB piece per wave-instruction) into an NBUF-deep ring of K stages
+// (128 bytes of K per row per stage: 64 bf16 / 32 f32).  conv_kernel stores a
+// stage chunk-major ([8 chunks][rows], one piece = 64 rows of one 16-byte K
+// chunk): a piece's (tap, channel, source) decode is wave-uniform (scalar), and
+// the 16-lane fragment groups read 256 contiguous bytes (conflict-free).  The
+// persistent kernels keep the row-major image (piece = 8 rows x 128 B, chunk c of
+// row r at slot c ^ (r & 7), the XOR applied to the per-lane SOURCE chunk since
+// the DMA destination is lane-linear).  Padding taps / out-of-image pixels read a
+// zero page.  Stage s+NBUF-1 is issued while
 // stage s is consumed; a counted s_waitcnt vmcnt + raw s_barrier retires one
 // stage per iteration (no vmcnt(0) drain in the loop).
 //   bf16: v_mfma_f32_16x16x32_bf16 per 16x16 tile per 32-deep k-step.
@@ -76,7 +79,12 @@ struct ConvArgsDev {
   ConvGroup g[kMaxGroups];
 };
 
-__device__ uint4 g_zero_page[64];   // zero source for padding taps (static, never written)
+__device__ uint4 g_zero_page[64];
+
+// conv_kernel stage layouts (bit 0: A chunk-major, bit 1: B chunk-major; see conv_kernel)
+#ifndef RGBAC_CONV_LAYOUT
+#define RGBAC_CONV_LAYOUT 0
+#endif   // zero source for padding taps (static, never written)
 
 // n / d for 0 <= n < 2^31 via a double reciprocal and one correction step
 // (|n*rd - n/d| < 2^-21, so the truncated quotient is off by at most one).
@@ -465,6 +473,34 @@ __device__ __forceinline__ void dma16(const void* src, uint4* lds_block) {
       : "memory");
 }
 
+// The same with a wave-uniform base address and a per-lane 32-bit byte offset (the SADDR
+// form: no per-lane 64-bit address arithmetic).
+__device__ __forceinline__ void dma16_s(const void* sbase, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds)
+      : "memory");
+}
+// dma16 with a precomputed wave-uniform LDS byte address (no per-call generic->LDS cast).
+__device__ __forceinline__ void dma16_l(const void* src, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   static_assert(N >= 0 && N <= 63, "vmcnt range");
@@ -493,7 +529,7 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
   constexpr int TM = BM / WGM / 16;           // 16-pixel tiles per wave
   constexpr int TN = BN / WGN / 16;           // 16-channel tiles per wave
   constexpr int IA = BN / 8, IB = BM / 8;     // DMA pieces per stage
-  constexpr int LW = (IA + IB + 3) / 4;       // pieces per wave per stage (uniform)
+  constexpr int LW = (IA + 3) / 4 + IB / 4;  // pieces per wave per stage (uniform)
   constexpr int STAGE = (BN + BM) * 8;        // uint4 per stage
   static_assert(WGM * WGN == 4, "4 waves");
   static_assert(TM >= 1 && TN >= 1, "tile");
@@ -559,41 +595,71 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
   const int pad = s.pad;
   const bool sq_in = s.square != 0;
 
-  // ---- per-lane DMA assignment: piece j = wave + 4*i; lane -> row (lane>>3),
-  //      source chunk c = (lane&7) ^ (lane>>3) so LDS slot (lane&7) holds chunk c.
-  const int lrow = lane >> 3;
-  const int c = (lane & 7) ^ lrow;
-  const T* wrow[LW];
-  int pbase[LW], biy[LW], bix[LW];
-  bool isA[LW], bval[LW];
-  int lofs[LW];                                 // uint4 offset of the piece in a stage
-  const T* wbase = reinterpret_cast<const T*>(g.w) + (size_t)phase * g.rows * g.k_pad;
+  // ---- stage image.  A region (BN rows) then B region (BM rows); one DMA piece = 64
+  //      consecutive uint4 slots (1 KiB).  Per operand, compile-time layout:
+  //        row-major : piece = 8 rows x 128 B, chunk c of row r at slot r*8 + (c ^ (r & 7))
+  //                    (conflict-free fragment reads; the XOR goes on the SOURCE chunk);
+  //        chunk-major: slots [8 chunks][rows], piece = 64 rows of one 16-byte chunk, so a
+  //                    B piece's (tap, channel, source) decode is wave-uniform (scalar).
+  //      Wave w issues A pieces w, w+4, .. (a surplus slot re-issues the last piece, so every
+  //      wave retires the same count per stage) and BM/32 B pieces.
+  constexpr bool ACM = (RGBAC_CONV_LAYOUT & 1) != 0;
+  constexpr bool BCM = (RGBAC_CONV_LAYOUT & 2) != 0;
+  constexpr int RB = BM / 64;                   // 64-row blocks of the B region
+  constexpr int NAW = (IA + 3) / 4;             // A pieces per wave
+  constexpr int NBW = IB / 4;                   // B pieces per wave
+  constexpr int NPX = BCM ? RB : NBW;           // per-lane pixel states
+  static_assert(BM % 64 == 0 && LW == NAW + NBW && NBW == 2 * RB, "piece geometry");
+  uint32_t aoff[NAW];                           // byte offset of the lane's A chunk (stage 0)
+  int alds[NAW];                                // uint4 slot of the A piece in a stage
+  const char* const wbase =
+      reinterpret_cast<const char*>(g.w) + (size_t)phase * g.rows * g.k_pad * sizeof(T);
 #pragma unroll
-  for (int i = 0; i < LW; ++i) {
-    int j = wave + 4 * i;
-    if (j >= IA + IB) j = IA + IB - 1;          // surplus slot re-issues the last piece
-    isA[i] = j < IA;
-    lofs[i] = j * 64;
-    const int arow = 8 * j + lrow;
-    wrow[i] = wbase + (size_t)(n0 + (isA[i] ? arow : 0)) * g.k_pad + c * EPV;
-    const int m = m0 + 8 * (j - IA) + lrow;
-    bval[i] = !isA[i] && m < Mtot;
-    const int mm = bval[i] ? m : 0;
+  for (int i = 0; i < NAW; ++i) {
+    const int q = min(wave + 4 * i, IA - 1);
+    alds[i] = q * 64;
+    int row, ch;
+    if constexpr (ACM) {
+      row = (q * 64 + lane) % BN; ch = (q * 64 + lane) / BN;
+    } else {
+      row = 8 * q + (lane >> 3); ch = (lane & 7) ^ (lane >> 3);
+    }
+    aoff[i] = (uint32_t)(((n0 + row) * g.k_pad + ch * EPV) * (int)sizeof(T));
+  }
+  // per pixel state: the lane's input pixel of tap (0, 0) and its per-tap validity bits
+  // (bit t set when tap t reads inside the image; bit 31 is never set)
+  int pb[NPX];
+  uint32_t vmask[NPX];
+#pragma unroll
+  for (int r = 0; r < NPX; ++r) {
+    const int m = m0 + (BCM ? 64 * r + lane : 8 * (wave + 4 * r) + (lane >> 3));
+    const bool mval = m < Mtot;
+    const int mm = mval ? m : 0;
     const int t = udiv(mm, s.Wm, s.rWm);
     const int mx = mm - t * s.Wm;
     const int b = udiv(t, s.Hm, s.rHm);
-    biy[i] = (t - b * s.Hm) * s.sy;
-    bix[i] = mx * s.sy;
-    pbase[i] = (b * in_h + biy[i]) * in_w + bix[i];   // input pixel of tap offset (0, 0)
+    const int biy = (t - b * s.Hm) * s.sy, bix = mx * s.sy;
+    pb[r] = (b * in_h + biy) * in_w + bix;
+    uint32_t vm = 0;
+    for (int tap = 0, ty = 0, tx = 0; tap < ntaps; ++tap) {
+      const int iy = biy + (convt ? 1 - ty : ty - pad), ix = bix + (convt ? 1 - tx : tx - pad);
+      if (mval && (unsigned)iy < (unsigned)in_h && (unsigned)ix < (unsigned)in_w) vm |= 1u << tap;
+      if (++tx == tw) { tx = 0; ++ty; }
+    }
+    vmask[r] = vm;
   }
 
-  // ---- incremental k -> (tap, ci) decode for this lane's chunk
-  const int k0 = s_beg * KS + c * EPV;
-  KDec dec;
-  dec.tap = k0 / cin_pad;
-  dec.ci = k0 - dec.tap * cin_pad;
-  dec.ty = dec.tap / tw;
-  dec.tx = dec.tap - dec.ty * tw;
+  // ---- K decode: chunk-major B -> the wave's two chunks (2w, 2w+1), scalar;
+  //      row-major B -> this lane's source chunk (lane & 7) ^ (lane >> 3)
+  KDec dec[BCM ? 2 : 1];
+#pragma unroll
+  for (int h = 0; h < (BCM ? 2 : 1); ++h) {
+    const int k0 = s_beg * KS + (BCM ? 2 * wave + h : (lane & 7) ^ (lane >> 3)) * EPV;
+    dec[h].tap = k0 / cin_pad;
+    dec[h].ci = k0 - dec[h].tap * cin_pad;
+    dec[h].ty = dec[h].tap / tw;
+    dec[h].tx = dec[h].tap - dec[h].ty * tw;
+  }
 
   f32x4 acc[TN][TM];
 #pragma unroll
@@ -602,48 +668,47 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
     for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int wm = wave % WGM, wn = wave / WGM;
-  const int fr = lane & 15, fq = lane >> 4, sw = lane & 7;
+  const int fr = lane & 15, fq = lane >> 4;
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lptr_t)smem);
 
   // Staging code for stage `st_issue` (used by the prologue and the steady-state loop).
   // A macro, not a lambda: captured locals would be address-taken, and the DMA
-  // statement's "memory" clobber then pins them -- and the source-pointer select --
-  // to scratch; and a merged prologue/steady-state loop makes the accumulators a
-  // loop-carried VGPR/AGPR copy pair.
+  // statement's "memory" clobber then pins them to scratch; and a merged prologue /
+  // steady-state loop makes the accumulators a loop-carried VGPR/AGPR copy pair.
+  // Per B piece the lane does: tap-bit test, pixel + tap offset, mul24 by the source's
+  // row pitch, 64-bit add and the zero-page select (the host keeps sources < 2^24 pixels).
 #define CONV_ISSUE_STAGE(st_issue)                                                            \
   do {                                                                                        \
-    /* branch-free per-lane addressing: source select, bounds and zero page by */             \
-    /* v_cndmask; 32-bit element offsets (the host bounds every source below 2 GiB) */        \
-    const int dy = convt ? 1 - dec.ty : dec.ty - pad;                                         \
-    const int dx = convt ? 1 - dec.tx : dec.tx - pad;                                         \
-    const int ci = dec.ci;                                                                    \
-    const bool in0 = ci < send0, in1 = ci < send1;                                            \
-    const char* src = in0 ? sp0 : (in1 ? sp1 : sp2);                                          \
-    const int sld = in0 ? sld0 : (in1 ? sld1 : sld2);                                         \
-    const int cs = ci - (in0 ? 0 : (in1 ? send0 : send1));                                    \
-    const bool kval = (dec.tap < ntaps) & (ci < send2);                                       \
-    const int doff = dy * in_w + dx;                                                          \
-    const int kk = (s_beg + (st_issue)) * KS;                                                 \
-    uint4* stage = smem + ((st_issue) % NBUF) * STAGE;                                        \
+    const uint32_t lst = lbase + (uint32_t)(((st_issue) % NBUF) * STAGE * 16);               \
+    const char* wst = wbase + (size_t)(s_beg + (st_issue)) * KS * sizeof(T);                  \
 _Pragma("unroll")                                                                             \
-    for (int i = 0; i < LW; ++i) {                                                            \
-      const void* gp;                                                                         \
-      if (isA[i]) {                                                                           \
-        gp = wrow[i] + kk;                                                                    \
-      } else {                                                                                \
-        const int iy = biy[i] + dy, ix = bix[i] + dx;                                         \
-        const bool ok = kval & bval[i] & ((unsigned)iy < (unsigned)in_h) &                    \
-                        ((unsigned)ix < (unsigned)in_w);                                      \
-        const unsigned off = ((unsigned)((pbase[i] + doff) * sld + cs)) * (unsigned)sizeof(T); \
-        gp = ok ? (const void*)(src + off) : (const void*)g_zero_page;                        \
+    for (int i = 0; i < NAW; ++i) dma16_s(wst, aoff[i], lst + alds[i] * 16);                 \
+_Pragma("unroll")                                                                             \
+    for (int h = 0; h < (BCM ? 2 : 1); ++h) {                                                 \
+      const int dy = convt ? 1 - dec[h].ty : dec[h].ty - pad;                                 \
+      const int dx = convt ? 1 - dec[h].tx : dec[h].tx - pad;                                 \
+      const int ci = dec[h].ci;                                                               \
+      const bool in0 = ci < send0, in1 = ci < send1;                                          \
+      const char* src = in0 ? sp0 : (in1 ? sp1 : sp2);                                        \
+      const int sldb = (in0 ? sld0 : (in1 ? sld1 : sld2)) * (int)sizeof(T);                   \
+      const int csb = (ci - (in0 ? 0 : (in1 ? send0 : send1))) * (int)sizeof(T);             \
+      const int bit = ((dec[h].tap < ntaps) & (ci < send2)) ? dec[h].tap : 31;                \
+      const int doff = dy * in_w + dx;                                                        \
+_Pragma("unroll")                                                                             \
+      for (int r = 0; r < (BCM ? RB : NBW); ++r) {                                            \
+        const bool ok = (vmask[r] >> bit) & 1u;                                               \
+        const unsigned off = (unsigned)__umul24((unsigned)(pb[r] + doff), (unsigned)sldb) +   \
+                             (unsigned)csb;                                                   \
+        const void* gp = ok ? (const void*)(src + off) : (const void*)g_zero_page;            \
+        const int slot = BCM ? (2 * wave + h) * BM + 64 * r : (wave + 4 * r) * 64;            \
+        dma16_l(gp, lst + (IA * 64 + slot) * 16);                                             \
       }                                                                                       \
-      dma16(gp, stage + lofs[i]);                                                             \
-    }                                                                                         \
-    /* advance this lane's decode to the next stage */                                        \
-    dec.ci += KS;                                                                             \
-    while (dec.ci >= cin_pad) {                                                               \
-      dec.ci -= cin_pad;                                                                      \
-      ++dec.tap;                                                                              \
-      if (++dec.tx == tw) { dec.tx = 0; ++dec.ty; }                                           \
+      dec[h].ci += KS;                                                                        \
+      while (dec[h].ci >= cin_pad) {                                                          \
+        dec[h].ci -= cin_pad;                                                                 \
+        ++dec[h].tap;                                                                         \
+        if (++dec[h].tx == tw) { dec[h].tx = 0; ++dec[h].ty; }                                \
+      }                                                                                       \
     }                                                                                         \
   } while (0)
 
@@ -662,13 +727,17 @@ _Pragma("unroll")                                                               
     const uint4* Bs = As + BN * 8;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      const int chunk = (4 * ks + fq) ^ sw;
+      const int chunk = 4 * ks + fq;
       uint4 a[TN], b[TM];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) a[j] = As[(wn * TN * 16 + j * 16 + fr) * 8 + chunk];
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * TN * 16 + j * 16 + fr;
+        a[j] = ACM ? As[chunk * BN + row] : As[row * 8 + (chunk ^ (fr & 7))];
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        b[i] = Bs[(wm * TM * 16 + i * 16 + fr) * 8 + chunk];
+        const int row = wm * TM * 16 + i * 16 + fr;
+        b[i] = BCM ? Bs[chunk * BM + row] : Bs[row * 8 + (chunk ^ (fr & 7))];
         if (sq_in) b[i] = square_chunk<T>(b[i]);
       }
 #pragma unroll
@@ -2027,6 +2096,9 @@ extern "C" int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroup
   }
   s.rWm = 1.0 / s.Wm;
   s.rHm = 1.0 / s.Hm;
+  RGBAC_REQUIRE(!(a->tile < kFirstWres || (a->tile >= kFirstDeep && a->tile < kFirstPers)) ||
+                    (long long)a->batch * a->in_h * a->in_w < (1ll << 24),
+                "streaming conv tiles address sources of < 2^24 pixels (24-bit gather multiply)");
   const long long M = (long long)a->batch * s.Hm * s.Wm;
   RGBAC_REQUIRE(M < (1ll << 31), "too many output pixels");
   s.M = (int)M;

@@ -10,7 +10,8 @@ import os
 import torch
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librgbac_hip.so")
+# RGBAC_LIB_PATH: an alternative build of the same library (A/B experiments)
+LIB_PATH = os.environ.get("RGBAC_LIB_PATH") or os.path.join(_HERE, "librgbac_hip.so")
 
 F32, BF16 = 0, 1
 ACT = dict(none=0, gelu=1, relu=2, lrelu=3, tanh_half=4, gate=5, gdn=6, igdn=7, masksel=8,

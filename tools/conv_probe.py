@@ -56,7 +56,7 @@ def main():
         e1.record()
         e1.synchronize()
         us = e0.elapsed_time(e1) / a.iters * 1e3
-        print(f"tile {rt.TILES[cand[0]]} ks {cand[1]}: {us:8.2f} us  {flops / us / 1e6:7.1f} TF/s  "
+        print(f"tile {cand[0]:2d} {rt.TILES[cand[0]]} ks {cand[1]}: {us:8.2f} us  {flops / us / 1e6:7.1f} TF/s  "
               f"{nbytes / us / 1e3:7.1f} GB/s", flush=True)
 
 
