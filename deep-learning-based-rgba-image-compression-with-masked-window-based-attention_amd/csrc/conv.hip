@@ -10,14 +10,14 @@
 //
 // Staging: both operands go HBM/L2 -> LDS by LDS-DMA (global_load_lds_dwordx4,
 // one 1-KiB piece per wave-instruction) into an NBUF-deep ring of K stages
-// (128 bytes of K per row per stage: 64 bf16 / 32 f32).  conv_kernel stores a
-// stage chunk-major ([8 chunks][rows], one piece = 64 rows of one 16-byte K
-// chunk): a piece's (tap, channel, source) decode is wave-uniform (scalar), and
-// the 16-lane fragment groups read 256 contiguous bytes (conflict-free).  The
-// persistent kernels keep the row-major image (piece = 8 rows x 128 B, chunk c of
-// row r at slot c ^ (r & 7), the XOR applied to the per-lane SOURCE chunk since
-// the DMA destination is lane-linear).  Padding taps / out-of-image pixels read a
-// zero page.  Stage s+NBUF-1 is issued while
+// (128 or 256 bytes of K per row per stage: 64/128 bf16, 32/64 f32).  The 16-byte
+// chunk c of row r lives at slot c ^ (r & 7) (conflict-free ds_read_b128 for the
+// 16-lane fragment groups); because the DMA destination is lane-linear, the XOR is
+// applied to the per-lane SOURCE chunk.  Weight pieces use the SADDR form (fixed
+// per-lane offset, scalar stage base); im2col pieces test a per-lane tap-validity
+// bitmask.  Padding taps / out-of-image pixels read a zero page.  (Measured and
+// dropped: a chunk-major image with 64-row pieces, whose K decode is scalar -- its
+// 64 cache lines per DMA instruction cost more than the VALU it saves.)  Stage s+NBUF-1 is issued while
 // stage s is consumed; a counted s_waitcnt vmcnt + raw s_barrier retires one
 // stage per iteration (no vmcnt(0) drain in the loop).
 //   bf16: v_mfma_f32_16x16x32_bf16 per 16x16 tile per 32-deep k-step.
@@ -80,11 +80,7 @@ struct ConvArgsDev {
 };
 
 __device__ uint4 g_zero_page[64];
-
-// conv_kernel stage layouts (bit 0: A chunk-major, bit 1: B chunk-major; see conv_kernel)
-#ifndef RGBAC_CONV_LAYOUT
-#define RGBAC_CONV_LAYOUT 0
-#endif   // zero source for padding taps (static, never written)
+   // zero source for padding taps (static, never written)
 
 // n / d for 0 <= n < 2^31 via a double reciprocal and one correction step
 // (|n*rd - n/d| < 2^-21, so the truncated quotient is off by at most one).
@@ -521,16 +517,21 @@ __device__ __forceinline__ void wait_ring(int after) {
   }
 }
 
-// BM x BN tile, 4 waves laid out WGM (along m) x WGN (along n), NBUF-stage ring.
-template <typename T, int BM, int BN, int WGM, int WGN, int NBUF>
+// BM x BN tile, 4 waves laid out WGM (along m) x WGN (along n), NBUF-stage ring of
+// K stages of KSM x 128 bytes per row (KSM = 2: half the barriers and ring bookkeeping per
+// MFMA, for the issue-bound small-M convs).
+template <typename T, int BM, int BN, int WGM, int WGN, int NBUF, int KSM = 1>
 __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
   constexpr int EPV = Elem<T>::EPV;
-  constexpr int KS = 8 * EPV;                 // K elements per stage (128 B per row)
+  constexpr int CPR = 8 * KSM;                // 16-byte chunks per row per stage
+  constexpr int KS = CPR * EPV;               // K elements per stage
+  constexpr int RPP = 64 / CPR;               // rows per DMA piece
   constexpr int TM = BM / WGM / 16;           // 16-pixel tiles per wave
   constexpr int TN = BN / WGN / 16;           // 16-channel tiles per wave
-  constexpr int IA = BN / 8, IB = BM / 8;     // DMA pieces per stage
+  constexpr int IA = BN / RPP, IB = BM / RPP; // DMA pieces per stage
   constexpr int LW = (IA + 3) / 4 + IB / 4;  // pieces per wave per stage (uniform)
-  constexpr int STAGE = (BN + BM) * 8;        // uint4 per stage
+  constexpr int STAGE = (BN + BM) * CPR;      // uint4 per stage
+  static_assert(KSM == 1 || KSM == 2, "stage width");
   static_assert(WGM * WGN == 4, "4 waves");
   static_assert(TM >= 1 && TN >= 1, "tile");
   static_assert(NBUF * STAGE * 4 >= BM * BN, "GAUSS epilogue reuses the ring as a [BM][BN] fp32 tile");
@@ -595,21 +596,21 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
   const int pad = s.pad;
   const bool sq_in = s.square != 0;
 
-  // ---- stage image.  A region (BN rows) then B region (BM rows); one DMA piece = 64
-  //      consecutive uint4 slots (1 KiB).  Per operand, compile-time layout:
-  //        row-major : piece = 8 rows x 128 B, chunk c of row r at slot r*8 + (c ^ (r & 7))
-  //                    (conflict-free fragment reads; the XOR goes on the SOURCE chunk);
-  //        chunk-major: slots [8 chunks][rows], piece = 64 rows of one 16-byte chunk, so a
-  //                    B piece's (tap, channel, source) decode is wave-uniform (scalar).
-  //      Wave w issues A pieces w, w+4, .. (a surplus slot re-issues the last piece, so every
-  //      wave retires the same count per stage) and BM/32 B pieces.
-  constexpr bool ACM = (RGBAC_CONV_LAYOUT & 1) != 0;
-  constexpr bool BCM = (RGBAC_CONV_LAYOUT & 2) != 0;
-  constexpr int RB = BM / 64;                   // 64-row blocks of the B region
+  // ---- stage image, row-major: A region (BN rows) then B region (BM rows), CPR slots per
+  //      row; chunk c of row r lives at slot r*CPR + (c ^ (r & 7)) (conflict-free fragment
+  //      reads: 8 consecutive rows of one chunk hit 8 distinct 16-byte bank groups).  One DMA
+  //      piece = 64 consecutive slots = RPP rows x CPR chunks; the DMA destination is
+  //      lane-linear, so the XOR goes on each lane's SOURCE chunk.  Wave w issues A pieces
+  //      w, w+4, .. (a surplus slot re-issues the last piece, so every wave retires the same
+  //      count per stage) and B pieces w, w+4, ..: all of a wave's pieces have the parity of
+  //      w, so with 4-row pieces too a lane's source chunk -- and its K decode -- is one
+  //      value for all its pieces.
   constexpr int NAW = (IA + 3) / 4;             // A pieces per wave
   constexpr int NBW = IB / 4;                   // B pieces per wave
-  constexpr int NPX = BCM ? RB : NBW;           // per-lane pixel states
-  static_assert(BM % 64 == 0 && LW == NAW + NBW && NBW == 2 * RB, "piece geometry");
+  static_assert(IB % 4 == 0 && LW == NAW + NBW, "piece geometry");
+  const int lrow = lane / CPR;
+  const int rsw = (RPP * wave + lrow) & 7;      // (row & 7) of every piece row this lane fills
+  const int c = (lane % CPR) ^ rsw;             // the lane's source chunk
   uint32_t aoff[NAW];                           // byte offset of the lane's A chunk (stage 0)
   int alds[NAW];                                // uint4 slot of the A piece in a stage
   const char* const wbase =
@@ -617,22 +618,18 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
 #pragma unroll
   for (int i = 0; i < NAW; ++i) {
     const int q = min(wave + 4 * i, IA - 1);
+    const int row = RPP * q + lrow;
     alds[i] = q * 64;
-    int row, ch;
-    if constexpr (ACM) {
-      row = (q * 64 + lane) % BN; ch = (q * 64 + lane) / BN;
-    } else {
-      row = 8 * q + (lane >> 3); ch = (lane & 7) ^ (lane >> 3);
-    }
-    aoff[i] = (uint32_t)(((n0 + row) * g.k_pad + ch * EPV) * (int)sizeof(T));
+    aoff[i] = (uint32_t)(((n0 + row) * g.k_pad + ((lane % CPR) ^ (row & 7)) * EPV) *
+                         (int)sizeof(T));
   }
-  // per pixel state: the lane's input pixel of tap (0, 0) and its per-tap validity bits
+  // per B piece: the lane's input pixel of tap (0, 0) and its per-tap validity bits
   // (bit t set when tap t reads inside the image; bit 31 is never set)
-  int pb[NPX];
-  uint32_t vmask[NPX];
+  int pb[NBW];
+  uint32_t vmask[NBW];
 #pragma unroll
-  for (int r = 0; r < NPX; ++r) {
-    const int m = m0 + (BCM ? 64 * r + lane : 8 * (wave + 4 * r) + (lane >> 3));
+  for (int r = 0; r < NBW; ++r) {
+    const int m = m0 + RPP * (wave + 4 * r) + lrow;
     const bool mval = m < Mtot;
     const int mm = mval ? m : 0;
     const int t = udiv(mm, s.Wm, s.rWm);
@@ -649,16 +646,14 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
     vmask[r] = vm;
   }
 
-  // ---- K decode: chunk-major B -> the wave's two chunks (2w, 2w+1), scalar;
-  //      row-major B -> this lane's source chunk (lane & 7) ^ (lane >> 3)
-  KDec dec[BCM ? 2 : 1];
-#pragma unroll
-  for (int h = 0; h < (BCM ? 2 : 1); ++h) {
-    const int k0 = s_beg * KS + (BCM ? 2 * wave + h : (lane & 7) ^ (lane >> 3)) * EPV;
-    dec[h].tap = k0 / cin_pad;
-    dec[h].ci = k0 - dec[h].tap * cin_pad;
-    dec[h].ty = dec[h].tap / tw;
-    dec[h].tx = dec[h].tap - dec[h].ty * tw;
+  // ---- incremental k -> (tap, ci) decode of this lane's source chunk
+  KDec dec;
+  {
+    const int k0 = s_beg * KS + c * EPV;
+    dec.tap = k0 / cin_pad;
+    dec.ci = k0 - dec.tap * cin_pad;
+    dec.ty = dec.tap / tw;
+    dec.tx = dec.tap - dec.ty * tw;
   }
 
   f32x4 acc[TN][TM];
@@ -683,32 +678,29 @@ __global__ void __launch_bounds__(256) conv_kernel(const ConvArgsDev args) {
     const char* wst = wbase + (size_t)(s_beg + (st_issue)) * KS * sizeof(T);                  \
 _Pragma("unroll")                                                                             \
     for (int i = 0; i < NAW; ++i) dma16_s(wst, aoff[i], lst + alds[i] * 16);                 \
+    const int dy = convt ? 1 - dec.ty : dec.ty - pad;                                         \
+    const int dx = convt ? 1 - dec.tx : dec.tx - pad;                                         \
+    const int ci = dec.ci;                                                                    \
+    const bool in0 = ci < send0, in1 = ci < send1;                                            \
+    const char* src = in0 ? sp0 : (in1 ? sp1 : sp2);                                          \
+    const int sldb = (in0 ? sld0 : (in1 ? sld1 : sld2)) * (int)sizeof(T);                     \
+    const int csb = (ci - (in0 ? 0 : (in1 ? send0 : send1))) * (int)sizeof(T);               \
+    const int bit = ((dec.tap < ntaps) & (ci < send2)) ? dec.tap : 31;                        \
+    const int doff = dy * in_w + dx;                                                          \
 _Pragma("unroll")                                                                             \
-    for (int h = 0; h < (BCM ? 2 : 1); ++h) {                                                 \
-      const int dy = convt ? 1 - dec[h].ty : dec[h].ty - pad;                                 \
-      const int dx = convt ? 1 - dec[h].tx : dec[h].tx - pad;                                 \
-      const int ci = dec[h].ci;                                                               \
-      const bool in0 = ci < send0, in1 = ci < send1;                                          \
-      const char* src = in0 ? sp0 : (in1 ? sp1 : sp2);                                        \
-      const int sldb = (in0 ? sld0 : (in1 ? sld1 : sld2)) * (int)sizeof(T);                   \
-      const int csb = (ci - (in0 ? 0 : (in1 ? send0 : send1))) * (int)sizeof(T);             \
-      const int bit = ((dec[h].tap < ntaps) & (ci < send2)) ? dec[h].tap : 31;                \
-      const int doff = dy * in_w + dx;                                                        \
-_Pragma("unroll")                                                                             \
-      for (int r = 0; r < (BCM ? RB : NBW); ++r) {                                            \
-        const bool ok = (vmask[r] >> bit) & 1u;                                               \
-        const unsigned off = (unsigned)__umul24((unsigned)(pb[r] + doff), (unsigned)sldb) +   \
-                             (unsigned)csb;                                                   \
-        const void* gp = ok ? (const void*)(src + off) : (const void*)g_zero_page;            \
-        const int slot = BCM ? (2 * wave + h) * BM + 64 * r : (wave + 4 * r) * 64;            \
-        dma16_l(gp, lst + (IA * 64 + slot) * 16);                                             \
-      }                                                                                       \
-      dec[h].ci += KS;                                                                        \
-      while (dec[h].ci >= cin_pad) {                                                          \
-        dec[h].ci -= cin_pad;                                                                 \
-        ++dec[h].tap;                                                                         \
-        if (++dec[h].tx == tw) { dec[h].tx = 0; ++dec[h].ty; }                                \
-      }                                                                                       \
+    for (int r = 0; r < NBW; ++r) {                                                           \
+      const bool ok = (vmask[r] >> bit) & 1u;                                                 \
+      const unsigned off = (unsigned)__umul24((unsigned)(pb[r] + doff), (unsigned)sldb) +     \
+                           (unsigned)csb;                                                     \
+      const void* gp = ok ? (const void*)(src + off) : (const void*)g_zero_page;              \
+      dma16_l(gp, lst + (IA + wave + 4 * r) * 64 * 16);                                       \
+    }                                                                                         \
+    /* advance this lane's decode to the next stage */                                        \
+    dec.ci += KS;                                                                             \
+    while (dec.ci >= cin_pad) {                                                               \
+      dec.ci -= cin_pad;                                                                      \
+      ++dec.tap;                                                                              \
+      if (++dec.tx == tw) { dec.tx = 0; ++dec.ty; }                                           \
     }                                                                                         \
   } while (0)
 
@@ -724,20 +716,16 @@ _Pragma("unroll")                                                               
     __builtin_amdgcn_sched_barrier(0);
     if (it + NBUF - 1 < ns) CONV_ISSUE_STAGE(it + NBUF - 1);
     const uint4* As = smem + (it % NBUF) * STAGE;
-    const uint4* Bs = As + BN * 8;
+    const uint4* Bs = As + BN * CPR;
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int chunk = 4 * ks + fq;
+    for (int ks = 0; ks < 2 * KSM; ++ks) {
+      const int chunk = (4 * ks + fq) ^ (fr & 7);
       uint4 a[TN], b[TM];
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wn * TN * 16 + j * 16 + fr;
-        a[j] = ACM ? As[chunk * BN + row] : As[row * 8 + (chunk ^ (fr & 7))];
-      }
+      for (int j = 0; j < TN; ++j) a[j] = As[(wn * TN * 16 + j * 16 + fr) * CPR + chunk];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const int row = wm * TM * 16 + i * 16 + fr;
-        b[i] = BCM ? Bs[chunk * BM + row] : Bs[row * 8 + (chunk ^ (fr & 7))];
+        b[i] = Bs[(wm * TM * 16 + i * 16 + fr) * CPR + chunk];
         if (sq_in) b[i] = square_chunk<T>(b[i]);
       }
 #pragma unroll
@@ -1945,13 +1933,13 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
     case 4: hipLaunchKernelGGL((conv_kernel<T, 64, 32, 2, 2, 3>), grid, dim3(256), 0, st, d); break;
     case 5: hipLaunchKernelGGL((conv_kernel<T, 128, 16, 4, 1, 3>), grid, dim3(256), 0, st, d); break;
     case 6: hipLaunchKernelGGL((conv_kernel<T, 64, 16, 4, 1, 3>), grid, dim3(256), 0, st, d); break;
-    case 20: hipLaunchKernelGGL((conv_kernel<T, 128, 128, 2, 2, 4>), grid, dim3(256), 0, st, d); break;
-    case 21: hipLaunchKernelGGL((conv_kernel<T, 128, 64, 4, 1, 5>), grid, dim3(256), 0, st, d); break;
-    case 22: hipLaunchKernelGGL((conv_kernel<T, 64, 64, 2, 2, 6>), grid, dim3(256), 0, st, d); break;
-    case 23: hipLaunchKernelGGL((conv_kernel<T, 128, 32, 4, 1, 6>), grid, dim3(256), 0, st, d); break;
-    case 24: hipLaunchKernelGGL((conv_kernel<T, 64, 32, 2, 2, 8>), grid, dim3(256), 0, st, d); break;
-    case 25: hipLaunchKernelGGL((conv_kernel<T, 128, 16, 4, 1, 6>), grid, dim3(256), 0, st, d); break;
-    default: hipLaunchKernelGGL((conv_kernel<T, 64, 16, 4, 1, 8>), grid, dim3(256), 0, st, d); break;
+    case 20: hipLaunchKernelGGL((conv_kernel<T, 128, 128, 2, 2, 2, 2>), grid, dim3(256), 0, st, d); break;
+    case 21: hipLaunchKernelGGL((conv_kernel<T, 128, 64, 4, 1, 2, 2>), grid, dim3(256), 0, st, d); break;
+    case 22: hipLaunchKernelGGL((conv_kernel<T, 64, 64, 2, 2, 2, 2>), grid, dim3(256), 0, st, d); break;
+    case 23: hipLaunchKernelGGL((conv_kernel<T, 128, 32, 4, 1, 2, 2>), grid, dim3(256), 0, st, d); break;
+    case 24: hipLaunchKernelGGL((conv_kernel<T, 64, 32, 2, 2, 3, 2>), grid, dim3(256), 0, st, d); break;
+    case 25: hipLaunchKernelGGL((conv_kernel<T, 128, 16, 4, 1, 2, 2>), grid, dim3(256), 0, st, d); break;
+    default: hipLaunchKernelGGL((conv_kernel<T, 64, 16, 4, 1, 3, 2>), grid, dim3(256), 0, st, d); break;
   }
   }
   {

@@ -67,7 +67,9 @@ class TPack:
         self.cout_pad, self.k_pad = pk.cout_pad, pk.k_pad
         self.idx = idx
         self.bias_idx = bias_idx
-        self.w = torch.empty(idx.shape, dtype=dtype, device=idx.device)
+        # zero slack behind the last row, as runtime.PackedConv (256-byte K stages)
+        n = idx.numel()
+        self.w = torch.zeros(n + 128, dtype=dtype, device=idx.device)[:n].view(idx.shape)
         self.bias = torch.zeros(pk.cout_pad, dtype=_F32, device=idx.device)
 
     def refresh(self, weight, bias=None):

@@ -122,7 +122,7 @@ FIRST_DIRECT = 13        # 13..18: direct kernel (plain conv, K <= DIRECT_STEPS 
 DIRECT_STEPS = 12
 DIRECT_LDS = 65536       # weight panel bytes of a direct tile (dynamic LDS limit)
 TILE_SPATIAL = 19        # conv3x3_c32_kernel: 16x16-pixel tiles, 3x3 s1, Cin 32, Cout <= 32, bf16
-FIRST_DEEP = 20          # 20..26: tiles 0..6 with a deeper LDS ring (4..8 K stages)
+FIRST_DEEP = 20          # 20..26: tiles 0..6 with 256-byte K stages (KSM = 2, 2..3 in the ring)
 FIRST_PERS = 27          # 27..33: tiles 0..6, persistent over output tiles (no GAUSS epilogue)
 STREAM_TILES = (tuple(range(FIRST_WRES)) + tuple(range(FIRST_DEEP, FIRST_DEEP + 7)) +
                 tuple(range(FIRST_PERS, FIRST_PERS + 7)))
@@ -352,7 +352,12 @@ class PackedConv:
             full = torch.zeros((cout, nt, cin_pad), device=dev)
             full[:, :, idx] = t
             wp[ph, :cout, :nt * cin_pad] = full.reshape(cout, nt * cin_pad)
-        self.w = wp.to(dtype).contiguous()
+        # zero slack behind the last row: a 256-byte-per-row K stage (KSM = 2 tiles) may read
+        # up to 64 elements past k_pad (those lanes multiply zero im2col chunks)
+        n = wp.numel()
+        flat = torch.zeros(n + 128, dtype=dtype, device=dev)
+        flat[:n].copy_(wp.reshape(-1))
+        self.w = flat[:n].view(wp.shape)
         self.bias = torch.zeros(self.cout_pad, device=dev)
         if bias is not None:
             self.bias[:cout] = bias.detach().float()
@@ -452,9 +457,9 @@ def _spatial_ok(preps):
 # profiler's kernel names are exactly rocprofv3's (csrc/conv.hip launch_conv).
 _TILE_SIG = {0: "128, 128, 2, 2, 2", 1: "128, 64, 4, 1, 3", 2: "64, 64, 2, 2, 3",
              3: "128, 32, 4, 1, 3", 4: "64, 32, 2, 2, 3", 5: "128, 16, 4, 1, 3",
-             6: "64, 16, 4, 1, 3", 20: "128, 128, 2, 2, 4", 21: "128, 64, 4, 1, 5",
-             22: "64, 64, 2, 2, 6", 23: "128, 32, 4, 1, 6", 24: "64, 32, 2, 2, 8",
-             25: "128, 16, 4, 1, 6", 26: "64, 16, 4, 1, 8"}
+             6: "64, 16, 4, 1, 3", 20: "128, 128, 2, 2, 2, 2", 21: "128, 64, 4, 1, 2, 2",
+             22: "64, 64, 2, 2, 2, 2", 23: "128, 32, 4, 1, 2, 2", 24: "64, 32, 2, 2, 3, 2",
+             25: "128, 16, 4, 1, 2, 2", 26: "64, 16, 4, 1, 3, 2"}
 _SMALLK_NKS = {1: 1, 2: 2, 3: 3, 4: 4, 5: 5, 6: 6, 7: 8, 8: 8, 9: 12, 10: 12, 11: 12, 12: 12}
 
 

@@ -8,7 +8,8 @@ for L in "$@"; do
   export RGBAC_LIB_PATH=$PWD/$PKG/rgbac/$L
   echo "==== $L"
   for P in "--cin 224 --cout 128 --k 3 --hw 32 --groups 2" "--cin 192 --cout 192 --k 5 --stride 2 --hw 128 --act none" \
-           "--cin 88 --cout 224 --k 3 --hw 32 --groups 2"; do
+           "--cin 88 --cout 224 --k 3 --hw 32 --groups 2" "--cin 224 --cout 128 --k 3 --hw 32" \
+           "--cin 256 --cout 288 --k 3 --hw 16 --groups 2" "--cin 192 --cout 576 --k 1 --hw 64 --act none"; do
     echo "== $P"
     timeout -k 10 120 python tools/conv_probe.py $P --iters 30 > gpurun_out/ab_${L}_$(echo $P | tr -d " -").txt
   done
