@@ -842,6 +842,37 @@ adam_clamp_kernel(long long n, float* __restrict__ p, float* __restrict__ g, flo
   }
 }
 
+// The same with the step count in device memory (graph-replayable training step): every
+// thread forms torch.optim.Adam's scalars from step = *step_dev + 1 in double exactly as the
+// host entry does; step_advance_kernel then stores the new count.
+__global__ void __launch_bounds__(256)
+adam_clamp_dstep_kernel(long long n, float* __restrict__ p, float* __restrict__ g,
+                        float* __restrict__ m, float* __restrict__ v, const long long* step_dev,
+                        double lr, double beta1, double beta2, double eps, float clip,
+                        float gscale) {
+  const double step = (double)(*step_dev + 1);
+  const double bc1 = 1.0 - pow(beta1, step);
+  const double bc2 = 1.0 - pow(beta2, step);
+  const float w1 = (float)(1.0 - beta1), b2 = (float)beta2, w2 = (float)(1.0 - beta2);
+  const float bc2_sqrt = (float)sqrt(bc2), epsf = (float)eps, step_size = (float)(lr / bc1);
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
+    float gv = g[e];
+    if (gscale != 1.0f) gv *= gscale;
+    if (clip > 0.0f) gv = fminf(fmaxf(gv, -clip), clip);
+    g[e] = gv;
+    const float mv = m[e] + w1 * (gv - m[e]);
+    const float vv = v[e] * b2 + w2 * (gv * gv);
+    m[e] = mv;
+    v[e] = vv;
+    const float denom = sqrtf(vv) / bc2_sqrt + epsf;
+    p[e] = p[e] + (-step_size) * (mv / denom);
+  }
+}
+
+__global__ void step_advance_kernel(long long* step_dev) {
+  if (threadIdx.x == 0) *step_dev += 1;
+}
+
 // ------------------------------------------------------------------ layout helpers
 // dir 0: shuffle   in (B,H,W,4C) -> out (B,2H,2W,C), out[2y+i][2x+j][c] = in[y][x][4c+2i+j]
 // dir 1: unshuffle in (B,2H,2W,C) -> out (B,H,W,4C)
@@ -1142,6 +1173,25 @@ extern "C" int rgbac_adam_clamp(int64_t n, float* param, float* grad, float* exp
                      (float)(1.0 - beta2), (float)std::sqrt(bc2), (float)eps,
                      (float)(lr / bc1), clip, grad_scale);
   return check_launch("adam_clamp_kernel");
+}
+
+extern "C" int rgbac_adam_clamp_dstep(int64_t n, float* param, float* grad, float* exp_avg,
+                                      float* exp_avg_sq, double lr, double beta1, double beta2,
+                                      double eps, int64_t* step_dev, float clip, float grad_scale,
+                                      void* stream) {
+  RGBAC_REQUIRE(n >= 0 && step_dev, "shape/step");
+  RGBAC_REQUIRE(n == 0 || (param && grad && exp_avg && exp_avg_sq), "null pointer");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (n > 0) {
+    hipLaunchKernelGGL(adam_clamp_dstep_kernel, dim3(grid_for(n)), dim3(256), 0, st, n, param,
+                       grad, exp_avg, exp_avg_sq, reinterpret_cast<const long long*>(step_dev),
+                       lr, beta1, beta2, eps, clip, grad_scale);
+    int rc = check_launch("adam_clamp_dstep_kernel");
+    if (rc) return rc;
+  }
+  hipLaunchKernelGGL(step_advance_kernel, dim3(1), dim3(64), 0, st,
+                     reinterpret_cast<long long*>(step_dev));
+  return check_launch("step_advance_kernel");
 }
 
 extern "C" int rgbac_pixel_shuffle(int dtype, int dir, int batch, int h, int w, int c,

@@ -49,6 +49,19 @@ class AdamClamp:
         self._attach_grads()
         self.step_count = 0
         self.grad_scale = 1.0
+        self.step_dev = None           # device step counter (graph-replayable step)
+
+    def use_device_step(self):
+        """Keep the step count in device memory from now on, so a training step captured in
+        a HIP graph replays the Adam bias corrections correctly (rgbac_adam_clamp_dstep)."""
+        if self.step_dev is None:
+            self.step_dev = torch.tensor([self.step_count], dtype=torch.int64,
+                                         device=self.flat.device)
+        return self
+
+    def _sync_step(self):
+        if self.step_dev is not None:
+            self.step_count = int(self.step_dev.item())
 
     def _attach_grads(self):
         for p, (off, k) in zip(self.params, self.offsets):
@@ -66,12 +79,15 @@ class AdamClamp:
         self._attach_grads()
 
     def state_dict(self):
+        self._sync_step()
         return dict(step=self.step_count, exp_avg=self.exp_avg, exp_avg_sq=self.exp_avg_sq,
                     param_groups=[{k: v for k, v in g.items() if k != "params"}
                                   for g in self.param_groups])
 
     def load_state_dict(self, sd):
         self.step_count = int(sd["step"])
+        if self.step_dev is not None:
+            self.step_dev.fill_(self.step_count)
         self.exp_avg.copy_(sd["exp_avg"])
         self.exp_avg_sq.copy_(sd["exp_avg_sq"])
         for g, s in zip(self.param_groups, sd["param_groups"]):
@@ -82,6 +98,15 @@ class AdamClamp:
         self.step_count += 1
         g = self.param_groups[0]
         b1, b2 = g["betas"]
+        if self.step_dev is not None:
+            _lib.call("rgbac_adam_clamp_dstep", self.numel, self.flat.data_ptr(),
+                      self.flat_grad.data_ptr(), self.exp_avg.data_ptr(),
+                      self.exp_avg_sq.data_ptr(), float(g["lr"]), float(b1), float(b2),
+                      float(g["eps"]), self.step_dev.data_ptr(),
+                      float(self.defaults["clip"] or 0.0), float(self.grad_scale),
+                      _lib.stream_ptr(self.flat.device))
+            rt.PARAM_GEN += 1
+            return
         _lib.call("rgbac_adam_clamp", self.numel, self.flat.data_ptr(), self.flat_grad.data_ptr(),
                   self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), float(g["lr"]), float(b1),
                   float(b2), float(g["eps"]), self.step_count, float(self.defaults["clip"] or 0.0),

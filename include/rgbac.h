@@ -328,6 +328,12 @@ int rgbac_adam_clamp(int64_t n, float* param, float* grad, float* exp_avg, float
                      double lr, double beta1, double beta2, double eps, int64_t step,
                      float clip, float grad_scale, void* stream);
 
+/* rgbac_adam_clamp with the step count in device memory (a CUDA/HIP-graph
+ * replayable training step): uses step = *step_dev + 1, then stores it.     */
+int rgbac_adam_clamp_dstep(int64_t n, float* param, float* grad, float* exp_avg,
+                           float* exp_avg_sq, double lr, double beta1, double beta2, double eps,
+                           int64_t* step_dev, float clip, float grad_scale, void* stream);
+
 /* PixelShuffle(2) (dir 0) / PixelUnshuffle(2) (dir 1) on NHWC; c = channels
  * after shuffling.  Channel copy for concatenation / split.                 */
 int rgbac_pixel_shuffle(int dtype, int dir, int batch, int h, int w, int c, const void* in,

@@ -333,6 +333,82 @@ def test_adam_clamp_matches_torch():
         torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-6, atol=1e-7)
 
 
+def test_adam_clamp_device_step_matches_host_step():
+    """rgbac_adam_clamp_dstep (step count in device memory, graph-replayable) reproduces the
+    host-step entry bit for bit over several steps, and keeps the count in sync."""
+    from rgbac.optim import AdamClamp
+    g = _gen(52)
+    ps = [torch.randn(s, generator=g).cuda().requires_grad_(True) for s in ((9, 4), (31,))]
+    qs = [p.detach().clone().requires_grad_(True) for p in ps]
+    oa = AdamClamp(ps, lr=1e-3, clip=0.5)
+    ob = AdamClamp(qs, lr=1e-3, clip=0.5).use_device_step()
+    for step in range(4):
+        grads = [torch.randn(p.shape, generator=g).cuda() * 2 for p in ps]
+        oa.zero_grad()
+        ob.zero_grad()
+        for p, q, gr in zip(ps, qs, grads):
+            (p * gr).sum().backward()
+            (q * gr).sum().backward()
+        oa.step()
+        ob.step()
+    for p, q in zip(ps, qs):
+        torch.testing.assert_close(p.detach(), q.detach(), rtol=1e-6, atol=1e-7)
+    assert ob.state_dict()["step"] == 4
+
+
+def test_rgb_train_step_graph_replay_matches_eager():
+    """The training step captured in a HIP graph (bench.py's config-3 loop) and replayed gives
+    the same parameters as the same steps run eagerly (bf16, B=2, 64x64, fixed noise)."""
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    from rgbac.optim import AdamClamp
+    torch.manual_seed(234)
+    base = AutoEncoder().train()
+    g = _gen(62)
+    B, H, W = 2, 64, 64
+    x = (torch.randint(0, 256, (B, 3, H, W), generator=g).float() / 255).cuda()
+    a = torch.ones((B, 1, H, W)).cuda()
+    me = [t.cuda() for t in ref.supply_mask(a.cpu())]
+    nz = (torch.rand((B, 1, 1, 192), generator=g) - 0.5).cuda()
+    ny = (torch.rand((B, 8, 8, 80), generator=g) - 0.5).cuda()
+    nets, opts = [], []
+    for _ in range(2):
+        n = AutoEncoder().cuda().train().set_compute_dtype(torch.bfloat16)
+        n.load_state_dict(base.state_dict())
+        nets.append(n)
+        opts.append(AdamClamp(n.parameters(), lr=1e-4, clip=5.0).use_device_step())
+
+    def step(n, o):
+        out = n(x, a, a, *me[:4], noise_z=nz, noise_y=ny)
+        o.zero_grad()
+        (4096.0 * out[1] + out[2]).backward()
+        o.step()
+        return out
+
+    for _ in range(5):
+        step(nets[0], opts[0])
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for _ in range(2):                 # capture records without running: 2 + 3 replays
+            step(nets[1], opts[1])
+    torch.cuda.current_stream().wait_stream(side)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        step(nets[1], opts[1])
+    for _ in range(3):
+        graph.replay()
+    torch.cuda.synchronize()
+    assert opts[1].state_dict()["step"] == 5
+    # same update direction and size as the eager steps (bitwise equality is not required:
+    # Adam's normalised update amplifies last-bit differences of near-zero gradients)
+    p0 = torch.cat([p.detach().reshape(-1) for p in base.parameters()]).cuda()
+    d0 = torch.cat([p.detach().reshape(-1) for p in nets[0].parameters()]) - p0
+    d1 = torch.cat([p.detach().reshape(-1) for p in nets[1].parameters()]) - p0
+    cos = (d0 @ d1 / (d0.norm() * d1.norm())).item()
+    assert cos > 0.99, cos
+    assert abs(d1.norm().item() / d0.norm().item() - 1) < 0.05
+
+
 @pytest.mark.parametrize("dtype", [torch.float32])
 def test_rgb_train_step_grads(dtype):
     """rd_loss = 4096*mse + bpp (trainRGB.py:178-186) backward: every parameter gradient
