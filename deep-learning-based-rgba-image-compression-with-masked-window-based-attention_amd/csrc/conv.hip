@@ -1652,11 +1652,11 @@ static void launch_smallk(const ConvArgsDev& d, int nks16, int max_cout, hipStre
 // channel c + nch of a pixel sit in the same lane) and writes one fp64 bits partial per tile.
 constexpr int kWsMaxSteps = 146;
 
-template <int R>
-__global__ void __launch_bounds__(256) conv_wstream_kernel(const ConvArgsDev args) {
+template <int R, int NW>
+__global__ void __launch_bounds__(64 * NW) conv_wstream_kernel(const ConvArgsDev args) {
   __shared__ int ktab[2 * kWsMaxSteps];
   __shared__ float bl[32];
-  __shared__ __attribute__((aligned(16))) float part[3][16][64];
+  __shared__ __attribute__((aligned(16))) float part[NW - 1][16][64];
   const ConvShared& s = args.s;
   const ConvGroup& g = args.g[blockIdx.z];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1664,7 +1664,7 @@ __global__ void __launch_bounds__(256) conv_wstream_kernel(const ConvArgsDev arg
   const int ntaps = s.ksize * s.ksize;
   const int kused = ntaps * g.cin_pad;
   const int nks = (kused + 15) / 16;
-  for (int kc = tid; kc < 2 * nks; kc += 256) {
+  for (int kc = tid; kc < 2 * nks; kc += 64 * NW) {
     const int k = kc * 8;
     const int tap = k / g.cin_pad;
     const int ci = k - tap * g.cin_pad;
@@ -1695,7 +1695,7 @@ __global__ void __launch_bounds__(256) conv_wstream_kernel(const ConvArgsDev arg
   const int pb = udiv(t_, s.Hm, s.rHm);
   const int py = t_ - pb * s.Hm;
   // this wave's k-steps [k0, k1)
-  const int k0 = (nks * wave) >> 2, k1 = (nks * (wave + 1)) >> 2;
+  const int k0 = (nks * wave) / NW, k1 = (nks * (wave + 1)) / NW;
   const bf16_t* wrow = reinterpret_cast<const bf16_t*>(g.w) + (size_t)r32 * g.k_pad + 8 * h;
 
 #define WS_LOAD(da, db, ks_)                                                                  \
@@ -1737,7 +1737,7 @@ __global__ void __launch_bounds__(256) conv_wstream_kernel(const ConvArgsDev arg
     }
   }
 #undef WS_LOAD
-  // ---- sum the four waves' partial tiles (waves 1..3 -> LDS -> wave 0)
+  // ---- sum the waves' partial tiles (waves 1..NW-1 -> LDS -> wave 0)
   if (wave > 0) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) part[wave - 1][r][lane] = acc[r];
@@ -1745,7 +1745,7 @@ __global__ void __launch_bounds__(256) conv_wstream_kernel(const ConvArgsDev arg
   __syncthreads();
   if (wave > 0) return;
 #pragma unroll
-  for (int w = 0; w < 3; ++w)
+  for (int w = 0; w < NW - 1; ++w)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] += part[w][r][lane];
 
@@ -1789,9 +1789,24 @@ __global__ void __launch_bounds__(256) conv_wstream_kernel(const ConvArgsDev arg
   }
 }
 
+// 8 waves split K when every wave still gets >= 8 k-steps (the latency-bound chain convs:
+// K = 2304 / 1152 -> 18 / 9 steps per wave instead of 36 / 18).
 static void launch_wstream(const ConvArgsDev& d, hipStream_t st) {
   const int ntile = (d.s.M + 31) / 32;
-  hipLaunchKernelGGL(conv_wstream_kernel<8>, dim3(ntile, 1, d.s.ngroups), dim3(256), 0, st, d);
+  int nks = 0;
+  for (int i = 0; i < d.s.ngroups; ++i) {
+    const int n = (d.s.ksize * d.s.ksize * d.g[i].cin_pad + 15) / 16;
+    if (n > nks) nks = n;
+  }
+  static const int nw_env = [] {
+    const char* e = getenv("RGBAC_WSTREAM_WAVES");
+    return e ? atoi(e) : 0;
+  }();
+  const int nw = nw_env == 4 || nw_env == 8 ? nw_env : (nks >= 64 ? 8 : 4);
+  if (nw == 8)
+    hipLaunchKernelGGL((conv_wstream_kernel<8, 8>), dim3(ntile, 1, d.s.ngroups), dim3(512), 0, st, d);
+  else
+    hipLaunchKernelGGL((conv_wstream_kernel<8, 4>), dim3(ntile, 1, d.s.ngroups), dim3(256), 0, st, d);
 }
 
 // Persistent grid: as many blocks per z-slice as fit on the chip at once (occupancy query,

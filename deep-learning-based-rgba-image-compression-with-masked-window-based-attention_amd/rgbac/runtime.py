@@ -469,7 +469,11 @@ def kernel_name(tile, preps):
     if tile == TILE_SPATIAL:
         return f"conv3x3_c32_kernel<{dt}>"
     if tile == TILE_WSTREAM:
-        return "conv_wstream_kernel<8>"
+        # the library's wave count choice (csrc/conv.hip launch_wstream)
+        nks = max((p.a.ksize * p.a.ksize * p.a.cin_pad + 15) // 16 for p in preps)
+        env = os.environ.get("RGBAC_WSTREAM_WAVES", "")
+        nw = int(env) if env in ("4", "8") else (8 if nks >= 64 else 4)
+        return f"conv_wstream_kernel<8, {nw}>"
     if tile == TILE_SMALLK:
         cout = max(p.pk.cout for p in preps)
         nt = 1 if cout <= 32 else (2 if cout <= 64 else 3)
