@@ -411,6 +411,50 @@ wgrad_reduce_kernel(long long nslot, const int* __restrict__ fmap, const float* 
   }
 }
 
+// Many-split variant (nsplit >= 16: the full-resolution layers split over up to ~200 pixel
+// chunks): a block covers 32 slots x 8 split groups; thread (g, slot) sums splits g, g+8, ..
+// in order, then thread (0, slot) adds the 8 group sums in order -- still a fixed order
+// (deterministic), but 8x the parallelism and 32 coalesced slots per load.
+__global__ void __launch_bounds__(256)
+wgrad_reduce_wide_kernel(long long nslot, const int* __restrict__ fmap,
+                         const float* __restrict__ part, int nsplit, long long slab,
+                         float* __restrict__ dw, int nbias, const float* __restrict__ bpart,
+                         int n_pad, float* __restrict__ db) {
+  __shared__ float red[8][32];
+  const int sl = threadIdx.x & 31, sg = threadIdx.x >> 5;
+  const long long e = blockIdx.x * 32ll + sl;
+  const long long total = nslot + nbias;
+  float acc = 0.0f;
+  if (e < total) {
+    const bool wslot = e < nslot;
+    if (!wslot || fmap[e] >= 0) {
+      const float* src = wslot ? part + e : bpart + (e - nslot);
+      const long long stride = wslot ? slab : (long long)n_pad;
+      // four independent loads in flight per iteration
+      int q = sg;
+      for (; q + 24 < nsplit; q += 32) {
+        const float v0 = src[q * stride], v1 = src[(q + 8) * stride];
+        const float v2 = src[(q + 16) * stride], v3 = src[(q + 24) * stride];
+        acc += v0; acc += v1; acc += v2; acc += v3;
+      }
+      for (; q < nsplit; q += 8) acc += src[q * stride];
+    }
+  }
+  red[sg][sl] = acc;
+  __syncthreads();
+  if (sg == 0 && e < total) {
+    float s = red[0][sl];
+#pragma unroll
+    for (int g = 1; g < 8; ++g) s += red[g][sl];
+    if (e < nslot) {
+      const int i = fmap[e];
+      if (i >= 0) dw[i] = s;
+    } else {
+      db[e - nslot] = s;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ attention core backward
 // Recomputes P = softmax(q k^T * scale + B + M) per window (fp32, same op order
 // as the VALU forward), then dV = P^T dO, dP = dO V^T, dS = P (dP - rowsum(P dP)),
@@ -921,6 +965,42 @@ gather_kernel(long long n, const float* __restrict__ src, const int* __restrict_
   }
 }
 
+// Many gathers in one launch (the per-step repack of every layer's forward and
+// input-gradient weights): task t = {src, idx, dst, n, dtype} as 5 int64 in device memory,
+// blocks [blk0[t], blk0[t+1]) cover its elements, 2048 per block; a block finds its task by
+// binary search over blk0.
+constexpr int kGatherChunk = 2048;
+__global__ void __launch_bounds__(256)
+gather_multi_kernel(int ntask, const long long* __restrict__ tasks,
+                    const long long* __restrict__ blk0) {
+  const long long b = blockIdx.x;
+  int lo = 0, hi = ntask - 1;
+  while (lo < hi) {                       // last t with blk0[t] <= b
+    const int mid = (lo + hi + 1) >> 1;
+    if (blk0[mid] <= b) lo = mid; else hi = mid - 1;
+  }
+  const long long* tk = tasks + 5 * lo;
+  const float* src = reinterpret_cast<const float*>(tk[0]);
+  const int* idx = reinterpret_cast<const int*>(tk[1]);
+  const long long n = tk[3];
+  const long long e0 = (b - blk0[lo]) * kGatherChunk;
+  if (tk[4] == RGBAC_F32) {
+    float* dst = reinterpret_cast<float*>(tk[2]);
+#pragma unroll
+    for (int r = 0; r < kGatherChunk / 256; ++r) {
+      const long long e = e0 + r * 256 + threadIdx.x;
+      if (e < n) { const int j = idx[e]; dst[e] = j >= 0 ? src[j] : 0.0f; }
+    }
+  } else {
+    bf16_t* dst = reinterpret_cast<bf16_t*>(tk[2]);
+#pragma unroll
+    for (int r = 0; r < kGatherChunk / 256; ++r) {
+      const long long e = e0 + r * 256 + threadIdx.x;
+      if (e < n) { const int j = idx[e]; Elem<bf16_t>::st(dst + e, j >= 0 ? src[j] : 0.0f); }
+    }
+  }
+}
+
 // partial[blk][c] = sum over the block's pixels of x[p][c]   (bias gradients)
 template <typename T>
 __global__ void __launch_bounds__(256)
@@ -1055,6 +1135,13 @@ extern "C" int rgbac_wgrad_reduce(int64_t nslot, const int32_t* fmap, const floa
                 "null pointer");
   RGBAC_REQUIRE(nbias <= n_pad, "nbias > n_pad");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (nsplit >= 16) {
+    const long long nblk = (nslot + nbias + 31) / 32;
+    if (nblk == 0) return RGBAC_OK;
+    hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)nblk), dim3(256), 0, st, nslot,
+                       fmap, partial, nsplit, slab, dw, nbias, bias_partial, n_pad, db);
+    return check_launch("wgrad_reduce_wide_kernel");
+  }
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(nslot + nbias)), dim3(256), 0, st, nslot,
                      fmap, partial, nsplit, slab, dw, nbias, bias_partial, n_pad, db);
   return check_launch("wgrad_reduce_kernel");
@@ -1242,6 +1329,18 @@ extern "C" int rgbac_weight_gather(int dtype, int64_t n, const float* src, const
     hipLaunchKernelGGL(gather_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, n, src, idx,
                        (bf16_t*)dst);
   return check_launch("gather_kernel");
+}
+
+extern "C" int rgbac_weight_gather_multi(int ntask, const int64_t* tasks, const int64_t* blk0,
+                                         int64_t nblk, void* stream) {
+  RGBAC_REQUIRE(ntask >= 0 && nblk >= 0 && (ntask == 0 || (tasks && blk0)), "args");
+  RGBAC_REQUIRE(nblk < (1ll << 31), "too many blocks");
+  if (ntask == 0 || nblk == 0) return RGBAC_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(gather_multi_kernel, dim3((unsigned)nblk), dim3(256), 0, st, ntask,
+                     reinterpret_cast<const long long*>(tasks),
+                     reinterpret_cast<const long long*>(blk0));
+  return check_launch("gather_multi_kernel");
 }
 
 extern "C" int rgbac_colsum(int dtype, int64_t npix, int channels, const void* x, int64_t ldx,

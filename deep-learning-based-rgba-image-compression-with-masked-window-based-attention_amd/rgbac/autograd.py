@@ -22,6 +22,7 @@ Parameter-side reparametrisations (GDN beta'/gamma', EntropyBottleneck
 softplus/tanh) stay torch autograd on O(#params) tensors.
 """
 import ctypes
+import os
 
 import torch
 from torch.autograd import Function
@@ -71,13 +72,21 @@ class TPack:
         n = idx.numel()
         self.w = torch.zeros(n + 128, dtype=dtype, device=idx.device)[:n].view(idx.shape)
         self.bias = torch.zeros(pk.cout_pad, dtype=_F32, device=idx.device)
+        self.src = None                # (weight ptr, bias ptr) of the last refresh
+        self.token = 0                 # == _PREFETCH[0]: re-gathered by this step's prefetch
+        self.gen = -1                  # rt.PARAM_GEN at that prefetch (an optimizer step bumps it)
 
     def refresh(self, weight, bias=None):
-        # always re-gathered: the optimizer kernel updates parameters in place
-        # through raw pointers (no autograd version bump), and one gather per
-        # layer per step is cheap next to the conv it feeds
+        # re-gathered every training step: the optimizer kernel updates parameters in
+        # place through raw pointers (no autograd version bump).  prefetch_packs() does
+        # all of a model's packs in one launch at the start of the step's forward; a pack
+        # it covered (same source pointers) is not gathered again in that step.
         w = weight.detach()
         assert w.dtype == _F32 and w.is_contiguous()
+        src = (w.data_ptr(), None if bias is None else bias.detach().data_ptr())
+        if self.token == _PREFETCH[0] and self.gen == rt.PARAM_GEN and self.src == src:
+            return self
+        self.src = src
         dev = w.device
         _lib.call("rgbac_weight_gather", _lib.dtype_code(self.w.dtype), self.w.numel(),
                   w.data_ptr(), self.idx.data_ptr(), self.w.data_ptr(), _lib.stream_ptr(dev))
@@ -86,6 +95,58 @@ class TPack:
             _lib.call("rgbac_weight_gather", _lib.F32, self.bias.numel(), b.data_ptr(),
                       self.bias_idx.data_ptr(), self.bias.data_ptr(), _lib.stream_ptr(dev))
         return self
+
+
+PREFETCH = os.environ.get("RGBAC_PACK_PREFETCH", "1") != "0"
+_PREFETCH = [1]              # current prefetch token (TPack.token == it: gathered this step)
+_TASKS = {}
+
+
+def prefetch_packs(model):
+    """Re-gather every training weight pack of ``model`` (forward and input-gradient packs
+    of all layers, + their biases) in ONE rgbac_weight_gather_multi launch, instead of one
+    gather launch per pack (~420 per RGB training step).  Packs appear on the first step
+    (its per-layer refreshes record their sources); from then on each step's forward calls
+    this first."""
+    if not PREFETCH:
+        return
+    _PREFETCH[0] += 1
+    packs = []
+    for m in model.modules():
+        for tc in m.__dict__.get("_rgbac_train", {}).values():
+            packs.extend(tc._fw.values())
+            packs.extend(tc._bw.values())
+    # only packs of the model's own parameters: a weight computed in the forward (GDN's
+    # reparametrised gamma/beta) does not exist yet at this point of the step
+    pset = {p.data_ptr() for p in model.parameters()}
+    packs = [tp for tp in packs if tp.src is not None and tp.src[0] in pset and
+             (tp.src[1] is None or tp.src[1] in pset)]
+    if not packs:
+        return
+    key = tuple((id(tp), tp.src) for tp in packs)
+    ent = _TASKS.get(id(model))
+    if ent is None or ent[0] != key:
+        if torch.cuda.is_current_stream_capturing():
+            return                     # no host->device table upload inside a graph capture
+        rows, blk0 = [], [0]
+        for tp in packs:
+            for dst, idx, sp, dt in ((tp.w, tp.idx, tp.src[0], _lib.dtype_code(tp.w.dtype)),
+                                     (tp.bias, tp.bias_idx, tp.src[1], _lib.F32)):
+                if sp is None or idx is None or dst.numel() == 0:
+                    continue
+                n = dst.numel()
+                rows.append([sp, idx.data_ptr(), dst.data_ptr(), n, dt])
+                blk0.append(blk0[-1] + -(-n // 2048))
+        dev = packs[0].w.device
+        tasks = torch.tensor(rows, dtype=torch.int64, device=dev)
+        b0 = torch.tensor(blk0, dtype=torch.int64, device=dev)
+        ent = (key, tasks, b0, len(rows), blk0[-1])
+        _TASKS[id(model)] = ent
+    _, tasks, b0, ntask, nblk = ent
+    _lib.call("rgbac_weight_gather_multi", ntask, tasks.data_ptr(), b0.data_ptr(), nblk,
+              _lib.stream_ptr(tasks.device))
+    for tp in packs:
+        tp.token, tp.gen = _PREFETCH[0], rt.PARAM_GEN
 
 
 class TrainConv:

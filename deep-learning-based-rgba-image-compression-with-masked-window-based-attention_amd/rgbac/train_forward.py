@@ -169,6 +169,7 @@ def latent_t(model, y, training, noise_z=None, noise_y=None):
 
 def rgb_forward_train(model, input, mask, reconmask, me2, me3, noise_z=None, noise_y=None):
     """AutoEncoderRGB_Journal.forward with autograd -> (x_hat, mse, bpp, y_bpp, z_bpp)."""
+    ag.prefetch_packs(model)                 # every weight pack of the step: one launch
     B, _, H, W = input.shape
     dt = model.compute_dtype
     x = input.contiguous().float()

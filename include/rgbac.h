@@ -345,6 +345,13 @@ int rgbac_channel_copy(int dtype, int64_t npix, int channels, const void* src, i
  * (src = fp32 PyTorch parameter, dst = packed [nphase][cout_pad][k_pad]).   */
 int rgbac_weight_gather(int dtype, int64_t n, const float* src, const int32_t* idx, void* dst,
                         void* stream);
+
+/* Many rgbac_weight_gather calls in one launch: tasks[5*t ..] = {src (const
+ * float*), idx (const int32_t*), dst, n, dtype} as int64 in DEVICE memory;
+ * task t owns blocks [blk0[t], blk0[t+1]) of 2048 elements (blk0 in device
+ * memory, ntask + 1 entries, blk0[ntask] = nblk).                           */
+int rgbac_weight_gather_multi(int ntask, const int64_t* tasks, const int64_t* blk0, int64_t nblk,
+                              void* stream);
 /* Per-channel sums over pixels into partial[nsplit][channels] (bias grads). */
 int rgbac_colsum(int dtype, int64_t npix, int channels, const void* x, int64_t ldx, int nsplit,
                  float* partial, void* stream);
