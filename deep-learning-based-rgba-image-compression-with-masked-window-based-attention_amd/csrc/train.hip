@@ -393,7 +393,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WgradDev a) {
 __global__ void __launch_bounds__(256)
 wgrad_reduce_kernel(long long nslot, const int* __restrict__ fmap, const float* __restrict__ part,
                     int nsplit, long long slab, float* __restrict__ dw, int nbias,
-                    const float* __restrict__ bpart, int n_pad, float* __restrict__ db) {
+                    const float* __restrict__ bpart, int n_pad, float* __restrict__ db, int acc) {
   const long long total = nslot + nbias;
   for (long long e = blockIdx.x * 256ll + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
     if (e < nslot) {
@@ -401,12 +401,12 @@ wgrad_reduce_kernel(long long nslot, const int* __restrict__ fmap, const float* 
       if (i < 0) continue;
       float s = 0.0f;
       for (int q = 0; q < nsplit; ++q) s += part[q * slab + e];
-      dw[i] = s;
+      dw[i] = acc ? dw[i] + s : s;
     } else {
       const int j = (int)(e - nslot);
       float s = 0.0f;
       for (int q = 0; q < nsplit; ++q) s += bpart[(size_t)q * n_pad + j];
-      db[j] = s;
+      db[j] = acc ? db[j] + s : s;
     }
   }
 }
@@ -419,7 +419,7 @@ __global__ void __launch_bounds__(256)
 wgrad_reduce_wide_kernel(long long nslot, const int* __restrict__ fmap,
                          const float* __restrict__ part, int nsplit, long long slab,
                          float* __restrict__ dw, int nbias, const float* __restrict__ bpart,
-                         int n_pad, float* __restrict__ db) {
+                         int n_pad, float* __restrict__ db, int accum) {
   __shared__ float red[8][32];
   const int sl = threadIdx.x & 31, sg = threadIdx.x >> 5;
   const long long e = blockIdx.x * 32ll + sl;
@@ -448,9 +448,9 @@ wgrad_reduce_wide_kernel(long long nslot, const int* __restrict__ fmap,
     for (int g = 1; g < 8; ++g) s += red[g][sl];
     if (e < nslot) {
       const int i = fmap[e];
-      if (i >= 0) dw[i] = s;
+      if (i >= 0) dw[i] = accum ? dw[i] + s : s;
     } else {
-      db[e - nslot] = s;
+      db[e - nslot] = accum ? db[e - nslot] + s : s;
     }
   }
 }
@@ -1129,7 +1129,8 @@ extern "C" int rgbac_conv_wgrad(const rgbac_wgrad_args* a, void* stream) {
 
 extern "C" int rgbac_wgrad_reduce(int64_t nslot, const int32_t* fmap, const float* partial,
                                   int nsplit, int64_t slab, float* dw, int nbias,
-                                  const float* bias_partial, int n_pad, float* db, void* stream) {
+                                  const float* bias_partial, int n_pad, float* db, int accumulate,
+                                  void* stream) {
   RGBAC_REQUIRE(nslot >= 0 && nsplit >= 1 && slab > 0 && nslot <= slab, "shape");
   RGBAC_REQUIRE((nslot == 0 || (fmap && partial && dw)) && (nbias == 0 || (bias_partial && db)),
                 "null pointer");
@@ -1139,11 +1140,11 @@ extern "C" int rgbac_wgrad_reduce(int64_t nslot, const int32_t* fmap, const floa
     const long long nblk = (nslot + nbias + 31) / 32;
     if (nblk == 0) return RGBAC_OK;
     hipLaunchKernelGGL(wgrad_reduce_wide_kernel, dim3((unsigned)nblk), dim3(256), 0, st, nslot,
-                       fmap, partial, nsplit, slab, dw, nbias, bias_partial, n_pad, db);
+                       fmap, partial, nsplit, slab, dw, nbias, bias_partial, n_pad, db, accumulate);
     return check_launch("wgrad_reduce_wide_kernel");
   }
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(nslot + nbias)), dim3(256), 0, st, nslot,
-                     fmap, partial, nsplit, slab, dw, nbias, bias_partial, n_pad, db);
+                     fmap, partial, nsplit, slab, dw, nbias, bias_partial, n_pad, db, accumulate);
   return check_launch("wgrad_reduce_kernel");
 }
 

@@ -264,9 +264,11 @@ def _nsplit(tiles, M, slab):
     return int(max(1, min(want, -(-M // 512), cap, 1024)))
 
 
-def wgrad(G, S, ksize, stride, pad, square, k_pad, fmap, numel, nbias=0, bias_from_g=True):
+def wgrad(G, S, ksize, stride, pad, square, k_pad, fmap, numel, nbias=0, bias_from_g=True,
+          acc_dw=None, acc_db=None):
     """dW (fp32, flat param layout) and optional db from G (Feat on the M grid) and
-    sources S [Feat] sampled with (ksize, stride, pad)."""
+    sources S [Feat] sampled with (ksize, stride, pad).  ``acc_dw`` / ``acc_db`` (both or
+    neither): fp32 tensors the sums are ADDED into instead (param.grad), returned as is."""
     dev = G.t.device
     n_pad = round_up(G.ldc, 64)
     M = G.B * G.H * G.W
@@ -299,20 +301,24 @@ def wgrad(G, S, ksize, stride, pad, square, k_pad, fmap, numel, nbias=0, bias_fr
              lambda: _lib.call("rgbac_conv_wgrad", ctypes.byref(a), st),
              f"wgrad_kernel k{ksize}s{stride} G{G.ldc}@{G.H}x{G.W} S{cin}@{s0.H}x{s0.W} "
              f"B{G.B} split{ns}{' sq' if square else ''}")
-    dw = torch.empty(numel, dtype=_F32, device=dev)
-    db = torch.empty(nbias, dtype=_F32, device=dev) if nbias else None
+    acc = acc_dw is not None
+    dw = acc_dw if acc else torch.empty(numel, dtype=_F32, device=dev)
+    db = acc_db if acc else (torch.empty(nbias, dtype=_F32, device=dev) if nbias else None)
+    assert not acc or (dw.numel() == numel and dw.is_contiguous() and
+                       (not nbias or (db is not None and db.numel() == nbias)))
     if nbias and not bias_from_g:
         raise ValueError("use colsum for biases not on G")
     nslot = min(fmap.shape[0], n_pad) * k_pad
     _lib.call("rgbac_wgrad_reduce", nslot, fmap.data_ptr(), part.data_ptr(), ns,
               n_pad * k_pad, dw.data_ptr(), nbias if bpart is not None else 0,
               None if bpart is None else bpart.data_ptr(), n_pad,
-              None if db is None else db.data_ptr(), st)
+              None if db is None else db.data_ptr(), 1 if acc else 0, st)
     return dw, db
 
 
-def colsum(f, C):
-    """Per-channel sum over pixels of Feat ``f`` (first C channels) -> fp32 (C,)."""
+def colsum(f, C, acc=None):
+    """Per-channel sum over pixels of Feat ``f`` (first C channels) -> fp32 (C,) (added into
+    ``acc`` instead when given)."""
     dev = f.t.device
     npix = f.B * f.H * f.W
     ns = int(max(1, min(1024, -(-npix // 256))))
@@ -320,9 +326,9 @@ def colsum(f, C):
     st = _stream(f.t)
     _lib.call("rgbac_colsum", _lib.dtype_code(f.t.dtype), npix, C, f.ptr(), f.ldc, ns,
               part.data_ptr(), st)
-    db = torch.empty(C, dtype=_F32, device=dev)
+    db = acc if acc is not None else torch.empty(C, dtype=_F32, device=dev)
     _lib.call("rgbac_wgrad_reduce", 0, None, None, ns, 1, None, C, part.data_ptr(), C,
-              db.data_ptr(), st)
+              db.data_ptr(), 1 if acc is not None else 0, st)
     return db
 
 
@@ -354,6 +360,20 @@ def _act_bwd(act, slope, dy, z, r1, sel, C, want_r1):
     return dz, dr1
 
 
+DIRECT_GRAD = [True]
+
+
+def _direct_grad(p):
+    """p.grad when weight-gradient sums may be added into it in place: a leaf parameter
+    whose .grad is an attached fp32 contiguous tensor of its shape."""
+    if not DIRECT_GRAD[0] or p is None or not p.is_leaf or not p.requires_grad:
+        return None
+    g = p.grad
+    if g is None or g.dtype != _F32 or not g.is_contiguous() or g.shape != p.shape:
+        return None
+    return g
+
+
 class ConvFn(Function):
     @staticmethod
     def forward(ctx, call, weight, bias, res0, res1, res2, sel, *srcs):
@@ -382,6 +402,7 @@ class ConvFn(Function):
                         sel=sel, square=call.square, bias=bias is not None, zout=z)
         rt.launch([pr])
         ctx.call = call
+        ctx.bias_param = bias if (bias is not None and bias.is_leaf) else None
         ctx.has = (bias is not None, res0 is not None, res1 is not None, res2 is not None)
         ctx.shape = (f0.B, Ho, Wo, Cs)
         keep_r1 = res1 if call.act in ("gate", "gdn", "igdn") else None
@@ -448,17 +469,32 @@ class ConvFn(Function):
         g_w = g_b = None
         if need[1] or (has_b and need[2]):
             nb = tc.rows if (has_b and tc.kind != "convt") else 0
+            # parameters with an attached fp32 .grad (rgbac.optim.AdamClamp's flat-buffer
+            # views): the reduce adds straight into .grad, and autograd gets None -- no
+            # per-parameter accumulate launch (DIRECT_GRAD; off under bucketed DP, whose
+            # all-reduces are triggered by the accumulate hooks)
+            bias_p = ctx.bias_param
+            acc_w = _direct_grad(weight) if need[1] else None
+            acc_b = _direct_grad(bias_p) if (has_b and need[2]) else None
+            direct = acc_w is not None and (not has_b or not need[2] or acc_b is not None)
+            if not direct:
+                acc_w = acc_b = None
             if tc.kind == "convt":
                 # G = the convT input, S = dL/dv on the output grid
                 dw, _ = wgrad(feats[0], [dz], tc.ksize, tc.stride if tc.ksize == 5 else 1,
-                              tc.ksize // 2, False, tc.wg_kpad, tc.wg_fmap, tc.numel)
-                db = colsum(dz, tc.cout) if has_b else None
+                              tc.ksize // 2, False, tc.wg_kpad, tc.wg_fmap, tc.numel,
+                              acc_dw=None if acc_w is None else acc_w.view(-1),
+                              acc_db=None)
+                db = colsum(dz, tc.cout, acc=acc_b) if has_b else None
             else:
                 p = tc.ksize // 2
                 dw, db = wgrad(G, feats, tc.ksize, tc.stride, p, call.square, tc.wg_kpad,
-                               tc.wg_fmap, tc.numel, nbias=nb)
-            g_w = dw.view(weight.shape)
-            g_b = db
+                               tc.wg_fmap, tc.numel, nbias=nb,
+                               acc_dw=None if acc_w is None else acc_w.view(-1),
+                               acc_db=acc_b if nb else None)
+            if not direct:
+                g_w = dw.view(weight.shape)
+                g_b = db
         return (None, g_w, g_b, g_res0, g_res1, g_res2, None, *g_srcs)
 
 

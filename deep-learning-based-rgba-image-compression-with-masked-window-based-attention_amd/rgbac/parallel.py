@@ -92,6 +92,10 @@ class DataParallelTrainer:
         self.buckets = None
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             self.buckets = GradBuckets(optimizer.params, optimizer.flat_grad, bucket_bytes)
+            # the bucket all-reduces are launched from post-accumulate-grad hooks: keep
+            # autograd's per-parameter accumulation (no in-place weight-gradient adds)
+            from . import autograd as ag
+            ag.DIRECT_GRAD[0] = False
 
     def step(self, loss):
         self.opt.zero_grad()

@@ -277,10 +277,11 @@ int rgbac_conv_wgrad(const rgbac_wgrad_args* args, void* stream);
 /* Fixed-order sum of the slabs, scattered into the PyTorch parameter layout:
  * dw[fmap[e]] = sum_s partial[s*slab + e] for slab slots e < nslot with
  * fmap[e] >= 0 (fmap = the packed layout's slot -> parameter element map);
- * db[j] = sum_s bias_partial[s*n_pad + j], j < nbias.                       */
+ * db[j] = sum_s bias_partial[s*n_pad + j], j < nbias.  accumulate != 0: add
+ * the sums into dw / db (gradients accumulated straight into param.grad).    */
 int rgbac_wgrad_reduce(int64_t nslot, const int32_t* fmap, const float* partial, int nsplit,
                        int64_t slab, float* dw, int nbias, const float* bias_partial, int n_pad,
-                       float* db, void* stream);
+                       float* db, int accumulate, void* stream);
 
 /* Backward of rgbac_winattn_core: dqkv [B,H,W,>=3C] (dq, dk, dv; zero for
  * dropped windows) and per-block dense bias gradients bias_partial

@@ -447,3 +447,66 @@ def test_rgb_train_step_grads(dtype):
         if e > 2e-2:
             bad.append((n, e))
     assert not bad, bad[:10]
+
+
+def test_weight_gather_multi_matches_single_gathers():
+    """rgbac_weight_gather_multi (one launch over many packs, blocks found by binary search)
+    equals one rgbac_weight_gather per pack, for bf16 and fp32 destinations, -1 pad slots and
+    sizes that are not multiples of the 2048-element block."""
+    from rgbac import _lib
+    g = _gen(71)
+    dev = torch.device("cuda")
+    src = torch.randn(10000, generator=g).to(dev)
+    tasks, want, got, blk0 = [], [], [], [0]
+    for n, dt in ((5000, torch.bfloat16), (1, torch.float32), (2048, torch.bfloat16),
+                  (7000, torch.float32), (4097, torch.bfloat16)):
+        idx = torch.randint(-1, 10000, (n,), generator=g, dtype=torch.int32).to(dev)
+        w = torch.empty(n, dtype=dt, device=dev)
+        _lib.call("rgbac_weight_gather", _lib.dtype_code(dt), n, src.data_ptr(), idx.data_ptr(),
+                  w.data_ptr(), _lib.stream_ptr(dev))
+        o = torch.full((n,), 7.0, dtype=dt, device=dev)
+        tasks.append([src.data_ptr(), idx.data_ptr(), o.data_ptr(), n, _lib.dtype_code(dt)])
+        blk0.append(blk0[-1] + -(-n // 2048))
+        want.append((w, idx))
+        got.append(o)
+    t = torch.tensor(tasks, dtype=torch.int64, device=dev)
+    b = torch.tensor(blk0, dtype=torch.int64, device=dev)
+    _lib.call("rgbac_weight_gather_multi", len(tasks), t.data_ptr(), b.data_ptr(), blk0[-1],
+              _lib.stream_ptr(dev))
+    torch.cuda.synchronize()
+    for (w, idx), o in zip(want, got):
+        assert torch.equal(w, o)
+
+
+def test_direct_weight_grad_accumulation_matches_autograd():
+    """Weight/bias gradients added straight into attached fp32 .grad buffers (AdamClamp's
+    flat views; rgbac.autograd.DIRECT_GRAD) equal autograd's own accumulation, including
+    a second backward accumulating on top of the first."""
+    from rgbac import autograd as ag
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    from rgbac.optim import AdamClamp
+    torch.manual_seed(234)
+    base = AutoEncoder().train()
+    g = _gen(63)
+    B, H, W = 2, 64, 64
+    x = (torch.randint(0, 256, (B, 3, H, W), generator=g).float() / 255).cuda()
+    a = torch.ones((B, 1, H, W)).cuda()
+    me = [t.cuda() for t in ref.supply_mask(a.cpu())]
+    nz = (torch.rand((B, 1, 1, 192), generator=g) - 0.5).cuda()
+    ny = (torch.rand((B, 8, 8, 80), generator=g) - 0.5).cuda()
+    grads = []
+    for direct in (False, True):
+        n = AutoEncoder().cuda().train()
+        n.load_state_dict(base.state_dict())
+        opt = AdamClamp(n.parameters(), lr=1e-4)
+        ag.DIRECT_GRAD[0] = direct
+        try:
+            opt.zero_grad()
+            for _ in range(2):
+                out = n(x, a, a, *me[:4], noise_z=nz, noise_y=ny)
+                (4096.0 * out[1] + out[2]).backward()
+        finally:
+            ag.DIRECT_GRAD[0] = True
+        torch.cuda.synchronize()
+        grads.append(opt.flat_grad.clone())
+    assert rel(grads[1], grads[0]) < 1e-5
