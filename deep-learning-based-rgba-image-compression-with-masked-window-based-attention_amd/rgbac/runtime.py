@@ -486,7 +486,8 @@ def kernel_name(tile, preps):
         return f"conv_wres_kernel<{dt},{bm}x{bn}>"
     if tile >= FIRST_PERS:
         return f"conv_pers_kernel<{dt}, {_TILE_SIG[tile - FIRST_PERS]}>"
-    return f"conv_kernel<{dt}, {_TILE_SIG[tile]}>"
+    # tiles 0..6 instantiate conv_kernel's KSM = 1 default (rocprofv3 prints it)
+    return f"conv_kernel<{dt}, {_TILE_SIG[tile]}{', 1' if tile < FIRST_WRES else ''}>"
 
 
 def _smallk_ok(preps):
