@@ -279,6 +279,86 @@ def main_train(args, world, rank, dev, dist):
         dist.destroy_process_group()
 
 
+def cpu_baseline_codec(budget_s):
+    """Oracle compress (CPU fp32 symbols + the pure-Python rANS restatement) on 1 image."""
+    from oracle import ans_ref as oa
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    torch.manual_seed(234)
+    net = AutoEncoder().eval()
+    net.update()
+    sd = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+    gc = net.gaussian_conditional
+    tab = (gc.quantized_cdf.tolist(), gc.cdf_length.tolist(), gc.offset.tolist())
+    x, a = synth_inputs(2, 256, 256, seed=0)
+    x, a = x[1:2], a[1:2]
+    n, t0 = 0, time.perf_counter()
+    while True:
+        with torch.no_grad():
+            _, syms, idxs, _ = oa.rgb_compress_symbols(sd, x, a, gc.scale_table)
+        enc = oa.BufferedRansEncoder()
+        enc.encode_with_indexes(torch.cat([s.reshape(-1) for s in syms]).tolist(),
+                                torch.cat([i.reshape(-1) for i in idxs]).tolist(), *tab)
+        enc.flush()
+        n += 1
+        if time.perf_counter() - t0 >= budget_s or n >= 100:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n * 256 * 256 / dt / 1e6, 4), "unit": "MPix/s",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle compress (fp32 symbols + pure-Python rANS of y), 1 image "
+                      f"256x256 (half-transparent alpha), {n} iterations, {dt:.1f} s"}
+
+
+def main_codec(args, dev):
+    """--codec: AutoEncoder.compress + decompress (AutoEncoderRGB_Journal.py:312-416) end to
+    end: GPU transforms + symbol/index kernels, device<->host copies, host rANS coder."""
+    from rgbac.layers.SupplyMask import mask_pyramid
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    torch.manual_seed(234)
+    net = AutoEncoder().eval().to(dev).set_compute_dtype(dt)
+    net.update()
+    B, S = args.batch, args.size
+    x, a = synth_inputs(B, S, S, seed=0)
+    x, a = x.to(dev), a.to(dev)
+    for _ in range(max(args.warmup, 1)):
+        out = net.compress(x, a)
+        rec = net.decompress(out["strings"], out["shape"], a)
+    torch.cuda.synchronize()
+    tc, td = [], []
+    for _ in range(args.steps):
+        t0 = time.perf_counter()
+        out = net.compress(x, a)
+        t1 = time.perf_counter()
+        rec = net.decompress(out["strings"], out["shape"], a)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        tc.append(t1 - t0)
+        td.append(t2 - t1)
+    tc.sort()
+    td.sort()
+    mc, md = tc[len(tc) // 2], td[len(td) // 2]
+    nbytes = sum(len(s) for s in out["strings"][0]) + sum(len(s) for s in out["strings"][1])
+    _, me = mask_pyramid(a, 4)
+    with torch.no_grad():
+        fwd = net(x, a, a, *me)
+    npx = B * S * S
+    rec = {"metric": "MPixels/sec compress+decompress (real rANS bitstream), 256x256 RGBA batch",
+           "value": round(npx / (mc + md) / 1e6, 3), "unit": "MPix/s", "n_gpus": 1,
+           "steps": args.steps, "warmup": args.warmup, "ms_per_step": round((mc + md) * 1e3, 3),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+           "data": "synthetic (seeded RGB k/255 + 4 alpha patterns; random-init weights)",
+           "config": {"workload": f"AutoEncoderRGB_Journal compress + decompress, {S}x{S}",
+                      "batch": B},
+           "compress_ms": round(mc * 1e3, 3), "decompress_ms": round(md * 1e3, 3),
+           "compress_mpix_s": round(npx / mc / 1e6, 3), "decompress_mpix_s": round(npx / md / 1e6, 3),
+           "actual_bpp": round(8 * nbytes / npx, 5), "estimated_bpp": round(fwd[2].item(), 5),
+           "cpu_baseline": None}
+    if not args.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline_codec(args.cpu_seconds)
+    print(json.dumps(rec), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -294,6 +374,8 @@ def main():
     ap.add_argument("--layers", default=None, help="write a per-layer time table to this file")
     ap.add_argument("--train", action="store_true",
                     help="time the training step (BASELINE config 3 / 5) instead of the forward")
+    ap.add_argument("--codec", action="store_true",
+                    help="time compress + decompress (real bitstream) instead of the forward")
     ap.add_argument("--tune-cache", default=None,
                     help="tile-choice cache to load (default: the committed profiles/ one for "
                          "the forward config); '' disables")
@@ -317,6 +399,8 @@ def main():
 
     if args.train:
         return main_train(args, world, rank, dev, dist)
+    if args.codec:
+        return main_codec(args, dev)
 
     from rgbac import runtime as rt
     from rgbac.layers.SupplyMask import mask_pyramid

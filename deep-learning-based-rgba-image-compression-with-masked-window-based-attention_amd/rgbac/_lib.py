@@ -78,6 +78,12 @@ class RuArgs(ctypes.Structure):
     ]
 
 
+class RansDecoderState(ctypes.Structure):
+    """rgbac_rans_decoder_t"""
+    _fields_ = [("state", ctypes.c_uint64), ("data", ctypes.c_void_p), ("size", ctypes.c_int64),
+                ("pos", ctypes.c_int64)]
+
+
 _VP, _I32, _I64, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_float
 _D = ctypes.c_double
 # name -> argtypes (restype int unless noted); must match include/rgbac.h
@@ -128,7 +134,21 @@ SIGNATURES = {
     "rgbac_weight_gather_multi": [_I32, _VP, _VP, _I64, _VP],
     "rgbac_colsum": [_I32, _I64, _I32, _VP, _I64, _I32, _VP, _VP],
     "rgbac_sum_partials": [_I32, _I32, _VP, _VP, _VP],
+    # bitstream (GPU symbol/index work + host rANS coder)
+    "rgbac_gauss_code": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _I64, _VP, _I64, _VP, _I32, _F,
+                         _VP, _VP, _VP, _I64, _VP],
+    "rgbac_eb_code": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _I64, _VP, _VP, _VP, _I64, _VP],
+    "rgbac_pmf_to_quantized_cdf": [_VP, _I32, _I32, _VP],
+    "rgbac_rans_encoder_create": [ctypes.POINTER(ctypes.c_void_p)],
+    "rgbac_rans_encoder_destroy": [_VP],
+    "rgbac_rans_encoder_put": [_VP, _VP, _VP, _I64, _VP, _I32, _VP, _VP, _I32],
+    "rgbac_rans_encoder_bound": [_VP],
+    "rgbac_rans_encoder_flush": [_VP, _VP, _I64, ctypes.POINTER(ctypes.c_int64)],
+    "rgbac_rans_decoder_init": [ctypes.POINTER(RansDecoderState), _VP, _I64],
+    "rgbac_rans_decode": [ctypes.POINTER(RansDecoderState), _VP, _I64, _VP, _I32, _VP, _VP, _I32,
+                          _VP],
 }
+_RESTYPE = {"rgbac_last_error": ctypes.c_char_p, "rgbac_rans_encoder_bound": ctypes.c_int64}
 
 _lib = None
 
@@ -146,7 +166,7 @@ def load(path=LIB_PATH):
     for name, args in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.argtypes = args
-        fn.restype = ctypes.c_char_p if name == "rgbac_last_error" else ctypes.c_int
+        fn.restype = _RESTYPE.get(name, ctypes.c_int)
     _lib = lib
     return lib
 

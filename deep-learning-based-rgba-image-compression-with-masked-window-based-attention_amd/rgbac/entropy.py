@@ -6,8 +6,10 @@ models/AutoEncoderRGB_Journal.py:4-6; version unpinned, the no-arg
 ``CompressionModel()`` implies >= 1.2).  compressai is not vendored and not
 installed, so these classes re-create its parameter/buffer layout (so
 checkpoints load unchanged) and its forward semantics, which run in
-rgbac_eb_forward / rgbac_gaussian_slice.  The rANS bitstream path
-(compress/decompress) is out of scope for this round.
+rgbac_eb_forward / rgbac_gaussian_slice.  The bitstream side (``update`` -> CDF tables,
+``build_indexes`` / ``quantize`` / ``dequantize``, ``compress`` / ``decompress``) follows
+compressai's EntropyModel API; the tables are built by rgbac.ans.pmf_to_quantized_cdf and
+the strings by the host rANS coder (csrc/rans.cpp), byte-compatible with compressai.ans.
 """
 import math
 
@@ -40,6 +42,83 @@ class _EntropyModel(nn.Module):
         self.register_buffer("_offset", torch.IntTensor())
         self.register_buffer("_quantized_cdf", torch.IntTensor())
         self.register_buffer("_cdf_length", torch.IntTensor())
+        self.entropy_coder_precision = 16
+
+    # compressai EntropyModel properties
+    @property
+    def offset(self):
+        return self._offset
+
+    @property
+    def quantized_cdf(self):
+        return self._quantized_cdf
+
+    @property
+    def cdf_length(self):
+        return self._cdf_length
+
+    def _check_cdf(self):
+        if self._offset.numel() == 0 or self._quantized_cdf.numel() == 0:
+            raise ValueError("Uninitialized CDFs. Run update() first")
+
+    def _pmf_to_cdf(self, pmf, tail_mass, pmf_length, max_length):
+        """EntropyModel._pmf_to_cdf: per row, quantise [pmf[:len], tail] to a 16-bit CDF."""
+        from .ans import pmf_to_quantized_cdf
+        cdf = torch.zeros((len(pmf_length), max_length + 2), dtype=torch.int32)
+        pmf, tail_mass, lens = pmf.detach().cpu(), tail_mass.detach().cpu(), pmf_length.tolist()
+        for i, p in enumerate(pmf):
+            prob = torch.cat((p[:lens[i]], tail_mass[i]), dim=0)
+            c = pmf_to_quantized_cdf(prob, self.entropy_coder_precision)
+            cdf[i, :len(c)] = torch.tensor(c, dtype=torch.int32)
+        return cdf.to(pmf_length.device)
+
+    def tables(self):
+        """(cdfs, cdf_lengths, offsets) packed for the host coder (cached per update)."""
+        from .ans import CdfTables
+        self._check_cdf()
+        bufs = (self._quantized_cdf, self._cdf_length, self._offset)
+        vers = tuple(b._version for b in bufs)
+        ent = self.__dict__.get("_rgbac_tables")      # holds the buffers: identity is safe
+        if ent is None or any(a is not b for a, b in zip(ent[0], bufs)) or ent[1] != vers:
+            ent = (bufs, vers, CdfTables(*bufs))
+            self.__dict__["_rgbac_tables"] = ent
+        return ent[2]
+
+    def quantize(self, inputs, mode, means=None):
+        """EntropyModel.quantize for mode "symbols" / "dequantize" (inference)."""
+        if mode not in ("symbols", "dequantize"):
+            raise ValueError(f'Invalid quantization mode: "{mode}"')
+        outputs = inputs.clone() if means is None else inputs - means
+        outputs = torch.round(outputs)
+        if mode == "dequantize":
+            return outputs if means is None else outputs + means
+        return outputs.int()
+
+    @staticmethod
+    def dequantize(inputs, means=None, dtype=torch.float):
+        outputs = inputs.type(dtype)
+        return outputs if means is None else outputs + means
+
+    def compress(self, inputs, indexes, means=None):
+        """EntropyModel.compress: one string per batch element."""
+        from .ans import RansEncoder
+        symbols = self.quantize(inputs, "symbols", means)
+        tab = self.tables()
+        sym, idx = symbols.cpu(), indexes.int().cpu()
+        return [RansEncoder().encode_with_indexes(sym[i].reshape(-1), idx[i].reshape(-1), tab)
+                for i in range(symbols.size(0))]
+
+    def decompress(self, strings, indexes, dtype=torch.float, means=None):
+        from .ans import RansDecoder
+        tab = self.tables()
+        outputs = torch.empty(indexes.size(), dtype=torch.int32)
+        idx = indexes.int().cpu()
+        for i, s in enumerate(strings):
+            dec = RansDecoder()
+            dec.set_stream(s)
+            outputs[i] = torch.from_numpy(dec.decode_stream_np(idx[i].reshape(-1), tab)).reshape(
+                outputs[i].size())
+        return self.dequantize(outputs.to(indexes.device), means, dtype)
 
 
 class EntropyBottleneck(_EntropyModel):
@@ -109,6 +188,47 @@ class EntropyBottleneck(_EntropyModel):
                 logits = logits + torch.tanh(fac) * torch.tanh(logits)
         return logits
 
+    def update(self, force=False, update_quantiles=False):
+        """EntropyBottleneck.update: per-channel 16-bit CDFs of the factorized density over
+        [median - minima, median + maxima] (+ tail bin)."""
+        if self._offset.numel() > 0 and not force:
+            return False
+        with torch.no_grad():
+            q = self.quantiles.detach()
+            medians = q[:, 0, 1]
+            minima = torch.clamp(torch.ceil(medians - q[:, 0, 0]).int(), min=0)
+            maxima = torch.clamp(torch.ceil(q[:, 0, 2] - medians).int(), min=0)
+            self._offset = -minima
+            pmf_start = medians - minima
+            pmf_length = maxima + minima + 1
+            max_length = int(pmf_length.max().item())
+            samples = torch.arange(max_length, device=q.device)[None, :] + pmf_start[:, None, None]
+            lower = self._logits_cumulative(samples - 0.5, stop_gradient=True)
+            upper = self._logits_cumulative(samples + 0.5, stop_gradient=True)
+            pmf = (torch.sigmoid(upper) - torch.sigmoid(lower))[:, 0, :]
+            tail_mass = torch.sigmoid(lower[:, 0, :1]) + torch.sigmoid(-upper[:, 0, -1:])
+            self._quantized_cdf = self._pmf_to_cdf(pmf, tail_mass, pmf_length, max_length)
+            self._cdf_length = pmf_length + 2
+        return True
+
+    def _build_indexes(self, size):
+        N, C = size[0], size[1]
+        view = (1, -1) + (1,) * (len(size) - 2)
+        return torch.arange(C, dtype=torch.int32).view(*view).expand(N, *size[1:]).int()
+
+    def compress(self, x):
+        """EntropyBottleneck.compress(x) -> one string per image (indexes = channel)."""
+        self._check_cdf()
+        med = self._get_medians().detach().reshape(1, -1, *([1] * (x.dim() - 2)))
+        return super().compress(x, self._build_indexes(x.size()), med)
+
+    def decompress(self, strings, size):
+        self._check_cdf()
+        out_size = (len(strings), self._quantized_cdf.size(0), *size)
+        med = self._get_medians().detach().reshape(1, -1, *([1] * len(size)))
+        idx = self._build_indexes(out_size).to(self._quantized_cdf.device)
+        return super().decompress(strings, idx, med.dtype, med)
+
     def loss(self):
         """Auxiliary quantile loss (compressai EntropyBottleneck.loss); tiny, host-side torch."""
         logits = self._logits_cumulative(self.quantiles, stop_gradient=True)
@@ -136,9 +256,45 @@ class GaussianConditional(_EntropyModel):
     def update_scale_table(self, scale_table, force=False):
         if self._offset.numel() > 0 and not force:
             return False
-        self.scale_table = torch.as_tensor(scale_table, dtype=torch.float32,
-                                           device=self.scale_bound.device)
+        self.scale_table = torch.Tensor(tuple(float(s) for s in scale_table)).to(
+            self.scale_bound.device)
+        self.update()
         return True
+
+    def update(self):
+        """GaussianConditional.update: one 16-bit CDF per scale_table entry, centred
+        Gaussian pmf over +-ceil(scale * multiplier) (+ tail bin)."""
+        from scipy.stats import norm
+        multiplier = -float(norm.ppf(self.tail_mass / 2))      # _standardized_quantile
+        with torch.no_grad():
+            st = self.scale_table
+            pmf_center = torch.ceil(st * multiplier).int()
+            pmf_length = 2 * pmf_center + 1
+            max_length = int(torch.max(pmf_length).item())
+            samples = torch.abs(torch.arange(max_length, device=st.device).int() -
+                                pmf_center[:, None]).float()
+            samples_scale = st.unsqueeze(1).float()
+            upper = _std_cumulative((0.5 - samples) / samples_scale)
+            lower = _std_cumulative((-0.5 - samples) / samples_scale)
+            pmf = upper - lower
+            tail_mass = 2 * lower[:, :1]
+            self._quantized_cdf = self._pmf_to_cdf(pmf, tail_mass, pmf_length, max_length)
+            self._offset = -pmf_center
+            self._cdf_length = pmf_length + 2
+
+    def build_indexes(self, scales):
+        """GaussianConditional.build_indexes (API surface; the model path runs it in
+        rgbac_gauss_code)."""
+        scales = torch.max(scales, self.lower_bound_scale.bound.to(scales.device))
+        indexes = scales.new_full(scales.size(), len(self.scale_table) - 1).int()
+        for s in self.scale_table[:-1]:
+            indexes -= (scales <= s).int()
+        return indexes
+
+
+def _std_cumulative(t):
+    # GaussianConditional._standardized_cumulative
+    return 0.5 * torch.erfc(float(-(2 ** -0.5)) * t)
 
 
 # ---------------------------------------------------------------- HIP calls

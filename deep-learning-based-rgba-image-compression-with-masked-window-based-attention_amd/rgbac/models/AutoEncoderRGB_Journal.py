@@ -55,9 +55,15 @@ class _CompressionModelMixin:
         return sum(m.loss() for m in self.modules() if isinstance(m, EntropyBottleneck))
 
     def update(self, scale_table=None, force=False):
+        """:306-311: GaussianConditional scale table + CDFs, then (CompressionModel.update)
+        every EntropyBottleneck's CDFs."""
         if scale_table is None:
             scale_table = get_scale_table()
-        return self.gaussian_conditional.update_scale_table(scale_table, force=force)
+        updated = self.gaussian_conditional.update_scale_table(scale_table, force=force)
+        for m in self.modules():
+            if isinstance(m, EntropyBottleneck):
+                updated |= m.update(force=force)
+        return updated
 
     def load_state_dict(self, state_dict, strict=True):
         # compressai resizes the (initially empty) CDF buffers before loading
@@ -68,13 +74,6 @@ class _CompressionModelMixin:
                 mod = self.get_submodule(name.rsplit(".", 1)[0])
                 setattr(mod, base, torch.empty_like(state_dict[name], device=buf.device))
         return nn.Module.load_state_dict(self, state_dict, strict=strict)
-
-    def compress(self, *args, **kwargs):
-        raise NotImplementedError("rANS bitstream coding is out of scope this round "
-                                  "(SURVEY.md §8f rank 1); forward() estimates bpp")
-
-    def decompress(self, *args, **kwargs):
-        raise NotImplementedError("rANS bitstream coding is out of scope this round")
 
 
 def _stack3(cin, cout=8):
@@ -133,6 +132,16 @@ class AutoEncoder(_CompressionModelMixin, nn.Module):
         self.entropy_bottleneck = EntropyBottleneck(192)
         self.gaussian_conditional = GaussianConditional(None)
         self.compute_dtype = torch.float32
+
+    def compress(self, input, mask):
+        """:312-371 on the HIP path (rgbac/models/_codec.py) + the host rANS coder."""
+        from ._codec import compress
+        return compress(self, input, mask)
+
+    def decompress(self, strings, shape, mask):
+        """:373-416; decodes the batch of len(strings[1]) images (the reference: 1)."""
+        from ._codec import decompress
+        return decompress(self, strings, shape, mask)
 
     def set_compute_dtype(self, dtype):
         assert dtype in (torch.float32, torch.bfloat16)

@@ -10,6 +10,7 @@ Data layout in HBM:
 torch is used here only for device allocation and the (cached) weight
 repack; every arithmetic op of the forward runs in librgbac_hip.so.
 """
+import contextlib
 import ctypes
 import json
 import os
@@ -214,6 +215,22 @@ def _heuristic(M, cout, nst):
 
 def tune_cache():
     return dict(_tune_cache)
+
+
+_FIXED = [0]
+
+
+@contextlib.contextmanager
+def fixed_tiles():
+    """Within this context every conv launch takes its tile / split-K from the shape rule
+    alone (no timing-based autotune, tune cache neither read nor written).  The bitstream
+    path needs bit-identical mu / sigma in compress and decompress, whichever process (and
+    tuning history) runs them: a different tile or split-K changes the fp32 summation order."""
+    _FIXED[0] += 1
+    try:
+        yield
+    finally:
+        _FIXED[0] -= 1
 
 
 def load_tune_cache(path):
@@ -556,7 +573,8 @@ def launch(preps):
     def run():
         _lib.call("rgbac_conv2d_grouped", ctypes.addressof(arr), n, _lib.stream_ptr(dev))
 
-    choice = FORCE if (FORCE and not gauss) else _tune_cache.get(key)
+    fixed = _FIXED[0] > 0
+    choice = None if fixed else (FORCE if (FORCE and not gauss) else _tune_cache.get(key))
     if choice is None:
         mtot = p0.mgrid * p0.nphase * n
         cout = max(pr.pk.cout for pr in preps)
@@ -569,7 +587,7 @@ def launch(preps):
             cands = _candidates(mtot, cout, nst, max(pr.nks for pr in preps),
                                 p0.pk.mode == CONV, _spatial_ok(preps), _smallk_ok(preps),
                                 _wstream_ok(preps))
-        if TUNE and not torch.cuda.is_current_stream_capturing():
+        if TUNE and not fixed and not torch.cuda.is_current_stream_capturing():
             best = None
             for cand in cands:
                 set_choice(*cand)
@@ -589,7 +607,8 @@ def launch(preps):
             choice = min(cands, key=lambda c: TILES[c[0]][1])
         else:
             choice = _heuristic(mtot, cout, nst)
-        _tune_cache[key] = choice
+        if not fixed:
+            _tune_cache[key] = choice
     if gauss and not (choice[0] == TILE_WSTREAM and _wstream_ok(preps)) and (
             choice[0] not in GAUSS_TILES or
             not _gauss_ok(choice[0], max(pr.pk.cout for pr in preps))):

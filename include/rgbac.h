@@ -378,6 +378,57 @@ int rgbac_timer_record(void* event, void* stream);
 int rgbac_timer_elapsed_ms(void* start, void* stop, float* ms);
 int rgbac_timer_destroy(void* event);
 
+/* ---------------------------------------------------------------- bitstream (§8f rank 1)
+ * GPU side of AutoEncoder.compress / decompress (AutoEncoderRGB_Journal.py:312-416).
+ * Symbols and CDF indexes are int32 in NCHW order of each slice: o = ((b*cs + c)*h + y)*w + x,
+ * the order of the reference's y_q_slice.reshape(-1).tolist() (:354-355) / index (:401).
+ *
+ * rgbac_gauss_code: one latent slice, NHWC activations.  ms holds (mu | sigma): mu in
+ * channels [0, cs), sigma in [cs, 2cs) (the cc_mean / cc_scale outputs, :343-348).
+ *   mode 0 (compress):   sym = int(round(y - mu)) (quantize "symbols", half-to-even),
+ *                        idx = build_indexes(sigma), pre = sym + mu           (:350-352)
+ *   mode 1 (indexes):    idx = build_indexes(sigma)                            (:400)
+ *   mode 2 (dequantize): pre = sym + mu                                        (:403)
+ * build_indexes: s' = max(sigma, scale_bound); idx = n_scales-1 - #{t < n_scales-1 :
+ * s' <= table[t]} (compressai GaussianConditional.build_indexes).  y is read at channel
+ * offset 0 of its pointer (pass y + slice offset). */
+int rgbac_gauss_code(int dtype, int mode, int batch, int h, int w, int cs, const void* y,
+                     int64_t ldy, const void* ms, int64_t ldm, const float* scale_table,
+                     int n_scales, float scale_bound, int32_t* sym, int32_t* idx, void* pre,
+                     int64_t ldp, void* stream);
+/* rgbac_eb_code: EntropyBottleneck.compress / decompress element work (:319-320,:374),
+ * z / z_hat NHWC (batch, h, w, channels), sym NCHW int32, medians fp32 [channels].
+ *   mode 0: sym = int(round(z - med)), z_hat = sym + med;   mode 1: z_hat = sym + med. */
+int rgbac_eb_code(int dtype, int mode, int batch, int h, int w, int channels, const void* z,
+                  int64_t ldz, const float* medians, int32_t* sym, void* z_hat, int64_t ldh,
+                  void* stream);
+
+/* Host-side range-ANS coder (csrc/rans.cpp), byte-compatible with compressai.ans:
+ * replaces BufferedRansEncoder.encode_with_indexes/flush (:334,:367-368), RansDecoder
+ * set_stream/decode_stream (:387-388,:401) and the EntropyModel compress/decompress coders.
+ * CDF tables: cdfs[ncdf][cdf_stride] int32, row i valid up to cdf_sizes[i]; offsets[ncdf]
+ * (compressai's _quantized_cdf / _cdf_length / _offset buffers). */
+int rgbac_pmf_to_quantized_cdf(const float* pmf, int n, int precision, uint32_t* cdf);
+int rgbac_rans_encoder_create(void** handle);
+int rgbac_rans_encoder_destroy(void* handle);
+int rgbac_rans_encoder_put(void* handle, const int32_t* symbols, const int32_t* indexes,
+                           int64_t n, const int32_t* cdfs, int cdf_stride,
+                           const int32_t* cdf_sizes, const int32_t* offsets, int ncdf);
+/* upper bound of the flushed stream size in bytes (-1 for a NULL handle) */
+int64_t rgbac_rans_encoder_bound(void* handle);
+int rgbac_rans_encoder_flush(void* handle, uint8_t* out, int64_t capacity, int64_t* nbytes);
+/* caller-owned decoder state over a caller-owned byte stream */
+typedef struct rgbac_rans_decoder {
+  uint64_t state;
+  const uint8_t* data;
+  int64_t size;
+  int64_t pos;
+} rgbac_rans_decoder_t;
+int rgbac_rans_decoder_init(rgbac_rans_decoder_t* dec, const uint8_t* data, int64_t nbytes);
+int rgbac_rans_decode(rgbac_rans_decoder_t* dec, const int32_t* indexes, int64_t n,
+                      const int32_t* cdfs, int cdf_stride, const int32_t* cdf_sizes,
+                      const int32_t* offsets, int ncdf, int32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -19,7 +19,7 @@ HEADER = os.path.join(ROOT, "include", "rgbac.h")
 
 def header_functions():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(rgbac_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|const char\*)\s+(rgbac_\w+)\s*\(", txt, re.M)))
 
 
 def test_library_exports_every_header_symbol():
