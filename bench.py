@@ -359,6 +359,88 @@ def main_codec(args, dev):
     print(json.dumps(rec), flush=True)
 
 
+def cpu_baseline_rgba(budget_s):
+    """Oracle alpha codec + constraint + RGB codec (trainRGB.py:282-306) on 1 image, fp32."""
+    from oracle import ref_model as ref
+    from rgbac.models.AutoEncoderMask_Journal import AutoEncoder as MaskNet
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder as RGBNet
+    torch.manual_seed(234)
+    sdr = {k: v.detach() for k, v in RGBNet().state_dict().items()}
+    sdm = {k: v.detach() for k, v in MaskNet().state_dict().items()}
+    x, a = synth_inputs(2, 256, 256, seed=0)
+    x, a = x[1:2], a[1:2]
+    n, t0 = 0, time.perf_counter()
+    while True:
+        with torch.no_grad():
+            ref.rgba_forward(sdm, sdr, x, a)
+        n += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n * 256 * 256 / dt / 1e6, 4), "unit": "MPix/s",
+            "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"oracle rgba_forward fp32 (alpha codec + constraint + RGB codec), 1 image "
+                      f"256x256 (half-transparent alpha), {n} iterations, {dt:.1f} s"}
+
+
+def main_rgba(args, dev):
+    """--rgba: the RGBA evaluation pipeline (trainRGB.py:282-306): alpha
+    codec forward -> clamp/round/constraint -> RGB codec forward -> clamp + bpp/PSNR, all on
+    the GPU, one HIP graph per step."""
+    from rgbac.models.AutoEncoderMask_Journal import AutoEncoder as MaskNet
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder as RGBNet
+    from rgbac.rgba import rgba_forward
+    dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    torch.manual_seed(234)
+    net = RGBNet().eval().to(dev).set_compute_dtype(dt)
+    msk = MaskNet().eval().to(dev).set_compute_dtype(dt)
+    B, S = args.batch, args.size
+    x, a = synth_inputs(B, S, S, seed=0)
+    x, a = x.to(dev), a.to(dev)
+
+    def step():
+        return rgba_forward(msk, net, x, a)
+
+    step()
+    torch.cuda.synchronize()
+    run = step
+    if not args.no_graph:
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                step()
+        torch.cuda.current_stream().wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            out = step()
+        run = graph.replay
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    if args.no_graph:
+        out = step()
+    npx = B * S * S
+    rec = {"metric": "MPixels/sec RGBA encode+decode (alpha codec -> constraint -> RGB codec)",
+           "value": round(npx * args.steps / el / 1e6, 3), "unit": "MPix/s", "n_gpus": 1,
+           "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+           "data": "synthetic (seeded RGB k/255 + 4 alpha patterns; random-init weights)",
+           "config": {"workload": f"RGBA eval pipeline trainRGB.py:282-306, {S}x{S}",
+                      "batch": B, "hip_graph": not args.no_graph},
+           "bpp": round(out[3].item(), 5), "psnr": round(out[4].item(), 4),
+           "cpu_baseline": None}
+    if not args.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline_rgba(args.cpu_seconds)
+    print(json.dumps(rec), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -374,6 +456,8 @@ def main():
     ap.add_argument("--layers", default=None, help="write a per-layer time table to this file")
     ap.add_argument("--train", action="store_true",
                     help="time the training step (BASELINE config 3 / 5) instead of the forward")
+    ap.add_argument("--rgba", action="store_true",
+                    help="RGBA eval pipeline: alpha codec -> constraint -> RGB codec")
     ap.add_argument("--codec", action="store_true",
                     help="time compress + decompress (real bitstream) instead of the forward")
     ap.add_argument("--tune-cache", default=None,
@@ -401,6 +485,8 @@ def main():
         return main_train(args, world, rank, dev, dist)
     if args.codec:
         return main_codec(args, dev)
+    if args.rgba:
+        return main_rgba(args, dev)
 
     from rgbac import runtime as rt
     from rgbac.layers.SupplyMask import mask_pyramid

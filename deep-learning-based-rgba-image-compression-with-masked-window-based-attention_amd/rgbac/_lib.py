@@ -138,6 +138,9 @@ SIGNATURES = {
     "rgbac_gauss_code": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _I64, _VP, _I64, _VP, _I32, _F,
                          _VP, _VP, _VP, _I64, _VP],
     "rgbac_eb_code": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _I64, _VP, _VP, _VP, _I64, _VP],
+    # RGBA eval pipeline (alpha recon -> RGB codec)
+    "rgbac_alpha_recon": [_I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP],
+    "rgbac_rgba_finish": [_I64, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP, _VP],
     "rgbac_pmf_to_quantized_cdf": [_VP, _I32, _I32, _VP],
     "rgbac_rans_encoder_create": [ctypes.POINTER(ctypes.c_void_p)],
     "rgbac_rans_encoder_destroy": [_VP],

@@ -403,6 +403,22 @@ int rgbac_eb_code(int dtype, int mode, int batch, int h, int w, int channels, co
                   int64_t ldz, const float* medians, int32_t* sym, void* z_hat, int64_t ldh,
                   void* stream);
 
+/* RGBA evaluation pipeline (csrc/rgba.hip), replaces trainRGB.py:284-304 between the alpha
+ * codec and the RGB codec.  All tensors fp32 NCHW, single channel for the alpha planes.
+ * rgbac_alpha_recon: recon = constraint(quantise ? round(clamp(x,0,1)*255)/255 : x)
+ *   (trainRGB.py:285-287 and constraint() :98-111; recon must not alias x).  When
+ *   true_mask is given, *not_all_ones is reset and set to 1 if any true_mask != 1
+ *   (the `torch.all(mask == 1.0)` test of :300, on the device).
+ * rgbac_rgba_finish: x_out = clamp(x_hat, 0, 1) (:290; may alias x_hat); optional scalars
+ *   bpp_total = bpp + (*not_all_ones ? *bpp_mask : 0) (:300-303) and
+ *   psnr = 10*log(1/mse)/log(10) (:306). */
+int rgbac_alpha_recon(int batch, int h, int w, int quantise, const float* x_hat_mask,
+                      float* recon_mask, const float* true_mask, int32_t* not_all_ones,
+                      void* stream);
+int rgbac_rgba_finish(int64_t n, const float* x_hat, float* x_out, const float* bpp,
+                      const float* bpp_mask, const int32_t* not_all_ones, const float* mse,
+                      float* bpp_total, float* psnr, void* stream);
+
 /* Host-side range-ANS coder (csrc/rans.cpp), byte-compatible with compressai.ans:
  * replaces BufferedRansEncoder.encode_with_indexes/flush (:334,:367-368), RansDecoder
  * set_stream/decode_stream (:387-388,:401) and the EntropyModel compress/decompress coders.

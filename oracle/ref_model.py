@@ -492,3 +492,24 @@ def constraint_rgb(t):
     t[iz] = 1
     t[io] = 0
     return t
+
+
+def recon_alpha(x_hat_mask):
+    """trainRGB.py:285-287: clamp(0,1) -> round(.*255)/255 -> constraint."""
+    t = torch.clamp(x_hat_mask, 0, 1)
+    t = torch.round(t * 255) / 255
+    return constraint_rgb(t)
+
+
+def rgba_forward(sd_mask, sd_rgb, masked_input, mask):
+    """trainRGB.py:282-306 (eval loop body, >=500k-step regime) ->
+    (clipped image, recon mask, mse, bpp incl. alpha bpp unless mask is all ones, psnr)."""
+    me = supply_mask(mask)                                       # EncMakeMask  :283
+    om = mask_forward(sd_mask, mask)                             # masknet      :284
+    rm = recon_alpha(om[0])                                      # :285-287
+    x_hat, mse, bpp = rgb_forward(sd_rgb, masked_input, mask, rm, *me[:4])[:3]   # :289
+    img = torch.clamp(x_hat, 0, 1)                               # :290
+    if not torch.all(mask == 1.0):                               # :300-303
+        bpp = bpp + om[2]
+    psnr = 10 * (torch.log(1. / mse) / torch.log(torch.tensor(10.)))   # :306
+    return img, rm, mse, bpp, psnr
