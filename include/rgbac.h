@@ -419,6 +419,21 @@ int rgbac_rgba_finish(int64_t n, const float* x_hat, float* x_out, const float* 
                       const float* bpp_mask, const int32_t* not_all_ones, const float* mse,
                       float* bpp_total, float* psnr, void* stream);
 
+/* MS-SSIM / SSIM metric (csrc/msssim.hip), replaces metrics/ms_ssim_torch.py:5-194.
+ * fp32 NCHW planes.  rgbac_ssim_level: one scale of _ssim (:36-83) with the VALID 1-D gaussian
+ *   win[win_size] (W pass then H pass, :21-33), C1 = (K1*range)^2, C2 = (K2*range)^2;
+ *   partials: caller scratch of batch*channels*ceil((h-ws+1)/16)*ceil((w-ws+1)/16)*2 floats;
+ *   ssim_out[b], cs_out[b] = CHW means of ssim_map / cs_map.  win_size odd, <= 15.
+ * rgbac_avgpool2: F.avg_pool2d(kernel 2, padding (h%2, w%2)) of planes x (h, w) (:183-185).
+ * rgbac_msssim_combine: per_image[b] = prod_{l<L-1} mcs[l][b]^w[l] * ssim_last[b]^w[L-1]
+ *   (the broadcast of :189-190), mean = batch mean (:192-193); either output may be NULL. */
+int rgbac_ssim_level(int batch, int channels, int h, int w, int win_size, const float* x,
+                     const float* y, const float* win, float c1, float c2, float* partials,
+                     float* ssim_out, float* cs_out, void* stream);
+int rgbac_avgpool2(int planes, int h, int w, const float* x, float* y, void* stream);
+int rgbac_msssim_combine(int levels, int batch, const float* mcs, const float* ssim_last,
+                         const float* weights, float* per_image, float* mean, void* stream);
+
 /* Host-side range-ANS coder (csrc/rans.cpp), byte-compatible with compressai.ans:
  * replaces BufferedRansEncoder.encode_with_indexes/flush (:334,:367-368), RansDecoder
  * set_stream/decode_stream (:387-388,:401) and the EntropyModel compress/decompress coders.

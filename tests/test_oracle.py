@@ -172,3 +172,19 @@ def test_models_run_small():
     with torch.no_grad():
         o2 = ref.mask_forward(m.state_dict(), a)
     assert o2[0].shape == a.shape and torch.isfinite(o2[0]).all()
+
+
+def test_ms_ssim_oracle_known_answers():
+    """ssim(X, X) = ms_ssim(X, X) = 1; constant images a, b: cs = C2/C2 = 1 and
+    ssim = (2ab + C1) / (a^2 + b^2 + C1) (ms_ssim_torch.py:70-71)."""
+    from oracle import ref_metrics as rm
+    g = torch.Generator().manual_seed(5)
+    X = torch.rand((2, 3, 176, 176), generator=g)
+    assert abs(rm.ms_ssim(X, X, data_range=1.0).item() - 1.0) < 1e-5
+    assert abs(rm.ssim(X, X, data_range=1.0).item() - 1.0) < 1e-5
+    a, b = 0.25, 0.75
+    A, Bc = torch.full((1, 1, 32, 32), a), torch.full((1, 1, 32, 32), b)
+    c1 = 0.01 ** 2
+    want = (2 * a * b + c1) / (a * a + b * b + c1)
+    s, cs = rm.ssim_level(A, Bc, rm.fspecial_gauss_1d(11, 1.5).repeat(1, 1, 1, 1), 1.0)
+    assert abs(s.item() - want) < 1e-5 and abs(cs.item() - 1.0) < 1e-5
