@@ -187,4 +187,5 @@ def test_ms_ssim_oracle_known_answers():
     c1 = 0.01 ** 2
     want = (2 * a * b + c1) / (a * a + b * b + c1)
     s, cs = rm.ssim_level(A, Bc, rm.fspecial_gauss_1d(11, 1.5).repeat(1, 1, 1, 1), 1.0)
-    assert abs(s.item() - want) < 1e-5 and abs(cs.item() - 1.0) < 1e-5
+    # fp32 E[X^2] - mu^2 cancels to ~1e-7 against C2 = 9e-4: 1e-3 covers that noise
+    assert abs(s.item() - want) < 1e-3 and abs(cs.item() - 1.0) < 1e-3
