@@ -425,6 +425,15 @@ def main_rgba(args, dev):
     el = time.perf_counter() - t0
     if args.no_graph:
         out = step()
+    # eval metric of the same loop (trainRGB.py:311), outside the timed codec region as there
+    from rgbac.metrics.ms_ssim_torch import ms_ssim
+    msv = ms_ssim(x, out[0], data_range=1.0).item()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(10):
+        ms_ssim(x, out[0], data_range=1.0)
+    torch.cuda.synchronize()
+    ms_ms = (time.perf_counter() - t0) / 10 * 1e3
     npx = B * S * S
     rec = {"metric": "MPixels/sec RGBA encode+decode (alpha codec -> constraint -> RGB codec)",
            "value": round(npx * args.steps / el / 1e6, 3), "unit": "MPix/s", "n_gpus": 1,
@@ -435,6 +444,7 @@ def main_rgba(args, dev):
            "config": {"workload": f"RGBA eval pipeline trainRGB.py:282-306, {S}x{S}",
                       "batch": B, "hip_graph": not args.no_graph},
            "bpp": round(out[3].item(), 5), "psnr": round(out[4].item(), 4),
+           "ms_ssim": round(msv, 6), "ms_ssim_ms_per_batch": round(ms_ms, 3),
            "cpu_baseline": None}
     if not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline_rgba(args.cpu_seconds)

@@ -45,13 +45,15 @@ def recon_alpha(x_hat_mask):
 
 
 @torch.no_grad()
-def rgba_forward(masknet, net, masked_input, mask):
+def rgba_forward(masknet, net, masked_input, mask, msssim=False):
     """One evaluation pass of trainRGB.py:282-306 for an RGBA batch on the GPU.
 
     masked_input: (B,3,H,W) RGB (where(alpha>0, rgb, alpha), MYdataset.py:113), mask: (B,1,H,W)
     true alpha.  Returns (clipped_recon_image, clipped_recon_mask, mse_loss, bpp, psnr, out_mask)
     where bpp already includes the alpha codec's bpp unless the mask is all ones (:300-303),
-    psnr = 10*log10(1/mse) (:306), and out_mask is the alpha codec's own 5-tuple."""
+    psnr = 10*log10(1/mse) (:306), and out_mask is the alpha codec's own 5-tuple.  With
+    msssim=True a 7th element is ms_ssim(masked_input, clipped image, data_range=1) (:311),
+    computed by the HIP metric kernels."""
     rt.check_gpu(masked_input, mask)
     mask = mask.contiguous().float()
     levels = mask_pyramid(mask, 6)[1]                        # EncMakeMask(mask)  (:283)
@@ -66,4 +68,8 @@ def rgba_forward(masknet, net, masked_input, mask):
     _lib.call("rgbac_rgba_finish", x_hat.numel(), x_hat.data_ptr(), img.data_ptr(),
               bpp_f.data_ptr(), bppm_f.data_ptr(), flag.data_ptr(), mse_f.data_ptr(),
               bpp_total.data_ptr(), psnr.data_ptr(), _lib.stream_ptr(x_hat.device))
+    if msssim:
+        from .metrics.ms_ssim_torch import ms_ssim
+        return (img, recon_mask, mse, bpp_total, psnr, out_mask,
+                ms_ssim(masked_input, img, data_range=1.0, size_average=True))
     return img, recon_mask, mse, bpp_total, psnr, out_mask

@@ -501,7 +501,7 @@ def recon_alpha(x_hat_mask):
     return constraint_rgb(t)
 
 
-def rgba_forward(sd_mask, sd_rgb, masked_input, mask):
+def rgba_forward(sd_mask, sd_rgb, masked_input, mask, msssim=False):
     """trainRGB.py:282-306 (eval loop body, >=500k-step regime) ->
     (clipped image, recon mask, mse, bpp incl. alpha bpp unless mask is all ones, psnr)."""
     me = supply_mask(mask)                                       # EncMakeMask  :283
@@ -512,4 +512,7 @@ def rgba_forward(sd_mask, sd_rgb, masked_input, mask):
     if not torch.all(mask == 1.0):                               # :300-303
         bpp = bpp + om[2]
     psnr = 10 * (torch.log(1. / mse) / torch.log(torch.tensor(10.)))   # :306
+    if msssim:                                                   # :311
+        from oracle import ref_metrics
+        return img, rm, mse, bpp, psnr, ref_metrics.ms_ssim(masked_input, img, data_range=1.0)
     return img, rm, mse, bpp, psnr

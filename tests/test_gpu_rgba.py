@@ -90,16 +90,17 @@ def test_rgba_forward_fp32(device):
     sdr = {k: v.detach().cpu() for k, v in rgb.state_dict().items()}
     sdm = {k: v.detach().cpu() for k, v in msk.state_dict().items()}
     g = torch.Generator().manual_seed(0)
-    B, H, W = 2, 64, 64
+    B, H, W = 2, 192, 192
     x = torch.round(torch.rand((B, 3, H, W), generator=g) * 255) / 255
     a = torch.ones((B, 1, H, W))
     a[0, :, :, : W // 2] = 0
-    a[1, :, 20:40, 10:50] = 0
+    a[1, :, 60:120, 30:150] = 0
     xm = torch.where(a > 0, x, a)
     with torch.no_grad():
-        want = ref.rgba_forward(sdm, sdr, xm, a)
-    img, rm, mse, bpp, psnr, om = rgba_forward(msk.to(device), rgb.to(device),
-                                                xm.to(device), a.to(device))
+        want = ref.rgba_forward(sdm, sdr, xm, a, msssim=True)
+    img, rm, mse, bpp, psnr, om, ms = rgba_forward(msk.to(device), rgb.to(device),
+                                                    xm.to(device), a.to(device), msssim=True)
+    assert abs(ms.item() - want[5].item()) < 1e-4
     # the recon mask is integer-valued work: identical unless the alpha net's fp32 output
     # sits within rounding noise of a .5/255 boundary
     diff = (rm.cpu() != want[1]).float().mean().item()
