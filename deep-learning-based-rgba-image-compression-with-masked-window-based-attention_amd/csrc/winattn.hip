@@ -15,6 +15,7 @@
 // Heads are processed one after another; q,k,v of a head are staged in LDS as
 // fp32 and the two small products (64 x ws^2 x d) run on the VALU in fp32.
 #include "common.h"
+#include <cstdlib>
 
 namespace rgbac {
 
@@ -171,7 +172,7 @@ __global__ void __launch_bounds__(256)
 winattn_mfma_kernel(int batch, int H, int W, int C, int heads, int shift, int masked,
                     float scale, const T* __restrict__ qkv, long long ldq,
                     const float* __restrict__ alpha, const float* __restrict__ bias,
-                    T* __restrict__ out, long long ldo, uint8_t* __restrict__ sel) {
+                    T* __restrict__ out, long long ldo, uint8_t* __restrict__ sel, int hpb) {
   constexpr int N = WS * WS;
   constexpr int NWIN = 64 / N;
   constexpr int EPV = Elem<T>::EPV;
@@ -196,6 +197,14 @@ winattn_mfma_kernel(int batch, int H, int W, int C, int heads, int shift, int ma
   const int fr = lane & 15, fq = lane >> 4;
   const int nwx = W / WS, nwy = H / WS;
   const int total = batch * nwx * nwy;
+  // Block -> (window group, head group), XCD-aware: blocks are dealt round-robin over the 8
+  // XCDs (block i -> XCD i % 8), so all head groups of one window group get block ids with
+  // the same residue and share that XCD's L2 for the window's qkv rows.
+  const int hgroups = heads / hpb;
+  const int xcd = blockIdx.x & 7, seq = blockIdx.x >> 3;
+  const int hg = seq % hgroups;
+  const int wgrp = (seq / hgroups) * 8 + xcd;
+  const int h0 = hg * hpb, h1 = h0 + hpb;
 
   // zero the LDS images (pad columns/rows and off-window P entries stay zero)
   for (int e = tid; e < 64 * QRS; e += 256) Qs[e] = Ks[e] = make_uint4(0, 0, 0, 0);
@@ -205,7 +214,7 @@ winattn_mfma_kernel(int batch, int H, int W, int C, int heads, int shift, int ma
   __syncthreads();
   if (tid < 64) {
     const int wi = tid / N, lt = tid % N;
-    const int gw = blockIdx.x * NWIN + wi;
+    const int gw = wgrp * NWIN + wi;
     int pix = -1, rid = 0;
     if (gw < total) {
       const int b = gw / (nwx * nwy);
@@ -223,13 +232,14 @@ winattn_mfma_kernel(int batch, int H, int W, int C, int heads, int shift, int ma
     rid_s[tid] = rid;
   }
   __syncthreads();
-  if (tid < 64 && pix_s[tid] >= 0 && sel) sel[pix_s[tid]] = (uint8_t)act_s[tid / N];
+  if (tid < 64 && pix_s[tid] >= 0 && sel && hg == 0) sel[pix_s[tid]] = (uint8_t)act_s[tid / N];
   bool any = false;
 #pragma unroll
   for (int w = 0; w < NWIN; ++w) any |= act_s[w] != 0;
   if (!any) {
-    for (int e = tid; e < 64 * C; e += 256) {
-      const int t = e / C, ch = e - t * C;
+    const int CH = hpb * DH;                     // this block's head slice only
+    for (int e = tid; e < 64 * CH; e += 256) {
+      const int t = e / CH, ch = h0 * DH + (e - t * CH);
       if (pix_s[t] >= 0) Elem<T>::st(out + (long long)pix_s[t] * ldo + ch, 0.0f);
     }
     return;
@@ -241,7 +251,7 @@ winattn_mfma_kernel(int batch, int H, int W, int C, int heads, int shift, int ma
   const int qpix = pix_s[qi];
   const int qrid = rid_s[qi];
 
-  for (int h = 0; h < heads; ++h) {
+  for (int h = h0; h < h1; ++h) {
     // ---- stage q*scale, k (rows) and v^T (transposed) with VEC-byte loads
     for (int e = tid; e < 3 * 64 * NP; e += 256) {
       const int which = e / (64 * NP);
@@ -386,15 +396,26 @@ extern "C" int rgbac_winattn_core(int dtype, int batch, int h, int w, int channe
   const long long windows = (long long)batch * (h / ws) * (w / ws);
   const int nwin = 64 / (ws * ws);
   const int blocks = (int)((windows + nwin - 1) / nwin);
+  // MFMA path: one block per (window group, head group); head groups of RGBAC_WINATTN_HPB
+  // heads (default 1: 8x the blocks of one-block-per-window, which left 2 blocks per CU
+  // walking 8 heads serially).  Window groups padded to a multiple of 8 (XCD-aware order).
+  static const int hpb_env = [] {
+    const char* e = getenv("RGBAC_WINATTN_HPB");
+    return e ? atoi(e) : 1;
+  }();
+  const int hpb = (hpb_env >= 1 && heads % hpb_env == 0) ? hpb_env : heads;
+  const long long mblocks_ll = (long long)((blocks + 7) / 8) * 8 * (heads / hpb);
+  RGBAC_REQUIRE(mblocks_ll < (1LL << 31), "too many windows for one launch");
+  const int mblocks = (int)mblocks_ll;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
 #define RGBAC_WA(T, WS)                                                                    \
   hipLaunchKernelGGL((winattn_core_kernel<T, WS>), dim3(blocks), dim3(256), 0, st, batch, h, \
                      w, channels, heads, shift, masked, scale, (const T*)qkv, ldq, alpha,    \
                      bias, (T*)out, ldo, sel)
 #define RGBAC_WM(T, WS, DH)                                                                \
-  hipLaunchKernelGGL((winattn_mfma_kernel<T, WS, DH>), dim3(blocks), dim3(256), 0, st, batch, h, \
-                     w, channels, heads, shift, masked, scale, (const T*)qkv, ldq, alpha,      \
-                     bias, (T*)out, ldo, sel)
+  hipLaunchKernelGGL((winattn_mfma_kernel<T, WS, DH>), dim3(mblocks), dim3(256), 0, st, batch, \
+                     h, w, channels, heads, shift, masked, scale, (const T*)qkv, ldq, alpha,   \
+                     bias, (T*)out, ldo, sel, hpb)
   const int dh = channels / heads;
   const bool mfma_shape = (ws == 8 && dh == 24) || (ws == 4 && dh == 10);
   if (mfma_shape && dtype == RGBAC_F32) {
