@@ -252,6 +252,16 @@ winattn_mfma_kernel(int batch, int H, int W, int C, int heads, int shift, int ma
   const int qrid = rid_s[qi];
 
   for (int h = h0; h < h1; ++h) {
+    // ---- relative-position bias of this lane's (query, key) pairs: issued before the staging
+    // loop so the scattered L2 reads overlap the q/k/v gathers and the barrier
+    const float* bh = bias + (size_t)h * N * N;
+    float bias_r[KT][4];
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      const int ktile = (WS == 8) ? kt : wave;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bias_r[kt][r] = bh[qloc * N + (ktile * 16 + fq * 4 + r) % N];
+    }
     // ---- stage q*scale, k (rows) and v^T (transposed) with VEC-byte loads
     for (int e = tid; e < 3 * 64 * NP; e += 256) {
       const int which = e / (64 * NP);
@@ -308,7 +318,6 @@ winattn_mfma_kernel(int batch, int H, int W, int C, int heads, int shift, int ma
       }
     }
     // ---- + relative position bias + shift mask, softmax over the window's keys
-    const float* bh = bias + (size_t)h * N * N;
     float mx = -INFINITY;
 #pragma unroll
     for (int kt = 0; kt < KT; ++kt) {
@@ -316,8 +325,7 @@ winattn_mfma_kernel(int batch, int H, int W, int C, int heads, int shift, int ma
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int kj = ktile * 16 + fq * 4 + r;
-        const int kloc = kj % N;
-        float v = s[kt][r] + bh[qloc * N + kloc];
+        float v = s[kt][r] + bias_r[kt][r];
         if (shift > 0 && rid_s[kj] != qrid) v += -100.0f;
         s[kt][r] = v;
         mx = fmaxf(mx, v);
