@@ -206,10 +206,17 @@ winattn_mfma_kernel(int batch, int H, int W, int C, int heads, int shift, int ma
   const int wgrp = (seq / hgroups) * 8 + xcd;
   const int h0 = hg * hpb, h1 = h0 + hpb;
 
-  // zero the LDS images (pad columns/rows and off-window P entries stay zero)
-  for (int e = tid; e < 64 * QRS; e += 256) Qs[e] = Ks[e] = make_uint4(0, 0, 0, 0);
-  for (int e = tid; e < CT * 16 * PRS; e += 256) Vt[e] = make_uint4(0, 0, 0, 0);
-  for (int e = tid; e < 64 * PRS; e += 256) Ps[e] = make_uint4(0, 0, 0, 0);
+  // zero only what the staging never writes but the MFMAs read: the q/k chunks past the head
+  // dim (K padding to the MFMA k-step), the V^T rows past it, and for ws 4 the off-window
+  // P entries (ws 8 writes every P column of every row each head)
+  constexpr int QC0 = DH / EPV, QC1 = DP / EPV;   // chunks [QC0, QC1) hold padding
+  for (int e = tid; e < 64 * (QC1 - QC0); e += 256) {
+    const int t = e / (QC1 - QC0), c = QC0 + e % (QC1 - QC0);
+    Qs[t * QRS + c] = Ks[t * QRS + c] = make_uint4(0, 0, 0, 0);
+  }
+  for (int e = tid; e < (CT * 16 - DH) * PRS; e += 256) Vt[DH * PRS + e] = make_uint4(0, 0, 0, 0);
+  if constexpr (WS == 4)
+    for (int e = tid; e < 64 * PRS; e += 256) Ps[e] = make_uint4(0, 0, 0, 0);
   if (tid < NWIN) act_s[tid] = masked ? 0 : 1;
   __syncthreads();
   if (tid < 64) {
