@@ -59,28 +59,118 @@ SPIN_FWD = 150_000_000
 SPIN_TRAIN = 600_000_000
 
 
-def cpu_baseline(budget_s):
-    """Oracle (CPU fp32 restatement) on 1 image of the same workload, this host's cores."""
-    from oracle import ref_model as ref
+LATENT_GAIN = 20.0     # tests/golden/make_golden.py: Encoder.x4 scaled so symbols are non-zero
+
+
+def rgb_net(latent_gain=LATENT_GAIN):
+    """Seed-234 random-init AutoEncoderRGB_Journal with Encoder.x4 (1x1 192 -> 80, the conv
+    feeding the latent) scaled by ``latent_gain``: at plain random init every latent symbol
+    round(y - mu) is 0 and bpp parity would be vacuous; with 20 they span about -5..10 like a
+    trained codec's.  Same architecture and FLOPs."""
     from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
     torch.manual_seed(234)
-    sd = {k: v.detach().cpu() for k, v in AutoEncoder().eval().state_dict().items()}
-    x, a = synth_inputs(2, 256, 256, seed=0)
-    x, a = x[1:2], a[1:2]          # the half-transparent pattern
-    me = ref.supply_mask(a)
+    net = AutoEncoder().eval()
     with torch.no_grad():
-        ref.rgb_forward(sd, x, a, a, *me[:4])          # warm-up
+        net.Encoder.x4.weight.mul_(latent_gain)
+        net.Encoder.x4.bias.mul_(latent_gain)
+    return net
+
+
+def host_cores():
+    """CPU cores this process may run on (len(os.sched_getaffinity(0)))."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def _set_cpu_threads():
+    """torch threads for the CPU baseline = len(sched_getaffinity(0)), capped by
+    OMP_NUM_THREADS when the job's CPU share sets it (the GPU box: 16) -- more threads than
+    the share oversubscribes it.  Returns the thread count actually used."""
+    n = host_cores()
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    torch.set_num_threads(n)
+    return n
+
+
+def parity_sample(S=256, n=4):
+    """The parity / CPU-baseline sample: the first ``n`` images of the bench batch (one per
+    alpha pattern: ones, left-half zero, ramped ellipse, all zero), seed 0."""
+    x, a = synth_inputs(n, S, S, seed=0)
+    return x, a
+
+
+def cpu_baseline(budget_s, S=256):
+    """Oracle (CPU fp32 restatement of the reference) on the 4-image parity sample (one image
+    per forward, B=1, as trainRGB.py's Kodak loop runs), this host's cores, cycling over the
+    sample until ``budget_s``.  Returns (baseline record, oracle outputs of the first pass:
+    [(bpp, mse, MS-SSIM of the clamped x_hat)] per image) -- the outputs are the parity reference of the
+    bench line (the oracle is used here only as the checker / timed CPU baseline)."""
+    from oracle import ref_metrics
+    from oracle import ref_model as ref
+    cores = _set_cpu_threads()
+    sd = {k: v.detach().cpu() for k, v in rgb_net().state_dict().items()}
+    x, a = parity_sample(S)
+    outs = []
+    with torch.no_grad():
+        mes = [ref.supply_mask(a[i:i + 1]) for i in range(x.shape[0])]
+        for i in range(x.shape[0]):                    # first pass = warm-up + parity outputs
+            o = ref.rgb_forward(sd, x[i:i + 1], a[i:i + 1], a[i:i + 1], *mes[i][:4])
+            msv = ref_metrics.ms_ssim(x[i:i + 1], o[0].clamp(0, 1), data_range=1.0).item()
+            outs.append((o[2].item(), o[1].item(), msv))
         n, t0 = 0, time.perf_counter()
         while True:
-            ref.rgb_forward(sd, x, a, a, *me[:4])
+            i = n % x.shape[0]
+            ref.rgb_forward(sd, x[i:i + 1], a[i:i + 1], a[i:i + 1], *mes[i][:4])
             n += 1
-            if time.perf_counter() - t0 >= budget_s or n >= 1000:
+            if (time.perf_counter() - t0 >= budget_s and n >= x.shape[0]) or n >= 4000:
                 break
         dt = time.perf_counter() - t0
-    return {"value": round(n * 256 * 256 / dt / 1e6, 4), "unit": "MPix/s",
-            "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"oracle rgb_forward fp32, 1 image 256x256 (half-transparent alpha), "
-                      f"{n} timed iterations after 1 warm-up, {dt:.1f} s"}
+    rec = {"value": round(n * S * S / dt / 1e6, 4), "unit": "MPix/s", "cores": cores,
+           "kind": "port",
+           "sample": f"oracle rgb_forward fp32 on the 4-image parity sample ({S}x{S}, B=1 per "
+                     f"forward, alpha ones/half/ellipse/zero), {n} timed forwards after 1 "
+                     f"warm-up pass, {dt:.1f} s, torch threads {cores} (sched_getaffinity {host_cores()})"}
+    return rec, outs
+
+
+def gpu_parity(net, dev, outs_ref, S=256):
+    """bpp / PSNR / MS-SSIM of the HIP forward (net's current compute dtype) on the parity
+    sample, one image per forward, against the oracle's outputs ``outs_ref``
+    (trainRGB.py:289-311: PSNR from the model's masked MSE, MS-SSIM of the clamped x_hat)."""
+    import math
+    from rgbac.layers.SupplyMask import mask_pyramid
+    from rgbac.metrics.ms_ssim_torch import ms_ssim
+    x, a = parity_sample(S)
+    d_bpp = d_psnr = d_ms = 0.0
+    rel_bpp = 0.0
+    per = []
+    from rgbac import runtime as rt
+    for i in range(x.shape[0]):
+        xi, ai = x[i:i + 1].to(dev), a[i:i + 1].to(dev)
+        _, me = mask_pyramid(ai, 4)
+        with torch.no_grad(), rt.fixed_tiles():        # shape-rule tiles: no autotune pass
+            o = net(xi, ai, ai, *me)
+        bpp, mse = o[2].item(), o[1].item()
+        rb, rm, rms = outs_ref[i]
+        psnr = 10 * math.log10(1.0 / mse) if mse > 0 else None
+        rpsnr = 10 * math.log10(1.0 / rm) if rm > 0 else None
+        msv = ms_ssim(xi, o[0].clamp(0, 1), data_range=1.0).item()
+        d_bpp = max(d_bpp, abs(bpp - rb))
+        rel_bpp = max(rel_bpp, abs(bpp - rb) / max(abs(rb), 1e-12))
+        if psnr is not None and rpsnr is not None:
+            d_psnr = max(d_psnr, abs(psnr - rpsnr))
+        d_ms = max(d_ms, abs(msv - rms))
+        per.append({"bpp": round(bpp, 6), "bpp_ref": round(rb, 6),
+                    "psnr": None if psnr is None else round(psnr, 4),
+                    "psnr_ref": None if rpsnr is None else round(rpsnr, 4),
+                    "ms_ssim": round(msv, 6), "ms_ssim_ref": round(rms, 6)})
+    return {"max_abs_d_bpp": float(f"{d_bpp:.3g}"), "max_rel_d_bpp": float(f"{rel_bpp:.3g}"),
+            "max_abs_d_psnr_db": float(f"{d_psnr:.3g}"), "max_abs_d_ms_ssim": float(f"{d_ms:.3g}"),
+            "per_image": per}
 
 
 def cpu_baseline_train(budget_s):
@@ -88,6 +178,7 @@ def cpu_baseline_train(budget_s):
     4096*mse + bpp) on 1 image of the same workload, this host's cores."""
     from oracle import ref_model as ref
     from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    cores = _set_cpu_threads()
     torch.manual_seed(234)
     sd = {k: v.detach().cpu().clone().requires_grad_(v.is_floating_point())
           for k, v in AutoEncoder().train().state_dict().items()}
@@ -110,9 +201,16 @@ def cpu_baseline_train(budget_s):
             break
     dt = time.perf_counter() - t0
     return {"value": round(n * 256 * 256 / dt / 1e6, 4), "unit": "MPix/s",
-            "cores": torch.get_num_threads(), "kind": "port",
+            "cores": cores, "kind": "port",
             "sample": f"oracle rgb_forward(training) + autograd backward fp32, 1 image 256x256 "
                       f"(half-transparent alpha), {n} timed iterations after 1 warm-up, {dt:.1f} s"}
+
+
+def latest_profile(suffix):
+    """profiles/rNN_<suffix> of the latest round that has one (or None)."""
+    import glob
+    hits = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_{suffix}")))
+    return hits[-1] if hits else None
 
 
 def pmc_traffic(kernel, path, config=None):
@@ -248,8 +346,9 @@ def main_train(args, world, rank, dev, dist):
         summ = prof.summary()
         if args.layers:
             write_layers(prof, args.layers, 2)
-        traffic_file = args.traffic_file if args.traffic_file is not None else \
-            os.path.join(ROOT, "profiles", "r01_pmc_traffic_train.json")
+        traffic_file = args.traffic_file
+        if traffic_file is None:
+            traffic_file = latest_profile("pmc_traffic_train.json")
         roof, total_ms = roofline_of(summ, args.dtype, 2, traffic_file)
         rec = {"metric": TRAIN_METRIC, "value": round(value, 2), "unit": "MPix/s",
                "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -283,6 +382,7 @@ def cpu_baseline_codec(budget_s):
     """Oracle compress (CPU fp32 symbols + the pure-Python rANS restatement) on 1 image."""
     from oracle import ans_ref as oa
     from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    cores = _set_cpu_threads()
     torch.manual_seed(234)
     net = AutoEncoder().eval()
     net.update()
@@ -304,7 +404,7 @@ def cpu_baseline_codec(budget_s):
             break
     dt = time.perf_counter() - t0
     return {"value": round(n * 256 * 256 / dt / 1e6, 4), "unit": "MPix/s",
-            "cores": torch.get_num_threads(), "kind": "port",
+            "cores": cores, "kind": "port",
             "sample": f"oracle compress (fp32 symbols + pure-Python rANS of y), 1 image "
                       f"256x256 (half-transparent alpha), {n} iterations, {dt:.1f} s"}
 
@@ -364,6 +464,7 @@ def cpu_baseline_rgba(budget_s):
     from oracle import ref_model as ref
     from rgbac.models.AutoEncoderMask_Journal import AutoEncoder as MaskNet
     from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder as RGBNet
+    cores = _set_cpu_threads()
     torch.manual_seed(234)
     sdr = {k: v.detach() for k, v in RGBNet().state_dict().items()}
     sdm = {k: v.detach() for k, v in MaskNet().state_dict().items()}
@@ -378,7 +479,7 @@ def cpu_baseline_rgba(budget_s):
             break
     dt = time.perf_counter() - t0
     return {"value": round(n * 256 * 256 / dt / 1e6, 4), "unit": "MPix/s",
-            "cores": torch.get_num_threads(), "kind": "port",
+            "cores": cores, "kind": "port",
             "sample": f"oracle rgba_forward fp32 (alpha codec + constraint + RGB codec), 1 image "
                       f"256x256 (half-transparent alpha), {n} iterations, {dt:.1f} s"}
 
@@ -461,6 +562,8 @@ def main():
     ap.add_argument("--dtype", choices=["bf16", "f32"], default="bf16")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity-mode", action="store_true",
+                    help="skip the fp32 parity-mode timing of the same config")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--kernels", action="store_true", help="add the per-kernel time table")
     ap.add_argument("--layers", default=None, help="write a per-layer time table to this file")
@@ -480,7 +583,14 @@ def main():
     if args.train and args.batch == 8 and "--batch" not in sys.argv:
         args.batch = 16
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `bench.py --gpus N` without a launcher: start N rank processes of this script
+        # ourselves (one per GPU, the torchrun environment contract), before this process
+        # touches the GPU; this parent only waits and returns the worst exit code.
+        return spawn_ranks(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world and "--gpus" in sys.argv:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -497,14 +607,76 @@ def main():
         return main_codec(args, dev)
     if args.rgba:
         return main_rgba(args, dev)
+    return main_forward(args, world, rank, dev, dist)
 
+
+def spawn_ranks(n):
+    """Launch ``n`` copies of this command line as ranks 0..n-1 (RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT), wait for all, return the max exit code."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, p.wait())
+    if rc:
+        raise SystemExit(rc)
+    return 0
+
+
+def capture(step, no_graph):
+    """Warm ``step`` on a side stream and capture it in a HIP graph -> (run, graph, out)."""
+    if no_graph:
+        return step, None, None
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = step()
+    return graph.replay, graph, out
+
+
+def time_steps(run, steps, dist, dev):
+    """Barrier + synchronize, ``steps`` timed steps, synchronize + barrier; the MAX over ranks."""
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = t.item()
+    return elapsed
+
+
+def main_forward(args, world, rank, dev, dist):
+    """BASELINE config 2 (B=8, 256^2, bf16) / config 4 (--size 1024 --batch 4): forward
+    encode+decode, replicas on N GPUs."""
     from rgbac import runtime as rt
     from rgbac.layers.SupplyMask import mask_pyramid
     from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
 
     dt = torch.bfloat16 if args.dtype == "bf16" else torch.float32
-    torch.manual_seed(234)
-    net = AutoEncoder().eval().to(dev).set_compute_dtype(dt)
+    net = rgb_net().to(dev).set_compute_dtype(dt)
     B, S = args.batch, args.size
     x, a = synth_inputs(B, S, S, seed=rank)
     x, a = x.to(dev), a.to(dev)
@@ -515,43 +687,38 @@ def main():
             return net(x, a, a, *me)
 
     tuned = tune_cache_setup(args, os.path.join(ROOT, "profiles", f"tune_fwd_{args.dtype}_b{B}_{S}.json"))
-    out = step()                                       # packs weights, warms caches (and tunes)
+    step()                                             # packs weights, warms caches (and tunes)
     torch.cuda.synchronize()
-    if args.save_tune and rank == 0:
-        rt.save_tune_cache(args.save_tune)
-    graph = None
-    if not args.no_graph:
-        s = torch.cuda.Stream()
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(2):
-                step()
-        torch.cuda.current_stream().wait_stream(s)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            out = step()
-        run = graph.replay
-    else:
-        run = step
+    run, graph, _ = capture(step, args.no_graph)
     for _ in range(args.warmup):
         run()
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        run()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
+    elapsed = time_steps(run, args.steps, dist, dev)
     ms = elapsed / args.steps * 1e3
     value = world * B * S * S * args.steps / elapsed / 1e6
+
+    # fp32 parity mode (the reference's own precision) on the same config, timed the same way
+    parity_mode = None
+    if dt != torch.float32 and not args.no_parity_mode:
+        if tune_cache_setup(args, os.path.join(ROOT, "profiles", f"tune_fwd_f32_b{B}_{S}.json")):
+            pass
+        net.set_compute_dtype(torch.float32)
+        step()
+        torch.cuda.synchronize()
+        run32, graph32, _ = capture(step, args.no_graph)
+        for _ in range(2):
+            run32()
+        psteps = max(3, args.steps // 4)
+        el32 = time_steps(run32, psteps, dist, dev)
+        del graph32, run32
+        parity_mode = {"dtype": "f32", "value": round(world * B * S * S * psteps / el32 / 1e6, 2),
+                       "unit": "MPix/s", "steps": psteps,
+                       "ms_per_step": round(el32 / psteps * 1e3, 3),
+                       "note": "same config at the reference's precision: fp32 storage, "
+                               "exact-fp32 MFMA (v_mfma_f32_16x16x4_f32), fp32 epilogues"}
+        net.set_compute_dtype(dt)
+    if args.save_tune and rank == 0:
+        rt.save_tune_cache(args.save_tune)
 
     if rank == 0:
         # ---- roofline attribution: eager steps, each queued behind a GPU spin so the host has
@@ -569,8 +736,9 @@ def main():
         summ = prof.summary()
         if args.layers:
             write_layers(prof, args.layers, nrep)
-        traffic_file = args.traffic_file if args.traffic_file is not None else \
-            os.path.join(ROOT, "profiles", "r01_pmc_traffic_fwd.json")
+        traffic_file = args.traffic_file
+        if traffic_file is None:
+            traffic_file = latest_profile("pmc_traffic_fwd.json")
         roof, total_ms = roofline_of(summ, args.dtype, nrep, traffic_file,
                                      {"batch": B, "size": S, "dtype": args.dtype})
         roof["timing"] = "eager steps behind a GPU spin, fence-free HIP events per launch"
@@ -581,22 +749,35 @@ def main():
                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                "dtype": args.dtype, "data": "synthetic (seeded RGB k/255 + 4 alpha patterns; "
-                                             "random-init weights, torch seed 234)",
+                                             "random-init weights, torch seed 234, Encoder.x4 "
+                                             "x20 so latent symbols are non-zero)",
                "config": {"workload": "AutoEncoderRGB_Journal forward encode+decode "
-                                      f"(BASELINE config 2), {S}x{S} RGBA",
+                                      f"(BASELINE config {2 if S == 256 else 4}), {S}x{S} RGBA",
                           "global_batch": B * world, "per_gpu_batch": B, "height": S, "width": S,
                           "parallelism": f"replicas{world}", "hip_graph": graph is not None,
                           "tile_cache": tuned and os.path.relpath(tuned, ROOT)},
                "roofline": roof,
-               "achieved_model_tflops": round(fwd_flops / (ms * 1e-3) / 1e12, 2)}
+               "achieved_model_tflops": round(fwd_flops / (ms * 1e-3) / 1e12, 2),
+               "parity_mode": parity_mode}
         if args.kernels:
             rec["kernels"] = {k: {"launches": v["launches"] // nrep, "ms": round(v["ms"] / nrep, 4),
                                   "share": round(v["ms"] / total_ms, 4),
                                   "tflops": round(v["flops"] / max(v["ms"], 1e-9) / 1e9, 2)}
                               for k, v in sorted(summ.items(), key=lambda kv: -kv[1]["ms"])}
         rec["cpu_baseline"] = None
+        rec["parity"] = None
         if world == 1 and not args.no_cpu_baseline:
-            rec["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+            rec["cpu_baseline"], outs_ref = cpu_baseline(args.cpu_seconds, S=min(S, 256))
+            # bpp / PSNR / MS-SSIM of the HIP forward vs the oracle on the same sample
+            # (outside the timed region), in the bench dtype and in the fp32 parity mode
+            par = {"sample": "4 images 256x256 of the bench batch (alpha ones / half / "
+                             "ellipse / zero), one forward each, vs the CPU oracle (fp32)"}
+            par[args.dtype] = gpu_parity(net, dev, outs_ref, S=min(S, 256))
+            if dt != torch.float32:
+                net.set_compute_dtype(torch.float32)
+                par["f32"] = gpu_parity(net, dev, outs_ref, S=min(S, 256))
+                net.set_compute_dtype(dt)
+            rec["parity"] = par
         print(json.dumps(rec), flush=True)
     if dist:
         dist.barrier()

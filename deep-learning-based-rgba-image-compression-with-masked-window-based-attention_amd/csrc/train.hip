@@ -466,7 +466,8 @@ __global__ void __launch_bounds__(256)
 winattn_bwd_kernel(int batch, int H, int W, int C, int heads, int shift, int masked, float scale,
                    const T* __restrict__ qkv, long long ldq, const float* __restrict__ alpha,
                    const float* __restrict__ bias, const T* __restrict__ dout, long long ldo,
-                   T* __restrict__ dqkv, long long lddq, float* __restrict__ bpart) {
+                   T* __restrict__ dqkv, long long lddq, float* __restrict__ bpart,
+                   const float* __restrict__ amask, int amask_nw) {
   constexpr int N = WS * WS;
   constexpr int NWIN = 64 / N;
   constexpr int DP = 25;
@@ -550,6 +551,7 @@ winattn_bwd_kernel(int batch, int H, int W, int C, int heads, int shift, int mas
                        (cj < W - WS ? 0 : (cj < W - shift ? 1 : 2));
         if (gi != gj) s += -100.0f;
       }
+      if (amask) s += amask[((size_t)((grp * NWIN + i / N) % amask_nw) * N + li) * N + j];
       P[i * (N + 1) + j] = s;
       G[i * (N + 1) + j] = dp;
     }
@@ -1148,11 +1150,12 @@ extern "C" int rgbac_wgrad_reduce(int64_t nslot, const int32_t* fmap, const floa
   return check_launch("wgrad_reduce_kernel");
 }
 
-extern "C" int rgbac_winattn_core_bwd(int dtype, int batch, int h, int w, int channels, int heads,
-                                      int ws, int shift, int masked, float scale, const void* qkv,
-                                      int64_t ldq, const float* alpha, const float* bias,
-                                      const void* dout, int64_t ldo, void* dqkv, int64_t lddq,
-                                      int nblk, float* bias_partial, void* stream) {
+extern "C" int rgbac_winattn_core_bwd_ex(int dtype, int batch, int h, int w, int channels,
+                                         int heads, int ws, int shift, int masked, float scale,
+                                         const void* qkv, int64_t ldq, const float* alpha,
+                                         const float* bias, const void* dout, int64_t ldo,
+                                         void* dqkv, int64_t lddq, int nblk, float* bias_partial,
+                                         const float* amask, int amask_nw, void* stream) {
   RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
   RGBAC_REQUIRE(ws == 4 || ws == 8, "window size must be 4 or 8");
   RGBAC_REQUIRE(batch > 0 && h > 0 && w > 0 && h % ws == 0 && w % ws == 0, "shape");
@@ -1161,16 +1164,27 @@ extern "C" int rgbac_winattn_core_bwd(int dtype, int batch, int h, int w, int ch
   RGBAC_REQUIRE(qkv && dout && dqkv && bias && bias_partial, "null pointer");
   RGBAC_REQUIRE(!masked || alpha, "masked attention needs alpha");
   RGBAC_REQUIRE(nblk >= 1 && nblk <= 65535, "nblk");
+  RGBAC_REQUIRE(!amask || amask_nw > 0, "an explicit mask needs nW > 0");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   dim3 grid(nblk, heads);
 #define K_(T, WS_)                                                                              \
   hipLaunchKernelGGL((winattn_bwd_kernel<T, WS_>), grid, dim3(256), 0, st, batch, h, w, channels, \
                      heads, shift, masked, scale, (const T*)qkv, ldq, alpha, bias,                \
-                     (const T*)dout, ldo, (T*)dqkv, lddq, bias_partial)
+                     (const T*)dout, ldo, (T*)dqkv, lddq, bias_partial, amask, amask_nw)
   if (ws == 8) { RGBAC_DT_DISPATCH(dtype, K_, 8); }
   else { RGBAC_DT_DISPATCH(dtype, K_, 4); }
 #undef K_
   return check_launch("winattn_bwd_kernel");
+}
+
+extern "C" int rgbac_winattn_core_bwd(int dtype, int batch, int h, int w, int channels, int heads,
+                                      int ws, int shift, int masked, float scale, const void* qkv,
+                                      int64_t ldq, const float* alpha, const float* bias,
+                                      const void* dout, int64_t ldo, void* dqkv, int64_t lddq,
+                                      int nblk, float* bias_partial, void* stream) {
+  return rgbac_winattn_core_bwd_ex(dtype, batch, h, w, channels, heads, ws, shift, masked, scale,
+                                   qkv, ldq, alpha, bias, dout, ldo, dqkv, lddq, nblk, bias_partial,
+                                   nullptr, 0, stream);
 }
 
 extern "C" int rgbac_relpos_bwd(int nblk, int heads, int ws, const float* bias_partial,

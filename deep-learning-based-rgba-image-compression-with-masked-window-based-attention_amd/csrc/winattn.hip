@@ -24,7 +24,8 @@ __global__ void __launch_bounds__(256)
 winattn_core_kernel(int batch, int H, int W, int C, int heads, int shift, int masked,
                     float scale, const T* __restrict__ qkv, long long ldq,
                     const float* __restrict__ alpha, const float* __restrict__ bias,
-                    T* __restrict__ out, long long ldo, uint8_t* __restrict__ sel) {
+                    T* __restrict__ out, long long ldo, uint8_t* __restrict__ sel,
+                    const float* __restrict__ amask, int amask_nw) {
   constexpr int N = WS * WS;
   constexpr int NWIN = 64 / N;
   constexpr int DMAX = 24;
@@ -117,6 +118,11 @@ winattn_core_kernel(int batch, int H, int W, int C, int heads, int shift, int ma
                        (cj < W - WS ? 0 : (cj < W - shift ? 1 : 2));
         if (gi != gj) s += -100.0f;
       }
+      if (amask) {
+        // WindowAttention.forward(x, mask): window gw adds mask[gw % nW] (:114-122)
+        const int gw = blockIdx.x * NWIN + i / N;
+        s += amask[((size_t)(gw % amask_nw) * N + li) * N + j];
+      }
       S[i * (N + 1) + j] = s;
     }
     __syncthreads();
@@ -172,7 +178,8 @@ __global__ void __launch_bounds__(256)
 winattn_mfma_kernel(int batch, int H, int W, int C, int heads, int shift, int masked,
                     float scale, const T* __restrict__ qkv, long long ldq,
                     const float* __restrict__ alpha, const float* __restrict__ bias,
-                    T* __restrict__ out, long long ldo, uint8_t* __restrict__ sel, int hpb) {
+                    T* __restrict__ out, long long ldo, uint8_t* __restrict__ sel, int hpb,
+                    const float* __restrict__ amask, int amask_nw) {
   constexpr int N = WS * WS;
   constexpr int NWIN = 64 / N;
   constexpr int EPV = Elem<T>::EPV;
@@ -257,6 +264,10 @@ winattn_mfma_kernel(int batch, int H, int W, int C, int heads, int shift, int ma
   const bool qact = act_s[qwin] != 0;
   const int qpix = pix_s[qi];
   const int qrid = rid_s[qi];
+  // explicit additive mask of WindowAttention.forward(x, mask): this query's row of
+  // mask[gw % nW] (masked_win_attention.py:114-122)
+  const float* qmask = amask ? amask + ((size_t)((wgrp * NWIN + qwin) % amask_nw) * N + qloc) * N
+                             : nullptr;
 
   for (int h = h0; h < h1; ++h) {
     // ---- relative-position bias of this lane's (query, key) pairs: issued before the staging
@@ -334,6 +345,7 @@ winattn_mfma_kernel(int batch, int H, int W, int C, int heads, int shift, int ma
         const int kj = ktile * 16 + fq * 4 + r;
         float v = s[kt][r] + bias_r[kt][r];
         if (shift > 0 && rid_s[kj] != qrid) v += -100.0f;
+        if (qmask) v += qmask[kj % N];
         s[kt][r] = v;
         mx = fmaxf(mx, v);
       }
@@ -394,10 +406,11 @@ winattn_mfma_kernel(int batch, int H, int W, int C, int heads, int shift, int ma
 
 using namespace rgbac;
 
-extern "C" int rgbac_winattn_core(int dtype, int batch, int h, int w, int channels, int heads,
-                                  int ws, int shift, int masked, float scale, const void* qkv,
-                                  int64_t ldq, const float* alpha, const float* bias, void* out,
-                                  int64_t ldo, uint8_t* sel, void* stream) {
+extern "C" int rgbac_winattn_core_ex(int dtype, int batch, int h, int w, int channels,
+                                     int heads, int ws, int shift, int masked, float scale,
+                                     const void* qkv, int64_t ldq, const float* alpha,
+                                     const float* bias, void* out, int64_t ldo, uint8_t* sel,
+                                     const float* amask, int amask_nw, int hpb, void* stream) {
   RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
   RGBAC_REQUIRE(ws == 4 || ws == 8, "window size must be 4 or 8");
   RGBAC_REQUIRE(batch > 0 && h > 0 && w > 0 && h % ws == 0 && w % ws == 0,
@@ -408,17 +421,15 @@ extern "C" int rgbac_winattn_core(int dtype, int batch, int h, int w, int channe
   RGBAC_REQUIRE(qkv && out && bias, "null pointer");
   RGBAC_REQUIRE(!masked || (alpha && sel), "masked attention needs alpha and sel");
   RGBAC_REQUIRE(ldq >= 3 * channels && ldo >= channels, "strides");
+  RGBAC_REQUIRE(!amask || amask_nw > 0, "an explicit mask needs nW > 0");
   const long long windows = (long long)batch * (h / ws) * (w / ws);
   const int nwin = 64 / (ws * ws);
   const int blocks = (int)((windows + nwin - 1) / nwin);
-  // MFMA path: one block per (window group, head group); head groups of RGBAC_WINATTN_HPB
-  // heads (default 1: 8x the blocks of one-block-per-window, which left 2 blocks per CU
-  // walking 8 heads serially).  Window groups padded to a multiple of 8 (XCD-aware order).
-  static const int hpb_env = [] {
-    const char* e = getenv("RGBAC_WINATTN_HPB");
-    return e ? atoi(e) : 1;
-  }();
-  const int hpb = (hpb_env >= 1 && heads % hpb_env == 0) ? hpb_env : heads;
+  // MFMA path: one block per (window group, head group) of hpb heads (1: 8x the blocks of
+  // one-block-per-window, which left 2 blocks per CU walking 8 heads serially); an hpb that
+  // does not divide heads falls back to 1.  Window groups padded to a multiple of 8
+  // (XCD-aware order; padding groups have no valid window and write nothing).
+  if (hpb < 1 || heads % hpb) hpb = 1;
   const long long mblocks_ll = (long long)((blocks + 7) / 8) * 8 * (heads / hpb);
   RGBAC_REQUIRE(mblocks_ll < (1LL << 31), "too many windows for one launch");
   const int mblocks = (int)mblocks_ll;
@@ -426,11 +437,11 @@ extern "C" int rgbac_winattn_core(int dtype, int batch, int h, int w, int channe
 #define RGBAC_WA(T, WS)                                                                    \
   hipLaunchKernelGGL((winattn_core_kernel<T, WS>), dim3(blocks), dim3(256), 0, st, batch, h, \
                      w, channels, heads, shift, masked, scale, (const T*)qkv, ldq, alpha,    \
-                     bias, (T*)out, ldo, sel)
+                     bias, (T*)out, ldo, sel, amask, amask_nw)
 #define RGBAC_WM(T, WS, DH)                                                                \
   hipLaunchKernelGGL((winattn_mfma_kernel<T, WS, DH>), dim3(mblocks), dim3(256), 0, st, batch, \
                      h, w, channels, heads, shift, masked, scale, (const T*)qkv, ldq, alpha,   \
-                     bias, (T*)out, ldo, sel, hpb)
+                     bias, (T*)out, ldo, sel, hpb, amask, amask_nw)
   const int dh = channels / heads;
   const bool mfma_shape = (ws == 8 && dh == 24) || (ws == 4 && dh == 10);
   if (mfma_shape && dtype == RGBAC_F32) {
@@ -445,4 +456,12 @@ extern "C" int rgbac_winattn_core(int dtype, int batch, int h, int w, int channe
 #undef RGBAC_WA
 #undef RGBAC_WM
   return check_launch("winattn_core");
+}
+
+extern "C" int rgbac_winattn_core(int dtype, int batch, int h, int w, int channels, int heads,
+                                  int ws, int shift, int masked, float scale, const void* qkv,
+                                  int64_t ldq, const float* alpha, const float* bias, void* out,
+                                  int64_t ldo, uint8_t* sel, void* stream) {
+  return rgbac_winattn_core_ex(dtype, batch, h, w, channels, heads, ws, shift, masked, scale, qkv,
+                               ldq, alpha, bias, out, ldo, sel, nullptr, 0, 1, stream);
 }

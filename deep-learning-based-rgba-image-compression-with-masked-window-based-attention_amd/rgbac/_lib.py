@@ -101,6 +101,8 @@ SIGNATURES = {
     "rgbac_timer_destroy": [_VP],
     "rgbac_winattn_core": [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _F,
                            _VP, _I64, _VP, _VP, _VP, _I64, _VP, _VP],
+    "rgbac_winattn_core_ex": [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _F,
+                              _VP, _I64, _VP, _VP, _VP, _I64, _VP, _VP, _I32, _I32, _VP],
     "rgbac_gaussian_slice": [_I32, _I64, _I32, _VP, _I64, _VP, _I64, _VP, _I64, _VP,
                              _VP, _I64, _VP, _VP, _VP],
     "rgbac_eb_forward": [_I32, _I64, _I32, _VP, _I64, _VP, _VP, _VP, _I64, _VP, _VP, _VP],
@@ -120,6 +122,9 @@ SIGNATURES = {
     "rgbac_wgrad_reduce": [_I64, _VP, _VP, _I32, _I64, _VP, _I32, _VP, _I32, _VP, _I32, _VP],
     "rgbac_winattn_core_bwd": [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _F, _VP,
                                _I64, _VP, _VP, _VP, _I64, _VP, _I64, _I32, _VP, _VP],
+    "rgbac_winattn_core_bwd_ex": [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _F,
+                                  _VP, _I64, _VP, _VP, _VP, _I64, _VP, _I64, _I32, _VP, _VP,
+                                  _I32, _VP],
     "rgbac_relpos_bwd": [_I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP],
     "rgbac_gaussian_bwd": [_I32, _I64, _I32, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP, _VP,
                            _I64, _VP, _I64, _VP, _I64, _VP, _I64, _VP],

@@ -546,8 +546,11 @@ def _relpos_csr(index, ntab):
 
 
 class WinAttnFn(Function):
+    """Attention core; ``amask``: explicit additive (nW, N, N) fp32 mask or None
+    (WindowAttention.forward(x, mask))."""
+
     @staticmethod
-    def forward(ctx, spec, qkv_t, table, alpha):
+    def forward(ctx, spec, qkv_t, table, alpha, amask=None):
         C, heads, ws, shift, masked, scale, index = spec
         B, H, W, ldq = qkv_t.shape
         dt = qkv_t.dtype
@@ -559,11 +562,13 @@ class WinAttnFn(Function):
         o = new_feat(B, H, W, C, dt, dev)
         sel = torch.empty((B, H, W), dtype=torch.uint8, device=dev) if masked else None
         al = alpha.contiguous().float() if masked else None
-        _lib.call("rgbac_winattn_core", _lib.dtype_code(dt), B, H, W, C, heads, ws, shift,
+        am = None if amask is None else amask.detach().contiguous().float()
+        _lib.call("rgbac_winattn_core_ex", _lib.dtype_code(dt), B, H, W, C, heads, ws, shift,
                   1 if masked else 0, scale, qkv_t.data_ptr(), ldq, _lib.ptr(al),
-                  dense.data_ptr(), o.ptr(), o.ldc, _lib.ptr(sel), _lib.stream_ptr(dev))
+                  dense.data_ptr(), o.ptr(), o.ldc, _lib.ptr(sel), _lib.ptr(am),
+                  0 if am is None else am.shape[0], 1, _lib.stream_ptr(dev))
         ctx.spec = spec
-        ctx.save_for_backward(qkv_t, dense, al, table)
+        ctx.save_for_backward(qkv_t, dense, al, table, am)
         if sel is None:
             sel = torch.empty(0, dtype=torch.uint8, device=dev)
         ctx.mark_non_differentiable(sel)
@@ -572,7 +577,7 @@ class WinAttnFn(Function):
     @staticmethod
     def backward(ctx, do_t, _dsel):
         C, heads, ws, shift, masked, scale, index = ctx.spec
-        qkv_t, dense, al, table = ctx.saved_tensors
+        qkv_t, dense, al, table, am = ctx.saved_tensors
         B, H, W, ldq = qkv_t.shape
         dt = qkv_t.dtype
         dev = qkv_t.device
@@ -585,11 +590,12 @@ class WinAttnFn(Function):
         st = _lib.stream_ptr(dev)
         rt.timed(f"winattn_bwd_kernel<{'f32' if dt == _F32 else 'bf16'},{ws}>",
                  8.0 * B * H * W * N * C, qkv_t.element_size() * B * H * W * 8 * C,
-                 lambda: _lib.call("rgbac_winattn_core_bwd", _lib.dtype_code(dt), B, H, W, C,
-                                   heads, ws, shift, 1 if masked else 0, scale, qkv_t.data_ptr(),
-                                   ldq, _lib.ptr(al), dense.data_ptr(), do_t.data_ptr(),
-                                   do_t.shape[3], dqkv.data_ptr(), ldq, nblk, part.data_ptr(),
-                                   st))
+                 lambda: _lib.call("rgbac_winattn_core_bwd_ex", _lib.dtype_code(dt), B, H, W,
+                                   C, heads, ws, shift, 1 if masked else 0, scale,
+                                   qkv_t.data_ptr(), ldq, _lib.ptr(al), dense.data_ptr(),
+                                   do_t.data_ptr(), do_t.shape[3], dqkv.data_ptr(), ldq, nblk,
+                                   part.data_ptr(), _lib.ptr(am),
+                                   0 if am is None else am.shape[0], st))
         dtab = None
         if ctx.needs_input_grad[2]:
             off, ij = _relpos_csr(index, table.shape[0])
@@ -597,7 +603,7 @@ class WinAttnFn(Function):
             dtab = torch.empty(table.shape, dtype=_F32, device=dev)
             _lib.call("rgbac_relpos_bwd", nblk, heads, ws, part.data_ptr(), off.data_ptr(),
                       ij.data_ptr(), dense_g.data_ptr(), dtab.data_ptr(), st)
-        return None, dqkv, dtab, None
+        return None, dqkv, dtab, None, None
 
 
 # --------------------------------------------------------------------------
@@ -684,6 +690,32 @@ class ToNCHWFn(Function):
 
 def to_nchw_t(f):
     return ToNCHWFn.apply(f.t, f.C)
+
+
+class ToNHWCFn(Function):
+    """fp32 NCHW -> NHWC Feat tensor of ``dtype`` (rgbac_nchw_to_nhwc), with its inverse as
+    the backward."""
+
+    @staticmethod
+    def forward(ctx, x, dtype):
+        f = rt.to_nhwc(x, dtype)
+        ctx.meta = (x.shape, f.C)
+        return f.t
+
+    @staticmethod
+    def backward(ctx, g):
+        shp, C = ctx.meta
+        g = g.contiguous()
+        B, _, H, W = shp
+        out = torch.empty(shp, dtype=torch.float32, device=g.device)
+        _lib.call("rgbac_nhwc_to_nchw", _lib.dtype_code(g.dtype), B, C, H, W, g.data_ptr(),
+                  g.shape[3], out.data_ptr(), _lib.stream_ptr(g.device))
+        return out, None
+
+
+def to_nhwc_t(x, dtype=torch.float32):
+    """Autograd-tracked NCHW (B, C, H, W) -> Feat."""
+    return Feat(ToNHWCFn.apply(x.contiguous().float(), dtype), x.shape[1])
 
 
 # --------------------------------------------------------------------------

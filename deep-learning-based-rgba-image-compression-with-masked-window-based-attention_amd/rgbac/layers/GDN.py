@@ -78,6 +78,11 @@ class GDN(nn.Module):
         if inputs.dim() == 5:
             bs, ch, d, w, h = shape
             inputs = inputs.reshape(bs, ch, d * w, h)
+        from .masked_win_attention import needs_grad
+        if needs_grad(self, inputs):
+            # differentiable like GDN.py:64-94 (LowerBound rule on beta/gamma included)
+            from ..train_forward import gdn_t, layer_t
+            return layer_t(lambda f: gdn_t(self, f), inputs).reshape(shape)
         with torch.no_grad():
             y = rt.to_nchw(self.nhwc(rt.to_nhwc(inputs, torch.float32)))
         return y.reshape(shape)

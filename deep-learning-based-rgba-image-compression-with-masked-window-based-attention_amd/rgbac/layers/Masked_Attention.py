@@ -14,7 +14,7 @@ import torch.nn as nn
 from .. import _lib
 from .. import runtime as rt
 from ._blocks import conv1x1, conv3x3
-from .masked_win_attention import WinBasedAttention
+from .masked_win_attention import WinBasedAttention, needs_grad
 
 
 class ResidualUnit(nn.Module):
@@ -31,6 +31,9 @@ class ResidualUnit(nn.Module):
 
     def forward(self, x):
         rt.check_gpu(x)
+        if needs_grad(self, x):
+            from ..train_forward import layer_t, residual_unit_t
+            return layer_t(lambda f: residual_unit_t(self, f), x)
         with torch.no_grad():
             return rt.to_nchw(self.nhwc(rt.to_nhwc(x, torch.float32)))
 
@@ -116,5 +119,8 @@ class Win_noShift_Attention(nn.Module):
 
     def forward(self, x, mask):
         rt.check_gpu(x, mask)
+        if needs_grad(self, x):
+            from ..train_forward import attention_block_t, layer_t
+            return layer_t(lambda f: attention_block_t(self, f, mask), x)
         with torch.no_grad():
             return rt.to_nchw(self.nhwc(rt.to_nhwc(x, torch.float32), mask))

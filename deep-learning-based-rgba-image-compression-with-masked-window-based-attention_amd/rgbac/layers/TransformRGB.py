@@ -9,6 +9,7 @@ import torch.nn as nn
 from .. import runtime as rt
 from .GDN import GDN
 from .Masked_Attention import Win_noShift_Attention
+from .masked_win_attention import needs_grad
 from ._blocks import conv3x3, subpel_conv3x3  # noqa: F401  (re-exported like the reference)
 
 
@@ -20,6 +21,18 @@ def _act_of(m):
     if isinstance(m, nn.GELU):
         return "gelu", 0.0
     raise TypeError(f"unsupported activation {type(m)}")
+
+
+def _layer_forward(module, nhwc_fn, train_fn, x):
+    """forward() of a conv block: the fused no-grad NHWC path, or -- when grad is needed --
+    the autograd Function ``train_forward.<train_fn>`` (HIP backward)."""
+    rt.check_gpu(x)
+    if needs_grad(module, x):
+        from .. import train_forward as tf
+        fn = getattr(tf, train_fn)
+        return tf.layer_t(lambda f: fn(module, f), x)
+    with torch.no_grad():
+        return rt.to_nchw(nhwc_fn(rt.to_nhwc(x, torch.float32)))
 
 
 def run_conv(m, srcs, **kw):
@@ -72,6 +85,10 @@ class EnhancementBlock(nn.Module):
         t = run_conv(self.conv1, [x.src()], act=act, act_param=slope)
         return run_conv(self.conv2, [t.src()], res0=x, res2=post)
 
+    def forward(self, input):
+        """TransformRGB.py:16-28: conv2(relu(conv1(x))) + x."""
+        return _layer_forward(self, lambda f: self.nhwc(f), "enhancement_t", input)
+
 
 class DSE(nn.Module):
     def __init__(self, num_filters=32):
@@ -90,9 +107,7 @@ class DSE(nn.Module):
         return run_conv(self.output_conv, [t.src()], res0=x)
 
     def forward(self, input):
-        rt.check_gpu(input)
-        with torch.no_grad():
-            return rt.to_nchw(self.nhwc(rt.to_nhwc(input, torch.float32)))
+        return _layer_forward(self, lambda f: self.nhwc(f), "dse_t", input)
 
 
 class Analysis_transform(nn.Module):
@@ -138,6 +153,9 @@ class Analysis_transform(nn.Module):
 
     def forward(self, input, mask, me1, me2, me3, me4):
         rt.check_gpu(input, me2, me3)
+        if needs_grad(self, input):
+            from ..train_forward import analysis_t, layer_t
+            return layer_t(lambda f: analysis_t(self, f, me2, me3), input)
         with torch.no_grad():
             return rt.to_nchw(self.nhwc(rt.to_nhwc(input, torch.float32), me2, me3))
 
@@ -167,5 +185,8 @@ class Synthesis_transform(nn.Module):
 
     def forward(self, input, reconmask, md1, md2, md3, md4):
         rt.check_gpu(input, md2, md3)
+        if needs_grad(self, input):
+            from ..train_forward import layer_t, synthesis_t
+            return layer_t(lambda f: synthesis_t(self, f, md2, md3), input)
         with torch.no_grad():
             return rt.to_nchw(self.nhwc(rt.to_nhwc(input, torch.float32), md2, md3))

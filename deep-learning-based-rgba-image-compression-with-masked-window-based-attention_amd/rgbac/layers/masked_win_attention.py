@@ -8,11 +8,37 @@ HIP pipeline per WinBasedAttention call (no permuted copies, no host sync):
             x + proj(o) on pixels of active windows, x elsewhere
             (result[~window_mask] = 0 then shortcut + x, :235-249).
 """
+import os
+
 import torch
 import torch.nn as nn
 
 from .. import _lib
 from .. import runtime as rt
+
+# Heads per workgroup of the MFMA attention core (rgbac_winattn_core_ex's hpb; values that do
+# not divide num_heads fall back to 1).  Read per call: RGBAC_WINATTN_HPB or HPB[0].
+HPB = [None]
+
+
+def heads_per_block():
+    if HPB[0] is not None:
+        return int(HPB[0])
+    try:
+        return int(os.environ.get("RGBAC_WINATTN_HPB", "1"))
+    except ValueError:
+        return 1
+
+
+def needs_grad(module, *tensors):
+    """True when a forward must build an autograd graph: grad mode on and an input or a
+    parameter of ``module`` requires grad (the layer then runs the autograd Functions of
+    rgbac/autograd.py, whose backward is HIP; it never detaches silently)."""
+    if not torch.is_grad_enabled():
+        return False
+    if any(t is not None and t.requires_grad for t in tensors):
+        return True
+    return any(p.requires_grad for p in module.parameters())
 
 
 def _to_2tuple(x):
@@ -88,9 +114,10 @@ class WindowAttention(nn.Module):
             ent = self.__dict__["_rgbac_bias"]
         return ent[1]
 
-    def run_nhwc(self, x, alpha, shift, masked, residual=True):
+    def run_nhwc(self, x, alpha, shift, masked, residual=True, amask=None):
         """x: Feat (B,H,W,C), alpha: fp32 (B,1,H,W) or None -> Feat x + attn(x)
-        (or attn(x) alone when ``residual`` is False)."""
+        (or attn(x) alone when ``residual`` is False); ``amask``: explicit additive mask
+        fp32 (nW, N, N) for window w = mask[w % nW] (WindowAttention.forward's ``mask``)."""
         C, ws = self.dim, self.window_size[0]
         dt = x.t.dtype
         qkv = rt.conv(rt.packed(self.qkv, dt, [(C, x.ldc)]), [x.src()])
@@ -107,11 +134,13 @@ class WindowAttention(nn.Module):
         rt.timed(kname,
                   4.0 * npix * ws * ws * C, qkv.t.element_size() * npix * 4 * C,
                   lambda: _lib.call(
-                      "rgbac_winattn_core", _lib.dtype_code(dt), x.B, x.H, x.W, C, self.num_heads,
-                      ws, shift, 1 if masked else 0,
+                      "rgbac_winattn_core_ex", _lib.dtype_code(dt), x.B, x.H, x.W, C,
+                      self.num_heads, ws, shift, 1 if masked else 0,
                       float(torch.tensor(self.scale, dtype=torch.float32)), qkv.ptr(), qkv.ldc,
                       _lib.ptr(alpha) if masked else None, self.dense_bias().data_ptr(), o.ptr(),
-                      o.ldc, _lib.ptr(sel), _lib.stream_ptr(x.t.device)))
+                      o.ldc, _lib.ptr(sel), _lib.ptr(amask),
+                      0 if amask is None else amask.shape[0], heads_per_block(),
+                      _lib.stream_ptr(x.t.device)))
         pk = rt.packed(self.proj, dt, [(C, o.ldc)])
         if not residual:
             return rt.conv(pk, [o.src()])
@@ -120,19 +149,48 @@ class WindowAttention(nn.Module):
         return rt.conv(pk, [o.src()], res0=x)
 
     def forward(self, x, mask=None):
-        """x: (num_windows*B, N, C) windows; only mask=None is supported standalone
-        (shift masks are generated analytically inside WinBasedAttention)."""
-        rt.check_gpu(x)
-        if mask is not None:
-            raise NotImplementedError("rgbac fuses the shift mask into WinBasedAttention; "
-                                      "standalone WindowAttention supports mask=None only")
+        """:96-131.  x: (num_windows*B, N, C) windows, N = ws*ws; mask: additive
+        (num_windows, N, N) (0 / -100 or -inf) or None -- window b adds mask[b % nW].
+        Each window is handled as a one-window image (shift 0, no window drop), so the
+        per-window gather of the fused core is the identity here."""
+        rt.check_gpu(x, mask)
         Bw, N, C = x.shape
         ws = self.window_size[0]
-        img = x.reshape(Bw, ws, ws, C).permute(0, 3, 1, 2)
+        if N != ws * ws or C != self.dim:
+            raise RuntimeError(f"WindowAttention: expected (B_, {ws * ws}, {self.dim}), "
+                               f"got {tuple(x.shape)}")
+        amask = None
+        if mask is not None:
+            nw = mask.shape[0]
+            if nw == 0:
+                # :115-118: an empty mask prints "nW error!"; the reference's broadcast then
+                # yields no windows, which only has a consistent shape when B_ == 0
+                print("nW error!")
+                if Bw == 0:
+                    return x.new_zeros((0, N, C))
+                raise RuntimeError("WindowAttention: empty mask (nW = 0) with B_ > 0 windows")
+            if Bw % nw:
+                raise RuntimeError(f"WindowAttention: B_={Bw} is not a multiple of nW={nw}")
+            amask = mask.detach().contiguous().float().reshape(nw, N, N)
+        if Bw == 0:
+            return x.new_zeros((0, N, C))
+        if needs_grad(self, x):
+            from ..train_forward import window_attention_t
+            return window_attention_t(self, x, amask)
         with torch.no_grad():
-            f = rt.to_nhwc(img, torch.float32)
-            out = rt.to_nchw(self.run_nhwc(f, None, 0, False, residual=False))
-        return out.permute(0, 2, 3, 1).reshape(Bw, N, C)
+            f = rt.Feat(_window_feat(x, ws), C)
+            o = self.run_nhwc(f, None, 0, False, residual=False, amask=amask)
+            return o.t[..., :C].reshape(Bw, N, C).float()
+
+
+def _window_feat(x, ws):
+    """(B_, N, C) windows -> NHWC (B_, ws, ws, round_up(C, 8)) fp32 tensor (zero pad)."""
+    Bw, N, C = x.shape
+    t = x.float().reshape(Bw, ws, ws, C)
+    ldc = rt.round_up(C, 8)
+    if ldc != C:
+        t = torch.nn.functional.pad(t, (0, ldc - C))
+    return t.contiguous()
 
 
 class WinBasedAttention(nn.Module):
@@ -158,5 +216,8 @@ class WinBasedAttention(nn.Module):
 
     def forward(self, x, img_alpha):
         rt.check_gpu(x, img_alpha)
+        if needs_grad(self, x):
+            from ..train_forward import win_attention_t, layer_t
+            return layer_t(lambda f: win_attention_t(self, f, img_alpha), x)
         with torch.no_grad():
             return rt.to_nchw(self.nhwc(rt.to_nhwc(x, torch.float32), img_alpha))

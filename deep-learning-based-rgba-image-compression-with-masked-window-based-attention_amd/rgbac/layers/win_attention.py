@@ -5,7 +5,7 @@ attended and the shift mask is shared by all images (:161, :104)."""
 import torch
 
 from .. import runtime as rt
-from .masked_win_attention import (WindowAttention, window_partition,  # noqa: F401
+from .masked_win_attention import (WindowAttention, needs_grad, window_partition,  # noqa: F401
                                    window_reverse)
 from .masked_win_attention import WinBasedAttention as _MaskedWinBasedAttention
 
@@ -18,5 +18,8 @@ class WinBasedAttention(_MaskedWinBasedAttention):
 
     def forward(self, x):
         rt.check_gpu(x)
+        if needs_grad(self, x):
+            from ..train_forward import layer_t, win_attention_t
+            return layer_t(lambda f: win_attention_t(self, f, None), x)
         with torch.no_grad():
             return rt.to_nchw(self.nhwc(rt.to_nhwc(x, torch.float32)))

@@ -8,11 +8,12 @@ import torch.nn as nn
 from .. import runtime as rt
 from ..entropy import EntropyBottleneck, GaussianConditional
 from ..layers.GDN import GDN
-from ..layers.TransformRGB import _act_of, prep_conv, run_conv
+from ..layers.TransformRGB import _act_of, _layer_forward, prep_conv, run_conv
 from ..layers._blocks import conv, conv3x3, deconv, subpel_conv3x3  # noqa: F401
 from ._latent import latent_path
 from .AutoEncoderRGB_Journal import (_CompressionModelMixin, _hyper_analysis, _hyper_synthesis,
-                                     _stack3, finalize, get_scale_table, ste_round)  # noqa: F401
+                                     _stack3, check_geometry, finalize, get_scale_table,  # noqa: F401
+                                     ste_round)
 
 
 class EnhancementBlock(nn.Module):
@@ -26,6 +27,10 @@ class EnhancementBlock(nn.Module):
         act, slope = _act_of(self.relu)
         t = run_conv(self.conv1, [x.src()], act=act, act_param=slope)
         return run_conv(self.conv2, [t.src()], res0=x, res2=post)
+
+    def forward(self, input):
+        """:23-28"""
+        return _layer_forward(self, lambda f: self.nhwc(f), "enhancement_t", input)
 
 
 class DSE(nn.Module):
@@ -44,6 +49,10 @@ class DSE(nn.Module):
         t = self.enh3.nhwc(t, post=first)
         return run_conv(self.output_conv, [t.src()], res0=x)
 
+    def forward(self, input):
+        """:39-48"""
+        return _layer_forward(self, lambda f: self.nhwc(f), "dse_t", input)
+
 
 class ResBlock(nn.Module):
     def __init__(self, num_filters=128):
@@ -56,6 +65,10 @@ class ResBlock(nn.Module):
 
     def nhwc(self, x):
         return run_resblocks([(self, x)])[0]
+
+    def forward(self, x):
+        """:105-110"""
+        return _layer_forward(self, lambda f: self.nhwc(f), "resblock_t", x)
 
 
 def run_resblocks(pairs):
@@ -86,6 +99,10 @@ class SimplifiedAttention(nn.Module):
             tr, at = run_resblocks([(getattr(self, f"trunk_ResBlock{k}"), tr),
                                     (getattr(self, f"attention_ResBlock{k}"), at)])
         return run_conv(self.conv1, [at.src()], act="gate", res1=tr, res2=x)
+
+    def forward(self, x):
+        """:124-136"""
+        return _layer_forward(self, lambda f: self.nhwc(f), "simplified_attention_t", x)
 
 
 def _run_seq(seq, x):
@@ -150,8 +167,12 @@ class AutoEncoder(_CompressionModelMixin, nn.Module):
     def forward(self, mask, *, noise_z=None, noise_y=None, debug=None):
         rt.check_gpu(mask)
         B, _, H, W = mask.shape
-        if H % 64 or W % 64:
-            raise ValueError("H and W must be multiples of 64")
+        check_geometry(H, W)
+        if debug is None and torch.is_grad_enabled() and \
+                any(p.requires_grad for p in self.parameters()):
+            # training step (trainmask.py:165-198): autograd graph over the HIP kernels
+            from ..train_forward import mask_forward_train
+            return mask_forward_train(self, mask, noise_z, noise_y)
         dt = self.compute_dtype
         with torch.no_grad():
             m = mask.contiguous().float()

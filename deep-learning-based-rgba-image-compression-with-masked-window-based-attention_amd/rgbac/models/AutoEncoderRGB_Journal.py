@@ -48,6 +48,25 @@ def reconstruct_error(input, output, input_mask, output_mask=None):
     return torch.mean(se / cnt)
 
 
+class GeometryError(RuntimeError, ValueError):
+    """Input size the reference's forward cannot process either (RuntimeError like the
+    reference's own failure, ValueError for callers of round 1's API)."""
+
+
+def check_geometry(H, W):
+    """The whole-model forward needs H, W multiples of 64, exactly like the reference: the
+    hyper-synthesis output is 8*ceil(H/64) x 8*ceil(W/64) and the slice loop concatenates it
+    with the H/8 x W/8 latent slices (AutoEncoderRGB_Journal.py:242,248;
+    AutoEncoderMask_Journal.py:271,276), which raises in torch.cat unless H/8, W/8 are
+    multiples of 8 -- the mu/scale crop (:245,:251) never makes e.g. 96x96 work.  The L3
+    layers (Analysis/Synthesis_transform, window attention) accept multiples of 32."""
+    if H % 64 or W % 64 or H <= 0 or W <= 0:
+        raise GeometryError(
+            f"H and W must be positive multiples of 64 (got {H}x{W}): the reference's slice loop "
+            f"concatenates the {8 * -(-H // 64)}x{8 * -(-W // 64)} hyper-synthesis output with "
+            f"the {H // 8}x{W // 8} latent (AutoEncoderRGB_Journal.py:242)")
+
+
 class _CompressionModelMixin:
     """The parts of compressai.models.CompressionModel the reference relies on."""
 
@@ -152,9 +171,7 @@ class AutoEncoder(_CompressionModelMixin, nn.Module):
                 noise_y=None, debug=None):
         rt.check_gpu(input, mask, reconmask, me2, me3)
         B, _, H, W = input.shape
-        if H % 64 or W % 64:
-            raise ValueError("H and W must be multiples of 64 (windows at /4 and /8, "
-                             "hyperprior at /64)")
+        check_geometry(H, W)
         if debug is None and torch.is_grad_enabled() and \
                 any(p.requires_grad for p in self.parameters()):
             # training step (trainRGB.py:178-198): autograd graph over the HIP kernels

@@ -134,8 +134,8 @@ def compress(model, input, mask):
     """:312-371 -> {"strings": [[y_string], z_strings], "shape": z spatial size}."""
     _check(model, input, mask)
     B, _, H, W = input.shape
-    if H % 64 or W % 64:
-        raise ValueError("H and W must be multiples of 64")
+    from .AutoEncoderRGB_Journal import check_geometry
+    check_geometry(H, W)
     with torch.no_grad():
         xf = rt.to_nhwc(input.contiguous().float(), model.compute_dtype)
         _, me = mask_pyramid(mask, 4)                            # EncMakeMask(mask) (:314)

@@ -129,6 +129,7 @@ def latent_path(model, y, training=False, noise_z=None, noise_y=None, debug=None
     # 32-pixel wave tiles); unused slots stay zero
     ypart = torch.zeros((ns, -(-npix // 32)), dtype=torch.float64, device=dev)
     liks = [None] * ns
+    musig = [None] * ns
     waves = [[i] for i in range(min(msup, ns))]
     if ns > msup:
         waves.append(list(range(msup, ns)))
@@ -199,6 +200,16 @@ def latent_path(model, y, training=False, noise_z=None, noise_y=None, debug=None
             preps.append(rt.prepare(pk, [t2[j].src(), t2[k + j].src()], out=pre, act="gauss",
                                     res1=(y, i * cs), aux0=nyi, aux1=liks[i], partial=ypart[i]))
         rt.launch(preps)
+        gauss_choice = rt.LAST_CHOICE[0]
+        if debug is not None:
+            # the (mu | sigma) the GAUSS epilogue consumed, re-run without the epilogue (the
+            # checker's view of the integer symbols round(y - mu), :255-257)
+            for j, i in enumerate(wave):
+                pk = _musigma_pack(model.cc_mean_transforms[i][4],
+                                   model.cc_scale_transforms[i][4], dt, t2[j].ldc)
+                musig[i] = rt.launch([rt.prepare(pk, [t2[j].src(), t2[k + j].src()],
+                                                 out=rt.new_feat(B, h, w, 2 * cs, dt, dev))],
+                                     force=gauss_choice)[0]
         # lrp stacks: y_hat_i = pre_i + 0.5 * tanh(lrp([means, y_hat_<i, pre_i]))
         if pre_ok:
             if "lrp" not in waited:
@@ -221,5 +232,5 @@ def latent_path(model, y, training=False, noise_z=None, noise_y=None, debug=None
         main.wait_stream(side)                 # join the side stream (graph capture needs it)
     if debug is not None:
         debug.update(z=z, z_hat=z_hat, z_lik=zlik, y_lik=liks, latent_means=means,
-                     latent_scales=scales, y_hat=YH)
+                     latent_scales=scales, y_hat=YH, musigma=musig)
     return YH, ypart, zpart

@@ -15,56 +15,94 @@ import torch.distributed as dist
 
 
 class GradBuckets:
+    """Bucketed all-reduce of the flat gradient buffer, launched from post-accumulate-grad
+    hooks.  A bucket is a set of parameters whose flat ranges are all-reduced (one collective
+    per contiguous run) as soon as the last of them has accumulated its gradient.
+
+    Parameters that receive no gradient in a step (EntropyBottleneck.quantiles: only the aux
+    loss, which trainRGB.py never back-propagates, reaches it) would hold their bucket back
+    until ``finish()``, losing its overlap with backward.  After the first step the buckets
+    are re-cut: such parameters move to a tail bucket reduced in ``finish()`` (zeros unless
+    they do receive a gradient later, which stays correct since the tail always waits for
+    the end of backward)."""
+
     def __init__(self, params, flat_grad, bucket_bytes=25 << 20, group=None):
         self.params = list(params)
         self.flat = flat_grad
         self.group = group
         self.world = dist.get_world_size(group)
         # param i occupies [off_i, off_i + n_i) of the flat buffer (AdamClamp layout)
-        offs, off = [], 0
+        self.offs, off = [], 0
         for p in self.params:
-            offs.append((off, p.numel()))
+            self.offs.append((off, p.numel()))
             off += p.numel()
         assert off == flat_grad.numel()
-        per = max(1, bucket_bytes // flat_grad.element_size())
-        self.buckets = []                  # [lo, hi, [param idx]]
-        cur, hi = [], off
-        for i in range(len(self.params) - 1, -1, -1):
+        self.per = max(1, bucket_bytes // flat_grad.element_size())
+        self._cut(list(range(len(self.params) - 1, -1, -1)), [])
+        self.fired = [False] * len(self.params)
+        self.learned = False
+        self.active = False
+        self.hooks = [p.register_post_accumulate_grad_hook(self._hook(i))
+                      for i, p in enumerate(self.params)]
+
+    def _runs(self, idx):
+        """Contiguous flat ranges covering params ``idx``."""
+        rs = sorted(self.offs[i] for i in idx)
+        out = []
+        for lo, n in rs:
+            if out and out[-1][1] == lo:
+                out[-1][1] = lo + n
+            else:
+                out.append([lo, lo + n])
+        return [tuple(r) for r in out]
+
+    def _cut(self, order, tail):
+        """Buckets of ~per elements over ``order`` (backward order), plus a tail bucket."""
+        self.buckets = []                  # [ranges, [param idx]]
+        cur, size = [], 0
+        for i in order:
             cur.append(i)
-            lo = offs[i][0]
-            if hi - lo >= per or i == 0:
-                self.buckets.append([lo, hi, cur])
-                cur, hi = [], lo
+            size += self.offs[i][1]
+            if size >= self.per:
+                self.buckets.append([self._runs(cur), cur])
+                cur, size = [], 0
+        if cur:
+            self.buckets.append([self._runs(cur), cur])
+        self.tail = None
+        if tail:
+            self.tail = len(self.buckets)
+            self.buckets.append([self._runs(tail), list(tail)])
         self.owner = {}
-        for b, (_, _, idx) in enumerate(self.buckets):
+        for b, (_, idx) in enumerate(self.buckets):
             for i in idx:
                 self.owner[i] = b
         self.pending = [0] * len(self.buckets)
         self.works = [None] * len(self.buckets)
-        self.active = False
-        self.hooks = [p.register_post_accumulate_grad_hook(self._hook(i))
-                      for i, p in enumerate(self.params)]
 
     def _hook(self, i):
         def fn(_p):
             if not self.active:
                 return
+            self.fired[i] = True
             b = self.owner[i]
+            if b == self.tail:
+                return
             self.pending[b] -= 1
             if self.pending[b] == 0:
                 self._launch(b)
         return fn
 
     def _launch(self, b):
-        lo, hi, _ = self.buckets[b]
-        self.works[b] = dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM,
-                                        group=self.group, async_op=True)
+        self.works[b] = [dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM,
+                                         group=self.group, async_op=True)
+                         for lo, hi in self.buckets[b][0]]
 
     def begin(self):
         """Call before loss.backward()."""
-        for b, (_, _, idx) in enumerate(self.buckets):
+        for b, (_, idx) in enumerate(self.buckets):
             self.pending[b] = len(idx)
             self.works[b] = None
+        self.fired = [False] * len(self.params)
         self.active = True
 
     def finish(self):
@@ -74,8 +112,15 @@ class GradBuckets:
         for b in range(len(self.buckets)):
             if self.works[b] is None:
                 self._launch(b)
-        for w in self.works:
-            w.wait()
+        for ws in self.works:
+            for w in ws:
+                w.wait()
+        if not self.learned and any(self.fired):
+            self.learned = True
+            quiet = [i for i, f in enumerate(self.fired) if not f]
+            if quiet:
+                order = [i for i in range(len(self.params) - 1, -1, -1) if self.fired[i]]
+                self._cut(order, quiet)
         return 1.0 / self.world
 
     def remove(self):

@@ -539,8 +539,12 @@ def _tile_counters(dev, n):
     return buf
 
 
-def launch(preps):
-    """Launch prepared convs (same geometry) as ONE grouped kernel; returns their outputs."""
+LAST_CHOICE = [None]      # (tile, ksplit) of the most recent launch (debug re-runs)
+
+
+def launch(preps, force=None):
+    """Launch prepared convs (same geometry) as ONE grouped kernel; returns their outputs.
+    ``force``: (tile, ksplit) to use instead of the tuned / heuristic choice."""
     n = len(preps)
     p0 = preps[0]
     dev = p0.out.t.device
@@ -575,6 +579,8 @@ def launch(preps):
 
     fixed = _FIXED[0] > 0
     choice = None if fixed else (FORCE if (FORCE and not gauss) else _tune_cache.get(key))
+    if force is not None:
+        choice = tuple(force)
     if choice is None:
         mtot = p0.mgrid * p0.nphase * n
         cout = max(pr.pk.cout for pr in preps)
@@ -615,6 +621,7 @@ def launch(preps):
         choice = (min((t for t in GAUSS_TILES if _gauss_ok(t, p0.pk.cout)),
                       key=lambda t: TILES[t][1]), 1)
     set_choice(*choice)
+    LAST_CHOICE[0] = tuple(choice)
     if PROFILER is None:
         run()
     else:

@@ -49,11 +49,38 @@ def win_attention_t(blk, x, alpha):
     scale = float(torch.tensor(wa.scale, dtype=torch.float32))
     spec = (C, wa.num_heads, ws, blk.shift_size, masked, scale, wa.relative_position_index)
     o_t, sel = ag.WinAttnFn.apply(spec, qkv.t, wa.relative_position_bias_table,
-                                  alpha if masked else None)
+                                  alpha if masked else None, None)
     o = Feat(o_t, C)
     if masked:
         return conv_t(wa.proj, [o], act="masksel", res1=x, sel=sel)
     return conv_t(wa.proj, [o], res0=x)
+
+
+def window_attention_t(wa, x, amask=None):
+    """WindowAttention.forward(x, mask) (masked_win_attention.py:96-131) with autograd:
+    x (B_, N, C) windows, each run as a one-window image (shift 0), ``amask`` the additive
+    (nW, N, N) mask or None.  -> (B_, N, C) fp32."""
+    Bw, N, C = x.shape
+    ws = wa.window_size[0]
+    t = x.float().reshape(Bw, ws, ws, C)
+    ldc = rt.round_up(C, 8)
+    if ldc != C:
+        t = F.pad(t, (0, ldc - C))
+    f = Feat(t.contiguous(), C)
+    qkv = conv_t(wa.qkv, [f])
+    scale = float(torch.tensor(wa.scale, dtype=torch.float32))
+    spec = (C, wa.num_heads, ws, 0, False, scale, wa.relative_position_index)
+    o_t, _ = ag.WinAttnFn.apply(spec, qkv.t, wa.relative_position_bias_table, None, amask)
+    out = conv_t(wa.proj, [Feat(o_t, C)])
+    return out.t[..., :C].reshape(Bw, N, C)
+
+
+def layer_t(fn, x, dtype=torch.float32):
+    """Run an NHWC training-path function on an NCHW fp32 tensor with autograd:
+    NCHW -> NHWC (ToNHWCFn) -> fn(Feat) -> NCHW (ToNCHWFn).  The L3 layers' forward uses
+    this when grad is needed, so composing them under autograd back-propagates through the
+    HIP kernels (reference layers are ordinary differentiable modules)."""
+    return ag.to_nchw_t(fn(ag.to_nhwc_t(x, dtype)))
 
 
 def attention_block_t(blk, x, mask):
@@ -120,6 +147,42 @@ def _seq_t(seq, x):
     return t
 
 
+def resblock_t(b, x):
+    """AutoEncoderMask_Journal.py:96-110: conv1x1+ReLU, conv3x3+ReLU, conv1x1, + x."""
+    t = conv_t(b.conv1, [x], act="relu")
+    t = conv_t(b.conv2, [t], act="relu")
+    return conv_t(b.conv3, [t], res0=x)
+
+
+def simplified_attention_t(sa, x):
+    """AutoEncoderMask_Journal.py:112-136: x + sigmoid(conv1(att(x))) * trunk(x)."""
+    tr, at = x, x
+    for k in (1, 2, 3):
+        tr = resblock_t(getattr(sa, f"trunk_ResBlock{k}"), tr)
+        at = resblock_t(getattr(sa, f"attention_ResBlock{k}"), at)
+    return conv_t(sa.conv1, [at], act="gate", res1=tr, res2=x)
+
+
+def mask_seq_t(seq, x):
+    """EncoderMask / DecoderMask (AutoEncoderMask_Journal.py:153-176) with autograd."""
+    from .layers.GDN import GDN
+    from .models.AutoEncoderMask_Journal import DSE as MaskDSE
+    from .models.AutoEncoderMask_Journal import SimplifiedAttention
+    t = x
+    for m in seq:
+        if isinstance(m, GDN):
+            t = gdn_t(m, t)
+        elif isinstance(m, SimplifiedAttention):
+            t = simplified_attention_t(m, t)
+        elif isinstance(m, MaskDSE):
+            t = dse_t(m, t)
+        elif isinstance(m, (nn.Conv2d, nn.ConvTranspose2d)):
+            t = conv_t(m, [t])
+        else:
+            raise TypeError(type(m))
+    return t
+
+
 def eb_params_t(eb):
     """The [C][64] param block of rgbac_eb_forward with autograd to the raw parameters
     (softplus / tanh chained by torch on O(C) tensors)."""
@@ -182,5 +245,24 @@ def rgb_forward_train(model, input, mask, reconmask, me2, me3, noise_z=None, noi
     mse = ag.MSEFn.apply(xh.t, xh.C, x, mask.contiguous().float(), 0)          # :285
     npix = float(B * H * W)
     y_bpp = ybits / npix                                                       # :290-295
+    z_bpp = zbits / npix
+    return ag.to_nchw_t(xh), mse, y_bpp + z_bpp, y_bpp, z_bpp
+
+
+def mask_forward_train(model, mask, noise_z=None, noise_y=None):
+    """AutoEncoderMask_Journal.forward with autograd (trainmask.py:165-198: net(mask) ->
+    rd_loss.backward()) -> (x_hat, mse, bpp, y_bpp, z_bpp)."""
+    ag.prefetch_packs(model)
+    B, _, H, W = mask.shape
+    dt = model.compute_dtype
+    m = mask.contiguous().float()
+    with torch.no_grad():
+        mf = rt.to_nhwc(m, dt)
+    y = mask_seq_t(model.EncoderMask, mf)                                       # :250
+    yh, ybits, zbits = latent_t(model, y, model.training, noise_z, noise_y)    # :251-298
+    xh = mask_seq_t(model.DecoderMask, yh)                                      # :300
+    mse = ag.MSEFn.apply(xh.t, xh.C, m, None, 1)                               # :309
+    npix = float(B * H * W)
+    y_bpp = ybits / npix
     z_bpp = zbits / npix
     return ag.to_nchw_t(xh), mse, y_bpp + z_bpp, y_bpp, z_bpp

@@ -161,6 +161,16 @@ int rgbac_winattn_core(int dtype, int batch, int h, int w, int channels,
                        const void* qkv, int64_t ldq, const float* alpha,
                        const float* bias, void* out, int64_t ldo, uint8_t* sel,
                        void* stream);
+/* The same with (a) an explicit additive mask, fp32 [amask_nw][ws*ws][ws*ws], added to
+ * the scores of window w as amask[w % amask_nw] (WindowAttention.forward(x, mask),
+ * layers/masked_win_attention.py:114-122; NULL = none), and (b) the head-group size hpb
+ * of the MFMA path (heads per workgroup; values that do not divide heads fall back to 1).
+ * rgbac_winattn_core == rgbac_winattn_core_ex(..., NULL, 0, 1, stream). */
+int rgbac_winattn_core_ex(int dtype, int batch, int h, int w, int channels,
+                          int heads, int ws, int shift, int masked, float scale,
+                          const void* qkv, int64_t ldq, const float* alpha,
+                          const float* bias, void* out, int64_t ldo, uint8_t* sel,
+                          const float* amask, int amask_nw, int hpb, void* stream);
 
 /* compressai GaussianConditional.forward + ste_round for one channel slice
  * (models/AutoEncoderRGB_Journal.py:255-257, bits :280):
@@ -293,6 +303,13 @@ int rgbac_winattn_core_bwd(int dtype, int batch, int h, int w, int channels, int
                            const float* alpha, const float* bias, const void* dout, int64_t ldo,
                            void* dqkv, int64_t lddq, int nblk, float* bias_partial,
                            void* stream);
+/* ... with the explicit additive mask of rgbac_winattn_core_ex (NULL = none). */
+int rgbac_winattn_core_bwd_ex(int dtype, int batch, int h, int w, int channels, int heads,
+                              int ws, int shift, int masked, float scale, const void* qkv,
+                              int64_t ldq, const float* alpha, const float* bias,
+                              const void* dout, int64_t ldo, void* dqkv, int64_t lddq, int nblk,
+                              float* bias_partial, const float* amask, int amask_nw,
+                              void* stream);
 /* csr_off[(2ws-1)^2 + 1] / csr_ij[N*N]: for table row t, the flattened (i, j)
  * positions with relative_position_index[i][j] == t (fixed order).          */
 int rgbac_relpos_bwd(int nblk, int heads, int ws, const float* bias_partial,

@@ -301,6 +301,15 @@ def eb_medians(sd, p):
 def eb_forward(z, sd, p, training=False, noise=None):
     """compressai EntropyBottleneck.forward -> (outputs, likelihood), NCHW in/out.
 
+    Version choice (parity unpinned: the reference pins no compressai version): the
+    likelihood is compressai >= 1.2's ``sigmoid(upper) - sigmoid(lower)``.  Releases before
+    1.2 computed ``|sigmoid(-s*upper) - sigmoid(-s*lower)|`` with s = -sign(lower + upper)
+    (the same value up to rounding, evaluated in the numerically safer tail).  >= 1.2 is the
+    one the reference's code implies: it calls ``CompressionModel()`` without the
+    ``entropy_bottleneck_channels`` argument (AutoEncoderRGB_Journal.py:122,
+    AutoEncoderMask_Journal.py:149), which only the >= 1.2 constructor accepts, and builds
+    its own ``EntropyBottleneck(192)`` (:200).  csrc/entropy.hip follows the same form.
+
     ``noise`` (same shape as z, U(-1/2,1/2)) replaces the module's internal RNG
     draw in training mode so tests can feed both sides identical noise.
     """
@@ -382,8 +391,10 @@ def _stack3(x, sd, p):
     return _conv(t, sd, p + ".4")
 
 
-def _latent_path(y, sd, num_slices, max_support, training, noise_z, noise_y):
-    """AutoEncoderRGB_Journal.py:222-271 / AutoEncoderMask_Journal.py:251-298."""
+def _latent_path(y, sd, num_slices, max_support, training, noise_z, noise_y, dbg=None):
+    """AutoEncoderRGB_Journal.py:222-271 / AutoEncoderMask_Journal.py:251-298.
+    ``dbg`` (dict or None) receives the per-slice (mu, scale) lists -- the checker's view of
+    the integer symbols round(y_slice - mu) (:257)."""
     z = _h_a(y, sd)
     _, z_lik = eb_forward(z, sd, "entropy_bottleneck", training, noise_z)
     med = eb_medians(sd, "entropy_bottleneck")
@@ -402,6 +413,10 @@ def _latent_path(y, sd, num_slices, max_support, training, noise_z, noise_y):
         nz = None if noise_y is None else noise_y[:, i * ysl.shape[1]:(i + 1) * ysl.shape[1]]
         _, lik = gc_forward(ysl, sc, mu, training, nz)
         liks.append(lik)
+        if dbg is not None:
+            dbg.setdefault("mu", []).append(mu)
+            dbg.setdefault("scale", []).append(sc)
+            dbg.setdefault("y", []).append(ysl)
         yh = ste_round(ysl - mu) + mu
         lrp = _stack3(torch.cat([ms, yh], dim=1), sd, f"lrp_transforms.{i}")
         yh = yh + 0.5 * torch.tanh(lrp)
@@ -421,12 +436,12 @@ def reconstruct_error(inp, out, in_mask):
 
 
 def rgb_forward(sd, inp, mask, reconmask, me1, me2, me3, me4, training=False,
-                noise_z=None, noise_y=None, masked=True):
+                noise_z=None, noise_y=None, masked=True, dbg=None):
     """AutoEncoderRGB_Journal.py:203-296 -> (x_hat, mse, bpp, y_bpp, z_bpp)."""
     rm = torch.round(reconmask * 255) / 255                      # :212-214
     md = supply_mask(rm)                                         # :215
     y = analysis(inp, sd, "Encoder", me2, me3, masked)           # :217
-    y_hat, y_lik, z_lik = _latent_path(y, sd, 10, 5, training, noise_z, noise_y)
+    y_hat, y_lik, z_lik = _latent_path(y, sd, 10, 5, training, noise_z, noise_y, dbg)
     x_hat = synthesis(y_hat, sd, "Decoder", md[1], md[2], masked)  # :273
     yb, zb = _bits(y_lik), _bits(z_lik)
     mse = reconstruct_error(inp, x_hat, mask)                    # :289

@@ -77,6 +77,7 @@ def test_hip_matches_golden_mask(device):
     mg = _models()
     g = _load("mask_64x64_b2.npz")
     net = mg.mask_model().to(device)
-    out = net(torch.from_numpy(g["alpha"]).to(device))
+    with torch.no_grad():
+        out = net(torch.from_numpy(g["alpha"]).to(device))
     assert _rel(out[0].cpu().numpy(), g["x_hat"]) < 1e-3
     np.testing.assert_allclose([t.item() for t in out[1:]], g["scalars"], rtol=1e-4)

@@ -1,0 +1,267 @@
+"""GPU: the L3 layer surface as a drop-in -- every layer's ``forward`` is
+differentiable like the reference's nn.Modules (backward on the HIP kernels, checked
+against the oracle's autograd), ``WindowAttention.forward(x, mask)`` with an explicit
+additive mask, the head-group split of the attention core, the multiple-of-32 geometry
+the layers accept (and the multiple-of-64 the whole codec needs, exactly like the
+reference), and the alpha codec's training step (trainmask.py:165-198).
+
+Tolerances: fp32 layer outputs 2e-5 (max-abs relative), layer gradients 1e-4 norm-wise
+(exact-fp32 MFMA, different summation order); whole alpha-codec parameter gradients
+2e-2 norm-wise like the RGB codec's (tests/test_gpu_train.py)."""
+import pytest
+import torch
+
+from oracle import ref_model as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.detach().float().cpu(), b.detach().float().cpu()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-12)).item()
+
+
+def nrel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+def _gen(seed):
+    return torch.Generator().manual_seed(seed)
+
+
+def _ref_sd(module, prefix="m"):
+    return {f"{prefix}.{k}": v.detach().cpu().clone().requires_grad_(v.is_floating_point())
+            for k, v in module.state_dict().items()}
+
+
+def _check_layer(module, run_gpu, run_ref, x, extra=(), out_tol=2e-5, grad_tol=1e-4):
+    """Forward + backward of ``module`` (GPU, via its own forward) against the oracle on the
+    same state: output, input gradient and every parameter gradient."""
+    sd = _ref_sd(module)
+    xr = x.clone().requires_grad_(True)
+    want = run_ref(xr, sd)
+    g = torch.randn(want.shape, generator=_gen(5))
+    (want * g).sum().backward()
+    m = module.cuda()
+    m.zero_grad(set_to_none=True)
+    xg = x.cuda().requires_grad_(True)
+    got = run_gpu(m, xg)
+    assert got.shape == want.shape
+    assert got.requires_grad, "forward detached its output"
+    assert rel(got, want) < out_tol, rel(got, want)
+    (got * g.cuda()).sum().backward()
+    assert nrel(xg.grad, xr.grad) < grad_tol, ("input", nrel(xg.grad, xr.grad))
+    bad = []
+    for n, p in m.named_parameters():
+        r = sd[f"m.{n}"].grad
+        if r is None or r.abs().max() == 0:
+            assert p.grad is None or p.grad.abs().max() == 0, n
+            continue
+        e = nrel(p.grad, r)
+        if e > grad_tol:
+            bad.append((n, e))
+    assert not bad, bad
+
+
+def test_gdn_forward_backward(device):
+    from rgbac.layers.GDN import GDN
+    torch.manual_seed(1)
+    for inverse in (False, True):
+        g = GDN(24, inverse=inverse)
+        with torch.no_grad():
+            g.beta.uniform_(0.5, 1.5)
+            g.gamma.add_(0.05 * torch.rand(g.gamma.shape))
+            g.beta[0] = 1e-4                      # below its bound: LowerBound gradient rule
+        x = torch.randn((2, 24, 12, 20), generator=_gen(2))
+        _check_layer(g, lambda m, t: m(t), lambda t, sd: ref.gdn(t, sd, "m", inverse=inverse), x)
+
+
+def test_residual_unit_forward_backward(device):
+    from rgbac.layers.Masked_Attention import ResidualUnit
+    torch.manual_seed(2)
+    u = ResidualUnit(32)
+    x = torch.randn((2, 32, 16, 8), generator=_gen(3))
+    _check_layer(u, lambda m, t: m(t), lambda t, sd: ref.residual_unit(t, sd, "m"), x)
+
+
+@pytest.mark.parametrize("ws,C", [(8, 48), (4, 80)])
+def test_win_noshift_attention_forward_backward(device, ws, C):
+    from rgbac.layers.Masked_Attention import Win_noShift_Attention
+    torch.manual_seed(3)
+    blk = Win_noShift_Attention(C, num_heads=8, window_size=ws, shift_size=ws // 2)
+    B, H, W = 2, 4 * ws, 3 * ws
+    x = torch.randn((B, C, H, W), generator=_gen(4))
+    al = torch.ones((B, 1, H, W))
+    al[1, :, :, : W // 2] = 0
+    alg = al.cuda()
+    _check_layer(blk, lambda m, t: m(t, alg),
+                 lambda t, sd: ref.win_noshift_attention(t, al, sd, "m", ws, ws // 2), x)
+
+
+def test_unmasked_win_based_attention_forward_backward(device):
+    from rgbac.layers.win_attention import WinBasedAttention
+    torch.manual_seed(4)
+    wa = WinBasedAttention(dim=48, num_heads=8, window_size=8, shift_size=4)
+    x = torch.randn((2, 48, 16, 24), generator=_gen(6))
+    _check_layer(wa, lambda m, t: m(t),
+                 lambda t, sd: ref.win_based_attention(t, None, sd, "m", 8, 4, 8, masked=False), x)
+
+
+def test_window_attention_explicit_mask_forward_backward(device):
+    """WindowAttention.forward(x, mask) (masked_win_attention.py:96-131): window b adds
+    mask[b % nW] to its scores; also mask=None and the empty-mask case."""
+    from rgbac.layers.masked_win_attention import WindowAttention
+    torch.manual_seed(5)
+    for ws, C in ((8, 192), (4, 80)):
+        wa = WindowAttention(C, window_size=(ws, ws), num_heads=8)
+        N, nW = ws * ws, 3
+        x = torch.randn((2 * nW, N, C), generator=_gen(7))
+        mask = torch.zeros((nW, N, N))
+        g = _gen(8)
+        mask[torch.rand((nW, N, N), generator=g) < 0.3] = -100.0
+        for mk in (mask, None):
+            _check_layer(wa, lambda m, t: m(t, None if mk is None else mk.cuda()),
+                         lambda t, sd: ref.window_attention(t, sd, "m", ws, 8, mk), x)
+        with pytest.raises(RuntimeError, match="nW"):
+            wa.cuda()(x.cuda(), torch.zeros((0, N, N), device=device))
+
+
+def test_winattn_head_groups_identical(device):
+    """The MFMA core's head-group split (hpb heads per workgroup) does not change results,
+    including window counts that are not a multiple of the 8 * windows-per-group padding."""
+    from rgbac.layers import masked_win_attention as mwa
+    from rgbac import runtime as rt
+    torch.manual_seed(6)
+    for ws, C, H, W in ((8, 192, 24, 40), (4, 80, 12, 20)):
+        blk = mwa.WinBasedAttention(dim=C, num_heads=8, window_size=ws, shift_size=ws // 2).cuda()
+        x = torch.randn((1, C, H, W), generator=_gen(9)).cuda()
+        al = torch.ones((1, 1, H, W), device=device)
+        al[..., : W // 3] = 0
+        f = rt.to_nhwc(x, torch.float32)
+        outs = []
+        saved = mwa.HPB[0]
+        try:
+            for hpb in (1, 2, 8, 3):               # 3 does not divide 8 heads: falls back to 1
+                mwa.HPB[0] = hpb
+                with torch.no_grad():
+                    outs.append(blk.nhwc(f, al).t.clone())
+        finally:
+            mwa.HPB[0] = saved
+        for o in outs[1:]:
+            assert torch.equal(o, outs[0])
+
+
+def test_transforms_at_multiples_of_32(device):
+    """Analysis / Synthesis_transform accept H, W multiples of 32 (96x160 here: windows at
+    /4 and /8 tile), with gradients; the whole codec needs multiples of 64 like the
+    reference, whose slice loop fails to concatenate the hyper-synthesis output otherwise."""
+    from rgbac.layers.TransformRGB import Analysis_transform, Synthesis_transform
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder, GeometryError
+    torch.manual_seed(7)
+    E = Analysis_transform(192, 80)
+    H, W = 96, 160
+    x = torch.rand((1, 3, H, W), generator=_gen(10))
+    a = torch.ones((1, 1, H, W))
+    a[..., :, :40] = 0
+    me = ref.supply_mask(a)
+    meg = [m.cuda() for m in me]
+    _check_layer(E, lambda m, t: m(t, None, meg[0], meg[1], meg[2], meg[3]),
+                 lambda t, sd: ref.analysis(t, sd, "m", me[1], me[2]), x,
+                 out_tol=1e-4, grad_tol=1e-3)
+    D = Synthesis_transform(192, 80)
+    y = torch.randn((1, 80, H // 8, W // 8), generator=_gen(11))
+    _check_layer(D, lambda m, t: m(t, None, meg[0], meg[1], meg[2], meg[3]),
+                 lambda t, sd: ref.synthesis(t, sd, "m", me[1], me[2]), y,
+                 out_tol=1e-4, grad_tol=1e-3)
+    net = AutoEncoder().cuda().eval()
+    xg, ag_ = x.cuda(), a.cuda()
+    with pytest.raises(GeometryError, match="multiples of 64"):
+        with torch.no_grad():
+            net(xg, ag_, ag_, *meg[:4])
+    with pytest.raises(RuntimeError):                  # the same error type as the reference's
+        with torch.no_grad():
+            net(xg, ag_, ag_, *meg[:4])
+
+
+def test_dse_and_mask_blocks_forward_backward(device):
+    from rgbac.layers.TransformRGB import DSE
+    from rgbac.models.AutoEncoderMask_Journal import DSE as MaskDSE
+    from rgbac.models.AutoEncoderMask_Journal import ResBlock, SimplifiedAttention
+    torch.manual_seed(8)
+    x3 = torch.randn((1, 3, 32, 48), generator=_gen(12))
+    _check_layer(DSE(32), lambda m, t: m(t), lambda t, sd: ref.dse(t, sd, "m"), x3)
+    x1 = torch.randn((1, 1, 32, 48), generator=_gen(13))
+    _check_layer(MaskDSE(1, 32), lambda m, t: m(t), lambda t, sd: ref.dse(t, sd, "m", leaky=True),
+                 x1)
+    xr = torch.randn((2, 64, 8, 16), generator=_gen(14))
+    _check_layer(SimplifiedAttention(64), lambda m, t: m(t),
+                 lambda t, sd: ref.simplified_attention(t, sd, "m"), xr)
+
+    def resblock_ref(t, sd):
+        import torch.nn.functional as F
+        r = F.relu(F.conv2d(t, sd["m.conv1.weight"], sd["m.conv1.bias"]))
+        r = F.relu(F.conv2d(r, sd["m.conv2.weight"], sd["m.conv2.bias"], padding=1))
+        return F.conv2d(r, sd["m.conv3.weight"], sd["m.conv3.bias"]) + t
+    _check_layer(ResBlock(64), lambda m, t: m(t), resblock_ref, xr)
+
+
+def test_layers_no_grad_path_unchanged(device):
+    """Under torch.no_grad() the layers keep the fused inference path (no autograd graph)."""
+    from rgbac.layers.GDN import GDN
+    g = GDN(16).cuda()
+    x = torch.randn((1, 16, 8, 8), device=device, requires_grad=True)
+    with torch.no_grad():
+        y = g(x)
+    assert not y.requires_grad
+    y2 = g(x)
+    assert y2.requires_grad
+    assert rel(y2, y) < 1e-6
+
+
+def test_mask_train_step_grads(device):
+    """trainmask.py:165-176: rd_loss = lambda*mse + bpp backward through the alpha codec on
+    the HIP path; every parameter gradient vs the oracle's autograd (same noise), fp32."""
+    from rgbac.models.AutoEncoderMask_Journal import AutoEncoder
+    torch.manual_seed(234)
+    net = AutoEncoder().train()
+    g = _gen(62)
+    B, H, W = 2, 64, 64
+    a = torch.ones((B, 1, H, W))
+    a[1, :, :, : W // 2] = 0
+    a[0, :, 20:40, 10:30] = torch.round(torch.rand((20, 20), generator=g) * 255) / 255
+    nz = torch.rand((B, 192, 1, 1), generator=g) - 0.5
+    ny = torch.rand((B, 80, 8, 8), generator=g) - 0.5
+    sd = {k: v.detach().clone().requires_grad_(v.is_floating_point())
+          for k, v in net.state_dict().items()}
+    out = ref.mask_forward(sd, a, training=True, noise_z=nz, noise_y=ny)
+    (4096 * out[1] + out[2]).backward()
+    netg = AutoEncoder().cuda().train()
+    netg.load_state_dict(net.state_dict())
+    o = netg(a.cuda(), noise_z=nz.permute(0, 2, 3, 1).cuda(), noise_y=ny.permute(0, 2, 3, 1).cuda())
+    assert o[0].requires_grad and o[1].requires_grad
+    assert abs(o[1].item() - out[1].item()) < 1e-3 * out[1].item()
+    assert abs(o[2].item() - out[2].item()) < 1e-3 * out[2].item()
+    (4096 * o[1] + o[2]).backward()
+    bad, errs = [], []
+    for n, p in netg.named_parameters():
+        r = sd[n].grad
+        if r is None or r.abs().max() == 0:
+            continue
+        e = nrel(p.grad, r)
+        errs.append(e)
+        if e > 2e-2:
+            bad.append((n, e))
+    errs.sort()
+    print("mask codec grads: median rel", errs[len(errs) // 2], "max", errs[-1])
+    assert not bad, bad[:10]
+    # a full trainmask.py step: clamp(+-5) + Adam on the same gradients (AdamClamp)
+    from rgbac.optim import AdamClamp
+    opt = AdamClamp(netg.parameters(), lr=1e-4)
+    before = torch.cat([p.detach().reshape(-1) for p in netg.parameters()]).clone()
+    opt.zero_grad()
+    o = netg(a.cuda(), noise_z=nz.permute(0, 2, 3, 1).cuda(), noise_y=ny.permute(0, 2, 3, 1).cuda())
+    (4096 * o[1] + o[2]).backward()
+    opt.step()
+    after = torch.cat([p.detach().reshape(-1) for p in netg.parameters()])
+    assert (after != before).any() and torch.isfinite(after).all()

@@ -119,3 +119,58 @@ def test_rgb_bf16_slice_precompute_matches(device, rgb_net):
         assert abs(got[2].item() - want[2].item()) < 0.05 * want[2].item()
     b0, b1 = outs[False][2].item(), outs[True][2].item()
     assert abs(b0 - b1) < 0.02 * b0
+
+
+def test_rgb_forward_fp32_north_star_bar(device):
+    """The north_star bar on real (non-zero) symbols: the seed-234 codec with Encoder.x4 x20
+    (tests/golden/make_golden.py LATENT_GAIN), B=4 (alpha ones / half / blob / zero), fp32
+    parity mode vs the oracle -- PSNR (trainRGB.py:305-306, from the model's masked MSE) and
+    MS-SSIM of the clamped reconstruction (:308-311) within 1e-4, bpp within 2e-5 relative,
+    and the integer symbols round(y - mu) of all slices identical except at near-ties."""
+    import importlib.util
+    import math
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "make_golden", os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                                    "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    from oracle import ref_metrics
+    from rgbac.metrics.ms_ssim_torch import ms_ssim
+    net = mg.rgb_model(mg.LATENT_GAIN)
+    sd = cpu_sd(net)
+    x, a = _inputs(4, 192, 192, seed=7)            # MS-SSIM's 5 levels need > 160 px
+    dev_net = net.to(device)
+    worst = {"psnr": 0.0, "msssim": 0.0, "bpp": 0.0, "flips": 0, "flips_far": 0, "nsym": 0}
+    for i in range(4):
+        xi, ai = x[i:i + 1], a[i:i + 1]
+        me = ref.supply_mask(ai)
+        dbg = {}
+        with torch.no_grad():
+            want = ref.rgb_forward(sd, xi, ai, ai, *me[:4], dbg=dbg)
+            gd = {}
+            got = dev_net(xi.to(device), ai.to(device), ai.to(device),
+                          *[m.to(device) for m in me[:4]], debug=gd)
+        worst["bpp"] = max(worst["bpp"], abs(got[2].item() - want[2].item()) / want[2].item())
+        if want[1].item() > 0:
+            dp = abs(10 * math.log10(1 / got[1].item()) - 10 * math.log10(1 / want[1].item()))
+            worst["psnr"] = max(worst["psnr"], dp)
+        ms_g = ms_ssim(xi.to(device), got[0].clamp(0, 1), data_range=1.0).item()
+        ms_r = ref_metrics.ms_ssim(xi, want[0].clamp(0, 1), data_range=1.0).item()
+        worst["msssim"] = max(worst["msssim"], abs(ms_g - ms_r))
+        y = gd["y"].t[..., :80].float().cpu()
+        for s in range(10):
+            mu_g = gd["musigma"][s].t[..., :8].float().cpu()
+            sym_g = torch.round(y[..., 8 * s:8 * s + 8] - mu_g).permute(0, 3, 1, 2)
+            d = dbg["y"][s] - dbg["mu"][s]
+            sym_r = torch.round(d)
+            near = (d - torch.floor(d) - 0.5).abs() < 1e-3
+            worst["flips"] += int((sym_g != sym_r).sum())
+            worst["flips_far"] += int(((sym_g != sym_r) & ~near).sum()) if s == 0 else 0
+            worst["nsym"] += sym_r.numel()
+    print("north-star bar (fp32):", worst)
+    assert worst["flips_far"] == 0
+    assert worst["flips"] <= 1e-4 * worst["nsym"] + 2
+    assert worst["bpp"] < 2e-5
+    assert worst["psnr"] < 1e-4
+    assert worst["msssim"] < 1e-4

@@ -8,6 +8,7 @@ import ctypes
 import os
 import re
 import subprocess
+import sys
 
 import pytest
 import torch
@@ -211,3 +212,41 @@ def test_convtranspose_small_cout_as_subpel(cout):
                        transposed=True)
     assert pk.mode == rt.SUBPEL2 and pk.ksize == 3 and pk.stride == 1 and pk.cout == 4 * cout
     assert torch.allclose(_emulate(pk, [x], 5, 6), m(x), atol=1e-5)
+
+
+def test_geometry_matches_reference_behaviour():
+    """The whole-codec forward needs H, W multiples of 64: the oracle (an op-for-op
+    restatement of AutoEncoderRGB_Journal.forward) fails at 96x96 exactly like the reference
+    (torch.cat of the 16x16 hyper-synthesis output with the 12x12 latent slice, :242), and
+    the HIP model refuses such sizes up front with a RuntimeError of its own."""
+    import torch
+    from oracle import ref_model as ref
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder, GeometryError, check_geometry
+    torch.manual_seed(234)
+    sd = {k: v.detach() for k, v in AutoEncoder().eval().state_dict().items()}
+    x = torch.rand((1, 3, 96, 96))
+    a = torch.ones((1, 1, 96, 96))
+    me = ref.supply_mask(a)
+    with pytest.raises(RuntimeError, match="Sizes of tensors must match"):
+        with torch.no_grad():
+            ref.rgb_forward(sd, x, a, a, *me[:4])
+    for hw in ((96, 96), (160, 224), (64, 96), (0, 64)):
+        with pytest.raises(GeometryError):
+            check_geometry(*hw)
+    assert issubclass(GeometryError, RuntimeError) and issubclass(GeometryError, ValueError)
+    check_geometry(64, 192)
+
+
+def test_bench_gpus_flag_spawns_ranks(monkeypatch):
+    """`bench.py --gpus N` without a launcher spawns N ranks itself (before any GPU call);
+    under a launcher a mismatching --gpus is rejected."""
+    import bench
+    calls = []
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench, "spawn_ranks", lambda n: calls.append(n) or 0)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "1"])
+    assert bench.main() == 0 and calls == [4]
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4"])
+    with pytest.raises(SystemExit):
+        bench.main()
