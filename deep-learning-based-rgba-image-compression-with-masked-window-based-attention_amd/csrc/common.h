@@ -17,11 +17,16 @@ struct bf16_t { uint16_t u; };
 __device__ __forceinline__ float bf2f(uint16_t u) {
   return __uint_as_float(((uint32_t)u) << 16);
 }
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_hw;
+// round to nearest even by the hardware conversion (v_cvt_pk_bf16_f32): for finite inputs the
+// same bits as (u + 0x7FFF + ((u >> 16) & 1)) >> 16, in one instruction per pair, and a NaN
+// stays a NaN (MI355X_MICROARCH.md, correctness boundaries)
 __device__ __forceinline__ uint16_t f2bf(float f) {
-  // round to nearest even (inputs here are finite)
-  uint32_t u = __float_as_uint(f);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+  return __builtin_bit_cast(uint16_t, (__bf16)f);
+}
+__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
+  const bf16x2_hw v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 // Element access for the two storage types.
@@ -49,8 +54,8 @@ template <> struct Elem<bf16_t> {
   }
   __device__ static void st4(bf16_t* p, const float (&v)[4]) {
     uint2 t;
-    t.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-    t.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    t.x = pack_bf16x2(v[0], v[1]);
+    t.y = pack_bf16x2(v[2], v[3]);
     *reinterpret_cast<uint2*>(p) = t;
   }
 };

@@ -1465,7 +1465,11 @@ static const TileCfg kTiles[] = {
     // 34: small-K wave-streaming kernel (32-pixel wave tiles x up to 192 channels)
     {32, 96},
     // 35: narrow-output wave-streaming kernel (32-pixel wave tiles x <= 32 channels, full K)
-    {32, 32}};
+    {32, 32},
+    // 36..41: patch-resident kernel (TH x 16 M-grid pixels x BN channels, 8 waves)
+    {128, 192}, {128, 128}, {128, 96}, {128, 256}, {64, 128}, {128, 64},
+    // 42..47: fragment-streamed patch kernel (TH x 16 pixels x BN channels)
+    {128, 192}, {64, 192}, {128, 128}, {64, 128}, {128, 256}, {128, 64}};
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 constexpr int kFirstWres = 7;
 constexpr int kWresStages = 6;
@@ -1476,6 +1480,8 @@ constexpr int kFirstDeep = 20;     // 20..26: deep-ring streaming tiles
 constexpr int kFirstPers = 27;     // 27..33: persistent streaming tiles
 constexpr int kTileSmallK = 34;    // conv_smallk_kernel (bf16, plain conv, K <= 256)
 constexpr int kTileWStream = 35;   // conv_wstream_kernel (bf16, stride 1, k 1/3, cout <= 32)
+constexpr int kFirstPatch = 36;    // 36..41: conv_patch_kernel (bf16; k3 s1 conv/subpel, convT)
+constexpr int kFirstFPatch = 42;   // 42..47: conv_fpatch_kernel (fragment-major weights)
 constexpr int kSmallKMax = 256;
 
 // ---------------------------------------------------------------------------
@@ -1831,6 +1837,479 @@ static void launch_pers(const ConvArgsDev& d, int ntile, int nz, hipStream_t st)
   hipLaunchKernelGGL(kern, dim3(G, 1, nz), dim3(256), 0, st, d);
 }
 
+
+
+// Lean phase epilogue of the patch kernels (CONV / CONVT_S2 modes): the lane's TM rows x TN
+// quads of 4 channels; bias loaded once per phase, the activation a template parameter and
+// the residual choice one wave-uniform branch per phase (the generic epilogue_tile_row
+// re-tests act / residual pointers / bounds per element, which measured ~1.7k VALU +
+// 1.1k SALU per wave per phase on the 192-channel convT -- more issue time than the
+// phase's MFMAs).  Needs cout % 4 == 0, no zout, no res1 (callers check).
+template <int TN, int TM, int ACT>
+__device__ __forceinline__ void patch_epi(const ConvShared& s, const ConvGroup& g, int ph, int b,
+                                          int yrow0, int x, const int (&nn)[TN],
+                                          const f32x4 (&acc)[TN][TM]) {
+  using T = bf16_t;
+  float bias[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bias[j][r] = g.bias ? g.bias[nn[j] + r] : 0.0f;
+  const bool convt = s.mode == RGBAC_CONVT_S2;
+  const int py = convt ? ph >> 1 : 0, px = convt ? ph & 1 : 0, sc = convt ? 2 : 1;
+  const int cout = g.cout;
+  T* const out = reinterpret_cast<T*>(g.out) + g.out_coff;
+  const T* const r0 = reinterpret_cast<const T*>(g.res0);
+  const T* const r2 = reinterpret_cast<const T*>(g.res2);
+  const long long ldo = g.out_ldc, ld0 = g.ld0, ld2 = g.ld2;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const long long opix = (long long)(b * s.out_h + sc * (yrow0 + i) + py) * s.out_w +
+                           sc * x + px;
+    float v[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[j][r] = acc[j][i][r] + bias[j][r];
+    if (r0) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        if (nn[j] < cout) {
+          float t[4];
+          Elem<T>::ld4(r0 + opix * ld0 + nn[j], t);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[j][r] += t[r];
+        }
+    }
+    if constexpr (ACT == RGBAC_ACT_GELU) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[j][r] = gelu_t<T>(v[j][r]);
+    } else if constexpr (ACT == RGBAC_ACT_RELU) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[j][r] = v[j][r] > 0.f ? v[j][r] : 0.f;
+    }
+    if (r2) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        if (nn[j] < cout) {
+          float t[4];
+          Elem<T>::ld4(r2 + opix * ld2 + nn[j], t);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[j][r] += t[r];
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+      if (nn[j] < cout) Elem<T>::st4(out + opix * ldo + nn[j], v[j]);
+  }
+}
+
+// Dispatch of a patch kernel's phase epilogue: the lean form where it applies, else the
+// generic per-row epilogue (SUBPEL2 stores, zout, res1 activations, ragged cout).
+template <int TN, int TM>
+__device__ __forceinline__ void patch_epilogue(const ConvShared& s, const ConvGroup& g, int ph,
+                                               int b, int yrow0, int x0, int fr,
+                                               const int (&nn)[TN], const f32x4 (&acc)[TN][TM]) {
+  const bool lean = s.mode != RGBAC_SUBPEL2 && !g.zout && !g.res1 && (g.cout & 3) == 0;
+  if (lean && s.act == RGBAC_ACT_NONE) {
+    patch_epi<TN, TM, RGBAC_ACT_NONE>(s, g, ph, b, yrow0, x0 + fr, nn, acc);
+  } else if (lean && s.act == RGBAC_ACT_GELU) {
+    patch_epi<TN, TM, RGBAC_ACT_GELU>(s, g, ph, b, yrow0, x0 + fr, nn, acc);
+  } else if (lean && s.act == RGBAC_ACT_RELU) {
+    patch_epi<TN, TM, RGBAC_ACT_RELU>(s, g, ph, b, yrow0, x0 + fr, nn, acc);
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = (b * s.Hm + yrow0 + i) * s.Wm + x0 + fr;
+      epilogue_tile_row<bf16_t, TN, TM>(s, g, ph, m, nn, acc, i);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Patch-resident implicit GEMM (bf16), for the 3x3 stride-1 convs (slice stacks, hyper
+// convs, subpel convs) and the 5x5/s2 ConvTranspose (all four output phases).
+//
+// The im2col-staging conv_kernel stages every input pixel once per tap (9x / 25x the input
+// bytes), and -- measured with PMC counters on the 192-channel convT -- spends ~11 SALU +
+// 15 VALU instructions per MFMA on its per-stage gather decode: it is instruction-issue
+// bound at ~14 % of the matrix pipe.  Here a workgroup owns a TH x 16 tile of the M grid
+// (the output grid, or for CONVT_S2 the input grid shared by the four phases) and BN
+// output channels:
+//   * per 64-channel chunk the (TH+2) x 18 input patch (halo 1) is staged ONCE by LDS-DMA
+//     into a double buffer; every tap reads its B fragments from it at a shifted row;
+//   * patch rows are 8 data chunks + 2 pad chunks of 16 bytes (160 B): the 16 consecutive
+//     rows of a fragment read are bank-conflict-free for any tap shift, and a fragment
+//     address is a per-lane constant + a wave-uniform tap offset (one v_add per row
+//     segment per stage, the k-step in the instruction's immediate offset);
+//   * the weights stream through a 3-deep ring of (tap, chunk) stages of BN x 64 (16-byte
+//     chunk c of row r at slot c ^ (r & 7)), one counted s_waitcnt + barrier per stage;
+//     the next chunk's patch pieces ride with the third stage of the current chunk (its
+//     buffer was last read a chunk ago);
+//   * 8 waves (2 per SIMD) as WGM x WGN; per stage a wave runs 2 k-steps of TN x TM
+//     v_mfma_f32_16x16x32_bf16 from (TN + TM) ds_read_b128 per k-step;
+//   * every per-stage index is carried incrementally (no integer division in the loop);
+//   * CONVT_S2: phases run one after another (9, 6, 6, 4 taps); the epilogue of a phase
+//     runs while the next phase's first stages are already in flight.
+template <int TH, int BN, int WGM, int WGN>
+__global__ void __launch_bounds__(512) conv_patch_kernel(const ConvArgsDev args) {
+  using T = bf16_t;
+  constexpr int NW = 8;
+  static_assert(WGM * WGN == NW, "8 waves");
+  constexpr int TW = 16, PW = TW + 2, PH = TH + 2, PR = PH * PW;
+  constexpr int RSC = 10;                         // uint4 per patch row: 8 data + 2 pad
+  constexpr int PPIECE = (PR * RSC + 63) / 64;    // 1-KiB DMA pieces per patch chunk
+  constexpr int PQ = (PPIECE + NW - 1) / NW;      // patch pieces per wave
+  constexpr int TM = TH / WGM, TN = BN / WGN / 16;
+  static_assert(TM >= 1 && TN >= 1 && TM * WGM == TH && TN * WGN * 16 == BN, "tile");
+  constexpr int IA = BN / 8;                      // weight pieces per stage
+  constexpr int NAW = (IA + NW - 1) / NW;         // per wave (a surplus slot re-issues)
+  constexpr int NBUF = 3;
+  constexpr int WSTAGE = BN * 8;                  // uint4 per weight stage
+  constexpr int PSTAGE = PPIECE * 64;             // uint4 per patch buffer
+  __shared__ __attribute__((aligned(16))) uint4 smem[NBUF * WSTAGE + 2 * PSTAGE];
+
+  const ConvShared& s = args.s;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int txn = s.Wm / TW, tyn = s.Hm / TH;
+  int nblk, txi, tyi, b, gi;
+  {
+    const int nwg = gridDim.x * gridDim.y;
+    int t = blockIdx.x + gridDim.x * blockIdx.y;
+    if (s.remap) {                               // XCD-contiguous runs, N tile fastest
+      const int xcd = t & 7, q = nwg >> 3, r = nwg & 7;
+      t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (t >> 3);
+    }
+    nblk = t % gridDim.y; t /= gridDim.y;
+    txi = t % txn; t /= txn;
+    tyi = t % tyn; t /= tyn;
+    b = t % s.batch;
+    gi = t / s.batch;
+  }
+  const ConvGroup& g = args.g[gi];
+  const int n0 = nblk * BN;
+  if (n0 >= g.cout) return;
+  const int y0 = tyi * TH, x0 = txi * TW;
+  const bool convt = s.mode == RGBAC_CONVT_S2;
+  const int nph = convt ? 4 : 1;
+  const int in_h = s.in_h, in_w = s.in_w, cin_pad = g.cin_pad;
+  const int nck = (cin_pad + 63) >> 6;
+  const int send0 = g.send0, send1 = g.send1, send2 = g.send2;
+  const char* const sp0 = reinterpret_cast<const char*>(g.sp0);
+  const char* const sp1 = reinterpret_cast<const char*>(g.sp1);
+  const char* const sp2 = reinterpret_cast<const char*>(g.sp2);
+  const int sld0 = (int)g.sld0, sld1 = (int)g.sld1, sld2 = (int)g.sld2;
+  // groups (phase, chunk); group sizes 9 (conv) or 9, 6, 6, 4 (convT phases)
+  const int ngroups = nph * nck;
+  const int ns = convt ? nck * 25 : nck * 9;
+
+  // ---- per-lane DMA geometry (constant through the K loop)
+  const int lrow = lane >> 3;
+  uint32_t aoff[NAW];
+  int alds[NAW];
+#pragma unroll
+  for (int i = 0; i < NAW; ++i) {
+    const int q = min(wave + NW * i, IA - 1);
+    const int row = 8 * q + lrow;
+    alds[i] = q * 64;
+    aoff[i] = (uint32_t)(((n0 + row) * g.k_pad + ((lane & 7) ^ (row & 7)) * 8) * 2);
+  }
+  int ppix[PQ], plds[PQ], pch[PQ];
+  bool pok[PQ];
+#pragma unroll
+  for (int i = 0; i < PQ; ++i) {
+    const int q = min(wave + NW * i, PPIECE - 1);
+    const int f = q * 64 + lane;
+    const int r = f / RSC, c = f - (f / RSC) * RSC;
+    plds[i] = q * 64;
+    pch[i] = c * 8;
+    const int py = r / PW, px = r - (r / PW) * PW;
+    const int iy = y0 - 1 + py, ix = x0 - 1 + px;
+    pok[i] = r < PR && c < 8 && (unsigned)iy < (unsigned)in_h && (unsigned)ix < (unsigned)in_w;
+    ppix[i] = pok[i] ? (b * in_h + iy) * in_w + ix : 0;
+  }
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lptr_t)smem);
+  const uint32_t lpatch = lbase + NBUF * WSTAGE * 16;
+  const size_t phstride = (size_t)g.rows * g.k_pad * 2;     // bytes per convT phase
+  const char* const wbase = reinterpret_cast<const char*>(g.w);
+
+#define PATCH_ISSUE(grp_, ck_)                                                                \
+  do {                                                                                        \
+    const uint32_t lpb = lpatch + (uint32_t)(((grp_) & 1) * PSTAGE * 16);                     \
+_Pragma("unroll")                                                                             \
+    for (int i = 0; i < PQ; ++i) {                                                            \
+      const int ch = ((ck_) << 6) + pch[i];                                                   \
+      const bool in0 = ch < send0, in1 = ch < send1;                                          \
+      const char* src = in0 ? sp0 : (in1 ? sp1 : sp2);                                        \
+      const int sld = in0 ? sld0 : (in1 ? sld1 : sld2);                                       \
+      const int cs = ch - (in0 ? 0 : (in1 ? send0 : send1));                                  \
+      const bool ok = pok[i] & (ch < send2);                                                  \
+      const unsigned off = ((unsigned)ppix[i] * (unsigned)sld + (unsigned)cs) * 2u;           \
+      const void* gp = ok ? (const void*)(src + off) : (const void*)g_zero_page;              \
+      dma16_l(gp, lpb + plds[i] * 16);                                                        \
+    }                                                                                         \
+  } while (0)
+
+  // issue-side state: stage weight address, tap / chunk / phase counters, group index
+  int itap = 0, intap = 9, ick = 0, iph = 0, igrp = 0;
+  const char* wph = wbase;                        // current phase's packed weights
+  const char* wst = wbase;                        // current stage's weight column
+  const int tapstep = cin_pad * 2;                // bytes from one tap's column to the next
+
+#define STAGE_ISSUE(st_)                                                                      \
+  do {                                                                                        \
+    const uint32_t lst = lbase + (uint32_t)(((st_) % NBUF) * WSTAGE * 16);                    \
+_Pragma("unroll")                                                                             \
+    for (int i = 0; i < NAW; ++i) dma16_s(wst, aoff[i], lst + alds[i] * 16);                  \
+    if (itap == 2 && igrp + 1 < ngroups) {       /* the next group's patch rides here */     \
+      const int nck_ = ick + 1 == nck ? 0 : ick + 1;                                          \
+      PATCH_ISSUE(igrp + 1, nck_);                                                            \
+    }                                                                                         \
+    wst += tapstep;                                                                           \
+    if (++itap == intap) {                                                                    \
+      itap = 0; ++igrp;                                                                       \
+      if (++ick == nck) {                                                                     \
+        ick = 0; ++iph;                                                                       \
+        wph += phstride;                                                                      \
+        intap = (3 - (iph >> 1)) * (3 - (iph & 1));                                           \
+      }                                                                                       \
+      wst = wph + (ick << 7);                                                                 \
+    }                                                                                         \
+  } while (0)
+
+  PATCH_ISSUE(0, 0);
+  STAGE_ISSUE(0);
+  if (ns > 1) STAGE_ISSUE(1);
+
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wm = wave % WGM, wn = wave / WGM;
+  const int fr = lane & 15, fq = lane >> 4;
+  // per-lane LDS element offsets (uint4 units): A rows of k-step 0 / 1, B row-segment bases
+  const int arow = (wn * TN * 16 + fr) * 8;
+  const int a0 = arow + ((0 + fq) ^ (fr & 7)), a1 = arow + ((4 + fq) ^ (fr & 7));
+  int bbase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) bbase[i] = ((wm * TM + i) * PW + fr) * RSC + fq;
+  // compute-side state: tap within the group, tap offset (uint4), group parity, phase
+  int ctap = 0, cntap = 9, ctx = 0, ctw = 3, cck = 0, cph = 0, cgrp = 0;
+  int toff = convt ? (2 * PW + 2) * RSC : 0;      // (oy * PW + ox) * RSC of the group's tap 0
+
+  for (int it = 0; it < ns; ++it) {
+    // retire stage `it`; the ops issued after its weight pieces may stay in flight: stage
+    // it+1's pieces, and a patch rider carried by stage it or it+1 (taps 2 or 1 of a group
+    // that is not the last one: groups have >= 4 taps)
+    const bool rider = (ctap == 1 || ctap == 2) && cgrp + 1 < ngroups;
+    if (it + 1 < ns) {
+      if (rider) wait_vm<NAW + PQ>();
+      else wait_vm<NAW>();
+    } else {
+      wait_vm<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (it + 2 < ns) STAGE_ISSUE(it + 2);
+    const uint4* As = smem + (it % NBUF) * WSTAGE;
+    const uint4* Ps = smem + NBUF * WSTAGE + (cgrp & 1) * PSTAGE + toff;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 a[TN], bb[TM];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) a[j] = As[(ks ? a1 : a0) + j * 128];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) bb[i] = Ps[bbase[i] + 4 * ks];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) mma_step<T>(acc[j][i], a[j], bb[i]);
+    }
+    // advance the compute-side tap: x fastest (convT taps step -1 in the patch, conv +1)
+    ++ctap;
+    if (++ctx == ctw) {                           // (ty, tw-1) -> (ty+1, 0)
+      ctx = 0;
+      toff += convt ? (-PW + ctw - 1) * RSC : (PW - ctw + 1) * RSC;
+    } else {
+      toff += convt ? -RSC : RSC;
+    }
+    if (ctap == cntap) {                          // end of a (phase, chunk) group
+      ctap = 0; ctx = 0; ++cgrp;
+      toff = convt ? (2 * PW + 2) * RSC : 0;
+      if (++cck == nck) {                         // end of a phase: epilogue
+        cck = 0;
+        int nn[TN];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) nn[j] = n0 + wn * TN * 16 + j * 16 + fq * 4;
+        patch_epilogue<TN, TM>(s, g, cph, b, y0 + wm * TM, x0, fr, nn, acc);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        ++cph;
+        ctw = 3 - (cph & 1);
+        cntap = (3 - (cph >> 1)) * ctw;
+      }
+    }
+  }
+#undef STAGE_ISSUE
+#undef PATCH_ISSUE
+}
+
+// ---------------------------------------------------------------------------
+// Fragment-streamed patch kernel (bf16): the same M-grid tiles as conv_patch_kernel (3x3
+// stride-1 conv / subpel, 5x5/s2 convT with its four phases), but with NO barrier in the K
+// loop: the block's whole input patch -- (TH+2) x 18 pixels x every input channel -- is
+// staged in LDS once (LDS-DMA, rows padded by two 16-byte chunks: the 16 consecutive rows of
+// a B-fragment read are then bank-conflict-free for any tap shift), and each wave streams
+// its A fragments straight from a FRAGMENT-MAJOR weight copy into an R-deep register ring:
+// one 1-KiB block per (phase, 16-row N tile, 32-deep k-step) holds the 64 lanes' 16-byte
+// fragments in lane order, so every weight load is a fully coalesced global_load_dwordx4.
+// K runs tap-major over channels padded to 32 per tap (k' = tap * cin32 + ci; zero weights
+// and zero patch channels in the padding).  Waves: 1 (M) x NW (N); wave = TH rows of 16
+// pixels x BN/NW channels.  Each phase's k-steps are padded to a multiple of R (idle steps)
+// so the unrolled ring never straddles a phase's epilogue.
+template <int TH, int BN, int NW, int R>
+__global__ void __launch_bounds__(64 * NW) conv_fpatch_kernel(const ConvArgsDev args) {
+  using T = bf16_t;
+  constexpr int TW = 16, PW = TW + 2, PR = (TH + 2) * PW;
+  constexpr int TM = TH, TN = BN / NW / 16;
+  static_assert(TN * NW * 16 == BN, "tile");
+  extern __shared__ __attribute__((aligned(16))) uint4 patch[];
+
+  const ConvShared& s = args.s;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int txn = s.Wm / TW, tyn = s.Hm / TH;
+  int nblk, txi, tyi, b, gi;
+  {
+    const int nwg = gridDim.x * gridDim.y;
+    int t = blockIdx.x + gridDim.x * blockIdx.y;
+    if (s.remap) {                               // XCD-contiguous runs, N tile fastest
+      const int xcd = t & 7, q = nwg >> 3, r = nwg & 7;
+      t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (t >> 3);
+    }
+    nblk = t % gridDim.y; t /= gridDim.y;
+    txi = t % txn; t /= txn;
+    tyi = t % tyn; t /= tyn;
+    b = t % s.batch;
+    gi = t / s.batch;
+  }
+  const ConvGroup& g = args.g[gi];
+  const int n0 = nblk * BN;
+  if (n0 >= g.cout) return;
+  const int y0 = tyi * TH, x0 = txi * TW;
+  const bool convt = s.mode == RGBAC_CONVT_S2;
+  const int nph = convt ? 4 : 1;
+  const int in_h = s.in_h, in_w = s.in_w, cin_pad = g.cin_pad;
+  const int cin32 = (cin_pad + 31) & ~31;
+  const int nch = cin32 >> 3;                    // 16-byte chunks of a patch row (real part)
+  const int RSc = nch + 2;                       // + 2 pad chunks (bank spread)
+  const int cpt = cin32 >> 5;                    // 32-deep k-steps per tap
+  const int nks_max = (convt ? 9 : 9) * cpt;     // k-steps of the widest phase (layout stride)
+
+  // ---- stage the whole patch: flat uint4 index f -> (row, chunk), zero page outside
+  {
+    const int send0 = g.send0, send1 = g.send1, send2 = g.send2;
+    const char* const sp0 = reinterpret_cast<const char*>(g.sp0);
+    const char* const sp1 = reinterpret_cast<const char*>(g.sp1);
+    const char* const sp2 = reinterpret_cast<const char*>(g.sp2);
+    const int sld0 = (int)g.sld0, sld1 = (int)g.sld1, sld2 = (int)g.sld2;
+    const int total = PR * RSc;
+    const int npiece = (total + 63) >> 6;
+    const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lptr_t)patch);
+    for (int pc = wave; pc < npiece; pc += NW) {
+      const int f = (pc << 6) + lane;
+      const int row = f / RSc, c = f - (f / RSc) * RSc;
+      const int py = row / PW, px = row - (row / PW) * PW;
+      const int iy = y0 - 1 + py, ix = x0 - 1 + px;
+      const int ch = c << 3;
+      const bool in0 = ch < send0, in1 = ch < send1;
+      const char* src = in0 ? sp0 : (in1 ? sp1 : sp2);
+      const int sld = in0 ? sld0 : (in1 ? sld1 : sld2);
+      const int cs = ch - (in0 ? 0 : (in1 ? send0 : send1));
+      const bool ok = row < PR && c < nch && ch < send2 && (unsigned)iy < (unsigned)in_h &&
+                      (unsigned)ix < (unsigned)in_w;
+      const unsigned off = ok ? ((unsigned)((b * in_h + iy) * in_w + ix) * (unsigned)sld +
+                                 (unsigned)cs) * 2u : 0u;
+      dma16_l(ok ? (const void*)(src + off) : (const void*)g_zero_page, lbase + (pc << 10));
+    }
+    wait_vm<0>();
+    __syncthreads();
+  }
+
+  // ---- per-phase k-steps (padded to a multiple of R) and the weight fragment pointer
+  const uint4* const wf = reinterpret_cast<const uint4*>(g.w);
+  const int nt16 = g.rows >> 4;
+  const int ntile0 = (n0 >> 4) + wave * TN;      // this wave's first 16-row N tile
+  auto phase_steps = [&](int ph) {
+    return (convt ? (3 - (ph >> 1)) * (3 - (ph & 1)) : 9) * cpt;
+  };
+  // load-side iterator over the padded flat step sequence
+  int lph = 0, lks = 0, lpad = (phase_steps(0) + R - 1) / R * R, lreal = phase_steps(0);
+#define FP_LOAD(dst)                                                                          \
+  do {                                                                                        \
+    if (lph < nph && lks < lreal) {                                                           \
+_Pragma("unroll")                                                                             \
+      for (int j = 0; j < TN; ++j)                                                            \
+        dst[j] = wf[((size_t)(lph * nt16 + ntile0 + j) * nks_max + lks) * 64 + lane];         \
+    }                                                                                         \
+    if (++lks == lpad) {                                                                      \
+      lks = 0;                                                                                \
+      if (++lph < nph) { lreal = phase_steps(lph); lpad = (lreal + R - 1) / R * R; }          \
+    }                                                                                         \
+  } while (0)
+
+  uint4 ring[R][TN];
+#pragma unroll
+  for (int u = 0; u < R; ++u) FP_LOAD(ring[u]);
+
+  f32x4 acc[TN][TM];
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int ph = 0; ph < nph; ++ph) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int real = phase_steps(ph);
+    const int tw = convt ? 3 - (ph & 1) : 3;
+    int tap = 0, cc = 0;                         // k-step -> (tap, 32-channel chunk)
+    for (int ks0 = 0; ks0 < real; ks0 += R) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        if (ks0 + u < real) {
+          const int tyo = tap / tw, txo = tap - (tap / tw) * tw;
+          const int oy = convt ? 2 - tyo : tyo, ox = convt ? 2 - txo : txo;
+          uint4 bb[TM];
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            const int pr = (i + oy) * PW + fr + ox;
+            bb[i] = patch[pr * RSc + cc * 4 + fq];
+          }
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int i = 0; i < TM; ++i) mma_step<T>(acc[j][i], ring[u][j], bb[i]);
+          if (++cc == cpt) { cc = 0; ++tap; }
+        }
+        FP_LOAD(ring[u]);
+      }
+    }
+    int nn[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) nn[j] = n0 + wave * TN * 16 + j * 16 + fq * 4;
+    patch_epilogue<TN, TM>(s, g, ph, b, y0, x0, fr, nn, acc);
+  }
+#undef FP_LOAD
+}
+
 template <typename T>
 static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t st, int part) {
   const ConvShared& s = d.s;
@@ -1839,7 +2318,7 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
                         (tile < kFirstWres || (tile >= kFirstDeep && tile < kFirstPers));
   if (part == 2) {                         // split-K reduce + epilogue kernels only
     if (s.ksplit == 1 || inlaunch || tile == kTileSpatial || tile == kTileSmallK ||
-        tile == kTileWStream ||
+        tile == kTileWStream || tile >= kFirstPatch ||
         (tile >= kFirstWres && tile < kFirstDeep))
       return RGBAC_OK;
     goto splitk_epilogue;
@@ -1901,6 +2380,65 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
       default: hipLaunchKernelGGL((conv_wres_kernel<T, 128, 16, 4, 1, NS>), grid, dim3(256), 0, st, d); break;
     }
     return check_launch("conv_wres_kernel");
+  }
+  if (tile >= kFirstFPatch) {
+    if constexpr (sizeof(T) == 2) {
+      const int th = tc.bm / 16;
+      const int nbn = (max_cout + tc.bn - 1) / tc.bn;
+      const long long nsp = (long long)s.batch * (s.Hm / th) * (s.Wm / 16) * s.ngroups;
+      int cmax = 0;
+      for (int i = 0; i < s.ngroups; ++i) cmax = d.g[i].cin_pad > cmax ? d.g[i].cin_pad : cmax;
+      const size_t lds = ((size_t)(th + 2) * 18 * (((cmax + 31) & ~31) / 8 + 2) * 16 + 1023) &
+                         ~(size_t)1023;                   // whole 1-KiB DMA pieces
+      if (lds > 160 * 1024) {
+        set_error("fragment-patch tile: the input patch exceeds 160 KiB of LDS");
+        return RGBAC_E_ARG;
+      }
+      dim3 grid((unsigned)nsp, (unsigned)nbn, 1);
+#define RGBAC_FP(TH_, BN_)                                                                    \
+  do {                                                                                        \
+    auto k_ = conv_fpatch_kernel<TH_, BN_, 4, 4>;                                             \
+    static bool attr_ = false;                                                                \
+    if (!attr_) {                                                                             \
+      (void)hipFuncSetAttribute((const void*)k_, hipFuncAttributeMaxDynamicSharedMemorySize,  \
+                                160 * 1024);                                                  \
+      attr_ = true;                                                                           \
+    }                                                                                         \
+    hipLaunchKernelGGL(k_, grid, dim3(256), lds, st, d);                                      \
+  } while (0)
+      switch (tile) {
+        case 42: RGBAC_FP(8, 192); break;
+        case 43: RGBAC_FP(4, 192); break;
+        case 44: RGBAC_FP(8, 128); break;
+        case 45: RGBAC_FP(4, 128); break;
+        case 46: RGBAC_FP(8, 256); break;
+        default: RGBAC_FP(8, 64); break;
+      }
+#undef RGBAC_FP
+      return check_launch("conv_fpatch_kernel");
+    } else {
+      set_error("the fragment-patch tiles are bf16 only");
+      return RGBAC_E_ARG;
+    }
+  }
+  if (tile >= kFirstPatch) {
+    if constexpr (sizeof(T) == 2) {
+      const int th = tile == 40 ? 4 : 8;
+      const long long nsp = (long long)s.batch * (s.Hm / th) * (s.Wm / 16) * s.ngroups;
+      dim3 grid((unsigned)nsp, (unsigned)((max_cout + tc.bn - 1) / tc.bn), 1);
+      switch (tile) {
+        case 36: hipLaunchKernelGGL((conv_patch_kernel<8, 192, 2, 4>), grid, dim3(512), 0, st, d); break;
+        case 37: hipLaunchKernelGGL((conv_patch_kernel<8, 128, 2, 4>), grid, dim3(512), 0, st, d); break;
+        case 38: hipLaunchKernelGGL((conv_patch_kernel<8, 96, 4, 2>), grid, dim3(512), 0, st, d); break;
+        case 39: hipLaunchKernelGGL((conv_patch_kernel<8, 256, 2, 4>), grid, dim3(512), 0, st, d); break;
+        case 40: hipLaunchKernelGGL((conv_patch_kernel<4, 128, 1, 8>), grid, dim3(512), 0, st, d); break;
+        default: hipLaunchKernelGGL((conv_patch_kernel<8, 64, 4, 2>), grid, dim3(512), 0, st, d); break;
+      }
+      return check_launch("conv_patch_kernel");
+    } else {
+      set_error("the patch tiles are bf16 only");
+      return RGBAC_E_ARG;
+    }
   }
   if (tile == kTileWStream) {
     if constexpr (sizeof(T) == 2) {
@@ -2126,6 +2664,24 @@ extern "C" int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroup
       RGBAC_REQUIRE(args[i].nsrc == 1 && args[i].cin_pad == 32 && args[i].src[0].channels == 32 &&
                         args[i].cout <= 32 && args[i].k_pad >= 288,
                     "the spatial 3x3 tile needs one 32-channel source and cout <= 32");
+  } else if (a->tile >= kFirstPatch) {
+    const int th = kTiles[a->tile].bm / 16;
+    RGBAC_REQUIRE(a->dtype == RGBAC_BF16 && a->ksplit == 1 && !a->square_input &&
+                      a->act != RGBAC_ACT_GAUSS &&
+                      (a->mode == RGBAC_CONVT_S2 ||
+                       (a->ksize == 3 && a->stride == 1 &&
+                        (a->mode == RGBAC_CONV || a->mode == RGBAC_SUBPEL2))) &&
+                      s.Wm % 16 == 0 && s.Hm % th == 0,
+                  "the patch tiles need bf16, ksplit 1, a 3x3 stride-1 conv/subpel or the 5x5/s2 "
+                  "convT, the M grid a multiple of 16 wide and of the tile height high");
+    RGBAC_REQUIRE((long long)a->batch * a->in_h * a->in_w < (1ll << 24),
+                  "patch tiles address sources of < 2^24 pixels");
+    for (int i = 0; i < ngroups; ++i)
+      RGBAC_REQUIRE(args[i].cout_pad >= ((args[i].cout + kTiles[a->tile].bn - 1) /
+                                         kTiles[a->tile].bn) * kTiles[a->tile].bn &&
+                        args[i].k_pad >= ntaps_max * args[i].cin_pad &&
+                        (a->tile < kFirstFPatch || args[i].cout_pad % 16 == 0),
+                    "patch tiles read whole BN-row weight tiles");
   } else if (a->tile == kTileWStream) {
     RGBAC_REQUIRE(a->dtype == RGBAC_BF16 && a->mode == RGBAC_CONV && a->ksplit == 1 &&
                       a->stride == 1 && (a->ksize == 1 || a->ksize == 3),

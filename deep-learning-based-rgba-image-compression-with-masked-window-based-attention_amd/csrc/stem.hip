@@ -39,12 +39,6 @@ __device__ __forceinline__ int w2_slot(int row, int chunk) {
   return row * kW2Chunks + (chunk ^ (row & 7));
 }
 
-typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
-// round-to-nearest-even pair conversion (v_cvt_pk_bf16_f32; same result as f2bf for finite x)
-__device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-  const bf16x2_t v = {(__bf16)a, (__bf16)b};
-  return __builtin_bit_cast(uint32_t, v);
-}
 
 __global__ void __launch_bounds__(256, 1)
 stem_gdn_kernel(int batch, int in_h, int in_w, const bf16_t* __restrict__ x, int x_ldc,

@@ -116,7 +116,9 @@ TILES = [(128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 1
          (256, 32),
          (128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 16),
          (128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 16),
-         (32, 96), (32, 32)]
+         (32, 96), (32, 32),
+         (128, 192), (128, 128), (128, 96), (128, 256), (64, 128), (128, 64),
+         (128, 192), (64, 192), (128, 128), (64, 128), (128, 256), (128, 64)]
 FIRST_WRES = 7
 WRES_STAGES = 6
 FIRST_DIRECT = 13        # 13..18: direct kernel (plain conv, K <= DIRECT_STEPS MFMA k-steps)
@@ -131,6 +133,68 @@ GAUSS_TILES = tuple(range(FIRST_WRES)) + tuple(range(FIRST_DEEP, FIRST_DEEP + 7)
 TILE_SMALLK = 34         # conv_smallk_kernel: bf16 1x1 stride-1 conv, one source, cin_pad <= 256
 TILE_WSTREAM = 35        # conv_wstream_kernel: bf16 stride-1 1x1/3x3, cout <= 32, K <= 2336
 WSTREAM_MAX_STEPS = 146
+FIRST_PATCH = 36         # 36..41: conv_patch_kernel (TH x 16 M-grid tile, BN channels, 8 waves)
+PATCH_SIG = {36: (8, 192, 2, 4), 37: (8, 128, 2, 4), 38: (8, 96, 4, 2), 39: (8, 256, 2, 4),
+             40: (4, 128, 1, 8), 41: (8, 64, 4, 2)}
+FIRST_FPATCH = 42        # 42..47: conv_fpatch_kernel (fragment-major weight copy, 4 waves)
+FPATCH_SIG = {42: (8, 192), 43: (4, 192), 44: (8, 128), 45: (4, 128), 46: (8, 256), 47: (8, 64)}
+PATCH = os.environ.get("RGBAC_PATCH", "1") != "0"
+
+
+def frag_weights(pk):
+    """Fragment-major copy of a PackedConv for the conv_fpatch tiles (cached on it):
+    [nphase][cout_pad / 16][ntaps_max * cin32 / 32][64 lanes][8] bf16 -- per (phase, 16-row
+    N tile, 32-deep k-step) the 64 lanes' 16-byte v_mfma_f32_16x16x32_bf16 A fragments in
+    lane order (lane l: row l & 15, k 8 * (l >> 4) .. +7), with K tap-major over the input
+    channels padded to 32 per tap (k' = tap * cin32 + ci; zeros in the padding)."""
+    f = getattr(pk, "frag", None)
+    if f is not None:
+        return f
+    nph, rows, _ = pk.w.shape
+    taps = 9 if pk.mode == CONVT_S2 else pk.ksize * pk.ksize
+    cp, c32 = pk.cin_pad, round_up(pk.cin_pad, 32)
+    w = pk.w[:, :, :taps * cp].reshape(nph, rows, taps, cp)
+    wt = torch.zeros((nph, rows, taps, c32), dtype=pk.w.dtype, device=pk.w.device)
+    wt[..., :cp] = w
+    nks = taps * c32 // 32
+    fr = wt.reshape(nph, rows // 16, 16, nks, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
+    pk.frag = fr
+    return fr
+
+
+def _patch_tiles(preps):
+    """Patch-resident tiles that apply to these (grouped) convs: bf16, the 5x5/s2 convT or a
+    3x3 stride-1 conv/subpel, no squared input / GAUSS epilogue, M grid a multiple of 16 wide
+    and of the tile height high, whole BN-row weight tiles inside the packed rows."""
+    if not PATCH:
+        return []
+    a = preps[0].a
+    if a.dtype != _lib.BF16 or a.square_input or a.act == ACT["gauss"]:
+        return []
+    if a.mode == CONVT_S2:
+        hm, wm = a.in_h, a.in_w
+    elif a.ksize == 3 and a.stride == 1 and a.mode in (CONV, SUBPEL2):
+        hm, wm = a.in_h, a.in_w
+    else:
+        return []
+    if wm % 16 or a.batch * a.in_h * a.in_w >= (1 << 24):
+        return []
+    out = []
+    for t, (th, bn, _, _) in PATCH_SIG.items():
+        if hm % th:
+            continue
+        if all(p.pk.cout_pad >= -(-p.pk.cout // bn) * bn for p in preps):
+            out.append(t)
+    # fragment-streamed tiles: PackedConv weights only (the training packs are re-gathered
+    # every step in the plain layout) and the whole patch in LDS
+    if all(isinstance(p.pk, PackedConv) for p in preps):
+        c32 = max(round_up(p.pk.cin_pad, 32) for p in preps)
+        for t, (th, bn) in FPATCH_SIG.items():
+            if hm % th or (th + 2) * 18 * (c32 // 8 + 2) * 16 > 160 * 1024:
+                continue
+            if all(p.pk.cout_pad >= -(-p.pk.cout // bn) * bn for p in preps):
+                out.append(t)
+    return out
 SMALLK_MAX = 256
 KSPLITS = (1, 2, 4, 8)
 TUNE = os.environ.get("RGBAC_TUNE", "1") != "0"
@@ -168,7 +232,7 @@ def _candidates(M, cout, nst, nks=None, plain=True, spatial=False, smallk=False,
         out.append((TILE_WSTREAM, 1))
     n16 = round_up(cout, 16)
     for t, (bm, bn) in enumerate(TILES):
-        if t in (TILE_SMALLK, TILE_WSTREAM):
+        if t in (TILE_SMALLK, TILE_WSTREAM) or t >= FIRST_PATCH:
             continue
         if t == TILE_SPATIAL:
             if spatial:
@@ -485,6 +549,10 @@ def kernel_name(tile, preps):
     dt = "float" if preps[0].a.dtype == 0 else "bf16_t"
     if tile == TILE_SPATIAL:
         return f"conv3x3_c32_kernel<{dt}>"
+    if tile >= FIRST_FPATCH:
+        return "conv_fpatch_kernel<%d, %d, 4, 4>" % FPATCH_SIG[tile]
+    if tile >= FIRST_PATCH:
+        return "conv_patch_kernel<%d, %d, %d, %d>" % PATCH_SIG[tile]
     if tile == TILE_WSTREAM:
         # the library's wave count choice (csrc/conv.hip launch_wstream)
         nks = max((p.a.ksize * p.a.ksize * p.a.cin_pad + 15) // 16 for p in preps)
@@ -568,6 +636,9 @@ def launch(preps, force=None):
             arr[i].tile, arr[i].ksplit = t, ks
             arr[i].tile_counters = cnt
             arr[i].workspace = None
+            # the fragment-streamed tiles read the fragment-major weight copy
+            arr[i].weight = (frag_weights(pr.pk).data_ptr() if t >= FIRST_FPATCH
+                             else pr.pk.w.data_ptr())
             if ks > 1:
                 ws = torch.empty(ks * pr.nphase * pr.mgrid * round_up(pr.pk.cout, 16),
                                  dtype=torch.float32, device=dev)
@@ -593,6 +664,7 @@ def launch(preps, force=None):
             cands = _candidates(mtot, cout, nst, max(pr.nks for pr in preps),
                                 p0.pk.mode == CONV, _spatial_ok(preps), _smallk_ok(preps),
                                 _wstream_ok(preps))
+            cands += [(t, 1) for t in _patch_tiles(preps)]
         if TUNE and not fixed and not torch.cuda.is_current_stream_capturing():
             best = None
             for cand in cands:

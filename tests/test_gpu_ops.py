@@ -535,3 +535,73 @@ def test_gauss_wstream_matches_ring_tile(device):
     assert (a[0] - b[0]).abs().max().item() <= 1.0 + 1e-6     # a rare .5-boundary symbol flip
     assert (a[0] != b[0]).float().mean().item() < 0.01
     assert abs(a[2] - b[2]) / abs(a[2]) < 1e-2
+
+
+# ------------------------------------------------------------------ patch-resident conv tiles
+PATCH_CASES = [
+    # mode, cin, cout, H, W
+    ("convt", 192, 192, 16, 32), ("convt", 80, 192, 8, 16), ("convt", 192, 3, 8, 16),
+    ("conv", 224, 128, 16, 16), ("conv", 120, 224, 8, 32), ("conv", 40, 40, 8, 16),
+    ("subpel", 192, 192, 8, 16), ("subpel", 192, 12, 16, 16),
+]
+
+
+@pytest.mark.parametrize("mode,cin,cout,H,W", PATCH_CASES)
+def test_conv_patch_tiles(device, mode, cin, cout, H, W):
+    """conv_patch_kernel (tiles 36..41, bf16): ConvTranspose 5x5/s2 (four phases from one
+    staged patch), 3x3 convs (incl. three concatenated sources and a partial last 64-channel
+    chunk) and subpel convs, with GELU / residual epilogues, against PyTorch fp32 on the
+    same bf16-rounded operands (tolerance: bf16 output rounding, 1e-2 of the max)."""
+    rt = _rt()
+    from rgbac.layers.TransformRGB import prep_conv, prep_subpel
+    from rgbac.layers._blocks import subpel_conv3x3
+    g = _gen(cin * 7 + cout + H)
+    B = 2
+    if mode == "convt":
+        m = nn.ConvTranspose2d(cin, cout, 5, stride=2, padding=2, output_padding=1)
+    elif mode == "conv":
+        m = nn.Conv2d(cin, cout, 3, padding=1)
+    else:
+        m = subpel_conv3x3(cin, cout, 2)
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(p.to(torch.bfloat16).float())
+    x = torch.randn((B, cin, H, W), generator=g).to(torch.bfloat16).float()
+    r = torch.randn((B, cout, H * (1 if mode == "conv" else 2), W * (1 if mode == "conv" else 2)),
+                    generator=g).to(torch.bfloat16).float()
+    if mode == "convt" and cout <= 4:
+        mode = "convt_small"                       # runs as conv3x3 + PixelShuffle (SUBPEL2)
+    if mode in ("subpel", "convt_small"):
+        want = F.gelu(m(x))
+    else:
+        want = F.gelu(m(x) + r)
+    dt = torch.bfloat16
+    xd = x.to(device)
+    m = m.to(device)
+    outs = {}
+    with torch.no_grad():
+        if mode == "conv" and cin == 120:           # three sources: 80 + 32 + 8 channels
+            fs = [rt.to_nhwc(xd[:, a:b], dt) for a, b in ((0, 80), (80, 112), (112, 120))]
+            srcs = [f.src() for f in fs]
+        else:
+            srcs = [rt.to_nhwc(xd, dt).src()]
+        fr = rt.to_nhwc(r.to(device), dt)
+        tiles = None
+        for force in [None] + [t for t in range(rt.FIRST_PATCH, rt.FIRST_PATCH + 12)]:
+            if mode == "subpel":
+                pr = prep_subpel(m, srcs, act="gelu")
+            elif mode == "convt_small":
+                pr = prep_conv(m, srcs, act="gelu")
+            else:
+                pr = prep_conv(m, srcs, act="gelu", res0=fr)
+            ok = rt._patch_tiles([pr])
+            if tiles is None:
+                tiles = ok
+            if force is not None and force not in ok:
+                continue
+            o = rt.launch([pr], force=None if force is None else (force, 1))[0]
+            outs[force] = rt.to_nchw(o).cpu()
+    assert tiles, "no patch tile applies"
+    for t, got in outs.items():
+        assert got.shape == want.shape
+        assert rel(got, want) < 1e-2, (t, rel(got, want))
