@@ -1467,9 +1467,11 @@ static const TileCfg kTiles[] = {
     // 35: narrow-output wave-streaming kernel (32-pixel wave tiles x <= 32 channels, full K)
     {32, 32},
     // 36..41: patch-resident kernel (TH x 16 M-grid pixels x BN channels, 8 waves)
-    {128, 192}, {128, 128}, {128, 96}, {128, 256}, {64, 128}, {128, 64},
+    {128, 192}, {128, 128}, {128, 96}, {128, 256}, {128, 192}, {128, 64},
     // 42..47: fragment-streamed patch kernel (TH x 16 pixels x BN channels)
-    {128, 192}, {64, 192}, {128, 128}, {64, 128}, {128, 256}, {128, 64}};
+    {128, 192}, {64, 192}, {128, 128}, {64, 128}, {128, 256}, {128, 64},
+    // 48, 49: patch-resident kernel with a 4-deep weight ring
+    {128, 64}, {128, 128}};
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 constexpr int kFirstWres = 7;
 constexpr int kWresStages = 6;
@@ -1482,6 +1484,7 @@ constexpr int kTileSmallK = 34;    // conv_smallk_kernel (bf16, plain conv, K <=
 constexpr int kTileWStream = 35;   // conv_wstream_kernel (bf16, stride 1, k 1/3, cout <= 32)
 constexpr int kFirstPatch = 36;    // 36..41: conv_patch_kernel (bf16; k3 s1 conv/subpel, convT)
 constexpr int kFirstFPatch = 42;   // 42..47: conv_fpatch_kernel (fragment-major weights)
+constexpr int kFirstPatch2 = 48;   // 48, 49: conv_patch_kernel with NBUF = 4
 constexpr int kSmallKMax = 256;
 
 // ---------------------------------------------------------------------------
@@ -1955,7 +1958,7 @@ __device__ __forceinline__ void patch_epilogue(const ConvShared& s, const ConvGr
 //   * every per-stage index is carried incrementally (no integer division in the loop);
 //   * CONVT_S2: phases run one after another (9, 6, 6, 4 taps); the epilogue of a phase
 //     runs while the next phase's first stages are already in flight.
-template <int TH, int BN, int WGM, int WGN>
+template <int TH, int BN, int WGM, int WGN, int NBUF>
 __global__ void __launch_bounds__(512) conv_patch_kernel(const ConvArgsDev args) {
   using T = bf16_t;
   constexpr int NW = 8;
@@ -1968,7 +1971,9 @@ __global__ void __launch_bounds__(512) conv_patch_kernel(const ConvArgsDev args)
   static_assert(TM >= 1 && TN >= 1 && TM * WGM == TH && TN * WGN * 16 == BN, "tile");
   constexpr int IA = BN / 8;                      // weight pieces per stage
   constexpr int NAW = (IA + NW - 1) / NW;         // per wave (a surplus slot re-issues)
-  constexpr int NBUF = 3;
+  static_assert(NBUF == 3 || NBUF == 4, "ring depth (the patch rider sits at tap NBUF-1 of "
+                                        "a group; groups have >= 4 taps)");
+  constexpr int RT = NBUF - 1;                    // tap of a group that carries the rider
   constexpr int WSTAGE = BN * 8;                  // uint4 per weight stage
   constexpr int PSTAGE = PPIECE * 64;             // uint4 per patch buffer
   __shared__ __attribute__((aligned(16))) uint4 smem[NBUF * WSTAGE + 2 * PSTAGE];
@@ -2066,7 +2071,7 @@ _Pragma("unroll")                                                               
     const uint32_t lst = lbase + (uint32_t)(((st_) % NBUF) * WSTAGE * 16);                    \
 _Pragma("unroll")                                                                             \
     for (int i = 0; i < NAW; ++i) dma16_s(wst, aoff[i], lst + alds[i] * 16);                  \
-    if (itap == 2 && igrp + 1 < ngroups) {       /* the next group's patch rides here */     \
+    if (itap == RT && igrp + 1 < ngroups) {      /* the next group's patch rides here */     \
       const int nck_ = ick + 1 == nck ? 0 : ick + 1;                                          \
       PATCH_ISSUE(igrp + 1, nck_);                                                            \
     }                                                                                         \
@@ -2083,8 +2088,9 @@ _Pragma("unroll")                                                               
   } while (0)
 
   PATCH_ISSUE(0, 0);
-  STAGE_ISSUE(0);
-  if (ns > 1) STAGE_ISSUE(1);
+#pragma unroll
+  for (int st = 0; st < NBUF - 1; ++st)
+    if (st < ns) STAGE_ISSUE(st);
 
   f32x4 acc[TN][TM];
 #pragma unroll
@@ -2104,20 +2110,25 @@ _Pragma("unroll")                                                               
   int toff = convt ? (2 * PW + 2) * RSC : 0;      // (oy * PW + ox) * RSC of the group's tap 0
 
   for (int it = 0; it < ns; ++it) {
-    // retire stage `it`; the ops issued after its weight pieces may stay in flight: stage
-    // it+1's pieces, and a patch rider carried by stage it or it+1 (taps 2 or 1 of a group
-    // that is not the last one: groups have >= 4 taps)
-    const bool rider = (ctap == 1 || ctap == 2) && cgrp + 1 < ngroups;
-    if (it + 1 < ns) {
-      if (rider) wait_vm<NAW + PQ>();
-      else wait_vm<NAW>();
-    } else {
-      wait_vm<0>();
+    // retire stage `it`; the ops issued after its weight pieces may stay in flight: the
+    // stages it+1 .. it+NBUF-2 already issued, and a patch rider carried by one of stages
+    // it .. it+NBUF-2 (tap RT of this group, if it is not the last group)
+    {
+      const bool rider = ctap >= RT - (NBUF - 2) && ctap <= RT && cgrp + 1 < ngroups;
+      const int after = min(NBUF - 2, ns - 1 - it);
+      if constexpr (NBUF == 4) {
+        if (after >= 2) { if (rider) wait_vm<2 * NAW + PQ>(); else wait_vm<2 * NAW>(); }
+        else if (after == 1) { if (rider) wait_vm<NAW + PQ>(); else wait_vm<NAW>(); }
+        else { if (rider) wait_vm<PQ>(); else wait_vm<0>(); }
+      } else {
+        if (after >= 1) { if (rider) wait_vm<NAW + PQ>(); else wait_vm<NAW>(); }
+        else { if (rider) wait_vm<PQ>(); else wait_vm<0>(); }
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
-    if (it + 2 < ns) STAGE_ISSUE(it + 2);
+    if (it + NBUF - 1 < ns) STAGE_ISSUE(it + NBUF - 1);
     const uint4* As = smem + (it % NBUF) * WSTAGE;
     const uint4* Ps = smem + NBUF * WSTAGE + (cgrp & 1) * PSTAGE + toff;
 #pragma unroll
@@ -2381,7 +2392,7 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
     }
     return check_launch("conv_wres_kernel");
   }
-  if (tile >= kFirstFPatch) {
+  if (tile >= kFirstFPatch && tile < kFirstPatch2) {
     if constexpr (sizeof(T) == 2) {
       const int th = tc.bm / 16;
       const int nbn = (max_cout + tc.bn - 1) / tc.bn;
@@ -2423,16 +2434,18 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
   }
   if (tile >= kFirstPatch) {
     if constexpr (sizeof(T) == 2) {
-      const int th = tile == 40 ? 4 : 8;
+      const int th = tc.bm / 16;
       const long long nsp = (long long)s.batch * (s.Hm / th) * (s.Wm / 16) * s.ngroups;
       dim3 grid((unsigned)nsp, (unsigned)((max_cout + tc.bn - 1) / tc.bn), 1);
       switch (tile) {
-        case 36: hipLaunchKernelGGL((conv_patch_kernel<8, 192, 2, 4>), grid, dim3(512), 0, st, d); break;
-        case 37: hipLaunchKernelGGL((conv_patch_kernel<8, 128, 2, 4>), grid, dim3(512), 0, st, d); break;
-        case 38: hipLaunchKernelGGL((conv_patch_kernel<8, 96, 4, 2>), grid, dim3(512), 0, st, d); break;
-        case 39: hipLaunchKernelGGL((conv_patch_kernel<8, 256, 2, 4>), grid, dim3(512), 0, st, d); break;
-        case 40: hipLaunchKernelGGL((conv_patch_kernel<4, 128, 1, 8>), grid, dim3(512), 0, st, d); break;
-        default: hipLaunchKernelGGL((conv_patch_kernel<8, 64, 4, 2>), grid, dim3(512), 0, st, d); break;
+        case 36: hipLaunchKernelGGL((conv_patch_kernel<8, 192, 2, 4, 3>), grid, dim3(512), 0, st, d); break;
+        case 37: hipLaunchKernelGGL((conv_patch_kernel<8, 128, 2, 4, 3>), grid, dim3(512), 0, st, d); break;
+        case 38: hipLaunchKernelGGL((conv_patch_kernel<8, 96, 4, 2, 3>), grid, dim3(512), 0, st, d); break;
+        case 39: hipLaunchKernelGGL((conv_patch_kernel<8, 256, 2, 4, 3>), grid, dim3(512), 0, st, d); break;
+        case 40: hipLaunchKernelGGL((conv_patch_kernel<8, 192, 2, 4, 4>), grid, dim3(512), 0, st, d); break;
+        case 48: hipLaunchKernelGGL((conv_patch_kernel<8, 64, 4, 2, 4>), grid, dim3(512), 0, st, d); break;
+        case 49: hipLaunchKernelGGL((conv_patch_kernel<8, 128, 2, 4, 4>), grid, dim3(512), 0, st, d); break;
+        default: hipLaunchKernelGGL((conv_patch_kernel<8, 64, 4, 2, 3>), grid, dim3(512), 0, st, d); break;
       }
       return check_launch("conv_patch_kernel");
     } else {
@@ -2680,7 +2693,8 @@ extern "C" int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroup
       RGBAC_REQUIRE(args[i].cout_pad >= ((args[i].cout + kTiles[a->tile].bn - 1) /
                                          kTiles[a->tile].bn) * kTiles[a->tile].bn &&
                         args[i].k_pad >= ntaps_max * args[i].cin_pad &&
-                        (a->tile < kFirstFPatch || args[i].cout_pad % 16 == 0),
+                        (a->tile < kFirstFPatch || a->tile >= kFirstPatch2 ||
+                         args[i].cout_pad % 16 == 0),
                     "patch tiles read whole BN-row weight tiles");
   } else if (a->tile == kTileWStream) {
     RGBAC_REQUIRE(a->dtype == RGBAC_BF16 && a->mode == RGBAC_CONV && a->ksplit == 1 &&

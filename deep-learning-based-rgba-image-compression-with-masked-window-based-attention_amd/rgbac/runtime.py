@@ -117,8 +117,9 @@ TILES = [(128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 1
          (128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 16),
          (128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 16),
          (32, 96), (32, 32),
-         (128, 192), (128, 128), (128, 96), (128, 256), (64, 128), (128, 64),
-         (128, 192), (64, 192), (128, 128), (64, 128), (128, 256), (128, 64)]
+         (128, 192), (128, 128), (128, 96), (128, 256), (128, 192), (128, 64),
+         (128, 192), (64, 192), (128, 128), (64, 128), (128, 256), (128, 64),
+         (128, 64), (128, 128)]
 FIRST_WRES = 7
 WRES_STAGES = 6
 FIRST_DIRECT = 13        # 13..18: direct kernel (plain conv, K <= DIRECT_STEPS MFMA k-steps)
@@ -134,8 +135,9 @@ TILE_SMALLK = 34         # conv_smallk_kernel: bf16 1x1 stride-1 conv, one sourc
 TILE_WSTREAM = 35        # conv_wstream_kernel: bf16 stride-1 1x1/3x3, cout <= 32, K <= 2336
 WSTREAM_MAX_STEPS = 146
 FIRST_PATCH = 36         # 36..41: conv_patch_kernel (TH x 16 M-grid tile, BN channels, 8 waves)
-PATCH_SIG = {36: (8, 192, 2, 4), 37: (8, 128, 2, 4), 38: (8, 96, 4, 2), 39: (8, 256, 2, 4),
-             40: (4, 128, 1, 8), 41: (8, 64, 4, 2)}
+PATCH_SIG = {36: (8, 192, 2, 4, 3), 37: (8, 128, 2, 4, 3), 38: (8, 96, 4, 2, 3),
+             39: (8, 256, 2, 4, 3), 40: (8, 192, 2, 4, 4), 41: (8, 64, 4, 2, 3),
+             48: (8, 64, 4, 2, 4), 49: (8, 128, 2, 4, 4)}
 FIRST_FPATCH = 42        # 42..47: conv_fpatch_kernel (fragment-major weight copy, 4 waves)
 FPATCH_SIG = {42: (8, 192), 43: (4, 192), 44: (8, 128), 45: (4, 128), 46: (8, 256), 47: (8, 64)}
 PATCH = os.environ.get("RGBAC_PATCH", "1") != "0"
@@ -180,7 +182,7 @@ def _patch_tiles(preps):
     if wm % 16 or a.batch * a.in_h * a.in_w >= (1 << 24):
         return []
     out = []
-    for t, (th, bn, _, _) in PATCH_SIG.items():
+    for t, (th, bn, _, _, _) in PATCH_SIG.items():
         if hm % th:
             continue
         if all(p.pk.cout_pad >= -(-p.pk.cout // bn) * bn for p in preps):
@@ -549,10 +551,10 @@ def kernel_name(tile, preps):
     dt = "float" if preps[0].a.dtype == 0 else "bf16_t"
     if tile == TILE_SPATIAL:
         return f"conv3x3_c32_kernel<{dt}>"
-    if tile >= FIRST_FPATCH:
+    if tile in FPATCH_SIG:
         return "conv_fpatch_kernel<%d, %d, 4, 4>" % FPATCH_SIG[tile]
-    if tile >= FIRST_PATCH:
-        return "conv_patch_kernel<%d, %d, %d, %d>" % PATCH_SIG[tile]
+    if tile in PATCH_SIG:
+        return "conv_patch_kernel<%d, %d, %d, %d, %d>" % PATCH_SIG[tile]
     if tile == TILE_WSTREAM:
         # the library's wave count choice (csrc/conv.hip launch_wstream)
         nks = max((p.a.ksize * p.a.ksize * p.a.cin_pad + 15) // 16 for p in preps)
@@ -637,7 +639,7 @@ def launch(preps, force=None):
             arr[i].tile_counters = cnt
             arr[i].workspace = None
             # the fragment-streamed tiles read the fragment-major weight copy
-            arr[i].weight = (frag_weights(pr.pk).data_ptr() if t >= FIRST_FPATCH
+            arr[i].weight = (frag_weights(pr.pk).data_ptr() if t in FPATCH_SIG
                              else pr.pk.w.data_ptr())
             if ks > 1:
                 ws = torch.empty(ks * pr.nphase * pr.mgrid * round_up(pr.pk.cout, 16),

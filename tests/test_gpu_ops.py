@@ -587,7 +587,7 @@ def test_conv_patch_tiles(device, mode, cin, cout, H, W):
             srcs = [rt.to_nhwc(xd, dt).src()]
         fr = rt.to_nhwc(r.to(device), dt)
         tiles = None
-        for force in [None] + [t for t in range(rt.FIRST_PATCH, rt.FIRST_PATCH + 12)]:
+        for force in [None] + sorted(set(rt.PATCH_SIG) | set(rt.FPATCH_SIG)):
             if mode == "subpel":
                 pr = prep_subpel(m, srcs, act="gelu")
             elif mode == "convt_small":
