@@ -115,6 +115,10 @@ SIGNATURES = {
     "rgbac_residual_unit": [_VP, _I32, _VP],
     "rgbac_stem_gdn": [_I32, _I32, _I32, _VP, _I64, _VP, _I32, _VP, _VP, _I32, _VP, _I32, _VP,
                        _I64, _VP],
+    "rgbac_winattn_block": [_I32, _I32, _I32, _I32, _I32, _F, _VP, _I64, _VP, _VP, _VP, _VP, _VP,
+                            _VP, _VP, _I64, _VP],
+    "rgbac_dse_block": [_I32, _I32, _I32, _I32, _I32, _F, _VP, _I64, _VP, _I64, _VP, _I32, _VP, _VP,
+                        _I32, _VP, _VP, _I32, _VP, _VP, _I32, _VP, _VP, _I64, _VP],
     # training step
     "rgbac_act_bwd": [_I32, _I32, _F, _I64, _I32, _VP, _I64, _VP, _I64, _VP, _I64, _VP, _VP,
                       _I64, _VP, _I64, _VP],

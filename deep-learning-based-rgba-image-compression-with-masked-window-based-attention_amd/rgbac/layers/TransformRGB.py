@@ -90,6 +90,56 @@ class EnhancementBlock(nn.Module):
         return _layer_forward(self, lambda f: self.nhwc(f), "enhancement_t", input)
 
 
+def dse_fused_ok(dse, x):
+    """The 3-launch fused DSE (rgbac_dse_block) applies: bf16, 32 filters, ReLU or LeakyReLU
+    blocks (one slope), a DSE input of 1 or 3 channels at ldc % 8 == 0."""
+    if not (rt.DSE_FUSED and x.t.dtype == torch.bfloat16 and x.C in (1, 3) and x.ldc % 8 == 0):
+        return False
+    if dse.input_conv.out_channels != 32:
+        return False
+    slopes = set()
+    for e in (dse.enh1, dse.enh2, dse.enh3):
+        if type(e.relu) not in (nn.ReLU, nn.LeakyReLU) or e.conv1.in_channels != 32 or \
+                e.conv1.kernel_size != (3, 3):
+            return False
+        slopes.add(_act_of(e.relu)[1])
+    return len(slopes) == 1
+
+
+def dse_fused(dse, x, only=None):
+    """DSE.forward (TransformRGB.py:39-49 / AutoEncoderMask_Journal.py:39-48) as three
+    rgbac_dse_block launches: in_conv fused into block 1, blocks 1-3 each one launch with
+    the ReLU map on chip, (+ x_first, out_conv, + identity) fused into block 3."""
+    dt, dev = x.t.dtype, x.t.device
+    c32 = [(32, 32)]
+    pin = rt.packed(dse.input_conv, dt, rt.segs_of(x.src()))
+    pout = rt.packed(dse.output_conv, dt, c32)
+    packs = [(rt.packed(e.conv1, dt, c32), rt.packed(e.conv2, dt, c32))
+             for e in (dse.enh1, dse.enh2, dse.enh3)]
+    slope = _act_of(dse.enh1.relu)[1]
+    out = rt.new_feat(x.B, x.H, x.W, x.C, dt, dev)
+    t = None
+    st = rt._lib.stream_ptr(dev)
+    npx = x.B * x.H * x.W
+    for mode, (p1, p2) in enumerate(packs):
+        dst = out if mode == 2 else rt.new_feat(x.B, x.H, x.W, 32, dt, dev)
+        args = (mode, x.B, x.H, x.W, x.C, slope, x.ptr(), x.ldc,
+                0 if t is None else t.ptr(), 0 if t is None else t.ldc,
+                pin.w.data_ptr(), pin.k_pad, pin.bias.data_ptr(),
+                p1.w.data_ptr(), p1.k_pad, p1.bias.data_ptr(),
+                p2.w.data_ptr(), p2.k_pad, p2.bias.data_ptr(),
+                pout.w.data_ptr(), pout.k_pad, pout.bias.data_ptr(), dst.ptr(), dst.ldc, st)
+        if only is not None and mode != only:         # (tools/dse_probe.py: one launch)
+            t = dst
+            continue
+        rt.timed("dse_block_kernel", 2.0 * npx * 32 * 288 * 2,
+                 2.0 * npx * ((8 if mode == 0 else 32) + (x.ldc if mode == 2 else 32)),
+                 lambda a=args: rt._lib.call("rgbac_dse_block", *a),
+                 f"dse_block_kernel mode{mode} 32ch {x.H}x{x.W} B{x.B}")
+        t = dst
+    return out
+
+
 class DSE(nn.Module):
     def __init__(self, num_filters=32):
         super().__init__()
@@ -100,6 +150,8 @@ class DSE(nn.Module):
         self.output_conv = nn.Conv2d(num_filters, 3, 1, stride=1)
 
     def nhwc(self, x):
+        if dse_fused_ok(self, x):
+            return dse_fused(self, x)
         first = run_conv(self.input_conv, [x.src()])
         t = self.enh1.nhwc(first)
         t = self.enh2.nhwc(t)

@@ -114,10 +114,70 @@ class WindowAttention(nn.Module):
             ent = self.__dict__["_rgbac_bias"]
         return ent[1]
 
+    def block_packs(self):
+        """Fragment-major bf16 packs for rgbac_winattn_block, cached per parameter version:
+        wq [4 pairs][54][64 lanes][8] (q | k | v of heads 2p, 2p+1: 3 x 3 16-row tiles x 6
+        32-deep k-steps), wp [8 heads][12][64][8] (proj columns of a head, padded 24 -> 32)."""
+        ps = (self.qkv.weight, self.qkv.bias, self.proj.weight, self.proj.bias,
+              self.relative_position_bias_table)
+        key = (rt.PARAM_GEN,) + tuple((t._version, t.data_ptr()) for t in ps)
+        ent = self.__dict__.get("_rgbac_block")
+        if ent is None or ent[0] != key:
+            with torch.no_grad():
+                dev = self.qkv.weight.device
+                ar = lambda k: torch.arange(k, device=dev)
+                Wq = self.qkv.weight.float()
+                p, f, l = ar(4)[:, None, None], ar(54)[None, :, None], ar(64)[None, None, :]
+                row = (f // 18) * 192 + 48 * p + 16 * ((f % 18) // 6) + (l & 15)
+                col = (32 * (f % 6) + 8 * (l >> 4))[..., None] + ar(8)
+                rowb, colb = torch.broadcast_tensors(row[..., None], col)
+                wq = Wq[rowb, colb].to(torch.bfloat16).contiguous()
+                Wp = self.proj.weight.float()
+                h, m = ar(8)[:, None, None, None], ar(12)[None, :, None, None]
+                l4, e = ar(64)[None, None, :, None], ar(8)[None, None, None, :]
+                rowp = (16 * m + (l4 & 15)).expand(8, 12, 64, 8)
+                hc = (8 * (l4 >> 4) + e).expand(8, 12, 64, 8)
+                colp = 24 * h + hc.clamp(max=23)
+                wp = torch.where(hc < 24, Wp[rowp, colp], torch.zeros((), device=dev))
+                wp = wp.to(torch.bfloat16).contiguous()
+                bqkv = self.qkv.bias.float().contiguous()
+                bproj = self.proj.bias.float().contiguous()
+                table = self.relative_position_bias_table.float().contiguous()
+            self.__dict__["_rgbac_block"] = (key, (wq, bqkv, wp, bproj, table))
+            ent = self.__dict__["_rgbac_block"]
+        return ent[1]
+
+    def block_fused_ok(self, x, residual, amask):
+        return (rt.WINBLOCK_FUSED and residual and amask is None and x.t.dtype == torch.bfloat16
+                and self.window_size[0] == 8 and self.dim == 192 and self.num_heads == 8
+                and self.qkv.bias is not None and x.ldc % 8 == 0 and x.H % 8 == 0
+                and x.W % 8 == 0)
+
+    def run_block(self, x, alpha, shift, masked):
+        """The whole block (qkv + attention + proj + MASKSEL residual) as one
+        rgbac_winattn_block launch: x + attn(x) on active windows, x elsewhere."""
+        wq, bqkv, wp, bproj, table = self.block_packs()
+        out = rt.new_feat(x.B, x.H, x.W, x.C, x.t.dtype, x.t.device)
+        if masked:
+            alpha = alpha.contiguous().float()
+        npix = x.B * x.H * x.W
+        rt.timed("winblock_kernel", 2.0 * npix * (576 * 192 + 2 * 64 * 192 + 192 * 192),
+                 2.0 * npix * 2 * x.ldc,
+                 lambda: _lib.call(
+                     "rgbac_winattn_block", x.B, x.H, x.W, shift, 1 if masked else 0,
+                     float(torch.tensor(self.scale, dtype=torch.float32)), x.ptr(), x.ldc,
+                     _lib.ptr(alpha) if masked else None, wq.data_ptr(), bqkv.data_ptr(),
+                     wp.data_ptr(), bproj.data_ptr(), table.data_ptr(), out.ptr(), out.ldc,
+                     _lib.stream_ptr(x.t.device)),
+                 f"winblock_kernel ws8 C192 {x.H}x{x.W} B{x.B} shift{shift}")
+        return out
+
     def run_nhwc(self, x, alpha, shift, masked, residual=True, amask=None):
         """x: Feat (B,H,W,C), alpha: fp32 (B,1,H,W) or None -> Feat x + attn(x)
         (or attn(x) alone when ``residual`` is False); ``amask``: explicit additive mask
         fp32 (nW, N, N) for window w = mask[w % nW] (WindowAttention.forward's ``mask``)."""
+        if self.block_fused_ok(x, residual, amask):
+            return self.run_block(x, alpha, shift, masked)
         C, ws = self.dim, self.window_size[0]
         dt = x.t.dtype
         qkv = rt.conv(rt.packed(self.qkv, dt, [(C, x.ldc)]), [x.src()])

@@ -8,7 +8,7 @@ import torch.nn as nn
 from .. import runtime as rt
 from ..entropy import EntropyBottleneck, GaussianConditional
 from ..layers.GDN import GDN
-from ..layers.TransformRGB import _act_of, _layer_forward, prep_conv, run_conv
+from ..layers.TransformRGB import _act_of, _layer_forward, dse_fused, dse_fused_ok, prep_conv, run_conv
 from ..layers._blocks import conv, conv3x3, deconv, subpel_conv3x3  # noqa: F401
 from ._latent import latent_path
 from .AutoEncoderRGB_Journal import (_CompressionModelMixin, _hyper_analysis, _hyper_synthesis,
@@ -43,6 +43,8 @@ class DSE(nn.Module):
         self.output_conv = nn.Conv2d(num_filters, in_ch, 1, stride=1)
 
     def nhwc(self, x):
+        if dse_fused_ok(self, x):
+            return dse_fused(self, x)
         first = run_conv(self.input_conv, [x.src()])
         t = self.enh1.nhwc(first)
         t = self.enh2.nhwc(t)

@@ -206,6 +206,8 @@ TILE_SET = os.environ.get("RGBAC_TILE_SET", "stream")
 _tune_cache = {}          # shape key -> (tile, ksplit)
 FORCE = None              # (tile, ksplit) override, used by the tile/split-K tests
 STEM_FUSED = os.environ.get("RGBAC_STEM_FUSED", "1") != "0"   # x1 + gdn1 as one launch (bf16)
+DSE_FUSED = os.environ.get("RGBAC_DSE_FUSED", "1") != "0"     # DSE as 3 fused launches (bf16)
+WINBLOCK_FUSED = os.environ.get("RGBAC_WINBLOCK", "1") != "0"  # ws-8 attention block, 1 launch
 
 
 def pick_cout_pad(cout):

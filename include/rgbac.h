@@ -386,6 +386,39 @@ int rgbac_stem_gdn(int batch, int in_h, int in_w, const void* x, int64_t x_ldc, 
                    int w1_kpad, const float* b1, const void* w2, int w2_kpad, const float* beta,
                    int inverse, void* out, int64_t out_ldc, void* stream);
 
+/* Fused masked shifted-window attention block, bf16, window 8, C = 192, 8 heads
+ * (reference: layers/masked_win_attention.py:96-131 WindowAttention.forward, :169-251
+ * WinBasedAttention.forward).  out = x + proj(attn(x)) on windows whose alpha is non-zero
+ * anywhere (all windows when masked == 0), out = x elsewhere; the cyclic shift, window
+ * partition / drop / reverse, the shifted-frame region mask and the relative position bias
+ * are index math inside the kernel.  x, out: NHWC bf16 [batch][h][w][ld] (h, w multiples of
+ * 8, out != x); alpha: fp32 [batch][h][w] (masked only); wq_packed / wp_packed: the
+ * fragment-major qkv / proj packs of WindowAttention.block_packs(); bqkv [576], bproj [192]
+ * fp32; table: relative_position_bias_table [225][8] fp32.  Replaces the qkv GEMM,
+ * rgbac_winattn_core_ex and the MASKSEL proj GEMM of one WinBasedAttention call. */
+int rgbac_winattn_block(int batch, int h, int w, int shift, int masked, float scale,
+                        const void* x, int64_t ldx, const float* alpha, const void* wq_packed,
+                        const float* bqkv, const void* wp_packed, const float* bproj,
+                        const float* table, void* out, int64_t ldo, void* stream);
+
+/* Fused DSE EnhancementBlock, bf16 NHWC (reference: layers/TransformRGB.py:16-49 --
+ * EnhancementBlock.forward :23-28 and DSE.forward :39-49; the alpha codec's DSE,
+ * models/AutoEncoderMask_Journal.py:39-48).  One launch computes
+ *   out = conv2(act(conv1(t))) + t         (3x3 32->32, zero padding; the act map stays on chip;
+ *                                           act = ReLU (slope 0) or LeakyReLU(slope))
+ * mode 0 (first block): t = in_conv(x) is evaluated on the fly from the DSE input x;
+ * mode 1 (middle block): t is read from `t` [batch][h][w][ldt], out is 32 channels;
+ * mode 2 (last block):  out = out_conv(bf16(block(t) + in_conv(x))) + x, cin channels.
+ * x: DSE input [batch][h][w][ldx] (cin <= 7 used channels, ldx % 8 == 0); w_in / w1 / w2 /
+ * w_out: rgbac_conv2d-packed bf16 weights ([rows][kp], k = tap*32 + c for the 3x3 packs,
+ * so kp1, kp2 >= 288), biases fp32.  Replaces the 8 launches of DSE.forward. */
+int rgbac_dse_block(int mode, int batch, int h, int w, int cin, float slope, const void* x,
+                    int64_t ldx,
+                    const void* t, int64_t ldt, const void* w_in, int kp_in, const float* b_in,
+                    const void* w1, int kp1, const float* b1, const void* w2, int kp2,
+                    const float* b2, const void* w_out, int kp_out, const float* b_out,
+                    void* out, int64_t ldo, void* stream);
+
 /* Kernel timing (bench.py's launch profiler; no reference counterpart).  Events are created
  * with hipEventDisableSystemFence (no cache writeback/invalidate per record); recorded on a
  * capturing stream they become external event nodes of the HIP graph, so per-launch times

@@ -1,0 +1,132 @@
+"""GPU: the fused block kernels against the unfused launch sequence they replace and the
+fp32 oracle (tests/../oracle/ref_model.py).
+
+DSE (rgbac_dse_block, reference layers/TransformRGB.py:16-49 and
+models/AutoEncoderMask_Journal.py:39-48): three launches instead of eight.  The fused path
+keeps every bf16 rounding point of the unfused one (block outputs, the ReLU map, x_first,
+block3 + x_first); only in_conv's 3-term sum is formed on the VALU instead of the MFMA, so
+an x_first value can differ by one bf16 ulp.  Bar: the fused output is as close to the fp32
+oracle as the unfused bf16 path (within 1.5x of its max error, or 1e-2 relative), and the
+two bf16 paths agree to 2 bf16 ulps of the output range at 99.9 % of the elements."""
+import pytest
+import torch
+
+from oracle import ref_model as ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _dse(kind, seed):
+    torch.manual_seed(seed)
+    if kind == "rgb":
+        from rgbac.layers.TransformRGB import DSE
+        m = DSE(32)
+    else:
+        from rgbac.models.AutoEncoderMask_Journal import DSE
+        m = DSE(1, 32)
+    with torch.no_grad():                  # larger than default init: the blocks matter
+        for e in (m.enh1, m.enh2, m.enh3):
+            e.conv1.weight.mul_(2.0)
+            e.conv2.weight.mul_(2.0)
+    return m.cuda().eval()
+
+
+@pytest.mark.parametrize("kind,B,H,W", [("rgb", 2, 64, 96), ("rgb", 1, 40, 50),
+                                        ("mask", 2, 48, 64), ("rgb", 2, 256, 256),
+                                        ("mask", 1, 17, 33)])
+def test_dse_fused_matches_unfused_and_oracle(device, kind, B, H, W):
+    from rgbac import runtime as rt
+    from rgbac.layers.TransformRGB import dse_fused, dse_fused_ok
+    m = _dse(kind, 3)
+    C = 3 if kind == "rgb" else 1
+    x = torch.rand((B, C, H, W), generator=torch.Generator().manual_seed(4)).cuda()
+    with torch.no_grad():
+        f = rt.to_nhwc(x, torch.bfloat16)
+        assert dse_fused_ok(m, f)
+        got = rt.to_nchw(dse_fused(m, f)).float().cpu()
+        old = rt.DSE_FUSED
+        rt.DSE_FUSED = False
+        try:
+            base = rt.to_nchw(m.nhwc(f)).float().cpu()
+        finally:
+            rt.DSE_FUSED = old
+    sd = {f"m.{k}": v.detach().cpu() for k, v in m.state_dict().items()}
+    want = ref.dse(x.cpu(), sd, "m", leaky=(kind == "mask")).detach()
+    scale = want.abs().max().item()
+    e_got = (got - want).abs().max().item() / scale
+    e_base = (base - want).abs().max().item() / scale
+    ulp = scale * 2.0 ** -7
+    frac = ((got - base).abs() > 2 * ulp).float().mean().item()
+    print(f"DSE {kind} {B}x{H}x{W}: fused err {e_got:.2e}, unfused err {e_base:.2e}, "
+          f"elements > 2 ulp apart {frac:.1e}")
+    assert e_got <= max(1.5 * e_base, 1e-2), (e_got, e_base)
+    assert frac <= 1e-3, frac
+
+
+def test_dse_module_forward_uses_fused_path(device):
+    """DSE.forward under no_grad at bf16 goes through rgbac_dse_block (3 launches)."""
+    from rgbac import runtime as rt
+    m = _dse("rgb", 5)
+    f = rt.to_nhwc(torch.rand((1, 3, 64, 64), device="cuda"), torch.bfloat16)
+    prof = rt.LaunchProfiler()
+    old = rt.PROFILER
+    rt.PROFILER = prof
+    try:
+        with torch.no_grad():
+            m.nhwc(f)
+    finally:
+        rt.PROFILER = old
+    names = [r[0] for r in prof.records]
+    assert names == ["dse_block_kernel"] * 3, names
+
+
+# ---------------------------------------------------------------------------------------
+# Masked shifted-window attention block (rgbac_winattn_block; reference
+# layers/masked_win_attention.py:96-131, 169-251): one launch instead of qkv GEMM + core +
+# MASKSEL proj GEMM.  The fused path skips the bf16 round trip of the qkv tensor (q is scaled
+# before its single rounding), so it is compared with the fp32 oracle at the unfused bf16
+# path's own error (within 1.5x, or 2e-2 of the output range), and with the unfused path at
+# 3 bf16 ulps of the output range on 99.5 % of the elements.
+@pytest.mark.parametrize("B,H,W,shift,masked", [(2, 64, 64, 4, True), (1, 32, 48, 0, False),
+                                                (1, 24, 40, 4, True), (2, 16, 16, 0, True),
+                                                (1, 8, 24, 0, True)])
+def test_winattn_block_fused_matches_unfused_and_oracle(device, B, H, W, shift, masked):
+    from rgbac import runtime as rt
+    from rgbac.layers.masked_win_attention import WinBasedAttention
+    torch.manual_seed(11)
+    m = WinBasedAttention(192, 8, 8, shift).cuda().eval()
+    with torch.no_grad():
+        m.attn.relative_position_bias_table.normal_(0, 0.5)   # make the bias matter
+    m.masked = masked
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn((B, 192, H, W), generator=g)
+    alpha = torch.ones((B, 1, H, W))
+    if masked:
+        alpha[:, :, : H // 2, : W // 2] = 0                  # some all-transparent windows
+        alpha[0, 0, 3, 5] = 1.0                              # ... and one nearly transparent
+    xg, ag = x.cuda(), alpha.cuda()
+    with torch.no_grad():
+        f = rt.to_nhwc(xg, torch.bfloat16)
+        assert m.attn.block_fused_ok(f, True, None)
+        got = rt.to_nchw(m.nhwc(f, ag)).float().cpu()
+        old = rt.WINBLOCK_FUSED
+        rt.WINBLOCK_FUSED = False
+        try:
+            base = rt.to_nchw(m.nhwc(f, ag)).float().cpu()
+        finally:
+            rt.WINBLOCK_FUSED = old
+    sd = {f"m.{k}": v.detach().cpu() for k, v in m.state_dict().items()}
+    want = ref.win_based_attention(x, alpha, sd, "m", 8, shift, heads=8,
+                                   masked=masked).detach()
+    scale = want.abs().max().item()
+    e_got = (got - want).abs().max().item() / scale
+    e_base = (base - want).abs().max().item() / scale
+    ulp = scale * 2.0 ** -7
+    frac = ((got - base).abs() > 3 * ulp).float().mean().item()
+    print(f"winblock {B}x{H}x{W} shift {shift} masked {masked}: fused err {e_got:.2e}, "
+          f"unfused err {e_base:.2e}, elements > 3 ulp apart {frac:.1e}")
+    assert e_got <= max(1.5 * e_base, 2e-2), (e_got, e_base)
+    assert frac <= 5e-3, frac
+    if masked and shift == 0 and H >= 32:                    # transparent windows: exactly x
+        xb = rt.to_nchw(f).float().cpu()
+        assert torch.equal(got[:, :, 8:H // 2, 8:W // 2], xb[:, :, 8:H // 2, 8:W // 2])
