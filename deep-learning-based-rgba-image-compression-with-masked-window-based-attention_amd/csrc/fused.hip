@@ -45,7 +45,12 @@ struct RuArgsDev {
 
 __device__ __forceinline__ float ru_gelu(float v) { return gelu_fast(v); }   // bf16 outputs
 
-template <int C, int CH, int TY, int TX, int OCC>
+// RB = 0: ResidualUnit (GELU after each conv, GELU after the residual add);
+// RB = 1: the alpha codec's ResBlock (AutoEncoderMask_Journal.py:96-110: ReLU, ReLU, + x).
+template <int RB>
+__device__ __forceinline__ float ru_act(float v) { return RB ? fmaxf(v, 0.0f) : ru_gelu(v); }
+
+template <int C, int CH, int TY, int TX, int OCC, int RB = 0>
 __global__ void __launch_bounds__(256, OCC) ru_fused_kernel(const RuArgsDev args) {
   // TY x TX output tile, (TY+2) x (TX+2) halo; 8x16 halves the weight traffic per pixel
   // (every tile streams all three weight matrices once) at 2 workgroups per CU
@@ -195,7 +200,7 @@ __global__ void __launch_bounds__(256, OCC) ru_fused_kernel(const RuArgsDev args
         const int n = j * 16 + fq * 4;
         float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = xin[i] ? ru_gelu(acc[j][i][r] + g.b1[n + r]) : 0.0f;
+        for (int r = 0; r < 4; ++r) v[r] = xin[i] ? ru_act<RB>(acc[j][i][r] + g.b1[n + r]) : 0.0f;
         Elem<bf16_t>::st4(reinterpret_cast<bf16_t*>(&T1[hp * TROW + n * 2]), v);
       }
     }
@@ -257,7 +262,7 @@ __global__ void __launch_bounds__(256, OCC) ru_fused_kernel(const RuArgsDev args
         const int n = (wn * NJ + j) * 16 + fq * 4;
         float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = ru_gelu(acc[j][i][r] + g.b2[n + r]);
+        for (int r = 0; r < 4; ++r) v[r] = ru_act<RB>(acc[j][i][r] + g.b2[n + r]);
         Elem<bf16_t>::st4(reinterpret_cast<bf16_t*>(&T2[p * TROW + n * 2]), v);
       }
     }
@@ -307,9 +312,178 @@ __global__ void __launch_bounds__(256, OCC) ru_fused_kernel(const RuArgsDev args
         const int n = (wn * NJ + j) * 16 + fq * 4;
         float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = ru_gelu(acc[j][i][r] + g.b3[n + r] + res[j][r]);
+        for (int r = 0; r < 4; ++r) {
+          const float t = acc[j][i][r] + g.b3[n + r] + res[j][r];
+          v[r] = RB ? t : ru_gelu(t);
+        }
         Elem<bf16_t>::st4(orow + n, v);
       }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// C = 80 bottleneck (CH = 40): the latent-resolution ResidualUnits of the ws-4 attention
+// blocks (M = 80) and the alpha codec's 80-channel ResBlocks.  Three small GEMMs per 8x8
+// tile -- every weight matrix fits in LDS at once, so it is staged once per workgroup from
+// host-built fragment-major packs (1 KiB per 16 rows x 32 k, zero padded):
+//   stage 1: T1 = act(W1 x + b1) on the 10x10 halo, 48 rows (40 real) x K 96 (80 real)
+//   stage 2: T2 = act(W2 (*) T1 + b2), 48 rows x K 9 taps x 64 (40 real)
+//   stage 3: y  = [GELU](W3 T2 + b3 + x), 80 rows x K 64 (40 real)
+// T1 / T2 pixels are 128-B rows (64 channels, 40..63 zero), chunk c at slot c ^ (p & 7).
+// LDS 73 KiB weights + 22 KiB maps: one workgroup per CU, 4 waves; per wave 18 + 54 + 10
+// MFMAs.  Three launches (and two HBM round trips of the 40-channel maps) become one.
+namespace rus {
+constexpr int W1F = 9, W2F = 54, W3F = 10;            // fragments per matrix
+constexpr int HY = 10, HX = 10, NH = 100, NHP = 112;  // halo pixels (7 fragments)
+}  // namespace rus
+
+template <int RB>
+__global__ void __launch_bounds__(256, 1) ru_small_kernel(const RuArgsDev args) {
+  using namespace rus;
+  __shared__ __attribute__((aligned(16))) uint4 Ws[(W1F + W2F + W3F) * 64];
+  __shared__ __attribute__((aligned(16))) uint4 T1[NHP * 8];
+  __shared__ __attribute__((aligned(16))) uint4 T2[64 * 8];
+  __shared__ float bs[48 + 48 + 80];
+  const RuGroup& g = args.g[blockIdx.z];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = lane & 15, q = lane >> 4;
+  const int tx_n = args.W / 8, ty_n = args.H / 8;
+  int t = blockIdx.x;
+  const int tx = t % tx_n; t /= tx_n;
+  const int ty = t % ty_n;
+  const int b = t / ty_n;
+  const int y0 = ty * 8, x0 = tx * 8;
+
+  // weights: the three packs are contiguous per matrix (w1, w2, w3)
+  for (int e = tid; e < (W1F + W2F + W3F) * 64; e += 256) {
+    const uint4* src = e < W1F * 64 ? reinterpret_cast<const uint4*>(g.w1) + e
+                     : e < (W1F + W2F) * 64 ? reinterpret_cast<const uint4*>(g.w2) + (e - W1F * 64)
+                     : reinterpret_cast<const uint4*>(g.w3) + (e - (W1F + W2F) * 64);
+    Ws[e] = *src;
+  }
+  for (int e = tid; e < 48 + 48 + 80; e += 256)
+    bs[e] = e < 48 ? g.b1[e] : e < 96 ? g.b2[e - 48] : g.b3[e - 96];
+  // zero channels 48..63 (chunks 6, 7) of T1 / T2: the stage-2 / stage-3 K padding
+  for (int e = tid; e < (NHP + 64) * 2; e += 256) {
+    const int p = e >> 1, c = 6 + (e & 1);
+    if (p < NHP) T1[p * 8 + (c ^ (p & 7))] = make_uint4(0, 0, 0, 0);
+    else T2[(p - NHP) * 8 + (c ^ ((p - NHP) & 7))] = make_uint4(0, 0, 0, 0);
+  }
+  // stage-1 input fragments straight from HBM: halo pixel 16f + n, channels 32ks + 8q
+  constexpr int F1 = 2;                                  // fragments w, w + 4 (< 7)
+  uint4 xb[F1][3];
+  bool xin[F1];
+#pragma unroll
+  for (int i = 0; i < F1; ++i) {
+    const int hp = 16 * (wave + 4 * i) + n;
+    const int hy = hp / HX, hx = hp - hy * HX;
+    const int iy = y0 + hy - 1, ix = x0 + hx - 1;
+    xin[i] = hp < NH && iy >= 0 && iy < args.H && ix >= 0 && ix < args.W;
+    const bf16_t* row = g.x + ((long long)(b * args.H + (xin[i] ? iy : 0)) * args.W +
+                               (xin[i] ? ix : 0)) * g.ldx;
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks) {
+      const int c8 = 4 * ks + q;                         // 8-channel chunk (10 real)
+      xb[i][ks] = (xin[i] && c8 < 10) ? *reinterpret_cast<const uint4*>(row + 8 * c8)
+                                      : make_uint4(0, 0, 0, 0);
+    }
+  }
+  __syncthreads();
+
+  // ================= stage 1
+  {
+    f32x4 acc[3][F1];
+#pragma unroll
+    for (int tt = 0; tt < 3; ++tt)
+#pragma unroll
+      for (int i = 0; i < F1; ++i) acc[tt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 3; ++ks)
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt) {
+        const uint4 a = Ws[(tt * 3 + ks) * 64 + lane];
+#pragma unroll
+        for (int i = 0; i < F1; ++i)
+          if (wave + 4 * i < 7) mma_step<bf16_t>(acc[tt][i], a, xb[i][ks]);
+      }
+#pragma unroll
+    for (int i = 0; i < F1; ++i) {
+      const int hp = 16 * (wave + 4 * i) + n;
+      if (wave + 4 * i >= 7) continue;
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt) {
+        const int c0 = 16 * tt + 4 * q;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = xin[i] ? ru_act<RB>(acc[tt][i][r] + bs[c0 + r]) : 0.0f;
+        *reinterpret_cast<uint2*>(reinterpret_cast<unsigned char*>(T1) + hp * 128 +
+                                  (((c0 >> 3) ^ (hp & 7)) << 4) + 2 * (c0 & 7)) =
+            make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      }
+    }
+  }
+  __syncthreads();
+
+  // ================= stage 2 (wave w: output pixels 16w .. 16w+15 = rows 2w, 2w+1)
+  const int p = 16 * wave + n, py = p >> 3, px = p & 7;
+  {
+    f32x4 acc[3];
+#pragma unroll
+    for (int tt = 0; tt < 3; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < 18; ++kk) {
+      const int tap = kk >> 1, c8 = 4 * (kk & 1) + q;
+      const int hp = (py + tap / 3) * HX + px + tap % 3;
+      const uint4 bv = T1[hp * 8 + (c8 ^ (hp & 7))];
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt)
+        mma_step<bf16_t>(acc[tt], Ws[(W1F + tt * 18 + kk) * 64 + lane], bv);
+    }
+#pragma unroll
+    for (int tt = 0; tt < 3; ++tt) {
+      const int c0 = 16 * tt + 4 * q;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = ru_act<RB>(acc[tt][r] + bs[48 + c0 + r]);
+      *reinterpret_cast<uint2*>(reinterpret_cast<unsigned char*>(T2) + p * 128 +
+                                (((c0 >> 3) ^ (p & 7)) << 4) + 2 * (c0 & 7)) =
+          make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+    }
+  }
+  __syncthreads();                                       // (T2 rows are wave-private: a
+                                                         //  wave reads only its own pixels)
+  // ================= stage 3: y = [GELU](W3 T2 + b3 + x)
+  {
+    f32x4 acc[5];
+#pragma unroll
+    for (int tt = 0; tt < 5; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c8 = 4 * ks + q;
+      const uint4 bv = T2[p * 8 + (c8 ^ (p & 7))];
+#pragma unroll
+      for (int tt = 0; tt < 5; ++tt)
+        mma_step<bf16_t>(acc[tt], Ws[(W1F + W2F + tt * 2 + ks) * 64 + lane], bv);
+    }
+    const int gy = y0 + py, gx = x0 + px;
+    const long long pix = (long long)(b * args.H + gy) * args.W + gx;
+    const bf16_t* xr = g.x + pix * g.ldx;
+    bf16_t* orow = g.out + pix * g.ldo;
+    float res[5][4];
+#pragma unroll
+    for (int tt = 0; tt < 5; ++tt) Elem<bf16_t>::ld4(xr + 16 * tt + 4 * q, res[tt]);
+#pragma unroll
+    for (int tt = 0; tt < 5; ++tt) {
+      const int c0 = 16 * tt + 4 * q;
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float t3 = acc[tt][r] + bs[96 + c0 + r] + res[tt][r];
+        v[r] = RB ? t3 : ru_gelu(t3);
+      }
+      Elem<bf16_t>::st4(orow + c0, v);
     }
   }
 }
@@ -319,10 +493,16 @@ __global__ void __launch_bounds__(256, OCC) ru_fused_kernel(const RuArgsDev args
 using namespace rgbac;
 
 extern "C" int rgbac_residual_unit(const rgbac_ru_args* args, int ngroups, void* stream) {
+  return rgbac_residual_unit_ex(args, ngroups, 0, stream);
+}
+
+extern "C" int rgbac_residual_unit_ex(const rgbac_ru_args* args, int ngroups, int kind,
+                                      void* stream) {
   RGBAC_REQUIRE(args != nullptr && ngroups >= 1 && ngroups <= kRuMaxGroups, "groups");
   const rgbac_ru_args* a = args;
   RGBAC_REQUIRE(a->dtype == RGBAC_BF16, "the fused residual unit is bf16 only");
-  RGBAC_REQUIRE(a->channels == 192, "fused residual unit supports C = 192");
+  RGBAC_REQUIRE(kind == 0 || kind == 1, "kind: 0 = ResidualUnit, 1 = ResBlock");
+  RGBAC_REQUIRE(a->channels == 192 || a->channels == 80, "fused units support C = 192 or 80");
   RGBAC_REQUIRE(a->batch > 0 && a->h > 0 && a->w > 0 && a->h % 8 == 0 && a->w % 8 == 0,
                 "H and W must be positive multiples of 8");
   RuArgsDev d{};
@@ -334,11 +514,12 @@ extern "C" int rgbac_residual_unit(const rgbac_ru_args* args, int ngroups, void*
     RGBAC_REQUIRE(q->x && q->out && q->w1 && q->w2 && q->w3 && q->b1 && q->b2 && q->b3,
                   "null pointer");
     RGBAC_REQUIRE(q->x != q->out, "out must not alias x (the halo is read by other tiles)");
-    RGBAC_REQUIRE(q->x_ldc >= 192 && q->x_ldc % 8 == 0 && q->out_ldc >= 192 && q->out_ldc % 4 == 0,
-                  "strides");
-    RGBAC_REQUIRE(q->w1_kpad >= 192 && q->w2_kpad >= 896 && q->w3_kpad >= 96 &&
-                      q->w1_kpad % 8 == 0 && q->w2_kpad % 8 == 0 && q->w3_kpad % 8 == 0,
-                  "packed weight k_pad (w1 >= 192, w2 >= 896 zero-padded, w3 >= 96)");
+    RGBAC_REQUIRE(q->x_ldc >= a->channels && q->x_ldc % 8 == 0 && q->out_ldc >= a->channels &&
+                      q->out_ldc % 4 == 0, "strides");
+    if (a->channels == 192)
+      RGBAC_REQUIRE(q->w1_kpad >= 192 && q->w2_kpad >= 896 && q->w3_kpad >= 96 &&
+                        q->w1_kpad % 8 == 0 && q->w2_kpad % 8 == 0 && q->w3_kpad % 8 == 0,
+                    "packed weight k_pad (w1 >= 192, w2 >= 896 zero-padded, w3 >= 96)");
     RGBAC_REQUIRE(((uintptr_t)q->x % 16) == 0 && ((uintptr_t)q->w1 % 16) == 0 &&
                       ((uintptr_t)q->w2 % 16) == 0 && ((uintptr_t)q->w3 % 16) == 0,
                   "16-byte alignment");
@@ -350,6 +531,13 @@ extern "C" int rgbac_residual_unit(const rgbac_ru_args* args, int ngroups, void*
     g.out = (bf16_t*)q->out; g.ldo = q->out_ldc;
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (a->channels == 80) {
+    const long long tiles = (long long)a->batch * (a->h / 8) * (a->w / 8);
+    RGBAC_REQUIRE(tiles < (1ll << 31), "too many tiles");
+    if (kind) hipLaunchKernelGGL(ru_small_kernel<1>, dim3((unsigned)tiles, 1, ngroups), dim3(256), 0, st, d);
+    else hipLaunchKernelGGL(ru_small_kernel<0>, dim3((unsigned)tiles, 1, ngroups), dim3(256), 0, st, d);
+    return check_launch("ru_small_kernel");
+  }
   static const int wide_env = [] {
     const char* e = getenv("RGBAC_RU_TILE");
     return (e && e[0] == '8') ? 0 : 1;              // RGBAC_RU_TILE=8: the 8x8 tile
@@ -357,13 +545,17 @@ extern "C" int rgbac_residual_unit(const rgbac_ru_args* args, int ngroups, void*
   if (wide_env && a->w % 16 == 0) {
     const long long tiles = (long long)a->batch * (a->h / 8) * (a->w / 16);
     RGBAC_REQUIRE(tiles < (1ll << 31), "too many tiles");
-    hipLaunchKernelGGL((ru_fused_kernel<192, 96, 8, 16, 2>), dim3((unsigned)tiles, 1, ngroups),
-                       dim3(256), 0, st, d);
+    if (kind) hipLaunchKernelGGL((ru_fused_kernel<192, 96, 8, 16, 2, 1>), dim3((unsigned)tiles, 1, ngroups),
+                                 dim3(256), 0, st, d);
+    else hipLaunchKernelGGL((ru_fused_kernel<192, 96, 8, 16, 2>), dim3((unsigned)tiles, 1, ngroups),
+                            dim3(256), 0, st, d);
   } else {
     const long long tiles = (long long)a->batch * (a->h / 8) * (a->w / 8);
     RGBAC_REQUIRE(tiles < (1ll << 31), "too many tiles");
-    hipLaunchKernelGGL((ru_fused_kernel<192, 96, 8, 8, 3>), dim3((unsigned)tiles, 1, ngroups),
-                       dim3(256), 0, st, d);
+    if (kind) hipLaunchKernelGGL((ru_fused_kernel<192, 96, 8, 8, 3, 1>), dim3((unsigned)tiles, 1, ngroups),
+                                 dim3(256), 0, st, d);
+    else hipLaunchKernelGGL((ru_fused_kernel<192, 96, 8, 8, 3>), dim3((unsigned)tiles, 1, ngroups),
+                            dim3(256), 0, st, d);
   }
   return check_launch("ru_fused_kernel");
 }

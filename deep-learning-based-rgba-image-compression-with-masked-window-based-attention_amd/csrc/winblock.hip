@@ -8,8 +8,8 @@
 // One launch replaces three (qkv 1x1 GEMM -> HBM, attention core, proj GEMM + MASKSEL):
 // the 576-channel qkv tensor (37.7 MB at 64x64 B8) never leaves the chip.
 //
-// One workgroup = 2 windows = 128 tokens, 4 waves of 32 tokens (a wave's tokens lie in one
-// window).  Per head pair (48 qkv channels of each kind):
+// One workgroup = 2 windows = 128 tokens, 8 waves of 16 tokens (or 4 of 32; a wave's tokens
+// lie in one window).  Per head pair (48 qkv channels of each kind):
 //   QKV   q^T, k^T = Wq|Wk (LDS) x X^T (registers); v = X x Wv^T   -> LDS (bf16, padded to 32)
 //   per head:  S^T = K Q^T (keys on the MFMA row axis), + B_rel (LDS table) + shift mask,
 //              softmax (rows in 4 lanes: two xor-shuffles) -> P (wave-private LDS),
@@ -20,30 +20,33 @@
 // streamed into LDS by LDS-DMA one pair / head ahead, waited on with counted vmcnt.
 //
 // MFMA v_mfma_f32_16x16x32_bf16 throughout (acc[row][col] += A[row][k] B[col][k]);
-// per wave: 4 x 108 (QKV) + 8 x (8 + 8 + 24) = 752 MFMAs per 2 windows.
+// per 32 tokens: 4 x 108 (QKV) + 8 x (8 + 8 + 24) = 752 MFMAs.  Softmax on exp2 with log2 e
+// folded into the q scale and the bias tables.
 //
 // LDS (bytes): WQ 54 KiB | WP 2 x 12 KiB | QK [2 heads][q,k][128 tok][64 B] 32 KiB |
-// VT [2 heads][32 ch][128 tok] 16 KiB | P/O [4 waves][4 KiB] | bias table 7200 |
-// qkv / proj biases 3072  -> 155,936 B: one workgroup per CU.
+// VT [2 heads][32 ch][128 tok] 16 KiB | P/O [4 waves][4 KiB] | relative-position bias
+// [table, table - 100 (the shift mask folded in)][8 heads][225] fp32 (head-major: the
+// per-lane gathers spread over the banks) | proj bias -> 161,616 B: one workgroup per CU.
 // Swizzles (all conflict-free for the ds_read_b128 lane groups): 64-B token rows
 // chunk ^ ((tok >> 1) & 3); V^T 256-B rows chunk ^ (ch & 15); P 128-B rows chunk ^ (q & 7).
+#include <cstdlib>
+
 #include "common.h"
 
 namespace rgbac {
 
 namespace wb {
-constexpr int WS = 8, NT = 64, C = 192, HEADS = 8, DH = 24, TOK = 128, NTH = 256;
+constexpr int WS = 8, NT = 64, C = 192, HEADS = 8, DH = 24, TOK = 128;
 constexpr int WQF = 54;                                // qkv fragments per head pair
-constexpr int WQF_W = 14;                              // DMA pieces per wave (54 + 2 repeats)
 constexpr int WPF = 12;                                // proj fragments per head
 constexpr int L_WQ = 0;
 constexpr int L_WP = L_WQ + WQF * 1024;                // 55296
 constexpr int L_QK = L_WP + 2 * WPF * 1024;            // 79872
 constexpr int L_VT = L_QK + 2 * 2 * TOK * 64;          // 112640
 constexpr int L_P = L_VT + 2 * 32 * TOK * 2;           // 129024
-constexpr int L_TB = L_P + 4 * 4096;                   // 145408
-constexpr int L_BQ = L_TB + 225 * 8 * 4;               // 152608: bqkv[576], bproj[192]
-constexpr int LDS = L_BQ + (576 + 192) * 4;            // 155680
+constexpr int L_TB = L_P + 4 * 4096;                   // 145408: bias [2][8 heads][225]
+constexpr int L_BQ = L_TB + 2 * 8 * 225 * 4;           // 159808: bproj[192]
+constexpr int LDS = L_BQ + 192 * 4;                    // 160576
 }  // namespace wb
 
 struct WinBlockArgs {
@@ -76,8 +79,15 @@ __device__ __forceinline__ void wb_wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-__global__ void __launch_bounds__(wb::NTH, 1) winblock_kernel(const WinBlockArgs a) {
+// NQT 16-token tiles per wave: NQT = 1 -> 8 waves (2 per SIMD: one wave's softmax VALU
+// overlaps the other's MFMAs), NQT = 2 -> 4 waves (twice the weight-fragment reuse).
+template <int NQT>
+__global__ void __launch_bounds__(64 * 8 / NQT, 1) winblock_kernel(const WinBlockArgs a) {
   using namespace wb;
+  constexpr int NWAVE = 8 / NQT, NTHR = 64 * NWAVE, TPW = 16 * NQT;
+  constexpr int WQ_W = (WQF + NWAVE - 1) / NWAVE;      // DMA pieces per wave (7 or 14)
+  constexpr int WP_W = (WPF + NWAVE - 1) / NWAVE;      // (2 or 3)
+  constexpr float LOG2E = 1.4426950408889634f;
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   __shared__ int pix_s[TOK];
   __shared__ int rid_s[TOK];
@@ -90,6 +100,9 @@ __global__ void __launch_bounds__(wb::NTH, 1) winblock_kernel(const WinBlockArgs
   const int nwx = W / WS, nwy = H / WS;
   const int total = a.batch * nwx * nwy;
   const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) void*)sm;
+  const int tok0 = TPW * w;                            // this wave's first token (of 128)
+  const int win = tok0 >> 6;                           // its window (0 or 1)
+  const int lq0 = tok0 & 63;                           // ... and first query within it
 
   // ---- window gather: token -> pixel (cyclic shift folded in), shifted-frame region id
   if (tid < 2) act_s[tid] = a.masked ? 0 : 1;
@@ -113,11 +126,10 @@ __global__ void __launch_bounds__(wb::NTH, 1) winblock_kernel(const WinBlockArgs
     rid_s[tid] = rid;
   }
   __syncthreads();
-  const int win = w >> 1;
-  const bool act = act_s[win] != 0 && pix_s[32 * w] >= 0;       // wave-uniform
+  const bool act = act_s[win] != 0 && pix_s[tok0] >= 0;         // wave-uniform
   if (act_s[0] == 0 && act_s[1] == 0) {
     // both windows transparent: out = x on their tokens
-    for (int e = tid; e < TOK * (C / 8); e += NTH) {
+    for (int e = tid; e < TOK * (C / 8); e += NTHR) {
       const int t = e / (C / 8), c8 = e - t * (C / 8);
       const int pix = pix_s[t];
       if (pix >= 0)
@@ -127,19 +139,21 @@ __global__ void __launch_bounds__(wb::NTH, 1) winblock_kernel(const WinBlockArgs
     return;
   }
 
-  // ---- weight streams: pair p's qkv fragments (14 DMA pieces per wave), head h's proj (3)
+  // ---- weight streams: pair p's qkv fragments, head h's proj fragments (pieces past the
+  // end repeat the last one: same bytes to the same place, so every wave issues as many)
   auto dma_wq = [&](int p) {
 #pragma unroll
-    for (int i = 0; i < WQF_W; ++i) {
-      int f = w + 4 * i;
-      if (f >= WQF) f = WQF - 1;                        // repeat of the last piece: same bytes
+    for (int i = 0; i < WQ_W; ++i) {
+      int f = w + NWAVE * i;
+      if (f >= WQF) f = WQF - 1;
       wb_dma16(a.wq + ((size_t)(p * WQF + f) * 64 + lane) * 8, lds0 + L_WQ + f * 1024);
     }
   };
   auto dma_wp = [&](int h) {
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const int f = w + 4 * i;
+    for (int i = 0; i < WP_W; ++i) {
+      int f = w + NWAVE * i;
+      if (f >= WPF) f = WPF - 1;
       wb_dma16(a.wp + ((size_t)(h * WPF + f) * 64 + lane) * 8,
                lds0 + L_WP + (h & 1) * WPF * 1024 + f * 1024);
     }
@@ -147,26 +161,31 @@ __global__ void __launch_bounds__(wb::NTH, 1) winblock_kernel(const WinBlockArgs
   dma_wq(0);
   dma_wp(0);
 
-  // ---- tables and zero padding (q/k channels 24..31: chunk 3; V^T rows 24..31)
+  // ---- tables (in log2 units: softmax runs on exp2) and zero padding (q/k channels 24..31:
+  // chunk 3; V^T rows 24..31)
   float* tb = reinterpret_cast<float*>(sm + L_TB);
-  for (int e = tid; e < 225 * 8; e += NTH) tb[e] = a.table[e];
+  for (int e = tid; e < 225 * 8; e += NTHR) {          // table [225][8] -> [var][8][225]
+    const int idx = e >> 3, hd = e & 7;
+    const float v = a.table[e];
+    tb[hd * 225 + idx] = v * LOG2E;
+    tb[8 * 225 + hd * 225 + idx] = (v + -100.0f) * LOG2E;   // the shift mask's -100 folded in
+  }
   float* bq = reinterpret_cast<float*>(sm + L_BQ);
-  for (int e = tid; e < 576; e += NTH) bq[e] = a.bqkv[e];
-  for (int e = tid; e < 192; e += NTH) bq[576 + e] = a.bproj[e];
-  for (int e = tid; e < 2 * 2 * TOK; e += NTH) {
+  for (int e = tid; e < 192; e += NTHR) bq[e] = a.bproj[e];
+  for (int e = tid; e < 2 * 2 * TOK; e += NTHR) {
     const int t = e & (TOK - 1);
     *reinterpret_cast<uint4*>(sm + L_QK + e * 64 + ((3 ^ ((t >> 1) & 3)) << 4)) = make_uint4(0, 0, 0, 0);
   }
-  for (int e = tid; e < 2 * 8 * 16; e += NTH) {        // [head][row 24..31][16 chunks]
+  for (int e = tid; e < 2 * 8 * 16; e += NTHR) {       // [head][row 24..31][16 chunks]
     const int hh = e >> 7, r = 24 + ((e >> 4) & 7), c = e & 15;
     *reinterpret_cast<uint4*>(sm + L_VT + (hh * 32 + r) * 256 + (c << 4)) = make_uint4(0, 0, 0, 0);
   }
 
-  // ---- this wave's x tile as MFMA fragments: X[j][ks] = tokens 32w+16j+n, k-chunk 4ks+qq
-  uint4 X[2][6];
+  // ---- this wave's x tile as MFMA fragments: X[j][ks] = tokens tok0+16j+n, k-chunk 4ks+qq
+  uint4 X[NQT][6];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int pix = pix_s[32 * w + 16 * j + n];
+  for (int j = 0; j < NQT; ++j) {
+    const int pix = pix_s[tok0 + 16 * j + n];
     const bf16_t* row = a.x + (long long)(pix < 0 ? 0 : pix) * a.ldx;
 #pragma unroll
     for (int ks = 0; ks < 6; ++ks)
@@ -174,13 +193,13 @@ __global__ void __launch_bounds__(wb::NTH, 1) winblock_kernel(const WinBlockArgs
                          : *reinterpret_cast<const uint4*>(row + 32 * ks + 8 * qq);
   }
 
-  // ---- per-lane relative-position-bias table offsets and shift-mask bits, head-invariant:
-  // S element (qt, kt, r) = (query 32(w&1)+16qt+n, key 16kt+4qq+r) of the window
-  int toff[2][4][4];
-  uint32_t mbits = 0;
+  // ---- per-lane relative-position-bias offsets (head-invariant; +900 h per head), into the
+  // "- 100" copy where the shift mask separates query and key:
+  // S element (qt, kt, r) = (query lq0+16qt+n, key 16kt+4qq+r) of the window
+  int toff[NQT][4][4];
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int iq = 32 * (w & 1) + 16 * qt + n;
+  for (int qt = 0; qt < NQT; ++qt) {
+    const int iq = lq0 + 16 * qt + n;
     const int qrid = rid_s[64 * win + iq];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
@@ -188,32 +207,34 @@ __global__ void __launch_bounds__(wb::NTH, 1) winblock_kernel(const WinBlockArgs
       for (int r = 0; r < 4; ++r) {
         const int jk = 16 * kt + 4 * qq + r;
         const int idx = ((iq >> 3) - (jk >> 3) + 7) * 15 + ((iq & 7) - (jk & 7) + 7);
-        toff[qt][kt][r] = L_TB + idx * 32;
-        if (shift > 0 && rid_s[64 * win + jk] != qrid) mbits |= 1u << (qt * 16 + kt * 4 + r);
+        const bool cut = shift > 0 && rid_s[64 * win + jk] != qrid;
+        toff[qt][kt][r] = L_TB + (cut ? 8 * 225 * 4 : 0) + idx * 4;
       }
   }
 
-  f32x4 acc[12][2];                                    // proj output: [16-ch tile][token tile]
+  f32x4 acc[12][NQT];                                  // proj output: [16-ch tile][token tile]
 #pragma unroll
-  for (int m = 0; m < 12; ++m) acc[m][0] = acc[m][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int m = 0; m < 12; ++m)
+#pragma unroll
+    for (int j = 0; j < NQT; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // LDS byte offsets of this lane's fragment reads
   const int swz64 = ((qq ^ ((n >> 1) & 3)) << 4);      // 64-B token rows, base % 16 == 0
+  const float qscale = a.scale * LOG2E;                // q * scale, in log2 units
   wb_wait_vm<0>();
   __syncthreads();
 
   for (int p = 0; p < 4; ++p) {
     if (p > 0) {
-      wb_wait_vm<3>();                                 // WQ(p) landed (WP(2p) may be in flight)
+      wb_wait_vm<WP_W>();                              // WQ(p) landed (WP(2p) may be in flight)
       __syncthreads();
     }
-    // ================= QKV of heads 2p, 2p+1 for this wave's 32 tokens
+    // ================= QKV of heads 2p, 2p+1 for this wave's tokens
     if (act) {
-      f32x4 aq[3][2], ak[3][2], av[2][3];
+      f32x4 aq[3][NQT], ak[3][NQT], av[NQT][3];
 #pragma unroll
       for (int t = 0; t < 3; ++t)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < NQT; ++j)
           aq[t][j] = ak[t][j] = av[j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 6; ++ks) {
@@ -227,7 +248,7 @@ __global__ void __launch_bounds__(wb::NTH, 1) winblock_kernel(const WinBlockArgs
 #pragma unroll
         for (int t = 0; t < 3; ++t)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
+          for (int j = 0; j < NQT; ++j) {
             mma_step<bf16_t>(aq[t][j], fq[t], X[j][ks]);
             mma_step<bf16_t>(ak[t][j], fk[t], X[j][ks]);
             mma_step<bf16_t>(av[j][t], X[j][ks], fv[t]);
@@ -238,28 +259,26 @@ __global__ void __launch_bounds__(wb::NTH, 1) winblock_kernel(const WinBlockArgs
       for (int t = 0; t < 3; ++t) {
         const int cp = 16 * t + 4 * qq;
         const int hh = cp >= DH ? 1 : 0, hc = cp - DH * hh;   // 4 channels, one head
+        const float4 bq4 = *reinterpret_cast<const float4*>(a.bqkv + 48 * p + cp);
+        const float4 bk4 = *reinterpret_cast<const float4*>(a.bqkv + 192 + 48 * p + cp);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int tok = 32 * w + 16 * j + n;
-          float vq[4], vk[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            vq[r] = (aq[t][j][r] + bq[48 * p + cp + r]) * a.scale;
-            vk[r] = ak[t][j][r] + bq[192 + 48 * p + cp + r];
-          }
+        for (int j = 0; j < NQT; ++j) {
+          const int tok = tok0 + 16 * j + n;
           const int off = tok * 64 + (((hc >> 3) ^ ((tok >> 1) & 3)) << 4) + 2 * (hc & 7);
-          *reinterpret_cast<uint2*>(sm + L_QK + (hh * 2 + 0) * TOK * 64 + off) =
-              make_uint2(pack_bf16x2(vq[0], vq[1]), pack_bf16x2(vq[2], vq[3]));
-          *reinterpret_cast<uint2*>(sm + L_QK + (hh * 2 + 1) * TOK * 64 + off) =
-              make_uint2(pack_bf16x2(vk[0], vk[1]), pack_bf16x2(vk[2], vk[3]));
+          *reinterpret_cast<uint2*>(sm + L_QK + (hh * 2 + 0) * TOK * 64 + off) = make_uint2(
+              pack_bf16x2((aq[t][j][0] + bq4.x) * qscale, (aq[t][j][1] + bq4.y) * qscale),
+              pack_bf16x2((aq[t][j][2] + bq4.z) * qscale, (aq[t][j][3] + bq4.w) * qscale));
+          *reinterpret_cast<uint2*>(sm + L_QK + (hh * 2 + 1) * TOK * 64 + off) = make_uint2(
+              pack_bf16x2(ak[t][j][0] + bk4.x, ak[t][j][1] + bk4.y),
+              pack_bf16x2(ak[t][j][2] + bk4.z, ak[t][j][3] + bk4.w));
         }
         // v: D[token][channel] -> lane holds tokens 16j+4qq+r of channel 16t+n
         const int cv = 16 * t + n;
         const int vh = cv >= DH ? 1 : 0, vc = cv - DH * vh;
-        const float bv = bq[384 + 48 * p + cv];
+        const float bv = a.bqkv[384 + 48 * p + cv];
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int tok = 32 * w + 16 * j + 4 * qq;
+        for (int j = 0; j < NQT; ++j) {
+          const int tok = tok0 + 16 * j + 4 * qq;
           const int off = (vh * 32 + vc) * 256 + (((tok >> 3) ^ (vc & 15)) << 4) + 2 * (tok & 7);
           *reinterpret_cast<uint2*>(sm + L_VT + off) =
               make_uint2(pack_bf16x2(av[j][t][0] + bv, av[j][t][1] + bv),
@@ -273,36 +292,36 @@ __global__ void __launch_bounds__(wb::NTH, 1) winblock_kernel(const WinBlockArgs
 #pragma unroll
     for (int hh = 0; hh < 2; ++hh) {
       const int h = 2 * p + hh;
-      unsigned char* const Pw = sm + L_P + w * 4096;   // this wave's P (32 x 64), then O
+      unsigned char* const Pw = sm + L_P + w * (2048 * NQT);   // this wave's P, then O
       if (act) {
-        // ---- S^T = K Q^T: keys (rows) of this window x this wave's 32 queries
-        f32x4 s[2][4];
-        uint4 fqv[2], fkv[4];
+        // ---- S^T = K Q^T: keys (rows) of this window x this wave's queries
+        f32x4 s[NQT][4];
+        uint4 fqv[NQT], fkv[4];
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
+        for (int qt = 0; qt < NQT; ++qt)
           fqv[qt] = *reinterpret_cast<const uint4*>(
-              sm + L_QK + (hh * 2 + 0) * TOK * 64 + (32 * w + 16 * qt + n) * 64 + swz64);
+              sm + L_QK + (hh * 2 + 0) * TOK * 64 + (tok0 + 16 * qt + n) * 64 + swz64);
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt)
           fkv[kt] = *reinterpret_cast<const uint4*>(
               sm + L_QK + (hh * 2 + 1) * TOK * 64 + (64 * win + 16 * kt + n) * 64 + swz64);
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
+        for (int qt = 0; qt < NQT; ++qt)
 #pragma unroll
           for (int kt = 0; kt < 4; ++kt) {
             s[qt][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
             mma_step<bf16_t>(s[qt][kt], fkv[kt], fqv[qt]);
           }
-        // ---- + B_rel + shift mask, softmax over the 64 keys (lane + lanes ^16, ^32, ^48)
+        // ---- + B_rel + shift mask, softmax (exp2: log2 e folded into q and the tables)
+        // over the 64 keys (lane + lanes ^16, ^32, ^48)
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
+        for (int qt = 0; qt < NQT; ++qt) {
           float mx = -INFINITY;
 #pragma unroll
           for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              float v = s[qt][kt][r] + *reinterpret_cast<const float*>(sm + toff[qt][kt][r] + 4 * h);
-              if (mbits & (1u << (qt * 16 + kt * 4 + r))) v += -100.0f;
+              const float v = s[qt][kt][r] + *reinterpret_cast<const float*>(sm + toff[qt][kt][r] + 900 * h);
               s[qt][kt][r] = v;
               mx = fmaxf(mx, v);
             }
@@ -313,13 +332,13 @@ __global__ void __launch_bounds__(wb::NTH, 1) winblock_kernel(const WinBlockArgs
           for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-              const float ex = expf(s[qt][kt][r] - mx);
+              const float ex = __builtin_amdgcn_exp2f(s[qt][kt][r] - mx);
               s[qt][kt][r] = ex;
               sum += ex;
             }
           sum += __shfl_xor(sum, 16);
           sum += __shfl_xor(sum, 32);
-          const float inv = 1.0f / sum;
+          const float inv = __builtin_amdgcn_rcpf(sum);
           const int qi = 16 * qt + n;
 #pragma unroll
           for (int kt = 0; kt < 4; ++kt) {
@@ -330,12 +349,14 @@ __global__ void __launch_bounds__(wb::NTH, 1) winblock_kernel(const WinBlockArgs
           }
         }
         // ---- O^T = V^T P^T: head channels (rows, 24..31 zero) x this wave's queries
-        f32x4 o[2][2];
+        f32x4 o[2][NQT];
 #pragma unroll
-        for (int ct = 0; ct < 2; ++ct) o[ct][0] = o[ct][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int ct = 0; ct < 2; ++ct)
+#pragma unroll
+          for (int qt = 0; qt < NQT; ++qt) o[ct][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-          uint4 fa[2], fb[2];
+          uint4 fa[2], fb[NQT];
 #pragma unroll
           for (int ct = 0; ct < 2; ++ct) {
             const int ch = 16 * ct + n;
@@ -343,21 +364,21 @@ __global__ void __launch_bounds__(wb::NTH, 1) winblock_kernel(const WinBlockArgs
                 sm + L_VT + (hh * 32 + ch) * 256 + (((8 * win + 4 * ks + qq) ^ (ch & 15)) << 4));
           }
 #pragma unroll
-          for (int qt = 0; qt < 2; ++qt) {
+          for (int qt = 0; qt < NQT; ++qt) {
             const int qi = 16 * qt + n;
             fb[qt] = *reinterpret_cast<const uint4*>(Pw + qi * 128 + (((4 * ks + qq) ^ (qi & 7)) << 4));
           }
 #pragma unroll
           for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
-            for (int qt = 0; qt < 2; ++qt) mma_step<bf16_t>(o[ct][qt], fa[ct], fb[qt]);
+            for (int qt = 0; qt < NQT; ++qt) mma_step<bf16_t>(o[ct][qt], fa[ct], fb[qt]);
         }
         // O (token rows of 32 channels, bf16) over this wave's P: every P read above has
         // completed (its MFMAs produced o)
 #pragma unroll
         for (int ct = 0; ct < 2; ++ct)
 #pragma unroll
-          for (int qt = 0; qt < 2; ++qt) {
+          for (int qt = 0; qt < NQT; ++qt) {
             const int tok = 16 * qt + n, c0 = 16 * ct + 4 * qq;
             *reinterpret_cast<uint2*>(Pw + tok * 64 + (((c0 >> 3) ^ ((tok >> 1) & 3)) << 4) + 2 * (c0 & 7)) =
                 make_uint2(pack_bf16x2(o[ct][qt][0], o[ct][qt][1]),
@@ -365,32 +386,32 @@ __global__ void __launch_bounds__(wb::NTH, 1) winblock_kernel(const WinBlockArgs
           }
       }
       // ---- WP(h) landed everywhere (WQ(p+1), issued after it, may still be in flight)
-      if (hh == 0 && p < 3) wb_wait_vm<WQF_W>();
+      if (hh == 0 && p < 3) wb_wait_vm<WQ_W>();
       else wb_wait_vm<0>();
       __syncthreads();
       if (h < HEADS - 1) dma_wp(h + 1);                // buffer (h+1)&1: proj(h-1) is done
       if (act) {
         // ---- out^T += Wproj[:, head h] O^T
-        uint4 fo[2];
+        uint4 fo[NQT];
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt)
+        for (int qt = 0; qt < NQT; ++qt)
           fo[qt] = *reinterpret_cast<const uint4*>(Pw + (16 * qt + n) * 64 + swz64);
 #pragma unroll
         for (int m = 0; m < 12; ++m) {
           const uint4 fw = *reinterpret_cast<const uint4*>(
               sm + L_WP + (h & 1) * WPF * 1024 + m * 1024 + lane * 16);
 #pragma unroll
-          for (int qt = 0; qt < 2; ++qt) mma_step<bf16_t>(acc[m][qt], fw, fo[qt]);
+          for (int qt = 0; qt < NQT; ++qt) mma_step<bf16_t>(acc[m][qt], fw, fo[qt]);
         }
       }
     }
   }
 
   // ---- epilogue: out = x + proj + b (active window) or x (MASKSEL, :236-240)
-  const float* bp = bq + 576;
+  const float* bp = reinterpret_cast<const float*>(sm + L_BQ);
 #pragma unroll
-  for (int qt = 0; qt < 2; ++qt) {
-    const int pix = pix_s[32 * w + 16 * qt + n];
+  for (int qt = 0; qt < NQT; ++qt) {
+    const int pix = pix_s[tok0 + 16 * qt + n];
     if (pix < 0) continue;
     const bf16_t* xr = a.x + (long long)pix * a.ldx;
     bf16_t* orow = a.out + (long long)pix * a.ldo;
@@ -433,13 +454,21 @@ extern "C" int rgbac_winattn_block(int batch, int h, int w, int shift, int maske
   d.wq = reinterpret_cast<const bf16_t*>(wq_packed); d.bqkv = bqkv;
   d.wp = reinterpret_cast<const bf16_t*>(wp_packed); d.bproj = bproj; d.table = table;
   d.out = reinterpret_cast<bf16_t*>(out); d.ldo = ldo;
+  static const int nqt = [] {
+    const char* e = getenv("RGBAC_WINBLOCK_NQT");      // 1: 8 waves (default), 2: 4 waves
+    return e && atoi(e) == 2 ? 2 : 1;
+  }();
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(winblock_kernel),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(winblock_kernel<1>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, wb::LDS);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(winblock_kernel<2>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, wb::LDS);
     attr = true;
   }
-  hipLaunchKernelGGL(winblock_kernel, dim3((int)((windows + 1) / 2)), dim3(wb::NTH), wb::LDS,
-                     reinterpret_cast<hipStream_t>(stream), d);
+  const dim3 grid((int)((windows + 1) / 2));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (nqt == 2) hipLaunchKernelGGL(winblock_kernel<2>, grid, dim3(256), wb::LDS, st, d);
+  else hipLaunchKernelGGL(winblock_kernel<1>, grid, dim3(512), wb::LDS, st, d);
   return check_launch("winblock_kernel");
 }

@@ -113,6 +113,7 @@ SIGNATURES = {
     "rgbac_nchw_to_nhwc": [_I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP],
     "rgbac_nhwc_to_nchw": [_I32, _I32, _I32, _I32, _I32, _VP, _I64, _VP, _VP],
     "rgbac_residual_unit": [_VP, _I32, _VP],
+    "rgbac_residual_unit_ex": [_VP, _I32, _I32, _VP],
     "rgbac_stem_gdn": [_I32, _I32, _I32, _VP, _I64, _VP, _I32, _VP, _VP, _I32, _VP, _I32, _VP,
                        _I64, _VP],
     "rgbac_winattn_block": [_I32, _I32, _I32, _I32, _I32, _F, _VP, _I64, _VP, _VP, _VP, _VP, _VP,

@@ -43,39 +43,95 @@ FUSED = os.environ.get("RGBAC_FUSED_RU", "1") != "0"
 
 def _fused_ok(pairs):
     x = pairs[0][1]
-    return (FUSED and x.t.dtype == torch.bfloat16 and x.C == 192 and x.H % 8 == 0 and
-            x.W % 8 == 0 and len(pairs) <= 4)
+    return (FUSED and x.t.dtype == torch.bfloat16 and x.C in (192, 80) and x.H % 8 == 0 and
+            x.W % 8 == 0 and len(pairs) <= 4 and x.ldc % 8 == 0)
 
 
-def run_residual_units_fused(pairs):
-    """The same units as ONE rgbac_residual_unit launch (csrc/fused.hip): both
-    intermediates stay in LDS, one read of x and one write of y per pixel."""
-    x0 = pairs[0][1]
-    arr = (_lib.RuArgs * len(pairs))()
+def small_unit_packs(c1, c2, c3):
+    """Fragment-major bf16 packs of a C = 80 bottleneck (1x1 80->40, 3x3 40->40, 1x1 40->80)
+    for rgbac_residual_unit_ex: w1 [3][3][64][8], w2 [3][18][64][8], w3 [5][2][64][8] (16
+    rows x 32 k per fragment; lane l holds row 16t + l%16, k 32ks + 8(l/16) .. +8; zero
+    padded), biases fp32 [48], [48], [80].  Cached on conv1 per parameter version."""
+    ps = [c1.weight, c1.bias, c2.weight, c2.bias, c3.weight, c3.bias]
+    key = (rt.PARAM_GEN,) + tuple((t._version, t.data_ptr()) for t in ps)
+    ent = c1.__dict__.get("_rgbac_small_ru")
+    if ent is None or ent[0] != key:
+        with torch.no_grad():
+            dev = c1.weight.device
+            ar = lambda k: torch.arange(k, device=dev)
+
+            def pack(w, nt, nks, kfn):
+                # w: (rows, K) fp32 in the pack's k order; kfn: (ks, lane, e) -> k index
+                t, ks = ar(nt)[:, None, None, None], ar(nks)[None, :, None, None]
+                l, e = ar(64)[None, None, :, None], ar(8)[None, None, None, :]
+                row = 16 * t + (l & 15)
+                k = kfn(ks, l, e)
+                ok = (row < w.shape[0]) & (k >= 0) & (k < w.shape[1])
+                row, k, ok = torch.broadcast_tensors(row, k, ok)
+                v = w[row.clamp(max=w.shape[0] - 1), k.clamp(0, w.shape[1] - 1)]
+                return torch.where(ok, v, torch.zeros((), device=dev)).to(torch.bfloat16).contiguous()
+
+            w1 = c1.weight.float().reshape(40, 80)
+            p1 = pack(w1, 3, 3, lambda ks, l, e: 32 * ks + 8 * (l >> 4) + e)
+            # w2: k = tap * 64 + ci (ci < 40 real), k-step kk = 2 * tap + half
+            w2 = torch.zeros((40, 9, 64), device=dev)
+            w2[:, :, :40] = c2.weight.float().permute(0, 2, 3, 1).reshape(40, 9, 40)
+            p2 = pack(w2.reshape(40, 9 * 64), 3, 18, lambda ks, l, e: 32 * ks + 8 * (l >> 4) + e)
+            w3 = c3.weight.float().reshape(80, 40)
+            p3 = pack(w3, 5, 2, lambda ks, l, e: 32 * ks + 8 * (l >> 4) + e)
+            b1 = torch.zeros(48, device=dev)
+            b1[:40] = c1.bias.float()
+            b2 = torch.zeros(48, device=dev)
+            b2[:40] = c2.bias.float()
+            b3 = c3.bias.float().contiguous()
+        c1.__dict__["_rgbac_small_ru"] = (key, (p1, p2, p3, b1, b2, b3))
+        ent = c1.__dict__["_rgbac_small_ru"]
+    return ent[1]
+
+
+def run_bottlenecks_fused(units, kind):
+    """Bottleneck residual blocks [((conv1, conv2, conv3), x), ...] of one geometry as ONE
+    rgbac_residual_unit_ex launch (csrc/fused.hip; kind 0 = ResidualUnit, 1 = ResBlock):
+    both intermediates stay in LDS, one read of x and one write of y per pixel."""
+    x0 = units[0][1]
+    C = x0.C
+    arr = (_lib.RuArgs * len(units))()
     outs, keep = [], []
-    for i, (u, x) in enumerate(pairs):
-        segs = [(x.C, x.ldc)]
-        p1 = rt.packed(u.conv[0], x.t.dtype, segs)
-        p2 = rt.packed(u.conv[2], x.t.dtype, [(p1.cout, rt.round_up(p1.cout, 8))])
-        p3 = rt.packed(u.conv[4], x.t.dtype, [(p2.cout, rt.round_up(p2.cout, 8))])
+    for i, ((c1, c2, c3), x) in enumerate(units):
         o = rt.new_feat(x.B, x.H, x.W, x.C, x.t.dtype, x.t.device)
         a = arr[i]
         a.dtype, a.channels, a.batch, a.h, a.w = _lib.BF16, x.C, x.B, x.H, x.W
         a.x, a.x_ldc = x.ptr(), x.ldc
-        a.w1, a.w2, a.w3 = p1.w.data_ptr(), p2.w.data_ptr(), p3.w.data_ptr()
-        a.w1_kpad, a.w2_kpad, a.w3_kpad = p1.k_pad, p2.k_pad, p3.k_pad
-        a.b1, a.b2, a.b3 = p1.bias.data_ptr(), p2.bias.data_ptr(), p3.bias.data_ptr()
+        if C == 80:
+            p1, p2, p3, b1, b2, b3 = small_unit_packs(c1, c2, c3)
+            a.w1, a.w2, a.w3 = p1.data_ptr(), p2.data_ptr(), p3.data_ptr()
+            a.w1_kpad = a.w2_kpad = a.w3_kpad = 0
+            a.b1, a.b2, a.b3 = b1.data_ptr(), b2.data_ptr(), b3.data_ptr()
+            keep.append((p1, p2, p3, b1, b2, b3))
+        else:
+            segs = [(x.C, x.ldc)]
+            p1 = rt.packed(c1, x.t.dtype, segs)
+            p2 = rt.packed(c2, x.t.dtype, [(p1.cout, rt.round_up(p1.cout, 8))])
+            p3 = rt.packed(c3, x.t.dtype, [(p2.cout, rt.round_up(p2.cout, 8))])
+            a.w1, a.w2, a.w3 = p1.w.data_ptr(), p2.w.data_ptr(), p3.w.data_ptr()
+            a.w1_kpad, a.w2_kpad, a.w3_kpad = p1.k_pad, p2.k_pad, p3.k_pad
+            a.b1, a.b2, a.b3 = p1.bias.data_ptr(), p2.bias.data_ptr(), p3.bias.data_ptr()
+            keep.append((p1, p2, p3))
         a.out, a.out_ldc = o.ptr(), o.ldc
         outs.append(o)
-        keep.append((p1, p2, p3))
     npix = x0.B * x0.H * x0.W
-    C = x0.C
-    flops = 2.0 * npix * len(pairs) * (C * C // 2 * 2 + 9 * (C // 2) ** 2)
-    rt.timed(f"ru_fused_kernel<{C}, {C // 2}>", flops, 2 * npix * len(pairs) * 2 * C,
-             lambda: _lib.call("rgbac_residual_unit", ctypes.addressof(arr), len(pairs),
+    flops = 2.0 * npix * len(units) * (C * C // 2 * 2 + 9 * (C // 2) ** 2)
+    kname = f"ru_fused_kernel<{C}, {C // 2}>" if C == 192 else f"ru_small_kernel<{kind}>"
+    rt.timed(kname, flops, 2 * npix * len(units) * 2 * C,
+             lambda: _lib.call("rgbac_residual_unit_ex", ctypes.addressof(arr), len(units), kind,
                                _lib.stream_ptr(x0.t.device)),
-             f"ru_fused_kernel g{len(pairs)} C{C} {x0.H}x{x0.W} B{x0.B}")
+             f"{kname} kind{kind} g{len(units)} C{C} {x0.H}x{x0.W} B{x0.B}")
     return outs
+
+
+def run_residual_units_fused(pairs):
+    """The same units as ONE fused launch (both intermediates in LDS)."""
+    return run_bottlenecks_fused([((u.conv[0], u.conv[2], u.conv[4]), x) for u, x in pairs], 0)
 
 
 def run_residual_units(pairs):

@@ -8,6 +8,7 @@ import torch.nn as nn
 from .. import runtime as rt
 from ..entropy import EntropyBottleneck, GaussianConditional
 from ..layers.GDN import GDN
+from ..layers.Masked_Attention import _fused_ok, run_bottlenecks_fused
 from ..layers.TransformRGB import _act_of, _layer_forward, dse_fused, dse_fused_ok, prep_conv, run_conv
 from ..layers._blocks import conv, conv3x3, deconv, subpel_conv3x3  # noqa: F401
 from ._latent import latent_path
@@ -56,6 +57,11 @@ class DSE(nn.Module):
         return _layer_forward(self, lambda f: self.nhwc(f), "dse_t", input)
 
 
+def _resblock_fused_ok(pairs):
+    return _fused_ok(pairs) and all(type(b.relu1) is nn.ReLU and type(b.relu2) is nn.ReLU
+                                    for b, _ in pairs)
+
+
 class ResBlock(nn.Module):
     def __init__(self, num_filters=128):
         super().__init__()
@@ -74,7 +80,10 @@ class ResBlock(nn.Module):
 
 
 def run_resblocks(pairs):
-    """Independent ResBlocks [(block, x), ...] of equal shape as grouped launches."""
+    """Independent ResBlocks [(block, x), ...] of equal shape: one fused launch (bf16, C 192
+    or 80, ReLU blocks) or three grouped conv launches."""
+    if _resblock_fused_ok(pairs):
+        return run_bottlenecks_fused([((b.conv1, b.conv2, b.conv3), x) for b, x in pairs], 1)
     ts = rt.launch([prep_conv(b.conv1, [x.src()], act="relu") for b, x in pairs])
     ts = rt.launch([prep_conv(b.conv2, [t.src()], act="relu") for (b, _), t in zip(pairs, ts)])
     return rt.launch([prep_conv(b.conv3, [t.src()], res0=x) for (b, x), t in zip(pairs, ts)])

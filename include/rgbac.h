@@ -242,6 +242,14 @@ typedef struct rgbac_ru_args {
   void* out; int64_t out_ldc;
 } rgbac_ru_args;
 int rgbac_residual_unit(const rgbac_ru_args* args, int ngroups, void* stream);
+/* The same with a kind and C = 80 (reference: Masked_Attention.py:150-169 ResidualUnit at
+ * M = 80; models/AutoEncoderMask_Journal.py:96-110 ResBlock at 192 and 80 channels).
+ * kind 0: ResidualUnit (GELU, GELU, GELU(. + x)); kind 1: ResBlock (ReLU, ReLU, . + x).
+ * C = 192: packed conv weights as rgbac_residual_unit.  C = 80: w1 / w2 / w3 are the
+ * fragment-major packs [3][3][64][8], [3][18][64][8], [5][2][64][8] bf16 (16-row x 32-k
+ * MFMA fragments, zero padded; rgbac.layers.Masked_Attention.small_unit_packs) and b1 / b2
+ * / b3 fp32 [48] / [48] / [80] (zero padded); k_pads are ignored. */
+int rgbac_residual_unit_ex(const rgbac_ru_args* args, int ngroups, int kind, void* stream);
 
 /* ====================================================================== *
  * Training step (trainRGB.py:178-198): backward kernels, optimizer.       *

@@ -449,18 +449,21 @@ def rgb_forward(sd, inp, mask, reconmask, me1, me2, me3, me4, training=False,
     return x_hat, mse, yb / npix + zb / npix, yb / npix, zb / npix
 
 
+def resblock(t, sd, q):
+    """AutoEncoderMask_Journal.py:96-110: conv3(relu(conv2(relu(conv1 t)))) + t."""
+    r = F.relu(_conv(t, sd, q + ".conv1"))
+    r = F.relu(_conv(r, sd, q + ".conv2"))
+    return _conv(r, sd, q + ".conv3") + t
+
+
 def simplified_attention(x, sd, p):
-    """AutoEncoderMask_Journal.py:96-136: x + sigmoid(conv1(res3(x))) * res3'(x)."""
-    def resblock(t, q):
-        r = F.relu(_conv(t, sd, q + ".conv1"))
-        r = F.relu(_conv(r, sd, q + ".conv2"))
-        return _conv(r, sd, q + ".conv3") + t
+    """AutoEncoderMask_Journal.py:112-136: x + sigmoid(conv1(res3(x))) * res3'(x)."""
     tr = x
     for i in (1, 2, 3):
-        tr = resblock(tr, f"{p}.trunk_ResBlock{i}")
+        tr = resblock(tr, sd, f"{p}.trunk_ResBlock{i}")
     at = x
     for i in (1, 2, 3):
-        at = resblock(at, f"{p}.attention_ResBlock{i}")
+        at = resblock(at, sd, f"{p}.attention_ResBlock{i}")
     at = torch.sigmoid(_conv(at, sd, p + ".conv1"))
     return x + at * tr
 
