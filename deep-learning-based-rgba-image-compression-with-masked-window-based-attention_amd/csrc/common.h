@@ -85,15 +85,18 @@ __device__ __forceinline__ void mma_step<float>(f32x4& acc, uint4 a, uint4 b) {
 // for x < 0, so no cancellation): ~16 instructions instead of erff's ~40
 // divergent ones.  Used where results are stored as bf16 (3 significant
 // digits); the fp32 parity mode keeps erff.
+// Written as max(x, 0) - |x|/2 * q (q = 1 - erf(|x|/sqrt 2)): the same value for both signs
+// with no compare/select, and exp(-x^2/2) as one v_exp_f32 of a scaled x^2.
 __device__ __forceinline__ float gelu_fast(float x) {
-  const float z = fabsf(x) * 0.70710678118654752440f;
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  const float ax = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752440f, ax, 1.0f));
   float p = fmaf(1.061405429f, t, -1.453152027f);
   p = fmaf(p, t, 1.421413741f);
   p = fmaf(p, t, -0.284496736f);
   p = fmaf(p, t, 0.254829592f);
-  const float q = p * t * __expf(-z * z);         // 1 - erf(|z|)
-  return 0.5f * x * (x >= 0.0f ? 2.0f - q : q);
+  const float e = __builtin_amdgcn_exp2f(x * x * -0.72134752044448170368f);   // exp(-x^2/2)
+  const float q = p * t * e;                      // 1 - erf(|x| / sqrt 2)
+  return fmaf(-0.5f * ax, q, fmaxf(x, 0.0f));
 }
 
 // ---------------------------------------------------------------- host side

@@ -61,8 +61,12 @@ __global__ void __launch_bounds__(256, OCC) ru_fused_kernel(const RuArgsDev args
   static_assert(NPX % 32 == 0 && NH >= NPX, "tile geometry");
   constexpr int NT1 = CH / 16;                         // n tiles of stages 1 / 2
   constexpr int NT3 = C / 16;                          // n tiles of stage 3
-  constexpr int TROW = CH * 2;    // T1 / T2 row bytes: unpadded rows give at most 2-way
-                                  // conflicts for the ds_read_b128 lane groups (208 B: 3-way)
+  // T1 / T2 row bytes.  A fragment read is 16 lanes on 16 pixel rows: with 16-pixel tile rows
+  // they are 16 consecutive rows, and 208-B rows (52 dwords: 52 r mod 64 distinct for r < 16)
+  // are conflict-free for the ds_read_b128 lane groups, where 192-B rows collide 2-way (47 %
+  // of the LDS cycles were conflict cycles).  8-pixel rows split a read over two tile rows:
+  // unpadded rows stay (208 B would give 3-way there).
+  constexpr int TROW = CH * 2 + (TX == 16 ? 16 : 0);
   constexpr int KC1 = C / 64;                          // stage-1 chunks (64 k each)
   constexpr int K2 = 9 * CH;
   constexpr int KC2 = (K2 + 63) / 64;                  // stage-2 chunks (64 k each)
