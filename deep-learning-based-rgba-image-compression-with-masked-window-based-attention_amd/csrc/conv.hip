@@ -1471,7 +1471,9 @@ static const TileCfg kTiles[] = {
     // 42..47: fragment-streamed patch kernel (TH x 16 pixels x BN channels)
     {128, 192}, {64, 192}, {128, 128}, {64, 128}, {128, 256}, {128, 64},
     // 48, 49: patch-resident kernel with a 4-deep weight ring
-    {128, 64}, {128, 128}};
+    {128, 64}, {128, 128},
+    // 50: fragment-streamed patch kernel, 4 x 16 pixels x 64 channels
+    {64, 64}};
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 constexpr int kFirstWres = 7;
 constexpr int kWresStages = 6;
@@ -1485,6 +1487,18 @@ constexpr int kTileWStream = 35;   // conv_wstream_kernel (bf16, stride 1, k 1/3
 constexpr int kFirstPatch = 36;    // 36..41: conv_patch_kernel (bf16; k3 s1 conv/subpel, convT)
 constexpr int kFirstFPatch = 42;   // 42..47: conv_fpatch_kernel (fragment-major weights)
 constexpr int kFirstPatch2 = 48;   // 48, 49: conv_patch_kernel with NBUF = 4
+constexpr int kTileFPatch464 = 50; // conv_fpatch_kernel<4, 64>
+#ifndef RGBAC_RC1
+#define RGBAC_RC1 24   // unrolled-K fragment-patch weight ring depth at TN 1 (TN 2: half)
+#endif
+// RGBAC_FPATCH_CPT=0 disables the unrolled-K fragment-patch variants (A/B switch)
+static bool fpatch_cpt_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("RGBAC_FPATCH_CPT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 constexpr int kSmallKMax = 256;
 
 // ---------------------------------------------------------------------------
@@ -2187,7 +2201,7 @@ _Pragma("unroll")                                                               
 // and zero patch channels in the padding).  Waves: 1 (M) x NW (N); wave = TH rows of 16
 // pixels x BN/NW channels.  Each phase's k-steps are padded to a multiple of R (idle steps)
 // so the unrolled ring never straddles a phase's epilogue.
-template <int TH, int BN, int NW, int R>
+template <int TH, int BN, int NW, int R, int CPT = 0>
 __global__ void __launch_bounds__(64 * NW) conv_fpatch_kernel(const ConvArgsDev args) {
   using T = bf16_t;
   constexpr int TW = 16, PW = TW + 2, PR = (TH + 2) * PW;
@@ -2225,6 +2239,29 @@ __global__ void __launch_bounds__(64 * NW) conv_fpatch_kernel(const ConvArgsDev 
   const int RSc = nch + 2;                       // + 2 pad chunks (bank spread)
   const int cpt = cin32 >> 5;                    // 32-deep k-steps per tap
   const int nks_max = (convt ? 9 : 9) * cpt;     // k-steps of the widest phase (layout stride)
+  const uint4* const wf = reinterpret_cast<const uint4*>(g.w);
+  const int ntile0 = (n0 >> 4) + wave * TN;      // this wave's first 16-row N tile
+
+  // CPT > 0 (conv mode, every group's cin rounds up to 32*CPT, host-checked): the K loop is
+  // fully unrolled -- 9 taps x CPT 32-deep k-steps -- so every patch read is a per-lane base +
+  // a compile-time immediate and the weight ring is statically indexed: no per-k-step
+  // division, tap bookkeeping or address arithmetic (the generic loop below spends ~14
+  // SALU/VALU instructions per MFMA on them: issue-bound at 8 % of the matrix pipe on the
+  // 32x32-latent slice convs).  The first R k-steps' weights are requested before the patch.
+  // A k-step is only TN x TM MFMAs (64-128 cycles), so the weight ring runs RC steps ahead
+  // (RC x the step >= an L2 round trip): 12 steps at TN 1, 8 at TN 2, 4 beyond.
+  constexpr int NKSC = 9 * (CPT > 0 ? CPT : 1);
+  constexpr int RC = CPT > 0 ? (TN == 1 ? RGBAC_RC1 : (TN == 2 ? RGBAC_RC1 / 2 : 4)) : 1;
+  const uint4* wj[TN];
+  uint4 cring[RC][TN];
+  if constexpr (CPT > 0) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) wj[j] = wf + ((size_t)(ntile0 + j) * NKSC) * 64 + lane;
+#pragma unroll
+    for (int u = 0; u < RC; ++u)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) cring[u][j] = wj[j][u * 64];
+  }
 
   // ---- stage the whole patch: flat uint4 index f -> (row, chunk), zero page outside
   {
@@ -2256,10 +2293,42 @@ __global__ void __launch_bounds__(64 * NW) conv_fpatch_kernel(const ConvArgsDev 
     __syncthreads();
   }
 
+  if constexpr (CPT > 0) {
+    constexpr int RS = 4 * CPT + 2;               // patch row stride (uint4) == RSc
+    const int fr = lane & 15, fq = lane >> 4;
+    int lb[TM];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) lb[i] = (i * PW + fr) * RS + fq;
+    f32x4 acc[TN][TM];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NKSC; ++ks) {
+      const int tap = ks / CPT, cc = ks - (ks / CPT) * CPT;
+      const int off = ((tap / 3) * PW + tap % 3) * RS + cc * 4;
+      uint4 bb[TM];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) bb[i] = patch[lb[i] + off];
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) mma_step<T>(acc[j][i], cring[ks % RC][j], bb[i]);
+      if (ks + RC < NKSC) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) cring[ks % RC][j] = wj[j][(ks + RC) * 64];
+      }
+    }
+    int nn[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) nn[j] = n0 + wave * TN * 16 + j * 16 + fq * 4;
+    patch_epilogue<TN, TM>(s, g, 0, b, y0, x0, fr, nn, acc);
+    return;
+  }
+
   // ---- per-phase k-steps (padded to a multiple of R) and the weight fragment pointer
-  const uint4* const wf = reinterpret_cast<const uint4*>(g.w);
   const int nt16 = g.rows >> 4;
-  const int ntile0 = (n0 >> 4) + wave * TN;      // this wave's first 16-row N tile
   auto phase_steps = [&](int ph) {
     return (convt ? (3 - (ph >> 1)) * (3 - (ph & 1)) : 9) * cpt;
   };
@@ -2392,7 +2461,7 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
     }
     return check_launch("conv_wres_kernel");
   }
-  if (tile >= kFirstFPatch && tile < kFirstPatch2) {
+  if ((tile >= kFirstFPatch && tile < kFirstPatch2) || tile == kTileFPatch464) {
     if constexpr (sizeof(T) == 2) {
       const int th = tc.bm / 16;
       const int nbn = (max_cout + tc.bn - 1) / tc.bn;
@@ -2406,9 +2475,19 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
         return RGBAC_E_ARG;
       }
       dim3 grid((unsigned)nsp, (unsigned)nbn, 1);
-#define RGBAC_FP(TH_, BN_)                                                                    \
+      // the unrolled-K variant when it is a conv and every group has the same cin32 of 3, 4
+      // or 7 k-steps per tap (the slice stacks: 80..128 and 224 input channels)
+      int cpt = 0;
+      if (s.mode == RGBAC_CONV) {
+        cpt = ((d.g[0].cin_pad + 31) & ~31) >> 5;
+        for (int i = 1; i < s.ngroups; ++i)
+          if ((((d.g[i].cin_pad + 31) & ~31) >> 5) != cpt) cpt = 0;
+        if (cpt != 3 && cpt != 4 && cpt != 7) cpt = 0;
+        if (!fpatch_cpt_enabled()) cpt = 0;
+      }
+#define RGBAC_FP1(TH_, BN_, C_)                                                               \
   do {                                                                                        \
-    auto k_ = conv_fpatch_kernel<TH_, BN_, 4, 4>;                                             \
+    auto k_ = conv_fpatch_kernel<TH_, BN_, 4, 4, C_>;                                         \
     static bool attr_ = false;                                                                \
     if (!attr_) {                                                                             \
       (void)hipFuncSetAttribute((const void*)k_, hipFuncAttributeMaxDynamicSharedMemorySize,  \
@@ -2417,15 +2496,25 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
     }                                                                                         \
     hipLaunchKernelGGL(k_, grid, dim3(256), lds, st, d);                                      \
   } while (0)
+#define RGBAC_FP(TH_, BN_)                                                                    \
+  do {                                                                                        \
+    if (TH_ != 4) RGBAC_FP1(TH_, BN_, 0);  /* 8-row tiles: the generic loop is faster */     \
+    else if (cpt == 3) RGBAC_FP1(TH_, BN_, 3);                                                \
+    else if (cpt == 4) RGBAC_FP1(TH_, BN_, 4);                                                \
+    else if (cpt == 7) RGBAC_FP1(TH_, BN_, 7);                                                \
+    else RGBAC_FP1(TH_, BN_, 0);                                                              \
+  } while (0)
       switch (tile) {
         case 42: RGBAC_FP(8, 192); break;
         case 43: RGBAC_FP(4, 192); break;
         case 44: RGBAC_FP(8, 128); break;
         case 45: RGBAC_FP(4, 128); break;
         case 46: RGBAC_FP(8, 256); break;
+        case kTileFPatch464: RGBAC_FP(4, 64); break;
         default: RGBAC_FP(8, 64); break;
       }
 #undef RGBAC_FP
+#undef RGBAC_FP1
       return check_launch("conv_fpatch_kernel");
     } else {
       set_error("the fragment-patch tiles are bf16 only");
@@ -2693,7 +2782,8 @@ extern "C" int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroup
       RGBAC_REQUIRE(args[i].cout_pad >= ((args[i].cout + kTiles[a->tile].bn - 1) /
                                          kTiles[a->tile].bn) * kTiles[a->tile].bn &&
                         args[i].k_pad >= ntaps_max * args[i].cin_pad &&
-                        (a->tile < kFirstFPatch || a->tile >= kFirstPatch2 ||
+                        ((a->tile < kFirstFPatch || a->tile >= kFirstPatch2) &&
+                             a->tile != kTileFPatch464 ||
                          args[i].cout_pad % 16 == 0),
                     "patch tiles read whole BN-row weight tiles");
   } else if (a->tile == kTileWStream) {

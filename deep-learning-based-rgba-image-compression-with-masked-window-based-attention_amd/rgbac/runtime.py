@@ -119,7 +119,8 @@ TILES = [(128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 1
          (32, 96), (32, 32),
          (128, 192), (128, 128), (128, 96), (128, 256), (128, 192), (128, 64),
          (128, 192), (64, 192), (128, 128), (64, 128), (128, 256), (128, 64),
-         (128, 64), (128, 128)]
+         (128, 64), (128, 128),
+         (64, 64)]
 FIRST_WRES = 7
 WRES_STAGES = 6
 FIRST_DIRECT = 13        # 13..18: direct kernel (plain conv, K <= DIRECT_STEPS MFMA k-steps)
@@ -139,7 +140,19 @@ PATCH_SIG = {36: (8, 192, 2, 4, 3), 37: (8, 128, 2, 4, 3), 38: (8, 96, 4, 2, 3),
              39: (8, 256, 2, 4, 3), 40: (8, 192, 2, 4, 4), 41: (8, 64, 4, 2, 3),
              48: (8, 64, 4, 2, 4), 49: (8, 128, 2, 4, 4)}
 FIRST_FPATCH = 42        # 42..47: conv_fpatch_kernel (fragment-major weight copy, 4 waves)
-FPATCH_SIG = {42: (8, 192), 43: (4, 192), 44: (8, 128), 45: (4, 128), 46: (8, 256), 47: (8, 64)}
+FPATCH_SIG = {42: (8, 192), 43: (4, 192), 44: (8, 128), 45: (4, 128), 46: (8, 256), 47: (8, 64),
+              50: (4, 64)}
+# the fragment-patch kernel's unrolled-K variants (csrc/conv.hip, CPT template argument)
+FPATCH_CPT = os.environ.get("RGBAC_FPATCH_CPT", "1") != "0"
+
+
+def fpatch_cpt(preps):
+    """CPT (32-deep k-steps per tap) of the unrolled-K fragment-patch variant the launcher
+    picks for these convs, or 0 for the generic loop."""
+    if not FPATCH_CPT or preps[0].pk.mode != CONV:
+        return 0
+    c = {round_up(p.pk.cin_pad, 32) // 32 for p in preps}
+    return c.pop() if len(c) == 1 and next(iter(c)) in (3, 4, 7) else 0
 PATCH = os.environ.get("RGBAC_PATCH", "1") != "0"
 
 
@@ -554,7 +567,8 @@ def kernel_name(tile, preps):
     if tile == TILE_SPATIAL:
         return f"conv3x3_c32_kernel<{dt}>"
     if tile in FPATCH_SIG:
-        return "conv_fpatch_kernel<%d, %d, 4, 4>" % FPATCH_SIG[tile]
+        c = fpatch_cpt(preps) if FPATCH_SIG[tile][0] == 4 else 0
+        return "conv_fpatch_kernel<%d, %d, 4, 4%s>" % (FPATCH_SIG[tile] + (f", {c}" if c else "",))
     if tile in PATCH_SIG:
         return "conv_patch_kernel<%d, %d, %d, %d, %d>" % PATCH_SIG[tile]
     if tile == TILE_WSTREAM:
@@ -612,6 +626,14 @@ def _tile_counters(dev, n):
 
 
 LAST_CHOICE = [None]      # (tile, ksplit) of the most recent launch (debug re-runs)
+_FLUSH = {}
+
+
+def _flush_buffer(dev):
+    buf = _FLUSH.get(dev)
+    if buf is None:
+        buf = _FLUSH[dev] = torch.zeros(16 << 20, dtype=torch.float32, device=dev)   # 64 MB
+    return buf
 
 
 def launch(preps, force=None):
@@ -670,18 +692,24 @@ def launch(preps, force=None):
                                 _wstream_ok(preps))
             cands += [(t, 1) for t in _patch_tiles(preps)]
         if TUNE and not fixed and not torch.cuda.is_current_stream_capturing():
+            # each timed run starts with the L2s flushed (a 64 MB write evicts all 8 XCDs'
+            # 4 MB): in the forward graph every layer's weights and inputs arrive cold, and a
+            # candidate that re-streams its weights per wave from L2 looks 2x faster hot
+            flush = _flush_buffer(dev)
             best = None
             for cand in cands:
                 set_choice(*cand)
                 run()                                           # warm-up
-                ev0 = torch.cuda.Event(enable_timing=True)
-                ev1 = torch.cuda.Event(enable_timing=True)
-                ev0.record()
+                ms = 0.0
                 for _ in range(3):
+                    flush.add_(1)
+                    ev0 = torch.cuda.Event(enable_timing=True)
+                    ev1 = torch.cuda.Event(enable_timing=True)
+                    ev0.record()
                     run()
-                ev1.record()
-                ev1.synchronize()
-                ms = ev0.elapsed_time(ev1)
+                    ev1.record()
+                    ev1.synchronize()
+                    ms += ev0.elapsed_time(ev1)
                 if best is None or ms < best[0]:
                     best = (ms, cand)
             choice = best[1]

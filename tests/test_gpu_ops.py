@@ -542,6 +542,7 @@ PATCH_CASES = [
     # mode, cin, cout, H, W
     ("convt", 192, 192, 16, 32), ("convt", 80, 192, 8, 16), ("convt", 192, 3, 8, 16),
     ("conv", 224, 128, 16, 16), ("conv", 120, 224, 8, 32), ("conv", 40, 40, 8, 16),
+    ("conv", 88, 224, 8, 16),
     ("subpel", 192, 192, 8, 16), ("subpel", 192, 12, 16, 16),
 ]
 

@@ -23,6 +23,7 @@ SHAPES = [  # name, kind, cin, cout, H, W, B, groups
     ("cc2 224->128 g10", "conv", 224, 128, 32, 32, 8, 10),
     ("cc1 88->224 g2", "conv", 88, 224, 32, 32, 8, 2),
     ("lrp2 224->128 g1", "conv", 224, 128, 32, 32, 8, 1),
+    ("lrp1 96->224 g1", "conv", 96, 224, 32, 32, 8, 1),
     ("ru 40->40 g2", "conv", 40, 40, 32, 32, 8, 2),
     ("x4 subpel 192->12", "subpel", 192, 12, 128, 128, 8, 1),
     ("hs 256->288 g2 16x16", "conv", 256, 288, 16, 16, 8, 2),
