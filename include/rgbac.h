@@ -394,6 +394,19 @@ int rgbac_stem_gdn(int batch, int in_h, int in_w, const void* x, int64_t x_ldc, 
                    int w1_kpad, const float* b1, const void* w2, int w2_kpad, const float* beta,
                    int inverse, void* out, int64_t out_ldc, void* stream);
 
+/* Training-data augmentation for a batch (reference: my_datasets/MYdataset.py:55-115,
+ * COCOP3MDataset.__getitem__ after the PNG decode): ToTensor (/255) -> RandomResizedCrop to
+ * out_h x out_w (crop + bilinear resize, antialiased like torchvision >= 0.17 when antialias
+ * != 0) -> horizontal / vertical flip -> alpha fill (alpha := 1) -> masked_image =
+ * where(alpha > 0, img, alpha).  descs: device array of `batch` descriptors
+ *   struct { const uint8_t* src; int32 h, w, crop_top, crop_left, crop_h, crop_w, flags, pad; }
+ * (src = h x w x 4 RGBA uint8; flags bit 0 hflip, 1 vflip, 2 alpha fill; the random draws are
+ * the host's, mirroring the reference's RNG calls: rgbac/data.py).  Outputs NCHW fp32:
+ * masked (B,3,H,W), alpha (B,1,H,W), img (B,3,H,W), rgba (B,4,H,W) -- the reference's tuple
+ * (masked_image, alpha, img, alpha, images_with_alpha). */
+int rgbac_rgba_augment(int batch, const void* descs, int out_h, int out_w, int antialias,
+                       float* masked, float* alpha, float* img, float* rgba, void* stream);
+
 /* Fused masked shifted-window attention block, bf16, window 8, C = 192, 8 heads
  * (reference: layers/masked_win_attention.py:96-131 WindowAttention.forward, :169-251
  * WinBasedAttention.forward).  out = x + proj(attn(x)) on windows whose alpha is non-zero
