@@ -492,9 +492,283 @@ __global__ void __launch_bounds__(256, 1) ru_small_kernel(const RuArgsDev args) 
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// C = 192 bottleneck, fragment-streamed (CH = 96): the same three GEMMs per 8x16 output tile
+// as ru_fused_kernel, but with NO barrier inside any K loop.  Every wave streams the weight
+// fragments it needs straight from host-built fragment-major packs (1 KiB per 16 rows x 32 k,
+// lane-ordered: each load is one fully coalesced global_load_dwordx4, served by L2 after the
+// first tiles) into a statically indexed register ring, instead of the 20 chunk-wise LDS
+// ring refills and barriers of ru_fused_kernel.  Barriers: 2 (T1 complete, T2 complete).
+//   stage 1: T1 = act(W1 x + b1) on the 10x18 halo: wave w owns halo rows 48w..48w+47
+//            (3 m tiles) x all 6 n tiles; its x fragments (6 k-steps) are loaded up front
+//   stage 2: T2 = act(W2 (*) T1 + b2): waves = 2 channel halves x 2 pixel halves,
+//            27 k-steps (tap-major, 3 per tap) of 3 x 4 MFMAs, ring R2 k-steps deep
+//   stage 3: y = [GELU](W3 T2 + b3 + x): 3 k-steps of 6 x 4 MFMAs
+// Each next stage's first weights (and the residual x) are requested before the current
+// stage's epilogue, so their latency hides behind its activation math.  T1 / T2 are separate
+// 208-B-row buffers (conflict-free 16-row fragment reads): 64 KiB, two workgroups per CU.
+namespace rsw {
+constexpr int TY = 8, TX = 16, HX = TX + 2, NH = (TY + 2) * HX;   // 180 halo pixels
+constexpr int TROW = 208;
+constexpr int ORW = 400;           // output staging row (100 dwords: 16 rows on distinct banks)
+constexpr int NK1 = 6, NK2 = 27, NK3 = 3;
+constexpr int R1 = 2, R3 = 2;
+constexpr int PRE2 = 4;            // stage-2 ring slots requested before the stage-1 epilogue
+}  // namespace rsw
+
+#ifdef RGBAC_RU_TIMING
+// probe builds only (tools/ru_stage_probe.py): per-workgroup stage timestamps of waves 0 / 3
+__device__ unsigned long long g_ru_t[8192][2][8];
+__device__ unsigned long long g_ru_w[8192][2];     // wall clock (100 MHz) at start / end
+#define RU_T(k)                                                                              \
+  do {                                                                                       \
+    const unsigned long long c_ = clock64();                                                 \
+    if (lane == 0 && (wave == 0 || wave == 3) && blockIdx.x < 8192 && blockIdx.z == 0)       \
+      g_ru_t[blockIdx.x][wave == 3][k] = c_;                                                 \
+    if ((k == 0 || k == 7) && tid == 0 && blockIdx.x < 8192 && blockIdx.z == 0)               \
+      g_ru_w[blockIdx.x][k == 7] = wall_clock64();                                           \
+  } while (0)
+#else
+#define RU_T(k) do {} while (0)
+#endif
+
+template <int RB>
+__global__ void __launch_bounds__(256, 2) ru_stream_kernel(const RuArgsDev args) {
+  using namespace rsw;
+  constexpr int R2 = RB ? 6 : 8;                   // stage-2 ring (ReLU variant: register fit)
+  // T1 | T2; after stage 3's MFMAs the same bytes stage the output tile (128 x 400-B rows)
+  __shared__ __attribute__((aligned(16))) unsigned char lds[NH * TROW + TY * TX * TROW];
+  unsigned char* const T1 = lds;
+  unsigned char* const T2 = lds + NH * TROW;
+  unsigned char* const OT = lds;
+  static_assert(TY * TX * ORW <= NH * TROW + TY * TX * TROW, "output staging fits");
+  // biases in LDS: an epilogue's bias read is then an LDS read (lgkmcnt), not a global load
+  // whose vmcnt wait would also drain the next stage's weight prefetch
+  __shared__ __attribute__((aligned(16))) float bs[96 + 96 + 192];
+  const RuGroup& g = args.g[blockIdx.z];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int tx_n = args.W / TX, ty_n = args.H / TY;
+  int t = blockIdx.x;
+  {                                                // XCD-contiguous runs of neighbouring tiles
+    const int nwg = gridDim.x, xcd = t & 7, q = nwg >> 3, r = nwg & 7;
+    t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (t >> 3);
+  }
+  const int tx = t % tx_n; t /= tx_n;
+  const int ty = t % ty_n;
+  const int b = t / ty_n;
+  const int y0 = ty * TY, x0 = tx * TX;
+
+  // ================= stage 1
+  RU_T(0);
+  for (int e = tid; e < 384; e += 256) bs[e] = e < 96 ? g.b1[e] : e < 192 ? g.b2[e - 96] : g.b3[e - 192];
+  const uint4* const W1 = reinterpret_cast<const uint4*>(g.w1) + lane;
+  uint4 w1r[R1][6];
+#pragma unroll
+  for (int u = 0; u < R1; ++u)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) w1r[u][j] = W1[(j * NK1 + u) * 64];
+  uint4 xb[NK1][3];
+  bool xin[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int hp = 48 * wave + 16 * i + fr;
+    const int hy = hp / HX, hx = hp - (hp / HX) * HX;
+    const int iy = y0 + hy - 1, ix = x0 + hx - 1;
+    xin[i] = hp < NH && iy >= 0 && iy < args.H && ix >= 0 && ix < args.W;
+    const bf16_t* row = g.x + ((long long)(b * args.H + (xin[i] ? iy : 0)) * args.W +
+                               (xin[i] ? ix : 0)) * g.ldx + fq * 8;
+#pragma unroll
+    for (int ks = 0; ks < NK1; ++ks)
+      xb[ks][i] = xin[i] ? *reinterpret_cast<const uint4*>(row + ks * 32) : make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();                                 // bs visible (behind the x / W1 loads)
+  f32x4 acc1[6][3];
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) acc1[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < NK1; ++ks) {
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+#pragma unroll
+      for (int i = 0; i < 3; ++i) mma_step<bf16_t>(acc1[j][i], w1r[ks % R1][j], xb[ks][i]);
+    if (ks + R1 < NK1) {
+#pragma unroll
+      for (int j = 0; j < 6; ++j) w1r[ks % R1][j] = W1[(j * NK1 + ks + R1) * 64];
+    }
+  }
+  RU_T(1);
+  // stage-2 weights for the first R2 k-steps, in flight during the stage-1 epilogue
+  const int wn = wave >> 1, wm = wave & 1;
+  const uint4* const W2 = reinterpret_cast<const uint4*>(g.w2) + lane + (size_t)(3 * wn) * NK2 * 64;
+  uint4 w2r[R2][3];
+#pragma unroll
+  for (int u = 0; u < PRE2; ++u)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) w2r[u][j] = W2[(j * NK2 + u) * 64];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int hp = 48 * wave + 16 * i + fr;
+    if (hp >= NH) continue;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int n = 16 * j + 4 * fq;
+      const float4 bb = *reinterpret_cast<const float4*>(bs + n);
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      if (xin[i]) {
+        v[0] = ru_act<RB>(acc1[j][i][0] + bb.x);
+        v[1] = ru_act<RB>(acc1[j][i][1] + bb.y);
+        v[2] = ru_act<RB>(acc1[j][i][2] + bb.z);
+        v[3] = ru_act<RB>(acc1[j][i][3] + bb.w);
+      }
+      Elem<bf16_t>::st4(reinterpret_cast<bf16_t*>(&T1[hp * TROW + n * 2]), v);
+    }
+  }
+  RU_T(2);
+#pragma unroll
+  for (int u = PRE2; u < R2; ++u)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) w2r[u][j] = W2[(j * NK2 + u) * 64];
+  __syncthreads();
+  RU_T(3);
+
+  // ================= stage 2: m tile i = tile row 4 wm + i (16 pixels), lane pixel x = fr
+  f32x4 acc2[3][4];
+#pragma unroll
+  for (int j = 0; j < 3; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc2[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const unsigned char* const t1l = T1 + (4 * wm * HX + fr) * TROW + fq * 16;
+#pragma unroll
+  for (int ks = 0; ks < NK2; ++ks) {
+    const int tap = ks / 3, c = ks % 3;
+    const int off = ((tap / 3) * HX + tap % 3) * TROW + c * 64;
+    uint4 bv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[i] = *reinterpret_cast<const uint4*>(t1l + i * HX * TROW + off);
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mma_step<bf16_t>(acc2[j][i], w2r[ks % R2][j], bv[i]);
+    if (ks + R2 < NK2) {
+#pragma unroll
+      for (int j = 0; j < 3; ++j) w2r[ks % R2][j] = W2[(j * NK2 + ks + R2) * 64];
+    }
+    // keep the next k-step's LDS reads from being hoisted further up (the fully unrolled loop
+    // otherwise front-loads them and spills)
+    asm volatile("" ::: "memory");
+  }
+  RU_T(4);
+  // stage-3 weights (first R3 k-steps) and the residual x, in flight during this epilogue
+  // (the residual loads must precede every output store: vmcnt counts stores too, so a load
+  // issued behind a store waits for it)
+  const uint4* const W3 = reinterpret_cast<const uint4*>(g.w3) + lane + (size_t)(6 * wn) * NK3 * 64;
+  uint4 w3r[R3][6];
+#pragma unroll
+  for (int u = 0; u < R3; ++u)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) w3r[u][j] = W3[(j * NK3 + u) * 64];
+  uint2 res[4][6];
+  auto load_res = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const long long pix = (long long)(b * args.H + y0 + 4 * wm + i) * args.W + x0 + fr;
+      const bf16_t* xr = g.x + pix * g.ldx + 96 * wn + 4 * fq;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) res[i][j] = *reinterpret_cast<const uint2*>(xr + 16 * j);
+    }
+  };
+  if constexpr (!RB) load_res();                   // (the ReLU variant: after stage 3's MFMAs)
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int n = 48 * wn + 16 * j + 4 * fq;
+    const float4 bb = *reinterpret_cast<const float4*>(bs + 96 + n);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = (4 * wm + i) * TX + fr;
+      float v[4];
+      v[0] = ru_act<RB>(acc2[j][i][0] + bb.x);
+      v[1] = ru_act<RB>(acc2[j][i][1] + bb.y);
+      v[2] = ru_act<RB>(acc2[j][i][2] + bb.z);
+      v[3] = ru_act<RB>(acc2[j][i][3] + bb.w);
+      Elem<bf16_t>::st4(reinterpret_cast<bf16_t*>(&T2[p * TROW + n * 2]), v);
+    }
+  }
+  RU_T(5);
+  __syncthreads();
+  RU_T(6);
+
+  // ================= stage 3
+  f32x4 acc3[6][4];
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc3[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const unsigned char* const t2l = T2 + (4 * wm * TX + fr) * TROW + fq * 16;
+#pragma unroll
+  for (int ks = 0; ks < NK3; ++ks) {
+    uint4 bv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[i] = *reinterpret_cast<const uint4*>(t2l + i * TX * TROW + ks * 64);
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mma_step<bf16_t>(acc3[j][i], w3r[ks % R3][j], bv[i]);
+    if (ks + R3 < NK3) {
+#pragma unroll
+      for (int j = 0; j < 6; ++j) w3r[ks % R3][j] = W3[(j * NK3 + ks + R3) * 64];
+    }
+  }
+  if constexpr (RB != 0) load_res();
+  __syncthreads();                                 // every wave is done reading T2
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int p = (4 * wm + i) * TX + fr;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int n = 96 * wn + 16 * j + 4 * fq;
+      const float4 bb = *reinterpret_cast<const float4*>(bs + 192 + n);
+      const uint2 rr = res[i][j];
+      float v[4];
+      v[0] = acc3[j][i][0] + bb.x + bf2f(rr.x & 0xFFFF);
+      v[1] = acc3[j][i][1] + bb.y + bf2f(rr.x >> 16);
+      v[2] = acc3[j][i][2] + bb.z + bf2f(rr.y & 0xFFFF);
+      v[3] = acc3[j][i][3] + bb.w + bf2f(rr.y >> 16);
+      if (!RB) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = ru_gelu(v[r]);
+      }
+      Elem<bf16_t>::st4(reinterpret_cast<bf16_t*>(OT + p * ORW + n * 2), v);
+    }
+  }
+  __syncthreads();
+  // whole 16-B chunks, consecutive lanes on consecutive chunks of a pixel's 384 bytes
+#pragma unroll
+  for (int u = 0; u < TY * TX * 24 / 256; ++u) {
+    const int c = tid + 256 * u, p = c / 24, q = c - (c / 24) * 24;
+    const long long pix = (long long)(b * args.H + y0 + p / TX) * args.W + x0 + p % TX;
+    *reinterpret_cast<uint4*>(g.out + pix * g.ldo + q * 8) =
+        *reinterpret_cast<const uint4*>(OT + p * ORW + q * 16);
+  }
+  RU_T(7);
+}
+#undef RU_T
+
 }  // namespace rgbac
 
 using namespace rgbac;
+
+#ifdef RGBAC_RU_TIMING
+extern "C" int rgbac_debug_ru_times(unsigned long long* host, int nblocks) {
+  if (nblocks > 8192) nblocks = 8192;
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ru_t), (size_t)nblocks * 16 * 8) != hipSuccess) return 1;
+  return hipMemcpyFromSymbol(host + (size_t)nblocks * 16, HIP_SYMBOL(g_ru_w), (size_t)nblocks * 2 * 8) ==
+                 hipSuccess ? 0 : 1;
+}
+#endif
 
 extern "C" int rgbac_residual_unit(const rgbac_ru_args* args, int ngroups, void* stream) {
   return rgbac_residual_unit_ex(args, ngroups, 0, stream);
@@ -520,7 +794,7 @@ extern "C" int rgbac_residual_unit_ex(const rgbac_ru_args* args, int ngroups, in
     RGBAC_REQUIRE(q->x != q->out, "out must not alias x (the halo is read by other tiles)");
     RGBAC_REQUIRE(q->x_ldc >= a->channels && q->x_ldc % 8 == 0 && q->out_ldc >= a->channels &&
                       q->out_ldc % 4 == 0, "strides");
-    if (a->channels == 192)
+    if (a->channels == 192 && q->w1_kpad != 0)
       RGBAC_REQUIRE(q->w1_kpad >= 192 && q->w2_kpad >= 896 && q->w3_kpad >= 96 &&
                         q->w1_kpad % 8 == 0 && q->w2_kpad % 8 == 0 && q->w3_kpad % 8 == 0,
                     "packed weight k_pad (w1 >= 192, w2 >= 896 zero-padded, w3 >= 96)");
@@ -541,6 +815,20 @@ extern "C" int rgbac_residual_unit_ex(const rgbac_ru_args* args, int ngroups, in
     if (kind) hipLaunchKernelGGL(ru_small_kernel<1>, dim3((unsigned)tiles, 1, ngroups), dim3(256), 0, st, d);
     else hipLaunchKernelGGL(ru_small_kernel<0>, dim3((unsigned)tiles, 1, ngroups), dim3(256), 0, st, d);
     return check_launch("ru_small_kernel");
+  }
+  if (a->w1_kpad == 0) {                             // fragment-major packs: streamed kernel
+    RGBAC_REQUIRE(a->h % 8 == 0 && a->w % 16 == 0, "the streamed unit needs H % 8 == 0, W % 16 == 0");
+    for (int i = 0; i < ngroups; ++i)
+      RGBAC_REQUIRE(args[i].w1_kpad == 0 && args[i].w2_kpad == 0 && args[i].w3_kpad == 0 &&
+                        ((uintptr_t)args[i].b1 % 16) == 0 && ((uintptr_t)args[i].b2 % 16) == 0 &&
+                        ((uintptr_t)args[i].b3 % 16) == 0 && args[i].out_ldc % 8 == 0 &&
+                        ((uintptr_t)args[i].out % 16) == 0,
+                    "grouped units must all be fragment-major (16-B aligned biases and out rows)");
+    const long long tiles = (long long)a->batch * (a->h / 8) * (a->w / 16);
+    RGBAC_REQUIRE(tiles < (1ll << 31), "too many tiles");
+    if (kind) hipLaunchKernelGGL(ru_stream_kernel<1>, dim3((unsigned)tiles, 1, ngroups), dim3(256), 0, st, d);
+    else hipLaunchKernelGGL(ru_stream_kernel<0>, dim3((unsigned)tiles, 1, ngroups), dim3(256), 0, st, d);
+    return check_launch("ru_stream_kernel");
   }
   static const int wide_env = [] {
     const char* e = getenv("RGBAC_RU_TILE");

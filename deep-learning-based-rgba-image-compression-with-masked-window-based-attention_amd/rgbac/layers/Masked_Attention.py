@@ -39,6 +39,8 @@ class ResidualUnit(nn.Module):
 
 
 FUSED = os.environ.get("RGBAC_FUSED_RU", "1") != "0"
+# C = 192 units on fragment-major packs (ru_stream_kernel); "0" keeps the chunk-ring kernel
+STREAM = os.environ.get("RGBAC_RU_STREAM", "1") != "0"
 
 
 def _fused_ok(pairs):
@@ -89,12 +91,48 @@ def small_unit_packs(c1, c2, c3):
     return ent[1]
 
 
+def wide_unit_packs(c1, c2, c3):
+    """Fragment-major bf16 packs of a C = 192 bottleneck (1x1 192->96, 3x3 96->96, 1x1 96->192)
+    for ru_stream_kernel: w1 [6][6][64][8], w2 [6][27][64][8] (k = tap * 96 + ci), w3
+    [12][3][64][8] (16 rows x 32 k per fragment; lane l holds row 16t + l%16, k 32ks +
+    8(l/16) .. +8), biases fp32 [96], [96], [192].  Cached on conv1 per parameter version."""
+    ps = [c1.weight, c1.bias, c2.weight, c2.bias, c3.weight, c3.bias]
+    key = (rt.PARAM_GEN,) + tuple((t._version, t.data_ptr()) for t in ps)
+    ent = c1.__dict__.get("_rgbac_wide_ru")
+    if ent is None or ent[0] != key:
+        with torch.no_grad():
+            kfn = lambda ks, l, e: 32 * ks + 8 * (l >> 4) + e
+            p1 = _frag_pack(c1.weight.float().reshape(96, 192), 6, 6, kfn)
+            w2 = c2.weight.float().permute(0, 2, 3, 1).reshape(96, 9 * 96)
+            p2 = _frag_pack(w2, 6, 27, kfn)
+            p3 = _frag_pack(c3.weight.float().reshape(192, 96), 12, 3, kfn)
+            bs = tuple(c.bias.float().contiguous().clone() for c in (c1, c2, c3))
+        c1.__dict__["_rgbac_wide_ru"] = (key, (p1, p2, p3) + bs)
+        ent = c1.__dict__["_rgbac_wide_ru"]
+    return ent[1]
+
+
+def _frag_pack(w, nt, nks, kfn):
+    """(rows, K) fp32 -> [nt][nks][64 lanes][8] bf16 MFMA A fragments (zero padded)."""
+    dev = w.device
+    ar = lambda k: torch.arange(k, device=dev)
+    t, ks = ar(nt)[:, None, None, None], ar(nks)[None, :, None, None]
+    l, e = ar(64)[None, None, :, None], ar(8)[None, None, None, :]
+    row = 16 * t + (l & 15)
+    k = kfn(ks, l, e)
+    ok = (row < w.shape[0]) & (k >= 0) & (k < w.shape[1])
+    row, k, ok = torch.broadcast_tensors(row, k, ok)
+    v = w[row.clamp(max=w.shape[0] - 1), k.clamp(0, w.shape[1] - 1)]
+    return torch.where(ok, v, torch.zeros((), device=dev)).to(torch.bfloat16).contiguous()
+
+
 def run_bottlenecks_fused(units, kind):
     """Bottleneck residual blocks [((conv1, conv2, conv3), x), ...] of one geometry as ONE
     rgbac_residual_unit_ex launch (csrc/fused.hip; kind 0 = ResidualUnit, 1 = ResBlock):
     both intermediates stay in LDS, one read of x and one write of y per pixel."""
     x0 = units[0][1]
     C = x0.C
+    stream = C == 192 and STREAM and x0.W % 16 == 0
     arr = (_lib.RuArgs * len(units))()
     outs, keep = [], []
     for i, ((c1, c2, c3), x) in enumerate(units):
@@ -102,8 +140,8 @@ def run_bottlenecks_fused(units, kind):
         a = arr[i]
         a.dtype, a.channels, a.batch, a.h, a.w = _lib.BF16, x.C, x.B, x.H, x.W
         a.x, a.x_ldc = x.ptr(), x.ldc
-        if C == 80:
-            p1, p2, p3, b1, b2, b3 = small_unit_packs(c1, c2, c3)
+        if C == 80 or stream:
+            p1, p2, p3, b1, b2, b3 = (small_unit_packs if C == 80 else wide_unit_packs)(c1, c2, c3)
             a.w1, a.w2, a.w3 = p1.data_ptr(), p2.data_ptr(), p3.data_ptr()
             a.w1_kpad = a.w2_kpad = a.w3_kpad = 0
             a.b1, a.b2, a.b3 = b1.data_ptr(), b2.data_ptr(), b3.data_ptr()
@@ -121,7 +159,8 @@ def run_bottlenecks_fused(units, kind):
         outs.append(o)
     npix = x0.B * x0.H * x0.W
     flops = 2.0 * npix * len(units) * (C * C // 2 * 2 + 9 * (C // 2) ** 2)
-    kname = f"ru_fused_kernel<{C}, {C // 2}>" if C == 192 else f"ru_small_kernel<{kind}>"
+    kname = (f"ru_small_kernel<{kind}>" if C == 80 else f"ru_stream_kernel<{kind}>" if stream
+             else f"ru_fused_kernel<{C}, {C // 2}>")
     rt.timed(kname, flops, 2 * npix * len(units) * 2 * C,
              lambda: _lib.call("rgbac_residual_unit_ex", ctypes.addressof(arr), len(units), kind,
                                _lib.stream_ptr(x0.t.device)),

@@ -248,7 +248,11 @@ int rgbac_residual_unit(const rgbac_ru_args* args, int ngroups, void* stream);
  * C = 192: packed conv weights as rgbac_residual_unit.  C = 80: w1 / w2 / w3 are the
  * fragment-major packs [3][3][64][8], [3][18][64][8], [5][2][64][8] bf16 (16-row x 32-k
  * MFMA fragments, zero padded; rgbac.layers.Masked_Attention.small_unit_packs) and b1 / b2
- * / b3 fp32 [48] / [48] / [80] (zero padded); k_pads are ignored. */
+ * / b3 fp32 [48] / [48] / [80] (zero padded); k_pads are ignored.
+ * C = 192 with every k_pad 0 (W % 16 == 0): fragment-major packs [6][6][64][8],
+ * [6][27][64][8] (k = tap * 96 + ci), [12][3][64][8] bf16 and b1 / b2 / b3 fp32 [96] / [96]
+ * / [192], 16-byte aligned (rgbac.layers.Masked_Attention.wide_unit_packs): the barrier-free
+ * weight-streaming kernel, one 8x16 output tile per workgroup. */
 int rgbac_residual_unit_ex(const rgbac_ru_args* args, int ngroups, int kind, void* stream);
 
 /* ====================================================================== *

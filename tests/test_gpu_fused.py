@@ -133,15 +133,18 @@ def test_winattn_block_fused_matches_unfused_and_oracle(device, B, H, W, shift, 
 
 
 # ---------------------------------------------------------------------------------------
-# Fused bottleneck residual blocks (rgbac_residual_unit_ex): the ResidualUnit at C = 80
-# (Masked_Attention.py:150-169, the latent ws-4 attention blocks) and the alpha codec's
+# Fused bottleneck residual blocks (rgbac_residual_unit_ex): the ResidualUnit at C = 192 / 80
+# (Masked_Attention.py:150-169; C = 192 with W % 16 == 0 runs the weight-streaming kernel,
+# 16 x 24 the chunk-ring one) and the alpha codec's
 # ResBlock at C = 192 / 80 (AutoEncoderMask_Journal.py:96-110).  Same bf16 rounding points
 # as the three-launch path (both intermediates are rounded to bf16 in LDS exactly where the
 # unfused path stores them), so the two agree to 2 bf16 ulps on 99.9 % of the elements and
 # the fused result is as close to the fp32 oracle as the unfused one.
 @pytest.mark.parametrize("kind,C,B,H,W,groups", [("ru", 80, 2, 32, 32, 2), ("ru", 80, 1, 16, 24, 1),
                                                  ("rb", 192, 1, 32, 48, 2), ("rb", 80, 2, 32, 32, 2),
-                                                 ("rb", 80, 1, 8, 16, 1)])
+                                                 ("rb", 80, 1, 8, 16, 1), ("ru", 192, 2, 64, 64, 2),
+                                                 ("ru", 192, 1, 24, 32, 1), ("rb", 192, 2, 16, 16, 1),
+                                                 ("ru", 192, 1, 16, 24, 2)])
 def test_bottleneck_fused_matches_unfused_and_oracle(device, kind, C, B, H, W, groups):
     from rgbac import runtime as rt
     from rgbac.layers import Masked_Attention as MA
@@ -175,4 +178,32 @@ def test_bottleneck_fused_matches_unfused_and_oracle(device, kind, C, B, H, W, g
         print(f"{kind} C{C} {B}x{H}x{W} g{groups}: fused err {e_got:.2e}, unfused {e_base:.2e}, "
               f"> 2 ulp apart {frac:.1e}")
         assert e_got <= max(1.5 * e_base, 1e-2), (e_got, e_base)
+        assert frac <= 1e-3, frac
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+def test_stream_unit_matches_chunk_ring_kernel(device, kind):
+    """ru_stream_kernel (fragment-major packs) against ru_fused_kernel (chunk-ring packs) on
+    the same C = 192 units: identical GEMM order per output and the same bf16 rounding
+    points, so they agree to 1 bf16 ulp of the output range at 99.9 % of the elements."""
+    from rgbac import runtime as rt
+    from rgbac.layers import Masked_Attention as MA
+    from rgbac.models import AutoEncoderMask_Journal as AM
+    torch.manual_seed(31 + kind)
+    mods = [(MA.ResidualUnit(192) if kind == 0 else AM.ResBlock(192)).cuda() for _ in range(2)]
+    units = [((m.conv[0], m.conv[2], m.conv[4]) if kind == 0 else (m.conv1, m.conv2, m.conv3))
+             for m in mods]
+    xs = [rt.to_nhwc(torch.randn((2, 192, 32, 64), device="cuda"), torch.bfloat16) for _ in mods]
+    with torch.no_grad():
+        got = [rt.to_nchw(o).float() for o in MA.run_bottlenecks_fused(list(zip(units, xs)), kind)]
+        old = MA.STREAM
+        MA.STREAM = False
+        try:
+            base = [rt.to_nchw(o).float() for o in MA.run_bottlenecks_fused(list(zip(units, xs)), kind)]
+        finally:
+            MA.STREAM = old
+    for a, b in zip(got, base):
+        scale = b.abs().max().item()
+        frac = ((a - b).abs() > scale * 2.0 ** -8).float().mean().item()
+        print(f"kind {kind}: max diff {(a - b).abs().max().item() / scale:.2e}, > 1 ulp {frac:.1e}")
         assert frac <= 1e-3, frac
