@@ -13,6 +13,6 @@ timeout -k 10 240 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/ktr
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o p -- python tools/graph_trace.py --reps 5 > gpurun_out/pmc_fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o p -- python tools/graph_trace.py --reps 5 > gpurun_out/pmc_write.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/pmc_mfma -o p -- python tools/graph_trace.py --reps 5 > gpurun_out/pmc_mfma.log 2>&1
-python tools/graph_trace.py --analyze gpurun_out/ktrace/*/t_kernel_trace.csv > gpurun_out/graph_trace.txt 2>&1 || true
-python tools/pmc_mfma.py gpurun_out/pmc_mfma/*/p_counter_collection.csv gpurun_out/pmc_mfma.json > gpurun_out/pmc_mfma.txt 2>&1 || true
-python tools/pmc_traffic.py gpurun_out/pmc_fetch/*/p_counter_collection.csv gpurun_out/pmc_write/*/p_counter_collection.csv gpurun_out/pmc_traffic.json > gpurun_out/pmc_traffic.txt 2>&1 || true
+python tools/graph_trace.py --analyze gpurun_out/ktrace/t_kernel_trace.csv > gpurun_out/graph_trace.txt 2>&1 || true
+python tools/pmc_mfma.py gpurun_out/pmc_mfma/p_counter_collection.csv gpurun_out/pmc_mfma.json > gpurun_out/pmc_mfma.txt 2>&1 || true
+python tools/pmc_traffic.py gpurun_out/pmc_fetch/p_counter_collection.csv gpurun_out/pmc_write/p_counter_collection.csv gpurun_out/pmc_traffic.json > gpurun_out/pmc_traffic.txt 2>&1 || true
