@@ -99,6 +99,7 @@ __device__ __forceinline__ float gelu_fast(float x) {
   return fmaf(-0.5f * ax, q, fmaxf(x, 0.0f));
 }
 
+
 // ---------------------------------------------------------------- host side
 void set_error(const std::string& msg);
 int check_launch(const char* what);

@@ -40,6 +40,7 @@ struct RuGroup {
 };
 struct RuArgsDev {
   int batch, H, W, ngroups;
+  int stagger;                     // ru_stream_kernel: s_sleep(16) rounds of the later half of the grid
   RuGroup g[kRuMaxGroups];
 };
 
@@ -49,6 +50,17 @@ __device__ __forceinline__ float ru_gelu(float v) { return gelu_fast(v); }   // 
 // RB = 1: the alpha codec's ResBlock (AutoEncoderMask_Journal.py:96-110: ReLU, ReLU, + x).
 template <int RB>
 __device__ __forceinline__ float ru_act(float v) { return RB ? fmaxf(v, 0.0f) : ru_gelu(v); }
+// v = act(a + b) on one accumulator quad
+template <int RB>
+__device__ __forceinline__ void ru_act4(float (&v)[4], const f32x4& a, const float4& b) {
+  if constexpr (RB) {
+    v[0] = fmaxf(a[0] + b.x, 0.0f); v[1] = fmaxf(a[1] + b.y, 0.0f);
+    v[2] = fmaxf(a[2] + b.z, 0.0f); v[3] = fmaxf(a[3] + b.w, 0.0f);
+  } else {
+    v[0] = ru_gelu(a[0] + b.x); v[1] = ru_gelu(a[1] + b.y);
+    v[2] = ru_gelu(a[2] + b.z); v[3] = ru_gelu(a[3] + b.w);
+  }
+}
 
 template <int C, int CH, int TY, int TX, int OCC, int RB = 0>
 __global__ void __launch_bounds__(256, OCC) ru_fused_kernel(const RuArgsDev args) {
@@ -507,8 +519,12 @@ __global__ void __launch_bounds__(256, 1) ru_small_kernel(const RuArgsDev args) 
 // Each next stage's first weights (and the residual x) are requested before the current
 // stage's epilogue, so their latency hides behind its activation math.  T1 / T2 are separate
 // 208-B-row buffers (conflict-free 16-row fragment reads): 64 KiB, two workgroups per CU.
+#ifndef RGBAC_RU_R2
+#define RGBAC_RU_R2 8      // ru_stream_kernel<0> stage-2 weight ring depth (k-steps)
+#endif
 namespace rsw {
 constexpr int TY = 8, TX = 16, HX = TX + 2, NH = (TY + 2) * HX;   // 180 halo pixels
+constexpr int NHP = 192;           // T1 rows (halo padded to the waves' 4 x 48 m-tile rows)
 constexpr int TROW = 208;
 constexpr int ORW = 400;           // output staging row (100 dwords: 16 rows on distinct banks)
 constexpr int NK1 = 6, NK2 = 27, NK3 = 3;
@@ -535,13 +551,16 @@ __device__ unsigned long long g_ru_w[8192][2];     // wall clock (100 MHz) at st
 template <int RB>
 __global__ void __launch_bounds__(256, 2) ru_stream_kernel(const RuArgsDev args) {
   using namespace rsw;
-  constexpr int R2 = RB ? 6 : 8;                   // stage-2 ring (ReLU variant: register fit)
+  constexpr int R2 = RB ? 6 : RGBAC_RU_R2;         // stage-2 ring (ReLU variant: register fit)
   // T1 | T2; after stage 3's MFMAs the same bytes stage the output tile (128 x 400-B rows)
-  __shared__ __attribute__((aligned(16))) unsigned char lds[NH * TROW + TY * TX * TROW];
+  // (T1 padded to NHP = 192 rows: the stage-1 epilogue of wave 3 stores its 12 rows past the
+  // halo without a guard, so all 18 GELU quads of a wave form one branch-free block)
+  __shared__ __attribute__((aligned(16))) unsigned char lds[NHP * TROW + TY * TX * TROW];
   unsigned char* const T1 = lds;
-  unsigned char* const T2 = lds + NH * TROW;
+  unsigned char* const T2 = lds + NHP * TROW;
   unsigned char* const OT = lds;
-  static_assert(TY * TX * ORW <= NH * TROW + TY * TX * TROW, "output staging fits");
+  static_assert(TY * TX * ORW <= NHP * TROW + TY * TX * TROW, "output staging fits");
+  static_assert(NHP >= 4 * 48, "every wave's 3 halo m tiles have rows");
   // biases in LDS: an epilogue's bias read is then an LDS read (lgkmcnt), not a global load
   // whose vmcnt wait would also drain the next stage's weight prefetch
   __shared__ __attribute__((aligned(16))) float bs[96 + 96 + 192];
@@ -560,6 +579,12 @@ __global__ void __launch_bounds__(256, 2) ru_stream_kernel(const RuArgsDev args)
   const int b = t / ty_n;
   const int y0 = ty * TY, x0 = tx * TX;
 
+  // The second workgroup a CU receives (the later half of the grid in dispatch order) starts
+  // `stagger` x 1024 cycles late: the two workgroups sharing each SIMD then run out of phase, so
+  // one's GELU epilogues (VALU) issue beside the other's MFMA loops instead of both alternating
+  // MFMA and VALU phases in lockstep.
+  if (args.stagger > 0 && (int)(blockIdx.z * gridDim.x + blockIdx.x) >= (int)(gridDim.x * gridDim.z) / 2)
+    for (int i = 0; i < args.stagger; ++i) __builtin_amdgcn_s_sleep(16);
   // ================= stage 1
   RU_T(0);
   for (int e = tid; e < 384; e += 256) bs[e] = e < 96 ? g.b1[e] : e < 192 ? g.b2[e - 96] : g.b3[e - 192];
@@ -571,18 +596,23 @@ __global__ void __launch_bounds__(256, 2) ru_stream_kernel(const RuArgsDev args)
     for (int j = 0; j < 6; ++j) w1r[u][j] = W1[(j * NK1 + u) * 64];
   uint4 xb[NK1][3];
   bool xin[3];
+  unsigned xoff[3];                                // element offsets (< 2^31, host-checked)
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const int hp = 48 * wave + 16 * i + fr;
     const int hy = hp / HX, hx = hp - (hp / HX) * HX;
     const int iy = y0 + hy - 1, ix = x0 + hx - 1;
     xin[i] = hp < NH && iy >= 0 && iy < args.H && ix >= 0 && ix < args.W;
-    const bf16_t* row = g.x + ((long long)(b * args.H + (xin[i] ? iy : 0)) * args.W +
-                               (xin[i] ? ix : 0)) * g.ldx + fq * 8;
-#pragma unroll
-    for (int ks = 0; ks < NK1; ++ks)
-      xb[ks][i] = xin[i] ? *reinterpret_cast<const uint4*>(row + ks * 32) : make_uint4(0, 0, 0, 0);
+    xoff[i] = (unsigned)(((b * args.H + (xin[i] ? iy : 0)) * args.W + (xin[i] ? ix : 0)) * g.ldx +
+                         fq * 8);
   }
+  // k-step-major issue order: the first k-step's MFMAs wait for 3 loads, not for 13
+#pragma unroll
+  for (int ks = 0; ks < NK1; ++ks)
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      xb[ks][i] = xin[i] ? *reinterpret_cast<const uint4*>(g.x + xoff[i] + ks * 32)
+                         : make_uint4(0, 0, 0, 0);
   __syncthreads();                                 // bs visible (behind the x / W1 loads)
   f32x4 acc1[6][3];
 #pragma unroll
@@ -609,22 +639,24 @@ __global__ void __launch_bounds__(256, 2) ru_stream_kernel(const RuArgsDev args)
   for (int u = 0; u < PRE2; ++u)
 #pragma unroll
     for (int j = 0; j < 3; ++j) w2r[u][j] = W2[(j * NK2 + u) * 64];
+  {
+    // biases of this lane's channels read once (no lgkmcnt wait between the stores), the 18
+    // quads computed branch-free (outside-image halo pixels selected to zero)
+    float4 b1v[6];
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const int hp = 48 * wave + 16 * i + fr;
-    if (hp >= NH) continue;
+    for (int j = 0; j < 6; ++j) b1v[j] = *reinterpret_cast<const float4*>(bs + 16 * j + 4 * fq);
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const int n = 16 * j + 4 * fq;
-      const float4 bb = *reinterpret_cast<const float4*>(bs + n);
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
-      if (xin[i]) {
-        v[0] = ru_act<RB>(acc1[j][i][0] + bb.x);
-        v[1] = ru_act<RB>(acc1[j][i][1] + bb.y);
-        v[2] = ru_act<RB>(acc1[j][i][2] + bb.z);
-        v[3] = ru_act<RB>(acc1[j][i][3] + bb.w);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        const int hp = 48 * wave + 16 * i + fr;
+        float v[4];
+        ru_act4<RB>(v, acc1[j][i], b1v[j]);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = xin[i] ? v[r] : 0.0f;
+        Elem<bf16_t>::st4(reinterpret_cast<bf16_t*>(&T1[hp * TROW + n * 2]), v);
       }
-      Elem<bf16_t>::st4(reinterpret_cast<bf16_t*>(&T1[hp * TROW + n * 2]), v);
     }
   }
   RU_T(2);
@@ -635,6 +667,10 @@ __global__ void __launch_bounds__(256, 2) ru_stream_kernel(const RuArgsDev args)
   __syncthreads();
   RU_T(3);
 
+  // residual element offset of this lane's first pixel / channel quad (32-bit, host-checked):
+  // one register carried through stage 2 instead of the tile coordinates
+  const unsigned roff = (unsigned)(((b * args.H + y0 + 4 * wm) * args.W + x0 + fr) * g.ldx +
+                                   96 * wn + 4 * fq);
   // ================= stage 2: m tile i = tile row 4 wm + i (16 pixels), lane pixel x = fr
   f32x4 acc2[3][4];
 #pragma unroll
@@ -675,25 +711,24 @@ __global__ void __launch_bounds__(256, 2) ru_stream_kernel(const RuArgsDev args)
   auto load_res = [&]() {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const long long pix = (long long)(b * args.H + y0 + 4 * wm + i) * args.W + x0 + fr;
-      const bf16_t* xr = g.x + pix * g.ldx + 96 * wn + 4 * fq;
+      const bf16_t* xr = g.x + roff + (unsigned)(i * args.W * g.ldx);
 #pragma unroll
       for (int j = 0; j < 6; ++j) res[i][j] = *reinterpret_cast<const uint2*>(xr + 16 * j);
     }
   };
   if constexpr (!RB) load_res();                   // (the ReLU variant: after stage 3's MFMAs)
+  float4 b2v[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) b2v[j] = *reinterpret_cast<const float4*>(bs + 96 + 48 * wn + 16 * j + 4 * fq);
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int n = 48 * wn + 16 * j + 4 * fq;
-    const float4 bb = *reinterpret_cast<const float4*>(bs + 96 + n);
+    const float4 bb = b2v[j];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int p = (4 * wm + i) * TX + fr;
       float v[4];
-      v[0] = ru_act<RB>(acc2[j][i][0] + bb.x);
-      v[1] = ru_act<RB>(acc2[j][i][1] + bb.y);
-      v[2] = ru_act<RB>(acc2[j][i][2] + bb.z);
-      v[3] = ru_act<RB>(acc2[j][i][3] + bb.w);
+      ru_act4<RB>(v, acc2[j][i], bb);
       Elem<bf16_t>::st4(reinterpret_cast<bf16_t*>(&T2[p * TROW + n * 2]), v);
     }
   }
@@ -723,6 +758,9 @@ __global__ void __launch_bounds__(256, 2) ru_stream_kernel(const RuArgsDev args)
     }
   }
   if constexpr (RB != 0) load_res();
+  float4 b3v[6];                                   // biases read once, before the output barrier
+#pragma unroll
+  for (int j = 0; j < 6; ++j) b3v[j] = *reinterpret_cast<const float4*>(bs + 192 + 96 * wn + 16 * j + 4 * fq);
   __syncthreads();                                 // every wave is done reading T2
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -730,7 +768,7 @@ __global__ void __launch_bounds__(256, 2) ru_stream_kernel(const RuArgsDev args)
 #pragma unroll
     for (int j = 0; j < 6; ++j) {
       const int n = 96 * wn + 16 * j + 4 * fq;
-      const float4 bb = *reinterpret_cast<const float4*>(bs + 192 + n);
+      const float4 bb = b3v[j];
       const uint2 rr = res[i][j];
       float v[4];
       v[0] = acc3[j][i][0] + bb.x + bf2f(rr.x & 0xFFFF);
@@ -785,6 +823,11 @@ extern "C" int rgbac_residual_unit_ex(const rgbac_ru_args* args, int ngroups, in
                 "H and W must be positive multiples of 8");
   RuArgsDev d{};
   d.batch = a->batch; d.H = a->h; d.W = a->w; d.ngroups = ngroups;
+  static const int stagger_env = [] {
+    const char* e = getenv("RGBAC_RU_STAGGER");
+    return e ? atoi(e) : 0;
+  }();
+  d.stagger = stagger_env;
   for (int i = 0; i < ngroups; ++i) {
     const rgbac_ru_args* q = &args[i];
     RGBAC_REQUIRE(q->dtype == a->dtype && q->channels == a->channels && q->batch == a->batch &&
@@ -826,6 +869,9 @@ extern "C" int rgbac_residual_unit_ex(const rgbac_ru_args* args, int ngroups, in
                     "grouped units must all be fragment-major (16-B aligned biases and out rows)");
     const long long tiles = (long long)a->batch * (a->h / 8) * (a->w / 16);
     RGBAC_REQUIRE(tiles < (1ll << 31), "too many tiles");
+    for (int i = 0; i < ngroups; ++i)
+      RGBAC_REQUIRE((long long)a->batch * a->h * a->w * args[i].x_ldc < (1ll << 31),
+                    "the streamed unit addresses x with 32-bit element offsets");
     if (kind) hipLaunchKernelGGL(ru_stream_kernel<1>, dim3((unsigned)tiles, 1, ngroups), dim3(256), 0, st, d);
     else hipLaunchKernelGGL(ru_stream_kernel<0>, dim3((unsigned)tiles, 1, ngroups), dim3(256), 0, st, d);
     return check_launch("ru_stream_kernel");

@@ -386,6 +386,218 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WgradDev a) {
   if (do_bias && tid < 64) a.bpart[(size_t)split * a.n_pad + n0 + tid] = bacc;
 }
 
+// ---------------------------------------------------------------------------------------
+// Ring-pipelined weight gradient (bf16, no squared input): the same 64(n) x BK(k) tiles, wave
+// layout, LDS images (pixel rows, XOR-swizzled 16-B chunks) and transposed fragment reads as
+// wgrad_kernel, but every stage is moved global -> LDS by LDS-DMA (global_load_lds_dwordx4,
+// 1 KiB per wave instruction, no register staging) into a WR-deep ring, so the loads of the
+// next WR-1 stages are in flight while a stage's MFMAs run.  wgrad_kernel stages through
+// registers one stage ahead: each 64-pixel stage (256 MFMA cycles per wave) waited for a full
+// global-memory round trip (~2k cycles under load) -- 4-6 % of the MFMA peak.
+//   A DMA piece is 1 KiB of one stage image: lane l writes image byte 16 l of the piece, i.e.
+//   row r = (piece rows) + l / chunks-per-row, slot l % chunks-per-row, which holds chunk
+//   c = slot ^ swz(r) (the swizzle is an involution) -- so each lane fetches the global
+//   16-byte chunk c of its row directly; out-of-range pixels / channels / taps read a zero page.
+//   The per-lane (tap, channel, source) of every S piece is fixed over the stages; the pixel of
+//   a piece row is decoded per stage.
+__device__ uint4 g_wgrad_zero[64];
+
+typedef __attribute__((address_space(3))) void* wg_lptr_t;
+
+__device__ __forceinline__ void wg_dma16(const void* src, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wg_wait_vm() {
+  static_assert(N >= 0 && N <= 63, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// retire the oldest ring stage with `after` later stages (PW pieces each) in flight
+template <int PW, int D>
+__device__ __forceinline__ void wg_wait_ring(int after) {
+  if constexpr (D <= 0) {
+    wg_wait_vm<0>();
+  } else {
+    if (after >= D) wg_wait_vm<PW * D>();
+    else wg_wait_ring<PW, D - 1>(after);
+  }
+}
+
+template <int KT, int WR>
+__global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
+  constexpr int BK = 32 * KT;
+  constexpr int RSG = 128, RSS = BK * 2;          // LDS row bytes (G: 64 channels, S: BK k)
+  constexpr int GB = 64 * RSG, SB = 64 * RSS;     // stage image bytes
+  constexpr int CRS = RSS / 16;                   // 16-B chunks per S row (8 or 16)
+  constexpr int RPS = 64 / CRS;                   // S rows per 1-KiB piece (8 or 4)
+  constexpr int PG = 2, PS = SB / 1024 / 4;       // pieces per wave per stage (G, S)
+  constexpr int PW = PG + PS;
+  __shared__ __attribute__((aligned(16))) unsigned char ring[WR * (GB + SB)];
+  __shared__ float bred[4][64];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int k0 = blockIdx.x * BK, n0 = blockIdx.y * 64, split = blockIdx.z;
+  const int mbeg = split * a.m_chunk;
+  const int mend = min(mbeg + a.m_chunk, a.M);
+  const bool do_bias = a.bpart && blockIdx.x == 0;
+  auto swzG = [](int r) { return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1); };
+  auto swzS = [](int r) {
+    if constexpr (BK == 64) return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1);
+    else return 2 * ((r & 3) + 4 * ((r >> 3) & 1));
+  };
+
+  // ---- per-lane DMA geometry, fixed over the stages
+  int grow[PG];
+  const char* gsrc[PG];
+  bool gok[PG];
+#pragma unroll
+  for (int j = 0; j < PG; ++j) {
+    const int q = wave + 4 * j;                   // G piece = rows 8q .. 8q+7
+    grow[j] = 8 * q + (lane >> 3);
+    const int c = (lane & 7) ^ swzG(grow[j]);
+    const int n = n0 + 8 * c;
+    gok[j] = n < a.gch;
+    gsrc[j] = reinterpret_cast<const char*>(a.g) + (size_t)(gok[j] ? n : 0) * 2;
+  }
+  int srow[PS], sdy[PS], sdx[PS], sld[PS];
+  const char* ssrc[PS];
+  bool sok[PS];
+#pragma unroll
+  for (int j = 0; j < PS; ++j) {
+    const int q = wave + 4 * j;                   // S piece = rows RPS q .. RPS q + RPS - 1
+    srow[j] = RPS * q + lane / CRS;
+    const int c = (lane % CRS) ^ swzS(srow[j]);
+    const int k = k0 + 8 * c;
+    const int tap = k / a.cin_pad, ci = k - (k / a.cin_pad) * a.cin_pad;
+    sdy[j] = tap / a.ksize - a.pad;
+    sdx[j] = tap % a.ksize - a.pad;
+    const char* base;
+    int ld, cs;
+    if (ci < a.send0) { base = (const char*)a.sp0; ld = (int)a.sld0; cs = ci; }
+    else if (ci < a.send1) { base = (const char*)a.sp1; ld = (int)a.sld1; cs = ci - a.send0; }
+    else { base = (const char*)a.sp2; ld = (int)a.sld2; cs = ci - a.send1; }
+    sok[j] = k < a.K && ci < a.send2;
+    ssrc[j] = base + (size_t)(sok[j] ? cs : 0) * 2;
+    sld[j] = ld * 2;                              // bytes per source pixel
+  }
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(wg_lptr_t)ring);
+  const int ldg2 = (int)a.ldg * 2;
+
+  auto issue = [&](int st) {                      // DMA stage st into ring slot st % WR
+    const int mb = mbeg + st * 64;
+    const uint32_t lg = lbase + (uint32_t)((st % WR) * (GB + SB));
+    const uint32_t ls = lg + GB;
+#pragma unroll
+    for (int j = 0; j < PG; ++j) {
+      const int m = mb + grow[j];
+      const bool ok = gok[j] && m < mend;
+      wg_dma16(ok ? (const void*)(gsrc[j] + (size_t)m * ldg2) : (const void*)g_wgrad_zero,
+               lg + (uint32_t)((wave + 4 * j) * 1024));
+    }
+#pragma unroll
+    for (int j = 0; j < PS; ++j) {
+      const int m = mb + srow[j];
+      const int t = wdiv(m, a.Wg, a.rWg);
+      const int x = m - t * a.Wg;
+      const int b = wdiv(t, a.Hg, a.rHg);
+      const int y = t - b * a.Hg;
+      const int iy = y * a.stride + sdy[j], ix = x * a.stride + sdx[j];
+      const bool ok = sok[j] && m < mend && (unsigned)iy < (unsigned)a.in_h &&
+                      (unsigned)ix < (unsigned)a.in_w;
+      const size_t pix = ok ? (size_t)((b * a.in_h + iy) * a.in_w + ix) : 0;
+      wg_dma16(ok ? (const void*)(ssrc[j] + pix * sld[j]) : (const void*)g_wgrad_zero,
+               ls + (uint32_t)((wave + 4 * j) * 1024));
+    }
+  };
+
+  f32x4 acc[2][KT];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < KT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc = 0.0f;
+  const int wn = wave >> 1, wk = wave & 1;
+  const int fi = lane & 15, fq = lane >> 4;
+  const int nst = mend > mbeg ? (mend - mbeg + 63) / 64 : 0;
+  for (int st = 0; st < WR - 1; ++st)
+    if (st < nst) issue(st);
+  for (int it = 0; it < nst; ++it) {
+    wg_wait_ring<PW, WR - 2>(min(WR - 2, nst - 1 - it));
+    __syncthreads();                              // stage it landed for every wave; slot
+                                                  // (it - 1) % WR is free again
+    if (it + WR - 1 < nst) issue(it + WR - 1);
+    const unsigned char* Gs = ring + (it % WR) * (GB + SB);
+    const unsigned char* Ss = Gs + GB;
+    if (do_bias) {                                // G column sums: 4 row groups x 64 channels
+      const int c = tid & 63, rg = tid >> 6;
+#pragma unroll 4
+      for (int r = 16 * rg; r < 16 * rg + 16; ++r)
+        bacc += bf2f(*reinterpret_cast<const uint16_t*>(
+            Gs + r * RSG + 16 * ((c >> 3) ^ swzG(r)) + (c & 7) * 2));
+    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      uint4 A[2], B[KT];
+      const int ra = kk * 32 + 8 * fq + (fi >> 2);
+      const int cq = fi & 3;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int ncol = wn * 32 + t * 16 + 4 * cq;
+        const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_v4s_ptr)(Gs + ra * RSG + 16 * ((ncol >> 3) ^ swzG(ra)) + (ncol & 7) * 2));
+        const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_v4s_ptr)(Gs + (ra + 4) * RSG + 16 * ((ncol >> 3) ^ swzG(ra + 4)) + (ncol & 7) * 2));
+        const uint2 ua0 = __builtin_bit_cast(uint2, a0), ua1 = __builtin_bit_cast(uint2, a1);
+        A[t] = make_uint4(ua0.x, ua0.y, ua1.x, ua1.y);
+      }
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const int kcol = wk * 16 * KT + t * 16 + 4 * cq;
+        const v4s b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_v4s_ptr)(Ss + ra * RSS + 16 * ((kcol >> 3) ^ swzS(ra)) + (kcol & 7) * 2));
+        const v4s b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_v4s_ptr)(Ss + (ra + 4) * RSS + 16 * ((kcol >> 3) ^ swzS(ra + 4)) + (kcol & 7) * 2));
+        const uint2 ub0 = __builtin_bit_cast(uint2, b0), ub1 = __builtin_bit_cast(uint2, b1);
+        B[t] = make_uint4(ub0.x, ub0.y, ub1.x, ub1.y);
+      }
+#pragma unroll
+      for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+        for (int tk = 0; tk < KT; ++tk) mma_step<bf16_t>(acc[tn][tk], A[tn], B[tk]);
+    }
+  }
+  float* P = a.part + (size_t)split * a.n_pad * a.k_pad;
+#pragma unroll
+  for (int tn = 0; tn < 2; ++tn)
+#pragma unroll
+    for (int tk = 0; tk < KT; ++tk)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + wn * 32 + tn * 16 + 4 * fq + r;
+        const int k = k0 + wk * 16 * KT + tk * 16 + fi;
+        if (k < a.k_pad) P[(size_t)n * a.k_pad + k] = acc[tn][tk][r];
+      }
+  if (do_bias) {
+    bred[tid >> 6][tid & 63] = bacc;
+    __syncthreads();
+    if (tid < 64)
+      a.bpart[(size_t)split * a.n_pad + n0 + tid] =
+          ((bred[0][tid] + bred[1][tid]) + bred[2][tid]) + bred[3][tid];
+  }
+}
+
 // Slab reduction in the slab's own (coalesced) order: for slab position e (row n,
 // column k of the packed layout), dw[fmap[e]] = sum_s part[s][e] (fmap < 0: a pad
 // slot, skipped; every parameter element owns exactly one slot);
@@ -1120,6 +1332,17 @@ extern "C" int rgbac_conv_wgrad(const rgbac_wgrad_args* a, void* stream) {
   // 64 x 128 tiles when K is wide (8 MFMAs per k-step per wave on 12 transposed reads)
   const bool wide = a->dtype == RGBAC_BF16 && a->k_pad >= 512;
   dim3 grid(wide ? (a->k_pad + 127) / 128 : a->k_pad / 64, a->n_pad / 64, a->nsplit);
+  // bf16 without the squared input: the LDS-DMA ring kernel (RGBAC_WGRAD_RING=0: the
+  // register-staged kernel, A/B switch)
+  static const bool ring_env = [] {
+    const char* e = getenv("RGBAC_WGRAD_RING");
+    return !(e && e[0] == '0');
+  }();
+  if (a->dtype == RGBAC_BF16 && !a->square_input && ring_env) {
+    if (wide) hipLaunchKernelGGL((wgrad_ring_kernel<4, 3>), grid, dim3(256), 0, st, d);
+    else hipLaunchKernelGGL((wgrad_ring_kernel<2, 4>), grid, dim3(256), 0, st, d);
+    return check_launch("wgrad_ring_kernel");
+  }
   if (a->dtype == RGBAC_F32)
     hipLaunchKernelGGL((wgrad_kernel<float, 2>), grid, dim3(256), 0, st, d);
   else if (wide)
