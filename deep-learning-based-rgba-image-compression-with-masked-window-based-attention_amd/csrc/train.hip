@@ -494,31 +494,64 @@ __global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
   }
   const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(wg_lptr_t)ring);
   const int ldg2 = (int)a.ldg * 2;
+  // pixel (b, y, x) of every S piece row for the next stage to issue: decoded once, then
+  // advanced by 64 pixels per stage (no per-stage division); 1x1 stride-1: the M index is the
+  // source pixel index
+  const bool pdirect = a.ksize == 1 && a.stride == 1;
+  const int adx = 64 % a.Wg, ady = 64 / a.Wg;
+  int pb[PS], py[PS], px[PS];
+#pragma unroll
+  for (int j = 0; j < PS; ++j) {
+    const int m = mbeg + srow[j];
+    const int t = wdiv(m, a.Wg, a.rWg);
+    px[j] = m - t * a.Wg;
+    pb[j] = wdiv(t, a.Hg, a.rHg);
+    py[j] = t - pb[j] * a.Hg;
+  }
 
+  // G piece addresses advance by 64 pixel rows per stage; stride-1 S piece addresses too
+  // (source pixel = M pixel + dy * W + dx on the same grid), only their bounds test needs the
+  // (y, x) state.  Stride 2 recomputes the source pixel from (b, y, x).
+  const bool s1 = a.stride == 1;
+  const char* gp[PG];
+  const char* sp[PS];
+  const void* const zp = (const void*)g_wgrad_zero;
+#pragma unroll
+  for (int j = 0; j < PG; ++j) gp[j] = gsrc[j] + (size_t)(mbeg + grow[j]) * ldg2;
+#pragma unroll
+  for (int j = 0; j < PS; ++j)
+    sp[j] = ssrc[j] + (long long)(mbeg + srow[j] + sdy[j] * a.in_w + sdx[j]) * sld[j];
+  const size_t gstep = (size_t)64 * ldg2;
   auto issue = [&](int st) {                      // DMA stage st into ring slot st % WR
     const int mb = mbeg + st * 64;
     const uint32_t lg = lbase + (uint32_t)((st % WR) * (GB + SB));
     const uint32_t ls = lg + GB;
 #pragma unroll
     for (int j = 0; j < PG; ++j) {
-      const int m = mb + grow[j];
-      const bool ok = gok[j] && m < mend;
-      wg_dma16(ok ? (const void*)(gsrc[j] + (size_t)m * ldg2) : (const void*)g_wgrad_zero,
-               lg + (uint32_t)((wave + 4 * j) * 1024));
+      const bool ok = gok[j] && mb + grow[j] < mend;
+      wg_dma16(ok ? (const void*)gp[j] : zp, lg + (uint32_t)((wave + 4 * j) * 1024));
+      gp[j] += gstep;
     }
 #pragma unroll
     for (int j = 0; j < PS; ++j) {
-      const int m = mb + srow[j];
-      const int t = wdiv(m, a.Wg, a.rWg);
-      const int x = m - t * a.Wg;
-      const int b = wdiv(t, a.Hg, a.rHg);
-      const int y = t - b * a.Hg;
-      const int iy = y * a.stride + sdy[j], ix = x * a.stride + sdx[j];
-      const bool ok = sok[j] && m < mend && (unsigned)iy < (unsigned)a.in_h &&
+      const int iy = py[j] * a.stride + sdy[j], ix = px[j] * a.stride + sdx[j];
+      const bool ok = sok[j] && mb + srow[j] < mend && (unsigned)iy < (unsigned)a.in_h &&
                       (unsigned)ix < (unsigned)a.in_w;
-      const size_t pix = ok ? (size_t)((b * a.in_h + iy) * a.in_w + ix) : 0;
-      wg_dma16(ok ? (const void*)(ssrc[j] + pix * sld[j]) : (const void*)g_wgrad_zero,
-               ls + (uint32_t)((wave + 4 * j) * 1024));
+      const void* src;
+      if (s1) {
+        src = ok ? (const void*)sp[j] : zp;
+        sp[j] += (size_t)64 * sld[j];
+      } else {
+        src = ok ? (const void*)(ssrc[j] + (size_t)((pb[j] * a.in_h + iy) * a.in_w + ix) * sld[j])
+                 : zp;
+      }
+      wg_dma16(src, ls + (uint32_t)((wave + 4 * j) * 1024));
+      if (!pdirect) {                             // advance to the next stage's pixel
+        px[j] += adx;
+        py[j] += ady;
+        if (px[j] >= a.Wg) { px[j] -= a.Wg; ++py[j]; }
+        while (py[j] >= a.Hg) { py[j] -= a.Hg; ++pb[j]; }
+      }
     }
   };
 
@@ -530,6 +563,20 @@ __global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
   float bacc = 0.0f;
   const int wn = wave >> 1, wk = wave & 1;
   const int fi = lane & 15, fq = lane >> 4;
+  int aoff[2], boff[KT];                          // per-lane fragment read offsets (bytes)
+  {
+    const int ra0 = 8 * fq + (fi >> 2), cq = fi & 3;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int ncol = wn * 32 + t * 16 + 4 * cq;
+      aoff[t] = ra0 * RSG + 16 * ((ncol >> 3) ^ swzG(ra0)) + (ncol & 7) * 2;
+    }
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      const int kcol = wk * 16 * KT + t * 16 + 4 * cq;
+      boff[t] = ra0 * RSS + 16 * ((kcol >> 3) ^ swzS(ra0)) + (kcol & 7) * 2;
+    }
+  }
   const int nst = mend > mbeg ? (mend - mbeg + 63) / 64 : 0;
   for (int st = 0; st < WR - 1; ++st)
     if (st < nst) issue(st);
@@ -550,25 +597,21 @@ __global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       uint4 A[2], B[KT];
-      const int ra = kk * 32 + 8 * fq + (fi >> 2);
-      const int cq = fi & 3;
+      // rows ra0 + 32 kk + 4 h share ra0's swizzle (it reads row bits 0, 1, 3 only): one
+      // per-lane offset per fragment column, the row step a compile-time immediate
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
-        const int ncol = wn * 32 + t * 16 + 4 * cq;
-        const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_v4s_ptr)(Gs + ra * RSG + 16 * ((ncol >> 3) ^ swzG(ra)) + (ncol & 7) * 2));
-        const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_v4s_ptr)(Gs + (ra + 4) * RSG + 16 * ((ncol >> 3) ^ swzG(ra + 4)) + (ncol & 7) * 2));
+        const unsigned char* q = Gs + aoff[t] + kk * 32 * RSG;
+        const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)q);
+        const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)(q + 4 * RSG));
         const uint2 ua0 = __builtin_bit_cast(uint2, a0), ua1 = __builtin_bit_cast(uint2, a1);
         A[t] = make_uint4(ua0.x, ua0.y, ua1.x, ua1.y);
       }
 #pragma unroll
       for (int t = 0; t < KT; ++t) {
-        const int kcol = wk * 16 * KT + t * 16 + 4 * cq;
-        const v4s b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_v4s_ptr)(Ss + ra * RSS + 16 * ((kcol >> 3) ^ swzS(ra)) + (kcol & 7) * 2));
-        const v4s b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-            (lds_v4s_ptr)(Ss + (ra + 4) * RSS + 16 * ((kcol >> 3) ^ swzS(ra + 4)) + (kcol & 7) * 2));
+        const unsigned char* q = Ss + boff[t] + kk * 32 * RSS;
+        const v4s b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)q);
+        const v4s b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)(q + 4 * RSS));
         const uint2 ub0 = __builtin_bit_cast(uint2, b0), ub1 = __builtin_bit_cast(uint2, b1);
         B[t] = make_uint4(ub0.x, ub0.y, ub1.x, ub1.y);
       }
