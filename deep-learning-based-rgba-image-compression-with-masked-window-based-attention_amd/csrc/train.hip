@@ -434,25 +434,32 @@ __device__ __forceinline__ void wg_wait_ring(int after) {
   }
 }
 
-template <int KT, int WR>
+template <int TN, int KT, int WR>
 __global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
-  constexpr int BK = 32 * KT;
-  constexpr int RSG = 128, RSS = BK * 2;          // LDS row bytes (G: 64 channels, S: BK k)
+  constexpr int BN = 32 * TN, BK = 32 * KT;
+  constexpr int RSG = BN * 2, RSS = BK * 2;       // LDS row bytes (G: BN channels, S: BK k)
   constexpr int GB = 64 * RSG, SB = 64 * RSS;     // stage image bytes
   constexpr int CRS = RSS / 16;                   // 16-B chunks per S row (8 or 16)
   constexpr int RPS = 64 / CRS;                   // S rows per 1-KiB piece (8 or 4)
-  constexpr int PG = 2, PS = SB / 1024 / 4;       // pieces per wave per stage (G, S)
+  constexpr int CRG = RSG / 16, RPG = 64 / CRG;   // the same for G rows
+  constexpr int PG = GB / 1024 / 4, PS = SB / 1024 / 4;   // pieces per wave per stage (G, S)
   constexpr int PW = PG + PS;
   __shared__ __attribute__((aligned(16))) unsigned char ring[WR * (GB + SB)];
-  __shared__ float bred[4][64];
+  __shared__ float bred[256 / BN][BN];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int k0 = blockIdx.x * BK, n0 = blockIdx.y * 64, split = blockIdx.z;
+  const int k0 = blockIdx.x * BK, n0 = blockIdx.y * BN, split = blockIdx.z;
   const int mbeg = split * a.m_chunk;
   const int mend = min(mbeg + a.m_chunk, a.M);
   const bool do_bias = a.bpart && blockIdx.x == 0;
-  auto swzG = [](int r) { return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1); };
+  // 128-B rows: chunk c of row r at c ^ (2 r1 + 4 r3); 256-B rows: c ^ 2 (r&3 + 4 r3)
+  // (r_i = bit i of r): conflict-free transposed reads, and rows r + 4 h + 32 kk keep r's
+  // swizzle (only row bits 0, 1, 3 enter it)
+  auto swzG = [](int r) {
+    if constexpr (BN == 64) return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1);
+    else return 2 * ((r & 3) + 4 * ((r >> 3) & 1));
+  };
   auto swzS = [](int r) {
     if constexpr (BK == 64) return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1);
     else return 2 * ((r & 3) + 4 * ((r >> 3) & 1));
@@ -464,9 +471,9 @@ __global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
   bool gok[PG];
 #pragma unroll
   for (int j = 0; j < PG; ++j) {
-    const int q = wave + 4 * j;                   // G piece = rows 8q .. 8q+7
-    grow[j] = 8 * q + (lane >> 3);
-    const int c = (lane & 7) ^ swzG(grow[j]);
+    const int q = wave + 4 * j;                   // G piece = rows RPG q .. RPG q + RPG - 1
+    grow[j] = RPG * q + lane / CRG;
+    const int c = (lane % CRG) ^ swzG(grow[j]);
     const int n = n0 + 8 * c;
     gok[j] = n < a.gch;
     gsrc[j] = reinterpret_cast<const char*>(a.g) + (size_t)(gok[j] ? n : 0) * 2;
@@ -555,20 +562,20 @@ __global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
     }
   };
 
-  f32x4 acc[2][KT];
+  f32x4 acc[TN][KT];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TN; ++i)
 #pragma unroll
     for (int j = 0; j < KT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bacc = 0.0f;
   const int wn = wave >> 1, wk = wave & 1;
   const int fi = lane & 15, fq = lane >> 4;
-  int aoff[2], boff[KT];                          // per-lane fragment read offsets (bytes)
+  int aoff[TN], boff[KT];                         // per-lane fragment read offsets (bytes)
   {
     const int ra0 = 8 * fq + (fi >> 2), cq = fi & 3;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int ncol = wn * 32 + t * 16 + 4 * cq;
+    for (int t = 0; t < TN; ++t) {
+      const int ncol = wn * 16 * TN + t * 16 + 4 * cq;
       aoff[t] = ra0 * RSG + 16 * ((ncol >> 3) ^ swzG(ra0)) + (ncol & 7) * 2;
     }
 #pragma unroll
@@ -587,20 +594,21 @@ __global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
     if (it + WR - 1 < nst) issue(it + WR - 1);
     const unsigned char* Gs = ring + (it % WR) * (GB + SB);
     const unsigned char* Ss = Gs + GB;
-    if (do_bias) {                                // G column sums: 4 row groups x 64 channels
-      const int c = tid & 63, rg = tid >> 6;
+    if (do_bias) {                                // G column sums: row groups x BN channels
+      constexpr int NRG = 256 / BN, RPR = 64 / NRG;
+      const int c = tid % BN, rg = tid / BN;
 #pragma unroll 4
-      for (int r = 16 * rg; r < 16 * rg + 16; ++r)
+      for (int r = RPR * rg; r < RPR * rg + RPR; ++r)
         bacc += bf2f(*reinterpret_cast<const uint16_t*>(
             Gs + r * RSG + 16 * ((c >> 3) ^ swzG(r)) + (c & 7) * 2));
     }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      uint4 A[2], B[KT];
+      uint4 A[TN], B[KT];
       // rows ra0 + 32 kk + 4 h share ra0's swizzle (it reads row bits 0, 1, 3 only): one
       // per-lane offset per fragment column, the row step a compile-time immediate
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
+      for (int t = 0; t < TN; ++t) {
         const unsigned char* q = Gs + aoff[t] + kk * 32 * RSG;
         const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)q);
         const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)(q + 4 * RSG));
@@ -616,28 +624,32 @@ __global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
         B[t] = make_uint4(ub0.x, ub0.y, ub1.x, ub1.y);
       }
 #pragma unroll
-      for (int tn = 0; tn < 2; ++tn)
+      for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
         for (int tk = 0; tk < KT; ++tk) mma_step<bf16_t>(acc[tn][tk], A[tn], B[tk]);
     }
   }
   float* P = a.part + (size_t)split * a.n_pad * a.k_pad;
 #pragma unroll
-  for (int tn = 0; tn < 2; ++tn)
+  for (int tn = 0; tn < TN; ++tn)
 #pragma unroll
     for (int tk = 0; tk < KT; ++tk)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int n = n0 + wn * 32 + tn * 16 + 4 * fq + r;
+        const int n = n0 + wn * 16 * TN + tn * 16 + 4 * fq + r;
         const int k = k0 + wk * 16 * KT + tk * 16 + fi;
-        if (k < a.k_pad) P[(size_t)n * a.k_pad + k] = acc[tn][tk][r];
+        if (k < a.k_pad && n < a.n_pad) P[(size_t)n * a.k_pad + k] = acc[tn][tk][r];
       }
   if (do_bias) {
-    bred[tid >> 6][tid & 63] = bacc;
+    constexpr int NRG = 256 / BN;
+    bred[tid / BN][tid % BN] = bacc;
     __syncthreads();
-    if (tid < 64)
-      a.bpart[(size_t)split * a.n_pad + n0 + tid] =
-          ((bred[0][tid] + bred[1][tid]) + bred[2][tid]) + bred[3][tid];
+    if (tid < BN && n0 + tid < a.n_pad) {
+      float sum = bred[0][tid];
+#pragma unroll
+      for (int g2 = 1; g2 < NRG; ++g2) sum += bred[g2][tid];
+      a.bpart[(size_t)split * a.n_pad + n0 + tid] = sum;
+    }
   }
 }
 
@@ -1382,8 +1394,13 @@ extern "C" int rgbac_conv_wgrad(const rgbac_wgrad_args* a, void* stream) {
     return !(e && e[0] == '0');
   }();
   if (a->dtype == RGBAC_BF16 && !a->square_input && ring_env) {
-    if (wide) hipLaunchKernelGGL((wgrad_ring_kernel<4, 3>), grid, dim3(256), 0, st, d);
-    else hipLaunchKernelGGL((wgrad_ring_kernel<2, 4>), grid, dim3(256), 0, st, d);
+    // (128 x 128 tiles, wgrad_ring_kernel<4, 4, 3>: one workgroup per CU -- measured no faster
+    // on the slice-stack shapes and -4 % on the training step, so not dispatched)
+    if (wide) {
+      hipLaunchKernelGGL((wgrad_ring_kernel<2, 4, 3>), grid, dim3(256), 0, st, d);
+    } else {
+      hipLaunchKernelGGL((wgrad_ring_kernel<2, 2, 4>), grid, dim3(256), 0, st, d);
+    }
     return check_launch("wgrad_ring_kernel");
   }
   if (a->dtype == RGBAC_F32)
