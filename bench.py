@@ -737,8 +737,9 @@ def main_forward(args, world, rank, dev, dist):
         if args.layers:
             write_layers(prof, args.layers, nrep)
         traffic_file = args.traffic_file
-        if traffic_file is None:
-            traffic_file = latest_profile("pmc_traffic_fwd.json")
+        if traffic_file is None:                       # a summary taken on this workload
+            traffic_file = (latest_profile(f"pmc_traffic_fwd_b{B}_{S}.json") or
+                            latest_profile("pmc_traffic_fwd.json"))
         roof, total_ms = roofline_of(summ, args.dtype, nrep, traffic_file,
                                      {"batch": B, "size": S, "dtype": args.dtype})
         roof["timing"] = "eager steps behind a GPU spin, fence-free HIP events per launch"

@@ -7,7 +7,7 @@ so it is doubled; WRITE_SIZE is taken as is.  Only dispatches inside the replay 
 the first spin kernel) are counted.  Output: JSON {short kernel name: {...}} keyed like
 bench.py's roofline kernel names.
 
-  python tools/pmc_traffic.py FETCH.csv WRITE.csv OUT.json
+  python tools/pmc_traffic.py FETCH.csv WRITE.csv OUT.json [BATCH SIZE]
 """
 import csv
 import json
@@ -42,7 +42,7 @@ def per_dispatch(path, counter):
     return acc
 
 
-def main(fetch_csv, write_csv, out):
+def main(fetch_csv, write_csv, out, batch=8, size=256):
     f = per_dispatch(fetch_csv, "FETCH_SIZE")
     w = per_dispatch(write_csv, "WRITE_SIZE")
     res = {}
@@ -57,11 +57,11 @@ def main(fetch_csv, write_csv, out):
     with open(out, "w") as fh:
         json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) over "
                              "tools/graph_trace.py forward graph replays; FETCH_SIZE x2 (gfx950)",
-                   "config": {"batch": 8, "size": 256, "dtype": "bf16"},
+                   "config": {"batch": int(batch), "size": int(size), "dtype": "bf16"},
                    "kernels": res}, fh, indent=1)
     for k, v in sorted(res.items(), key=lambda kv: -kv[1]["hbm_bytes_per_dispatch"]):
         print(f"{v['hbm_bytes_per_dispatch'] / 1e6:9.2f} MB/dispatch  {k}")
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    main(*sys.argv[1:6])
