@@ -793,17 +793,46 @@ winattn_bwd_kernel(int batch, int H, int W, int C, int heads, int shift, int mas
       gs[t * DP + j] = g;
     }
     __syncthreads();
-    // ---- scores (same arithmetic as the forward) and dP = dO V^T
+    // ---- scores (same arithmetic as the forward) and dP = dO V^T: each thread a CB x CB
+    // block of (token, key) pairs of one window, so a q-step's 2 CB row / column values feed
+    // 2 CB^2 FMAs from registers (one LDS read per FMA in the 1 x 1 form)
     const float* bh = bias + (size_t)h * N * N;
-    for (int e = tid; e < 64 * N; e += 256) {
-      const int i = e / N, j = e - i * N;
-      const int wbase = (i / N) * N;
-      const int li = i - wbase;
-      float s = 0.f, dp = 0.f;
+    constexpr int CB = (N == 64) ? 4 : 2;          // 64 x N pairs = 256 threads x CB^2
+    constexpr int TPR = N / CB;
+    {
+      const int i0 = (tid / TPR) * CB, j0 = (tid % TPR) * CB;
+      const int wb0 = (i0 / N) * N;
+      float sb[CB][CB], db[CB][CB];
+#pragma unroll
+      for (int r = 0; r < CB; ++r)
+#pragma unroll
+        for (int c = 0; c < CB; ++c) { sb[r][c] = 0.f; db[r][c] = 0.f; }
       for (int q = 0; q < d; ++q) {
-        s = fmaf(qs[i * DP + q], ks[(wbase + j) * DP + q], s);
-        dp = fmaf(gs[i * DP + q], vs[(wbase + j) * DP + q], dp);
+        float qv[CB], gv[CB], kv[CB], vv[CB];
+#pragma unroll
+        for (int r = 0; r < CB; ++r) {
+          qv[r] = qs[(i0 + r) * DP + q];
+          gv[r] = gs[(i0 + r) * DP + q];
+          kv[r] = ks[(wb0 + j0 + r) * DP + q];
+          vv[r] = vs[(wb0 + j0 + r) * DP + q];
+        }
+#pragma unroll
+        for (int r = 0; r < CB; ++r)
+#pragma unroll
+          for (int c = 0; c < CB; ++c) {
+            sb[r][c] = fmaf(qv[r], kv[c], sb[r][c]);
+            db[r][c] = fmaf(gv[r], vv[c], db[r][c]);
+          }
       }
+#pragma unroll
+      for (int r = 0; r < CB; ++r)
+#pragma unroll
+        for (int c = 0; c < CB; ++c) {
+      const int i = i0 + r, j = j0 + c;
+      const int wbase = wb0;
+      const int li = i - wbase;
+      float s = sb[r][c];
+      const float dp = db[r][c];
       s += bh[li * N + j];
       if (shift > 0) {
         const int wi = i / N;
@@ -821,6 +850,7 @@ winattn_bwd_kernel(int batch, int H, int W, int C, int heads, int shift, int mas
       if (amask) s += amask[((size_t)((grp * NWIN + i / N) % amask_nw) * N + li) * N + j];
       P[i * (N + 1) + j] = s;
       G[i * (N + 1) + j] = dp;
+        }
     }
     __syncthreads();
     // ---- softmax rows and D_i = sum_j P dP (4 lanes per row)
@@ -869,24 +899,44 @@ winattn_bwd_kernel(int batch, int H, int W, int C, int heads, int shift, int mas
         for (int w = 0; w < NWIN; ++w) bacc[r] += G[(w * N + li) * (N + 1) + j];
       }
     }
-    // ---- dq, dk, dv at the tokens' original pixels
-    for (int e = tid; e < 64 * d; e += 256) {
-      const int i = e / d, c = e - i * d;
+    // ---- dq, dk, dv at the tokens' original pixels: thread = (token i, a quarter of the head
+    // channels); per key j the three dS / P scalars are read once for up to 6 channels
+    {
+      constexpr int MAXC = 6;                      // d <= 24 (host-checked)
+      const int i = tid >> 2, cpt = (d + 3) >> 2, c0 = (tid & 3) * cpt;
       const int wbase = (i / N) * N;
       const int li = i - wbase;
-      float dq = 0.f, dk = 0.f, dv = 0.f;
+      float dq[MAXC], dk[MAXC], dv[MAXC];
+#pragma unroll
+      for (int k = 0; k < MAXC; ++k) { dq[k] = 0.f; dk[k] = 0.f; dv[k] = 0.f; }
       for (int j = 0; j < N; ++j) {
-        dq = fmaf(G[i * (N + 1) + j], ks[(wbase + j) * DP + c], dq);
-        dk = fmaf(G[(wbase + j) * (N + 1) + li], qs[(wbase + j) * DP + c], dk);
-        dv = fmaf(P[(wbase + j) * (N + 1) + li], gs[(wbase + j) * DP + c], dv);
+        const float gij = G[i * (N + 1) + j];
+        const float gji = G[(wbase + j) * (N + 1) + li];
+        const float pji = P[(wbase + j) * (N + 1) + li];
+        const float* kr = ks + (wbase + j) * DP + c0;
+        const float* qr = qs + (wbase + j) * DP + c0;
+        const float* gr = gs + (wbase + j) * DP + c0;
+#pragma unroll
+        for (int k = 0; k < MAXC; ++k)
+          if (k < cpt) {
+            dq[k] = fmaf(gij, kr[k], dq[k]);
+            dk[k] = fmaf(gji, qr[k], dk[k]);
+            dv[k] = fmaf(pji, gr[k], dv[k]);
+          }
       }
       const int pix = pix_s[i];
       if (pix >= 0) {
         const bool on = act_s[i / N] != 0;
-        T* row = dqkv + (long long)pix * lddq + h * d + c;
-        Elem<T>::st(row, on ? dq * scale : 0.0f);
-        Elem<T>::st(row + C, on ? dk : 0.0f);
-        Elem<T>::st(row + 2 * C, on ? dv : 0.0f);
+#pragma unroll
+        for (int k = 0; k < MAXC; ++k) {
+          const int c = c0 + k;
+          if (k < cpt && c < d) {
+            T* row = dqkv + (long long)pix * lddq + h * d + c;
+            Elem<T>::st(row, on ? dq[k] * scale : 0.0f);
+            Elem<T>::st(row + C, on ? dk[k] : 0.0f);
+            Elem<T>::st(row + 2 * C, on ? dv[k] : 0.0f);
+          }
+        }
       }
     }
     __syncthreads();
