@@ -349,6 +349,21 @@ __global__ void __launch_bounds__(256, OCC) ru_fused_kernel(const RuArgsDev args
 // T1 / T2 pixels are 128-B rows (64 channels, 40..63 zero), chunk c at slot c ^ (p & 7).
 // LDS 73 KiB weights + 22 KiB maps: one workgroup per CU, 4 waves; per wave 18 + 54 + 10
 // MFMAs.  Three launches (and two HBM round trips of the 40-channel maps) become one.
+typedef __attribute__((address_space(3))) void* ru_lptr_t;
+// one LDS-DMA piece: each lane moves 16 bytes from src to lds + 16 * lane (M0 saved / restored;
+// waited for by an explicit s_waitcnt)
+__device__ __forceinline__ void ru_dma16(const void* src, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
 namespace rus {
 constexpr int W1F = 9, W2F = 54, W3F = 10;            // fragments per matrix
 constexpr int HY = 10, HX = 10, NH = 100, NHP = 112;  // halo pixels (7 fragments)
@@ -372,12 +387,17 @@ __global__ void __launch_bounds__(256, 1) ru_small_kernel(const RuArgsDev args) 
   const int b = t / ty_n;
   const int y0 = ty * 8, x0 = tx * 8;
 
-  // weights: the three packs are contiguous per matrix (w1, w2, w3)
-  for (int e = tid; e < (W1F + W2F + W3F) * 64; e += 256) {
-    const uint4* src = e < W1F * 64 ? reinterpret_cast<const uint4*>(g.w1) + e
-                     : e < (W1F + W2F) * 64 ? reinterpret_cast<const uint4*>(g.w2) + (e - W1F * 64)
-                     : reinterpret_cast<const uint4*>(g.w3) + (e - (W1F + W2F) * 64);
-    Ws[e] = *src;
+  // weights: the three fragment-major packs (1 KiB per fragment) land in LDS by LDS-DMA, one
+  // piece per wave instruction with no wait in between -- the register-staged copy loop it
+  // replaces waited for an L2 round trip every few of its 18 iterations
+  {
+    const uint32_t lws = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(ru_lptr_t)Ws);
+    for (int pc = wave; pc < W1F + W2F + W3F; pc += 4) {
+      const uint4* src = pc < W1F ? reinterpret_cast<const uint4*>(g.w1) + pc * 64
+                       : pc < W1F + W2F ? reinterpret_cast<const uint4*>(g.w2) + (pc - W1F) * 64
+                       : reinterpret_cast<const uint4*>(g.w3) + (pc - W1F - W2F) * 64;
+      ru_dma16(src + lane, lws + (uint32_t)pc * 1024u);
+    }
   }
   for (int e = tid; e < 48 + 48 + 80; e += 256)
     bs[e] = e < 48 ? g.b1[e] : e < 96 ? g.b2[e - 48] : g.b3[e - 96];
@@ -406,6 +426,7 @@ __global__ void __launch_bounds__(256, 1) ru_small_kernel(const RuArgsDev args) 
                                       : make_uint4(0, 0, 0, 0);
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this wave's weight pieces landed
   __syncthreads();
 
   // ================= stage 1
