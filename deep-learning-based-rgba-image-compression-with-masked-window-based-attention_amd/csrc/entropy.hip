@@ -161,36 +161,50 @@ __global__ void __launch_bounds__(256)
 finalize_kernel(int mode, int batch, int nblk, double npix, const double* __restrict__ part,
                 const double* __restrict__ yb, int ny, const double* __restrict__ zb, int nz,
                 float* __restrict__ out) {
-  __shared__ double red[4];
+  // One block; every reduction is a wave reduction (shuffles, no barrier) and the four waves'
+  // results meet once in LDS, combined in wave order (fixed order: deterministic).  Wave w owns
+  // images w, w + 4, ...  (The block-wide form spent two barriers per image and bits term.)
+  __shared__ double wred[4][5];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double ys = 0.0, zs = 0.0;
   for (int i = threadIdx.x; i < ny; i += 256) ys += yb[i];
   for (int i = threadIdx.x; i < nz; i += 256) zs += zb[i];
-  ys = block_sum_f64(ys, red);
-  zs = block_sum_f64(zs, red);
+  for (int o = 32; o > 0; o >>= 1) {
+    ys += __shfl_xor(ys, o);
+    zs += __shfl_xor(zs, o);
+  }
   double mse_acc = 0.0, se_all = 0.0, cnt_all = 0.0;
-  for (int b = 0; b < batch; ++b) {
+  for (int b = wave; b < batch; b += 4) {
     double se = 0.0, cnt = 0.0;
-    for (int i = threadIdx.x; i < nblk; i += 256) {
+    for (int i = lane; i < nblk; i += 64) {
       se += part[((size_t)b * nblk + i) * 2 + 0];
       cnt += part[((size_t)b * nblk + i) * 2 + 1];
     }
-    se = block_sum_f64(se, red);
-    cnt = block_sum_f64(cnt, red);
-    if (threadIdx.x == 0) {
-      // per-image mean: torch.div(mse, clamp(num_unmasked, min=1)) in fp32
-      const float sef = (float)se, cf = fmaxf((float)cnt, 1.0f);
-      mse_acc += (double)(sef / cf);
-      se_all += se;
-      cnt_all += cnt;
+    for (int o = 32; o > 0; o >>= 1) {
+      se += __shfl_xor(se, o);
+      cnt += __shfl_xor(cnt, o);
     }
+    // per-image mean: torch.div(mse, clamp(num_unmasked, min=1)) in fp32
+    const float sef = (float)se, cf = fmaxf((float)cnt, 1.0f);
+    mse_acc += (double)(sef / cf);
+    se_all += se;
+    cnt_all += cnt;
   }
+  if (lane == 0) {
+    wred[wave][0] = ys; wred[wave][1] = zs; wred[wave][2] = mse_acc;
+    wred[wave][3] = se_all; wred[wave][4] = cnt_all;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
+    double t[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) t[k] = ((wred[0][k] + wred[1][k]) + wred[2][k]) + wred[3][k];
     float mse;
     if (mode == 0)
-      mse = (float)(mse_acc / batch);
+      mse = (float)(t[2] / batch);
     else
-      mse = (float)(se_all / cnt_all);
-    const float ybits = (float)ys, zbits = (float)zs;
+      mse = (float)(t[3] / t[4]);
+    const float ybits = (float)t[0], zbits = (float)t[1];
     const float yb_pp = ybits / (float)npix, zb_pp = zbits / (float)npix;
     out[0] = mse;
     out[1] = yb_pp + zb_pp;
