@@ -449,10 +449,24 @@ __global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int k0 = blockIdx.x * BK, n0 = blockIdx.y * BN, split = blockIdx.z;
+  // XCD-aware tile order: the hardware deals workgroup i to XCD i mod 8, so consecutive ids
+  // (the k tiles of one pixel split, which read the same G / S pixels) would land on 8
+  // different L2s and each fetch the pixels from HBM.  Remapped, an XCD runs a contiguous run
+  // of (k tile fastest, n tile, split) and its L2 serves the other k tiles' re-reads.
+  int kt, nt, split;
+  {
+    const int nwg = gridDim.x * gridDim.y * gridDim.z;
+    int t = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const int xcd = t & 7, q = nwg >> 3, r = nwg & 7;
+    t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (t >> 3);
+    kt = t % gridDim.x; t /= gridDim.x;
+    nt = t % gridDim.y;
+    split = t / gridDim.y;
+  }
+  const int k0 = kt * BK, n0 = nt * BN;
   const int mbeg = split * a.m_chunk;
   const int mend = min(mbeg + a.m_chunk, a.M);
-  const bool do_bias = a.bpart && blockIdx.x == 0;
+  const bool do_bias = a.bpart && kt == 0;
   // 128-B rows: chunk c of row r at c ^ (2 r1 + 4 r3); 256-B rows: c ^ 2 (r&3 + 4 r3)
   // (r_i = bit i of r): conflict-free transposed reads, and rows r + 4 h + 32 kk keep r's
   // swizzle (only row bits 0, 1, 3 enter it)
