@@ -32,6 +32,18 @@ __device__ __forceinline__ float t_cdf(float t) {       // 0.5 * erfc(-t / sqrt 
   return 0.5f * erfcf(-0.70710678118654752440f * t);
 }
 
+// e / d and e % d for 0 <= e < 2^50, d > 0, from a double reciprocal and one correction step
+// (the elementwise backward kernels' 64-bit integer division compiled to a ~100-instruction
+// software routine per element)
+__device__ __forceinline__ long long ediv(long long e, int d, double rd, int& rem) {
+  long long q = (long long)((double)e * rd);
+  long long r = e - q * d;
+  if (r < 0) { --q; r += d; }
+  else if (r >= d) { ++q; r -= d; }
+  rem = (int)r;
+  return q;
+}
+
 // ------------------------------------------------------------------ act_bwd
 // dz = dL/dv for y = act(v [, r1]); dr1 = dL/dr1 where r1 enters the activation
 // (GATE: y = r1*sigmoid(v); GDN: y = r1/sqrt(v); IGDN: y = r1*sqrt(v)).
@@ -91,10 +103,12 @@ act_bwd_kernel(int act, float slope, long long npix, int C, const T* __restrict_
                const uint8_t* __restrict__ sel, T* __restrict__ dz, long long lddz,
                T* __restrict__ dr1, long long lddr1) {
   const int q4 = (int)(lddz / 4);
+  const double rq4 = 1.0 / q4;
   const long long n = npix * q4;
   for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
-    const long long p = e / q4;
-    const int c0 = (int)(e - p * q4) * 4;
+    int cq;
+    const long long p = ediv(e, q4, rq4, cq);
+    const int c0 = cq * 4;
     float gz[4] = {0.f, 0.f, 0.f, 0.f}, gr[4] = {0.f, 0.f, 0.f, 0.f};
     if (c0 + 3 < C) {
       float g[4], v[4] = {0.f, 0.f, 0.f, 0.f}, a[4] = {0.f, 0.f, 0.f, 0.f};
@@ -999,9 +1013,10 @@ gaussian_bwd_kernel(long long n, int nch, const T* __restrict__ y, long long ldy
                     const T* __restrict__ dhat, long long lddh, T* __restrict__ dy, long long lddy,
                     T* __restrict__ dmu, long long lddmu, T* __restrict__ dsc, long long lddsc) {
   const float gb = *gbits;
+  const double rn = 1.0 / nch;
   for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
-    const long long pix = e / nch;
-    const int ch = (int)(e - pix * nch);
+    int ch;
+    const long long pix = ediv(e, nch, rn, ch);
     const float yv = Elem<T>::ld(y + pix * ldy + ch);
     const float mv = Elem<T>::ld(mu + pix * ldmu + ch);
     const float sv = Elem<T>::ld(sc + pix * lds + ch);
@@ -1258,13 +1273,12 @@ __global__ void __launch_bounds__(256)
 pixel_shuffle_kernel(int dir, int batch, int H, int W, int C, const T* __restrict__ in,
                      long long ldi, T* __restrict__ out, long long ldo) {
   const long long n = (long long)batch * H * W * 4 * C;
+  const double r4c = 1.0 / (4 * C), rw = 1.0 / W, rh = 1.0 / H;
   for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
-    const int cc = (int)(e % (4 * C));
-    const long long pix = e / (4 * C);
-    const int x = (int)(pix % W);
-    const long long t = pix / W;
-    const int y = (int)(t % H);
-    const int b = (int)(t / H);
+    int cc, x, y;
+    const long long pix = ediv(e, 4 * C, r4c, cc);
+    const long long t = ediv(pix, W, rw, x);
+    const int b = (int)ediv(t, H, rh, y);
     const int c = cc >> 2, i = (cc >> 1) & 1, j = cc & 1;
     const long long lo = pix * (dir == 0 ? ldi : ldo) + cc;
     const long long hi = ((long long)(b * 2 * H + 2 * y + i) * (2 * W) + 2 * x + j) * (dir == 0 ? ldo : ldi) + c;
@@ -1279,9 +1293,10 @@ __global__ void __launch_bounds__(256)
 channel_copy_kernel(long long npix, int C, const T* __restrict__ src, long long lds, int scoff,
                     T* __restrict__ dst, long long ldd, int dcoff) {
   const long long n = npix * C;
+  const double rc = 1.0 / C;
   for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
-    const long long p = e / C;
-    const int c = (int)(e - p * C);
+    int c;
+    const long long p = ediv(e, C, rc, c);
     dst[p * ldd + dcoff + c] = src[p * lds + scoff + c];
   }
 }
