@@ -634,7 +634,10 @@ class CatFn(Function):
         outs = []
         off = 0
         for c, shp in zip(ctx.Cs, ctx.shapes):
-            o = Feat(torch.zeros(shp, dtype=g.t.dtype, device=g.t.device), c)
+            # the copy writes channels [0, c) of every pixel: only channel padding (ldc > c)
+            # needs the zero fill (the slice supports are unpadded: ~140 fills per step saved)
+            alloc = torch.empty if shp[-1] == c else torch.zeros
+            o = Feat(alloc(shp, dtype=g.t.dtype, device=g.t.device), c)
             _copy(o, 0, g, off, c)
             off += c
             outs.append(o.t)
@@ -662,7 +665,8 @@ class SliceFn(Function):
     @staticmethod
     def backward(ctx, g):
         shp, Cin, coff, C = ctx.meta
-        o = Feat(torch.zeros(shp, dtype=g.dtype, device=g.device), Cin)
+        alloc = torch.empty if (coff == 0 and C == shp[-1]) else torch.zeros
+        o = Feat(alloc(shp, dtype=g.dtype, device=g.device), Cin)
         _copy(o, coff, Feat(g.contiguous(), C), 0, C)
         return o.t, None, None, None
 
