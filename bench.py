@@ -76,6 +76,19 @@ def rgb_net(latent_gain=LATENT_GAIN):
     return net
 
 
+def mask_net(latent_gain=LATENT_GAIN):
+    """Seed-234 random-init AutoEncoderMask_Journal with EncoderMask.7 (1x1 192 -> 80, the conv
+    feeding the last attention block and the latent) scaled by ``latent_gain``, for the same
+    reason as rgb_net: non-zero latent symbols."""
+    from rgbac.models.AutoEncoderMask_Journal import AutoEncoder
+    torch.manual_seed(234)
+    net = AutoEncoder().eval()
+    with torch.no_grad():
+        net.EncoderMask[7].weight.mul_(latent_gain)
+        net.EncoderMask[7].bias.mul_(latent_gain)
+    return net
+
+
 def host_cores():
     """CPU cores this process may run on (len(os.sched_getaffinity(0)))."""
     try:
@@ -137,24 +150,54 @@ def cpu_baseline(budget_s, S=256):
     return rec, outs
 
 
-def gpu_parity(net, dev, outs_ref, S=256):
+def gpu_parity(net, dev, outs_ref, S=256, account=False):
     """bpp / PSNR / MS-SSIM of the HIP forward (net's current compute dtype) on the parity
     sample, one image per forward, against the oracle's outputs ``outs_ref``
-    (trainRGB.py:289-311: PSNR from the model's masked MSE, MS-SSIM of the clamped x_hat)."""
+    (trainRGB.py:289-311: PSNR from the model's masked MSE, MS-SSIM of the clamped x_hat).
+    ``account`` (fp32 mode): per image, every latent symbol round(y - mu) compared with the
+    teacher-forced oracle (oracle/parity.py): flips, how many sit at near-ties, and the
+    teacher-forced PSNR / MS-SSIM / bpp deltas (outside the timed region, checker only)."""
     import math
     from rgbac.layers.SupplyMask import mask_pyramid
     from rgbac.metrics.ms_ssim_torch import ms_ssim
+    from rgbac.models._latent import debug_views
     x, a = parity_sample(S)
     d_bpp = d_psnr = d_ms = 0.0
     rel_bpp = 0.0
     per = []
+    acc = {"flips": 0, "near_tie_flips": 0, "far_flips": 0, "z_flips": 0, "z_far_flips": 0,
+           "symbols": 0, "nonzero_symbols": 0, "noise_floor": 0.0, "tf_max_abs_d_psnr_db": 0.0,
+           "tf_max_abs_d_ms_ssim": 0.0, "max_bits_unflipped_rel": 0.0}
+    sd = None
+    if account:
+        from oracle import parity
+        sd = {k: v.detach().cpu() for k, v in net.state_dict().items()}
     from rgbac import runtime as rt
     for i in range(x.shape[0]):
         xi, ai = x[i:i + 1].to(dev), a[i:i + 1].to(dev)
         _, me = mask_pyramid(ai, 4)
+        dbg = {} if account else None
         with torch.no_grad(), rt.fixed_tiles():        # shape-rule tiles: no autotune pass
-            o = net(xi, ai, ai, *me)
+            o = net(xi, ai, ai, *me, debug=dbg)
         bpp, mse = o[2].item(), o[1].item()
+        rec_acc = None
+        if account:
+            rep = parity.north_star_report(sd, "rgb", x[i:i + 1], a[i:i + 1], debug_views(dbg),
+                                           (o[0].cpu(), mse, bpp))
+            for k in ("flips", "near_tie_flips", "far_flips", "z_flips", "z_far_flips",
+                      "symbols", "nonzero_symbols"):
+                acc[k] += rep.get(k, 0)
+            acc["noise_floor"] = max(acc["noise_floor"], rep["noise_floor"])
+            acc["tf_max_abs_d_psnr_db"] = max(acc["tf_max_abs_d_psnr_db"], rep["tf_d_psnr_db"] or 0.0)
+            acc["tf_max_abs_d_ms_ssim"] = max(acc["tf_max_abs_d_ms_ssim"], rep["tf_d_ms_ssim"])
+            acc["max_bits_unflipped_rel"] = max(acc["max_bits_unflipped_rel"],
+                                                rep["bits_unflipped_rel"])
+            rec_acc = {"flips": rep["flips"], "near_tie_flips": rep["near_tie_flips"],
+                       "far_flips": rep["far_flips"], "z_flips": rep.get("z_flips", 0),
+                       "per_slice_flips": rep["per_slice_flips"],
+                       "tf_d_psnr_db": None if rep["tf_d_psnr_db"] is None
+                       else float(f"{rep['tf_d_psnr_db']:.3g}"),
+                       "tf_d_ms_ssim": float(f"{rep['tf_d_ms_ssim']:.3g}")}
         rb, rm, rms = outs_ref[i]
         psnr = 10 * math.log10(1.0 / mse) if mse > 0 else None
         rpsnr = 10 * math.log10(1.0 / rm) if rm > 0 else None
@@ -168,9 +211,21 @@ def gpu_parity(net, dev, outs_ref, S=256):
                     "psnr": None if psnr is None else round(psnr, 4),
                     "psnr_ref": None if rpsnr is None else round(rpsnr, 4),
                     "ms_ssim": round(msv, 6), "ms_ssim_ref": round(rms, 6)})
-    return {"max_abs_d_bpp": float(f"{d_bpp:.3g}"), "max_rel_d_bpp": float(f"{rel_bpp:.3g}"),
-            "max_abs_d_psnr_db": float(f"{d_psnr:.3g}"), "max_abs_d_ms_ssim": float(f"{d_ms:.3g}"),
-            "per_image": per}
+        if rec_acc is not None:
+            per[-1]["symbols"] = rec_acc
+    res = {"max_abs_d_bpp": float(f"{d_bpp:.3g}"), "max_rel_d_bpp": float(f"{rel_bpp:.3g}"),
+           "max_abs_d_psnr_db": float(f"{d_psnr:.3g}"), "max_abs_d_ms_ssim": float(f"{d_ms:.3g}"),
+           "per_image": per}
+    if account:
+        acc = {k: (float(f"{v:.3g}") if isinstance(v, float) else v) for k, v in acc.items()}
+        acc["bar"] = ("integer symbols: every flip at a near-tie (far_flips == 0); teacher-forced "
+                      "(oracle fed the device y_hat / z_hat) |dPSNR| < 1e-4 dB, |dMS-SSIM| < 1e-4; "
+                      "bits over unflipped symbols equal")
+        acc["bar_met"] = bool(acc["far_flips"] == 0 and acc["z_far_flips"] == 0 and
+                              acc["tf_max_abs_d_psnr_db"] < 1e-4 and
+                              acc["tf_max_abs_d_ms_ssim"] < 1e-4)
+        res["symbol_accounting"] = acc
+    return res
 
 
 def cpu_baseline_train(budget_s):
@@ -284,8 +339,12 @@ def main_train(args, world, rank, dev, dist):
 
     def step():
         out = net(x, a, a, *me)
-        trainer.step(4096.0 * out[1] + out[2])        # trainRGB.py:183-198 (lambda 4096)
-        return out
+        loss = 4096.0 * out[1] + out[2]                 # trainRGB.py:183-198 (lambda 4096)
+        trainer.step(loss)
+        # only the detached loss leaves the step: a live output would keep this step's
+        # autograd graph -- and its AccumulateGrad nodes, bound to the stream they were
+        # created on -- alive into the next (captured) step
+        return loss.detach()
 
     tuned = tune_cache_setup(args, os.path.join(ROOT, "profiles", f"tune_train_{args.dtype}_b{B}_{S}.json"))
     step()
@@ -301,7 +360,8 @@ def main_train(args, world, rank, dev, dist):
     # runs keep the eager step (bucketed RCCL all-reduces launched from autograd hooks).
     run = step
     graph = None
-    if not args.no_graph and world == 1:
+    captured = not args.no_graph and world == 1
+    if captured:
         opt.use_device_step()
         side = torch.cuda.Stream(dev)
         side.wait_stream(torch.cuda.current_stream(dev))
@@ -336,6 +396,10 @@ def main_train(args, world, rank, dev, dist):
         elapsed = t.item()
     ms = elapsed / args.steps * 1e3
     value = world * B * S * S * args.steps / elapsed / 1e6
+    loss_val = out.item()
+    del out, run
+    if graph is not None:
+        del gout, graph                       # the captured graph's autograd nodes
     if rank == 0:
         prof = rt.LaunchProfiler()
         rt.PROFILER = prof
@@ -360,9 +424,9 @@ def main_train(args, world, rank, dev, dist):
                                       "backward of 4096*mse+bpp + clamp(+-5) + Adam "
                                       f"(BASELINE config {3 if world == 1 else 5}), {S}x{S} RGBA",
                           "global_batch": B * world, "per_gpu_batch": B, "height": S,
-                          "width": S, "parallelism": f"dp{world}", "hip_graph": graph is not None,
+                          "width": S, "parallelism": f"dp{world}", "hip_graph": captured,
                           "tile_cache": tuned and os.path.relpath(tuned, ROOT),
-                          "loss": round(4096.0 * out[1].item() + out[2].item(), 4)},
+                          "loss": round(loss_val, 4)},
                "roofline": roof}
         if args.kernels:
             rec["kernels"] = {k: {"launches": v["launches"] // 2, "ms": round(v["ms"] / 2, 4),
@@ -376,6 +440,85 @@ def main_train(args, world, rank, dev, dist):
     if dist:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def dp_train_record(args, world, rank, dev, dist):
+    """BASELINE config 5 inside the driver's own scaling command: the trainRGB.py step
+    (forward + backward of 4096*mse + bpp, clamp(+-5), Adam) at 16 images per rank, 256^2, bf16,
+    data-parallel over the ranks of THIS run -- bucketed RCCL all-reduce of the 34 M fp32
+    gradients launched from post-accumulate-grad hooks (rgbac.parallel.DataParallelTrainer).
+    The step runs eagerly at every world size (world 1 included), so the N-rank and 1-rank
+    numbers are timed the same way.  Every rank calls this (collectives); rank 0 gets the record.
+    ``exposed_allreduce_ms``: GPU time between the end of backward and the last bucket's
+    completion (what backward did not hide); ``allreduce_ms`` the same 136 MB reduced alone."""
+    from rgbac.layers.SupplyMask import mask_pyramid
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    from rgbac.optim import AdamClamp
+    from rgbac.parallel import DataParallelTrainer
+    from rgbac import runtime as rt
+    B, S = args.dp_batch, 256
+    tuned = os.path.join(ROOT, "profiles", f"tune_train_bf16_b{B}_{S}.json")
+    if os.path.exists(tuned):
+        rt.load_tune_cache(tuned)
+    torch.manual_seed(234)
+    net = AutoEncoder().train().to(dev).set_compute_dtype(torch.bfloat16)
+    opt = AdamClamp(net.parameters(), lr=1e-4, clip=5.0)
+    trainer = DataParallelTrainer(net, opt)
+    x, a = synth_inputs(B, S, S, seed=1000 + rank)     # this rank's shard of the global batch
+    x, a = x.to(dev), a.to(dev)
+    _, me = mask_pyramid(a, 4)
+    losses = []
+
+    def step():
+        out = net(x, a, a, *me)
+        loss = 4096.0 * out[1] + out[2]                 # trainRGB.py:183-186 (lambda 4096)
+        trainer.step(loss)
+        losses.append(loss.detach())
+
+    for _ in range(args.dp_warmup):
+        step()
+    torch.cuda.synchronize()
+    trainer.comm_events = []
+    losses.clear()
+    elapsed = time_steps(step, args.dp_steps, dist, dev)
+    exposed = 0.0
+    if trainer.comm_events:
+        exposed = sum(e0.elapsed_time(e1) for e0, e1 in trainer.comm_events) / len(trainer.comm_events)
+    trainer.comm_events = None
+    ar_ms = 0.0
+    if dist:
+        flat = opt.flat_grad
+        for _ in range(2):
+            dist.all_reduce(flat)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            dist.all_reduce(flat)
+        e1.record()
+        torch.cuda.synchronize()
+        ar_ms = e0.elapsed_time(e1) / 5
+        t = torch.tensor([exposed, ar_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        exposed, ar_ms = t.tolist()
+        n_ranks = dist.get_world_size()
+    else:
+        n_ranks = 1
+    finite = all(bool(torch.isfinite(l).item()) for l in losses)
+    grad_bytes = opt.flat_grad.numel() * opt.flat_grad.element_size()
+    del net, opt, trainer
+    if rank != 0:
+        return None
+    return {"metric": TRAIN_METRIC, "config": "BASELINE config 5 (config 3 at world 1): "
+            f"data-parallel trainRGB.py step, {B}/rank x {n_ranks} ranks, {S}x{S}, bf16, eager "
+            "step at every world size, bucketed RCCL all-reduce overlapped with backward",
+            "value": round(n_ranks * B * S * S * args.dp_steps / elapsed / 1e6, 3), "unit": "MPix/s",
+            "n_ranks": n_ranks, "global_batch": B * n_ranks, "steps": args.dp_steps,
+            "warmup": args.dp_warmup, "ms_per_step": round(elapsed / args.dp_steps * 1e3, 3),
+            "exposed_allreduce_ms": round(exposed, 3), "allreduce_ms": round(ar_ms, 3),
+            "gradient_bytes": grad_bytes,
+            "overlap_fraction": None if ar_ms <= 0 else round(max(0.0, 1 - exposed / ar_ms), 3),
+            "loss_finite": finite}
 
 
 def cpu_baseline_codec(budget_s):
@@ -552,6 +695,78 @@ def main_rgba(args, dev):
     print(json.dumps(rec), flush=True)
 
 
+def main_alpha(args, dev):
+    """--alpha: BASELINE config 1 -- AutoEncoderMask_Journal encode+decode of one 256x256 alpha
+    tile (trainmask.py:242-293, config4096.json), HIP graph replay, in the bench dtype and in
+    fp32; cpu_baseline = the oracle's mask_forward on the same tile (the reference runs this
+    config on PyTorch CPU); parity (fp32, teacher-forced symbol accounting) vs the oracle."""
+    from oracle import parity as opar
+    from oracle import ref_model as ref
+    from rgbac import runtime as rt
+    from rgbac.models._latent import debug_views
+    B, S = args.batch if "--batch" in sys.argv else 1, args.size
+    _, a = synth_inputs(max(B, 4), S, S, seed=0)
+    a = a[2:3].repeat(B, 1, 1, 1) if B == 1 else a[:B]     # the ramped-ellipse alpha tile
+    net = mask_net().to(dev)
+    sd = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
+    ad = a.to(dev)
+    res = {}
+    for dtn in ([args.dtype, "f32"] if args.dtype != "f32" else ["f32"]):
+        net.set_compute_dtype(torch.bfloat16 if dtn == "bf16" else torch.float32)
+
+        def step():
+            with torch.no_grad():
+                return net(ad)
+        step()
+        torch.cuda.synchronize()
+        run, graph, _ = capture(step, args.no_graph)
+        for _ in range(args.warmup):
+            run()
+        el = time_steps(run, args.steps, None, dev)
+        res[dtn] = {"value": round(B * S * S * args.steps / el / 1e6, 3),
+                    "ms_per_step": round(el / args.steps * 1e3, 4)}
+        del run, graph
+    # parity (fp32, one tile) and the CPU baseline
+    net.set_compute_dtype(torch.float32)
+    dbg = {}
+    with torch.no_grad(), rt.fixed_tiles():
+        o = net(ad[:1], debug=dbg)
+    dev_out = (o[0].cpu(),) + tuple(t.item() for t in o[1:])
+    rep = opar.north_star_report(sd, "mask", a[:1], None, debug_views(dbg), dev_out)
+    cores = _set_cpu_threads()
+    with torch.no_grad():
+        r = ref.mask_forward(sd, a[:1])
+        n, t0 = 0, time.perf_counter()
+        while True:
+            ref.mask_forward(sd, a[:1])
+            n += 1
+            if time.perf_counter() - t0 >= args.cpu_seconds or n >= 2000:
+                break
+        dt_cpu = time.perf_counter() - t0
+    main = res[args.dtype]
+    rec = {"metric": "MPixels/sec alpha-codec encode+decode (AutoEncoderMask_Journal), 256x256 tile",
+           "value": main["value"], "unit": "MPix/s", "n_gpus": 1, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": main["ms_per_step"], "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+           "data": "synthetic (ramped-ellipse alpha k/255; random-init weights, torch seed 234, "
+                   "EncoderMask.7 x20 so latent symbols are non-zero)",
+           "config": {"workload": f"BASELINE config 1: AutoEncoderMask_Journal forward, {S}x{S}",
+                      "batch": B, "hip_graph": not args.no_graph},
+           "parity_mode": {"dtype": "f32", **res["f32"]},
+           "parity": {"sample": f"the same tile, fp32, vs the CPU oracle",
+                      "rel_d_bpp": float(f"{abs(dev_out[2] - r[2].item()) / r[2].item():.3g}"),
+                      "d_psnr_db": float(f"{abs(opar.psnr_db(dev_out[1]) - opar.psnr_db(r[1].item())):.3g}"),
+                      "max_abs_d_x_hat": float(f"{(dev_out[0] - r[0]).abs().max().item():.3g}"),
+                      "symbols": rep["symbols"], "nonzero_symbols": rep["nonzero_symbols"],
+                      "flips": rep["flips"], "far_flips": rep["far_flips"],
+                      "tf_d_psnr_db": rep["tf_d_psnr_db"], "tf_d_ms_ssim": rep["tf_d_ms_ssim"]},
+           "cpu_baseline": {"value": round(n * S * S / dt_cpu / 1e6, 4), "unit": "MPix/s",
+                            "cores": cores, "kind": "port",
+                            "sample": f"oracle mask_forward fp32, the same {S}x{S} tile, {n} "
+                                      f"forwards, {dt_cpu:.1f} s, torch threads {cores}"}}
+    print(json.dumps(rec), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -571,12 +786,19 @@ def main():
                     help="time the training step (BASELINE config 3 / 5) instead of the forward")
     ap.add_argument("--rgba", action="store_true",
                     help="RGBA eval pipeline: alpha codec -> constraint -> RGB codec")
+    ap.add_argument("--alpha", action="store_true",
+                    help="BASELINE config 1: the alpha codec on one 256x256 tile")
     ap.add_argument("--codec", action="store_true",
                     help="time compress + decompress (real bitstream) instead of the forward")
     ap.add_argument("--tune-cache", default=None,
                     help="tile-choice cache to load (default: the committed profiles/ one for "
                          "the forward config); '' disables")
     ap.add_argument("--save-tune", default=None, help="write the tile-choice cache here")
+    ap.add_argument("--no-dp-train", action="store_true",
+                    help="skip the data-parallel training sub-record (config 5 / dp_train)")
+    ap.add_argument("--dp-batch", type=int, default=16, help="dp_train images per rank")
+    ap.add_argument("--dp-steps", type=int, default=5)
+    ap.add_argument("--dp-warmup", type=int, default=3)
     ap.add_argument("--traffic-file", default=None,
                     help="PMC traffic summary (default: the committed profiles/ one)")
     args = ap.parse_args()
@@ -607,6 +829,8 @@ def main():
         return main_codec(args, dev)
     if args.rgba:
         return main_rgba(args, dev)
+    if args.alpha:
+        return main_alpha(args, dev)
     return main_forward(args, world, rank, dev, dist)
 
 
@@ -719,6 +943,10 @@ def main_forward(args, world, rank, dev, dist):
         net.set_compute_dtype(dt)
     if args.save_tune and rank == 0:
         rt.save_tune_cache(args.save_tune)
+    # config 5 (DP training) in the same ranks, so the driver's scaling run measures it too
+    dp = None
+    if not args.no_dp_train:
+        dp = dp_train_record(args, world, rank, dev, dist)
 
     if rank == 0:
         # ---- roofline attribution: eager steps, each queued behind a GPU spin so the host has
@@ -759,7 +987,7 @@ def main_forward(args, world, rank, dev, dist):
                           "tile_cache": tuned and os.path.relpath(tuned, ROOT)},
                "roofline": roof,
                "achieved_model_tflops": round(fwd_flops / (ms * 1e-3) / 1e12, 2),
-               "parity_mode": parity_mode}
+               "parity_mode": parity_mode, "dp_train": dp}
         if args.kernels:
             rec["kernels"] = {k: {"launches": v["launches"] // nrep, "ms": round(v["ms"] / nrep, 4),
                                   "share": round(v["ms"] / total_ms, 4),
@@ -768,15 +996,16 @@ def main_forward(args, world, rank, dev, dist):
         rec["cpu_baseline"] = None
         rec["parity"] = None
         if world == 1 and not args.no_cpu_baseline:
-            rec["cpu_baseline"], outs_ref = cpu_baseline(args.cpu_seconds, S=min(S, 256))
+            # the CPU baseline and parity sample are the bench's own size (config 4: 1024^2)
+            rec["cpu_baseline"], outs_ref = cpu_baseline(args.cpu_seconds, S=S)
             # bpp / PSNR / MS-SSIM of the HIP forward vs the oracle on the same sample
             # (outside the timed region), in the bench dtype and in the fp32 parity mode
-            par = {"sample": "4 images 256x256 of the bench batch (alpha ones / half / "
+            par = {"sample": f"4 images {S}x{S} of the bench batch (alpha ones / half / "
                              "ellipse / zero), one forward each, vs the CPU oracle (fp32)"}
-            par[args.dtype] = gpu_parity(net, dev, outs_ref, S=min(S, 256))
+            par[args.dtype] = gpu_parity(net, dev, outs_ref, S=S, account=dt == torch.float32)
             if dt != torch.float32:
                 net.set_compute_dtype(torch.float32)
-                par["f32"] = gpu_parity(net, dev, outs_ref, S=min(S, 256))
+                par["f32"] = gpu_parity(net, dev, outs_ref, S=S, account=True)
                 net.set_compute_dtype(dt)
             rec["parity"] = par
         print(json.dumps(rec), flush=True)

@@ -2679,6 +2679,12 @@ static int fill_group(const rgbac_conv_args* a, int ntaps_max, ConvGroup& g) {
 using namespace rgbac;
 
 extern "C" int rgbac_conv_num_tiles(void) { return kNumTiles; }
+// 1 for the fragment-streamed patch tiles (42..47, 50), whose `weight` must be the
+// fragment-major copy documented in rgbac.h; 0 for the plain packed layout; -1 out of range.
+extern "C" int rgbac_conv_tile_weight_layout(int tile) {
+  if (tile < 0 || tile >= kNumTiles) return -1;
+  return ((tile >= 42 && tile <= 47) || tile == 50) ? 1 : 0;
+}
 extern "C" int rgbac_conv_max_groups(void) { return kMaxGroups; }
 
 extern "C" int rgbac_conv2d_grouped(const rgbac_conv_args* args, int ngroups, void* stream) {

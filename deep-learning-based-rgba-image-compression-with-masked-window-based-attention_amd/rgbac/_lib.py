@@ -92,6 +92,7 @@ SIGNATURES = {
     "rgbac_last_error": [],
     "rgbac_conv2d": [ctypes.POINTER(ConvArgs), _VP],
     "rgbac_conv_num_tiles": [],
+    "rgbac_conv_tile_weight_layout": [ctypes.c_int],
     "rgbac_conv2d_grouped": [ctypes.c_void_p, _I32, _VP],
     "rgbac_conv2d_grouped_part": [ctypes.c_void_p, _I32, _I32, _VP],
     "rgbac_conv_max_groups": [],

@@ -1,12 +1,23 @@
-"""Training-data pipeline on the GPU (reference: my_datasets/MYdataset.py:55-115, COCOP3MDataset).
+"""Training-data pipeline on the GPU (reference: my_datasets/MYdataset.py:55-115, COCOP3MDataset;
+my_datasets/MYprepare.py:7-10, prepare_dataset_train_COCOP3M).
 
 The reference decodes each PNG with PIL, converts to tensors and runs RandomResizedCrop,
-random flips and the alpha "fill" on the CPU per item.  Here the host keeps only the PNG
-decode and the random draws -- made with the SAME RNG calls in the SAME order as the
-reference (torch RNG for the crop box and the fill, Python `random` for the flips), so a
-seeded run draws identical parameters -- and one `rgbac_rgba_augment` launch does the pixel
-work for a whole batch on the GPU (csrc/augment.hip), writing the reference's 5-tuple
-`(masked_image, alpha, img, alpha, images_with_alpha)` directly.
+random flips and the alpha "fill" on the CPU per item, inside `DataLoader(num_workers=4,
+pin_memory=True)` worker processes.  Here the split is:
+
+* worker processes (`COCOP3MDataset.__getitem__`, CPU only -- no GPU context is ever created
+  in a forked worker): PNG decode, the random draws -- the SAME RNG calls in the SAME order as
+  the reference (torch RNG for the crop box and the fill, Python `random` for the flips), so a
+  seeded run draws identical parameters -- and the crop box cut out as uint8 (the only source
+  pixels the resize reads);
+* `collate_rgba` (also in the workers): the batch's variable-size crops packed into ONE flat
+  uint8 tensor + a descriptor tensor, which `pin_memory=True` pins as usual;
+* the main process (`GPUAugmentLoader`): one non-blocking H2D copy of the packed crops and ONE
+  `rgbac_rgba_augment` launch per batch (csrc/augment.hip: antialiased bilinear resize, flips,
+  fill, masking), yielding the reference's 5-tuple `(masked_image, alpha, img, alpha,
+  images_with_alpha)` as (B, C, H, W) fp32 GPU tensors.
+
+`prepare_dataset_train_COCOP3M` has MYprepare's signature and returns (loader, dataset).
 
 Crop + resize follow torchvision's `resized_crop` on a tensor: crop, then
 `F.interpolate(mode="bilinear", align_corners=False, antialias=True)` (torchvision >= 0.17;
@@ -93,6 +104,10 @@ def augment_batch(images, params, height=256, width=256, antialias=True, device=
         if h > MAX_DOWNSCALE * height or w > MAX_DOWNSCALE * width:
             raise ValueError("augment_batch: crop downscale factor above 31 is not supported")
         arr[k] = _Desc(t.data_ptr(), H, W, i, j, h, w, int(fh) | (int(fv) << 1) | (int(fill) << 2), 0)
+    return _launch_augment(arr, B, height, width, antialias, dev, keep=srcs)
+
+
+def _launch_augment(arr, B, height, width, antialias, dev, keep=None):
     descs = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev)
     masked = torch.empty((B, 3, height, width), device=dev)
     alpha = torch.empty((B, 1, height, width), device=dev)
@@ -101,8 +116,8 @@ def augment_batch(images, params, height=256, width=256, antialias=True, device=
     _lib.call("rgbac_rgba_augment", B, descs.data_ptr(), height, width, 1 if antialias else 0,
               masked.data_ptr(), alpha.data_ptr(), img.data_ptr(), rgba.data_ptr(),
               _lib.stream_ptr(dev))
-    # the sources and descriptors may be freed now: the caching allocator orders their reuse
-    # after this launch on the same stream
+    # the sources (``keep``) and descriptors may be freed now: the caching allocator orders
+    # their reuse after this launch on the same stream
     return masked, alpha, img, alpha, rgba
 
 
@@ -117,30 +132,104 @@ def decode_rgba(path):
 
 
 class COCOP3MDataset(torch.utils.data.Dataset):
-    """Drop-in for my_datasets.MYdataset.COCOP3MDataset (same ctor, len, item tuple).  Items
-    are augmented on the GPU one at a time; for the batched path use `decode_item` in the
-    DataLoader workers and `collate_gpu` as the collate function (one launch per batch)."""
+    """my_datasets.MYdataset.COCOP3MDataset (same constructor arguments, same file list, same
+    length).  ``__getitem__`` runs in DataLoader workers and touches no GPU: it returns
+    (crop, params) -- the crop box of the decoded RGBA image as a CPU (h, w, 4) uint8 tensor and
+    an int32 tensor (i, j, h, w, hflip, vflip, fill, index); the pixel transform happens batched
+    on the GPU in the main process (`collate_rgba` + `GPUAugmentLoader`, or `augment_items`)."""
 
     def __init__(self, coco_path="P3Mdata/COCOdata", p3m_path="P3Mdata/MASKpatches", height=256,
-                 width=256, fill_mix_ratio=0.25, device="cuda"):
+                 width=256, fill_mix_ratio=0.25):
         self.images = (glob.glob(os.path.join(coco_path, "*.png")) +
                        glob.glob(os.path.join(p3m_path, "*.png")))
         self.height, self.width = height, width
         self.fill_mix_ratio = fill_mix_ratio
-        self.device = device
 
     def __len__(self):
         return len(self.images)
 
-    def decode_item(self, index):
-        u8 = decode_rgba(self.images[index])
-        return u8, draw_params(u8.shape[0], u8.shape[1], self.fill_mix_ratio)
-
-    def collate_gpu(self, items):
-        imgs, params = zip(*items)
-        return augment_batch(list(imgs), list(params), self.height, self.width,
-                             device=self.device)
-
     def __getitem__(self, index):
-        out = self.collate_gpu([self.decode_item(index)])
-        return tuple(t[0] for t in out)
+        u8 = decode_rgba(self.images[index])                         # MYdataset.py:73-79
+        i, j, h, w, fh, fv, fill = draw_params(u8.shape[0], u8.shape[1], self.fill_mix_ratio)
+        crop = torch.from_numpy(np.ascontiguousarray(u8[i:i + h, j:j + w]))
+        return crop, torch.tensor([i, j, h, w, fh, fv, fill, index], dtype=torch.int32)
+
+
+def collate_rgba(items):
+    """DataLoader collate_fn: a list of dataset items (crop, params) -> {"pixels": one flat
+    uint8 tensor holding every crop, "desc": int64 (B, 8) [byte offset, h, w, flags, i, j,
+    dataset index, 0]} -- plain CPU tensors: pin_memory pins them, and they cross the worker
+    queue as two buffers."""
+    sizes = [int(c.numel()) for c, _ in items]
+    pixels = torch.empty(sum(sizes), dtype=torch.uint8)
+    desc = torch.zeros((len(items), 8), dtype=torch.int64)
+    off = 0
+    for k, ((crop, p), n) in enumerate(zip(items, sizes)):
+        pixels[off:off + n].copy_(crop.reshape(-1))
+        p = [int(v) for v in p]
+        idx = p[7] if len(p) > 7 else -1
+        desc[k] = torch.tensor([off, crop.shape[0], crop.shape[1],
+                                p[4] | (p[5] << 1) | (p[6] << 2), p[0], p[1], idx, 0])
+        off += n
+    return {"pixels": pixels, "desc": desc}
+
+
+def augment_packed(batch, height=256, width=256, antialias=True, device="cuda"):
+    """A `collate_rgba` batch -> the reference's 5-tuple on ``device`` (one H2D copy, one
+    launch).  The copy is non-blocking from pinned memory; the launch follows it on the same
+    stream."""
+    dev = torch.device(device)
+    pix = batch["pixels"].to(dev, non_blocking=True)
+    desc = batch["desc"]
+    B = desc.shape[0]
+    if B == 0:
+        raise ValueError("augment_packed: empty batch")
+    arr = (_Desc * B)()
+    base = pix.data_ptr()
+    for k in range(B):
+        off, h, w, flags = (int(v) for v in desc[k, :4])
+        if h < 1 or w < 1 or off + h * w * 4 > pix.numel():
+            raise ValueError(f"augment_packed: bad crop descriptor {desc[k].tolist()}")
+        if h > MAX_DOWNSCALE * height or w > MAX_DOWNSCALE * width:
+            raise ValueError("augment_packed: crop downscale factor above 31 is not supported")
+        arr[k] = _Desc(base + off, h, w, 0, 0, h, w, flags, 0)
+    return _launch_augment(arr, B, height, width, antialias, dev, keep=pix)
+
+
+def augment_items(items, height=256, width=256, antialias=True, device="cuda"):
+    """`COCOP3MDataset` items (e.g. ``[ds[k] for k in idx]``) -> the batched 5-tuple."""
+    return augment_packed(collate_rgba(items), height, width, antialias, device)
+
+
+class GPUAugmentLoader:
+    """Wraps a DataLoader whose collate_fn is `collate_rgba`: every batch it yields is augmented
+    on the GPU in THIS (main) process and comes out as the reference's 5-tuple, so the training
+    loop reads it exactly like the reference's loader (trainRGB.py:165-177; the tensors are
+    already on ``device``, and `.to(device)` on them is a no-op)."""
+
+    def __init__(self, loader, height=256, width=256, device="cuda", antialias=True):
+        self.loader = loader
+        self.dataset = loader.dataset
+        self.batch_size = loader.batch_size
+        self.height, self.width = height, width
+        self.device, self.antialias = device, antialias
+
+    def __len__(self):
+        return len(self.loader)
+
+    def __iter__(self):
+        for batch in self.loader:
+            yield augment_packed(batch, self.height, self.width, self.antialias, self.device)
+
+
+def prepare_dataset_train_COCOP3M(batch_size=1, COCOrootpath="../P3Mdata/COCOdata",
+                                  P3Mrootpath="../P3Mdata/MASKpatches", height=256, width=256,
+                                  fill_mix_ratio=0.25, num_workers=4, device="cuda"):
+    """my_datasets/MYprepare.py:7-10 -> (train_dataloader, train_dataset): the same
+    DataLoader(shuffle=True, pin_memory=True, num_workers=4) over COCOP3MDataset, with the
+    pixel transform moved to one GPU launch per batch in the main process."""
+    ds = COCOP3MDataset(coco_path=COCOrootpath, p3m_path=P3Mrootpath, height=height,
+                        width=width, fill_mix_ratio=fill_mix_ratio)
+    dl = torch.utils.data.DataLoader(ds, batch_size=batch_size, shuffle=True, pin_memory=True,
+                                     num_workers=num_workers, collate_fn=collate_rgba)
+    return GPUAugmentLoader(dl, height, width, device), ds

@@ -234,3 +234,17 @@ def latent_path(model, y, training=False, noise_z=None, noise_y=None, debug=None
         debug.update(z=z, z_hat=z_hat, z_lik=zlik, y_lik=liks, latent_means=means,
                      latent_scales=scales, y_hat=YH, musigma=musig)
     return YH, ypart, zpart
+
+
+def debug_views(debug):
+    """CPU NCHW fp32 copies of a ``debug=`` forward's latent tensors (parity tooling):
+    y, per-slice mu (the first half of the (mu | sigma) the GAUSS epilogue consumed) and
+    likelihoods, y_hat (decoder input), z and z_hat.  In bf16 mode the stored mu is rounded to
+    bf16 (the epilogue used fp32), so symbol accounting is meaningful in fp32 mode only."""
+    y = rt.to_nchw(debug["y"]).cpu()
+    mus = [rt.to_nchw(ms).cpu()[:, :ms.C // 2] for ms in debug["musigma"]]
+    cs = mus[0].shape[1]
+    return {"y": [y[:, i * cs:(i + 1) * cs] for i in range(len(mus))], "mu": mus,
+            "lik": [t.permute(0, 3, 1, 2).cpu() for t in debug["y_lik"]],
+            "y_hat": rt.to_nchw(debug["y_hat"]).cpu(), "z": rt.to_nchw(debug["z"]).cpu(),
+            "z_hat": rt.to_nchw(debug["z_hat"]).cpu()}

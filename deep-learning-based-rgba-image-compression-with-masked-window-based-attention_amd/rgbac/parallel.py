@@ -117,6 +117,11 @@ class GradBuckets:
                 w.wait()
         if not self.learned and any(self.fired):
             self.learned = True
+            # every rank must cut the same buckets (else ranks would issue all-reduces of
+            # different ranges and counts): a parameter counts as fired if it fired anywhere
+            fired = torch.tensor(self.fired, dtype=torch.int32, device=self.flat.device)
+            dist.all_reduce(fired, op=dist.ReduceOp.MAX, group=self.group)
+            self.fired = [bool(f) for f in fired.tolist()]
             quiet = [i for i, f in enumerate(self.fired) if not f]
             if quiet:
                 order = [i for i in range(len(self.params) - 1, -1, -1) if self.fired[i]]
@@ -135,6 +140,10 @@ class DataParallelTrainer:
     def __init__(self, net, optimizer, bucket_bytes=25 << 20):
         self.net, self.opt = net, optimizer
         self.buckets = None
+        # optional exposed-communication probe: a list receiving (end of backward, gradients
+        # reduced) event pairs recorded on the compute stream -- the all-reduce time backward
+        # did not hide
+        self.comm_events = None
         if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
             self.buckets = GradBuckets(optimizer.params, optimizer.flat_grad, bucket_bytes)
             # the bucket all-reduces are launched from post-accumulate-grad hooks: keep
@@ -148,5 +157,12 @@ class DataParallelTrainer:
             self.buckets.begin()
         loss.backward()
         if self.buckets is not None:
+            ev = None
+            if self.comm_events is not None:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             self.opt.grad_scale = self.buckets.finish()
+            if ev is not None:
+                ev[1].record()
+                self.comm_events.append(ev)
         self.opt.step()

@@ -719,6 +719,12 @@ def launch(preps, force=None):
             choice = _heuristic(mtot, cout, nst)
         if not fixed:
             _tune_cache[key] = choice
+    if choice[0] in FPATCH_SIG and not all(isinstance(pr.pk, PackedConv) for pr in preps):
+        # a cached / forced fragment-streamed tile (tuned on a forward PackedConv of the same
+        # shape) handed to a training pack: TPack weights are re-gathered in the plain layout
+        # every step, so a cached fragment-major copy would go stale -- take the shape rule
+        choice = _heuristic(p0.mgrid * p0.nphase * n, max(pr.pk.cout for pr in preps),
+                            max(pr.nst for pr in preps))
     if gauss and not (choice[0] == TILE_WSTREAM and _wstream_ok(preps)) and (
             choice[0] not in GAUSS_TILES or
             not _gauss_ok(choice[0], max(pr.pk.cout for pr in preps))):

@@ -98,7 +98,17 @@ typedef struct rgbac_conv_args {
   const uint8_t* sel;                      /* MASKSEL: per output pixel flag   */
   int32_t tile;                /* tile shape index, 0..rgbac_conv_num_tiles()-1:
                                   0:128x128 1:128x64 2:64x64 3:128x32 4:64x32
-                                  5:128x16 6:64x16 (pixels x channels)          */
+                                  5:128x16 6:64x16 (pixels x channels).
+                                  Tiles with rgbac_conv_tile_weight_layout(tile) == 1
+                                  (42..47, 50: fragment-streamed patch tiles) read
+                                  `weight` as the FRAGMENT-MAJOR copy of the pack:
+                                  bf16 [nphase][cout_pad/16][ntaps*cin32/32][64][8],
+                                  cin32 = round_up(cin_pad, 32), K tap-major with each
+                                  tap's channels zero-padded to cin32; lane l of a
+                                  (16-row, 32-deep) block holds row l&15, k 8*(l>>4)..+7
+                                  (the v_mfma_f32_16x16x32_bf16 A fragment).  The
+                                  kernel cannot tell the layouts apart: passing the
+                                  plain pack to these tiles gives wrong outputs.   */
   int32_t ksplit;              /* split-K factor (1 = fused epilogue in-kernel)   */
   void* workspace;             /* ksplit>1: fp32 [ksplit][nphase][M][round16(cout)] */
   const float* aux0;           /* GAUSS: fp32 noise [M][cout/2] or NULL            */
@@ -127,6 +137,9 @@ const char* rgbac_last_error(void);
  *   lrp tanh update), models/AutoEncoderMask_Journal.py:96-244. */
 int rgbac_conv2d(const rgbac_conv_args* args, void* stream);
 int rgbac_conv_num_tiles(void);
+/* 1 if `tile` reads the fragment-major weight copy (see rgbac_conv_args.tile),
+ * 0 for the plain [nphase][cout_pad][k_pad] pack, -1 if out of range. */
+int rgbac_conv_tile_weight_layout(int tile);
 
 /* ngroups (1..rgbac_conv_max_groups()) independent convs in one launch.  All
  * groups share dtype, mode, batch, input/output size, ksize, stride, tile,

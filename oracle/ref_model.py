@@ -391,14 +391,26 @@ def _stack3(x, sd, p):
     return _conv(t, sd, p + ".4")
 
 
-def _latent_path(y, sd, num_slices, max_support, training, noise_z, noise_y, dbg=None):
+def _latent_path(y, sd, num_slices, max_support, training, noise_z, noise_y, dbg=None,
+                 force_hats=None, force_zhat=None):
     """AutoEncoderRGB_Journal.py:222-271 / AutoEncoderMask_Journal.py:251-298.
     ``dbg`` (dict or None) receives the per-slice (mu, scale) lists -- the checker's view of
-    the integer symbols round(y_slice - mu) (:257)."""
+    the integer symbols round(y_slice - mu) (:257).
+
+    ``force_hats`` (B, M, h, w) or None -- teacher forcing for the parity accounting: slice
+    i's support (:241) and the returned y_hat are the GIVEN y_hat slices (the device path's)
+    instead of this restatement's own, so a symbol that flipped at a near-tie in an earlier
+    slice does not cascade into later slices' mu / sigma; each slice's own arithmetic
+    (mu, sigma, round(y - mu), likelihood) is still the oracle's.  ``force_zhat`` (B, 192,
+    h/8, w/8) likewise replaces z_hat (:227-229) as the hyper-synthesis input."""
     z = _h_a(y, sd)
     _, z_lik = eb_forward(z, sd, "entropy_bottleneck", training, noise_z)
     med = eb_medians(sd, "entropy_bottleneck")
     z_hat = ste_round(z - med) + med
+    if dbg is not None:
+        dbg.update(z=z, z_med=med)
+    if force_zhat is not None:
+        z_hat = force_zhat
     scales = _hyper_s(z_hat, sd, "h_scale_s")
     means = _hyper_s(z_hat, sd, "h_mean_s")
     H, W = y.shape[2:]
@@ -417,10 +429,16 @@ def _latent_path(y, sd, num_slices, max_support, training, noise_z, noise_y, dbg
             dbg.setdefault("mu", []).append(mu)
             dbg.setdefault("scale", []).append(sc)
             dbg.setdefault("y", []).append(ysl)
+            dbg.setdefault("lik", []).append(lik)
         yh = ste_round(ysl - mu) + mu
         lrp = _stack3(torch.cat([ms, yh], dim=1), sd, f"lrp_transforms.{i}")
         yh = yh + 0.5 * torch.tanh(lrp)
+        if force_hats is not None:
+            cs = ysl.shape[1]
+            yh = force_hats[:, i * cs:(i + 1) * cs]
         hats.append(yh)
+    if dbg is not None:
+        dbg.update(y_hat=torch.cat(hats, dim=1), z_hat=z_hat)
     return torch.cat(hats, dim=1), torch.cat(liks, dim=1), z_lik
 
 
@@ -436,12 +454,16 @@ def reconstruct_error(inp, out, in_mask):
 
 
 def rgb_forward(sd, inp, mask, reconmask, me1, me2, me3, me4, training=False,
-                noise_z=None, noise_y=None, masked=True, dbg=None):
-    """AutoEncoderRGB_Journal.py:203-296 -> (x_hat, mse, bpp, y_bpp, z_bpp)."""
+                noise_z=None, noise_y=None, masked=True, dbg=None, force_hats=None,
+                force_zhat=None):
+    """AutoEncoderRGB_Journal.py:203-296 -> (x_hat, mse, bpp, y_bpp, z_bpp).
+    ``force_hats`` / ``force_zhat``: teacher-forced y_hat / z_hat (see _latent_path) --
+    parity accounting only."""
     rm = torch.round(reconmask * 255) / 255                      # :212-214
     md = supply_mask(rm)                                         # :215
     y = analysis(inp, sd, "Encoder", me2, me3, masked)           # :217
-    y_hat, y_lik, z_lik = _latent_path(y, sd, 10, 5, training, noise_z, noise_y, dbg)
+    y_hat, y_lik, z_lik = _latent_path(y, sd, 10, 5, training, noise_z, noise_y, dbg,
+                                       force_hats, force_zhat)
     x_hat = synthesis(y_hat, sd, "Decoder", md[1], md[2], masked)  # :273
     yb, zb = _bits(y_lik), _bits(z_lik)
     mse = reconstruct_error(inp, x_hat, mask)                    # :289
@@ -489,10 +511,13 @@ def mask_decoder(y, sd):
     return dse(t, sd, "DecoderMask.9", leaky=True)
 
 
-def mask_forward(sd, m, training=False, noise_z=None, noise_y=None):
-    """AutoEncoderMask_Journal.py:248-316 -> (x_hat, mse, bpp, y_bpp, z_bpp)."""
+def mask_forward(sd, m, training=False, noise_z=None, noise_y=None, dbg=None, force_hats=None,
+                 force_zhat=None):
+    """AutoEncoderMask_Journal.py:248-316 -> (x_hat, mse, bpp, y_bpp, z_bpp).
+    ``dbg`` / ``force_hats``: as rgb_forward (parity accounting only)."""
     y = mask_encoder(m, sd)
-    y_hat, y_lik, z_lik = _latent_path(y, sd, 5, 5, training, noise_z, noise_y)
+    y_hat, y_lik, z_lik = _latent_path(y, sd, 5, 5, training, noise_z, noise_y, dbg,
+                                       force_hats, force_zhat)
     x_hat = mask_decoder(y_hat, sd)
     yb, zb = _bits(y_lik), _bits(z_lik)
     mse = torch.mean((x_hat - m).pow(2))                         # :309

@@ -249,11 +249,11 @@ def test_mask_train_step_grads(device):
         if r is None or r.abs().max() == 0:
             continue
         e = nrel(p.grad, r)
-        errs.append(e)
-        if e > 2e-2:
+        errs.append((e, n))
+        if e > 1e-3:
             bad.append((n, e))
     errs.sort()
-    print("mask codec grads: median rel", errs[len(errs) // 2], "max", errs[-1])
+    print("mask codec grads: median rel", errs[len(errs) // 2], "max", errs[-3:])
     assert not bad, bad[:10]
     # a full trainmask.py step: clamp(+-5) + Adam on the same gradients (AdamClamp)
     from rgbac.optim import AdamClamp

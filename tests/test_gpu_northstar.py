@@ -1,0 +1,227 @@
+"""The north_star parity bar on exactly the bench's parity inputs (BASELINE config 2's
+workload, fp32 parity mode): 256x256, alpha ones / left-half zero / ramped ellipse / all
+zero (bench.synth_inputs, seed 0), the bench's codec (seed 234, Encoder.x4 x 20 so latent
+symbols span about -5..10 instead of all rounding to 0), one image per forward (as the
+reference's Kodak loop, trainRGB.py:276-311) and the B=8 batch.
+
+Bar: "bpp bit-exact after integer quantisation, PSNR / MS-SSIM within 1e-4".  Every latent
+symbol round(y - mu) of the device path is compared with the oracle's, slice by slice,
+teacher-forced (oracle/parity.py: the oracle gets the device's z_hat / y_hat as supports and
+decoder input, so a near-tie flip in slice i is not blamed on slice i+1):
+  * no flip outside a near-tie (|d_dev - d_ref| at the flip within the fp32 noise floor of
+    the unflipped symbols; that floor itself < 1e-3), z symbols likewise;
+  * bits over the unflipped symbols equal to 1e-5 relative;
+  * teacher-forced |dPSNR| < 1e-4 dB and |dMS-SSIM| < 1e-4;
+  * free-running (no forcing): the same deltas when no symbol flipped, otherwise reported.
+(AutoEncoderRGB_Journal.py:255-257,280-281; trainRGB.py:289-311.)"""
+import os
+import sys
+
+import pytest
+import torch
+
+from oracle import parity
+from oracle import ref_model as ref
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+@pytest.fixture(scope="module")
+def codec(device):
+    from bench import rgb_net
+    net = rgb_net()
+    sd = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
+    return net.to(device).set_compute_dtype(torch.float32), sd
+
+
+def _device_forward(net, x, a, device):
+    from rgbac import runtime as rt
+    from rgbac.layers.SupplyMask import mask_pyramid
+    from rgbac.models._latent import debug_views
+    xd, ad = x.to(device), a.to(device)
+    _, me = mask_pyramid(ad, 4)
+    dbg = {}
+    with torch.no_grad(), rt.fixed_tiles():
+        out = net(xd, ad, ad, *me, debug=dbg)
+    torch.cuda.synchronize()
+    return (out[0].cpu(),) + tuple(t.item() for t in out[1:]), debug_views(dbg)
+
+
+def _check(rep, e2e, tag):
+    print(f"{tag}: symbols {rep['symbols']} (non-zero {rep['nonzero_symbols']}), flips "
+          f"{rep['flips']} (near-tie {rep['near_tie_flips']}, far {rep['far_flips']}), per slice "
+          f"{rep['per_slice_flips']}, z flips {rep.get('z_flips')}, noise floor "
+          f"{rep['noise_floor']:.2e}, bits(unflipped) rel {rep['bits_unflipped_rel']:.2e}, "
+          f"teacher-forced dPSNR {rep['tf_d_psnr_db']} dMS-SSIM {rep['tf_d_ms_ssim']:.2e} "
+          f"max|dx_hat| {rep['tf_max_abs_dx_hat']:.2e}; free-running {e2e}")
+    assert rep["nonzero_symbols"] > rep["symbols"] // 4, "vacuous: symbols mostly zero"
+    assert rep["noise_floor"] < 1e-3
+    assert rep["far_flips"] == 0 and rep.get("z_far_flips", 0) == 0
+    assert rep["bits_unflipped_rel"] < 1e-5
+    if rep["tf_d_psnr_db"] is not None:
+        assert rep["tf_d_psnr_db"] < 1e-4
+    assert rep["tf_d_ms_ssim"] < 1e-4
+    if rep["flips"] == 0 and rep.get("z_flips", 0) == 0:
+        if e2e["d_psnr_db"] is not None:
+            assert e2e["d_psnr_db"] < 1e-4
+        assert e2e["d_ms_ssim"] < 1e-4
+        assert e2e["rel_d_bpp"] < 1e-5
+
+
+def _free_running(sd, x, a, dev_out):
+    from oracle import ref_metrics
+    me = ref.supply_mask(a)
+    with torch.no_grad():
+        r = ref.rgb_forward(sd, x, a, a, *me[:4])
+        msd = ref_metrics.ms_ssim(x, dev_out[0].clamp(0, 1), data_range=1.0).item()
+        msr = ref_metrics.ms_ssim(x, r[0].clamp(0, 1), data_range=1.0).item()
+    pd, pr = parity.psnr_db(dev_out[1]), parity.psnr_db(r[1].item())
+    return {"d_psnr_db": None if pd is None or pr is None else abs(pd - pr),
+            "d_ms_ssim": abs(msd - msr),
+            "rel_d_bpp": abs(dev_out[2] - r[2].item()) / max(abs(r[2].item()), 1e-30),
+            "bpp": dev_out[2], "bpp_ref": r[2].item()}
+
+
+@pytest.mark.parametrize("img", [0, 1, 2, 3], ids=["ones", "half", "ellipse", "zero"])
+def test_bench_sample_b1_fp32(device, codec, img):
+    from bench import parity_sample
+    net, sd = codec
+    x, a = parity_sample(256)
+    x, a = x[img:img + 1], a[img:img + 1]
+    dev_out, views = _device_forward(net, x, a, device)
+    rep = parity.north_star_report(sd, "rgb", x, a, views, dev_out)
+    _check(rep, _free_running(sd, x, a, dev_out), f"image {img}")
+
+
+def test_bench_batch_b8_fp32(device, codec):
+    from bench import synth_inputs
+    net, sd = codec
+    x, a = synth_inputs(8, 256, 256, seed=0)
+    dev_out, views = _device_forward(net, x, a, device)
+    rep = parity.north_star_report(sd, "rgb", x, a, views, dev_out)
+    _check(rep, _free_running(sd, x, a, dev_out), "batch 8")
+
+
+# --------------------------------------------------------------------------------------
+# BASELINE config 1: AutoEncoderMask_Journal on one 256x256 alpha tile (trainmask.py:242-293)
+# --------------------------------------------------------------------------------------
+@pytest.mark.parametrize("img", [1, 2], ids=["half", "ellipse"])
+def test_config1_alpha_codec_256_fp32(device, img):
+    """The alpha codec (AutoEncoderMask_Journal.py:248-316) at config 1's size, fp32, one tile:
+    x_hat / mse / bpp vs the oracle, every latent symbol accounted for (teacher-forced), the
+    same bar as the RGB codec."""
+    from bench import mask_net, parity_sample
+    from rgbac import runtime as rt
+    from rgbac.models._latent import debug_views
+    net = mask_net()
+    sd = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
+    net = net.to(device).set_compute_dtype(torch.float32)
+    _, a = parity_sample(256)
+    m = a[img:img + 1]
+    dbg = {}
+    with torch.no_grad(), rt.fixed_tiles():
+        out = net(m.to(device), debug=dbg)
+    torch.cuda.synchronize()
+    dev_out = (out[0].cpu(),) + tuple(t.item() for t in out[1:])
+    rep = parity.north_star_report(sd, "mask", m, None, debug_views(dbg), dev_out)
+    with torch.no_grad():
+        r = ref.mask_forward(sd, m)
+    free = {"d_psnr_db": abs(parity.psnr_db(dev_out[1]) - parity.psnr_db(r[1].item())),
+            "d_ms_ssim": 0.0,
+            "rel_d_bpp": abs(dev_out[2] - r[2].item()) / max(abs(r[2].item()), 1e-30),
+            "max_abs_dx_hat": (dev_out[0] - r[0]).abs().max().item()}
+    _check(rep, free, f"alpha codec tile {img}")
+    if rep["flips"] == 0:
+        assert free["max_abs_dx_hat"] < 1e-3
+
+
+# --------------------------------------------------------------------------------------
+# BASELINE config 3: the trainRGB.py step at B=16, 256^2, bf16, graph-captured
+# --------------------------------------------------------------------------------------
+def test_config3_train_step_b16_256_graph_capture(device):
+    """bench.py --train's step at its own size: forward + backward of 4096*mse + bpp +
+    clamp(+-5) + Adam (trainRGB.py:178-198), B=16, 256^2, bf16, captured once in a HIP graph
+    and replayed.  Properties: finite loss and gradients, replayed parameters follow the eager
+    twin (same update direction within the cosine bar of the B=2 test), the step counter
+    advances on device, and no AccumulateGrad stream-mismatch warning is raised in the
+    warm-up, capture or replay (the graph would otherwise depend on a stale node's stream)."""
+    import warnings
+    from bench import synth_inputs
+    from rgbac import runtime as rt
+    from rgbac.layers.SupplyMask import mask_pyramid
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    from rgbac.optim import AdamClamp
+    tc = os.path.join(ROOT, "profiles", "tune_train_bf16_b16_256.json")
+    if os.path.exists(tc):
+        rt.load_tune_cache(tc)
+    torch.manual_seed(234)
+    base = AutoEncoder().train()
+    B, S = 16, 256
+    x, a = synth_inputs(B, S, S, seed=0)
+    x, a = x.to(device), a.to(device)
+    _, me = mask_pyramid(a, 4)
+    g = torch.Generator().manual_seed(5)
+    nz = (torch.rand((B, S // 64, S // 64, 192), generator=g) - 0.5).to(device)
+    ny = (torch.rand((B, S // 8, S // 8, 80), generator=g) - 0.5).to(device)
+    nets, opts = [], []
+    for _ in range(2):
+        n = AutoEncoder().to(device).train().set_compute_dtype(torch.bfloat16)
+        n.load_state_dict(base.state_dict())
+        nets.append(n)
+        opts.append(AdamClamp(n.parameters(), lr=1e-4, clip=5.0).use_device_step())
+    losses = []
+
+    def step(i):
+        out = nets[i](x, a, a, *me, noise_z=nz, noise_y=ny)
+        loss = 4096.0 * out[1] + out[2]
+        opts[i].zero_grad()
+        loss.backward()
+        opts[i].step()
+        return loss.detach()
+
+    caught = {}
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        for _ in range(5):
+            losses.append(step(0))
+        torch.cuda.synchronize()
+        caught["eager"] = [str(m.message) for m in w]
+        w.clear()
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(2):
+                step(1)
+        torch.cuda.current_stream().wait_stream(side)
+        torch.cuda.synchronize()
+        caught["warmup"] = [str(m.message) for m in w]
+        w.clear()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            gl = step(1)
+        caught["capture"] = [str(m.message) for m in w]
+        w.clear()
+        for _ in range(3):
+            graph.replay()
+            losses.append(gl.clone())
+        torch.cuda.synchronize()
+        caught["replay"] = [str(m.message) for m in w]
+    bad = {k: [m for m in v if "AccumulateGrad" in m] for k, v in caught.items()}
+    print("warnings per phase:", {k: len(v) for k, v in bad.items()})
+    assert not any(bad.values()), bad
+    assert all(torch.isfinite(t).item() for t in losses)
+    assert opts[1].state_dict()["step"] == 5
+    for n in nets:
+        for p in n.parameters():
+            assert torch.isfinite(p).all()
+    p0 = torch.cat([p.detach().reshape(-1) for p in base.parameters()]).to(device)
+    d0 = torch.cat([p.detach().reshape(-1) for p in nets[0].parameters()]) - p0
+    d1 = torch.cat([p.detach().reshape(-1) for p in nets[1].parameters()]) - p0
+    cos = (d0 @ d1 / (d0.norm() * d1.norm())).item()
+    print(f"config 3: losses {[round(t.item(), 3) for t in losses]}, cos(eager, graph) {cos:.5f}")
+    assert cos > 0.99, cos
+    assert abs(d1.norm().item() / d0.norm().item() - 1) < 0.05

@@ -438,14 +438,17 @@ def test_rgb_train_step_grads(dtype):
     assert abs(o[1].item() - out[1].item()) < 1e-3 * out[1].item()
     assert abs(o[2].item() - out[2].item()) < 1e-3 * out[2].item()
     (4096 * o[1] + o[2]).backward()
-    bad = []
+    bad, errs = [], []
     for n, p in netg.named_parameters():
         r = sd[n].grad
         if r is None or r.abs().max() == 0:
             continue
         e = nrel(p.grad, r)
-        if e > 2e-2:
+        errs.append((e, n))
+        if e > 1e-3:
             bad.append((n, e))
+    errs.sort()
+    print("rgb codec grads: median rel", errs[len(errs) // 2], "max", errs[-3:])
     assert not bad, bad[:10]
 
 
@@ -510,3 +513,30 @@ def test_direct_weight_grad_accumulation_matches_autograd():
         torch.cuda.synchronize()
         grads.append(opt.flat_grad.clone())
     assert rel(grads[1], grads[0]) < 1e-5
+
+
+def test_fpatch_tile_never_reaches_a_training_pack():
+    """A fragment-streamed tile (42..47, 50) cached or forced for a conv shape is valid for a
+    forward PackedConv only: a training pack (TPack, re-gathered in the plain layout every
+    step) of the same shape must fall back to a plain-layout tile and give the same output
+    (a stale fragment-major copy would otherwise be used from step 2 on)."""
+    from rgbac import runtime as rt
+    from rgbac.autograd import TPack
+    g = _gen(81)
+    dev = torch.device("cuda")
+    w = torch.randn((128, 128, 3, 3), generator=g).to(dev) * 0.05
+    b = torch.randn(128, generator=g).to(dev)
+    x = rt.to_nhwc(torch.randn((2, 128, 32, 32), generator=g).to(dev), torch.bfloat16)
+    pk = rt.PackedConv(w, b, rt.CONV, [(128, 128)], torch.bfloat16)
+    tp = TPack(pk, torch.zeros(pk.w.shape, dtype=torch.long, device=dev), torch.bfloat16)
+    tp.w.copy_(pk.w)
+    tp.bias.copy_(pk.bias)
+    want = rt.launch([rt.prepare(pk, [x.src()])], force=(1, 1))[0]
+    got = rt.launch([rt.prepare(tp, [x.src()])], force=(44, 1))[0]
+    assert rt.LAST_CHOICE[0][0] not in rt.FPATCH_SIG
+    assert getattr(tp, "frag", None) is None
+    torch.cuda.synchronize()
+    assert torch.equal(got.t, want.t) or (got.t.float() - want.t.float()).abs().max() < 2e-2
+    # the forward pack itself does take the fragment tile
+    rt.launch([rt.prepare(pk, [x.src()])], force=(44, 1))
+    assert rt.LAST_CHOICE[0][0] == 44

@@ -4,6 +4,7 @@ The reference ships no tests or vectors and cannot be imported here (SURVEY.md
 §8c), so these KATs are derived from first principles for each restated op.
 """
 import math
+import os
 
 import numpy as np
 import pytest
@@ -189,3 +190,33 @@ def test_ms_ssim_oracle_known_answers():
     s, cs = rm.ssim_level(A, Bc, rm.fspecial_gauss_1d(11, 1.5).repeat(1, 1, 1, 1), 1.0)
     # fp32 E[X^2] - mu^2 cancels to ~1e-7 against C2 = 9e-4: 1e-3 covers that noise
     assert abs(s.item() - want) < 1e-3 and abs(cs.item() - 1.0) < 1e-3
+
+
+def test_teacher_forcing_with_own_latents_is_identity():
+    """oracle/parity.py: forcing the oracle's OWN z_hat / y_hat reproduces its free-running
+    forward exactly, and the accounting of a forward against itself finds no flip."""
+    import importlib.util
+    from oracle import parity
+    spec = importlib.util.spec_from_file_location(
+        "make_golden", os.path.join(os.path.dirname(__file__), "golden", "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    sd = mg.rgb_model(mg.LATENT_GAIN).state_dict()
+    x, a = mg.rgb_inputs(2, 64, 64, seed=3)
+    me = ref.supply_mask(a)
+    dbg = {}
+    with torch.no_grad():
+        free = ref.rgb_forward(sd, x, a, a, *me[:4], dbg=dbg)
+    tf, dbg2 = parity.teacher_forced(sd, "rgb", x, dbg["y_hat"], dbg["z_hat"], a, a)
+    for u, v in zip(free, tf):
+        assert torch.equal(u, v)
+    rep = parity.symbol_accounting(dbg["y"], dbg["mu"], dbg2["y"], dbg2["mu"], dbg["z"],
+                                   dbg2["z"], dbg2["z_med"], dbg["lik"], dbg2["lik"])
+    assert rep["flips"] == 0 and rep["z_flips"] == 0 and rep["noise_floor"] == 0.0
+    assert rep["nonzero_symbols"] > rep["symbols"] // 4
+    assert rep["bits_unflipped_rel"] == 0.0
+    # a planted flip far from any tie is classified "far"
+    y_bad = [t.clone() for t in dbg["y"]]
+    y_bad[3][0, 0, 0, 0] += 1.0
+    rep = parity.symbol_accounting(y_bad, dbg["mu"], dbg2["y"], dbg2["mu"])
+    assert rep["flips"] == 1 and rep["far_flips"] == 1
