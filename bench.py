@@ -189,7 +189,7 @@ def gpu_parity(net, dev, outs_ref, S=256, account=False):
                 acc[k] += rep.get(k, 0)
             acc["noise_floor"] = max(acc["noise_floor"], rep["noise_floor"])
             acc["tf_max_abs_d_psnr_db"] = max(acc["tf_max_abs_d_psnr_db"], rep["tf_d_psnr_db"] or 0.0)
-            acc["tf_max_abs_d_ms_ssim"] = max(acc["tf_max_abs_d_ms_ssim"], rep["tf_d_ms_ssim"])
+            acc["tf_max_abs_d_ms_ssim"] = max(acc["tf_max_abs_d_ms_ssim"], rep["tf_d_ms_ssim"] or 0.0)
             acc["max_bits_unflipped_rel"] = max(acc["max_bits_unflipped_rel"],
                                                 rep["bits_unflipped_rel"])
             rec_acc = {"flips": rep["flips"], "near_tie_flips": rep["near_tie_flips"],
@@ -197,7 +197,8 @@ def gpu_parity(net, dev, outs_ref, S=256, account=False):
                        "per_slice_flips": rep["per_slice_flips"],
                        "tf_d_psnr_db": None if rep["tf_d_psnr_db"] is None
                        else float(f"{rep['tf_d_psnr_db']:.3g}"),
-                       "tf_d_ms_ssim": float(f"{rep['tf_d_ms_ssim']:.3g}")}
+                       "tf_d_ms_ssim": None if rep["tf_d_ms_ssim"] is None
+                       else float(f"{rep['tf_d_ms_ssim']:.3g}")}
         rb, rm, rms = outs_ref[i]
         psnr = 10 * math.log10(1.0 / mse) if mse > 0 else None
         rpsnr = 10 * math.log10(1.0 / rm) if rm > 0 else None

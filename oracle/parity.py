@@ -131,9 +131,11 @@ def north_star_report(sd, kind, inp, mask, dev, dev_out):
     rep["tf_max_abs_dx_hat"] = (xd - xr).abs().max().item()
     pd, pr = psnr_db(float(dev_out[1])), psnr_db(tf[1].item())
     rep["tf_d_psnr_db"] = None if pd is None or pr is None else abs(pd - pr)
-    with torch.no_grad():
-        msd = ref_metrics.ms_ssim(inp, xd.clamp(0, 1), data_range=1.0).item()
-        msr = ref_metrics.ms_ssim(inp, xr.clamp(0, 1), data_range=1.0).item()
-    rep["tf_d_ms_ssim"] = abs(msd - msr)
+    rep["tf_d_ms_ssim"] = None
+    if min(inp.shape[-2:]) > 160:                # ms_ssim_torch.py:158-160 (5 levels, win 11)
+        with torch.no_grad():
+            msd = ref_metrics.ms_ssim(inp, xd.clamp(0, 1), data_range=1.0).item()
+            msr = ref_metrics.ms_ssim(inp, xr.clamp(0, 1), data_range=1.0).item()
+        rep["tf_d_ms_ssim"] = abs(msd - msr)
     rep["tf_rel_d_bpp"] = abs(float(dev_out[2]) - tf[2].item()) / max(abs(tf[2].item()), 1e-30)
     return rep

@@ -56,7 +56,7 @@ def _check(rep, e2e, tag):
           f"{rep['flips']} (near-tie {rep['near_tie_flips']}, far {rep['far_flips']}), per slice "
           f"{rep['per_slice_flips']}, z flips {rep.get('z_flips')}, noise floor "
           f"{rep['noise_floor']:.2e}, bits(unflipped) rel {rep['bits_unflipped_rel']:.2e}, "
-          f"teacher-forced dPSNR {rep['tf_d_psnr_db']} dMS-SSIM {rep['tf_d_ms_ssim']:.2e} "
+          f"teacher-forced dPSNR {rep['tf_d_psnr_db']} dMS-SSIM {rep['tf_d_ms_ssim']} "
           f"max|dx_hat| {rep['tf_max_abs_dx_hat']:.2e}; free-running {e2e}")
     assert rep["nonzero_symbols"] > rep["symbols"] // 4, "vacuous: symbols mostly zero"
     assert rep["noise_floor"] < 1e-3
