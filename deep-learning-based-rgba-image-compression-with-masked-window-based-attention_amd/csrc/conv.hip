@@ -1473,7 +1473,9 @@ static const TileCfg kTiles[] = {
     // 48, 49: patch-resident kernel with a 4-deep weight ring
     {128, 64}, {128, 128},
     // 50: fragment-streamed patch kernel, 4 x 16 pixels x 64 channels
-    {64, 64}};
+    {64, 64},
+    // 51..53: fragment-streamed patch kernel, unrolled K split by kernel row (KS = 3)
+    {64, 64}, {64, 128}, {64, 192}};
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 constexpr int kFirstWres = 7;
 constexpr int kWresStages = 6;
@@ -1488,6 +1490,7 @@ constexpr int kFirstPatch = 36;    // 36..41: conv_patch_kernel (bf16; k3 s1 con
 constexpr int kFirstFPatch = 42;   // 42..47: conv_fpatch_kernel (fragment-major weights)
 constexpr int kFirstPatch2 = 48;   // 48, 49: conv_patch_kernel with NBUF = 4
 constexpr int kTileFPatch464 = 50; // conv_fpatch_kernel<4, 64>
+constexpr int kFirstFPatchKS = 51; // 51..53: conv_fpatch_kernel<4, 64|128|192, ..., KS = 3>
 #ifndef RGBAC_RC1
 #define RGBAC_RC1 24   // unrolled-K fragment-patch weight ring depth at TN 1 (TN 2: half)
 #endif
@@ -2201,17 +2204,27 @@ _Pragma("unroll")                                                               
 // and zero patch channels in the padding).  Waves: 1 (M) x NW (N); wave = TH rows of 16
 // pixels x BN/NW channels.  Each phase's k-steps are padded to a multiple of R (idle steps)
 // so the unrolled ring never straddles a phase's epilogue.
-template <int TH, int BN, int NW, int R, int CPT = 0>
-__global__ void __launch_bounds__(64 * NW) conv_fpatch_kernel(const ConvArgsDev args) {
+//
+// KS = 3 (unrolled-K variants only): the K loop is split by kernel row -- 3 x NW waves, wave
+// (kp, wn) runs the 3 taps of row dy = kp (3 x CPT k-steps) for N wave wn, so each SIMD holds
+// three independent k-step chains instead of one (the 32x32-latent slice convs launch about
+// one workgroup per CU: with one wave per SIMD every k-step paid its LDS / L2 latency in
+// full).  The row partials are summed through LDS (over the dead patch) in the fixed order
+// dy 0 + dy 1 + dy 2 and the dy-0 waves run the epilogue.
+template <int TH, int BN, int NW, int R, int CPT = 0, int KS = 1>
+__global__ void __launch_bounds__(64 * NW * KS) conv_fpatch_kernel(const ConvArgsDev args) {
   using T = bf16_t;
   constexpr int TW = 16, PW = TW + 2, PR = (TH + 2) * PW;
   constexpr int TM = TH, TN = BN / NW / 16;
   static_assert(TN * NW * 16 == BN, "tile");
+  static_assert(KS == 1 || (KS == 3 && CPT > 0), "K split by kernel row: unrolled-K only");
   extern __shared__ __attribute__((aligned(16))) uint4 patch[];
 
   const ConvShared& s = args.s;
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave = KS > 1 ? wave_all % NW : wave_all;       // N wave
+  const int kp = KS > 1 ? wave_all / NW : 0;                // kernel row of this K part
   const int txn = s.Wm / TW, tyn = s.Hm / TH;
   int nblk, txi, tyi, b, gi;
   {
@@ -2251,12 +2264,16 @@ __global__ void __launch_bounds__(64 * NW) conv_fpatch_kernel(const ConvArgsDev 
   // A k-step is only TN x TM MFMAs (64-128 cycles), so the weight ring runs RC steps ahead
   // (RC x the step >= an L2 round trip): 12 steps at TN 1, 8 at TN 2, 4 beyond.
   constexpr int NKSC = 9 * (CPT > 0 ? CPT : 1);
-  constexpr int RC = CPT > 0 ? (TN == 1 ? RGBAC_RC1 : (TN == 2 ? RGBAC_RC1 / 2 : 4)) : 1;
+  constexpr int NKSP = NKSC / KS;                // k-steps of this wave's K part
+  constexpr int RC0 = CPT > 0 ? (TN == 1 ? RGBAC_RC1 : (TN == 2 ? RGBAC_RC1 / 2 : 4)) : 1;
+  constexpr int RC1 = KS > 1 ? (RC0 + 1) / 2 : RC0;   // three chains per SIMD share the latency
+  constexpr int RC = RC1 < NKSP ? RC1 : NKSP;
   const uint4* wj[TN];
   uint4 cring[RC][TN];
   if constexpr (CPT > 0) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) wj[j] = wf + ((size_t)(ntile0 + j) * NKSC) * 64 + lane;
+    for (int j = 0; j < TN; ++j)
+      wj[j] = wf + ((size_t)(ntile0 + j) * NKSC + kp * NKSP) * 64 + lane;
 #pragma unroll
     for (int u = 0; u < RC; ++u)
 #pragma unroll
@@ -2273,7 +2290,7 @@ __global__ void __launch_bounds__(64 * NW) conv_fpatch_kernel(const ConvArgsDev 
     const int total = PR * RSc;
     const int npiece = (total + 63) >> 6;
     const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lptr_t)patch);
-    for (int pc = wave; pc < npiece; pc += NW) {
+    for (int pc = wave_all; pc < npiece; pc += NW * KS) {
       const int f = (pc << 6) + lane;
       const int row = f / RSc, c = f - (f / RSc) * RSc;
       const int py = row / PW, px = row - (row / PW) * PW;
@@ -2298,14 +2315,15 @@ __global__ void __launch_bounds__(64 * NW) conv_fpatch_kernel(const ConvArgsDev 
     const int fr = lane & 15, fq = lane >> 4;
     int lb[TM];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) lb[i] = (i * PW + fr) * RS + fq;
+    for (int i = 0; i < TM; ++i) lb[i] = ((i + kp) * PW + fr) * RS + fq;
     f32x4 acc[TN][TM];
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < NKSC; ++ks) {
+    for (int ks = 0; ks < NKSP; ++ks) {
+      // KS 3: ks < 3 * CPT, so tap / 3 == 0 and the row offset sits in lb
       const int tap = ks / CPT, cc = ks - (ks / CPT) * CPT;
       const int off = ((tap / 3) * PW + tap % 3) * RS + cc * 4;
       uint4 bb[TM];
@@ -2315,10 +2333,33 @@ __global__ void __launch_bounds__(64 * NW) conv_fpatch_kernel(const ConvArgsDev 
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int i = 0; i < TM; ++i) mma_step<T>(acc[j][i], cring[ks % RC][j], bb[i]);
-      if (ks + RC < NKSC) {
+      if (ks + RC < NKSP) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) cring[ks % RC][j] = wj[j][(ks + RC) * 64];
       }
+    }
+    if constexpr (KS > 1) {
+      f32x4* const red = reinterpret_cast<f32x4*>(patch);
+      __syncthreads();                            // every wave is done with the patch
+      if (kp > 0) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            red[((((kp - 1) * NW + wave) * TN + j) * TM + i) * 64 + lane] = acc[j][i];
+      }
+      __syncthreads();
+      if (kp > 0) return;
+#pragma unroll
+      for (int q = 0; q < KS - 1; ++q)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int i = 0; i < TM; ++i) {
+            const f32x4 t = red[(((q * NW + wave) * TN + j) * TM + i) * 64 + lane];
+            acc[j][i] = f32x4{acc[j][i][0] + t[0], acc[j][i][1] + t[1], acc[j][i][2] + t[2],
+                              acc[j][i][3] + t[3]};
+          }
     }
     int nn[TN];
 #pragma unroll
@@ -2461,15 +2502,20 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
     }
     return check_launch("conv_wres_kernel");
   }
-  if ((tile >= kFirstFPatch && tile < kFirstPatch2) || tile == kTileFPatch464) {
+  if ((tile >= kFirstFPatch && tile < kFirstPatch2) || tile >= kTileFPatch464) {
     if constexpr (sizeof(T) == 2) {
       const int th = tc.bm / 16;
       const int nbn = (max_cout + tc.bn - 1) / tc.bn;
       const long long nsp = (long long)s.batch * (s.Hm / th) * (s.Wm / 16) * s.ngroups;
       int cmax = 0;
       for (int i = 0; i < s.ngroups; ++i) cmax = d.g[i].cin_pad > cmax ? d.g[i].cin_pad : cmax;
-      const size_t lds = ((size_t)(th + 2) * 18 * (((cmax + 31) & ~31) / 8 + 2) * 16 + 1023) &
-                         ~(size_t)1023;                   // whole 1-KiB DMA pieces
+      size_t lds = ((size_t)(th + 2) * 18 * (((cmax + 31) & ~31) / 8 + 2) * 16 + 1023) &
+                   ~(size_t)1023;                         // whole 1-KiB DMA pieces
+      const bool ks3 = tile >= kFirstFPatchKS;
+      if (ks3) {                                          // row partials over the patch
+        const size_t red = (size_t)2 * (tc.bn / 16) * th * 64 * 16;
+        if (red > lds) lds = red;
+      }
       if (lds > 160 * 1024) {
         set_error("fragment-patch tile: the input patch exceeds 160 KiB of LDS");
         return RGBAC_E_ARG;
@@ -2485,6 +2531,10 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
         if (cpt != 3 && cpt != 4 && cpt != 7) cpt = 0;
         if (!fpatch_cpt_enabled()) cpt = 0;
       }
+      if (ks3 && cpt == 0) {
+        set_error("K-split fragment-patch tiles: 3x3 conv with 96/128/224-channel inputs only");
+        return RGBAC_E_ARG;
+      }
 #define RGBAC_FP1(TH_, BN_, C_)                                                               \
   do {                                                                                        \
     auto k_ = conv_fpatch_kernel<TH_, BN_, 4, 4, C_>;                                         \
@@ -2495,6 +2545,23 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
       attr_ = true;                                                                           \
     }                                                                                         \
     hipLaunchKernelGGL(k_, grid, dim3(256), lds, st, d);                                      \
+  } while (0)
+#define RGBAC_FPK(BN_, C_)                                                                    \
+  do {                                                                                        \
+    auto k_ = conv_fpatch_kernel<4, BN_, 4, 4, C_, 3>;                                        \
+    static bool attr_ = false;                                                                \
+    if (!attr_) {                                                                             \
+      (void)hipFuncSetAttribute((const void*)k_, hipFuncAttributeMaxDynamicSharedMemorySize,  \
+                                160 * 1024);                                                  \
+      attr_ = true;                                                                           \
+    }                                                                                         \
+    hipLaunchKernelGGL(k_, grid, dim3(768), lds, st, d);                                      \
+  } while (0)
+#define RGBAC_FPKS(BN_)                                                                       \
+  do {                                                                                        \
+    if (cpt == 3) RGBAC_FPK(BN_, 3);                                                          \
+    else if (cpt == 4) RGBAC_FPK(BN_, 4);                                                     \
+    else RGBAC_FPK(BN_, 7);                                                                   \
   } while (0)
 #define RGBAC_FP(TH_, BN_)                                                                    \
   do {                                                                                        \
@@ -2511,10 +2578,15 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
         case 45: RGBAC_FP(4, 128); break;
         case 46: RGBAC_FP(8, 256); break;
         case kTileFPatch464: RGBAC_FP(4, 64); break;
+        case kFirstFPatchKS: RGBAC_FPKS(64); break;
+        case kFirstFPatchKS + 1: RGBAC_FPKS(128); break;
+        case kFirstFPatchKS + 2: RGBAC_FPKS(192); break;
         default: RGBAC_FP(8, 64); break;
       }
 #undef RGBAC_FP
 #undef RGBAC_FP1
+#undef RGBAC_FPKS
+#undef RGBAC_FPK
       return check_launch("conv_fpatch_kernel");
     } else {
       set_error("the fragment-patch tiles are bf16 only");
@@ -2679,11 +2751,11 @@ static int fill_group(const rgbac_conv_args* a, int ntaps_max, ConvGroup& g) {
 using namespace rgbac;
 
 extern "C" int rgbac_conv_num_tiles(void) { return kNumTiles; }
-// 1 for the fragment-streamed patch tiles (42..47, 50), whose `weight` must be the
+// 1 for the fragment-streamed patch tiles (42..47, 50..53), whose `weight` must be the
 // fragment-major copy documented in rgbac.h; 0 for the plain packed layout; -1 out of range.
 extern "C" int rgbac_conv_tile_weight_layout(int tile) {
   if (tile < 0 || tile >= kNumTiles) return -1;
-  return ((tile >= 42 && tile <= 47) || tile == 50) ? 1 : 0;
+  return ((tile >= 42 && tile <= 47) || tile >= 50) ? 1 : 0;
 }
 extern "C" int rgbac_conv_max_groups(void) { return kMaxGroups; }
 
@@ -2789,7 +2861,7 @@ extern "C" int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroup
                                          kTiles[a->tile].bn) * kTiles[a->tile].bn &&
                         args[i].k_pad >= ntaps_max * args[i].cin_pad &&
                         ((a->tile < kFirstFPatch || a->tile >= kFirstPatch2) &&
-                             a->tile != kTileFPatch464 ||
+                             a->tile < kTileFPatch464 ||
                          args[i].cout_pad % 16 == 0),
                     "patch tiles read whole BN-row weight tiles");
   } else if (a->tile == kTileWStream) {

@@ -120,7 +120,8 @@ TILES = [(128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 1
          (128, 192), (128, 128), (128, 96), (128, 256), (128, 192), (128, 64),
          (128, 192), (64, 192), (128, 128), (64, 128), (128, 256), (128, 64),
          (128, 64), (128, 128),
-         (64, 64)]
+         (64, 64),
+         (64, 64), (64, 128), (64, 192)]
 FIRST_WRES = 7
 WRES_STAGES = 6
 FIRST_DIRECT = 13        # 13..18: direct kernel (plain conv, K <= DIRECT_STEPS MFMA k-steps)
@@ -141,7 +142,10 @@ PATCH_SIG = {36: (8, 192, 2, 4, 3), 37: (8, 128, 2, 4, 3), 38: (8, 96, 4, 2, 3),
              48: (8, 64, 4, 2, 4), 49: (8, 128, 2, 4, 4)}
 FIRST_FPATCH = 42        # 42..47: conv_fpatch_kernel (fragment-major weight copy, 4 waves)
 FPATCH_SIG = {42: (8, 192), 43: (4, 192), 44: (8, 128), 45: (4, 128), 46: (8, 256), 47: (8, 64),
-              50: (4, 64)}
+              50: (4, 64), 51: (4, 64), 52: (4, 128), 53: (4, 192)}
+# 51..53: the unrolled-K variants with K split by kernel row (KS = 3, 12 waves): only where
+# the unrolled-K variant applies (fpatch_cpt != 0)
+FPATCH_KS = (51, 52, 53)
 # the fragment-patch kernel's unrolled-K variants (csrc/conv.hip, CPT template argument)
 FPATCH_CPT = os.environ.get("RGBAC_FPATCH_CPT", "1") != "0"
 
@@ -204,8 +208,11 @@ def _patch_tiles(preps):
     # every step in the plain layout) and the whole patch in LDS
     if all(isinstance(p.pk, PackedConv) for p in preps):
         c32 = max(round_up(p.pk.cin_pad, 32) for p in preps)
+        cpt = fpatch_cpt(preps)
         for t, (th, bn) in FPATCH_SIG.items():
             if hm % th or (th + 2) * 18 * (c32 // 8 + 2) * 16 > 160 * 1024:
+                continue
+            if t in FPATCH_KS and not cpt:
                 continue
             if all(p.pk.cout_pad >= -(-p.pk.cout // bn) * bn for p in preps):
                 out.append(t)
@@ -566,6 +573,8 @@ def kernel_name(tile, preps):
     dt = "float" if preps[0].a.dtype == 0 else "bf16_t"
     if tile == TILE_SPATIAL:
         return f"conv3x3_c32_kernel<{dt}>"
+    if tile in FPATCH_KS:
+        return "conv_fpatch_kernel<4, %d, 4, 4, %d, 3>" % (FPATCH_SIG[tile][1], fpatch_cpt(preps))
     if tile in FPATCH_SIG:
         c = fpatch_cpt(preps) if FPATCH_SIG[tile][0] == 4 else 0
         return "conv_fpatch_kernel<%d, %d, 4, 4%s>" % (FPATCH_SIG[tile] + (f", {c}" if c else "",))
