@@ -43,6 +43,22 @@
 
 namespace rgbac {
 
+#ifdef RGBAC_WG_TIMING
+// probe builds only (tools/wg_probe.py): per-workgroup 100-MHz wall-clock stamps at phase
+// boundaries of the slice-chain conv kernels (0 start, 1 operands staged / K loop entered,
+// 2 K loop done, 3 end), recorded by thread 0
+__device__ unsigned long long g_wg_t[16384][4];
+#define WG_T(k)                                                                              \
+  do {                                                                                       \
+    if (threadIdx.x == 0) {                                                                  \
+      const unsigned b_ = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);    \
+      if (b_ < 16384) g_wg_t[b_][k] = wall_clock64();                                        \
+    }                                                                                        \
+  } while (0)
+#else
+#define WG_T(k) do {} while (0)
+#endif
+
 constexpr int kMaxGroups = 10;
 
 struct ConvGroup {                  // per-group operands
@@ -438,6 +454,21 @@ template <typename T>
 __device__ __forceinline__ float gauss_elem(const ConvGroup& g, int m, int c, int nch, float mu,
                                             float sg) {
   const float yv = Elem<T>::ld(reinterpret_cast<const T*>(g.res1) + (long long)m * g.ld1 + c);
+  const float hat = rintf(yv - mu) + mu;
+  Elem<T>::st(reinterpret_cast<T*>(g.out) + (long long)m * g.out_ldc + g.out_coff + c, hat);
+  const float xin = g.aux0 ? yv + g.aux0[(long long)m * nch + c] : hat;
+  const float v = fabsf(xin - mu);
+  const float sc = fmaxf(sg, 0.11f);
+  const float lik = fmaxf(std_cum_f((0.5f - v) / sc) - std_cum_f((-0.5f - v) / sc), 1e-9f);
+  if (g.aux1) g.aux1[(long long)m * nch + c] = lik;
+  const float bits = (-1.0f * logf(lik + 1e-10f)) / 0.69314718055994530942f;
+  return fminf(fmaxf(bits, 0.0f), 50.0f);
+}
+
+// gauss_elem with y (res1) already loaded by the caller
+template <typename T>
+__device__ __forceinline__ float gauss_elem_y(const ConvGroup& g, int m, int c, int nch, float mu,
+                                              float sg, float yv) {
   const float hat = rintf(yv - mu) + mu;
   Elem<T>::st(reinterpret_cast<T*>(g.out) + (long long)m * g.out_ldc + g.out_coff + c, hat);
   const float xin = g.aux0 ? yv + g.aux0[(long long)m * nch + c] : hat;
@@ -1475,7 +1506,14 @@ static const TileCfg kTiles[] = {
     // 50: fragment-streamed patch kernel, 4 x 16 pixels x 64 channels
     {64, 64},
     // 51..53: fragment-streamed patch kernel, unrolled K split by kernel row (KS = 3)
-    {64, 64}, {64, 128}, {64, 192}};
+    {64, 64}, {64, 128}, {64, 192},
+    // 54: full-width pointwise kernel (32-pixel wave tiles x all 192 output channels)
+    {32, 192},
+    // 55: narrow-output patch kernel (4 x 16 pixels x <= 32 channels, K split over 8 waves)
+    {64, 32},
+    // 56..58: K-split fragment-patch kernel on taller tiles (TH x 16 pixels: the weight
+    // panel, most of a workgroup's bytes, amortised over 2-4x the pixels)
+    {128, 64}, {128, 128}, {256, 32}};
 constexpr int kNumTiles = sizeof(kTiles) / sizeof(kTiles[0]);
 constexpr int kFirstWres = 7;
 constexpr int kWresStages = 6;
@@ -1491,6 +1529,15 @@ constexpr int kFirstFPatch = 42;   // 42..47: conv_fpatch_kernel (fragment-major
 constexpr int kFirstPatch2 = 48;   // 48, 49: conv_patch_kernel with NBUF = 4
 constexpr int kTileFPatch464 = 50; // conv_fpatch_kernel<4, 64>
 constexpr int kFirstFPatchKS = 51; // 51..53: conv_fpatch_kernel<4, 64|128|192, ..., KS = 3>
+constexpr int kTilePW = 54;        // conv_pw_kernel (bf16 1x1, one source, cin/cout <= 192)
+constexpr int kTileNPatch = 55;    // conv_npatch_kernel (bf16 3x3 s1, cout <= 32, fragment-major)
+constexpr int kFirstFPatchKS2 = 56; // 56..58: conv_fpatch_kernel<8,64|8,128|16,32, ..., KS = 3>
+__host__ __device__ constexpr bool fpatch_tile(int t) {
+  return (t >= 42 && t <= 47) || (t >= 50 && t <= 53) || (t >= 56 && t <= 58);
+}
+__host__ __device__ constexpr bool fpatch_ks_tile(int t) {
+  return (t >= 51 && t <= 53) || (t >= 56 && t <= 58);
+}
 #ifndef RGBAC_RC1
 #define RGBAC_RC1 24   // unrolled-K fragment-patch weight ring depth at TN 1 (TN 2: half)
 #endif
@@ -1665,6 +1712,387 @@ static void launch_smallk(const ConvArgsDev& d, int nks16, int max_cout, hipStre
 }
 
 // ---------------------------------------------------------------------------
+// Full-width pointwise kernel (bf16; 1x1 stride-1 conv, one source, cin_pad <= 16 * NKS,
+// cout <= 192): the HBM-bound 1x1 convs at full resolution -- GDN / IGDN norm pools, the
+// attention block's output gate, ... .  conv_smallk_kernel holds 96 output rows per
+// workgroup (two column blocks re-read the input: 1.5x the algorithmic bytes on the 128^2
+// IGDN), stages its weight panel through registers behind a barrier and pays one memory
+// round trip per 32-channel column of the epilogue.  Here:
+//   * one workgroup holds all 192 rows of the weight panel in LDS (LDS-DMA, 16-byte chunk c
+//     of row r at slot c ^ (r & 7): conflict-free ds_read_b128 for the 8-lane groups), so
+//     every input pixel is read from HBM once;
+//   * each wave streams 32-pixel tiles: per 16-deep k-step ONE 16-byte load per lane
+//     straight into VGPRs feeds 6 v_mfma_f32_32x32x16_bf16, and is reloaded with the NEXT
+//     tile's fragment right behind its MFMAs (a register ring: the next tile's input is in
+//     flight during this tile's MFMAs and epilogue);
+//   * the epilogue operands (res0 / res1 / res2, raw bf16) of ALL 24 channel quads of the
+//     tile are requested before the MFMAs: one memory latency per tile, not per column.
+// Persistent grid (one workgroup per CU, 4 waves); no barrier after the weight panel.
+template <int NKS>
+__global__ void __launch_bounds__(256, 1) conv_pw_kernel(const ConvArgsDev args) {
+  constexpr int NT = 6, BN = 192, NCH = 2 * NKS;   // 16-byte chunks per weight row
+  static_assert(NCH % 8 == 0, "swizzle groups of 8 chunks");
+  constexpr int NPIECE = BN * NCH / 64;            // 1-KiB LDS-DMA pieces of the panel
+  extern __shared__ __attribute__((aligned(16))) uint4 Wl[];
+  __shared__ float bl[BN];
+  const ConvShared& s = args.s;
+  const ConvGroup& g = args.g[blockIdx.z];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nchunk = g.cin_pad >> 3;               // real 8-channel chunks of K
+  {
+    // weight panel: LDS slot d = 64 p + lane -> (row, slot), source chunk slot ^ (row & 7)
+    const bf16_t* wbase = reinterpret_cast<const bf16_t*>(g.w);
+    const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lptr_t)Wl);
+    for (int p = wave; p < NPIECE; p += 4) {
+      const int d = p * 64 + lane;
+      const int row = d / NCH, slot = d - (d / NCH) * NCH;
+      const int ch = slot ^ (row & 7);
+      const bool ok = row < g.rows && ch < nchunk;
+      dma16_l(ok ? (const void*)(wbase + (size_t)row * g.k_pad + ch * 8) : (const void*)g_zero_page,
+              lbase + p * 1024);
+    }
+  }
+  for (int e = tid; e < BN; e += 256) bl[e] = (g.bias && e < g.cout) ? g.bias[e] : 0.0f;
+  wait_vm<0>();
+  __syncthreads();
+
+  const int Mtot = s.M, act = s.act;
+  const int ld = (int)g.sld0;
+  const bool sq_in = s.square != 0;
+  const int r32 = lane & 31, h = lane >> 5;
+  const char* const src = reinterpret_cast<const char*>(g.sp0) + 16 * h;
+  const int ntile = (Mtot + 31) / 32;
+  const int tstride = gridDim.x * 4;
+  int tile = blockIdx.x * 4 + wave;
+  if (tile >= ntile) return;
+
+#define PWW_LOAD(dst, st, rowp_, valid_)                                                      \
+  do {                                                                                        \
+    const bool ok_ = (valid_) & (2 * (st) + h < nchunk);                                      \
+    const uint4* p_ = ok_ ? reinterpret_cast<const uint4*>((rowp_) + 32 * (st)) : g_zero_page; \
+    dst = *p_;                                                                                \
+  } while (0)
+
+  uint4 bv[NKS];
+  {
+    const int m = tile * 32 + r32;
+    const bool valid = m < Mtot;
+    const char* rowp = src + (size_t)(valid ? m : 0) * ld * 2;
+#pragma unroll
+    for (int st = 0; st < NKS; ++st) PWW_LOAD(bv[st], st, rowp, valid);
+  }
+  const bf16_t* const R0 = reinterpret_cast<const bf16_t*>(g.res0);
+  const bf16_t* const R1 = reinterpret_cast<const bf16_t*>(g.res1);
+  const bf16_t* const R2 = reinterpret_cast<const bf16_t*>(g.res2);
+  const int cout = g.cout;
+  for (; tile < ntile; tile += tstride) {
+    const int m = tile * 32 + r32;
+    const bool valid = m < Mtot;
+    const long long mm = valid ? m : 0;
+    // epilogue operands of the whole tile (raw bf16 quads), requested before the MFMAs
+    uint2 e0[NT][4], e1[NT][4], e2[NT][4];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = j * 32 + 8 * q + 4 * h;
+        const bool on = valid && n < cout;
+        e0[j][q] = (R0 && on) ? *reinterpret_cast<const uint2*>(R0 + mm * g.ld0 + n) : make_uint2(0, 0);
+        e1[j][q] = (R1 && on) ? *reinterpret_cast<const uint2*>(R1 + mm * g.ld1 + n) : make_uint2(0, 0);
+        e2[j][q] = (R2 && on) ? *reinterpret_cast<const uint2*>(R2 + mm * g.ld2 + n) : make_uint2(0, 0);
+      }
+    const bool sel_on = act == RGBAC_ACT_MASKSEL ? (valid && g.sel[mm] != 0) : true;
+    const int mn = (tile + tstride) * 32 + r32;
+    const bool nvalid = mn < Mtot;
+    const char* nrowp = src + (size_t)(nvalid ? mn : 0) * ld * 2;
+    f32x16 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+#pragma unroll
+    for (int st = 0; st < NKS; ++st) {
+      uint4 b = bv[st];
+      if (sq_in) b = square_chunk<bf16_t>(b);
+      const bf16x8 bb = __builtin_bit_cast(bf16x8, b);
+      const int slot = (2 * st + h) ^ (r32 & 7);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const uint4 a = Wl[(j * 32 + r32) * NCH + slot];
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), bb,
+                                                         acc[j], 0, 0, 0);
+      }
+      PWW_LOAD(bv[st], st, nrowp, nvalid);
+    }
+    if (valid) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int nl = j * 32 + 8 * q + 4 * h;
+          if (nl < cout) {
+            EpiIn in;
+            in.r0[0] = bf2f(e0[j][q].x & 0xFFFF); in.r0[1] = bf2f(e0[j][q].x >> 16);
+            in.r0[2] = bf2f(e0[j][q].y & 0xFFFF); in.r0[3] = bf2f(e0[j][q].y >> 16);
+            in.r1[0] = bf2f(e1[j][q].x & 0xFFFF); in.r1[1] = bf2f(e1[j][q].x >> 16);
+            in.r1[2] = bf2f(e1[j][q].y & 0xFFFF); in.r1[3] = bf2f(e1[j][q].y >> 16);
+            in.r2[0] = bf2f(e2[j][q].x & 0xFFFF); in.r2[1] = bf2f(e2[j][q].x >> 16);
+            in.r2[2] = bf2f(e2[j][q].y & 0xFFFF); in.r2[3] = bf2f(e2[j][q].y >> 16);
+            in.on = sel_on;
+            float v[4] = {acc[j][4 * q], acc[j][4 * q + 1], acc[j][4 * q + 2], acc[j][4 * q + 3]};
+            const float bias[4] = {bl[nl], bl[nl + 1], bl[nl + 2], bl[nl + 3]};
+            epilogue4_fin<bf16_t>(s, g, (long long)m, nl, v, bias, in);
+          }
+        }
+    }
+  }
+#undef PWW_LOAD
+}
+
+template <int NKS>
+static void launch_pw_k(const ConvArgsDev& d, hipStream_t st) {
+  auto kern = conv_pw_kernel<NKS>;
+  constexpr size_t lds = (size_t)192 * 2 * NKS * 16;
+  static bool attr = false;
+  static int ncu = 0;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu < 1) ncu = 256;
+    attr = true;
+  }
+  const int nz = d.s.ngroups;
+  const int ntile = (d.s.M + 31) / 32;
+  int gx = (ncu + nz - 1) / nz;
+  const int need = (ntile + 3) / 4;
+  if (gx > need) gx = need;
+  if (gx < 1) gx = 1;
+  hipLaunchKernelGGL(kern, dim3(gx, 1, nz), dim3(256), lds, st, d);
+}
+
+static void launch_pw(const ConvArgsDev& d, int cin_max, hipStream_t st) {
+  if (cin_max <= 64) launch_pw_k<4>(d, st);
+  else if (cin_max <= 128) launch_pw_k<8>(d, st);
+  else launch_pw_k<12>(d, st);
+}
+
+// ---------------------------------------------------------------------------
+// Narrow-output patch kernel (bf16; 3x3 stride-1 conv, up to three concatenated sources,
+// cout <= 32): the slice chain's tail convs -- (mu | sigma) + GaussianConditional (256 -> 16)
+// and the lrp output conv (128 -> 8, y_hat = pre + tanh / 2).  conv_wstream_kernel gathers
+// every im2col fragment from L2 (9 x the input bytes per 32-pixel tile) and re-streams the
+// whole weight panel per 32 pixels; a per-workgroup timestamp probe showed its loads, not its
+// MFMAs, set the time (10.6 of 13.5 us per workgroup at 8192 pixels).  Here a workgroup owns a
+// 4 x 16-pixel tile: its (4+2) x 18-pixel input patch is staged in LDS ONCE by LDS-DMA (as
+// conv_fpatch_kernel), its 8 waves split K (each streams only its own k-steps of the
+// fragment-major weights into a register ring: every weight byte is read once per tile), the
+// wave partials are summed through LDS in a fixed order, and waves 0..3 run the epilogue of
+// one pixel row each, with the biases and the GAUSS input y requested before the K loop.
+// GAUSS: (mu | sigma) of 8 channels sit in lanes fq < 2 / fq >= 2 of one 16-row N tile (the
+// sigma quad arrives by a lane ^ 32 shuffle); of 16 channels in N tiles 0 / 1 of one lane.
+template <int TN>
+__global__ void __launch_bounds__(512) conv_npatch_kernel(const ConvArgsDev args) {
+  using T = bf16_t;
+  constexpr int TH = 4, TM = 4, TW = 16, PW = TW + 2, PR = (TH + 2) * PW, NW = 8, R = 4;
+  extern __shared__ __attribute__((aligned(16))) uint4 patch[];
+  __shared__ double wsum[TM];
+  WG_T(0);
+  const ConvShared& s = args.s;
+  const ConvGroup& g = args.g[blockIdx.z];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int txn = s.Wm / TW, tyn = s.Hm / TH;
+  int t = blockIdx.x;
+  const int txi = t % txn; t /= txn;
+  const int tyi = t % tyn;
+  const int b = t / tyn;
+  const int y0 = tyi * TH, x0 = txi * TW;
+  const int in_h = s.in_h, in_w = s.in_w, cin_pad = g.cin_pad;
+  const int cin32 = (cin_pad + 31) & ~31;
+  const int nch = cin32 >> 3, RSc = nch + 2, cpt = cin32 >> 5;
+  const int nks = 9 * cpt;
+  const int k0 = nks * wave / NW, k1 = nks * (wave + 1) / NW;
+  const bool gauss = s.act == RGBAC_ACT_GAUSS;
+  const int cout = g.cout, nho = cout >> 1;       // GAUSS: mu / sigma channels
+
+  // ---- operands of this wave's epilogue row (waves 0..TM-1), requested first
+  const int ei = wave < TM ? wave : 0;
+  const int m_e = (b * s.Hm + y0 + ei) * s.Wm + x0 + fr;
+  float pb[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = 16 * j + 4 * fq + r;
+      pb[j][r] = (g.bias && n < cout) ? g.bias[n] : 0.0f;
+    }
+  float yv[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool ylane = gauss && wave < TM && 4 * fq < nho;  // lanes holding mu channels 4fq..+3
+  if (ylane) {
+    const T* yr = reinterpret_cast<const T*>(g.res1) + (long long)m_e * g.ld1 + 4 * fq;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) yv[r] = Elem<T>::ld(yr + r);
+  }
+
+  // ---- weight ring prologue: this wave's k-steps [k0, k1) of the fragment-major copy
+  const uint4* const wf = reinterpret_cast<const uint4*>(g.w);
+  uint4 ring[R][TN];
+  int lks = k0;
+#pragma unroll
+  for (int u = 0; u < R; ++u) {
+    if (lks < k1) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) ring[u][j] = wf[((size_t)j * nks + lks) * 64 + lane];
+    }
+    ++lks;
+  }
+
+  // ---- stage the input patch (as conv_fpatch_kernel): flat uint4 f -> (row, chunk)
+  {
+    const int send0 = g.send0, send1 = g.send1, send2 = g.send2;
+    const char* const sp0 = reinterpret_cast<const char*>(g.sp0);
+    const char* const sp1 = reinterpret_cast<const char*>(g.sp1);
+    const char* const sp2 = reinterpret_cast<const char*>(g.sp2);
+    const int sld0 = (int)g.sld0, sld1 = (int)g.sld1, sld2 = (int)g.sld2;
+    const int total = PR * RSc;
+    const int npiece = (total + 63) >> 6;
+    const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lptr_t)patch);
+    for (int pc = wave; pc < npiece; pc += NW) {
+      const int f = (pc << 6) + lane;
+      const int row = f / RSc, c = f - (f / RSc) * RSc;
+      const int py = row / PW, px = row - (row / PW) * PW;
+      const int iy = y0 - 1 + py, ix = x0 - 1 + px;
+      const int ch = c << 3;
+      const bool in0 = ch < send0, in1 = ch < send1;
+      const char* src = in0 ? sp0 : (in1 ? sp1 : sp2);
+      const int sld = in0 ? sld0 : (in1 ? sld1 : sld2);
+      const int cs = ch - (in0 ? 0 : (in1 ? send0 : send1));
+      const bool ok = row < PR && c < nch && ch < send2 && (unsigned)iy < (unsigned)in_h &&
+                      (unsigned)ix < (unsigned)in_w;
+      const unsigned off = ok ? ((unsigned)((b * in_h + iy) * in_w + ix) * (unsigned)sld +
+                                 (unsigned)cs) * 2u : 0u;
+      dma16_l(ok ? (const void*)(src + off) : (const void*)g_zero_page, lbase + (pc << 10));
+    }
+    wait_vm<0>();
+    __syncthreads();
+  }
+  WG_T(1);
+
+  // ---- this wave's share of K: k-step ks = tap * cpt + cc
+  f32x4 acc[TN][TM];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int tap = k0 / cpt, cc = k0 - (k0 / cpt) * cpt;
+  for (int ks0 = k0; ks0 < k1; ks0 += R) {
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      if (ks0 + u < k1) {
+        const int dy = tap / 3, dx = tap - 3 * (tap / 3);
+        uint4 bb[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) bb[i] = patch[((i + dy) * PW + fr + dx) * RSc + cc * 4 + fq];
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int i = 0; i < TM; ++i) mma_step<T>(acc[j][i], ring[u][j], bb[i]);
+        if (++cc == cpt) { cc = 0; ++tap; }
+      }
+      if (lks < k1) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) ring[u][j] = wf[((size_t)j * nks + lks) * 64 + lane];
+      }
+      ++lks;
+    }
+  }
+  WG_T(2);
+
+  // ---- wave partials -> LDS (over the dead patch) -> fixed-order sum per epilogue row
+  f32x4* const red = reinterpret_cast<f32x4*>(patch);
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) red[((wave * TN + j) * TM + i) * 64 + lane] = acc[j][i];
+  __syncthreads();
+  double bits = 0.0;
+  if (wave < TM) {
+    float v[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[j][r] = 0.0f;
+      for (int w = 0; w < NW; ++w) {
+        const f32x4 p = red[((w * TN + j) * TM + ei) * 64 + lane];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[j][r] += p[r];
+      }
+    }
+    if (gauss) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[j][r] += pb[j][r];
+      float sg[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        sg[r] = TN == 1 ? __shfl_xor(v[0][r], 32) : v[TN - 1][r];   // nho 8: lane ^ 32
+      if (ylane) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          bits += (double)gauss_elem_y<T>(g, m_e, 4 * fq + r, nho, v[0][r], sg[r], yv[r]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = 16 * j + 4 * fq;
+        if (n < cout) {
+          EpiIn in;
+          in.template load<T>(g, s.act, (long long)m_e, n);
+          epilogue4_fin<T>(s, g, (long long)m_e, n, v[j], pb[j], in);
+        }
+      }
+    }
+  }
+  if (gauss) {
+    for (int o = 32; o > 0; o >>= 1) bits += __shfl_xor(bits, o);
+    if (wave < TM && lane == 0) wsum[wave] = bits;
+    __syncthreads();
+    if (tid == 0) g.partial[blockIdx.x] = ((wsum[0] + wsum[1]) + wsum[2]) + wsum[3];
+  }
+  WG_T(3);
+}
+
+static void launch_npatch(const ConvArgsDev& d, int max_cout, hipStream_t st) {
+  int cmax = 0;
+  for (int i = 0; i < d.s.ngroups; ++i) cmax = d.g[i].cin_pad > cmax ? d.g[i].cin_pad : cmax;
+  const size_t patch = (size_t)6 * 18 * (((cmax + 31) & ~31) / 8 + 2) * 16;
+  const int tn = max_cout > 16 ? 2 : 1;
+  const size_t red = (size_t)8 * tn * 4 * 64 * 16;
+  const size_t lds = ((patch > red ? patch : red) + 1023) & ~(size_t)1023;
+  const dim3 grid((unsigned)((long long)d.s.batch * (d.s.Hm / 4) * (d.s.Wm / 16)), 1, d.s.ngroups);
+  static bool attr = false;
+  if (!attr) {
+    // (below 160 KiB: the kernel also holds a few static LDS words, and a rejected attribute
+    // call would leave its error for the launch check)
+    (void)hipFuncSetAttribute((const void*)conv_npatch_kernel<1>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+    (void)hipFuncSetAttribute((const void*)conv_npatch_kernel<2>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
+    (void)hipGetLastError();
+    attr = true;
+  }
+  if (tn == 2) hipLaunchKernelGGL(conv_npatch_kernel<2>, grid, dim3(512), lds, st, d);
+  else hipLaunchKernelGGL(conv_npatch_kernel<1>, grid, dim3(512), lds, st, d);
+}
+
+// ---------------------------------------------------------------------------
 // Narrow-output K-split kernel (bf16, plain conv, stride 1, k = 1 or 3, up to three
 // concatenated sources, cout <= 32, K = taps * cin_pad <= 16 * kWsMaxSteps): the slice
 // chain's (mu | sigma) + GaussianConditional convs (256 -> 16, K = 2304) and lrp output
@@ -1683,6 +2111,7 @@ __global__ void __launch_bounds__(64 * NW) conv_wstream_kernel(const ConvArgsDev
   __shared__ int ktab[2 * kWsMaxSteps];
   __shared__ float bl[32];
   __shared__ __attribute__((aligned(16))) float part[NW - 1][16][64];
+  WG_T(0);
   const ConvShared& s = args.s;
   const ConvGroup& g = args.g[blockIdx.z];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1763,6 +2192,7 @@ __global__ void __launch_bounds__(64 * NW) conv_wstream_kernel(const ConvArgsDev
     }
   }
 #undef WS_LOAD
+  WG_T(1);
   // ---- sum the waves' partial tiles (waves 1..NW-1 -> LDS -> wave 0)
   if (wave > 0) {
 #pragma unroll
@@ -1770,6 +2200,7 @@ __global__ void __launch_bounds__(64 * NW) conv_wstream_kernel(const ConvArgsDev
   }
   __syncthreads();
   if (wave > 0) return;
+  WG_T(2);
 #pragma unroll
   for (int w = 0; w < NW - 1; ++w)
 #pragma unroll
@@ -1813,6 +2244,7 @@ __global__ void __launch_bounds__(64 * NW) conv_wstream_kernel(const ConvArgsDev
       }
     }
   }
+  WG_T(3);
 }
 
 // 8 waves split K when every wave still gets >= 8 k-steps (the latency-bound chain convs:
@@ -1868,13 +2300,15 @@ static void launch_pers(const ConvArgsDev& d, int ntile, int nz, hipStream_t st)
 template <int TN, int TM, int ACT>
 __device__ __forceinline__ void patch_epi(const ConvShared& s, const ConvGroup& g, int ph, int b,
                                           int yrow0, int x, const int (&nn)[TN],
-                                          const f32x4 (&acc)[TN][TM]) {
+                                          const f32x4 (&acc)[TN][TM],
+                                          const float (*pbias)[4] = nullptr) {
   using T = bf16_t;
   float bias[TN][4];
 #pragma unroll
   for (int j = 0; j < TN; ++j)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) bias[j][r] = g.bias ? g.bias[nn[j] + r] : 0.0f;
+    for (int r = 0; r < 4; ++r)
+      bias[j][r] = pbias ? pbias[j][r] : (g.bias ? g.bias[nn[j] + r] : 0.0f);
   const bool convt = s.mode == RGBAC_CONVT_S2;
   const int py = convt ? ph >> 1 : 0, px = convt ? ph & 1 : 0, sc = convt ? 2 : 1;
   const int cout = g.cout;
@@ -1930,17 +2364,19 @@ __device__ __forceinline__ void patch_epi(const ConvShared& s, const ConvGroup& 
 
 // Dispatch of a patch kernel's phase epilogue: the lean form where it applies, else the
 // generic per-row epilogue (SUBPEL2 stores, zout, res1 activations, ragged cout).
+// ``pbias``: the lane's biases (bias[nn[j] + r]) loaded up front by the caller, or nullptr.
 template <int TN, int TM>
 __device__ __forceinline__ void patch_epilogue(const ConvShared& s, const ConvGroup& g, int ph,
                                                int b, int yrow0, int x0, int fr,
-                                               const int (&nn)[TN], const f32x4 (&acc)[TN][TM]) {
+                                               const int (&nn)[TN], const f32x4 (&acc)[TN][TM],
+                                               const float (*pbias)[4] = nullptr) {
   const bool lean = s.mode != RGBAC_SUBPEL2 && !g.zout && !g.res1 && (g.cout & 3) == 0;
   if (lean && s.act == RGBAC_ACT_NONE) {
-    patch_epi<TN, TM, RGBAC_ACT_NONE>(s, g, ph, b, yrow0, x0 + fr, nn, acc);
+    patch_epi<TN, TM, RGBAC_ACT_NONE>(s, g, ph, b, yrow0, x0 + fr, nn, acc, pbias);
   } else if (lean && s.act == RGBAC_ACT_GELU) {
-    patch_epi<TN, TM, RGBAC_ACT_GELU>(s, g, ph, b, yrow0, x0 + fr, nn, acc);
+    patch_epi<TN, TM, RGBAC_ACT_GELU>(s, g, ph, b, yrow0, x0 + fr, nn, acc, pbias);
   } else if (lean && s.act == RGBAC_ACT_RELU) {
-    patch_epi<TN, TM, RGBAC_ACT_RELU>(s, g, ph, b, yrow0, x0 + fr, nn, acc);
+    patch_epi<TN, TM, RGBAC_ACT_RELU>(s, g, ph, b, yrow0, x0 + fr, nn, acc, pbias);
   } else {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -2219,6 +2655,7 @@ __global__ void __launch_bounds__(64 * NW * KS) conv_fpatch_kernel(const ConvArg
   static_assert(TN * NW * 16 == BN, "tile");
   static_assert(KS == 1 || (KS == 3 && CPT > 0), "K split by kernel row: unrolled-K only");
   extern __shared__ __attribute__((aligned(16))) uint4 patch[];
+  WG_T(0);
 
   const ConvShared& s = args.s;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -2270,7 +2707,16 @@ __global__ void __launch_bounds__(64 * NW * KS) conv_fpatch_kernel(const ConvArg
   constexpr int RC = RC1 < NKSP ? RC1 : NKSP;
   const uint4* wj[TN];
   uint4 cring[RC][TN];
+  // the unrolled-K variants' epilogue biases, requested first (a cold bias read in the
+  // epilogue cost a memory round trip at the end of the dependency chain)
+  float pbias[TN][4];
   if constexpr (CPT > 0) {
+    const int nb0 = n0 + wave * TN * 16 + (lane >> 4) * 4;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        pbias[j][r] = (g.bias && nb0 + j * 16 + r < g.cout) ? g.bias[nb0 + j * 16 + r] : 0.0f;
 #pragma unroll
     for (int j = 0; j < TN; ++j)
       wj[j] = wf + ((size_t)(ntile0 + j) * NKSC + kp * NKSP) * 64 + lane;
@@ -2309,6 +2755,7 @@ __global__ void __launch_bounds__(64 * NW * KS) conv_fpatch_kernel(const ConvArg
     wait_vm<0>();
     __syncthreads();
   }
+  WG_T(1);
 
   if constexpr (CPT > 0) {
     constexpr int RS = 4 * CPT + 2;               // patch row stride (uint4) == RSc
@@ -2338,6 +2785,7 @@ __global__ void __launch_bounds__(64 * NW * KS) conv_fpatch_kernel(const ConvArg
         for (int j = 0; j < TN; ++j) cring[ks % RC][j] = wj[j][(ks + RC) * 64];
       }
     }
+    WG_T(2);
     if constexpr (KS > 1) {
       f32x4* const red = reinterpret_cast<f32x4*>(patch);
       __syncthreads();                            // every wave is done with the patch
@@ -2364,7 +2812,8 @@ __global__ void __launch_bounds__(64 * NW * KS) conv_fpatch_kernel(const ConvArg
     int nn[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) nn[j] = n0 + wave * TN * 16 + j * 16 + fq * 4;
-    patch_epilogue<TN, TM>(s, g, 0, b, y0, x0, fr, nn, acc);
+    patch_epilogue<TN, TM>(s, g, 0, b, y0, x0, fr, nn, acc, pbias);
+    WG_T(3);
     return;
   }
 
@@ -2502,7 +2951,27 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
     }
     return check_launch("conv_wres_kernel");
   }
-  if ((tile >= kFirstFPatch && tile < kFirstPatch2) || tile >= kTileFPatch464) {
+  if (tile == kTileNPatch) {
+    if constexpr (sizeof(T) == 2) {
+      launch_npatch(d, max_cout, st);
+      return check_launch("conv_npatch_kernel");
+    } else {
+      set_error("the narrow patch tile is bf16 only");
+      return RGBAC_E_ARG;
+    }
+  }
+  if (tile == kTilePW) {
+    if constexpr (sizeof(T) == 2) {
+      int cmax = 0;
+      for (int i = 0; i < s.ngroups; ++i) cmax = d.g[i].cin_pad > cmax ? d.g[i].cin_pad : cmax;
+      launch_pw(d, cmax, st);
+      return check_launch("conv_pw_kernel");
+    } else {
+      set_error("the full-width pointwise tile is bf16 only");
+      return RGBAC_E_ARG;
+    }
+  }
+  if (fpatch_tile(tile)) {
     if constexpr (sizeof(T) == 2) {
       const int th = tc.bm / 16;
       const int nbn = (max_cout + tc.bn - 1) / tc.bn;
@@ -2511,7 +2980,7 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
       for (int i = 0; i < s.ngroups; ++i) cmax = d.g[i].cin_pad > cmax ? d.g[i].cin_pad : cmax;
       size_t lds = ((size_t)(th + 2) * 18 * (((cmax + 31) & ~31) / 8 + 2) * 16 + 1023) &
                    ~(size_t)1023;                         // whole 1-KiB DMA pieces
-      const bool ks3 = tile >= kFirstFPatchKS;
+      const bool ks3 = fpatch_ks_tile(tile);
       if (ks3) {                                          // row partials over the patch
         const size_t red = (size_t)2 * (tc.bn / 16) * th * 64 * 16;
         if (red > lds) lds = red;
@@ -2546,22 +3015,22 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
     }                                                                                         \
     hipLaunchKernelGGL(k_, grid, dim3(256), lds, st, d);                                      \
   } while (0)
-#define RGBAC_FPK(BN_, C_)                                                                    \
+#define RGBAC_FPK(TH_, BN_, NW_, C_)                                                          \
   do {                                                                                        \
-    auto k_ = conv_fpatch_kernel<4, BN_, 4, 4, C_, 3>;                                        \
+    auto k_ = conv_fpatch_kernel<TH_, BN_, NW_, 4, C_, 3>;                                    \
     static bool attr_ = false;                                                                \
     if (!attr_) {                                                                             \
       (void)hipFuncSetAttribute((const void*)k_, hipFuncAttributeMaxDynamicSharedMemorySize,  \
                                 160 * 1024);                                                  \
       attr_ = true;                                                                           \
     }                                                                                         \
-    hipLaunchKernelGGL(k_, grid, dim3(768), lds, st, d);                                      \
+    hipLaunchKernelGGL(k_, grid, dim3(64 * NW_ * 3), lds, st, d);                             \
   } while (0)
-#define RGBAC_FPKS(BN_)                                                                       \
+#define RGBAC_FPKS(TH_, BN_, NW_)                                                             \
   do {                                                                                        \
-    if (cpt == 3) RGBAC_FPK(BN_, 3);                                                          \
-    else if (cpt == 4) RGBAC_FPK(BN_, 4);                                                     \
-    else RGBAC_FPK(BN_, 7);                                                                   \
+    if (cpt == 3) RGBAC_FPK(TH_, BN_, NW_, 3);                                                \
+    else if (cpt == 4) RGBAC_FPK(TH_, BN_, NW_, 4);                                           \
+    else RGBAC_FPK(TH_, BN_, NW_, 7);                                                         \
   } while (0)
 #define RGBAC_FP(TH_, BN_)                                                                    \
   do {                                                                                        \
@@ -2578,9 +3047,12 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
         case 45: RGBAC_FP(4, 128); break;
         case 46: RGBAC_FP(8, 256); break;
         case kTileFPatch464: RGBAC_FP(4, 64); break;
-        case kFirstFPatchKS: RGBAC_FPKS(64); break;
-        case kFirstFPatchKS + 1: RGBAC_FPKS(128); break;
-        case kFirstFPatchKS + 2: RGBAC_FPKS(192); break;
+        case kFirstFPatchKS: RGBAC_FPKS(4, 64, 4); break;
+        case kFirstFPatchKS + 1: RGBAC_FPKS(4, 128, 4); break;
+        case kFirstFPatchKS + 2: RGBAC_FPKS(4, 192, 4); break;
+        case kFirstFPatchKS2: RGBAC_FPKS(8, 64, 4); break;
+        case kFirstFPatchKS2 + 1: RGBAC_FPKS(8, 128, 4); break;
+        case kFirstFPatchKS2 + 2: RGBAC_FPKS(16, 32, 2); break;
         default: RGBAC_FP(8, 64); break;
       }
 #undef RGBAC_FP
@@ -2750,12 +3222,24 @@ static int fill_group(const rgbac_conv_args* a, int ntaps_max, ConvGroup& g) {
 
 using namespace rgbac;
 
+#ifdef RGBAC_WG_TIMING
+extern "C" int rgbac_debug_wg_times(unsigned long long* host, int nblocks) {
+  if (nblocks > 16384) nblocks = 16384;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wg_t), (size_t)nblocks * 4 * 8) == hipSuccess ? 0 : 1;
+}
+extern "C" int rgbac_debug_wg_reset(void) {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_wg_t)) != hipSuccess) return 1;
+  return hipMemset(p, 0, sizeof(g_wg_t)) == hipSuccess ? 0 : 1;
+}
+#endif
+
 extern "C" int rgbac_conv_num_tiles(void) { return kNumTiles; }
 // 1 for the fragment-streamed patch tiles (42..47, 50..53), whose `weight` must be the
 // fragment-major copy documented in rgbac.h; 0 for the plain packed layout; -1 out of range.
 extern "C" int rgbac_conv_tile_weight_layout(int tile) {
   if (tile < 0 || tile >= kNumTiles) return -1;
-  return ((tile >= 42 && tile <= 47) || tile >= 50) ? 1 : 0;
+  return (fpatch_tile(tile) || tile == kTileNPatch) ? 1 : 0;
 }
 extern "C" int rgbac_conv_max_groups(void) { return kMaxGroups; }
 
@@ -2835,7 +3319,32 @@ extern "C" int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroup
     return (e && e[0] == '0') ? 0 : 1;
   }();
   s.remap = remap_env;
-  if (a->tile == kTileSpatial) {
+  if (a->tile == kTileNPatch) {
+    RGBAC_REQUIRE(a->dtype == RGBAC_BF16 && a->mode == RGBAC_CONV && a->ksplit == 1 &&
+                      a->ksize == 3 && a->stride == 1 && s.Wm % 16 == 0 &&
+                      s.Hm % 4 == 0,
+                  "the narrow patch tile needs bf16, a 3x3 stride-1 conv, ksplit 1, the "
+                  "output grid a multiple of 16 wide and 4 high");
+    RGBAC_REQUIRE((long long)a->batch * a->in_h * a->in_w < (1ll << 24),
+                  "the narrow patch tile addresses sources of < 2^24 pixels");
+    for (int i = 0; i < ngroups; ++i) {
+      RGBAC_REQUIRE(args[i].cout <= 32 && args[i].cout_pad % 16 == 0 &&
+                        args[i].cout_pad >= (args[i].cout > 16 ? 32 : 16) &&
+                        (size_t)6 * 18 * (((args[i].cin_pad + 31) & ~31) / 8 + 2) * 16 <=
+                            128 * 1024,
+                    "the narrow patch tile needs cout <= 32 and the input patch within 128 KiB");
+      RGBAC_REQUIRE(a->act != RGBAC_ACT_GAUSS || args[i].cout == 16 || args[i].cout == 32,
+                    "GAUSS on the narrow patch tile needs (mu|sigma) halves of 8 or 16 channels");
+    }
+  } else if (a->tile == kTilePW) {
+    RGBAC_REQUIRE(a->dtype == RGBAC_BF16 && a->mode == RGBAC_CONV && a->ksplit == 1 &&
+                      a->ksize == 1 && a->stride == 1 && a->act != RGBAC_ACT_GAUSS,
+                  "the full-width pointwise tile needs bf16, a 1x1 stride-1 conv, ksplit 1 and "
+                  "no GAUSS epilogue");
+    for (int i = 0; i < ngroups; ++i)
+      RGBAC_REQUIRE(args[i].nsrc == 1 && args[i].cin_pad <= 192 && args[i].cout <= 192,
+                    "the full-width pointwise tile needs one source, cin_pad <= 192, cout <= 192");
+  } else if (a->tile == kTileSpatial) {
     RGBAC_REQUIRE(a->dtype == RGBAC_BF16 && a->mode == RGBAC_CONV && a->ksize == 3 &&
                       a->stride == 1 && a->ksplit == 1 && a->act != RGBAC_ACT_GAUSS &&
                       s.Hm % 16 == 0 && s.Wm % 16 == 0,
@@ -2860,8 +3369,7 @@ extern "C" int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroup
       RGBAC_REQUIRE(args[i].cout_pad >= ((args[i].cout + kTiles[a->tile].bn - 1) /
                                          kTiles[a->tile].bn) * kTiles[a->tile].bn &&
                         args[i].k_pad >= ntaps_max * args[i].cin_pad &&
-                        ((a->tile < kFirstFPatch || a->tile >= kFirstPatch2) &&
-                             a->tile < kTileFPatch464 ||
+                        (!fpatch_tile(a->tile) ||
                          args[i].cout_pad % 16 == 0),
                     "patch tiles read whole BN-row weight tiles");
   } else if (a->tile == kTileWStream) {
@@ -2908,7 +3416,7 @@ extern "C" int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroup
     }
     if (a->act == RGBAC_ACT_GAUSS) {
       RGBAC_REQUIRE(a->mode == RGBAC_CONV && a->ksplit == 1, "GAUSS needs a plain conv, ksplit 1");
-      RGBAC_REQUIRE(a->tile < kFirstPers || a->tile == kTileWStream,
+      RGBAC_REQUIRE(a->tile < kFirstPers || a->tile == kTileWStream || a->tile == kTileNPatch,
                     "GAUSS needs a non-persistent tile");
       RGBAC_REQUIRE(b->cout % 2 == 0 && b->cout <= kTiles[a->tile].bn,
                     "GAUSS needs (mu|sigma) channels in one N tile");

@@ -121,7 +121,10 @@ TILES = [(128, 128), (128, 64), (64, 64), (128, 32), (64, 32), (128, 16), (64, 1
          (128, 192), (64, 192), (128, 128), (64, 128), (128, 256), (128, 64),
          (128, 64), (128, 128),
          (64, 64),
-         (64, 64), (64, 128), (64, 192)]
+         (64, 64), (64, 128), (64, 192),
+         (32, 192),
+         (64, 32),
+         (128, 64), (128, 128), (256, 32)]
 FIRST_WRES = 7
 WRES_STAGES = 6
 FIRST_DIRECT = 13        # 13..18: direct kernel (plain conv, K <= DIRECT_STEPS MFMA k-steps)
@@ -142,10 +145,15 @@ PATCH_SIG = {36: (8, 192, 2, 4, 3), 37: (8, 128, 2, 4, 3), 38: (8, 96, 4, 2, 3),
              48: (8, 64, 4, 2, 4), 49: (8, 128, 2, 4, 4)}
 FIRST_FPATCH = 42        # 42..47: conv_fpatch_kernel (fragment-major weight copy, 4 waves)
 FPATCH_SIG = {42: (8, 192), 43: (4, 192), 44: (8, 128), 45: (4, 128), 46: (8, 256), 47: (8, 64),
-              50: (4, 64), 51: (4, 64), 52: (4, 128), 53: (4, 192)}
+              50: (4, 64), 51: (4, 64), 52: (4, 128), 53: (4, 192),
+              56: (8, 64), 57: (8, 128), 58: (16, 32)}
 # 51..53: the unrolled-K variants with K split by kernel row (KS = 3, 12 waves): only where
 # the unrolled-K variant applies (fpatch_cpt != 0)
-FPATCH_KS = (51, 52, 53)
+FPATCH_KS = {51: 4, 52: 4, 53: 4, 56: 4, 57: 4, 58: 2}    # tile -> N waves (x 3 K parts)
+TILE_PW = 54             # conv_pw_kernel: bf16 1x1 stride-1 conv, one source, cin/cout <= 192
+TILE_NPATCH = 55         # conv_npatch_kernel: bf16 3x3 stride-1 conv, cout <= 32 (chain tails)
+# tiles that read the fragment-major weight copy (frag_weights): forward PackedConv only
+FRAG_TILES = frozenset(FPATCH_SIG) | {TILE_NPATCH}
 # the fragment-patch kernel's unrolled-K variants (csrc/conv.hip, CPT template argument)
 FPATCH_CPT = os.environ.get("RGBAC_FPATCH_CPT", "1") != "0"
 
@@ -211,6 +219,8 @@ def _patch_tiles(preps):
         cpt = fpatch_cpt(preps)
         for t, (th, bn) in FPATCH_SIG.items():
             if hm % th or (th + 2) * 18 * (c32 // 8 + 2) * 16 > 160 * 1024:
+                continue
+            if t in FPATCH_KS and 2 * (bn // 16) * th * 1024 > 160 * 1024:
                 continue
             if t in FPATCH_KS and not cpt:
                 continue
@@ -574,7 +584,8 @@ def kernel_name(tile, preps):
     if tile == TILE_SPATIAL:
         return f"conv3x3_c32_kernel<{dt}>"
     if tile in FPATCH_KS:
-        return "conv_fpatch_kernel<4, %d, 4, 4, %d, 3>" % (FPATCH_SIG[tile][1], fpatch_cpt(preps))
+        return "conv_fpatch_kernel<%d, %d, %d, 4, %d, 3>" % (FPATCH_SIG[tile] + (FPATCH_KS[tile],
+                                                                           fpatch_cpt(preps)))
     if tile in FPATCH_SIG:
         c = fpatch_cpt(preps) if FPATCH_SIG[tile][0] == 4 else 0
         return "conv_fpatch_kernel<%d, %d, 4, 4%s>" % (FPATCH_SIG[tile] + (f", {c}" if c else "",))
@@ -586,6 +597,11 @@ def kernel_name(tile, preps):
         env = os.environ.get("RGBAC_WSTREAM_WAVES", "")
         nw = int(env) if env in ("4", "8") else (8 if nks >= 64 else 4)
         return f"conv_wstream_kernel<8, {nw}>"
+    if tile == TILE_NPATCH:
+        return f"conv_npatch_kernel<{2 if max(p.pk.cout for p in preps) > 16 else 1}>"
+    if tile == TILE_PW:
+        cin = max(p.a.cin_pad for p in preps)
+        return f"conv_pw_kernel<{4 if cin <= 64 else (8 if cin <= 128 else 12)}>"
     if tile == TILE_SMALLK:
         cout = max(p.pk.cout for p in preps)
         nt = 1 if cout <= 32 else (2 if cout <= 64 else 3)
@@ -600,6 +616,28 @@ def kernel_name(tile, preps):
         return f"conv_pers_kernel<{dt}, {_TILE_SIG[tile - FIRST_PERS]}>"
     # tiles 0..6 instantiate conv_kernel's KSM = 1 default (rocprofv3 prints it)
     return f"conv_kernel<{dt}, {_TILE_SIG[tile]}{', 1' if tile < FIRST_WRES else ''}>"
+
+
+def _npatch_ok(preps):
+    a = preps[0].a
+    if not (a.dtype == _lib.BF16 and a.mode == CONV and a.ksize == 3 and a.stride == 1 and
+            a.in_w % 16 == 0 and a.in_h % 4 == 0 and a.batch * a.in_h * a.in_w < (1 << 24)):
+        return False
+    if not all(isinstance(p.pk, PackedConv) for p in preps):
+        return False
+    for p in preps:
+        if p.pk.cout > 32 or 6 * 18 * (round_up(p.pk.cin_pad, 32) // 8 + 2) * 16 > 128 * 1024:
+            return False
+        if a.act == ACT["gauss"] and p.pk.cout not in (16, 32):
+            return False
+    return True
+
+
+def _pw_ok(preps):
+    a = preps[0].a
+    return (a.dtype == _lib.BF16 and a.mode == CONV and a.act != ACT["gauss"] and
+            a.ksize == 1 and a.stride == 1 and
+            all(p.a.nsrc == 1 and p.a.cin_pad <= 192 and p.pk.cout <= 192 for p in preps))
 
 
 def _smallk_ok(preps):
@@ -672,7 +710,7 @@ def launch(preps, force=None):
             arr[i].tile_counters = cnt
             arr[i].workspace = None
             # the fragment-streamed tiles read the fragment-major weight copy
-            arr[i].weight = (frag_weights(pr.pk).data_ptr() if t in FPATCH_SIG
+            arr[i].weight = (frag_weights(pr.pk).data_ptr() if t in FRAG_TILES
                              else pr.pk.w.data_ptr())
             if ks > 1:
                 ws = torch.empty(ks * pr.nphase * pr.mgrid * round_up(pr.pk.cout, 16),
@@ -695,11 +733,17 @@ def launch(preps, force=None):
             cands = [(t, 1) for t in GAUSS_TILES if _gauss_ok(t, cout)]
             if _wstream_ok(preps):
                 cands.append((TILE_WSTREAM, 1))
+            if _npatch_ok(preps):
+                cands.append((TILE_NPATCH, 1))
         else:
             cands = _candidates(mtot, cout, nst, max(pr.nks for pr in preps),
                                 p0.pk.mode == CONV, _spatial_ok(preps), _smallk_ok(preps),
                                 _wstream_ok(preps))
             cands += [(t, 1) for t in _patch_tiles(preps)]
+            if _pw_ok(preps):
+                cands.append((TILE_PW, 1))
+            if _npatch_ok(preps):
+                cands.append((TILE_NPATCH, 1))
         if TUNE and not fixed and not torch.cuda.is_current_stream_capturing():
             # each timed run starts with the L2s flushed (a 64 MB write evicts all 8 XCDs'
             # 4 MB): in the forward graph every layer's weights and inputs arrive cold, and a
@@ -728,13 +772,14 @@ def launch(preps, force=None):
             choice = _heuristic(mtot, cout, nst)
         if not fixed:
             _tune_cache[key] = choice
-    if choice[0] in FPATCH_SIG and not all(isinstance(pr.pk, PackedConv) for pr in preps):
+    if choice[0] in FRAG_TILES and not all(isinstance(pr.pk, PackedConv) for pr in preps):
         # a cached / forced fragment-streamed tile (tuned on a forward PackedConv of the same
         # shape) handed to a training pack: TPack weights are re-gathered in the plain layout
         # every step, so a cached fragment-major copy would go stale -- take the shape rule
         choice = _heuristic(p0.mgrid * p0.nphase * n, max(pr.pk.cout for pr in preps),
                             max(pr.nst for pr in preps))
-    if gauss and not (choice[0] == TILE_WSTREAM and _wstream_ok(preps)) and (
+    if gauss and not (choice[0] == TILE_WSTREAM and _wstream_ok(preps)) and \
+            not (choice[0] == TILE_NPATCH and _npatch_ok(preps)) and (
             choice[0] not in GAUSS_TILES or
             not _gauss_ok(choice[0], max(pr.pk.cout for pr in preps))):
         choice = (min((t for t in GAUSS_TILES if _gauss_ok(t, p0.pk.cout)),

@@ -100,7 +100,8 @@ typedef struct rgbac_conv_args {
                                   0:128x128 1:128x64 2:64x64 3:128x32 4:64x32
                                   5:128x16 6:64x16 (pixels x channels).
                                   Tiles with rgbac_conv_tile_weight_layout(tile) == 1
-                                  (42..47, 50..53: fragment-streamed patch tiles) read
+                                  (42..47, 50..53, 56..58: fragment-streamed patch
+                                  tiles; 55: narrow-output patch tile) read
                                   `weight` as the FRAGMENT-MAJOR copy of the pack:
                                   bf16 [nphase][cout_pad/16][ntaps*cin32/32][64][8],
                                   cin32 = round_up(cin_pad, 32), K tap-major with each

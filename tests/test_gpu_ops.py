@@ -415,6 +415,62 @@ def test_conv_smallk_tile(device, cin, cout, k, s, act):
         rt.FORCE = None
 
 
+@pytest.mark.parametrize("cin,cout,kind", [(192, 192, "gelu"), (3, 32, "none"), (32, 3, "none"),
+                                           (80, 40, "gelu"), (96, 80, "none"), (192, 100, "relu"),
+                                           (192, 192, "gdn"), (192, 192, "igdn"), (80, 80, "igdn"),
+                                           (192, 192, "gate"), (192, 192, "masksel")])
+def test_conv_pw_tile(device, cin, cout, kind):
+    """The full-width pointwise tile (54, bf16): every output channel of a 32-pixel tile in one
+    wave, epilogue operands prefetched.  Same MFMA sequence as the small-K tile, so the two
+    agree bit for bit on the model's 1x1 epilogues (GDN / IGDN on the squared input, the
+    attention block's gate a * sigmoid(b) + x, MASKSEL), and the plain convs match fp32 torch."""
+    rt = _rt()
+    from rgbac.layers.TransformRGB import run_conv
+    g = _gen(900 + cin + cout)
+    B, H, W = 3, 46, 70                        # ragged: 9660 pixels, a partial last tile
+    x = torch.randn((B, cin, H, W), generator=g)
+    a = torch.randn((B, cout, H, W), generator=g)
+    r = torch.randn((B, cout, H, W), generator=g)
+    dt = torch.bfloat16
+    m = nn.Conv2d(cin, cout, 1)
+    with torch.no_grad():
+        if kind in ("gdn", "igdn"):
+            m.weight.copy_(0.1 * torch.rand(cout, cin, 1, 1, generator=g))
+            m.bias.copy_(0.5 + torch.rand(cout, generator=g))
+    md = m.to(device)
+    fx = rt.to_nhwc(x.to(device), dt)
+    fa = rt.to_nhwc(a.to(device), dt)
+    fr = rt.to_nhwc(r.to(device), dt)
+    sel = (torch.rand((B * H * W,), generator=g) > 0.5).to(torch.uint8).to(device)
+    outs = {}
+    for tile in (rt.TILE_SMALLK, rt.TILE_PW):
+        rt.FORCE = (tile, 1)
+        try:
+            with torch.no_grad():
+                if kind in ("gdn", "igdn"):
+                    pk = rt.packed(md, dt, [(cin, rt.round_up(cin, 8))])
+                    o = rt.conv(pk, [fx.src()], square=True, act=kind, res1=fx)
+                elif kind == "gate":
+                    pk = rt.packed(md, dt, [(cin, rt.round_up(cin, 8))])
+                    o = rt.conv(pk, [fx.src()], act="gate", res1=fa, res2=fr)
+                elif kind == "masksel":
+                    pk = rt.packed(md, dt, [(cin, rt.round_up(cin, 8))])
+                    o = rt.conv(pk, [fx.src()], act="masksel", res1=fa, sel=sel)
+                else:
+                    o = run_conv(md, [fx.src()], act=kind, res0=fr)
+            outs[tile] = rt.to_nchw(o).float().cpu()
+        finally:
+            rt.FORCE = None
+    assert torch.equal(outs[rt.TILE_PW], outs[rt.TILE_SMALLK]), kind
+    if kind in ("gelu", "none", "relu"):
+        f = {"gelu": F.gelu, "relu": F.relu, "none": lambda t: t}[kind]
+        xb = x.to(dt).float()
+        with torch.no_grad():
+            want = f(F.conv2d(xb, m.weight.to(dt).float().cpu(), m.bias.float().cpu()) +
+                     r.to(dt).float())
+        assert rel(outs[rt.TILE_PW], want) < 2e-2
+
+
 @pytest.mark.parametrize("H,W", [(64, 96), (256, 256), (40, 72)])
 def test_stem_gdn_fused(device, H, W):
     """Fused x1 (conv5x5/s2 3->192) + gdn1 (bf16) against the unfused bf16 kernels and the
@@ -466,17 +522,23 @@ def test_conv_inlaunch_splitk(device, tile):
         rt.FORCE, rt.INLAUNCH_SPLITK = None, False
 
 
+@pytest.mark.parametrize("tile", ["wstream", "npatch"])
 @pytest.mark.parametrize("cin,cout,k,act,nsrc", [(128, 8, 3, "tanh_half", 3), (256, 16, 3, "none", 2),
-                                                 (64, 24, 3, "gelu", 1), (96, 32, 1, "relu", 1)])
-def test_conv_wstream_tile(device, cin, cout, k, act, nsrc):
-    """The narrow-output wave-streaming tile (bf16): 3x3 / 1x1 convs with concatenated sources
-    and residual / tanh-update epilogues against PyTorch."""
+                                                 (64, 24, 3, "gelu", 1), (96, 32, 1, "relu", 1),
+                                                 (216, 8, 3, "tanh_half", 3)])
+def test_conv_wstream_tile(device, cin, cout, k, act, nsrc, tile):
+    """The narrow-output tiles (bf16): the wave-streaming tile (35) and the narrow patch tile
+    (55, 3x3 only): convs with concatenated sources and residual / tanh-update epilogues
+    against PyTorch."""
     rt = _rt()
     from rgbac.layers.TransformRGB import run_conv
+    if tile == "npatch" and k != 3:
+        pytest.skip("the narrow patch tile is 3x3 only")
     g = _gen(600 + cin + cout)
     m = nn.Conv2d(cin, cout, k, padding=k // 2)
     parts = [cin // nsrc] * (nsrc - 1) + [cin - (cin // nsrc) * (nsrc - 1)]
-    xs = [torch.randn((2, c, 20, 36), generator=g) for c in parts]
+    W = 36 if tile == "wstream" else 48                 # the patch tile: 16-pixel-wide tiles
+    xs = [torch.randn((2, c, 20, W), generator=g) for c in parts]
     y = m(torch.cat(xs, 1))
     r = torch.randn(y.shape, generator=g)
     if act == "tanh_half":
@@ -486,7 +548,7 @@ def test_conv_wstream_tile(device, cin, cout, k, act, nsrc):
         f = {"gelu": F.gelu, "relu": F.relu, "none": lambda t: t}[act]
         want = f(y + r)
         kw = dict(act=act)
-    rt.FORCE = (rt.TILE_WSTREAM, 1)
+    rt.FORCE = (rt.TILE_WSTREAM if tile == "wstream" else rt.TILE_NPATCH, 1)
     try:
         with torch.no_grad():
             fs = [rt.to_nhwc(t.to(device), torch.bfloat16) for t in xs]
@@ -501,12 +563,15 @@ def test_conv_wstream_tile(device, cin, cout, k, act, nsrc):
         rt.FORCE = None
 
 
-def test_gauss_wstream_matches_ring_tile(device):
-    """GaussianConditional epilogue on the narrow wave-streaming tile == on the LDS-ring tile
-    (same bf16 inputs): y_hat, likelihoods and the bits sum."""
+@pytest.mark.parametrize("tile,cs", [("wstream", 8), ("npatch", 8), ("npatch", 16)])
+def test_gauss_wstream_matches_ring_tile(device, tile, cs):
+    """GaussianConditional epilogue on the narrow wave-streaming tile (35) and the narrow patch
+    tile (55; (mu | sigma) of 8 channels across lanes ^ 32, of 16 in two N tiles) == on the
+    LDS-ring tile (same bf16 inputs): y_hat, likelihoods and the bits sum."""
     rt = _rt()
-    g = _gen(77)
-    B, H, W, cs = 2, 16, 20, 8
+    g = _gen(77 + cs)
+    B, H, W = 2, 16, (20 if tile == "wstream" else 32)
+    ntile = rt.TILE_WSTREAM if tile == "wstream" else rt.TILE_NPATCH
     dt = torch.bfloat16
     mconv = nn.Conv2d(128, cs, 3, padding=1)
     sconv = nn.Conv2d(128, cs, 3, padding=1)
@@ -519,7 +584,8 @@ def test_gauss_wstream_matches_ring_tile(device):
     fy = rt.to_nhwc(y.to(device), dt)
     pk = _musigma_pack(mconv, sconv, dt, fm.ldc)
     res = {}
-    for tile in (6, rt.TILE_WSTREAM):
+    ring = 6 if 2 * cs <= 16 else 4                       # an LDS-ring tile whose N holds (mu|sigma)
+    for tl in (ring, ntile):
         out = rt.new_feat(B, H, W, cs, dt, device)
         lik = torch.empty((B, H, W, cs), dtype=torch.float32, device=device)
         part = torch.zeros(-(-B * H * W // 32), dtype=torch.float64, device=device)
@@ -527,11 +593,14 @@ def test_gauss_wstream_matches_ring_tile(device):
                         aux1=lik, partial=part)
         arr = (rt._lib.ConvArgs * 1)()
         arr[0] = pr.a
-        arr[0].tile, arr[0].ksplit = tile, 1
+        arr[0].tile, arr[0].ksplit = tl, 1
+        if tl in rt.FRAG_TILES:
+            arr[0].weight = rt.frag_weights(pk).data_ptr()
         rt._lib.call("rgbac_conv2d_grouped", ctypes.addressof(arr), 1, rt._lib.stream_ptr(device))
         torch.cuda.synchronize()
-        res[tile] = (rt.to_nchw(out), lik.clone(), part.sum().item())
-    a, b = res[6], res[rt.TILE_WSTREAM]
+        res[tl] = (rt.to_nchw(out), lik.clone(), part.sum().item())
+    a, b = res[ring], res[ntile]
+    assert torch.isfinite(b[1]).all() and (b[1] > 0).all()
     assert (a[0] - b[0]).abs().max().item() <= 1.0 + 1e-6     # a rare .5-boundary symbol flip
     assert (a[0] != b[0]).float().mean().item() < 0.01
     assert abs(a[2] - b[2]) / abs(a[2]) < 1e-2
