@@ -1712,27 +1712,28 @@ static void launch_smallk(const ConvArgsDev& d, int nks16, int max_cout, hipStre
 }
 
 // ---------------------------------------------------------------------------
-// Full-width pointwise kernel (bf16; 1x1 stride-1 conv, one source, cin_pad <= 16 * NKS,
+// Full-width pointwise kernel (bf16; 1x1 stride-1 conv, one source, cin_pad <= 32 * NKS,
 // cout <= 192): the HBM-bound 1x1 convs at full resolution -- GDN / IGDN norm pools, the
 // attention block's output gate, ... .  conv_smallk_kernel holds 96 output rows per
 // workgroup (two column blocks re-read the input: 1.5x the algorithmic bytes on the 128^2
-// IGDN), stages its weight panel through registers behind a barrier and pays one memory
-// round trip per 32-channel column of the epilogue.  Here:
-//   * one workgroup holds all 192 rows of the weight panel in LDS (LDS-DMA, 16-byte chunk c
-//     of row r at slot c ^ (r & 7): conflict-free ds_read_b128 for the 8-lane groups), so
-//     every input pixel is read from HBM once;
-//   * each wave streams 32-pixel tiles: per 16-deep k-step ONE 16-byte load per lane
-//     straight into VGPRs feeds 6 v_mfma_f32_32x32x16_bf16, and is reloaded with the NEXT
-//     tile's fragment right behind its MFMAs (a register ring: the next tile's input is in
-//     flight during this tile's MFMAs and epilogue);
-//   * the epilogue operands (res0 / res1 / res2, raw bf16) of ALL 24 channel quads of the
-//     tile are requested before the MFMAs: one memory latency per tile, not per column.
-// Persistent grid (one workgroup per CU, 4 waves); no barrier after the weight panel.
+// IGDN) and pays one memory round trip per 32-channel column of the epilogue.  Here:
+//   * a 512-thread workgroup holds all 192 rows of the weight panel in LDS (LDS-DMA, 16-byte
+//     chunk c of row r at slot c ^ (r & 7): conflict-free ds_read_b128 for the 8-lane
+//     groups), so every input pixel is read from HBM once; two workgroups per CU (16 waves,
+//     <= 128 VGPRs) keep enough loads in flight for HBM;
+//   * each wave streams 16-pixel tiles: per 32-deep k-step ONE 16-byte load per lane
+//     straight into VGPRs feeds 12 v_mfma_f32_16x16x32_bf16 (all 192 output channels), and
+//     is reloaded with the NEXT tile's fragment right behind its MFMAs (a register ring);
+//   * the tile's res1 operand (GDN / IGDN x, the gate's a, MASKSEL's x: 12 raw quads per
+//     lane) is requested as one batch before the epilogue math: one memory latency per
+//     tile, not per column (<= 128 VGPRs: four waves per SIMD hide it).
+// Persistent grid; no barrier after the weight panel.
 template <int NKS>
-__global__ void __launch_bounds__(256, 1) conv_pw_kernel(const ConvArgsDev args) {
-  constexpr int NT = 6, BN = 192, NCH = 2 * NKS;   // 16-byte chunks per weight row
+__global__ void __launch_bounds__(512, 4) conv_pw_kernel(const ConvArgsDev args) {
+  constexpr int NT = 12, BN = 192, NCH = 4 * NKS;  // 16-byte chunks per weight row
   static_assert(NCH % 8 == 0, "swizzle groups of 8 chunks");
   constexpr int NPIECE = BN * NCH / 64;            // 1-KiB LDS-DMA pieces of the panel
+  constexpr int NW = 8;
   extern __shared__ __attribute__((aligned(16))) uint4 Wl[];
   __shared__ float bl[BN];
   const ConvShared& s = args.s;
@@ -1744,7 +1745,7 @@ __global__ void __launch_bounds__(256, 1) conv_pw_kernel(const ConvArgsDev args)
     // weight panel: LDS slot d = 64 p + lane -> (row, slot), source chunk slot ^ (row & 7)
     const bf16_t* wbase = reinterpret_cast<const bf16_t*>(g.w);
     const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lptr_t)Wl);
-    for (int p = wave; p < NPIECE; p += 4) {
+    for (int p = wave; p < NPIECE; p += NW) {
       const int d = p * 64 + lane;
       const int row = d / NCH, slot = d - (d / NCH) * NCH;
       const int ch = slot ^ (row & 7);
@@ -1753,98 +1754,86 @@ __global__ void __launch_bounds__(256, 1) conv_pw_kernel(const ConvArgsDev args)
               lbase + p * 1024);
     }
   }
-  for (int e = tid; e < BN; e += 256) bl[e] = (g.bias && e < g.cout) ? g.bias[e] : 0.0f;
+  for (int e = tid; e < BN; e += 64 * NW) bl[e] = (g.bias && e < g.cout) ? g.bias[e] : 0.0f;
   wait_vm<0>();
   __syncthreads();
 
   const int Mtot = s.M, act = s.act;
   const int ld = (int)g.sld0;
   const bool sq_in = s.square != 0;
-  const int r32 = lane & 31, h = lane >> 5;
-  const char* const src = reinterpret_cast<const char*>(g.sp0) + 16 * h;
-  const int ntile = (Mtot + 31) / 32;
-  const int tstride = gridDim.x * 4;
-  int tile = blockIdx.x * 4 + wave;
+  const int fr = lane & 15, fq = lane >> 4;
+  const char* const src = reinterpret_cast<const char*>(g.sp0) + 16 * fq;
+  const int ntile = (Mtot + 15) / 16;
+  const int tstride = gridDim.x * NW;
+  int tile = blockIdx.x * NW + wave;
   if (tile >= ntile) return;
 
 #define PWW_LOAD(dst, st, rowp_, valid_)                                                      \
   do {                                                                                        \
-    const bool ok_ = (valid_) & (2 * (st) + h < nchunk);                                      \
-    const uint4* p_ = ok_ ? reinterpret_cast<const uint4*>((rowp_) + 32 * (st)) : g_zero_page; \
+    const bool ok_ = (valid_) & (4 * (st) + fq < nchunk);                                     \
+    const uint4* p_ = ok_ ? reinterpret_cast<const uint4*>((rowp_) + 64 * (st)) : g_zero_page; \
     dst = *p_;                                                                                \
   } while (0)
 
   uint4 bv[NKS];
   {
-    const int m = tile * 32 + r32;
+    const int m = tile * 16 + fr;
     const bool valid = m < Mtot;
     const char* rowp = src + (size_t)(valid ? m : 0) * ld * 2;
 #pragma unroll
     for (int st = 0; st < NKS; ++st) PWW_LOAD(bv[st], st, rowp, valid);
   }
-  const bf16_t* const R0 = reinterpret_cast<const bf16_t*>(g.res0);
   const bf16_t* const R1 = reinterpret_cast<const bf16_t*>(g.res1);
-  const bf16_t* const R2 = reinterpret_cast<const bf16_t*>(g.res2);
   const int cout = g.cout;
   for (; tile < ntile; tile += tstride) {
-    const int m = tile * 32 + r32;
+    const int m = tile * 16 + fr;
     const bool valid = m < Mtot;
     const long long mm = valid ? m : 0;
-    // epilogue operands of the whole tile (raw bf16 quads), requested before the MFMAs
-    uint2 e0[NT][4], e1[NT][4], e2[NT][4];
-#pragma unroll
-    for (int j = 0; j < NT; ++j)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int n = j * 32 + 8 * q + 4 * h;
-        const bool on = valid && n < cout;
-        e0[j][q] = (R0 && on) ? *reinterpret_cast<const uint2*>(R0 + mm * g.ld0 + n) : make_uint2(0, 0);
-        e1[j][q] = (R1 && on) ? *reinterpret_cast<const uint2*>(R1 + mm * g.ld1 + n) : make_uint2(0, 0);
-        e2[j][q] = (R2 && on) ? *reinterpret_cast<const uint2*>(R2 + mm * g.ld2 + n) : make_uint2(0, 0);
-      }
     const bool sel_on = act == RGBAC_ACT_MASKSEL ? (valid && g.sel[mm] != 0) : true;
-    const int mn = (tile + tstride) * 32 + r32;
+    const int mn = (tile + tstride) * 16 + fr;
     const bool nvalid = mn < Mtot;
     const char* nrowp = src + (size_t)(nvalid ? mn : 0) * ld * 2;
-    f32x16 acc[NT];
+    f32x4 acc[NT];
 #pragma unroll
-    for (int j = 0; j < NT; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[j][r] = 0.0f;
+    for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int st = 0; st < NKS; ++st) {
       uint4 b = bv[st];
       if (sq_in) b = square_chunk<bf16_t>(b);
-      const bf16x8 bb = __builtin_bit_cast(bf16x8, b);
-      const int slot = (2 * st + h) ^ (r32 & 7);
+      const int slot = (4 * st + fq) ^ (fr & 7);
 #pragma unroll
       for (int j = 0; j < NT; ++j) {
-        const uint4 a = Wl[(j * 32 + r32) * NCH + slot];
-        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), bb,
-                                                         acc[j], 0, 0, 0);
+        const uint4 a = Wl[(16 * j + fr) * NCH + slot];
+        mma_step<bf16_t>(acc[j], a, b);
       }
       PWW_LOAD(bv[st], st, nrowp, nvalid);
     }
     if (valid) {
+      // res1 quads of the whole tile (raw bf16), all requested before any epilogue math
+      uint2 e1[NT];
 #pragma unroll
-      for (int j = 0; j < NT; ++j)
+      for (int j = 0; j < NT; ++j) {
+        const int n = 16 * j + 4 * fq;
+        e1[j] = (R1 && n < cout) ? *reinterpret_cast<const uint2*>(R1 + mm * g.ld1 + n)
+                                 : make_uint2(0, 0);
+      }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int nl = j * 32 + 8 * q + 4 * h;
-          if (nl < cout) {
-            EpiIn in;
-            in.r0[0] = bf2f(e0[j][q].x & 0xFFFF); in.r0[1] = bf2f(e0[j][q].x >> 16);
-            in.r0[2] = bf2f(e0[j][q].y & 0xFFFF); in.r0[3] = bf2f(e0[j][q].y >> 16);
-            in.r1[0] = bf2f(e1[j][q].x & 0xFFFF); in.r1[1] = bf2f(e1[j][q].x >> 16);
-            in.r1[2] = bf2f(e1[j][q].y & 0xFFFF); in.r1[3] = bf2f(e1[j][q].y >> 16);
-            in.r2[0] = bf2f(e2[j][q].x & 0xFFFF); in.r2[1] = bf2f(e2[j][q].x >> 16);
-            in.r2[2] = bf2f(e2[j][q].y & 0xFFFF); in.r2[3] = bf2f(e2[j][q].y >> 16);
-            in.on = sel_on;
-            float v[4] = {acc[j][4 * q], acc[j][4 * q + 1], acc[j][4 * q + 2], acc[j][4 * q + 3]};
-            const float bias[4] = {bl[nl], bl[nl + 1], bl[nl + 2], bl[nl + 3]};
-            epilogue4_fin<bf16_t>(s, g, (long long)m, nl, v, bias, in);
-          }
+      for (int j = 0; j < NT; ++j) {
+        const int n = 16 * j + 4 * fq;
+        if (n < cout) {
+          EpiIn in;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { in.r0[r] = 0.f; in.r2[r] = 0.f; }
+          in.r1[0] = bf2f(e1[j].x & 0xFFFF); in.r1[1] = bf2f(e1[j].x >> 16);
+          in.r1[2] = bf2f(e1[j].y & 0xFFFF); in.r1[3] = bf2f(e1[j].y >> 16);
+          if (g.res0) load_res<bf16_t>(g.res0, g.ld0, mm, n, cout, in.r0);
+          if (g.res2) load_res<bf16_t>(g.res2, g.ld2, mm, n, cout, in.r2);
+          in.on = sel_on;
+          float v[4] = {acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
+          const float bias[4] = {bl[n], bl[n + 1], bl[n + 2], bl[n + 3]};
+          epilogue4_fin<bf16_t>(s, g, (long long)m, n, v, bias, in);
         }
+      }
     }
   }
 #undef PWW_LOAD
@@ -1853,7 +1842,7 @@ __global__ void __launch_bounds__(256, 1) conv_pw_kernel(const ConvArgsDev args)
 template <int NKS>
 static void launch_pw_k(const ConvArgsDev& d, hipStream_t st) {
   auto kern = conv_pw_kernel<NKS>;
-  constexpr size_t lds = (size_t)192 * 2 * NKS * 16;
+  constexpr size_t lds = (size_t)192 * 4 * NKS * 16;
   static bool attr = false;
   static int ncu = 0;
   if (!attr) {
@@ -1863,21 +1852,22 @@ static void launch_pw_k(const ConvArgsDev& d, hipStream_t st) {
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (ncu < 1) ncu = 256;
+    (void)hipGetLastError();
     attr = true;
   }
   const int nz = d.s.ngroups;
-  const int ntile = (d.s.M + 31) / 32;
-  int gx = (ncu + nz - 1) / nz;
-  const int need = (ntile + 3) / 4;
+  const int ntile = (d.s.M + 15) / 16;
+  int gx = (2 * ncu + nz - 1) / nz;
+  const int need = (ntile + 7) / 8;
   if (gx > need) gx = need;
   if (gx < 1) gx = 1;
-  hipLaunchKernelGGL(kern, dim3(gx, 1, nz), dim3(256), lds, st, d);
+  hipLaunchKernelGGL(kern, dim3(gx, 1, nz), dim3(512), lds, st, d);
 }
 
 static void launch_pw(const ConvArgsDev& d, int cin_max, hipStream_t st) {
-  if (cin_max <= 64) launch_pw_k<4>(d, st);
-  else if (cin_max <= 128) launch_pw_k<8>(d, st);
-  else launch_pw_k<12>(d, st);
+  if (cin_max <= 64) launch_pw_k<2>(d, st);
+  else if (cin_max <= 128) launch_pw_k<4>(d, st);
+  else launch_pw_k<6>(d, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -2993,15 +2983,19 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
       // the unrolled-K variant when it is a conv and every group has the same cin32 of 3, 4
       // or 7 k-steps per tap (the slice stacks: 80..128 and 224 input channels)
       int cpt = 0;
-      if (s.mode == RGBAC_CONV) {
+      if (s.mode == RGBAC_CONV || (ks3 && s.mode == RGBAC_SUBPEL2)) {
         cpt = ((d.g[0].cin_pad + 31) & ~31) >> 5;
         for (int i = 1; i < s.ngroups; ++i)
           if ((((d.g[i].cin_pad + 31) & ~31) >> 5) != cpt) cpt = 0;
-        if (cpt != 3 && cpt != 4 && cpt != 7) cpt = 0;
+        // 8..10 k-steps per tap (the hyperprior's 256..320-channel 3x3 convs / subpel convs
+        // on the 16x16 grid): the K-split tiles 51 / 52 only
+        const bool wide = ks3 && (tile == kFirstFPatchKS || tile == kFirstFPatchKS + 1);
+        if (!(cpt == 3 || cpt == 4 || cpt == 7 || (wide && cpt >= 8 && cpt <= 10))) cpt = 0;
         if (!fpatch_cpt_enabled()) cpt = 0;
       }
       if (ks3 && cpt == 0) {
-        set_error("K-split fragment-patch tiles: 3x3 conv with 96/128/224-channel inputs only");
+        set_error("K-split fragment-patch tiles: 3x3 conv with 96/128/224 (tiles 51/52 also "
+                  "256/288/320)-channel inputs only");
         return RGBAC_E_ARG;
       }
 #define RGBAC_FP1(TH_, BN_, C_)                                                               \
@@ -3032,6 +3026,13 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
     else if (cpt == 4) RGBAC_FPK(TH_, BN_, NW_, 4);                                           \
     else RGBAC_FPK(TH_, BN_, NW_, 7);                                                         \
   } while (0)
+#define RGBAC_FPKW(BN_)                                                                       \
+  do {                                                                                        \
+    if (cpt == 8) RGBAC_FPK(4, BN_, 4, 8);                                                    \
+    else if (cpt == 9) RGBAC_FPK(4, BN_, 4, 9);                                               \
+    else if (cpt == 10) RGBAC_FPK(4, BN_, 4, 10);                                             \
+    else RGBAC_FPKS(4, BN_, 4);                                                               \
+  } while (0)
 #define RGBAC_FP(TH_, BN_)                                                                    \
   do {                                                                                        \
     if (TH_ != 4) RGBAC_FP1(TH_, BN_, 0);  /* 8-row tiles: the generic loop is faster */     \
@@ -3047,8 +3048,8 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
         case 45: RGBAC_FP(4, 128); break;
         case 46: RGBAC_FP(8, 256); break;
         case kTileFPatch464: RGBAC_FP(4, 64); break;
-        case kFirstFPatchKS: RGBAC_FPKS(4, 64, 4); break;
-        case kFirstFPatchKS + 1: RGBAC_FPKS(4, 128, 4); break;
+        case kFirstFPatchKS: RGBAC_FPKW(64); break;
+        case kFirstFPatchKS + 1: RGBAC_FPKW(128); break;
         case kFirstFPatchKS + 2: RGBAC_FPKS(4, 192, 4); break;
         case kFirstFPatchKS2: RGBAC_FPKS(8, 64, 4); break;
         case kFirstFPatchKS2 + 1: RGBAC_FPKS(8, 128, 4); break;
@@ -3057,6 +3058,7 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
       }
 #undef RGBAC_FP
 #undef RGBAC_FP1
+#undef RGBAC_FPKW
 #undef RGBAC_FPKS
 #undef RGBAC_FPK
       return check_launch("conv_fpatch_kernel");

@@ -242,6 +242,82 @@ __global__ void avgpool3s2_kernel(int batch, int H, int W, int Ho, int Wo,
   }
 }
 
+// The whole mask pyramid of rgbac_mask_pyramid (optional round(255 a) / 255, then L levels of
+// AvgPool2d(3, 2, 1, count_include_pad)) in ONE launch instead of 1 + L: a workgroup owns a
+// TP x TP tile of the last level and recomputes, in LDS, every level's region that tile
+// depends on (region of level l = 2 x that of level l + 1, plus one), writing the core rows
+// of every level it owns.  Each value is the same float sum in the same tap order as
+// avgpool3s2_kernel (out-of-image taps there are skipped, here added as +0): bit-identical.
+struct PyrOuts { float* p[4]; };
+
+template <int L>
+__global__ void __launch_bounds__(256) pyramid_kernel(int batch, int H, int W,
+                                                      const float* __restrict__ alpha,
+                                                      int round255, float* __restrict__ rounded,
+                                                      PyrOuts outs) {
+  constexpr int TP = 64 >> L;                          // last-level tile: 32 / 16 / 8 / 4
+  constexpr int N0 = (TP + 1) * (1 << L) - 1;          // level-0 region side (65 .. 79)
+  extern __shared__ float pyr[];
+  float* bufA = pyr;
+  float* bufB = pyr + N0 * N0;
+  int sh[L + 1], sw[L + 1];
+  sh[0] = H; sw[0] = W;
+#pragma unroll
+  for (int l = 1; l <= L; ++l) { sh[l] = (sh[l - 1] - 1) / 2 + 1; sw[l] = (sw[l - 1] - 1) / 2 + 1; }
+  const int ntx = (sw[L] + TP - 1) / TP, nty = (sh[L] + TP - 1) / TP;
+  int t = blockIdx.x;
+  const int tx = t % ntx; t /= ntx;
+  const int ty = t % nty;
+  const int b = t / nty;
+  // level-0 region origin and side
+  const int s0 = 1 << L;
+  const int ry = ty * TP * s0 - (s0 - 1), rx = tx * TP * s0 - (s0 - 1);
+  const float* ab = alpha + (long long)b * H * W;
+  for (int e = threadIdx.x; e < N0 * N0; e += 256) {
+    const int i = e / N0, j = e - (e / N0) * N0;
+    const int y = ry + i, x = rx + j;
+    float v = 0.0f;
+    if (y >= 0 && y < H && x >= 0 && x < W) {
+      v = ab[(long long)y * W + x];
+      if (round255) {
+        v = rintf(v * 255.0f) / 255.0f;
+        // core rows / cols of level 0 owned by this tile
+        if (i >= s0 - 1 && i < s0 - 1 + TP * s0 && j >= s0 - 1 && j < s0 - 1 + TP * s0)
+          rounded[((long long)b * H + y) * W + x] = v;
+      }
+    }
+    bufA[e] = v;
+  }
+  __syncthreads();
+  int n = N0;                                          // side of the previous level's region
+#pragma unroll
+  for (int l = 1; l <= L; ++l) {
+    const int m = (n - 1) / 2;                         // this level's region side
+    const int sc = 1 << (L - l);
+    const int oy = ty * TP * sc - (sc - 1), ox = tx * TP * sc - (sc - 1);   // region origin
+    float* const o = outs.p[l - 1];
+    for (int e = threadIdx.x; e < m * m; e += 256) {
+      const int i = e / m, j = e - (e / m) * m;
+      const int y = oy + i, x = ox + j;
+      float v = 0.0f;
+      if (y >= 0 && y < sh[l] && x >= 0 && x < sw[l]) {
+        float s = 0.f;
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx) s += bufA[(2 * i + dy) * n + 2 * j + dx];
+        v = s / 9.0f;
+        if (i >= sc - 1 && i < sc - 1 + TP * sc && j >= sc - 1 && j < sc - 1 + TP * sc)
+          o[((long long)b * sh[l] + y) * sw[l] + x] = v;
+      }
+      bufB[e] = v;
+    }
+    __syncthreads();
+    float* tmp = bufA; bufA = bufB; bufB = tmp;
+    n = m;
+  }
+}
+
 template <typename T>
 __global__ void nchw_to_nhwc_kernel(int batch, int C, int HW, const float* __restrict__ src,
                                     T* __restrict__ dst, long long ldc) {
@@ -354,6 +430,29 @@ extern "C" int rgbac_mask_pyramid(int batch, int h, int w, const float* alpha, i
   RGBAC_REQUIRE(levels >= 0 && levels <= 8, "levels");
   RGBAC_REQUIRE(!round255 || rounded, "round255 needs an output buffer");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  static const bool fused = [] {
+    const char* e = getenv("RGBAC_PYRAMID_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  if (fused && levels >= 1 && levels <= 4) {           // the forward's 4-level pyramids: 1 launch
+    for (int l = 0; l < levels; ++l) RGBAC_REQUIRE(outs && outs[l], "null pyramid output");
+    PyrOuts po{};
+    for (int l = 0; l < levels; ++l) po.p[l] = outs[l];
+    int hl = h, wl = w;
+    for (int l = 0; l < levels; ++l) { hl = (hl - 1) / 2 + 1; wl = (wl - 1) / 2 + 1; }
+    const int tp = 64 >> levels;
+    const long long nblk = (long long)batch * ((hl + tp - 1) / tp) * ((wl + tp - 1) / tp);
+    RGBAC_REQUIRE(nblk < (1ll << 31), "too many pyramid tiles");
+    const int n0 = (tp + 1) * (1 << levels) - 1;
+    const size_t lds = (size_t)2 * n0 * n0 * sizeof(float);
+    switch (levels) {
+      case 1: hipLaunchKernelGGL(pyramid_kernel<1>, dim3((unsigned)nblk), dim3(256), lds, st, batch, h, w, alpha, round255, rounded, po); break;
+      case 2: hipLaunchKernelGGL(pyramid_kernel<2>, dim3((unsigned)nblk), dim3(256), lds, st, batch, h, w, alpha, round255, rounded, po); break;
+      case 3: hipLaunchKernelGGL(pyramid_kernel<3>, dim3((unsigned)nblk), dim3(256), lds, st, batch, h, w, alpha, round255, rounded, po); break;
+      default: hipLaunchKernelGGL(pyramid_kernel<4>, dim3((unsigned)nblk), dim3(256), lds, st, batch, h, w, alpha, round255, rounded, po); break;
+    }
+    return check_launch("pyramid_kernel");
+  }
   const float* cur = alpha;
   if (round255) {
     const long long n = (long long)batch * h * w;

@@ -165,6 +165,20 @@ def fpatch_cpt(preps):
         return 0
     c = {round_up(p.pk.cin_pad, 32) // 32 for p in preps}
     return c.pop() if len(c) == 1 and next(iter(c)) in (3, 4, 7) else 0
+def fpatch_cpt_ks(preps, tile):
+    """CPT of a K-split fragment-patch tile (51-53, 56-58) for these convs, 0 if it does not
+    apply: conv with 3 / 4 / 7 k-steps per tap, and on tiles 51 / 52 also subpel convs and
+    8..10 k-steps per tap (csrc/conv.hip launch_conv)."""
+    if not FPATCH_CPT:
+        return 0
+    wide = tile in (51, 52)
+    if preps[0].pk.mode != CONV and not (wide and preps[0].pk.mode == SUBPEL2):
+        return 0
+    c = {round_up(p.pk.cin_pad, 32) // 32 for p in preps}
+    if len(c) != 1:
+        return 0
+    c = c.pop()
+    return c if c in (3, 4, 7) or (wide and 8 <= c <= 10) else 0
 PATCH = os.environ.get("RGBAC_PATCH", "1") != "0"
 
 
@@ -216,13 +230,12 @@ def _patch_tiles(preps):
     # every step in the plain layout) and the whole patch in LDS
     if all(isinstance(p.pk, PackedConv) for p in preps):
         c32 = max(round_up(p.pk.cin_pad, 32) for p in preps)
-        cpt = fpatch_cpt(preps)
         for t, (th, bn) in FPATCH_SIG.items():
             if hm % th or (th + 2) * 18 * (c32 // 8 + 2) * 16 > 160 * 1024:
                 continue
             if t in FPATCH_KS and 2 * (bn // 16) * th * 1024 > 160 * 1024:
                 continue
-            if t in FPATCH_KS and not cpt:
+            if t in FPATCH_KS and not fpatch_cpt_ks(preps, t):
                 continue
             if all(p.pk.cout_pad >= -(-p.pk.cout // bn) * bn for p in preps):
                 out.append(t)
@@ -585,7 +598,7 @@ def kernel_name(tile, preps):
         return f"conv3x3_c32_kernel<{dt}>"
     if tile in FPATCH_KS:
         return "conv_fpatch_kernel<%d, %d, %d, 4, %d, 3>" % (FPATCH_SIG[tile] + (FPATCH_KS[tile],
-                                                                           fpatch_cpt(preps)))
+                                                                           fpatch_cpt_ks(preps, tile)))
     if tile in FPATCH_SIG:
         c = fpatch_cpt(preps) if FPATCH_SIG[tile][0] == 4 else 0
         return "conv_fpatch_kernel<%d, %d, 4, 4%s>" % (FPATCH_SIG[tile] + (f", {c}" if c else "",))

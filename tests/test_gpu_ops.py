@@ -214,6 +214,29 @@ def test_mask_pyramid(device):
     assert torch.equal(r.cpu(), torch.round(a * 0.999 * 255) / 255)
 
 
+@pytest.mark.parametrize("levels", [1, 2, 3, 4])
+@pytest.mark.parametrize("H,W", [(256, 256), (70, 94), (33, 17)])
+def test_mask_pyramid_fused_matches_chain(device, levels, H, W):
+    """The one-launch pyramid (round255 + up to 4 AvgPool levels, LDS-recomputed halos) is
+    bit-identical to the launch-per-level chain (RGBAC_PYRAMID_FUSED=0) and to torch's
+    AvgPool2d(3, 2, 1) on the rounded alpha, ragged and odd sizes included."""
+    from rgbac.layers.SupplyMask import mask_pyramid
+    g = _gen(7 + levels + H)
+    a = torch.rand((3, 1, H, W), generator=g)
+    r, lv = mask_pyramid(a.to(device), levels, round255=True)
+    want_r = torch.round(a * 255) / 255
+    assert torch.equal(r.cpu(), want_r)
+    t = want_r
+    for l in range(levels):
+        t = F.avg_pool2d(t, 3, 2, 1)
+        assert lv[l].shape == t.shape
+        assert (lv[l].cpu() - t).abs().max().item() <= 3e-7, l
+    r6, lv6 = mask_pyramid(a.to(device), 6, round255=True)     # > 4 levels: the chain
+    assert torch.equal(r6.cpu(), r.cpu())
+    for l in range(levels):
+        assert torch.equal(lv6[l].cpu(), lv[l].cpu()), l
+
+
 # ------------------------------------------------------------------ every tile x split-K
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("tile", list(range(7)) + list(range(20, 34)))
@@ -420,10 +443,11 @@ def test_conv_smallk_tile(device, cin, cout, k, s, act):
                                            (192, 192, "gdn"), (192, 192, "igdn"), (80, 80, "igdn"),
                                            (192, 192, "gate"), (192, 192, "masksel")])
 def test_conv_pw_tile(device, cin, cout, kind):
-    """The full-width pointwise tile (54, bf16): every output channel of a 32-pixel tile in one
-    wave, epilogue operands prefetched.  Same MFMA sequence as the small-K tile, so the two
-    agree bit for bit on the model's 1x1 epilogues (GDN / IGDN on the squared input, the
-    attention block's gate a * sigmoid(b) + x, MASKSEL), and the plain convs match fp32 torch."""
+    """The full-width pointwise tile (54, bf16): every output channel of a 16-pixel tile in one
+    wave, the res1 operand prefetched.  Against the small-K tile on the model's 1x1 epilogues
+    (GDN / IGDN on the squared input, the attention block's gate a * sigmoid(b) + x, MASKSEL;
+    a different MFMA shape, so within bf16 output rounding), and the plain convs against fp32
+    torch on the same bf16 operands."""
     rt = _rt()
     from rgbac.layers.TransformRGB import run_conv
     g = _gen(900 + cin + cout)
@@ -461,7 +485,7 @@ def test_conv_pw_tile(device, cin, cout, kind):
             outs[tile] = rt.to_nchw(o).float().cpu()
         finally:
             rt.FORCE = None
-    assert torch.equal(outs[rt.TILE_PW], outs[rt.TILE_SMALLK]), kind
+    assert rel(outs[rt.TILE_PW], outs[rt.TILE_SMALLK]) < 1e-2, kind
     if kind in ("gelu", "none", "relu"):
         f = {"gelu": F.gelu, "relu": F.relu, "none": lambda t: t}[kind]
         xb = x.to(dt).float()
@@ -613,6 +637,8 @@ PATCH_CASES = [
     ("conv", 224, 128, 16, 16), ("conv", 120, 224, 8, 32), ("conv", 40, 40, 8, 16),
     ("conv", 88, 224, 8, 16),
     ("subpel", 192, 192, 8, 16), ("subpel", 192, 12, 16, 16),
+    # the hyperprior's 16x16-grid convs (8..10 k-steps per tap: K-split tiles 51 / 52)
+    ("conv", 256, 288, 16, 16), ("subpel", 288, 80, 16, 16), ("conv", 320, 288, 16, 16),
 ]
 
 

@@ -21,8 +21,7 @@ def run(args):
     from rgbac.layers.SupplyMask import mask_pyramid
     from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
     dev = torch.device("cuda:0")
-    torch.manual_seed(234)
-    net = AutoEncoder().eval().to(dev).set_compute_dtype(torch.bfloat16)
+    net = bench.rgb_net().to(dev).set_compute_dtype(torch.bfloat16)   # the bench's codec
     x, a = bench.synth_inputs(args.batch, args.size, args.size, seed=0)
     x, a = x.to(dev), a.to(dev)
     _, me = mask_pyramid(a, 4)

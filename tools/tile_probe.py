@@ -13,7 +13,8 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "deep-learning-based-rgba-image-compres
                                          "masked-window-based-attention_amd")]
 
 from rgbac import runtime as rt  # noqa: E402
-from rgbac.layers.TransformRGB import prep_conv  # noqa: E402
+from rgbac.layers.TransformRGB import prep_conv, prep_subpel  # noqa: E402
+from rgbac.layers._blocks import subpel_conv3x3  # noqa: E402
 
 # name, cin list, cout, k, H, W, B, groups, kind ("conv" | "gdn" | "gate")
 SHAPES = [
@@ -28,6 +29,9 @@ SHAPES = [
     ("cc1 120->224 g10", [80, 40], 224, 3, 32, 32, 8, 10, "conv"),
     ("lrp1 128->224 g5", [80, 40, 8], 224, 3, 32, 32, 8, 5, "conv"),
     ("cc2 224->128 g10", [224], 128, 3, 32, 32, 8, 10, "conv"),
+    ("hs 256->288 g2 16x16", [256], 288, 3, 16, 16, 8, 2, "conv"),
+    ("hs subpel 288->80 g2 16x16", [288], 80, 3, 16, 16, 8, 2, "subpel"),
+    ("ha 320->288 16x16", [320], 288, 3, 16, 16, 8, 1, "conv"),
 ]
 
 
@@ -44,7 +48,8 @@ def main():
         preps = []
         for gi in range(G):
             torch.manual_seed(gi)
-            m = nn.Conv2d(sum(cins), cout, k, padding=k // 2).to(dev)
+            m = (subpel_conv3x3(sum(cins), cout, 2) if kind == "subpel"
+                 else nn.Conv2d(sum(cins), cout, k, padding=k // 2)).to(dev)
             if kind in ("gdn", "igdn"):
                 with torch.no_grad():
                     m.weight.uniform_(0, 0.01)
@@ -58,6 +63,8 @@ def main():
                 r1 = rt.to_nhwc(torch.randn((B, cout, H, W), device=dev), dt)
                 pk = rt.packed(m, dt, [(cins[0], rt.round_up(cins[0], 8))])
                 preps.append(rt.prepare(pk, srcs, act="gate", res1=r1, res2=r1))
+            elif kind == "subpel":
+                preps.append(prep_subpel(m, srcs))
             else:
                 preps.append(prep_conv(m, srcs, act="gelu"))
         p0 = preps[0]
