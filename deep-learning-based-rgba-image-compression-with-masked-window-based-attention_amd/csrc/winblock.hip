@@ -8,27 +8,32 @@
 // One launch replaces three (qkv 1x1 GEMM -> HBM, attention core, proj GEMM + MASKSEL):
 // the 576-channel qkv tensor (37.7 MB at 64x64 B8) never leaves the chip.
 //
-// One workgroup = 2 windows = 128 tokens, 8 waves of 16 tokens (or 4 of 32; a wave's tokens
-// lie in one window).  Per head pair (48 qkv channels of each kind):
-//   QKV   q^T, k^T = Wq|Wk (LDS) x X^T (registers); v = X x Wv^T   -> LDS (bf16, padded to 32)
-//   per head:  S^T = K Q^T (keys on the MFMA row axis), + B_rel (LDS table) + shift mask,
-//              softmax (rows in 4 lanes: two xor-shuffles) -> P (wave-private LDS),
-//              O^T = V^T P^T -> O (aliases P), out^T += Wproj[:, head] (LDS) x O^T (registers)
-// The x tile stays in registers as MFMA fragments for all four pairs; the proj output
-// (192 x 32 per wave) accumulates in registers over the 8 heads; the MASKSEL residual is
-// the epilogue.  Weights are pre-packed fragment-major (1 KiB per 16 rows x 32 k) and
-// streamed into LDS by LDS-DMA one pair / head ahead, waited on with counted vmcnt.
+// One workgroup = 2 windows = 128 tokens, 8 waves; wave w owns the 16 tokens 16w..16w+15
+// (token tile w & 3 of window w >> 2).  The attention chain runs in REGISTERS: every product
+// after the qkv GEMM takes its operand straight from the accumulator of the one before
+// (v_mfma_f32_16x16x32_bf16: an accumulator tile holds column lane&15, rows 4(lane>>4)+r, so
+// two 16-row tiles side by side are one 32-deep k-step whose k order is permuted the same way
+// in both operands of the next product):
+//   q^T, k^T = Wq|Wk X^T  (channels x tokens)        v = X Wv^T  (tokens x channels)
+//   S^T = K Q^T    per head: ONE k-step (channel tiles (0, 1) or (1, 2) of the pair, the other
+//                  head's 8 channels of tile 1 zeroed in q)
+//   P^T = softmax over keys (rows: 4 lanes apart, two xor-shuffles; exp2 with log2 e folded
+//                  into the q scale and the bias tables)
+//   O^T = V^T P^T  (key-tile pairs as k-steps; tile 1's rows masked per head)
+//   out^T += Wp O^T every two head pairs (3 k-steps of O^T tile pairs; the proj weights are
+//                  packed in that permuted k order on the host)
+// Only k^T and v cross waves (the four token tiles of a window share the keys): each wave
+// stores its k^T / v fragments to LDS once per head pair (14 KiB per window) and reads the
+// window's.  Weights are pre-packed fragment-major (1 KiB per 16 rows x 32 k) and streamed
+// into LDS by LDS-DMA one pair ahead, waited on at the pair's barrier.  Two barriers per
+// head pair (exchange visible / exchange free), nine in all.
 //
-// MFMA v_mfma_f32_16x16x32_bf16 throughout (acc[row][col] += A[row][k] B[col][k]);
-// per 32 tokens: 4 x 108 (QKV) + 8 x (8 + 8 + 24) = 752 MFMAs.  Softmax on exp2 with log2 e
-// folded into the q scale and the bias tables.
+// MFMAs per 16 tokens: 54 x 4 (qkv) + 8 x (4 + 4) (scores, PV) + 36 x 2 (proj) = 352.
 //
-// LDS (bytes): WQ 54 KiB | WP 2 x 12 KiB | QK [2 heads][q,k][128 tok][64 B] 32 KiB |
-// VT [2 heads][32 ch][128 tok] 16 KiB | P/O [4 waves][4 KiB] | relative-position bias
-// [table, table - 100 (the shift mask folded in)][8 heads][225] fp32 (head-major: the
-// per-lane gathers spread over the banks) | proj bias -> 161,616 B: one workgroup per CU.
-// Swizzles (all conflict-free for the ds_read_b128 lane groups): 64-B token rows
-// chunk ^ ((tok >> 1) & 3); V^T 256-B rows chunk ^ (ch & 15); P 128-B rows chunk ^ (q & 7).
+// LDS (bytes): WQ 54 KiB | WP 36 KiB | K^T [2 win][2 heads][4 key tiles] 16 KiB |
+// V^T [2 win][3 channel tiles][2 key pairs] 12 KiB | relative-position bias [table,
+// table - 100 (the shift mask folded in)][8 heads][225] fp32 | proj bias -> 136,000 B.
+// All fragment images are lane-major (16 B per lane): conflict-free ds_read/write_b128.
 #include <cstdlib>
 
 #include "common.h"
@@ -36,17 +41,18 @@
 namespace rgbac {
 
 namespace wb {
-constexpr int WS = 8, NT = 64, C = 192, HEADS = 8, DH = 24, TOK = 128;
+constexpr int WS = 8, C = 192, HEADS = 8, TOK = 128;
 constexpr int WQF = 54;                                // qkv fragments per head pair
-constexpr int WPF = 12;                                // proj fragments per head
+constexpr int WPF = 36;                                // proj fragments per two head pairs
 constexpr int L_WQ = 0;
 constexpr int L_WP = L_WQ + WQF * 1024;                // 55296
-constexpr int L_QK = L_WP + 2 * WPF * 1024;            // 79872
-constexpr int L_VT = L_QK + 2 * 2 * TOK * 64;          // 112640
-constexpr int L_P = L_VT + 2 * 32 * TOK * 2;           // 129024
-constexpr int L_TB = L_P + 4 * 4096;                   // 145408: bias [2][8 heads][225]
-constexpr int L_BQ = L_TB + 2 * 8 * 225 * 4;           // 159808: bproj[192]
-constexpr int LDS = L_BQ + 192 * 4;                    // 160576
+constexpr int L_XK = L_WP + WPF * 1024;                // 92160
+constexpr int L_XV = L_XK + 2 * 2 * 4 * 1024;          // 108544
+constexpr int L_TB = L_XV + 2 * 3 * 2 * 1024;          // 120832: bias [2][8 heads][225]
+constexpr int L_BQ = L_TB + 2 * 8 * 225 * 4;           // 135232: bproj[192]
+constexpr int LDS = L_BQ + 192 * 4;                    // 136000
+constexpr int WQ_W = (WQF + 7) / 8;                    // DMA pieces per wave (7)
+constexpr int WP_W = (WPF + 7) / 8;                    // (5)
 }  // namespace wb
 
 struct WinBlockArgs {
@@ -56,7 +62,7 @@ struct WinBlockArgs {
   const float* alpha;                    // (B, H, W) fp32 when masked
   const bf16_t* wq;                      // [4 pairs][54][64 lanes][8]
   const float* bqkv;                     // [576]
-  const bf16_t* wp;                      // [8 heads][12][64][8]
+  const bf16_t* wp;                      // [2 pair pairs][12 m][3 k-steps][64][8] (permuted k)
   const float* bproj;                    // [192]
   const float* table;                    // relative_position_bias_table [225][8]
   bf16_t* out; long long ldo;
@@ -74,19 +80,15 @@ __device__ __forceinline__ void wb_dma16(const void* src, uint32_t lds) {
       : "v"(src), "s"(lds)
       : "memory");
 }
-template <int N>
-__device__ __forceinline__ void wb_wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
+__device__ __forceinline__ void wb_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// NQT 16-token tiles per wave: NQT = 1 -> 8 waves (2 per SIMD: one wave's softmax VALU
-// overlaps the other's MFMAs), NQT = 2 -> 4 waves (twice the weight-fragment reuse).
-template <int NQT>
-__global__ void __launch_bounds__(64 * 8 / NQT, 1) winblock_kernel(const WinBlockArgs a) {
+__device__ __forceinline__ uint2 pk4(const f32x4& v) {
+  return make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+}
+__device__ __forceinline__ uint4 cat2(uint2 lo, uint2 hi) { return make_uint4(lo.x, lo.y, hi.x, hi.y); }
+
+__global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlockArgs a) {
   using namespace wb;
-  constexpr int NWAVE = 8 / NQT, NTHR = 64 * NWAVE, TPW = 16 * NQT;
-  constexpr int WQ_W = (WQF + NWAVE - 1) / NWAVE;      // DMA pieces per wave (7 or 14)
-  constexpr int WP_W = (WPF + NWAVE - 1) / NWAVE;      // (2 or 3)
   constexpr float LOG2E = 1.4426950408889634f;
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
   __shared__ int pix_s[TOK];
@@ -100,9 +102,8 @@ __global__ void __launch_bounds__(64 * 8 / NQT, 1) winblock_kernel(const WinBloc
   const int nwx = W / WS, nwy = H / WS;
   const int total = a.batch * nwx * nwy;
   const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) void*)sm;
-  const int tok0 = TPW * w;                            // this wave's first token (of 128)
-  const int win = tok0 >> 6;                           // its window (0 or 1)
-  const int lq0 = tok0 & 63;                           // ... and first query within it
+  const int tok0 = 16 * w;                             // this wave's first token (of 128)
+  const int win = w >> 2, tt = w & 3;                  // its window and token tile in it
 
   // ---- window gather: token -> pixel (cyclic shift folded in), shifted-frame region id
   if (tid < 2) act_s[tid] = a.masked ? 0 : 1;
@@ -129,7 +130,7 @@ __global__ void __launch_bounds__(64 * 8 / NQT, 1) winblock_kernel(const WinBloc
   const bool act = act_s[win] != 0 && pix_s[tok0] >= 0;         // wave-uniform
   if (act_s[0] == 0 && act_s[1] == 0) {
     // both windows transparent: out = x on their tokens
-    for (int e = tid; e < TOK * (C / 8); e += NTHR) {
+    for (int e = tid; e < TOK * (C / 8); e += 512) {
       const int t = e / (C / 8), c8 = e - t * (C / 8);
       const int pix = pix_s[t];
       if (pix >= 0)
@@ -139,67 +140,54 @@ __global__ void __launch_bounds__(64 * 8 / NQT, 1) winblock_kernel(const WinBloc
     return;
   }
 
-  // ---- weight streams: pair p's qkv fragments, head h's proj fragments (pieces past the
-  // end repeat the last one: same bytes to the same place, so every wave issues as many)
+  // ---- weight streams (pieces past the end repeat the last one: same bytes to the same
+  // place, so every wave issues as many)
   auto dma_wq = [&](int p) {
 #pragma unroll
     for (int i = 0; i < WQ_W; ++i) {
-      int f = w + NWAVE * i;
+      int f = w + 8 * i;
       if (f >= WQF) f = WQF - 1;
       wb_dma16(a.wq + ((size_t)(p * WQF + f) * 64 + lane) * 8, lds0 + L_WQ + f * 1024);
     }
   };
-  auto dma_wp = [&](int h) {
+  auto dma_wp = [&](int u) {
 #pragma unroll
     for (int i = 0; i < WP_W; ++i) {
-      int f = w + NWAVE * i;
+      int f = w + 8 * i;
       if (f >= WPF) f = WPF - 1;
-      wb_dma16(a.wp + ((size_t)(h * WPF + f) * 64 + lane) * 8,
-               lds0 + L_WP + (h & 1) * WPF * 1024 + f * 1024);
+      wb_dma16(a.wp + ((size_t)(u * WPF + f) * 64 + lane) * 8, lds0 + L_WP + f * 1024);
     }
   };
   dma_wq(0);
   dma_wp(0);
 
-  // ---- tables (in log2 units: softmax runs on exp2) and zero padding (q/k channels 24..31:
-  // chunk 3; V^T rows 24..31)
+  // ---- tables (in log2 units: softmax runs on exp2)
   float* tb = reinterpret_cast<float*>(sm + L_TB);
-  for (int e = tid; e < 225 * 8; e += NTHR) {          // table [225][8] -> [var][8][225]
+  for (int e = tid; e < 225 * 8; e += 512) {           // table [225][8] -> [var][8][225]
     const int idx = e >> 3, hd = e & 7;
     const float v = a.table[e];
     tb[hd * 225 + idx] = v * LOG2E;
     tb[8 * 225 + hd * 225 + idx] = (v + -100.0f) * LOG2E;   // the shift mask's -100 folded in
   }
   float* bq = reinterpret_cast<float*>(sm + L_BQ);
-  for (int e = tid; e < 192; e += NTHR) bq[e] = a.bproj[e];
-  for (int e = tid; e < 2 * 2 * TOK; e += NTHR) {
-    const int t = e & (TOK - 1);
-    *reinterpret_cast<uint4*>(sm + L_QK + e * 64 + ((3 ^ ((t >> 1) & 3)) << 4)) = make_uint4(0, 0, 0, 0);
-  }
-  for (int e = tid; e < 2 * 8 * 16; e += NTHR) {       // [head][row 24..31][16 chunks]
-    const int hh = e >> 7, r = 24 + ((e >> 4) & 7), c = e & 15;
-    *reinterpret_cast<uint4*>(sm + L_VT + (hh * 32 + r) * 256 + (c << 4)) = make_uint4(0, 0, 0, 0);
-  }
+  for (int e = tid; e < 192; e += 512) bq[e] = a.bproj[e];
 
-  // ---- this wave's x tile as MFMA fragments: X[j][ks] = tokens tok0+16j+n, k-chunk 4ks+qq
-  uint4 X[NQT][6];
-#pragma unroll
-  for (int j = 0; j < NQT; ++j) {
-    const int pix = pix_s[tok0 + 16 * j + n];
+  // ---- this wave's x tile as MFMA fragments: X[ks] = tokens tok0+n, k-chunk 4ks+qq
+  uint4 X[6];
+  {
+    const int pix = pix_s[tok0 + n];
     const bf16_t* row = a.x + (long long)(pix < 0 ? 0 : pix) * a.ldx;
 #pragma unroll
     for (int ks = 0; ks < 6; ++ks)
-      X[j][ks] = pix < 0 ? make_uint4(0, 0, 0, 0)
-                         : *reinterpret_cast<const uint4*>(row + 32 * ks + 8 * qq);
+      X[ks] = pix < 0 ? make_uint4(0, 0, 0, 0) : *reinterpret_cast<const uint4*>(row + 32 * ks + 8 * qq);
   }
 
   // ---- per-lane relative-position-bias offsets (head-invariant; +900 h per head), into the
   // "- 100" copy where the shift mask separates query and key:
-  // S element (qt, kt, r) = (query lq0+16qt+n, key 16kt+4qq+r) of the window
-  int toff[NQT][4][4];
-#pragma unroll
-  for (int qt = 0; qt < NQT; ++qt) {
-    const int iq = lq0 + 16 * qt + n;
+  // S^T element (kt, r) = (key 16kt+4qq+r, query 16tt+n) of the window
+  int toff[4][4];
+  {
+    const int iq = 16 * tt + n;
     const int qrid = rid_s[64 * win + iq];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
@@ -208,34 +196,45 @@ __global__ void __launch_bounds__(64 * 8 / NQT, 1) winblock_kernel(const WinBloc
         const int jk = 16 * kt + 4 * qq + r;
         const int idx = ((iq >> 3) - (jk >> 3) + 7) * 15 + ((iq & 7) - (jk & 7) + 7);
         const bool cut = shift > 0 && rid_s[64 * win + jk] != qrid;
-        toff[qt][kt][r] = L_TB + (cut ? 8 * 225 * 4 : 0) + idx * 4;
+        toff[kt][r] = L_TB + (cut ? 8 * 225 * 4 : 0) + idx * 4;
       }
   }
 
-  f32x4 acc[12][NQT];                                  // proj output: [16-ch tile][token tile]
+  f32x4 acc[12];                                       // proj output^T: 16-channel tiles
 #pragma unroll
-  for (int m = 0; m < 12; ++m)
+  for (int m = 0; m < 12; ++m) acc[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+  uint2 prevO[3];                                      // O^T of the even pair (packed bf16)
 #pragma unroll
-    for (int j = 0; j < NQT; ++j) acc[m][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < 3; ++c) prevO[c] = make_uint2(0, 0);
 
-  const int swz64 = ((qq ^ ((n >> 1) & 3)) << 4);      // 64-B token rows, base % 16 == 0
   const float qscale = a.scale * LOG2E;                // q * scale, in log2 units
-  wb_wait_vm<0>();
+  const uint32_t lo8 = n < 8 ? 0xFFFFFFFFu : 0u;       // lane holds channel row < 8 of a tile
+  const uint32_t qlo = qq < 2 ? 0xFFFFFFFFu : 0u;      // lane's accumulator rows are < 8
+  unsigned char* const xk = sm + L_XK + win * 8192;
+  unsigned char* const xv = sm + L_XV + win * 6144;
+  wb_wait_all();
   __syncthreads();
 
   for (int p = 0; p < 4; ++p) {
     if (p > 0) {
-      wb_wait_vm<WP_W>();                              // WQ(p) landed (WP(2p) may be in flight)
-      __syncthreads();
+      wb_wait_all();                                   // WQ(p) (and WP(1) at p = 3) landed
+      __syncthreads();                                 // ... everywhere; exchange free
+      if (p == 2) dma_wp(1);                           // proj(0) done in every wave
     }
-    // ================= QKV of heads 2p, 2p+1 for this wave's tokens
+    // ================= q^T, k^T, v of heads 2p, 2p+1 for this wave's 16 tokens
+    uint4 qf[2];
     if (act) {
-      f32x4 aq[3][NQT], ak[3][NQT], av[NQT][3];
+      f32x4 aq[3], ak[3], av[3];
 #pragma unroll
-      for (int t = 0; t < 3; ++t)
+      for (int t = 0; t < 3; ++t) aq[t] = ak[t] = av[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      float4 bq4[3], bk4[3];
+      float bv[3];
 #pragma unroll
-        for (int j = 0; j < NQT; ++j)
-          aq[t][j] = ak[t][j] = av[j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int t = 0; t < 3; ++t) {
+        bq4[t] = *reinterpret_cast<const float4*>(a.bqkv + 48 * p + 16 * t + 4 * qq);
+        bk4[t] = *reinterpret_cast<const float4*>(a.bqkv + 192 + 48 * p + 16 * t + 4 * qq);
+        bv[t] = a.bqkv[384 + 48 * p + 16 * t + n];
+      }
 #pragma unroll
       for (int ks = 0; ks < 6; ++ks) {
         uint4 fq[3], fk[3], fv[3];
@@ -246,187 +245,141 @@ __global__ void __launch_bounds__(64 * 8 / NQT, 1) winblock_kernel(const WinBloc
           fv[t] = *reinterpret_cast<const uint4*>(sm + L_WQ + (36 + t * 6 + ks) * 1024 + lane * 16);
         }
 #pragma unroll
-        for (int t = 0; t < 3; ++t)
-#pragma unroll
-          for (int j = 0; j < NQT; ++j) {
-            mma_step<bf16_t>(aq[t][j], fq[t], X[j][ks]);
-            mma_step<bf16_t>(ak[t][j], fk[t], X[j][ks]);
-            mma_step<bf16_t>(av[j][t], X[j][ks], fv[t]);
-          }
+        for (int t = 0; t < 3; ++t) {
+          mma_step<bf16_t>(aq[t], fq[t], X[ks]);
+          mma_step<bf16_t>(ak[t], fk[t], X[ks]);
+          mma_step<bf16_t>(av[t], X[ks], fv[t]);
+        }
       }
-      // q (x scale), k -> token rows; v -> V^T rows.  Pair channel cp = 16t + 4qq + r.
+      // q^T (x scale), k^T: rows = pair channels 16t + 4qq + r, column = token n
+      uint2 q2[3], k2[3];
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
-        const int cp = 16 * t + 4 * qq;
-        const int hh = cp >= DH ? 1 : 0, hc = cp - DH * hh;   // 4 channels, one head
-        const float4 bq4 = *reinterpret_cast<const float4*>(a.bqkv + 48 * p + cp);
-        const float4 bk4 = *reinterpret_cast<const float4*>(a.bqkv + 192 + 48 * p + cp);
+        q2[t] = make_uint2(pack_bf16x2((aq[t][0] + bq4[t].x) * qscale, (aq[t][1] + bq4[t].y) * qscale),
+                           pack_bf16x2((aq[t][2] + bq4[t].z) * qscale, (aq[t][3] + bq4[t].w) * qscale));
+        k2[t] = make_uint2(pack_bf16x2(ak[t][0] + bk4[t].x, ak[t][1] + bk4[t].y),
+                           pack_bf16x2(ak[t][2] + bk4[t].z, ak[t][3] + bk4[t].w));
+      }
+      // head 2p: channels 0..23 = tile 0 + rows 0..7 of tile 1; head 2p+1: rows 8..15 of
+      // tile 1 + tile 2.  Zeroing the other head's rows in q alone cuts them from q . k.
+      qf[0] = make_uint4(q2[0].x, q2[0].y, q2[1].x & qlo, q2[1].y & qlo);
+      qf[1] = make_uint4(q2[1].x & ~qlo, q2[1].y & ~qlo, q2[2].x, q2[2].y);
+      // K (keys x channels) fragments of this token tile for both heads
+      *reinterpret_cast<uint4*>(xk + (0 * 4 + tt) * 1024 + lane * 16) = cat2(k2[0], k2[1]);
+      *reinterpret_cast<uint4*>(xk + (1 * 4 + tt) * 1024 + lane * 16) = cat2(k2[1], k2[2]);
+      // V^T (channels x keys): this token tile is one half of key pair tt >> 1
 #pragma unroll
-        for (int j = 0; j < NQT; ++j) {
-          const int tok = tok0 + 16 * j + n;
-          const int off = tok * 64 + (((hc >> 3) ^ ((tok >> 1) & 3)) << 4) + 2 * (hc & 7);
-          *reinterpret_cast<uint2*>(sm + L_QK + (hh * 2 + 0) * TOK * 64 + off) = make_uint2(
-              pack_bf16x2((aq[t][j][0] + bq4.x) * qscale, (aq[t][j][1] + bq4.y) * qscale),
-              pack_bf16x2((aq[t][j][2] + bq4.z) * qscale, (aq[t][j][3] + bq4.w) * qscale));
-          *reinterpret_cast<uint2*>(sm + L_QK + (hh * 2 + 1) * TOK * 64 + off) = make_uint2(
-              pack_bf16x2(ak[t][j][0] + bk4.x, ak[t][j][1] + bk4.y),
-              pack_bf16x2(ak[t][j][2] + bk4.z, ak[t][j][3] + bk4.w));
-        }
-        // v: D[token][channel] -> lane holds tokens 16j+4qq+r of channel 16t+n
-        const int cv = 16 * t + n;
-        const int vh = cv >= DH ? 1 : 0, vc = cv - DH * vh;
-        const float bv = a.bqkv[384 + 48 * p + cv];
-#pragma unroll
-        for (int j = 0; j < NQT; ++j) {
-          const int tok = tok0 + 16 * j + 4 * qq;
-          const int off = (vh * 32 + vc) * 256 + (((tok >> 3) ^ (vc & 15)) << 4) + 2 * (tok & 7);
-          *reinterpret_cast<uint2*>(sm + L_VT + off) =
-              make_uint2(pack_bf16x2(av[j][t][0] + bv, av[j][t][1] + bv),
-                         pack_bf16x2(av[j][t][2] + bv, av[j][t][3] + bv));
-        }
+      for (int t = 0; t < 3; ++t) {
+        const float4 vv = make_float4(av[t][0] + bv[t], av[t][1] + bv[t], av[t][2] + bv[t], av[t][3] + bv[t]);
+        *reinterpret_cast<uint2*>(xv + (t * 2 + (tt >> 1)) * 1024 + lane * 16 + 8 * (tt & 1)) =
+            make_uint2(pack_bf16x2(vv.x, vv.y), pack_bf16x2(vv.z, vv.w));
       }
     }
-    __syncthreads();                                   // q/k/v of the pair visible; WQ free
+    __syncthreads();                                   // K / V^T of the window visible; WQ free
     if (p < 3) dma_wq(p + 1);
 
+    if (act) {
+      f32x4 o[3];
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      const int h = 2 * p + hh;
-      unsigned char* const Pw = sm + L_P + w * (2048 * NQT);   // this wave's P, then O
-      if (act) {
-        // ---- S^T = K Q^T: keys (rows) of this window x this wave's queries
-        f32x4 s[NQT][4];
-        uint4 fqv[NQT], fkv[4];
+      for (int c = 0; c < 3; ++c) o[c] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int qt = 0; qt < NQT; ++qt)
-          fqv[qt] = *reinterpret_cast<const uint4*>(
-              sm + L_QK + (hh * 2 + 0) * TOK * 64 + (tok0 + 16 * qt + n) * 64 + swz64);
+      for (int hh = 0; hh < 2; ++hh) {
+        const int h = 2 * p + hh;
+        // ---- S^T = K Q^T: rows = keys 16kt + 4qq + r, column = query n
+        f32x4 s[4];
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+          const uint4 kf = *reinterpret_cast<const uint4*>(xk + (hh * 4 + kt) * 1024 + lane * 16);
+          s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+          mma_step<bf16_t>(s[kt], kf, qf[hh]);
+        }
+        // ---- + B_rel + shift mask, softmax over the 64 keys (lane + lanes ^16, ^32, ^48)
+        float mx = -INFINITY;
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt)
-          fkv[kt] = *reinterpret_cast<const uint4*>(
-              sm + L_QK + (hh * 2 + 1) * TOK * 64 + (64 * win + 16 * kt + n) * 64 + swz64);
 #pragma unroll
-        for (int qt = 0; qt < NQT; ++qt)
-#pragma unroll
-          for (int kt = 0; kt < 4; ++kt) {
-            s[qt][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-            mma_step<bf16_t>(s[qt][kt], fkv[kt], fqv[qt]);
+          for (int r = 0; r < 4; ++r) {
+            const float v = s[kt][r] + *reinterpret_cast<const float*>(sm + toff[kt][r] + 900 * h);
+            s[kt][r] = v;
+            mx = fmaxf(mx, v);
           }
-        // ---- + B_rel + shift mask, softmax (exp2: log2 e folded into q and the tables)
-        // over the 64 keys (lane + lanes ^16, ^32, ^48)
+        mx = fmaxf(mx, __shfl_xor(mx, 16));
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        float sum = 0.f;
 #pragma unroll
-        for (int qt = 0; qt < NQT; ++qt) {
-          float mx = -INFINITY;
+        for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-          for (int kt = 0; kt < 4; ++kt)
+          for (int r = 0; r < 4; ++r) {
+            const float ex = __builtin_amdgcn_exp2f(s[kt][r] - mx);
+            s[kt][r] = ex;
+            sum += ex;
+          }
+        sum += __shfl_xor(sum, 16);
+        sum += __shfl_xor(sum, 32);
+        const float inv = __builtin_amdgcn_rcpf(sum);
+        uint4 pf[2];                                   // P^T key pairs (0,1), (2,3)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float v = s[qt][kt][r] + *reinterpret_cast<const float*>(sm + toff[qt][kt][r] + 900 * h);
-              s[qt][kt][r] = v;
-              mx = fmaxf(mx, v);
+        for (int kp = 0; kp < 2; ++kp) {
+          f32x4 a0 = s[2 * kp], a1 = s[2 * kp + 1];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) { a0[r] *= inv; a1[r] *= inv; }
+          pf[kp] = cat2(pk4(a0), pk4(a1));
+        }
+        // ---- O^T = V^T P^T over this head's channel tiles (tile 1: its 8 rows only)
+#pragma unroll
+        for (int ci = 0; ci < 2; ++ci) {
+          const int c = hh + ci;
+#pragma unroll
+          for (int kp = 0; kp < 2; ++kp) {
+            uint4 vf = *reinterpret_cast<const uint4*>(xv + (c * 2 + kp) * 1024 + lane * 16);
+            if (c == 1) {
+              const uint32_t keep = hh == 0 ? lo8 : ~lo8;
+              vf.x &= keep; vf.y &= keep; vf.z &= keep; vf.w &= keep;
             }
-          mx = fmaxf(mx, __shfl_xor(mx, 16));
-          mx = fmaxf(mx, __shfl_xor(mx, 32));
-          float sum = 0.f;
-#pragma unroll
-          for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float ex = __builtin_amdgcn_exp2f(s[qt][kt][r] - mx);
-              s[qt][kt][r] = ex;
-              sum += ex;
-            }
-          sum += __shfl_xor(sum, 16);
-          sum += __shfl_xor(sum, 32);
-          const float inv = __builtin_amdgcn_rcpf(sum);
-          const int qi = 16 * qt + n;
-#pragma unroll
-          for (int kt = 0; kt < 4; ++kt) {
-            const int k0 = 16 * kt + 4 * qq;
-            *reinterpret_cast<uint2*>(Pw + qi * 128 + (((k0 >> 3) ^ (qi & 7)) << 4) + 2 * (k0 & 7)) =
-                make_uint2(pack_bf16x2(s[qt][kt][0] * inv, s[qt][kt][1] * inv),
-                           pack_bf16x2(s[qt][kt][2] * inv, s[qt][kt][3] * inv));
+            mma_step<bf16_t>(o[c], vf, pf[kp]);
           }
         }
-        // ---- O^T = V^T P^T: head channels (rows, 24..31 zero) x this wave's queries
-        f32x4 o[2][NQT];
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-          for (int qt = 0; qt < NQT; ++qt) o[ct][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          uint4 fa[2], fb[NQT];
-#pragma unroll
-          for (int ct = 0; ct < 2; ++ct) {
-            const int ch = 16 * ct + n;
-            fa[ct] = *reinterpret_cast<const uint4*>(
-                sm + L_VT + (hh * 32 + ch) * 256 + (((8 * win + 4 * ks + qq) ^ (ch & 15)) << 4));
-          }
-#pragma unroll
-          for (int qt = 0; qt < NQT; ++qt) {
-            const int qi = 16 * qt + n;
-            fb[qt] = *reinterpret_cast<const uint4*>(Pw + qi * 128 + (((4 * ks + qq) ^ (qi & 7)) << 4));
-          }
-#pragma unroll
-          for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-            for (int qt = 0; qt < NQT; ++qt) mma_step<bf16_t>(o[ct][qt], fa[ct], fb[qt]);
-        }
-        // O (token rows of 32 channels, bf16) over this wave's P: every P read above has
-        // completed (its MFMAs produced o)
-#pragma unroll
-        for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-          for (int qt = 0; qt < NQT; ++qt) {
-            const int tok = 16 * qt + n, c0 = 16 * ct + 4 * qq;
-            *reinterpret_cast<uint2*>(Pw + tok * 64 + (((c0 >> 3) ^ ((tok >> 1) & 3)) << 4) + 2 * (c0 & 7)) =
-                make_uint2(pack_bf16x2(o[ct][qt][0], o[ct][qt][1]),
-                           pack_bf16x2(o[ct][qt][2], o[ct][qt][3]));
-          }
       }
-      // ---- WP(h) landed everywhere (WQ(p+1), issued after it, may still be in flight)
-      if (hh == 0 && p < 3) wb_wait_vm<WQ_W>();
-      else wb_wait_vm<0>();
-      __syncthreads();
-      if (h < HEADS - 1) dma_wp(h + 1);                // buffer (h+1)&1: proj(h-1) is done
-      if (act) {
-        // ---- out^T += Wproj[:, head h] O^T
-        uint4 fo[NQT];
+      if ((p & 1) == 0) {
 #pragma unroll
-        for (int qt = 0; qt < NQT; ++qt)
-          fo[qt] = *reinterpret_cast<const uint4*>(Pw + (16 * qt + n) * 64 + swz64);
+        for (int c = 0; c < 3; ++c) prevO[c] = pk4(o[c]);
+      } else {
+        // ---- out^T += Wp[:, 96u .. 96u + 95] O^T (pairs 2u, 2u+1: six channel tiles as
+        // three k-steps of tile pairs)
+        uint4 ob[3];
+        ob[0] = cat2(prevO[0], prevO[1]);
+        ob[1] = cat2(prevO[2], pk4(o[0]));
+        ob[2] = cat2(pk4(o[1]), pk4(o[2]));
 #pragma unroll
-        for (int m = 0; m < 12; ++m) {
-          const uint4 fw = *reinterpret_cast<const uint4*>(
-              sm + L_WP + (h & 1) * WPF * 1024 + m * 1024 + lane * 16);
+        for (int m = 0; m < 12; ++m)
 #pragma unroll
-          for (int qt = 0; qt < NQT; ++qt) mma_step<bf16_t>(acc[m][qt], fw, fo[qt]);
-        }
+          for (int s = 0; s < 3; ++s) {
+            const uint4 wf = *reinterpret_cast<const uint4*>(sm + L_WP + (m * 3 + s) * 1024 + lane * 16);
+            mma_step<bf16_t>(acc[m], wf, ob[s]);
+          }
       }
     }
   }
 
   // ---- epilogue: out = x + proj + b (active window) or x (MASKSEL, :236-240)
   const float* bp = reinterpret_cast<const float*>(sm + L_BQ);
+  const int pix = pix_s[tok0 + n];
+  if (pix < 0) return;
+  const bf16_t* xr = a.x + (long long)pix * a.ldx;
+  bf16_t* orow = a.out + (long long)pix * a.ldo;
+  uint2 xv4[12];
 #pragma unroll
-  for (int qt = 0; qt < NQT; ++qt) {
-    const int pix = pix_s[tok0 + 16 * qt + n];
-    if (pix < 0) continue;
-    const bf16_t* xr = a.x + (long long)pix * a.ldx;
-    bf16_t* orow = a.out + (long long)pix * a.ldo;
+  for (int m = 0; m < 12; ++m) xv4[m] = *reinterpret_cast<const uint2*>(xr + 16 * m + 4 * qq);
 #pragma unroll
-    for (int m = 0; m < 12; ++m) {
-      const int c0 = 16 * m + 4 * qq;
-      const uint2 xv = *reinterpret_cast<const uint2*>(xr + c0);
-      float v[4] = {bf2f(xv.x & 0xFFFF), bf2f(xv.x >> 16), bf2f(xv.y & 0xFFFF), bf2f(xv.y >> 16)};
-      if (act) {
+  for (int m = 0; m < 12; ++m) {
+    const int c0 = 16 * m + 4 * qq;
+    const uint2 xv = xv4[m];
+    float v[4] = {bf2f(xv.x & 0xFFFF), bf2f(xv.x >> 16), bf2f(xv.y & 0xFFFF), bf2f(xv.y >> 16)};
+    if (act) {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] += acc[m][qt][r] + bp[c0 + r];
-      }
-      *reinterpret_cast<uint2*>(orow + c0) =
-          make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      for (int r = 0; r < 4; ++r) v[r] += acc[m][r] + bp[c0 + r];
     }
+    *reinterpret_cast<uint2*>(orow + c0) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
   }
 }
 
@@ -448,27 +401,20 @@ extern "C" int rgbac_winattn_block(int batch, int h, int w, int shift, int maske
   RGBAC_REQUIRE(x != out, "out must not alias x");
   const long long windows = (long long)batch * (h / 8) * (w / 8);
   RGBAC_REQUIRE(windows < (1LL << 30), "too many windows");
+  RGBAC_REQUIRE((long long)batch * h * w < (1LL << 31), "pixel index must fit in 31 bits");
   WinBlockArgs d;
   d.batch = batch; d.H = h; d.W = w; d.shift = shift; d.masked = masked; d.scale = scale;
   d.x = reinterpret_cast<const bf16_t*>(x); d.ldx = ldx; d.alpha = alpha;
   d.wq = reinterpret_cast<const bf16_t*>(wq_packed); d.bqkv = bqkv;
   d.wp = reinterpret_cast<const bf16_t*>(wp_packed); d.bproj = bproj; d.table = table;
   d.out = reinterpret_cast<bf16_t*>(out); d.ldo = ldo;
-  static const int nqt = [] {
-    const char* e = getenv("RGBAC_WINBLOCK_NQT");      // 1: 8 waves (default), 2: 4 waves
-    return e && atoi(e) == 2 ? 2 : 1;
-  }();
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(winblock_kernel<1>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, wb::LDS);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(winblock_kernel<2>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(winblock_kernel),
                         hipFuncAttributeMaxDynamicSharedMemorySize, wb::LDS);
     attr = true;
   }
   const dim3 grid((int)((windows + 1) / 2));
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (nqt == 2) hipLaunchKernelGGL(winblock_kernel<2>, grid, dim3(256), wb::LDS, st, d);
-  else hipLaunchKernelGGL(winblock_kernel<1>, grid, dim3(512), wb::LDS, st, d);
+  hipLaunchKernelGGL(winblock_kernel, grid, dim3(512), wb::LDS, reinterpret_cast<hipStream_t>(stream), d);
   return check_launch("winblock_kernel");
 }

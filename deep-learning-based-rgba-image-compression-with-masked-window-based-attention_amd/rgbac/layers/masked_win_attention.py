@@ -117,7 +117,9 @@ class WindowAttention(nn.Module):
     def block_packs(self):
         """Fragment-major bf16 packs for rgbac_winattn_block, cached per parameter version:
         wq [4 pairs][54][64 lanes][8] (q | k | v of heads 2p, 2p+1: 3 x 3 16-row tiles x 6
-        32-deep k-steps), wp [8 heads][12][64][8] (proj columns of a head, padded 24 -> 32)."""
+        32-deep k-steps), wp [2][12][3][64][8]: proj input channels 96u .. 96u + 95 (head
+        pairs 2u, 2u + 1) as 3 k-steps in the kernel's accumulator-operand order -- element e
+        of lane l in k-step s is input channel 96u + 32s + 4(l >> 4) + (e & 3) + 16(e >> 2)."""
         ps = (self.qkv.weight, self.qkv.bias, self.proj.weight, self.proj.bias,
               self.relative_position_bias_table)
         key = (rt.PARAM_GEN,) + tuple((t._version, t.data_ptr()) for t in ps)
@@ -133,13 +135,14 @@ class WindowAttention(nn.Module):
                 rowb, colb = torch.broadcast_tensors(row[..., None], col)
                 wq = Wq[rowb, colb].to(torch.bfloat16).contiguous()
                 Wp = self.proj.weight.float()
-                h, m = ar(8)[:, None, None, None], ar(12)[None, :, None, None]
-                l4, e = ar(64)[None, None, :, None], ar(8)[None, None, None, :]
-                rowp = (16 * m + (l4 & 15)).expand(8, 12, 64, 8)
-                hc = (8 * (l4 >> 4) + e).expand(8, 12, 64, 8)
-                colp = 24 * h + hc.clamp(max=23)
-                wp = torch.where(hc < 24, Wp[rowp, colp], torch.zeros((), device=dev))
-                wp = wp.to(torch.bfloat16).contiguous()
+                u = ar(2).view(2, 1, 1, 1, 1)
+                m = ar(12).view(1, 12, 1, 1, 1)
+                s = ar(3).view(1, 1, 3, 1, 1)
+                l4 = ar(64).view(1, 1, 1, 64, 1)
+                e = ar(8).view(1, 1, 1, 1, 8)
+                rowp = (16 * m + (l4 & 15)).expand(2, 12, 3, 64, 8)
+                colp = (96 * u + 32 * s + 4 * (l4 >> 4) + (e & 3) + 16 * (e >> 2)).expand(2, 12, 3, 64, 8)
+                wp = Wp[rowp, colp].to(torch.bfloat16).contiguous()
                 bqkv = self.qkv.bias.float().contiguous()
                 bproj = self.proj.bias.float().contiguous()
                 table = self.relative_position_bias_table.float().contiguous()
