@@ -383,6 +383,211 @@ __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlockArgs a) 
   }
 }
 
+
+// ---------------------------------------------------------------------------------------
+// The same block at ws 4, C 80, 8 heads of 10 (the 1/16-resolution attention blocks,
+// TransformRGB.py:63,80): a window is 16 tokens = ONE 16-token tile, so each wave owns a
+// whole window and nothing crosses waves.  q^T, k^T (channels x tokens) and v (tokens x
+// channels) come from 16x16x32 MFMAs over x; every later product sums over 16 keys or over
+// one 16-channel accumulator tile, so it takes its operands straight from the accumulators
+// with v_mfma_f32_16x16x16_bf16 (lane l: row l & 15, k = 4(l >> 4) + j = the accumulator's
+// rows 4(l >> 4) + r):
+//   S^T  = sum over the 1-2 channel tiles a head touches of K_t Q_t^T  (q masked to the head's
+//          10 channels)
+//   P^T  = softmax over the 16 keys (4 lanes apart: two xor-shuffles)
+//   O^T_t += V_t^T P^T  (rows of tile t outside the head masked)
+//   out^T = Wp O^T  (5 x 5 fragments)
+// One workgroup = NW windows; weights (46 KiB qkv + 12.5 KiB proj, fragment-major) are
+// LDS-DMA'd once per workgroup; one barrier.
+namespace wb4 {
+constexpr int WS = 4, C = 80, HEADS = 8, DH = 10;
+constexpr int WQF = 45;                                // 15 m-tiles x 3 k-steps, 1 KiB each
+constexpr int WPP = 13;                                // proj: 25 x 512 B, DMA'd as 13 KiB
+constexpr int NPIECE = WQF + WPP;
+constexpr int L_WQ = 0;
+constexpr int L_WP = WQF * 1024;                       // 46080
+constexpr int L_TB = L_WP + WPP * 1024;                // 59392: bias [2][8 heads][49] fp32
+constexpr int LDS = L_TB + 2 * 8 * 49 * 4;             // 62528
+}  // namespace wb4
+
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+__device__ __forceinline__ void mma16(f32x4& acc, uint2 a, uint2 b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s16x4, a),
+                                                  __builtin_bit_cast(s16x4, b), acc, 0, 0, 0);
+}
+
+template <int NW>
+__global__ void __launch_bounds__(64 * NW) winblock4_kernel(const WinBlockArgs a) {
+  using namespace wb4;
+  constexpr float LOG2E = 1.4426950408889634f;
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = lane & 15, qq = lane >> 4;
+  const int H = a.H, W = a.W, shift = a.shift;
+  const int nwx = W / WS, nwy = H / WS;
+  const int total = a.batch * nwx * nwy;
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) void*)sm;
+
+  // ---- weights: NPIECE 1-KiB LDS-DMA pieces dealt over the waves
+  for (int f = w; f < NPIECE; f += NW) {
+    const bf16_t* src = f < WQF ? a.wq + ((size_t)f * 64 + lane) * 8
+                                : a.wp + ((size_t)(f - WQF) * 64 + lane) * 8;
+    wb_dma16(src, lds0 + f * 1024);
+  }
+  float* tb = reinterpret_cast<float*>(sm + L_TB);
+  for (int e = tid; e < 49 * 8; e += 64 * NW) {        // table [49][8] -> [var][8][49]
+    const int idx = e >> 3, hd = e & 7;
+    const float v = a.table[e];
+    tb[hd * 49 + idx] = v * LOG2E;
+    tb[8 * 49 + hd * 49 + idx] = (v + -100.0f) * LOG2E;
+  }
+
+  // ---- this wave's window: token n -> pixel (cyclic shift folded in)
+  const int gw = blockIdx.x * NW + w;
+  const bool live = gw < total;
+  int wy = 0, wx = 0, b = 0;
+  if (live) {
+    b = gw / (nwx * nwy);
+    const int rem = gw - b * nwx * nwy;
+    wy = rem / nwx; wx = rem - wy * nwx;
+  }
+  auto rid_of = [&](int t) {
+    const int r = wy * WS + (t >> 2), c = wx * WS + (t & 3);
+    return 3 * (r < H - WS ? 0 : (r < H - shift ? 1 : 2)) + (c < W - WS ? 0 : (c < W - shift ? 1 : 2));
+  };
+  int pix = 0;
+  {
+    int oy = wy * WS + (n >> 2) + shift; if (oy >= H) oy -= H;
+    int ox = wx * WS + (n & 3) + shift; if (ox >= W) ox -= W;
+    pix = (b * H + oy) * W + ox;
+  }
+  // remove_zero_windows (:38-47): the window's 16 alpha values, wave-uniform verdict
+  const bool act = live && (!a.masked || __any(a.alpha[pix] != 0.0f));
+  const bf16_t* xr = a.x + (long long)pix * a.ldx;
+  uint4 X[3];
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks)
+    X[ks] = (act && (ks < 2 || qq < 2)) ? *reinterpret_cast<const uint4*>(xr + 32 * ks + 8 * qq)
+                                       : make_uint4(0, 0, 0, 0);
+  // relative-position-bias offsets of this lane's S^T elements (key 4qq + r, query n)
+  int toff[4];
+  {
+    const int qrid = rid_of(n);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int jk = 4 * qq + r;
+      const int idx = ((n >> 2) - (jk >> 2) + 3) * 7 + ((n & 3) - (jk & 3) + 3);
+      const bool cut = shift > 0 && rid_of(jk) != qrid;
+      toff[r] = L_TB + (cut ? 8 * 49 * 4 : 0) + idx * 4;
+    }
+  }
+  wb_wait_all();
+  __syncthreads();
+  if (!live) return;
+  bf16_t* orow = a.out + (long long)pix * a.ldo;
+  if (!act) {                                          // transparent window: out = x
+    if (qq < 2) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k)
+        *reinterpret_cast<uint4*>(orow + 40 * qq + 8 * k) = *reinterpret_cast<const uint4*>(xr + 40 * qq + 8 * k);
+    }
+    return;
+  }
+
+  // ================= q^T, k^T (channels x tokens), v (tokens x channels)
+  f32x4 aq[5], ak[5], av[5];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) aq[t] = ak[t] = av[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 3; ++ks) {
+#pragma unroll
+    for (int t = 0; t < 5; ++t) {
+      const uint4 fq = *reinterpret_cast<const uint4*>(sm + L_WQ + (t * 3 + ks) * 1024 + lane * 16);
+      const uint4 fk = *reinterpret_cast<const uint4*>(sm + L_WQ + ((5 + t) * 3 + ks) * 1024 + lane * 16);
+      const uint4 fv = *reinterpret_cast<const uint4*>(sm + L_WQ + ((10 + t) * 3 + ks) * 1024 + lane * 16);
+      mma_step<bf16_t>(aq[t], fq, X[ks]);
+      mma_step<bf16_t>(ak[t], fk, X[ks]);
+      mma_step<bf16_t>(av[t], X[ks], fv);
+    }
+  }
+  const float qscale = a.scale * LOG2E;
+  uint2 k2[5], v2[5];
+  float qv[5][4];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) {
+    const float4 bq4 = *reinterpret_cast<const float4*>(a.bqkv + 16 * t + 4 * qq);
+    const float4 bk4 = *reinterpret_cast<const float4*>(a.bqkv + 80 + 16 * t + 4 * qq);
+    const float bv = a.bqkv[160 + 16 * t + n];
+    qv[t][0] = (aq[t][0] + bq4.x) * qscale; qv[t][1] = (aq[t][1] + bq4.y) * qscale;
+    qv[t][2] = (aq[t][2] + bq4.z) * qscale; qv[t][3] = (aq[t][3] + bq4.w) * qscale;
+    k2[t] = make_uint2(pack_bf16x2(ak[t][0] + bk4.x, ak[t][1] + bk4.y),
+                       pack_bf16x2(ak[t][2] + bk4.z, ak[t][3] + bk4.w));
+    v2[t] = make_uint2(pack_bf16x2(av[t][0] + bv, av[t][1] + bv), pack_bf16x2(av[t][2] + bv, av[t][3] + bv));
+  }
+
+  f32x4 o[5];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) o[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int h = 0; h < HEADS; ++h) {
+    const int c0 = DH * h, c1 = DH * h + DH;           // the head's channels [c0, c1)
+    const int t0 = c0 >> 4, t1 = (c1 - 1) >> 4;
+    f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = t0; t <= t1; ++t) {
+      float m4[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ch = 16 * t + 4 * qq + j;
+        m4[j] = (ch >= c0 && ch < c1) ? qv[t][j] : 0.0f;
+      }
+      mma16(s, k2[t], make_uint2(pack_bf16x2(m4[0], m4[1]), pack_bf16x2(m4[2], m4[3])));
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s[r] += *reinterpret_cast<const float*>(sm + toff[r] + 196 * h);
+      mx = fmaxf(mx, s[r]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 16));
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    float sum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      s[r] = __builtin_amdgcn_exp2f(s[r] - mx);
+      sum += s[r];
+    }
+    sum += __shfl_xor(sum, 16);
+    sum += __shfl_xor(sum, 32);
+    const float inv = __builtin_amdgcn_rcpf(sum);
+    const uint2 pf = make_uint2(pack_bf16x2(s[0] * inv, s[1] * inv), pack_bf16x2(s[2] * inv, s[3] * inv));
+#pragma unroll
+    for (int t = t0; t <= t1; ++t) {
+      const int ch = 16 * t + n;                       // V^T row of this lane
+      const uint32_t keep = (ch >= c0 && ch < c1) ? 0xFFFFFFFFu : 0u;
+      mma16(o[t], make_uint2(v2[t].x & keep, v2[t].y & keep), pf);
+    }
+  }
+  // ================= out^T = Wp O^T, + b + x
+  uint2 ob[5];
+#pragma unroll
+  for (int t = 0; t < 5; ++t) ob[t] = pk4(o[t]);
+#pragma unroll
+  for (int m = 0; m < 5; ++m) {
+    f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < 5; ++kt)
+      mma16(acc, *reinterpret_cast<const uint2*>(sm + L_WP + (m * 5 + kt) * 512 + lane * 8), ob[kt]);
+    const int c0 = 16 * m + 4 * qq;
+    const float4 bp = *reinterpret_cast<const float4*>(a.bproj + c0);
+    const uint2 xv = *reinterpret_cast<const uint2*>(xr + c0);
+    const float v0 = bf2f(xv.x & 0xFFFF) + acc[0] + bp.x, v1 = bf2f(xv.x >> 16) + acc[1] + bp.y;
+    const float v2_ = bf2f(xv.y & 0xFFFF) + acc[2] + bp.z, v3 = bf2f(xv.y >> 16) + acc[3] + bp.w;
+    *reinterpret_cast<uint2*>(orow + c0) = make_uint2(pack_bf16x2(v0, v1), pack_bf16x2(v2_, v3));
+  }
+}
+
 }  // namespace rgbac
 
 using namespace rgbac;
@@ -417,4 +622,53 @@ extern "C" int rgbac_winattn_block(int batch, int h, int w, int shift, int maske
   const dim3 grid((int)((windows + 1) / 2));
   hipLaunchKernelGGL(winblock_kernel, grid, dim3(512), wb::LDS, reinterpret_cast<hipStream_t>(stream), d);
   return check_launch("winblock_kernel");
+}
+
+extern "C" int rgbac_winattn_block_ws4(int batch, int h, int w, int shift, int masked, float scale,
+                                       const void* x, int64_t ldx, const float* alpha,
+                                       const void* wq_packed, const float* bqkv,
+                                       const void* wp_packed, const float* bproj,
+                                       const float* table, void* out, int64_t ldo, void* stream) {
+  RGBAC_REQUIRE(batch > 0 && h > 0 && w > 0 && h % 4 == 0 && w % 4 == 0,
+                "H and W must be positive multiples of the window size 4");
+  RGBAC_REQUIRE(shift >= 0 && shift < 4, "0 <= shift < 4");
+  RGBAC_REQUIRE(x && out && wq_packed && bqkv && wp_packed && bproj && table, "null pointer");
+  RGBAC_REQUIRE(!masked || alpha, "masked attention needs alpha");
+  RGBAC_REQUIRE(ldx >= 80 && ldo >= 80 && ldx % 8 == 0 && ldo % 8 == 0, "strides");
+  RGBAC_REQUIRE(((uintptr_t)x % 16) == 0 && ((uintptr_t)out % 16) == 0 &&
+                    ((uintptr_t)bqkv % 16) == 0 && ((uintptr_t)bproj % 16) == 0, "16-byte alignment");
+  RGBAC_REQUIRE(x != out, "out must not alias x");
+  RGBAC_REQUIRE((long long)batch * h * w < (1LL << 31), "pixel index must fit in 31 bits");
+  const long long windows = (long long)batch * (h / 4) * (w / 4);
+  WinBlockArgs d;
+  d.batch = batch; d.H = h; d.W = w; d.shift = shift; d.masked = masked; d.scale = scale;
+  d.x = reinterpret_cast<const bf16_t*>(x); d.ldx = ldx; d.alpha = alpha;
+  d.wq = reinterpret_cast<const bf16_t*>(wq_packed); d.bqkv = bqkv;
+  d.wp = reinterpret_cast<const bf16_t*>(wp_packed); d.bproj = bproj; d.table = table;
+  d.out = reinterpret_cast<bf16_t*>(out); d.ldo = ldo;
+  static const int nw_env = [] {
+    const char* e = getenv("RGBAC_WINBLOCK4_NW");        // windows (waves) per workgroup
+    const int v = e ? atoi(e) : 0;
+    return v == 1 || v == 2 || v == 4 || v == 8 ? v : 0;
+  }();
+  // enough workgroups for every CU before more windows per weight fetch
+  const int nw = nw_env ? nw_env : (windows >= 2048 ? 4 : 2);
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(winblock4_kernel<1>), hipFuncAttributeMaxDynamicSharedMemorySize, wb4::LDS);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(winblock4_kernel<2>), hipFuncAttributeMaxDynamicSharedMemorySize, wb4::LDS);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(winblock4_kernel<4>), hipFuncAttributeMaxDynamicSharedMemorySize, wb4::LDS);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(winblock4_kernel<8>), hipFuncAttributeMaxDynamicSharedMemorySize, wb4::LDS);
+    attr = true;
+  }
+  const long long grid = (windows + nw - 1) / nw;
+  RGBAC_REQUIRE(grid < (1LL << 31), "too many windows");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  switch (nw) {
+    case 1: hipLaunchKernelGGL(winblock4_kernel<1>, dim3((unsigned)grid), dim3(64), wb4::LDS, st, d); break;
+    case 2: hipLaunchKernelGGL(winblock4_kernel<2>, dim3((unsigned)grid), dim3(128), wb4::LDS, st, d); break;
+    case 4: hipLaunchKernelGGL(winblock4_kernel<4>, dim3((unsigned)grid), dim3(256), wb4::LDS, st, d); break;
+    default: hipLaunchKernelGGL(winblock4_kernel<8>, dim3((unsigned)grid), dim3(512), wb4::LDS, st, d); break;
+  }
+  return check_launch("winblock4_kernel");
 }

@@ -119,6 +119,8 @@ SIGNATURES = {
                        _I64, _VP],
     "rgbac_winattn_block": [_I32, _I32, _I32, _I32, _I32, _F, _VP, _I64, _VP, _VP, _VP, _VP, _VP,
                             _VP, _VP, _I64, _VP],
+    "rgbac_winattn_block_ws4": [_I32, _I32, _I32, _I32, _I32, _F, _VP, _I64, _VP, _VP, _VP, _VP,
+                                _VP, _VP, _VP, _I64, _VP],
     "rgbac_rgba_augment": [_I32, _VP, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP],
     "rgbac_dse_block": [_I32, _I32, _I32, _I32, _I32, _F, _VP, _I64, _VP, _I64, _VP, _I32, _VP, _VP,
                         _I32, _VP, _VP, _I32, _VP, _VP, _I32, _VP, _VP, _I64, _VP],

@@ -115,11 +115,15 @@ class WindowAttention(nn.Module):
         return ent[1]
 
     def block_packs(self):
-        """Fragment-major bf16 packs for rgbac_winattn_block, cached per parameter version:
-        wq [4 pairs][54][64 lanes][8] (q | k | v of heads 2p, 2p+1: 3 x 3 16-row tiles x 6
-        32-deep k-steps), wp [2][12][3][64][8]: proj input channels 96u .. 96u + 95 (head
-        pairs 2u, 2u + 1) as 3 k-steps in the kernel's accumulator-operand order -- element e
-        of lane l in k-step s is input channel 96u + 32s + 4(l >> 4) + (e & 3) + 16(e >> 2)."""
+        """Fragment-major bf16 packs for the fused block kernels, cached per parameter version.
+        ws 8 / C 192 (rgbac_winattn_block): wq [4 pairs][54][64 lanes][8] (q | k | v of heads
+        2p, 2p+1: 3 x 3 16-row tiles x 6 32-deep k-steps), wp [2][12][3][64][8]: proj input
+        channels 96u .. 96u + 95 (head pairs 2u, 2u + 1) as 3 k-steps in the kernel's
+        accumulator-operand order -- element e of lane l in k-step s is input channel
+        96u + 32s + 4(l >> 4) + (e & 3) + 16(e >> 2).
+        ws 4 / C 80 (rgbac_winattn_block_ws4): wq [15 tiles][3 k-steps][64][8] (k >= 80 zero),
+        wp [5][5][64][4] 16x16x16 fragments (lane l: row 16m + (l & 15), input channels
+        16kt + 4(l >> 4) .. +3) in a 13 KiB buffer (the kernel DMAs whole KiB)."""
         ps = (self.qkv.weight, self.qkv.bias, self.proj.weight, self.proj.bias,
               self.relative_position_bias_table)
         key = (rt.PARAM_GEN,) + tuple((t._version, t.data_ptr()) for t in ps)
@@ -129,20 +133,36 @@ class WindowAttention(nn.Module):
                 dev = self.qkv.weight.device
                 ar = lambda k: torch.arange(k, device=dev)
                 Wq = self.qkv.weight.float()
-                p, f, l = ar(4)[:, None, None], ar(54)[None, :, None], ar(64)[None, None, :]
-                row = (f // 18) * 192 + 48 * p + 16 * ((f % 18) // 6) + (l & 15)
-                col = (32 * (f % 6) + 8 * (l >> 4))[..., None] + ar(8)
-                rowb, colb = torch.broadcast_tensors(row[..., None], col)
-                wq = Wq[rowb, colb].to(torch.bfloat16).contiguous()
                 Wp = self.proj.weight.float()
-                u = ar(2).view(2, 1, 1, 1, 1)
-                m = ar(12).view(1, 12, 1, 1, 1)
-                s = ar(3).view(1, 1, 3, 1, 1)
-                l4 = ar(64).view(1, 1, 1, 64, 1)
-                e = ar(8).view(1, 1, 1, 1, 8)
-                rowp = (16 * m + (l4 & 15)).expand(2, 12, 3, 64, 8)
-                colp = (96 * u + 32 * s + 4 * (l4 >> 4) + (e & 3) + 16 * (e >> 2)).expand(2, 12, 3, 64, 8)
-                wp = Wp[rowp, colp].to(torch.bfloat16).contiguous()
+                if self.window_size[0] == 8:
+                    p, f, l = ar(4)[:, None, None], ar(54)[None, :, None], ar(64)[None, None, :]
+                    row = (f // 18) * 192 + 48 * p + 16 * ((f % 18) // 6) + (l & 15)
+                    col = (32 * (f % 6) + 8 * (l >> 4))[..., None] + ar(8)
+                    rowb, colb = torch.broadcast_tensors(row[..., None], col)
+                    wq = Wq[rowb, colb].to(torch.bfloat16).contiguous()
+                    u = ar(2).view(2, 1, 1, 1, 1)
+                    m = ar(12).view(1, 12, 1, 1, 1)
+                    s = ar(3).view(1, 1, 3, 1, 1)
+                    l4 = ar(64).view(1, 1, 1, 64, 1)
+                    e = ar(8).view(1, 1, 1, 1, 8)
+                    rowp = (16 * m + (l4 & 15)).expand(2, 12, 3, 64, 8)
+                    colp = (96 * u + 32 * s + 4 * (l4 >> 4) + (e & 3) +
+                            16 * (e >> 2)).expand(2, 12, 3, 64, 8)
+                    wp = Wp[rowp, colp].to(torch.bfloat16).contiguous()
+                else:
+                    C = self.dim
+                    t, ks = ar(3 * C // 16).view(-1, 1, 1, 1), ar(3).view(1, 3, 1, 1)
+                    l4, e = ar(64).view(1, 1, 64, 1), ar(8).view(1, 1, 1, 8)
+                    row = (16 * t + (l4 & 15)).expand(-1, 3, 64, 8)
+                    col = (32 * ks + 8 * (l4 >> 4) + e).expand(3 * C // 16, 3, 64, 8)
+                    wq = torch.where(col < C, Wq[row, col.clamp(max=C - 1)],
+                                     torch.zeros((), device=dev)).to(torch.bfloat16).contiguous()
+                    m, kt = ar(C // 16).view(-1, 1, 1, 1), ar(C // 16).view(1, -1, 1, 1)
+                    l4, e = ar(64).view(1, 1, 64, 1), ar(4).view(1, 1, 1, 4)
+                    rowp = (16 * m + (l4 & 15)).expand(C // 16, C // 16, 64, 4)
+                    colp = (16 * kt + 4 * (l4 >> 4) + e).expand(C // 16, C // 16, 64, 4)
+                    wp = torch.zeros(13 * 512, dtype=torch.bfloat16, device=dev)
+                    wp[:rowp.numel()] = Wp[rowp, colp].to(torch.bfloat16).reshape(-1)
                 bqkv = self.qkv.bias.float().contiguous()
                 bproj = self.proj.bias.float().contiguous()
                 table = self.relative_position_bias_table.float().contiguous()
@@ -151,28 +171,36 @@ class WindowAttention(nn.Module):
         return ent[1]
 
     def block_fused_ok(self, x, residual, amask):
-        return (rt.WINBLOCK_FUSED and residual and amask is None and x.t.dtype == torch.bfloat16
-                and self.window_size[0] == 8 and self.dim == 192 and self.num_heads == 8
-                and self.qkv.bias is not None and x.ldc % 8 == 0 and x.H % 8 == 0
-                and x.W % 8 == 0)
+        if not (rt.WINBLOCK_FUSED and residual and amask is None and
+                x.t.dtype == torch.bfloat16 and self.num_heads == 8 and
+                self.qkv.bias is not None and x.ldc % 8 == 0):
+            return False
+        ws = self.window_size[0]
+        if ws == 8 and self.dim == 192:
+            return x.H % 8 == 0 and x.W % 8 == 0
+        return (ws == 4 and self.dim == 80 and x.H % 4 == 0 and x.W % 4 == 0 and
+                rt.WINBLOCK4_FUSED)
 
     def run_block(self, x, alpha, shift, masked):
         """The whole block (qkv + attention + proj + MASKSEL residual) as one
-        rgbac_winattn_block launch: x + attn(x) on active windows, x elsewhere."""
+        rgbac_winattn_block(_ws4) launch: x + attn(x) on active windows, x elsewhere."""
         wq, bqkv, wp, bproj, table = self.block_packs()
         out = rt.new_feat(x.B, x.H, x.W, x.C, x.t.dtype, x.t.device)
         if masked:
             alpha = alpha.contiguous().float()
         npix = x.B * x.H * x.W
-        rt.timed("winblock_kernel", 2.0 * npix * (576 * 192 + 2 * 64 * 192 + 192 * 192),
+        C, ws = self.dim, self.window_size[0]
+        fn = "rgbac_winattn_block" if ws == 8 else "rgbac_winattn_block_ws4"
+        kname = "winblock_kernel" if ws == 8 else "winblock4_kernel"
+        rt.timed(kname, 2.0 * npix * (3 * C * C + 2 * ws * ws * C + C * C),
                  2.0 * npix * 2 * x.ldc,
                  lambda: _lib.call(
-                     "rgbac_winattn_block", x.B, x.H, x.W, shift, 1 if masked else 0,
+                     fn, x.B, x.H, x.W, shift, 1 if masked else 0,
                      float(torch.tensor(self.scale, dtype=torch.float32)), x.ptr(), x.ldc,
                      _lib.ptr(alpha) if masked else None, wq.data_ptr(), bqkv.data_ptr(),
                      wp.data_ptr(), bproj.data_ptr(), table.data_ptr(), out.ptr(), out.ldc,
                      _lib.stream_ptr(x.t.device)),
-                 f"winblock_kernel ws8 C192 {x.H}x{x.W} B{x.B} shift{shift}")
+                 f"{kname} ws{ws} C{C} {x.H}x{x.W} B{x.B} shift{shift}")
         return out
 
     def run_nhwc(self, x, alpha, shift, masked, residual=True, amask=None):

@@ -251,6 +251,7 @@ FORCE = None              # (tile, ksplit) override, used by the tile/split-K te
 STEM_FUSED = os.environ.get("RGBAC_STEM_FUSED", "1") != "0"   # x1 + gdn1 as one launch (bf16)
 DSE_FUSED = os.environ.get("RGBAC_DSE_FUSED", "1") != "0"     # DSE as 3 fused launches (bf16)
 WINBLOCK_FUSED = os.environ.get("RGBAC_WINBLOCK", "1") != "0"  # ws-8 attention block, 1 launch
+WINBLOCK4_FUSED = os.environ.get("RGBAC_WINBLOCK4", "1") != "0"  # ws-4 / C-80 block, 1 launch
 
 
 def pick_cout_pad(cout):

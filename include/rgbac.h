@@ -432,13 +432,29 @@ int rgbac_rgba_augment(int batch, const void* descs, int out_h, int out_w, int a
  * partition / drop / reverse, the shifted-frame region mask and the relative position bias
  * are index math inside the kernel.  x, out: NHWC bf16 [batch][h][w][ld] (h, w multiples of
  * 8, out != x); alpha: fp32 [batch][h][w] (masked only); wq_packed / wp_packed: the
- * fragment-major qkv / proj packs of WindowAttention.block_packs(); bqkv [576], bproj [192]
+ * fragment-major qkv / proj packs of WindowAttention.block_packs() (wq [4][54][64][8]; wp
+ * [2][12][3][64][8] in the kernel's accumulator-operand k order: element e of lane l in
+ * k-step s of pair-pair u is input channel 96u + 32s + 4(l >> 4) + (e & 3) + 16(e >> 2));
+ * bqkv [576], bproj [192]
  * fp32; table: relative_position_bias_table [225][8] fp32.  Replaces the qkv GEMM,
  * rgbac_winattn_core_ex and the MASKSEL proj GEMM of one WinBasedAttention call. */
 int rgbac_winattn_block(int batch, int h, int w, int shift, int masked, float scale,
                         const void* x, int64_t ldx, const float* alpha, const void* wq_packed,
                         const float* bqkv, const void* wp_packed, const float* bproj,
                         const float* table, void* out, int64_t ldo, void* stream);
+
+/* The same block at window 4, C = 80, 8 heads of 10 (the 1/16-resolution attention blocks,
+ * layers/TransformRGB.py:63,80): one wave per window, every product after the qkv GEMM in
+ * registers.  h, w multiples of 4, shift < 4; x, out NHWC bf16 (ld >= 80, multiple of 8,
+ * 16-byte aligned); wq_packed [45][64][8] bf16 (15 16-row tiles of the qkv weight (q | k |
+ * v) x 3 32-deep k-steps, k >= 80 zero); wp_packed [5][5][64][4] bf16 (16x16x16 fragments of
+ * the proj weight: lane l holds row 16m + (l & 15), input channels 16kt + 4(l >> 4) .. +3),
+ * allocated to 13 KiB (zero tail); bqkv [240], bproj [80] fp32 (16-byte aligned); table
+ * [49][8] fp32. */
+int rgbac_winattn_block_ws4(int batch, int h, int w, int shift, int masked, float scale,
+                            const void* x, int64_t ldx, const float* alpha, const void* wq_packed,
+                            const float* bqkv, const void* wp_packed, const float* bproj,
+                            const float* table, void* out, int64_t ldo, void* stream);
 
 /* Fused DSE EnhancementBlock, bf16 NHWC (reference: layers/TransformRGB.py:16-49 --
  * EnhancementBlock.forward :23-28 and DSE.forward :39-49; the alpha codec's DSE,

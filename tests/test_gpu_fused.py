@@ -87,19 +87,22 @@ def test_dse_module_forward_uses_fused_path(device):
 # before its single rounding), so it is compared with the fp32 oracle at the unfused bf16
 # path's own error (within 1.5x, or 2e-2 of the output range), and with the unfused path at
 # 3 bf16 ulps of the output range on 99.5 % of the elements.
-@pytest.mark.parametrize("B,H,W,shift,masked", [(2, 64, 64, 4, True), (1, 32, 48, 0, False),
-                                                (1, 24, 40, 4, True), (2, 16, 16, 0, True),
-                                                (1, 8, 24, 0, True)])
-def test_winattn_block_fused_matches_unfused_and_oracle(device, B, H, W, shift, masked):
+@pytest.mark.parametrize("C,ws,B,H,W,shift,masked", [
+    (192, 8, 2, 64, 64, 4, True), (192, 8, 1, 32, 48, 0, False), (192, 8, 1, 24, 40, 4, True),
+    (192, 8, 2, 16, 16, 0, True), (192, 8, 1, 8, 24, 0, True),
+    # ws 4 / C 80 (rgbac_winattn_block_ws4): heads of 10 channels straddle the 16-row tiles
+    (80, 4, 2, 32, 32, 2, True), (80, 4, 1, 16, 24, 0, False), (80, 4, 1, 12, 20, 2, True),
+    (80, 4, 2, 8, 8, 0, True), (80, 4, 3, 4, 12, 0, True)])
+def test_winattn_block_fused_matches_unfused_and_oracle(device, C, ws, B, H, W, shift, masked):
     from rgbac import runtime as rt
     from rgbac.layers.masked_win_attention import WinBasedAttention
     torch.manual_seed(11)
-    m = WinBasedAttention(192, 8, 8, shift).cuda().eval()
+    m = WinBasedAttention(C, 8, ws, shift).cuda().eval()
     with torch.no_grad():
         m.attn.relative_position_bias_table.normal_(0, 0.5)   # make the bias matter
     m.masked = masked
     g = torch.Generator().manual_seed(12)
-    x = torch.randn((B, 192, H, W), generator=g)
+    x = torch.randn((B, C, H, W), generator=g)
     alpha = torch.ones((B, 1, H, W))
     if masked:
         alpha[:, :, : H // 2, : W // 2] = 0                  # some all-transparent windows
@@ -109,14 +112,14 @@ def test_winattn_block_fused_matches_unfused_and_oracle(device, B, H, W, shift, 
         f = rt.to_nhwc(xg, torch.bfloat16)
         assert m.attn.block_fused_ok(f, True, None)
         got = rt.to_nchw(m.nhwc(f, ag)).float().cpu()
-        old = rt.WINBLOCK_FUSED
-        rt.WINBLOCK_FUSED = False
+        old = (rt.WINBLOCK_FUSED, rt.WINBLOCK4_FUSED)
+        rt.WINBLOCK_FUSED = rt.WINBLOCK4_FUSED = False
         try:
             base = rt.to_nchw(m.nhwc(f, ag)).float().cpu()
         finally:
-            rt.WINBLOCK_FUSED = old
+            rt.WINBLOCK_FUSED, rt.WINBLOCK4_FUSED = old
     sd = {f"m.{k}": v.detach().cpu() for k, v in m.state_dict().items()}
-    want = ref.win_based_attention(x, alpha, sd, "m", 8, shift, heads=8,
+    want = ref.win_based_attention(x, alpha, sd, "m", ws, shift, heads=8,
                                    masked=masked).detach()
     scale = want.abs().max().item()
     e_got = (got - want).abs().max().item() / scale
@@ -127,9 +130,9 @@ def test_winattn_block_fused_matches_unfused_and_oracle(device, B, H, W, shift, 
           f"unfused err {e_base:.2e}, elements > 3 ulp apart {frac:.1e}")
     assert e_got <= max(1.5 * e_base, 2e-2), (e_got, e_base)
     assert frac <= 5e-3, frac
-    if masked and shift == 0 and H >= 32:                    # transparent windows: exactly x
+    if masked and shift == 0 and H >= 4 * ws:                # transparent windows: exactly x
         xb = rt.to_nchw(f).float().cpu()
-        assert torch.equal(got[:, :, 8:H // 2, 8:W // 2], xb[:, :, 8:H // 2, 8:W // 2])
+        assert torch.equal(got[:, :, ws:H // 2, ws:W // 2], xb[:, :, ws:H // 2, ws:W // 2])
 
 
 # ---------------------------------------------------------------------------------------
