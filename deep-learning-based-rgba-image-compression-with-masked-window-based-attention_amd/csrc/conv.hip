@@ -1755,8 +1755,6 @@ __global__ void __launch_bounds__(512, 4) conv_pw_kernel(const ConvArgsDev args)
     }
   }
   for (int e = tid; e < BN; e += 64 * NW) bl[e] = (g.bias && e < g.cout) ? g.bias[e] : 0.0f;
-  wait_vm<0>();
-  __syncthreads();
 
   const int Mtot = s.M, act = s.act;
   const int ld = (int)g.sld0;
@@ -1766,7 +1764,6 @@ __global__ void __launch_bounds__(512, 4) conv_pw_kernel(const ConvArgsDev args)
   const int ntile = (Mtot + 15) / 16;
   const int tstride = gridDim.x * NW;
   int tile = blockIdx.x * NW + wave;
-  if (tile >= ntile) return;
 
 #define PWW_LOAD(dst, st, rowp_, valid_)                                                      \
   do {                                                                                        \
@@ -1775,6 +1772,8 @@ __global__ void __launch_bounds__(512, 4) conv_pw_kernel(const ConvArgsDev args)
     dst = *p_;                                                                                \
   } while (0)
 
+  // the first tile's input fragments are requested beside the weight panel, so the two
+  // memory latencies overlap (one wait for both)
   uint4 bv[NKS];
   {
     const int m = tile * 16 + fr;
@@ -1783,6 +1782,9 @@ __global__ void __launch_bounds__(512, 4) conv_pw_kernel(const ConvArgsDev args)
 #pragma unroll
     for (int st = 0; st < NKS; ++st) PWW_LOAD(bv[st], st, rowp, valid);
   }
+  wait_vm<0>();
+  __syncthreads();
+  if (tile >= ntile) return;
   const bf16_t* const R1 = reinterpret_cast<const bf16_t*>(g.res1);
   const int cout = g.cout;
   for (; tile < ntile; tile += tstride) {

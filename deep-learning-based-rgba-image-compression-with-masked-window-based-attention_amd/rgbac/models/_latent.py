@@ -66,15 +66,20 @@ def _musigma_pack(mconv, sconv, dtype, cin):
     return ent[1]
 
 
-# bf16 inference: the latent-means/scales half of every slice's first cc / lrp conv is
-# computed up front by three grouped launches on a side stream (the convs are linear in
-# their input channels: conv([means, y_hat_<i]) = conv_means(means) + conv_yhat(y_hat_<i)),
-# overlapping the latency-bound slice chain; the chain's first convs then only read the
-# y_hat channels (K = 9 * 8i instead of 9 * (80 + 8i)) and add the precomputed partial in
-# their epilogue (res0).  fp32 parity mode keeps the reference's single-conv summation.
-# Off by default: measured 156 vs 166 MPix/s on config 2 -- the chain's first convs stay
-# launch-bound at K = 9 * 8i, while the 30 precompute GEMMs (3.4 GFLOP) compete for the CUs.
-PRECOMPUTE = os.environ.get("RGBAC_SLICE_PRECOMPUTE", "0") == "1"
+# bf16 inference: the latent-means/scales half of a slice's first cc / lrp conv can be
+# computed on a side stream (the convs are linear in their input channels:
+# conv([means, y_hat_<i]) = conv_means(means) + conv_yhat(y_hat_<i)), overlapping the
+# latency-bound slice chain; the chain's first convs then only read the y_hat channels and add
+# the precomputed partial in their epilogue (res0).  fp32 parity mode keeps the reference's
+# single-conv summation.  Modes (RGBAC_SLICE_PRECOMPUTE):
+#   "all"  every slice (round 1: 156 vs 166 MPix/s -- the chain's first convs stay
+#          launch-bound at K = 9 * 8i, while 30 precompute GEMMs compete for the CUs);
+#   "tail" only the slices >= max_support_slices: their stacks run as ONE wide wave after the
+#          sequential slices, whose latency-bound launches leave most CUs idle -- the side
+#          stream fills them with the means half of the wide wave's cc1 (g10) and lrp1 (g5)
+#          convs (2/3 of their K), so the wide wave's own first convs shrink to the y_hat part.
+PRECOMPUTE = {"1": "all", "all": "all", "tail": "tail"}.get(
+    os.environ.get("RGBAC_SLICE_PRECOMPUTE", "0"), None)
 _SIDE = {}
 
 
@@ -134,42 +139,64 @@ def latent_path(model, y, training=False, noise_z=None, noise_y=None, debug=None
     if ns > msup:
         waves.append(list(range(msup, ns)))
     Cm = means.C
-    pre_ok = (PRECOMPUTE and not training and debug is None and dt == torch.bfloat16 and
-              ns > 1 and not torch.is_grad_enabled())
+    pre_ok = (PRECOMPUTE is not None and not training and debug is None and
+              dt == torch.bfloat16 and ns > 1 and not torch.is_grad_enabled())
+    # slices whose first convs read precomputed partials: cc from p0c, lrp from p0l
+    p0c, p0l = (1, 0) if PRECOMPUTE == "all" else (msup, msup)
+    if pre_ok and PRECOMPUTE == "tail" and ns <= msup:
+        pre_ok = False
     if pre_ok:
         main = torch.cuda.current_stream(dev)
         side = _side_stream(dev)
         side.wait_stream(main)
         Wc = model.cc_mean_transforms[0][0].out_channels
         Wl = model.lrp_transforms[0][0].out_channels
-        Plrp = rt.new_feat(B, h, w, ns * Wl, dt, dev)
-        Pm = rt.new_feat(B, h, w, (ns - 1) * Wc, dt, dev)
-        Ps = rt.new_feat(B, h, w, (ns - 1) * Wc, dt, dev)
+        Plrp = rt.new_feat(B, h, w, (ns - p0l) * Wl, dt, dev)
+        Pm = rt.new_feat(B, h, w, (ns - p0c) * Wc, dt, dev)
+        Ps = rt.new_feat(B, h, w, (ns - p0c) * Wc, dt, dev)
         for f in (Plrp, Pm, Ps):
             f.t.record_stream(side)
         ev_lrp, ev_cc = torch.cuda.Event(), torch.cuda.Event()
         with torch.cuda.stream(side):
-            rt.launch([_part_prepare(model.lrp_transforms[i][0], [means.src()], 0, Cm, True,
-                                     out=Plrp, out_coff=Wl * i) for i in range(ns)])
-            ev_lrp.record(side)
-            rt.launch([_part_prepare(model.cc_mean_transforms[i][0], [means.src()], 0, Cm, True,
-                                     out=Pm, out_coff=Wc * (i - 1)) for i in range(1, ns)])
-            rt.launch([_part_prepare(model.cc_scale_transforms[i][0], [scales.src()], 0, Cm,
-                                     True, out=Ps, out_coff=Wc * (i - 1)) for i in range(1, ns)])
-            ev_cc.record(side)
+            if PRECOMPUTE == "tail":
+                # the wide wave's cc1 partials first (it needs them first), mean and scale
+                # stacks as one grouped launch
+                rt.launch([_part_prepare(model.cc_mean_transforms[i][0], [means.src()], 0, Cm,
+                                         True, out=Pm, out_coff=Wc * (i - p0c))
+                           for i in range(p0c, ns)] +
+                          [_part_prepare(model.cc_scale_transforms[i][0], [scales.src()], 0, Cm,
+                                         True, out=Ps, out_coff=Wc * (i - p0c))
+                           for i in range(p0c, ns)])
+                ev_cc.record(side)
+                rt.launch([_part_prepare(model.lrp_transforms[i][0], [means.src()], 0, Cm, True,
+                                         out=Plrp, out_coff=Wl * (i - p0l))
+                           for i in range(p0l, ns)])
+                ev_lrp.record(side)
+            else:
+                rt.launch([_part_prepare(model.lrp_transforms[i][0], [means.src()], 0, Cm, True,
+                                         out=Plrp, out_coff=Wl * (i - p0l))
+                           for i in range(p0l, ns)])
+                ev_lrp.record(side)
+                rt.launch([_part_prepare(model.cc_mean_transforms[i][0], [means.src()], 0, Cm,
+                                         True, out=Pm, out_coff=Wc * (i - p0c))
+                           for i in range(p0c, ns)])
+                rt.launch([_part_prepare(model.cc_scale_transforms[i][0], [scales.src()], 0, Cm,
+                                         True, out=Ps, out_coff=Wc * (i - p0c))
+                           for i in range(p0c, ns)])
+                ev_cc.record(side)
     waited = set()
     for wave in waves:
         sup = [cs * min(i, msup) for i in wave]
         # cc_mean / cc_scale stacks of every slice in the wave, as one grouped launch per layer
-        if pre_ok and wave[0] > 0:
+        if pre_ok and wave[0] >= p0c:
             if "cc" not in waited:
                 main.wait_event(ev_cc)
                 waited.add("cc")
             t1 = rt.launch(
                 [_part_prepare(model.cc_mean_transforms[i][0], [YH.src(0, n)], Cm, Cm + n, False,
-                               act="gelu", res0=(Pm, Wc * (i - 1))) for i, n in zip(wave, sup)] +
+                               act="gelu", res0=(Pm, Wc * (i - p0c))) for i, n in zip(wave, sup)] +
                 [_part_prepare(model.cc_scale_transforms[i][0], [YH.src(0, n)], Cm, Cm + n,
-                               False, act="gelu", res0=(Ps, Wc * (i - 1)))
+                               False, act="gelu", res0=(Ps, Wc * (i - p0c)))
                  for i, n in zip(wave, sup)])
         else:
             t1 = rt.launch(
@@ -211,13 +238,13 @@ def latent_path(model, y, training=False, noise_z=None, noise_y=None, debug=None
                                                  out=rt.new_feat(B, h, w, 2 * cs, dt, dev))],
                                      force=gauss_choice)[0]
         # lrp stacks: y_hat_i = pre_i + 0.5 * tanh(lrp([means, y_hat_<i, pre_i]))
-        if pre_ok:
+        if pre_ok and wave[0] >= p0l:
             if "lrp" not in waited:
                 main.wait_event(ev_lrp)
                 waited.add("lrp")
             l1 = rt.launch([_part_prepare(model.lrp_transforms[i][0],
                                           [YH.src(0, n), pres[j].src()], Cm, Cm + n + cs, False,
-                                          act="gelu", res0=(Plrp, Wl * i))
+                                          act="gelu", res0=(Plrp, Wl * (i - p0l)))
                             for j, (i, n) in enumerate(zip(wave, sup))])
         else:
             l1 = rt.launch([prep_conv(model.lrp_transforms[i][0],

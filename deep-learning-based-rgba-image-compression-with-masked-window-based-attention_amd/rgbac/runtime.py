@@ -615,7 +615,8 @@ def kernel_name(tile, preps):
         return f"conv_npatch_kernel<{2 if max(p.pk.cout for p in preps) > 16 else 1}>"
     if tile == TILE_PW:
         cin = max(p.a.cin_pad for p in preps)
-        return f"conv_pw_kernel<{4 if cin <= 64 else (8 if cin <= 128 else 12)}>"
+        # csrc/conv.hip launch_pw: 32-deep k-steps held in LDS (2 / 4 / 6)
+        return f"conv_pw_kernel<{2 if cin <= 64 else (4 if cin <= 128 else 6)}>"
     if tile == TILE_SMALLK:
         cout = max(p.pk.cout for p in preps)
         nt = 1 if cout <= 32 else (2 if cout <= 64 else 3)

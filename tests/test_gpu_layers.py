@@ -7,7 +7,8 @@ reference), and the alpha codec's training step (trainmask.py:165-198).
 
 Tolerances: fp32 layer outputs 2e-5 (max-abs relative), layer gradients 1e-4 norm-wise
 (exact-fp32 MFMA, different summation order); whole alpha-codec parameter gradients
-2e-2 norm-wise like the RGB codec's (tests/test_gpu_train.py)."""
+1e-3 norm-wise (measured max 3.6e-4 on the attention ResBlock convs of DecoderMask, median
+8e-7; the RGB codec's are held to 1e-4, tests/test_gpu_train.py)."""
 import pytest
 import torch
 

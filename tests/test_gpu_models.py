@@ -96,8 +96,9 @@ def test_mask_forward_fp32(device):
 
 def test_rgb_bf16_slice_precompute_matches(device, rgb_net):
     """bf16 inference with the side-stream precompute of the slice convs' latent-means/scales
-    half (rgbac.models._latent.PRECOMPUTE) and with the single-conv path: both within the
-    bf16 bar of the fp32 oracle, and the same bpp within bf16 noise."""
+    half (rgbac.models._latent.PRECOMPUTE: every slice, or only the wide tail wave) and with
+    the single-conv path: all within the bf16 bar of the fp32 oracle, and the same bpp within
+    bf16 noise."""
     from rgbac.models import _latent
     x, a = _inputs(4, 64, 64, seed=3)
     me = ref.supply_mask(a)
@@ -106,7 +107,7 @@ def test_rgb_bf16_slice_precompute_matches(device, rgb_net):
     net = rgb_net.to(device).set_compute_dtype(torch.bfloat16)
     outs, saved = {}, _latent.PRECOMPUTE
     try:
-        for flag in (False, True):
+        for flag in (None, "all", "tail"):
             _latent.PRECOMPUTE = flag
             with torch.no_grad():
                 outs[flag] = net(x.to(device), a.to(device), a.to(device),
@@ -117,8 +118,9 @@ def test_rgb_bf16_slice_precompute_matches(device, rgb_net):
     for got in outs.values():
         assert rel(got[0], want[0]) < 5e-2
         assert abs(got[2].item() - want[2].item()) < 0.05 * want[2].item()
-    b0, b1 = outs[False][2].item(), outs[True][2].item()
-    assert abs(b0 - b1) < 0.02 * b0
+    b0 = outs[None][2].item()
+    for flag in ("all", "tail"):
+        assert abs(b0 - outs[flag][2].item()) < 0.02 * b0, flag
 
 
 def test_rgb_forward_fp32_north_star_bar(device):

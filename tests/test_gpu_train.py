@@ -5,8 +5,8 @@ attention, entropy models and the whole RGB codec.
 
 Tolerances (relative to the reference gradient's max magnitude unless stated):
 fp32 single ops 1e-4 (exact-f32 MFMA, different summation order); bf16 single
-convs 4e-2; whole-model parameter gradients 2e-2 norm-wise (||g - g_ref|| /
-||g_ref||; 60-layer chains and rare round(y - mu) flips of the STE path).
+convs 4e-2; whole-model parameter gradients 1e-4 norm-wise (||g - g_ref|| /
+||g_ref||; measured max 5e-6 over every parameter of the RGB codec, median 3e-7).
 """
 import zlib
 
@@ -452,7 +452,7 @@ def test_rgb_train_step_grads(dtype):
             continue
         e = nrel(p.grad, r)
         errs.append((e, n))
-        if e > 1e-3:
+        if e > 1e-4:
             bad.append((n, e))
     errs.sort()
     print("rgb codec grads: median rel", errs[len(errs) // 2], "max", errs[-3:])
