@@ -17,8 +17,8 @@
 //   q^T, k^T = Wq|Wk X^T  (channels x tokens)        v = X Wv^T  (tokens x channels)
 //   S^T = K Q^T    per head: ONE k-step (channel tiles (0, 1) or (1, 2) of the pair, the other
 //                  head's 8 channels of tile 1 zeroed in q)
-//   P^T = softmax over keys (rows: 4 lanes apart, two xor-shuffles; exp2 with log2 e folded
-//                  into the q scale and the bias tables)
+//   P^T = softmax over keys (rows: 4 lanes apart, reduced by two permlane swaps; exp2 with
+//                  log2 e folded into the q scale and the bias tables)
 //   O^T = V^T P^T  (key-tile pairs as k-steps; tile 1's rows masked per head)
 //   out^T += Wp O^T every two head pairs (3 k-steps of O^T tile pairs; the proj weights are
 //                  packed in that permuted k order on the host)
@@ -81,6 +81,27 @@ __device__ __forceinline__ void wb_dma16(const void* src, uint32_t lds) {
       : "memory");
 }
 __device__ __forceinline__ void wb_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Reductions over the lane pairs l ^ 16 and l ^ 32 without an LDS round trip
+// (v_permlane16_swap / v_permlane32_swap, gfx950): with the same value in both operands, the
+// two results hold the pair's two values in the same order on both lanes, so op(r0, r1) is the
+// pair's reduction, bit-identical on both lanes.
+__device__ __forceinline__ float pair16_max(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float pair32_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float pair16_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float pair32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
 
 __device__ __forceinline__ uint2 pk4(const f32x4& v) {
   return make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
@@ -303,8 +324,8 @@ __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlockArgs a) 
             s[kt][r] = v;
             mx = fmaxf(mx, v);
           }
-        mx = fmaxf(mx, __shfl_xor(mx, 16));
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        mx = pair16_max(mx);
+        mx = pair32_max(mx);
         float sum = 0.f;
 #pragma unroll
         for (int kt = 0; kt < 4; ++kt)
@@ -314,8 +335,8 @@ __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlockArgs a) 
             s[kt][r] = ex;
             sum += ex;
           }
-        sum += __shfl_xor(sum, 16);
-        sum += __shfl_xor(sum, 32);
+        sum = pair16_sum(sum);
+        sum = pair32_sum(sum);
         const float inv = __builtin_amdgcn_rcpf(sum);
         uint4 pf[2];                                   // P^T key pairs (0,1), (2,3)
 #pragma unroll
@@ -550,16 +571,16 @@ __global__ void __launch_bounds__(64 * NW) winblock4_kernel(const WinBlockArgs a
       s[r] += *reinterpret_cast<const float*>(sm + toff[r] + 196 * h);
       mx = fmaxf(mx, s[r]);
     }
-    mx = fmaxf(mx, __shfl_xor(mx, 16));
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    mx = pair16_max(mx);
+    mx = pair32_max(mx);
     float sum = 0.f;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       s[r] = __builtin_amdgcn_exp2f(s[r] - mx);
       sum += s[r];
     }
-    sum += __shfl_xor(sum, 16);
-    sum += __shfl_xor(sum, 32);
+    sum = pair16_sum(sum);
+    sum = pair32_sum(sum);
     const float inv = __builtin_amdgcn_rcpf(sum);
     const uint2 pf = make_uint2(pack_bf16x2(s[0] * inv, s[1] * inv), pack_bf16x2(s[2] * inv, s[3] * inv));
 #pragma unroll

@@ -117,7 +117,9 @@ def dse_fused(dse, x, only=None):
     packs = [(rt.packed(e.conv1, dt, c32), rt.packed(e.conv2, dt, c32))
              for e in (dse.enh1, dse.enh2, dse.enh3)]
     slope = _act_of(dse.enh1.relu)[1]
-    out = rt.new_feat(x.B, x.H, x.W, x.C, dt, dev)
+    # block 3 writes the x.C real channels; every consumer of the DSE output (mse_partial,
+    # nhwc_to_nchw) reads only those, so the pad channels are not zero-filled
+    out = rt.new_feat(x.B, x.H, x.W, x.C, dt, dev, zero=False)
     t = None
     st = rt._lib.stream_ptr(dev)
     npx = x.B * x.H * x.W
@@ -232,7 +234,14 @@ class Synthesis_transform(nn.Module):
         t = self.igdn2.nhwc(run_conv(self.x2, [t.src()]))
         t = self.attention2.nhwc(t, md2)
         t = self.igdn3.nhwc(run_conv(self.x3, [t.src()]))
-        t = run_conv(self.x4, [t.src()])
+        # x4's 3-channel output (ldc 8): the fused DSE reads only its real channels (channel 7
+        # carries the kernel's in-image mark), so it skips the zero fill of the pad channels
+        # (a 16.8 MB memset at 256^2 B8); any other consumer gets them zeroed
+        x4o = rt.new_feat(t.B, 2 * t.H, 2 * t.W, self.x4.out_channels, t.t.dtype, t.t.device,
+                          zero=False)
+        if not dse_fused_ok(self.dse, x4o):
+            x4o.t.zero_()
+        t = run_conv(self.x4, [t.src()], out=x4o)
         return self.dse.nhwc(t)
 
     def forward(self, input, reconmask, md1, md2, md3, md4):
