@@ -25,8 +25,9 @@
 // Only k^T and v cross waves (the four token tiles of a window share the keys): each wave
 // stores its k^T / v fragments to LDS once per head pair (14 KiB per window) and reads the
 // window's.  Weights are pre-packed fragment-major (1 KiB per 16 rows x 32 k) and streamed
-// into LDS by LDS-DMA one pair ahead, waited on at the pair's barrier.  Two barriers per
-// head pair (exchange visible / exchange free), nine in all.
+// into LDS by LDS-DMA one pair ahead, waited on at the pair's barrier (counted vmcnt where a
+// younger stream may stay in flight).  Two barriers per head pair (exchange visible /
+// exchange free), nine in all.
 //
 // MFMAs per 16 tokens: 54 x 4 (qkv) + 8 x (4 + 4) (scores, PV) + 36 x 2 (proj) = 352.
 //
@@ -81,6 +82,10 @@ __device__ __forceinline__ void wb_dma16(const void* src, uint32_t lds) {
       : "memory");
 }
 __device__ __forceinline__ void wb_wait_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+template <int N>
+__device__ __forceinline__ void wb_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
 
 // Reductions over the lane pairs l ^ 16 and l ^ 32 without an LDS round trip
 // (v_permlane16_swap / v_permlane32_swap, gfx950): with the same value in both operands, the
@@ -108,6 +113,21 @@ __device__ __forceinline__ uint2 pk4(const f32x4& v) {
 }
 __device__ __forceinline__ uint4 cat2(uint2 lo, uint2 hi) { return make_uint4(lo.x, lo.y, hi.x, hi.y); }
 
+#ifdef RGBAC_WB_TIMING
+// probe builds only (tools/winblock_stage_probe.py): per-workgroup phase stamps of wave 0
+__device__ unsigned long long g_wb_t[8192][18];
+__device__ unsigned long long g_wb_w[8192][2];     // wall clock (100 MHz) at start / end
+#define WB_T(k)                                                                              \
+  do {                                                                                       \
+    const unsigned long long c_ = clock64();                                                 \
+    if (tid == 0 && blockIdx.x < 8192) g_wb_t[blockIdx.x][k] = c_;                           \
+    if (((k) == 0 || (k) == 17) && tid == 0 && blockIdx.x < 8192)                            \
+      g_wb_w[blockIdx.x][(k) == 17] = wall_clock64();                                        \
+  } while (0)
+#else
+#define WB_T(k) do {} while (0)
+#endif
+
 __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlockArgs a) {
   using namespace wb;
   constexpr float LOG2E = 1.4426950408889634f;
@@ -125,6 +145,7 @@ __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlockArgs a) 
   const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) void*)sm;
   const int tok0 = 16 * w;                             // this wave's first token (of 128)
   const int win = w >> 2, tt = w & 3;                  // its window and token tile in it
+  WB_T(0);
 
   // ---- window gather: token -> pixel (cyclic shift folded in), shifted-frame region id
   if (tid < 2) act_s[tid] = a.masked ? 0 : 1;
@@ -179,8 +200,10 @@ __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlockArgs a) 
       wb_dma16(a.wp + ((size_t)(u * WPF + f) * 64 + lane) * 8, lds0 + L_WP + f * 1024);
     }
   };
+  // only pair 0's qkv weights before the first barrier: the proj weights of pairs 0-1 stream
+  // behind pair 0 (a workgroup's weight stream, 288 KiB, is what bounds it: every CU pulls
+  // its own copy at ~12 B/cycle, MI355X_MICROARCH.md prologue-burst row)
   dma_wq(0);
-  dma_wp(0);
 
   // ---- tables (in log2 units: softmax runs on exp2)
   float* tb = reinterpret_cast<float*>(sm + L_TB);
@@ -238,10 +261,12 @@ __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlockArgs a) 
 
   for (int p = 0; p < 4; ++p) {
     if (p > 0) {
-      wb_wait_all();                                   // WQ(p) (and WP(1) at p = 3) landed
+      if (p == 1) wb_wait_vm<WP_W>();                  // WQ(1) landed (WP(0), issued after it,
+      else wb_wait_all();                              //  may be in flight); WQ(p) (+ WP(1))
       __syncthreads();                                 // ... everywhere; exchange free
       if (p == 2) dma_wp(1);                           // proj(0) done in every wave
     }
+    WB_T(1 + 4 * p);
     // ================= q^T, k^T, v of heads 2p, 2p+1 for this wave's 16 tokens
     uint4 qf[2];
     if (act) {
@@ -296,8 +321,12 @@ __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlockArgs a) 
             make_uint2(pack_bf16x2(vv.x, vv.y), pack_bf16x2(vv.z, vv.w));
       }
     }
+    WB_T(2 + 4 * p);
+    if (p == 1) wb_wait_all();                         // WP(0) landed (proj(0) ends this pair)
     __syncthreads();                                   // K / V^T of the window visible; WQ free
+    WB_T(3 + 4 * p);
     if (p < 3) dma_wq(p + 1);
+    if (p == 0) dma_wp(0);
 
     if (act) {
       f32x4 o[3];
@@ -380,11 +409,13 @@ __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlockArgs a) 
           }
       }
     }
+    WB_T(4 + 4 * p);
   }
 
   // ---- epilogue: out = x + proj + b (active window) or x (MASKSEL, :236-240)
   const float* bp = reinterpret_cast<const float*>(sm + L_BQ);
   const int pix = pix_s[tok0 + n];
+  WB_T(17);
   if (pix < 0) return;
   const bf16_t* xr = a.x + (long long)pix * a.ldx;
   bf16_t* orow = a.out + (long long)pix * a.ldo;
@@ -612,6 +643,15 @@ __global__ void __launch_bounds__(64 * NW) winblock4_kernel(const WinBlockArgs a
 }  // namespace rgbac
 
 using namespace rgbac;
+
+#ifdef RGBAC_WB_TIMING
+extern "C" int rgbac_debug_wb_times(unsigned long long* host, int nblocks) {
+  if (nblocks > 8192) nblocks = 8192;
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wb_t), (size_t)nblocks * 18 * 8) != hipSuccess) return 1;
+  return hipMemcpyFromSymbol(host + (size_t)nblocks * 18, HIP_SYMBOL(g_wb_w), (size_t)nblocks * 2 * 8) ==
+                 hipSuccess ? 0 : 1;
+}
+#endif
 
 extern "C" int rgbac_winattn_block(int batch, int h, int w, int shift, int masked, float scale,
                                    const void* x, int64_t ldx, const float* alpha,
