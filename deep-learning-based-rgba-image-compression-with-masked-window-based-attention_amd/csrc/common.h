@@ -100,6 +100,23 @@ __device__ __forceinline__ float gelu_fast(float x) {
 }
 
 
+// Lane exchanges without an LDS round trip (gfx950 v_permlane16_swap / v_permlane32_swap;
+// __shfl_xor is a ds_bpermute).  With the same value in both operands the swap returns
+// {the lower row's / half's value, the upper one's} on both lanes of a pair.
+__device__ __forceinline__ uint32_t xor32_u(uint32_t v) {        // value of lane ^ 32
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return (threadIdx.x & 32) ? r[0] : r[1];
+}
+__device__ __forceinline__ float xor32_f(float v) { return __uint_as_float(xor32_u(__float_as_uint(v))); }
+__device__ __forceinline__ float sum32_f(float v) {             // v + v(lane ^ 32), same on both
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float sum16_f(float v) {             // v + v(lane ^ 16), same on both
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
 // ---------------------------------------------------------------- host side
 void set_error(const std::string& msg);
 int check_launch(const char* what);

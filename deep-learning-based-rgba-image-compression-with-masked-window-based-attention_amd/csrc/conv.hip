@@ -2034,7 +2034,7 @@ __global__ void __launch_bounds__(512) conv_npatch_kernel(const ConvArgsDev args
       float sg[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        sg[r] = TN == 1 ? __shfl_xor(v[0][r], 32) : v[TN - 1][r];   // nho 8: lane ^ 32
+        sg[r] = TN == 1 ? xor32_f(v[0][r]) : v[TN - 1][r];          // nho 8: lane ^ 32
       if (ylane) {
 #pragma unroll
         for (int r = 0; r < 4; ++r)

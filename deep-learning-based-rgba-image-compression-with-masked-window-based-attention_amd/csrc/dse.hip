@@ -346,8 +346,8 @@ __global__ void __launch_bounds__(dse::NTH) dse_block_kernel(const DseArgsDev a)
             }
 #pragma unroll
           for (int c = 0; c < NC; ++c) {
-            o[c] += __shfl_xor(o[c], 16);
-            o[c] += __shfl_xor(o[c], 32);
+            o[c] = sum16_f(o[c]);
+            o[c] = sum32_f(o[c]);
           }
           if (inside && q == 0) {
             bf16_t* dst = a.out + pix * a.ldo;

@@ -18,7 +18,7 @@
 //   gdn  : the accumulator holds, per lane, pixel lane&31 and channel quads
 //          32t + 8g + 4h (h = lane>>5); the GDN GEMM's B fragment for k-step ks needs
 //          channels 16ks + 8h .. +7 of the same pixel: one quad is the lane's own, the
-//          other is the partner lane's (lane ^ 32) -- one __shfl_xor per k-step, no LDS.
+//          other is the partner lane's (lane ^ 32) -- one v_permlane32_swap per k-step.
 //   out  : y / sqrt(norm + beta') in the accumulator layout, 8-byte stores.
 #include "common.h"
 
@@ -33,6 +33,21 @@ constexpr int kW1Chunks = 2 * kStemKS1 + 1;   // 16-byte chunks per W1 row (26 +
 constexpr int kW2Chunks = kStemC / 8;     // 24
 
 typedef __attribute__((ext_vector_type(16))) float f32x16_s;
+
+__device__ uint4 g_stem_zero[64];           // source of the W1 rows' padding chunk
+
+__device__ __forceinline__ void stem_dma16(const void* src, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(lds)
+      : "memory");
+}
 
 __device__ __forceinline__ int w1_slot(int row, int chunk) { return row * kW1Chunks + chunk; }
 __device__ __forceinline__ int w2_slot(int row, int chunk) {
@@ -50,34 +65,25 @@ stem_gdn_kernel(int batch, int in_h, int in_w, const bf16_t* __restrict__ x, int
   __shared__ float B1s[kStemC], BEs[kStemC];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // panel staging: batches of 4 independent 16-byte loads per thread in flight before
-  // their LDS stores (a load -> store loop would pay one L2 round trip per chunk)
+  // panel staging by LDS-DMA: 1-KiB pieces (64 16-byte slots) straight into the (padded /
+  // swizzled) panel images, every piece in flight at once and one wait for all -- the
+  // register round trip (load 4 chunks, wait, store) paid ~10 memory latencies per CU
   {
-    constexpr int L1 = kW1Chunks - 1;               // chunks loaded per W1 row (26)
-    constexpr int N1 = kStemC * L1, N2 = kStemC * kW2Chunks, NB = 4;
-    for (int e0 = tid; e0 < N1 + N2; e0 += 256 * NB) {
-      uint4 v[NB];
-#pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        const int e = e0 + 256 * i;
-        if (e < N1) {
-          const int r = e / L1, ch = e - r * L1;
-          v[i] = *reinterpret_cast<const uint4*>(w1 + (size_t)r * w1_kpad + ch * 8);
-        } else if (e < N1 + N2) {
-          const int f = e - N1, r = f / kW2Chunks, ch = f - r * kW2Chunks;
-          v[i] = *reinterpret_cast<const uint4*>(w2 + (size_t)r * w2_kpad + ch * 8);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < NB; ++i) {
-        const int e = e0 + 256 * i;
-        if (e < N1) {
-          const int r = e / L1, ch = e - r * L1;
-          W1s[w1_slot(r, ch)] = v[i];
-        } else if (e < N1 + N2) {
-          const int f = e - N1, r = f / kW2Chunks, ch = f - r * kW2Chunks;
-          W2s[w2_slot(r, ch)] = v[i];
-        }
+    const uint32_t l1 = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(size_t)(__attribute__((address_space(3))) void*)W1s);
+    const uint32_t l2 = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(size_t)(__attribute__((address_space(3))) void*)W2s);
+    constexpr int P1 = kStemC * kW1Chunks / 64, P2 = kStemC * kW2Chunks / 64;
+    static_assert(P1 * 64 == kStemC * kW1Chunks && P2 * 64 == kStemC * kW2Chunks, "whole pieces");
+    for (int p = wave; p < P1 + P2; p += 4) {
+      if (p < P1) {
+        const int e = p * 64 + lane, r = e / kW1Chunks, ch = e - r * kW1Chunks;
+        stem_dma16(ch < kW1Chunks - 1 ? (const void*)(w1 + (size_t)r * w1_kpad + ch * 8)
+                                      : (const void*)g_stem_zero,
+                   l1 + p * 1024);
+      } else {
+        const int e = (p - P1) * 64 + lane, r = e / kW2Chunks, sl = e - r * kW2Chunks;
+        stem_dma16(w2 + (size_t)r * w2_kpad + (sl ^ (r & 7)) * 8, l2 + (p - P1) * 1024);
       }
     }
   }
@@ -85,7 +91,6 @@ stem_gdn_kernel(int batch, int in_h, int in_w, const bf16_t* __restrict__ x, int
     B1s[tid] = b1 ? b1[tid] : 0.0f;
     BEs[tid] = beta[tid];
   }
-  __syncthreads();
 
   const int r32 = lane & 31, h = lane >> 5;
   const int Ho = (in_h + 1) / 2, Wo = (in_w + 1) / 2;
@@ -124,6 +129,9 @@ stem_gdn_kernel(int batch, int in_h, int in_w, const bf16_t* __restrict__ x, int
 #pragma unroll
     for (int ks = 0; ks < kStemKS1; ++ks) bv[ks] = load_b(ks, pb, oy, ox, v);
   }
+  // the panels and the first tile's im2col fragments, one wait
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   for (int tile = blockIdx.x * 4 + wave; tile < ntile; tile += tstride) {
     const int m = tile * 32 + r32;
     const bool valid = m < M;
@@ -134,16 +142,25 @@ stem_gdn_kernel(int batch, int in_h, int in_w, const bf16_t* __restrict__ x, int
     for (int t = 0; t < kStemNT; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    // A fragments one k-step ahead: k-step ks + 1's LDS reads are in flight under k-step ks's
+    // six MFMAs (the scheduling barrier keeps the compiler from hoisting all 78 and spilling)
+    uint4 an[kStemNT];
+#pragma unroll
+    for (int t = 0; t < kStemNT; ++t) an[t] = W1s[w1_slot(32 * t + r32, h)];
 #pragma unroll
     for (int ks = 0; ks < kStemKS1; ++ks) {
       const bf16x8 bb = __builtin_bit_cast(bf16x8, bv[ks]);
+      uint4 a[kStemNT];
 #pragma unroll
-      for (int t = 0; t < kStemNT; ++t) {
-        const uint4 a = W1s[w1_slot(32 * t + r32, 2 * ks + h)];
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), bb,
-                                                         acc[t], 0, 0, 0);
+      for (int t = 0; t < kStemNT; ++t) a[t] = an[t];
+      if (ks + 1 < kStemKS1) {
+#pragma unroll
+        for (int t = 0; t < kStemNT; ++t) an[t] = W1s[w1_slot(32 * t + r32, 2 * (ks + 1) + h)];
       }
-      // one k-step's LDS fragments at a time (else all 78 are hoisted and spill)
+#pragma unroll
+      for (int t = 0; t < kStemNT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[t]), bb,
+                                                         acc[t], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
 
@@ -176,6 +193,9 @@ stem_gdn_kernel(int batch, int in_h, int in_w, const bf16_t* __restrict__ x, int
     for (int t = 0; t < kStemNT; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    uint4 wn[kStemNT];
+#pragma unroll
+    for (int t = 0; t < kStemNT; ++t) wn[t] = W2s[w2_slot(32 * t + r32, h)];
 #pragma unroll
     for (int ks = 0; ks < kStemKS2; ++ks) {
       // B fragment: channels 16ks + 8h .. +7 = quad g_need = 2(ks&1) + h of tile ks/2, both
@@ -187,8 +207,9 @@ stem_gdn_kernel(int batch, int in_h, int in_w, const bf16_t* __restrict__ x, int
       const uint32_t s0 = sq2(h ? ypk[tt][ga][0] : ypk[tt][gb][0]);
       const uint32_t s1 = sq2(h ? ypk[tt][ga][1] : ypk[tt][gb][1]);
       (void)g_send;
-      const uint32_t r0 = __shfl_xor(s0, 32);
-      const uint32_t r1 = __shfl_xor(s1, 32);
+      // the partner half's quad: v_permlane32_swap (a VALU lane exchange, no LDS round trip)
+      const uint32_t r0 = xor32_u(s0);
+      const uint32_t r1 = xor32_u(s1);
       const uint32_t o0 = sq2(h ? ypk[tt][gb][0] : ypk[tt][ga][0]);
       const uint32_t o1 = sq2(h ? ypk[tt][gb][1] : ypk[tt][ga][1]);
       (void)g_need;
@@ -197,12 +218,17 @@ stem_gdn_kernel(int batch, int in_h, int in_w, const bf16_t* __restrict__ x, int
       if (h == 0) b = make_uint4(o0, o1, r0, r1);
       else b = make_uint4(r0, r1, o0, o1);
       const bf16x8 bb = __builtin_bit_cast(bf16x8, b);
+      uint4 a[kStemNT];
 #pragma unroll
-      for (int t = 0; t < kStemNT; ++t) {
-        const uint4 a = W2s[w2_slot(32 * t + r32, 2 * ks + h)];
-        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), bb,
-                                                         acc[t], 0, 0, 0);
+      for (int t = 0; t < kStemNT; ++t) a[t] = wn[t];
+      if (ks + 1 < kStemKS2) {
+#pragma unroll
+        for (int t = 0; t < kStemNT; ++t) wn[t] = W2s[w2_slot(32 * t + r32, 2 * (ks + 1) + h)];
       }
+#pragma unroll
+      for (int t = 0; t < kStemNT; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[t]), bb,
+                                                         acc[t], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
 
