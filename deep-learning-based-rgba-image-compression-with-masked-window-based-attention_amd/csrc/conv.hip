@@ -2040,6 +2040,14 @@ __global__ void __launch_bounds__(512) conv_npatch_kernel(const ConvArgsDev args
         for (int r = 0; r < 4; ++r)
           bits += (double)gauss_elem_y<T>(g, m_e, 4 * fq + r, nho, v[0][r], sg[r], yv[r]);
       }
+    } else if (s.mode == RGBAC_SUBPEL2) {
+      // subpel conv (the decoder's last ConvTranspose as conv3x3 + PixelShuffle): bias,
+      // optional GELU and the shuffled store of epilogue4 (no residual operands, host-checked)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = 16 * j + 4 * fq;
+        if (n < cout) epilogue4<T>(s, g, 0, m_e, n, v[j]);
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -3324,11 +3332,15 @@ extern "C" int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroup
   }();
   s.remap = remap_env;
   if (a->tile == kTileNPatch) {
-    RGBAC_REQUIRE(a->dtype == RGBAC_BF16 && a->mode == RGBAC_CONV && a->ksplit == 1 &&
-                      a->ksize == 3 && a->stride == 1 && s.Wm % 16 == 0 &&
+    RGBAC_REQUIRE(a->dtype == RGBAC_BF16 &&
+                      (a->mode == RGBAC_CONV ||
+                       (a->mode == RGBAC_SUBPEL2 && !a->res0 && !a->res1 && !a->res2 &&
+                        (a->act == RGBAC_ACT_NONE || a->act == RGBAC_ACT_GELU))) &&
+                      a->ksplit == 1 && a->ksize == 3 && a->stride == 1 && s.Wm % 16 == 0 &&
                       s.Hm % 4 == 0,
-                  "the narrow patch tile needs bf16, a 3x3 stride-1 conv, ksplit 1, the "
-                  "output grid a multiple of 16 wide and 4 high");
+                  "the narrow patch tile needs bf16, a 3x3 stride-1 conv (or subpel conv with "
+                  "no residual, act none / GELU), ksplit 1, the grid a multiple of 16 wide "
+                  "and 4 high");
     RGBAC_REQUIRE((long long)a->batch * a->in_h * a->in_w < (1ll << 24),
                   "the narrow patch tile addresses sources of < 2^24 pixels");
     for (int i = 0; i < ngroups; ++i) {

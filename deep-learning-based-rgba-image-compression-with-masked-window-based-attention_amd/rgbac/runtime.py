@@ -633,10 +633,19 @@ def kernel_name(tile, preps):
     return f"conv_kernel<{dt}, {_TILE_SIG[tile]}{', 1' if tile < FIRST_WRES else ''}>"
 
 
+# RGBAC_NPATCH_SUBPEL=0: keep subpel convs off the narrow patch tile (A/B against older builds)
+NPATCH_SUBPEL = os.environ.get("RGBAC_NPATCH_SUBPEL", "1") != "0"
+
+
 def _npatch_ok(preps):
     a = preps[0].a
-    if not (a.dtype == _lib.BF16 and a.mode == CONV and a.ksize == 3 and a.stride == 1 and
-            a.in_w % 16 == 0 and a.in_h % 4 == 0 and a.batch * a.in_h * a.in_w < (1 << 24)):
+    # subpel convs (the decoder's 3-channel ConvTranspose as conv3x3 + PixelShuffle) take the
+    # plain epilogue: bias, optional GELU, shuffled store -- no residual operands
+    subpel_ok = (NPATCH_SUBPEL and a.mode == SUBPEL2 and a.act in (ACT["none"], ACT["gelu"]) and
+                 all(not (p.a.res0 or p.a.res1 or p.a.res2) for p in preps))
+    if not (a.dtype == _lib.BF16 and (a.mode == CONV or subpel_ok) and a.ksize == 3 and
+            a.stride == 1 and a.in_w % 16 == 0 and a.in_h % 4 == 0 and
+            a.batch * a.in_h * a.in_w < (1 << 24)):
         return False
     if not all(isinstance(p.pk, PackedConv) for p in preps):
         return False

@@ -683,7 +683,7 @@ def test_conv_patch_tiles(device, mode, cin, cout, H, W):
             srcs = [rt.to_nhwc(xd, dt).src()]
         fr = rt.to_nhwc(r.to(device), dt)
         tiles = None
-        for force in [None] + sorted(set(rt.PATCH_SIG) | set(rt.FPATCH_SIG)):
+        for force in [None] + sorted(set(rt.PATCH_SIG) | set(rt.FPATCH_SIG) | {rt.TILE_NPATCH}):
             if mode == "subpel":
                 pr = prep_subpel(m, srcs, act="gelu")
             elif mode == "convt_small":
@@ -691,6 +691,8 @@ def test_conv_patch_tiles(device, mode, cin, cout, H, W):
             else:
                 pr = prep_conv(m, srcs, act="gelu", res0=fr)
             ok = rt._patch_tiles([pr])
+            if rt._npatch_ok([pr]):                 # narrow patch tile: cout <= 32 (x4's subpel)
+                ok = ok + [rt.TILE_NPATCH]
             if tiles is None:
                 tiles = ok
             if force is not None and force not in ok:

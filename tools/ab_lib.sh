@@ -11,6 +11,6 @@ if [ -n "$TESTK" ]; then
   timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 100 --timeout-method thread -k "$TESTK" > gpurun_out/${TAG}_tests.log 2>&1
 fi
 for i in 1 2 3; do
-  RGBAC_LIB_PATH=$BASE timeout -k 10 200 python bench.py --no-dp-train --no-cpu-baseline --no-parity-mode > gpurun_out/${TAG}_A$i.json 2>> gpurun_out/${TAG}.err
+  env $A_ENV RGBAC_LIB_PATH=$BASE timeout -k 10 200 python bench.py --no-dp-train --no-cpu-baseline --no-parity-mode > gpurun_out/${TAG}_A$i.json 2>> gpurun_out/${TAG}.err
   timeout -k 10 200 python bench.py --no-dp-train --no-cpu-baseline --no-parity-mode > gpurun_out/${TAG}_B$i.json 2>> gpurun_out/${TAG}.err
 done
