@@ -974,6 +974,319 @@ winattn_bwd_kernel(int batch, int H, int W, int C, int heads, int shift, int mas
   for (int r = 0; r < NR; ++r) bp[N == 64 ? tid + 256 * r : tid] = bacc[r];
 }
 
+// ------------------------------------------------------------------ attention core backward, MFMA
+// The model's two shapes, (ws 8, head dim 24) and (ws 4, head dim 10), with the grid and the
+// bias-partial contract of winattn_bwd_kernel.  Per (window group, head h), in LDS:
+//   Qs Ks Vs Gs [64][DP]     q*scale, k, v, dO with the token on rows (DP: head dim padded to a
+//                            k-step, zeros)
+//   QT KT GT    [16 CT][64]  q*scale, k, dO transposed (token index contiguous)
+//   PT DT       [64][64]     P and dS with the KEY on rows;  DQ [64][64]: dS, query on rows
+// Wave w: S^T = K Q^T and dP^T = V dO^T over query tile w (keys on the MFMA rows, one query per
+// lane column -- the softmax and D_i = sum_j P dP row reductions are two lane swaps, as in the
+// forward winattn_mfma_kernel); then over token tile w, dQ^T = K^T dS^T, dK^T = (scale Q)^T dS
+// and dV^T = dO^T P leave 4 consecutive channels of one token per lane (vector stores).  The
+// next group's q/k/v/dO rows are loaded into registers while the current one computes.
+// bf16: P and dS enter the last three products rounded to bf16 (fp32 accumulation), like the
+// bf16 P of the forward; f32: v_mfma_f32_16x16x4_f32 throughout.
+namespace wbwd {
+template <typename T, int DH>
+struct Lay {
+  static constexpr int EPV = Elem<T>::EPV, KSTEP = 4 * EPV;
+  static constexpr int DP = (DH + KSTEP - 1) / KSTEP * KSTEP;
+  static constexpr int QRS = DP / EPV + 1;      // token-major row stride, 16-B chunks (+1 pad)
+  static constexpr int PRS = 64 / EPV + 1;      // 64-column row stride, chunks
+  static constexpr int CT = (DH + 15) / 16;     // 16-channel output tiles
+  static constexpr int ROWS = 64 * QRS, TRS = CT * 16 * PRS, PS = 64 * PRS;
+  static constexpr int QS = 0, KS = ROWS, VS = 2 * ROWS, GS = 3 * ROWS;
+  static constexpr int QT = 4 * ROWS, KT = QT + TRS, GT = KT + TRS;
+  static constexpr int PT = GT + TRS, DT = PT + PS, DQ = DT + PS;
+  static constexpr int CHUNKS = DQ + PS;
+  static constexpr int BYTES = CHUNKS * 16 + (64 + 64 + 4) * 4;   // + pix_s, rid_s, act_s
+};
+template <int V> struct Raw;
+template <> struct Raw<16> { using type = uint4; };
+template <> struct Raw<8> { using type = uint2; };
+template <> struct Raw<4> { using type = uint32_t; };
+__device__ __forceinline__ float max16_f(float v) {             // max(v, v(lane ^ 16))
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float max32_f(float v) {             // max(v, v(lane ^ 32))
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+}  // namespace wbwd
+
+template <typename T, int WS, int DH>
+__global__ void __launch_bounds__(256)
+winattn_bwd_mfma_kernel(int batch, int H, int W, int C, int heads, int shift, int masked,
+                        float scale, const T* __restrict__ qkv, long long ldq,
+                        const float* __restrict__ alpha, const float* __restrict__ bias,
+                        const T* __restrict__ dout, long long ldo, T* __restrict__ dqkv,
+                        long long lddq, float* __restrict__ bpart,
+                        const float* __restrict__ amask, int amask_nw) {
+  using Ly = wbwd::Lay<T, DH>;
+  constexpr int N = WS * WS, NWIN = 64 / N;
+  constexpr int EPV = Ly::EPV, KSTEP = Ly::KSTEP, DP = Ly::DP, QRS = Ly::QRS, PRS = Ly::PRS;
+  constexpr int CT = Ly::CT;
+  constexpr int ROWB = DH * (int)sizeof(T);
+  constexpr int VEC = (ROWB % 16 == 0) ? 16 : (ROWB % 8 == 0 ? 8 : 4);
+  constexpr int NP = ROWB / VEC, EV = VEC / (int)sizeof(T);
+  constexpr int NPIECE = 4 * 64 * NP;           // q, k, v, dO rows of 64 tokens
+  constexpr int PPT = (NPIECE + 255) / 256;
+  constexpr int KT = (WS == 8) ? 4 : 1;         // key tiles per query tile
+  using RawT = typename wbwd::Raw<VEC>::type;
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  uint4* const c16 = reinterpret_cast<uint4*>(sm);
+  T* const el = reinterpret_cast<T*>(sm);       // element view (chunk c = el + c * EPV)
+  int* const pix_s = reinterpret_cast<int*>(sm + Ly::CHUNKS * 16);
+  int* const rid_s = pix_s + 64;
+  int* const act_s = rid_s + 64;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int h = blockIdx.y;
+  const int nwx = W / WS, nwy = H / WS;
+  const int total = batch * nwx * nwy;
+  const int ngroups = (total + NWIN - 1) / NWIN;
+
+  // token t of window group grp -> pixel (-1 past the last window), shifted-frame region id
+  auto tok_pix = [&](int grp, int t, int& rid) -> int {
+    const int gw = grp * NWIN + t / N, lt = t % N;
+    rid = 0;
+    if (gw >= total) return -1;
+    const int b = gw / (nwx * nwy);
+    const int rem = gw - b * nwx * nwy;
+    const int wy = rem / nwx, wx = rem - wy * nwx;
+    const int r = wy * WS + lt / WS, c = wx * WS + lt % WS;
+    rid = 3 * (r < H - WS ? 0 : (r < H - shift ? 1 : 2)) + (c < W - WS ? 0 : (c < W - shift ? 1 : 2));
+    int oy = r + shift; if (oy >= H) oy -= H;
+    int ox = c + shift; if (ox >= W) ox -= W;
+    return (b * H + oy) * W + ox;
+  };
+  RawT raw[PPT];
+  auto load_group = [&](int grp) {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int e = tid + 256 * i;
+      raw[i] = RawT{};
+      if (NPIECE % 256 == 0 || e < NPIECE) {
+        const int which = e / (64 * NP), rem = e - which * 64 * NP;
+        const int t = rem / NP, pc = rem - t * NP;
+        int rid;
+        const int pix = tok_pix(grp, t, rid);
+        if (pix >= 0) {
+          const T* src = which < 3 ? qkv + (long long)pix * ldq + which * C + h * DH + pc * EV
+                                   : dout + (long long)pix * ldo + h * DH + pc * EV;
+          raw[i] = *reinterpret_cast<const RawT*>(src);
+        }
+      }
+    }
+  };
+
+  // zero what the staging never writes but the MFMAs read: chunks past the head dim, the
+  // transposed rows past it, and for ws 4 the off-window entries of PT / DT / DQ
+  {
+    constexpr int C0 = DH / EPV, C1 = DP / EPV;
+    for (int e = tid; e < 4 * 64 * (C1 - C0); e += 256) {
+      const int a = e / (64 * (C1 - C0)), r = e - a * 64 * (C1 - C0);
+      c16[a * Ly::ROWS + (r / (C1 - C0)) * QRS + C0 + r % (C1 - C0)] = make_uint4(0, 0, 0, 0);
+    }
+    constexpr int TZ = (CT * 16 - DH) * PRS;
+    for (int e = tid; e < 3 * TZ; e += 256)
+      c16[Ly::QT + (e / TZ) * Ly::TRS + DH * PRS + e % TZ] = make_uint4(0, 0, 0, 0);
+    if constexpr (WS == 4)
+      for (int e = tid; e < 3 * Ly::PS; e += 256) c16[Ly::PT + e] = make_uint4(0, 0, 0, 0);
+  }
+  __syncthreads();
+
+  const int qi = wave * 16 + fr;                // this lane's query (S^T column) / output token
+  const int qloc = qi % N;
+  float bias_r[KT][4], bacc[KT][4];
+  {
+    const float* bh = bias + (size_t)h * N * N;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      const int ktile = (WS == 8) ? kt : wave;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        bias_r[kt][r] = bh[qloc * N + (ktile * 16 + fq * 4 + r) % N];
+        bacc[kt][r] = 0.0f;
+      }
+    }
+  }
+  if (blockIdx.x < ngroups) load_group(blockIdx.x);
+
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    // ---- window bookkeeping (wave 0): pixels, region ids, active windows by ballot
+    if (tid < 64) {
+      int rid;
+      const int pix = tok_pix(grp, tid, rid);
+      const bool a = pix >= 0 && (!masked || alpha[pix] != 0.0f);
+      const unsigned long long bal = __ballot(a);
+      pix_s[tid] = pix;
+      rid_s[tid] = rid;
+      const unsigned long long wmask = (N == 64) ? ~0ull : (((1ull << N) - 1) << (tid / N * N));
+      if (tid % N == 0) act_s[tid / N] = (bal & wmask) != 0;
+    }
+    // ---- stage this group's rows (q scaled) and the transposed copies
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int e = tid + 256 * i;
+      if (NPIECE % 256 == 0 || e < NPIECE) {
+        const int which = e / (64 * NP), rem = e - which * 64 * NP;
+        const int t = rem / NP, pc = rem - t * NP;
+        const T* v = reinterpret_cast<const T*>(&raw[i]);
+        T* row = el + (which * Ly::ROWS + t * QRS) * EPV + pc * EV;
+        if (which == 0) {
+#pragma unroll
+          for (int q = 0; q < EV; ++q) Elem<T>::st(row + q, Elem<T>::ld(v + q) * scale);
+        } else {
+          *reinterpret_cast<RawT*>(row) = raw[i];
+        }
+        if (which != 2) {
+          const int tb = which == 0 ? Ly::QT : (which == 1 ? Ly::KT : Ly::GT);
+          T* tr = el + (tb + (pc * EV) * PRS) * EPV + t;
+#pragma unroll
+          for (int q = 0; q < EV; ++q)
+            Elem<T>::st(tr + q * PRS * EPV, which == 0 ? Elem<T>::ld(v + q) * scale : Elem<T>::ld(v + q));
+        }
+      }
+    }
+    __syncthreads();
+    if (grp + (int)gridDim.x < ngroups) load_group(grp + gridDim.x);
+
+    // ---- S^T, dP^T over this wave's query tile; softmax; D_i; dS
+    const int qwin = qi / N;
+    const bool qact = act_s[qwin] != 0;
+    const int qrid = rid_s[qi];
+    const float* qmask = amask ? amask + ((size_t)((grp * NWIN + qwin) % amask_nw) * N + qloc) * N
+                               : nullptr;
+    f32x4 s[KT], g[KT];
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      const int ktile = (WS == 8) ? kt : wave;
+      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      g[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < DP / KSTEP; ++ks) {
+        const int kr = (ktile * 16 + fr) * QRS + 4 * ks + fq, qr = qi * QRS + 4 * ks + fq;
+        mma_step<T>(s[kt], c16[Ly::KS + kr], c16[Ly::QS + qr]);
+        mma_step<T>(g[kt], c16[Ly::VS + kr], c16[Ly::GS + qr]);
+      }
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      const int ktile = (WS == 8) ? kt : wave;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int kj = ktile * 16 + fq * 4 + r;
+        float v = s[kt][r] + bias_r[kt][r];
+        if (shift > 0 && rid_s[kj] != qrid) v += -100.0f;
+        if (qmask) v += qmask[kj % N];
+        s[kt][r] = v;
+        mx = fmaxf(mx, v);
+      }
+    }
+    mx = wbwd::max32_f(wbwd::max16_f(mx));
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float ex = expf(s[kt][r] - mx);
+        s[kt][r] = ex;
+        sum += ex;
+      }
+    sum = sum32_f(sum16_f(sum));
+    const float inv = 1.0f / sum;
+    float dd = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s[kt][r] *= inv;
+        dd = fmaf(s[kt][r], g[kt][r], dd);
+      }
+    dd = sum32_f(sum16_f(dd));
+    T* const pt = el + Ly::PT * EPV;
+    T* const dt = el + Ly::DT * EPV;
+    T* const dq = el + Ly::DQ * EPV;
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      const int ktile = (WS == 8) ? kt : wave;
+      float ds[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        ds[r] = qact ? s[kt][r] * (g[kt][r] - dd) : 0.0f;
+        bacc[kt][r] += ds[r];
+        const int kj = ktile * 16 + fq * 4 + r;
+        Elem<T>::st(pt + kj * PRS * EPV + qi, s[kt][r]);
+        Elem<T>::st(dt + kj * PRS * EPV + qi, ds[r]);
+      }
+      Elem<T>::st4(dq + qi * PRS * EPV + ktile * 16 + fq * 4, ds);
+    }
+    __syncthreads();
+
+    // ---- dQ^T, dK^T, dV^T over token tile `wave` (= this lane's qi)
+    const int pix = pix_s[qi];
+    const bool on = act_s[qwin] != 0;
+#pragma unroll
+    for (int ct = 0; ct < CT; ++ct) {
+      f32x4 oq = f32x4{0.f, 0.f, 0.f, 0.f}, ok = oq, ov = oq;
+#pragma unroll
+      for (int ks = 0; ks < 64 / KSTEP; ++ks) {
+        const int tr = (ct * 16 + fr) * PRS + 4 * ks + fq, pr = qi * PRS + 4 * ks + fq;
+        mma_step<T>(oq, c16[Ly::KT + tr], c16[Ly::DQ + pr]);
+        mma_step<T>(ok, c16[Ly::QT + tr], c16[Ly::DT + pr]);
+        mma_step<T>(ov, c16[Ly::GT + tr], c16[Ly::PT + pr]);
+      }
+      const int c0 = ct * 16 + fq * 4;
+      if (pix >= 0 && c0 < DH) {
+        float vq[4], vk[4], vv[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          vq[r] = on ? oq[r] * scale : 0.0f;
+          vk[r] = on ? ok[r] : 0.0f;
+          vv[r] = on ? ov[r] : 0.0f;
+        }
+        T* dst = dqkv + (long long)pix * lddq + h * DH + c0;
+        if constexpr (DH % 4 == 0) {
+          Elem<T>::st4(dst, vq);
+          Elem<T>::st4(dst + C, vk);
+          Elem<T>::st4(dst + 2 * C, vv);
+        } else {
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (c0 + r < DH) {
+              Elem<T>::st(dst + r, vq[r]);
+              Elem<T>::st(dst + C + r, vk[r]);
+              Elem<T>::st(dst + 2 * C + r, vv[r]);
+            }
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- dense-bias gradient partial of (block, head): entry (query-local i, key-local j)
+  float* bp = bpart + ((size_t)blockIdx.x * heads + h) * N * N;
+  if constexpr (WS == 8) {
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+      *reinterpret_cast<float4*>(bp + qi * N + kt * 16 + fq * 4) =
+          make_float4(bacc[kt][0], bacc[kt][1], bacc[kt][2], bacc[kt][3]);
+  } else {
+    // ws 4: wave w held window w of each group; sum the four waves' (i, j) entries
+    float* red = reinterpret_cast<float*>(sm);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) red[wave * 256 + fr * N + fq * 4 + r] = bacc[0][r];
+    __syncthreads();
+    bp[tid] = red[tid] + red[256 + tid] + red[512 + tid] + red[768 + tid];
+  }
+}
+
 // dtable[e][h] = sum over blocks and (i, j) with index[i][j] == e of bpart[blk][h][i][j]
 __global__ void __launch_bounds__(256)
 relpos_reduce_kernel(int nblk, int heads, int N, const float* __restrict__ bpart,
@@ -1512,6 +1825,24 @@ extern "C" int rgbac_wgrad_reduce(int64_t nslot, const int32_t* fmap, const floa
   return check_launch("wgrad_reduce_kernel");
 }
 
+template <typename T, int WS, int DH>
+static void launch_attn_bwd_mfma(dim3 grid, hipStream_t st, int batch, int h, int w, int channels,
+                                 int heads, int shift, int masked, float scale, const void* qkv,
+                                 int64_t ldq, const float* alpha, const float* bias,
+                                 const void* dout, int64_t ldo, void* dqkv, int64_t lddq,
+                                 float* bias_partial, const float* amask, int amask_nw) {
+  constexpr int bytes = wbwd::Lay<T, DH>::BYTES;
+  static const bool attr = [] {                   // > 64 KiB of dynamic LDS for f32
+    hipFuncSetAttribute(reinterpret_cast<const void*>(winattn_bwd_mfma_kernel<T, WS, DH>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    return true;
+  }();
+  (void)attr;
+  hipLaunchKernelGGL((winattn_bwd_mfma_kernel<T, WS, DH>), grid, dim3(256), bytes, st, batch, h, w,
+                     channels, heads, shift, masked, scale, (const T*)qkv, ldq, alpha, bias,
+                     (const T*)dout, ldo, (T*)dqkv, lddq, bias_partial, amask, amask_nw);
+}
+
 extern "C" int rgbac_winattn_core_bwd_ex(int dtype, int batch, int h, int w, int channels,
                                          int heads, int ws, int shift, int masked, float scale,
                                          const void* qkv, int64_t ldq, const float* alpha,
@@ -1529,6 +1860,23 @@ extern "C" int rgbac_winattn_core_bwd_ex(int dtype, int batch, int h, int w, int
   RGBAC_REQUIRE(!amask || amask_nw > 0, "an explicit mask needs nW > 0");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   dim3 grid(nblk, heads);
+  // MFMA path for the model's two shapes (as the forward's winattn_mfma_kernel);
+  // RGBAC_ATTN_BWD_VALU=1 keeps the VALU kernel (A/B)
+  static const bool force_valu = [] {
+    const char* e = getenv("RGBAC_ATTN_BWD_VALU");
+    return e && e[0] == '1';
+  }();
+  const int dh = channels / heads;
+  if (!force_valu && ((ws == 8 && dh == 24) || (ws == 4 && dh == 10))) {
+    if (dtype == RGBAC_F32) {
+      if (ws == 8) launch_attn_bwd_mfma<float, 8, 24>(grid, st, batch, h, w, channels, heads, shift, masked, scale, qkv, ldq, alpha, bias, dout, ldo, dqkv, lddq, bias_partial, amask, amask_nw);
+      else launch_attn_bwd_mfma<float, 4, 10>(grid, st, batch, h, w, channels, heads, shift, masked, scale, qkv, ldq, alpha, bias, dout, ldo, dqkv, lddq, bias_partial, amask, amask_nw);
+    } else {
+      if (ws == 8) launch_attn_bwd_mfma<bf16_t, 8, 24>(grid, st, batch, h, w, channels, heads, shift, masked, scale, qkv, ldq, alpha, bias, dout, ldo, dqkv, lddq, bias_partial, amask, amask_nw);
+      else launch_attn_bwd_mfma<bf16_t, 4, 10>(grid, st, batch, h, w, channels, heads, shift, masked, scale, qkv, ldq, alpha, bias, dout, ldo, dqkv, lddq, bias_partial, amask, amask_nw);
+    }
+    return check_launch("winattn_bwd_mfma_kernel");
+  }
 #define K_(T, WS_)                                                                              \
   hipLaunchKernelGGL((winattn_bwd_kernel<T, WS_>), grid, dim3(256), 0, st, batch, h, w, channels, \
                      heads, shift, masked, scale, (const T*)qkv, ldq, alpha, bias,                \

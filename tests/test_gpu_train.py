@@ -243,6 +243,80 @@ def test_attention_block_grads(dim, ws, H, kind):
         assert nrel(p.grad, r) < 1e-3, k
 
 
+def _attn_core_bwd(dt, qkv, dense, dout, alpha, C, ws, shift, nblk, amask=None):
+    from rgbac import _lib
+    B, H, W, _ = qkv.shape
+    heads = dense.shape[0]
+    q = qkv.to(dt).contiguous()
+    go = dout.to(dt).contiguous()
+    dq = torch.zeros_like(q)
+    part = torch.full((nblk * heads * ws ** 4,), float("nan"), device=q.device)
+    _lib.call("rgbac_winattn_core_bwd_ex", _lib.dtype_code(dt), B, H, W, C, heads, ws, shift,
+              0 if alpha is None else 1, (C // heads) ** -0.5, q.data_ptr(), 3 * C,
+              _lib.ptr(alpha), dense.data_ptr(), go.data_ptr(), C, dq.data_ptr(), 3 * C, nblk,
+              part.data_ptr(), _lib.ptr(amask), 0 if amask is None else amask.shape[0],
+              _lib.stream_ptr(q.device))
+    torch.cuda.synchronize()
+    return dq.float(), part.view(nblk, heads, ws * ws, ws * ws).sum(0)
+
+
+@pytest.mark.parametrize("ws,C,shift,kind,nblk", [
+    (8, 192, 0, "ones", 64), (8, 192, 4, "rand", 5), (8, 192, 4, "half", 64),
+    (4, 80, 2, "half", 64), (4, 80, 0, "ones", 3), (4, 80, 2, "rand", 64),
+    (8, 96, 4, "half", 64), (4, 64, 2, "rand", 64)])
+def test_winattn_core_bwd_bf16_vs_f32(ws, C, shift, kind, nblk):
+    """bf16 attention-core backward (MFMA for head dims 24 / 10: P and dS enter dQ/dK/dV
+    rounded to bf16; VALU otherwise) against the f32 one on the same bf16-valued inputs,
+    with fewer blocks than window groups (grid-stride) for nblk < 64; the dense-bias
+    partials of every block are written (NaN-filled before the call)."""
+    g = _gen(ws * C + shift + len(kind))
+    B, H, W, heads = 2, 16, 24, 8
+    N = ws * ws
+    qkv = torch.randn((B, H, W, 3 * C), generator=g).bfloat16().float().cuda()
+    dout = torch.randn((B, H, W, C), generator=g).bfloat16().float().cuda()
+    dense = (torch.randn((heads, N, N), generator=g) * 0.5).cuda()
+    al = None if kind == "ones" else _alpha(kind, B, H, W, g).cuda().contiguous()
+    groups = -(-(B * (H // ws) * (W // ws)) // (64 // N))
+    nblk = min(nblk, groups)
+    d32, p32 = _attn_core_bwd(torch.float32, qkv, dense, dout, al, C, ws, shift, nblk)
+    d16, p16 = _attn_core_bwd(torch.bfloat16, qkv, dense, dout, al, C, ws, shift, nblk)
+    assert torch.isfinite(p32).all() and torch.isfinite(p16).all()
+    for k in range(3):
+        sl = slice(k * C, (k + 1) * C)
+        assert nrel(d16[..., sl], d32[..., sl]) < 1.5e-2, k
+    assert nrel(p16, p32) < 1.5e-2
+
+
+def test_winattn_core_bwd_explicit_mask():
+    """The explicit (nW, N, N) additive mask of WindowAttention.forward(x, mask) in the
+    attention-core backward (both kernels' shapes): f32 vs a torch autograd restatement."""
+    from rgbac import _lib  # noqa: F401  (the library must load)
+    g = _gen(77)
+    for ws, C in ((8, 192), (4, 80)):
+        B, H, W, heads = 1, 16, 16, 8
+        N, nW, d = ws * ws, 3, C // heads
+        qkv = torch.randn((B, H, W, 3 * C), generator=g)
+        dout = torch.randn((B, H, W, C), generator=g)
+        dense = torch.randn((heads, N, N), generator=g) * 0.5
+        am = torch.zeros((nW, N, N))
+        am[torch.rand((nW, N, N), generator=g) < 0.3] = -100.0
+        groups = -(-(B * (H // ws) * (W // ws)) // (64 // N))
+        dq, part = _attn_core_bwd(torch.float32, qkv.cuda(), dense.cuda(), dout.cuda(), None, C,
+                                  ws, 0, min(groups, 64), am.cuda())
+        # torch restatement: windows in raster order, window b adds am[b % nW]
+        x = qkv.clone().requires_grad_(True)
+        bias = dense.clone().requires_grad_(True)
+        win = x.view(B, H // ws, ws, W // ws, ws, 3, heads, d).permute(5, 0, 1, 3, 6, 2, 4, 7)
+        win = win.reshape(3, -1, heads, N, d)
+        s = (win[0] * d ** -0.5) @ win[1].transpose(-1, -2) + bias
+        s = s + am.repeat(win.shape[1] // nW + 1, 1, 1)[: win.shape[1]].unsqueeze(1)
+        o = s.softmax(-1) @ win[2]
+        o = o.view(B, H // ws, W // ws, heads, ws, ws, d).permute(0, 1, 4, 2, 5, 3, 6)
+        o.reshape(B, H, W, C).backward(dout)
+        assert nrel(dq.cpu(), x.grad) < 1e-5, ws
+        assert nrel(part.cpu(), bias.grad) < 1e-5, ws
+
+
 def test_gaussian_slice_grads():
     from rgbac import autograd as ag
     rt = _rt()
