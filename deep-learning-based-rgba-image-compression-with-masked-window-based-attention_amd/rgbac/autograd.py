@@ -582,7 +582,9 @@ class WinAttnFn(Function):
         dt = qkv_t.dtype
         dev = qkv_t.device
         do_t = do_t.contiguous()
-        dqkv = torch.zeros_like(qkv_t)
+        # both backward kernels write every q/k/v channel of every pixel (zeros in inactive
+        # windows); only row padding past 3C would stay unwritten
+        dqkv = (torch.empty_like if ldq == 3 * C else torch.zeros_like)(qkv_t)
         N = ws * ws
         groups = -(-(B * (H // ws) * (W // ws)) // (64 // N))
         nblk = int(min(groups, 64))
@@ -614,16 +616,42 @@ def _copy(dst, dcoff, src, scoff, C):
               src.ptr(), src.ldc, scoff, dst.ptr(), dst.ldc, dcoff, _lib.stream_ptr(src.t.device))
 
 
+# RGBAC_CAT_MULTI=0: one rgbac_channel_copy launch per part (A/B)
+_CAT_MULTI = os.environ.get("RGBAC_CAT_MULTI", "1") != "0"
+
+
+def _copy_multi(pairs, npix):
+    """[(dst Feat, dst channel offset, src Feat, src channel offset, channels)] -> one
+    rgbac_channel_copy_multi launch per 16 copies."""
+    if not _CAT_MULTI:
+        for dst, dcoff, src, scoff, C in pairs:
+            _copy(dst, dcoff, src, scoff, C)
+        return
+    for k in range(0, len(pairs), 16):
+        part = pairs[k:k + 16]
+        desc = (ctypes.c_int64 * (7 * len(part)))()
+        for i, (dst, dcoff, src, scoff, C) in enumerate(part):
+            desc[7 * i: 7 * i + 7] = [src.ptr(), src.ldc, scoff, C, dst.ptr(), dst.ldc, dcoff]
+        src0 = part[0][2]
+        _lib.call("rgbac_channel_copy_multi", _lib.dtype_code(src0.t.dtype), npix, len(part),
+                  ctypes.addressof(desc), _lib.stream_ptr(src0.t.device))
+
+
 class CatFn(Function):
+    """torch.cat(parts, dim=1) of NHWC Feats (the slice supports of
+    AutoEncoderRGB_Journal.py:249-262): all parts in one copy launch, and the backward split
+    likewise."""
+
     @staticmethod
     def forward(ctx, Cs, *ts):
         fs = [Feat(t, c) for t, c in zip(ts, Cs)]
         f0 = fs[0]
         out = new_feat(f0.B, f0.H, f0.W, sum(Cs), f0.t.dtype, f0.t.device)
-        off = 0
+        pairs, off = [], 0
         for f in fs:
-            _copy(out, off, f, 0, f.C)
+            pairs.append((out, off, f, 0, f.C))
             off += f.C
+        _copy_multi(pairs, f0.B * f0.H * f0.W)
         ctx.Cs = Cs
         ctx.shapes = [t.shape for t in ts]
         return out.t
@@ -631,16 +659,17 @@ class CatFn(Function):
     @staticmethod
     def backward(ctx, g):
         g = Feat(g.contiguous(), sum(ctx.Cs))
-        outs = []
+        outs, pairs = [], []
         off = 0
         for c, shp in zip(ctx.Cs, ctx.shapes):
             # the copy writes channels [0, c) of every pixel: only channel padding (ldc > c)
             # needs the zero fill (the slice supports are unpadded: ~140 fills per step saved)
             alloc = torch.empty if shp[-1] == c else torch.zeros
             o = Feat(alloc(shp, dtype=g.t.dtype, device=g.t.device), c)
-            _copy(o, 0, g, off, c)
+            pairs.append((o, 0, g, off, c))
             off += c
             outs.append(o.t)
+        _copy_multi(pairs, g.B * g.H * g.W)
         return (None, *outs)
 
 

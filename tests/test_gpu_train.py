@@ -249,7 +249,7 @@ def _attn_core_bwd(dt, qkv, dense, dout, alpha, C, ws, shift, nblk, amask=None):
     heads = dense.shape[0]
     q = qkv.to(dt).contiguous()
     go = dout.to(dt).contiguous()
-    dq = torch.zeros_like(q)
+    dq = torch.full_like(q, float("nan"))         # every q/k/v channel must be written
     part = torch.full((nblk * heads * ws ** 4,), float("nan"), device=q.device)
     _lib.call("rgbac_winattn_core_bwd_ex", _lib.dtype_code(dt), B, H, W, C, heads, ws, shift,
               0 if alpha is None else 1, (C // heads) ** -0.5, q.data_ptr(), 3 * C,
@@ -268,7 +268,8 @@ def test_winattn_core_bwd_bf16_vs_f32(ws, C, shift, kind, nblk):
     """bf16 attention-core backward (MFMA for head dims 24 / 10: P and dS enter dQ/dK/dV
     rounded to bf16; VALU otherwise) against the f32 one on the same bf16-valued inputs,
     with fewer blocks than window groups (grid-stride) for nblk < 64; the dense-bias
-    partials of every block are written (NaN-filled before the call)."""
+    partials of every block and every q/k/v gradient channel are written (NaN-filled
+    before the call: the autograd Function allocates dqkv uninitialised)."""
     g = _gen(ws * C + shift + len(kind))
     B, H, W, heads = 2, 16, 24, 8
     N = ws * ws
@@ -281,6 +282,7 @@ def test_winattn_core_bwd_bf16_vs_f32(ws, C, shift, kind, nblk):
     d32, p32 = _attn_core_bwd(torch.float32, qkv, dense, dout, al, C, ws, shift, nblk)
     d16, p16 = _attn_core_bwd(torch.bfloat16, qkv, dense, dout, al, C, ws, shift, nblk)
     assert torch.isfinite(p32).all() and torch.isfinite(p16).all()
+    assert torch.isfinite(d32).all() and torch.isfinite(d16).all()
     for k in range(3):
         sl = slice(k * C, (k + 1) * C)
         assert nrel(d16[..., sl], d32[..., sl]) < 1.5e-2, k
@@ -621,3 +623,28 @@ def test_fpatch_tile_never_reaches_a_training_pack():
     # the forward pack itself does take the fragment tile
     rt.launch([rt.prepare(pk, [x.src()])], force=(44, 1))
     assert rt.LAST_CHOICE[0][0] == 44
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_channel_copy_multi(dtype):
+    """rgbac_channel_copy_multi (CatFn forward / backward in one launch) == torch channel
+    slicing: vector (16-byte aligned) and scalar tasks, 1 and 17 tasks (two launches)."""
+    from rgbac import autograd as ag
+    from rgbac.runtime import Feat
+    g = _gen(5)
+    B, H, W = 2, 16, 12
+    for Cs in ([8, 16, 24], [3, 5, 8, 13], [32], [8] * 17):
+        parts = [Feat(torch.randn((B, H, W, c + (c % 8 and 8 - c % 8)), generator=g).to(dtype).cuda(), c)
+                 for c in Cs]
+        cat = ag.cat_t(parts)
+        want = torch.cat([p.t[..., : p.C] for p in parts], -1)
+        assert torch.equal(cat.t[..., : cat.C], want)
+        gy = torch.randn(cat.t.shape, generator=g).to(dtype).cuda()
+        leaves = [p.t.requires_grad_(True) for p in parts]
+        out = ag.CatFn.apply(Cs, *leaves)
+        out.backward(gy)
+        off = 0
+        for p, c in zip(leaves, Cs):
+            assert torch.equal(p.grad[..., :c], gy[..., off:off + c])
+            assert not p.grad[..., c:].any()
+            off += c
