@@ -144,6 +144,7 @@ SIGNATURES = {
     "rgbac_adam_clamp_dstep": [_I64, _VP, _VP, _VP, _VP, _D, _D, _D, _D, _VP, _F, _F, _VP],
     "rgbac_pixel_shuffle": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _I64, _VP, _I64, _VP],
     "rgbac_channel_copy": [_I32, _I64, _I32, _VP, _I64, _I32, _VP, _I64, _I32, _VP],
+    "rgbac_channel_copy_multi": [_I32, _I64, _I32, _VP, _VP],
     "rgbac_weight_gather": [_I32, _I64, _VP, _VP, _VP, _VP],
     "rgbac_weight_gather_multi": [_I32, _VP, _VP, _I64, _VP],
     "rgbac_colsum": [_I32, _I64, _I32, _VP, _I64, _I32, _VP, _VP],

@@ -384,6 +384,13 @@ int rgbac_pixel_shuffle(int dtype, int dir, int batch, int h, int w, int c, cons
                         int64_t ldi, void* out, int64_t ldo, void* stream);
 int rgbac_channel_copy(int dtype, int64_t npix, int channels, const void* src, int64_t lds,
                        int scoff, void* dst, int64_t ldd, int dcoff, void* stream);
+/* Up to 16 channel copies over the same npix in one launch: desc = ntasks x 7 int64
+ * {src, lds, scoff, channels, dst, ldd, dcoff} (host memory, read at the call; pointers as
+ * integers).  Replaces the per-part rgbac_channel_copy launches of a concatenation
+ * (torch.cat(..., dim=1) of the slice supports, AutoEncoderRGB_Journal.py:249-262) and of
+ * its backward split.                                                      */
+int rgbac_channel_copy_multi(int dtype, int64_t npix, int ntasks, const int64_t* desc,
+                             void* stream);
 
 /* Weight repack through a cached index map: dst[i] = idx[i] >= 0 ? src[idx[i]] : 0
  * (src = fp32 PyTorch parameter, dst = packed [nphase][cout_pad][k_pad]).   */
