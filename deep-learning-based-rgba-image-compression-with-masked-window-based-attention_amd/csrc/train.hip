@@ -20,6 +20,7 @@
 //   pixel_shuffle_kernel / channel_copy_kernel   layout helpers (subpel, concat)
 #include <algorithm>
 #include <cmath>
+#include <type_traits>
 
 #include "common.h"
 
@@ -50,13 +51,29 @@ __device__ __forceinline__ long long ediv(long long e, int d, double rd, int& re
 // (GATE: y = r1*sigmoid(v); GDN: y = r1/sqrt(v); IGDN: y = r1*sqrt(v)).
 // Channels [C, ld) of the outputs are written as zeros.  One thread per group of
 // 4 channels of a pixel (vector loads/stores; all leading dims are multiples of 4).
+// GELU'(v) = Phi(v) + v phi(v) with the Abramowitz & Stegun 7.1.26 erfc of the forward's
+// gelu_fast (|erf error| <= 1.5e-7; exp(-v^2/2) shared by both terms): ~15 instructions
+// instead of erfcf + expf.  bf16 only (the f32 parity path keeps erfcf).
+__device__ __forceinline__ float gelu_grad_fast(float v) {
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752440f, fabsf(v), 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(v * v * -0.72134752044448170368f);   // exp(-v^2/2)
+  const float q = p * t * e;                     // erfc(|v| / sqrt 2)
+  const float cdf = v >= 0.0f ? fmaf(-0.5f, q, 1.0f) : 0.5f * q;
+  return fmaf(0.39894228040143267794f * v, e, cdf);
+}
+
+template <bool FAST>
 __device__ __forceinline__ void act_bwd1(int act, float slope, float g, float v, float a,
                                          bool on, float& gz, float& gr) {
   gz = g;
   gr = 0.0f;
   switch (act) {
     case RGBAC_ACT_GELU:
-      gz = g * (t_cdf(v) + v * t_phi(v));
+      gz = FAST ? g * gelu_grad_fast(v) : g * (t_cdf(v) + v * t_phi(v));
       break;
     case RGBAC_ACT_RELU:
       gz = v > 0.0f ? g : 0.0f;
@@ -97,7 +114,7 @@ __device__ __forceinline__ void act_bwd1(int act, float slope, float g, float v,
   }
 }
 
-template <typename T>
+template <typename T, bool FAST>
 __global__ void __launch_bounds__(256)
 act_bwd_kernel(int act, float slope, long long npix, int C, const T* __restrict__ dy, long long ldy,
                const T* __restrict__ z, long long ldz, const T* __restrict__ r1, long long ld1,
@@ -119,7 +136,8 @@ act_bwd_kernel(int act, float slope, long long npix, int C, const T* __restrict_
         Elem<T>::ld4(r1 + p * ld1 + c0, a);
       const bool on = sel ? sel[p] != 0 : true;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) act_bwd1(act, slope, g[r], v[r], a[r], on, gz[r], gr[r]);
+      for (int r = 0; r < 4; ++r)
+        act_bwd1<FAST>(act, slope, g[r], v[r], a[r], on, gz[r], gr[r]);
     } else {
       const bool on = sel ? sel[p] != 0 : true;
 #pragma unroll
@@ -130,7 +148,7 @@ act_bwd_kernel(int act, float slope, long long npix, int C, const T* __restrict_
           const float v = z ? Elem<T>::ld(z + p * ldz + c) : 0.0f;
           const float a = (r1 && (act == RGBAC_ACT_GATE || act == RGBAC_ACT_GDN ||
                                   act == RGBAC_ACT_IGDN)) ? Elem<T>::ld(r1 + p * ld1 + c) : 0.0f;
-          act_bwd1(act, slope, g, v, a, on, gz[r], gr[r]);
+          act_bwd1<FAST>(act, slope, g, v, a, on, gz[r], gr[r]);
         }
       }
     }
@@ -1763,11 +1781,18 @@ extern "C" int rgbac_act_bwd(int dtype, int act, float act_param, int64_t npix, 
   if (npix == 0) return RGBAC_OK;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int g = grid_for(npix * lddz / 4);
-#define K_(T, ...)                                                                            \
-  hipLaunchKernelGGL(act_bwd_kernel<T>, dim3(g), dim3(256), 0, st, act, act_param, npix,        \
+  // bf16: the fast GELU derivative (RGBAC_GELU_BWD_EXACT=1 keeps erfcf, A/B)
+  static const bool exact = [] {
+    const char* e = getenv("RGBAC_GELU_BWD_EXACT");
+    return e && e[0] == '1';
+  }();
+#define K_(T, F)                                                                              \
+  hipLaunchKernelGGL((act_bwd_kernel<T, F>), dim3(g), dim3(256), 0, st, act, act_param, npix,   \
                      channels, (const T*)dy, ldy, (const T*)z, ldz, (const T*)res1, ld1, sel,   \
                      (T*)dz, lddz, (T*)dres1, lddr1)
-  RGBAC_DT_DISPATCH(dtype, K_, 0);
+  if (dtype == RGBAC_F32) K_(float, false);
+  else if (exact) K_(bf16_t, false);
+  else K_(bf16_t, true);
 #undef K_
   return check_launch("act_bwd_kernel");
 }
