@@ -157,6 +157,36 @@ act_bwd_kernel(int act, float slope, long long npix, int C, const T* __restrict_
   }
 }
 
+// bf16 act_bwd over unpadded, equally strided operands (C == every leading dim, no select):
+// a flat elementwise pass, 8 channels per thread with 16-byte loads and no pixel/channel
+// division.
+template <bool FAST>
+__global__ void __launch_bounds__(256)
+act_bwd_flat_kernel(int act, float slope, long long n8, const uint4* __restrict__ dy,
+                    const uint4* __restrict__ z, const uint4* __restrict__ r1,
+                    uint4* __restrict__ dz, uint4* __restrict__ dr1) {
+  const bool use_r1 = r1 && (act == RGBAC_ACT_GATE || act == RGBAC_ACT_GDN || act == RGBAC_ACT_IGDN);
+  for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n8; e += (long long)gridDim.x * 256) {
+    const uint4 gq = dy[e], zq = z[e];
+    const uint4 aq = use_r1 ? r1[e] : make_uint4(0, 0, 0, 0);
+    const uint32_t gw[4] = {gq.x, gq.y, gq.z, gq.w}, zw[4] = {zq.x, zq.y, zq.z, zq.w},
+                   aw[4] = {aq.x, aq.y, aq.z, aq.w};
+    uint32_t ow[4], rw[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float gz0, gr0, gz1, gr1;
+      act_bwd1<FAST>(act, slope, bf2f(gw[i] & 0xFFFF), bf2f(zw[i] & 0xFFFF), bf2f(aw[i] & 0xFFFF),
+                     true, gz0, gr0);
+      act_bwd1<FAST>(act, slope, bf2f(gw[i] >> 16), bf2f(zw[i] >> 16), bf2f(aw[i] >> 16), true,
+                     gz1, gr1);
+      ow[i] = pack_bf16x2(gz0, gz1);
+      rw[i] = pack_bf16x2(gr0, gr1);
+    }
+    dz[e] = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    if (dr1) dr1[e] = make_uint4(rw[0], rw[1], rw[2], rw[3]);
+  }
+}
+
 // ------------------------------------------------------------------ wgrad
 struct WgradDev {
   const void* g; long long ldg; int gch;
@@ -1790,6 +1820,25 @@ extern "C" int rgbac_act_bwd(int dtype, int act, float act_param, int64_t npix, 
   hipLaunchKernelGGL((act_bwd_kernel<T, F>), dim3(g), dim3(256), 0, st, act, act_param, npix,   \
                      channels, (const T*)dy, ldy, (const T*)z, ldz, (const T*)res1, ld1, sel,   \
                      (T*)dz, lddz, (T*)dres1, lddr1)
+  static const bool no_flat = [] {
+    const char* e = getenv("RGBAC_ACT_BWD_FLAT");
+    return e && e[0] == '0';
+  }();
+  auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  const bool flat = !no_flat && dtype == RGBAC_BF16 && !sel && z && channels == lddz &&
+                    ldy == lddz && ldz == lddz && (!res1 || ld1 == lddz) &&
+                    (npix * lddz) % 8 == 0 && al16(dy) && al16(z) && al16(dz) &&
+                    (!res1 || al16(res1)) && (!dres1 || al16(dres1));
+  if (flat) {
+    const long long n8 = npix * lddz / 8;
+#define F_(F)                                                                                  \
+  hipLaunchKernelGGL((act_bwd_flat_kernel<F>), dim3(grid_for(n8)), dim3(256), 0, st, act,       \
+                     act_param, n8, (const uint4*)dy, (const uint4*)z, (const uint4*)res1,      \
+                     (uint4*)dz, (uint4*)dres1)
+    if (exact) F_(false); else F_(true);
+#undef F_
+    return check_launch("act_bwd_flat_kernel");
+  }
   if (dtype == RGBAC_F32) K_(float, false);
   else if (exact) K_(bf16_t, false);
   else K_(bf16_t, true);
