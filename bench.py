@@ -348,39 +348,18 @@ def main_train(args, world, rank, dev, dist):
         return loss.detach()
 
     tuned = tune_cache_setup(args, os.path.join(ROOT, "profiles", f"tune_train_{args.dtype}_b{B}_{S}.json"))
-    step()
+    step()                    # tunes; with DP buckets this is also their learning step
     torch.cuda.synchronize()
     if args.save_tune and rank == 0:
         rt.save_tune_cache(args.save_tune)
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # One process per GPU without a collective in the step (world 1): the whole step --
-    # forward, backward, clamp + Adam (device step counter) -- is captured once and replayed
-    # from a HIP graph, so the host's per-launch cost leaves the timed loop.  Data-parallel
-    # runs keep the eager step (bucketed RCCL all-reduces launched from autograd hooks).
-    run = step
-    graph = None
-    captured = not args.no_graph and world == 1
-    if captured:
-        opt.use_device_step()
-        side = torch.cuda.Stream(dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side):
-            for _ in range(2):
-                step()
-        torch.cuda.current_stream(dev).wait_stream(side)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            gout = step()
-        torch.cuda.synchronize()
-
-        def run():
-            graph.replay()
-            return gout
-        for _ in range(2):
-            run()
-        torch.cuda.synchronize()
+    # The whole step -- forward, backward (with the bucketed RCCL all-reduces under DP),
+    # clamp + Adam (device step counter) -- is captured once and replayed from a HIP graph at
+    # every world size, so the host's per-launch cost leaves the timed loop.
+    run, graph, gout = capture_train(step, opt, dev, args.no_graph)
+    captured = graph is not None
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
@@ -443,20 +422,61 @@ def main_train(args, world, rank, dev, dist):
         dist.destroy_process_group()
 
 
+def capture_train(step, opt, dev, no_graph, before=None):
+    """Capture one training step (forward, backward, all-reduces, clamp + Adam) in a HIP
+    graph: Adam switches to its device step counter, two warm steps run on a side stream
+    (the capture stream's allocations and autograd nodes), then the capture.  ``before``:
+    called right before the captured step (e.g. to arm timing events).  Returns
+    (run, graph, captured output); (step, None, None) with ``no_graph``."""
+    if no_graph:
+        return step, None, None
+    opt.use_device_step()
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    if before is not None:
+        before()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        gout = step()
+    torch.cuda.synchronize()
+
+    def run():
+        graph.replay()
+        return gout
+    for _ in range(2):
+        run()
+    torch.cuda.synchronize()
+    return run, graph, gout
+
+
 def dp_train_record(args, world, rank, dev, dist):
     """BASELINE config 5 inside the driver's own scaling command: the trainRGB.py step
     (forward + backward of 4096*mse + bpp, clamp(+-5), Adam) at 16 images per rank, 256^2, bf16,
     data-parallel over the ranks of THIS run -- bucketed RCCL all-reduce of the 34 M fp32
-    gradients launched from post-accumulate-grad hooks (rgbac.parallel.DataParallelTrainer).
-    The step runs eagerly at every world size (world 1 included), so the N-rank and 1-rank
-    numbers are timed the same way.  Every rank calls this (collectives); rank 0 gets the record.
-    ``exposed_allreduce_ms``: GPU time between the end of backward and the last bucket's
-    completion (what backward did not hide); ``allreduce_ms`` the same 136 MB reduced alone."""
+    gradients launched from post-accumulate-grad hooks (rgbac.parallel.DataParallelTrainer),
+    the step captured in a HIP graph (RCCL collectives included) and replayed.  At world 1
+    (plain ``python bench.py``) a one-rank RCCL process group is created and the buckets are
+    forced on, so the 1-rank and N-rank numbers run the same code path: same backward, same
+    hook-launched all-reduces, same graph.  Every rank calls this (collectives); rank 0 gets
+    the record.  ``exposed_allreduce_ms``: replayed-step time minus that of the same step
+    captured without the all-reduces (what backward did not hide); ``allreduce_ms`` the same
+    136 MB reduced alone."""
+    import torch.distributed as tdist
     from rgbac.layers.SupplyMask import mask_pyramid
     from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
     from rgbac.optim import AdamClamp
     from rgbac.parallel import DataParallelTrainer
     from rgbac import runtime as rt
+    own_group = False
+    if not tdist.is_initialized():
+        # plain `python bench.py`: one rank, an in-process store, RCCL communicator of one
+        tdist.init_process_group("nccl", store=tdist.HashStore(), rank=0, world_size=1,
+                                 device_id=dev)
+        own_group = True
     B, S = args.dp_batch, 256
     tuned = os.path.join(ROOT, "profiles", f"tune_train_bf16_b{B}_{S}.json")
     if os.path.exists(tuned):
@@ -464,61 +484,97 @@ def dp_train_record(args, world, rank, dev, dist):
     torch.manual_seed(234)
     net = AutoEncoder().train().to(dev).set_compute_dtype(torch.bfloat16)
     opt = AdamClamp(net.parameters(), lr=1e-4, clip=5.0)
-    trainer = DataParallelTrainer(net, opt)
+    trainer = DataParallelTrainer(net, opt, force_buckets=True)
     x, a = synth_inputs(B, S, S, seed=1000 + rank)     # this rank's shard of the global batch
     x, a = x.to(dev), a.to(dev)
     _, me = mask_pyramid(a, 4)
-    losses = []
 
     def step():
         out = net(x, a, a, *me)
         loss = 4096.0 * out[1] + out[2]                 # trainRGB.py:183-186 (lambda 4096)
         trainer.step(loss)
-        losses.append(loss.detach())
+        return loss.detach()
 
-    for _ in range(args.dp_warmup):
+    step()                                              # learning step of the buckets
+    for _ in range(max(0, args.dp_warmup - 1)):
         step()
     torch.cuda.synchronize()
-    trainer.comm_events = []
-    losses.clear()
-    elapsed = time_steps(step, args.dp_steps, dist, dev)
-    exposed = 0.0
-    if trainer.comm_events:
-        exposed = sum(e0.elapsed_time(e1) for e0, e1 in trainer.comm_events) / len(trainer.comm_events)
-    trainer.comm_events = None
-    ar_ms = 0.0
-    if dist:
-        flat = opt.flat_grad
-        for _ in range(2):
-            dist.all_reduce(flat)
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(5):
-            dist.all_reduce(flat)
-        e1.record()
-        torch.cuda.synchronize()
-        ar_ms = e0.elapsed_time(e1) / 5
-        t = torch.tensor([exposed, ar_ms], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        exposed, ar_ms = t.tolist()
-        n_ranks = dist.get_world_size()
-    else:
-        n_ranks = 1
-    finite = all(bool(torch.isfinite(l).item()) for l in losses)
-    grad_bytes = opt.flat_grad.numel() * opt.flat_grad.element_size()
-    del net, opt, trainer
+    nb = len(trainer.buckets.buckets)
+    launched = trainer.buckets.launched_in_backward()
+    graph_err = None
+    try:
+        run, graph, gout = capture_train(step, opt, dev, args.no_graph)
+    except RuntimeError as e:                           # recorded, the eager step is timed
+        graph_err = f"{type(e).__name__}: {str(e)[:200]}"
+        run, graph, gout = step, None, None
+    for _ in range(2):
+        run()
+    torch.cuda.synchronize()
+    elapsed = time_steps(run, args.dp_steps, dist, dev)
+    # exposed all-reduce time = what backward did not hide: the same step captured once more
+    # with the bucket all-reduces left out (GradBuckets.skip), the two graphs replayed in
+    # alternation, HIP events around the replays on the replaying stream (timing events
+    # cannot be recorded inside a capture on ROCm).  Measured after the timed loop: the
+    # comm-free replays update each rank's replica with its own gradient only.
+    exposed = None
+    if graph is not None:
+        trainer.buckets.skip = True
+        try:
+            run_nc, graph_nc, _ = capture_train(step, opt, dev, False)
+        finally:
+            trainer.buckets.skip = False
+        t_dp, t_nc = [], []
+        for _ in range(4):
+            for fn, acc in ((run, t_dp), (run_nc, t_nc)):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(3):
+                    fn()
+                e1.record()
+                e1.synchronize()
+                acc.append(e0.elapsed_time(e1) / 3)
+        exposed = max(0.0, min(t_dp) - min(t_nc))
+        del run_nc, graph_nc
+    loss_val = run()
+    finite = bool(torch.isfinite(loss_val).item())
+    flat = opt.flat_grad
+    for _ in range(2):
+        tdist.all_reduce(flat)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        tdist.all_reduce(flat)
+    e1.record()
+    torch.cuda.synchronize()
+    ar_ms = e0.elapsed_time(e1) / 5
+    t = torch.tensor([-1.0 if exposed is None else exposed, ar_ms], device=dev,
+                     dtype=torch.float64)
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    exposed, ar_ms = t.tolist()
+    exposed = None if exposed < 0 else exposed
+    n_ranks = tdist.get_world_size()
+    grad_bytes = flat.numel() * flat.element_size()
+    trainer.buckets.remove()
+    del run, graph, gout, net, opt, trainer
+    if own_group:
+        tdist.destroy_process_group()
     if rank != 0:
         return None
     return {"metric": TRAIN_METRIC, "config": "BASELINE config 5 (config 3 at world 1): "
-            f"data-parallel trainRGB.py step, {B}/rank x {n_ranks} ranks, {S}x{S}, bf16, eager "
-            "step at every world size, bucketed RCCL all-reduce overlapped with backward",
+            f"data-parallel trainRGB.py step, {B}/rank x {n_ranks} ranks, {S}x{S}, bf16, the "
+            "same code path at every world size: bucketed RCCL all-reduce launched from "
+            "post-accumulate-grad hooks during backward, step captured in a HIP graph",
             "value": round(n_ranks * B * S * S * args.dp_steps / elapsed / 1e6, 3), "unit": "MPix/s",
             "n_ranks": n_ranks, "global_batch": B * n_ranks, "steps": args.dp_steps,
             "warmup": args.dp_warmup, "ms_per_step": round(elapsed / args.dp_steps * 1e3, 3),
-            "exposed_allreduce_ms": round(exposed, 3), "allreduce_ms": round(ar_ms, 3),
-            "gradient_bytes": grad_bytes,
-            "overlap_fraction": None if ar_ms <= 0 else round(max(0.0, 1 - exposed / ar_ms), 3),
+            "backend": "nccl (RCCL)", "hip_graph": graph_err is None and not args.no_graph,
+            "graph_error": graph_err, "buckets": nb, "buckets_launched_in_backward": launched,
+            "exposed_allreduce_ms": None if exposed is None else round(exposed, 4),
+            "allreduce_ms": round(ar_ms, 4), "gradient_bytes": grad_bytes,
+            "overlap_fraction": None if (exposed is None or ar_ms <= 0)
+            else round(min(1.0, max(0.0, 1 - exposed / ar_ms)), 3),
             "loss_finite": finite}
 
 

@@ -1719,6 +1719,8 @@ gather_kernel(long long n, const float* __restrict__ src, const int* __restrict_
 // blocks [blk0[t], blk0[t+1]) cover its elements, 2048 per block; a block finds its task by
 // binary search over blk0.
 constexpr int kGatherChunk = 2048;
+// the bf16 path covers a block's chunk as 256 threads x 8 elements
+static_assert(kGatherChunk == 256 * 8, "gather_multi_kernel: bf16 chunk = 256 threads x 8");
 __global__ void __launch_bounds__(256)
 gather_multi_kernel(int ntask, const long long* __restrict__ tasks,
                     const long long* __restrict__ blk0) {
@@ -1998,7 +2000,15 @@ extern "C" int rgbac_winattn_core_bwd_ex(int dtype, int batch, int h, int w, int
     return e && e[0] == '1';
   }();
   const int dh = channels / heads;
-  if (!force_valu && ((ws == 8 && dh == 24) || (ws == 4 && dh == 10))) {
+  // the MFMA kernel moves q/k/v, dO and dQKV rows in vectors of up to 16 bytes: it needs
+  // 16-byte aligned bases and row strides; any other layout takes the VALU kernel (scalar
+  // accesses, any stride)
+  const int64_t esz = dtype == RGBAC_F32 ? 4 : 2;
+  const bool vec_ok =
+      ((reinterpret_cast<uintptr_t>(qkv) | reinterpret_cast<uintptr_t>(dout) |
+        reinterpret_cast<uintptr_t>(dqkv)) & 15) == 0 &&
+      (ldq * esz) % 16 == 0 && (ldo * esz) % 16 == 0 && (lddq * esz) % 16 == 0;
+  if (!force_valu && vec_ok && ((ws == 8 && dh == 24) || (ws == 4 && dh == 10))) {
     if (dtype == RGBAC_F32) {
       if (ws == 8) launch_attn_bwd_mfma<float, 8, 24>(grid, st, batch, h, w, channels, heads, shift, masked, scale, qkv, ldq, alpha, bias, dout, ldo, dqkv, lddq, bias_partial, amask, amask_nw);
       else launch_attn_bwd_mfma<float, 4, 10>(grid, st, batch, h, w, channels, heads, shift, masked, scale, qkv, ldq, alpha, bias, dout, ldo, dqkv, lddq, bias_partial, amask, amask_nw);

@@ -471,8 +471,10 @@ class ConvFn(Function):
             nb = tc.rows if (has_b and tc.kind != "convt") else 0
             # parameters with an attached fp32 .grad (rgbac.optim.AdamClamp's flat-buffer
             # views): the reduce adds straight into .grad, and autograd gets None -- no
-            # per-parameter accumulate launch (DIRECT_GRAD; off under bucketed DP, whose
-            # all-reduces are triggered by the accumulate hooks)
+            # per-parameter accumulate launch (DIRECT_GRAD).  autograd still runs the
+            # parameter's AccumulateGrad node (with no gradient) once every use of it has
+            # been back-propagated, so its post-accumulate hook -- which launches the
+            # data-parallel bucket all-reduces (rgbac/parallel.py) -- fires after these adds
             bias_p = ctx.bias_param
             acc_w = _direct_grad(weight) if need[1] else None
             acc_b = _direct_grad(bias_p) if (has_b and need[2]) else None

@@ -1,12 +1,19 @@
 """Masked shifted-window attention (reference: layers/masked_win_attention.py).
 
-HIP pipeline per WinBasedAttention call (no permuted copies, no host sync):
-  1. qkv  = rgbac_conv2d 1x1 (Linear(C, 3C) per pixel, MFMA)            [B,H,W,3C]
-  2. core = rgbac_winattn_core: shift + partition + window drop + scores +
-            rel-pos bias + region mask + softmax + P.V + reverse + unshift
-  3. out  = rgbac_conv2d 1x1 (proj) with the MASKSEL epilogue:
-            x + proj(o) on pixels of active windows, x elsewhere
-            (result[~window_mask] = 0 then shortcut + x, :235-249).
+HIP paths per WinBasedAttention call (no permuted copies, no host sync):
+
+* inference, bf16, the model's two shapes -- ONE fused launch per block:
+  ``winblock_kernel`` (ws 8, C 192: rgbac_winattn_block) and ``winblock4_kernel``
+  (ws 4, C 80: rgbac_winattn_block_ws4) gather the shifted window with the
+  partition / window drop folded into index math, run qkv Linear, scores + rel-pos
+  bias + region mask, softmax, P.V and the proj Linear on MFMA with the attention
+  chain in registers, and store x + proj(o) on pixels of active windows, x elsewhere
+  (result[~window_mask] = 0 then shortcut + x, :235-249);
+* every other case (fp32 parity mode, other shapes, training) -- the 3-launch
+  pipeline: qkv = rgbac_conv2d 1x1 [B,H,W,3C]; core = rgbac_winattn_core (shift +
+  partition + window drop + scores + bias + region mask + softmax + P.V + reverse +
+  unshift); out = rgbac_conv2d 1x1 (proj) with the MASKSEL epilogue.  Training runs
+  it through rgbac.autograd (WinAttnFn, HIP backward).
 """
 import os
 

@@ -4,27 +4,39 @@ One process per GPU (torchrun); every rank runs the full model on its shard of
 the global batch.  The only exchange is the gradient all-reduce: the flat fp32
 gradient buffer of rgbac.optim.AdamClamp is cut into ~25 MB buckets in REVERSE
 parameter order (the order backward produces them), and each bucket's
-all-reduce (backend "nccl" = RCCL over xGMI) is launched from the parameters'
-post-accumulate-grad hooks as soon as its last gradient lands -- overlapped with
-the rest of backward on RCCL's own stream.  ``finish()`` waits for all buckets
-and hands the 1/world mean to the optimizer kernel, which applies it before the
-per-element clamp (the reference clamps the global-batch gradient).
+all-reduce (backend "nccl" = RCCL over xGMI) is launched as soon as the last
+gradient of its parameters has landed -- overlapped with the rest of backward
+on RCCL's own stream.  ``finish()`` waits for all buckets and hands the 1/world
+mean to the optimizer kernel, which applies it before the per-element clamp (the
+reference clamps the global-batch gradient).
+
+A bucket's gradients have landed when the post-accumulate-grad hooks of all its
+parameters have fired.  That holds for both ways a gradient reaches the flat
+buffer: autograd's own AccumulateGrad (GDN / EntropyBottleneck
+reparametrisations, the relative-position tables, ...), and the weight-gradient
+reduce kernel adding its sums straight into ``.grad`` (rgbac.autograd
+DIRECT_GRAD: the conv's backward returns None for the weight, yet autograd still
+runs the parameter's AccumulateGrad node -- and its hook -- once every use of the
+parameter has been back-propagated, i.e. after the last add was enqueued).  So
+the data-parallel step runs exactly the backward of the 1-GPU step.
+
+The first step is a learning step: it counts the hook calls of each parameter (a
+parameter that takes no part in the loss -- EntropyBottleneck.quantiles would be
+one if its medians were not in the graph -- never fires) and launches every
+bucket in ``finish()``.  The counts are
+MAX-reduced over the ranks so every rank cuts the same buckets; from step 2 on
+a bucket launches from the notification that completes its count, and
+parameters that never notify sit in a tail bucket reduced in ``finish()``.
+Steps from then on issue the same collectives in the same order on every rank,
+so a step can be captured in a HIP graph (RCCL collectives are stream-ordered).
 """
 import torch
 import torch.distributed as dist
 
 
 class GradBuckets:
-    """Bucketed all-reduce of the flat gradient buffer, launched from post-accumulate-grad
-    hooks.  A bucket is a set of parameters whose flat ranges are all-reduced (one collective
-    per contiguous run) as soon as the last of them has accumulated its gradient.
-
-    Parameters that receive no gradient in a step (EntropyBottleneck.quantiles: only the aux
-    loss, which trainRGB.py never back-propagates, reaches it) would hold their bucket back
-    until ``finish()``, losing its overlap with backward.  After the first step the buckets
-    are re-cut: such parameters move to a tail bucket reduced in ``finish()`` (zeros unless
-    they do receive a gradient later, which stays correct since the tail always waits for
-    the end of backward)."""
+    """Bucketed all-reduce of the flat gradient buffer, launched from the parameters'
+    post-accumulate-grad hooks."""
 
     def __init__(self, params, flat_grad, bucket_bytes=25 << 20, group=None):
         self.params = list(params)
@@ -38,12 +50,18 @@ class GradBuckets:
             off += p.numel()
         assert off == flat_grad.numel()
         self.per = max(1, bucket_bytes // flat_grad.element_size())
+        self.expect = None                 # notifications per parameter per step (learned)
+        self.count = [0] * len(self.params)
         self._cut(list(range(len(self.params) - 1, -1, -1)), [])
-        self.fired = [False] * len(self.params)
-        self.learned = False
         self.active = False
+        # measurement only (bench.py's exposed all-reduce time): issue no collective at all
+        self.skip = False
         self.hooks = [p.register_post_accumulate_grad_hook(self._hook(i))
                       for i, p in enumerate(self.params)]
+
+    @property
+    def learned(self):
+        return self.expect is not None
 
     def _runs(self, idx):
         """Contiguous flat ranges covering params ``idx``."""
@@ -81,18 +99,29 @@ class GradBuckets:
 
     def _hook(self, i):
         def fn(_p):
-            if not self.active:
-                return
-            self.fired[i] = True
-            b = self.owner[i]
-            if b == self.tail:
-                return
-            self.pending[b] -= 1
-            if self.pending[b] == 0:
-                self._launch(b)
+            self._note(i)
         return fn
 
+    def _note(self, i):
+        if not self.active:
+            return
+        self.count[i] += 1
+        if not self.learned:
+            return                         # learning step: every bucket goes out in finish()
+        b = self.owner[i]
+        if b == self.tail:
+            return
+        self.pending[b] -= 1
+        if self.pending[b] == 0:
+            self._launch(b)
+        elif self.pending[b] < 0:
+            raise RuntimeError(f"rgbac.parallel: parameter {i} notified more often than in "
+                               "the learning step (the autograd graph changed between steps)")
+
     def _launch(self, b):
+        if self.skip:
+            self.works[b] = []
+            return
         self.works[b] = [dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM,
                                          group=self.group, async_op=True)
                          for lo, hi in self.buckets[b][0]]
@@ -100,14 +129,19 @@ class GradBuckets:
     def begin(self):
         """Call before loss.backward()."""
         for b, (_, idx) in enumerate(self.buckets):
-            self.pending[b] = len(idx)
+            self.pending[b] = sum(self.expect[i] for i in idx) if self.learned else len(idx)
             self.works[b] = None
-        self.fired = [False] * len(self.params)
+        self.count = [0] * len(self.params)
         self.active = True
 
+    def launched_in_backward(self):
+        """Buckets whose all-reduce went out before finish() in this step."""
+        return sum(w is not None for w in self.works)
+
     def finish(self):
-        """Call after loss.backward(): all-reduce what backward did not launch (parameters
-        without a gradient this step), wait for every bucket; returns 1/world."""
+        """Call after loss.backward(): all-reduce what backward did not launch (the tail, or
+        everything in the learning step), wait for every bucket (stream-ordered: the
+        current stream waits for RCCL's); returns 1/world."""
         self.active = False
         for b in range(len(self.buckets)):
             if self.works[b] is None:
@@ -115,17 +149,15 @@ class GradBuckets:
         for ws in self.works:
             for w in ws:
                 w.wait()
-        if not self.learned and any(self.fired):
-            self.learned = True
+        if not self.learned:
             # every rank must cut the same buckets (else ranks would issue all-reduces of
-            # different ranges and counts): a parameter counts as fired if it fired anywhere
-            fired = torch.tensor(self.fired, dtype=torch.int32, device=self.flat.device)
-            dist.all_reduce(fired, op=dist.ReduceOp.MAX, group=self.group)
-            self.fired = [bool(f) for f in fired.tolist()]
-            quiet = [i for i, f in enumerate(self.fired) if not f]
-            if quiet:
-                order = [i for i in range(len(self.params) - 1, -1, -1) if self.fired[i]]
-                self._cut(order, quiet)
+            # different ranges and counts): every rank takes part, whatever it counted
+            cnt = torch.tensor(self.count, dtype=torch.int32, device=self.flat.device)
+            dist.all_reduce(cnt, op=dist.ReduceOp.MAX, group=self.group)
+            self.expect = [int(c) for c in cnt.tolist()]
+            quiet = [i for i, c in enumerate(self.expect) if c == 0]
+            order = [i for i in range(len(self.params) - 1, -1, -1) if self.expect[i]]
+            self._cut(order, quiet)
         return 1.0 / self.world
 
     def remove(self):
@@ -135,21 +167,29 @@ class GradBuckets:
 
 class DataParallelTrainer:
     """net + AdamClamp + GradBuckets: ``step(loss)`` = backward with overlapped all-reduce,
-    clamp, Adam (one launch)."""
+    clamp, Adam (one launch).
 
-    def __init__(self, net, optimizer, bucket_bytes=25 << 20):
+    Buckets exist whenever a process group is up with more than one rank, or with
+    ``force_buckets`` at any world size (world 1 then runs the real RCCL path: the hooks
+    issue single-rank all-reduces, and the parameters stay bit-identical to the plain
+    step).  ``comm_events``: an optional list receiving, per step, a pair of timing events
+    recorded on the compute stream at the end of backward and after the last bucket has been
+    waited for -- the all-reduce time backward did not hide.  Pass ``external=True`` events
+    (``make_comm_events``) when the step is captured in a HIP graph."""
+
+    def __init__(self, net, optimizer, bucket_bytes=25 << 20, force_buckets=False, group=None):
         self.net, self.opt = net, optimizer
         self.buckets = None
-        # optional exposed-communication probe: a list receiving (end of backward, gradients
-        # reduced) event pairs recorded on the compute stream -- the all-reduce time backward
-        # did not hide
         self.comm_events = None
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
-            self.buckets = GradBuckets(optimizer.params, optimizer.flat_grad, bucket_bytes)
-            # the bucket all-reduces are launched from post-accumulate-grad hooks: keep
-            # autograd's per-parameter accumulation (no in-place weight-gradient adds)
-            from . import autograd as ag
-            ag.DIRECT_GRAD[0] = False
+        if dist.is_available() and dist.is_initialized() and \
+                (force_buckets or dist.get_world_size(group) > 1):
+            self.buckets = GradBuckets(optimizer.params, optimizer.flat_grad, bucket_bytes,
+                                       group=group)
+
+    @staticmethod
+    def make_comm_events(external=False):
+        return (torch.cuda.Event(enable_timing=True, external=external),
+                torch.cuda.Event(enable_timing=True, external=external))
 
     def step(self, loss):
         self.opt.zero_grad()
@@ -159,10 +199,12 @@ class DataParallelTrainer:
         if self.buckets is not None:
             ev = None
             if self.comm_events is not None:
-                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev = self.comm_events if isinstance(self.comm_events, tuple) else \
+                    self.make_comm_events()
                 ev[0].record()
             self.opt.grad_scale = self.buckets.finish()
             if ev is not None:
                 ev[1].record()
-                self.comm_events.append(ev)
+                if isinstance(self.comm_events, list):
+                    self.comm_events.append(ev)
         self.opt.step()

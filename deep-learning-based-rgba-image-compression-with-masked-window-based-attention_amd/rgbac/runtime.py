@@ -675,6 +675,27 @@ def _gauss_ok(t, cout):
     return TILES[t][1] >= cout
 
 
+def _choice_valid(t, preps):
+    """Whether tile ``t`` accepts these (grouped, non-GAUSS) convs: the special tiles have
+    the preconditions their launchers check (csrc/conv.hip RGBAC_REQUIRE); the streaming /
+    persistent / weight-resident tiles take any conv."""
+    if t == TILE_PW:
+        return _pw_ok(preps)
+    if t == TILE_NPATCH:
+        return _npatch_ok(preps)
+    if t == TILE_WSTREAM:
+        return _wstream_ok(preps)
+    if t == TILE_SMALLK:
+        return _smallk_ok(preps)
+    if t == TILE_SPATIAL:
+        return _spatial_ok(preps)
+    if t >= FIRST_PATCH:
+        return t in _patch_tiles(preps)
+    if FIRST_DIRECT <= t < FIRST_DEEP:
+        return preps[0].pk.mode == CONV
+    return True
+
+
 # Split-K tickets for the in-launch reduction (rgbac_conv_args.tile_counters): one zeroed
 # int32 buffer per device shared by every launch -- launches on a stream run one after the
 # other and the last split block of each tile resets its ticket, so it is zero again between
@@ -796,10 +817,15 @@ def launch(preps, force=None):
             choice = _heuristic(mtot, cout, nst)
         if not fixed:
             _tune_cache[key] = choice
-    if choice[0] in FRAG_TILES and not all(isinstance(pr.pk, PackedConv) for pr in preps):
-        # a cached / forced fragment-streamed tile (tuned on a forward PackedConv of the same
-        # shape) handed to a training pack: TPack weights are re-gathered in the plain layout
-        # every step, so a cached fragment-major copy would go stale -- take the shape rule
+    if not gauss and not _choice_valid(choice[0], preps):
+        # a cached / forced tile the C side would refuse for THESE convs: the cache key
+        # (dtype / mode / ksize / stride / shape / cin_pad / cout) does not hold the source
+        # count, the residual operands, the activation or the pack type, so the same key
+        # can come from a conv the special tiles accept (e.g. TILE_PW tuned on a
+        # one-source conv, handed a two-source one), or a fragment-streamed tile tuned on a
+        # forward PackedConv handed a training pack (TPack weights are re-gathered in the
+        # plain layout every step, a cached fragment-major copy would go stale) -- take the
+        # shape rule
         choice = _heuristic(p0.mgrid * p0.nphase * n, max(pr.pk.cout for pr in preps),
                             max(pr.nst for pr in preps))
     if gauss and not (choice[0] == TILE_WSTREAM and _wstream_ok(preps)) and \

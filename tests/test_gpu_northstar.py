@@ -225,3 +225,63 @@ def test_config3_train_step_b16_256_graph_capture(device):
     print(f"config 3: losses {[round(t.item(), 3) for t in losses]}, cos(eager, graph) {cos:.5f}")
     assert cos > 0.99, cos
     assert abs(d1.norm().item() / d0.norm().item() - 1) < 0.05
+
+
+# --------------------------------------------------------------------------------------
+# BASELINE config 2 exactly as bench.py times it: B=8, 256^2, bf16, committed tile cache,
+# HIP graph replay
+# --------------------------------------------------------------------------------------
+BF16_BAR = {"rel_d_bpp": 3e-3, "d_psnr_db": 2e-2, "d_ms_ssim": 2e-3}
+
+
+def test_config2_bf16_headline_b8_256(device):
+    """The headline path itself (bench.py's default line): bench.rgb_net, bench.synth_inputs
+    (seed 0), B=8, 256^2, bf16 compute, the committed tile choices of
+    profiles/tune_fwd_bf16_b8_256.json (no tuning dispatch: the cache covers every launch of
+    the step), the step captured in a HIP graph and replayed -- checked against the fp32 CPU
+    oracle on the same batch.  bf16 bar (stated here; the bench's round-3 lines measured rel
+    dbpp 1e-3, dPSNR 6e-3 dB, dMS-SSIM 6.4e-4 per image): rel |dbpp| < 3e-3 on the batch,
+    |dPSNR| < 2e-2 dB of the batch MSE (trainRGB.py:305), per-image |dMS-SSIM| < 2e-3 of the
+    clamped x_hat (trainRGB.py:308-311).  The graph replay equals the eager forward exactly."""
+    from bench import capture, rgb_net, synth_inputs
+    from oracle import ref_metrics
+    from rgbac import runtime as rt
+    from rgbac.layers.SupplyMask import mask_pyramid
+    tc = os.path.join(ROOT, "profiles", "tune_fwd_bf16_b8_256.json")
+    assert os.path.exists(tc)
+    rt.load_tune_cache(tc)
+    n_cache = len(rt.tune_cache())
+    net = rgb_net()
+    sd = {k: v.detach().cpu().clone() for k, v in net.state_dict().items()}
+    net = net.to(device).set_compute_dtype(torch.bfloat16)
+    x, a = synth_inputs(8, 256, 256, seed=0)
+    xd, ad = x.to(device), a.to(device)
+    _, me = mask_pyramid(ad, 4)
+
+    def step():
+        with torch.no_grad():
+            return net(xd, ad, ad, *me)
+    eager = [t.clone() for t in step()]
+    run, graph, gout = capture(step, False)
+    run()
+    torch.cuda.synchronize()
+    assert len(rt.tune_cache()) == n_cache, "a launch of the headline step was not in the cache"
+    for e, g in zip(eager, gout):
+        assert torch.equal(e, g)
+    x_hat = gout[0].float().cpu()
+    mse, bpp = gout[1].item(), gout[2].item()
+    del run, graph
+    with torch.no_grad():
+        r = ref.rgb_forward(sd, x, a, a, *ref.supply_mask(a)[:4])
+        d_ms = [abs(ref_metrics.ms_ssim(x[i:i + 1], x_hat[i:i + 1].clamp(0, 1),
+                                        data_range=1.0).item() -
+                    ref_metrics.ms_ssim(x[i:i + 1], r[0][i:i + 1].clamp(0, 1),
+                                        data_range=1.0).item()) for i in range(8)]
+    rel_bpp = abs(bpp - r[2].item()) / r[2].item()
+    d_psnr = abs(parity.psnr_db(mse) - parity.psnr_db(r[1].item()))
+    print(f"config 2 bf16 headline: bpp {bpp:.6f} vs {r[2].item():.6f} (rel {rel_bpp:.2e}), "
+          f"PSNR d {d_psnr:.2e} dB, MS-SSIM d max {max(d_ms):.2e}")
+    assert torch.isfinite(gout[0]).all()
+    assert rel_bpp < BF16_BAR["rel_d_bpp"]
+    assert d_psnr < BF16_BAR["d_psnr_db"]
+    assert max(d_ms) < BF16_BAR["d_ms_ssim"]

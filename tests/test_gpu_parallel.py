@@ -87,7 +87,7 @@ def _worker(rank, world, port, q):
         _, me = mask_pyramid(args[1], 4)
         out = net(args[0], args[1], args[1], *me, noise_z=args[2], noise_y=args[3])
         (4096.0 * out[1] + out[2]).backward()
-        launched = sum(w is not None for w in tr.buckets.works)
+        launched = tr.buckets.launched_in_backward()
         nb = len(tr.buckets.buckets)
         opt.grad_scale = tr.buckets.finish()
         opt.step()
@@ -137,3 +137,103 @@ def test_dp_world2_matches_single_process(device):
     # :227-229) -- and had one been, it would sit in a tail bucket (tests/test_parallel.py)
     tail_n = 0 if tail0 is None else 1
     assert l0 == nb0 - tail_n, (l0, nb0, tail0)
+
+
+def _nccl_world1_worker(q):
+    """Child process: the plain 1-GPU step (no process group) vs DataParallelTrainer under a
+    one-rank RCCL process group with the buckets forced on -- 2 eager steps, then the step
+    captured in a HIP graph (the hook-launched RCCL all-reduces inside it) and replayed."""
+    import faulthandler
+    import sys
+    # a hang shows up as this child's Python stacks on stderr (and ends it) before the
+    # parent's queue timeout
+    faulthandler.dump_traceback_later(120, exit=True)
+
+    def say(msg):
+        print(f"[dp nccl world 1] {msg}", file=sys.stderr, flush=True)
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [root, os.path.join(root, "deep-learning-based-rgba-image-compression-with-"
+                                             "masked-window-based-attention_amd")]
+    import torch.distributed as dist
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    say("child up")
+    from bench import capture_train
+    from rgbac import runtime as rt
+    from rgbac.optim import AdamClamp
+    from rgbac.parallel import DataParallelTrainer
+    x, a, nz, ny = [t.cuda() for t in _batch(2)]
+    out = {}
+    with rt.fixed_tiles():
+        net0 = _net()
+        opt0 = AdamClamp(net0.parameters(), lr=1e-4).use_device_step()
+        tr0 = DataParallelTrainer(net0, opt0)
+        assert tr0.buckets is None
+        ref = []
+        for _ in range(6):
+            _step(net0, tr0, x, a, nz, ny)
+            ref.append(opt0.flat.clone())
+        say("reference steps done")
+        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1,
+                                device_id=dev)
+        say("process group up")
+        try:
+            net1 = _net()
+            opt1 = AdamClamp(net1.parameters(), lr=1e-4).use_device_step()
+            tr1 = DataParallelTrainer(net1, opt1, bucket_bytes=4 << 20, force_buckets=True)
+            assert tr1.buckets is not None
+            _step(net1, tr1, x, a, nz, ny)                       # learning step
+            out["launched1"] = tr1.buckets.launched_in_backward()
+            say("learning step done")
+            _step(net1, tr1, x, a, nz, ny)
+            out["launched2"] = tr1.buckets.launched_in_backward()
+            out["nb"] = len(tr1.buckets.buckets)
+            out["tail"] = tr1.buckets.tail
+            torch.cuda.synchronize()
+            out["eq2"] = torch.equal(opt1.flat, ref[1])
+
+            def step():
+                _step(net1, tr1, x, a, nz, ny)
+                return opt1.flat
+            # capture_train: 2 warm steps (3, 4) on a side stream, capture, 2 replays (5, 6)
+            say("eager DP steps done")
+            run, graph, _ = capture_train(step, opt1, dev, False)
+            say("captured and replayed")
+            out["launched_capture"] = tr1.buckets.launched_in_backward()
+            torch.cuda.synchronize()
+            out["eq6"] = torch.equal(opt1.flat, ref[5])
+            out["diff6"] = (opt1.flat - ref[5]).abs().max().item()
+            run()
+            torch.cuda.synchronize()
+            out["moved7"] = not torch.equal(opt1.flat, ref[5])
+            del run, graph
+        finally:
+            dist.destroy_process_group()
+    q.put(out)
+
+
+def test_dp_nccl_world1_buckets_bitexact(device):
+    """the config-5 code path on RCCL -- buckets forced on at world 1 so
+    the post-accumulate-grad hooks issue async RCCL all-reduces during backward (direct
+    weight-gradient adds kept on: the same backward as the 1-GPU step), eager and captured
+    in a HIP graph; the parameters equal the plain step's bit for bit (a one-rank SUM is the
+    identity and the 1/world scale is 1)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_world1_worker, args=(q,))
+    p.start()
+    try:
+        out = q.get(timeout=170)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert p.exitcode == 0
+    print("DP nccl world 1:", out)
+    assert out["launched1"] == 0                         # learning step: all in finish()
+    tail_n = 0 if out["tail"] is None else 1
+    assert out["launched2"] == out["nb"] - tail_n > 1    # then from the hooks, in backward
+    assert out["launched_capture"] == out["nb"] - tail_n
+    assert out["eq2"], "eager DP step differs from the plain step"
+    assert out["eq6"], out["diff6"]
+    assert out["moved7"]

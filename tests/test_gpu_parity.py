@@ -205,6 +205,25 @@ def test_config4_1024_fp32_matches_oracle_fixture(device):
     assert diff.float().mean().item() <= 1e-4
     s = np.array([t.item() for t in out[1:]])
     np.testing.assert_allclose(s, fx["scalars"], rtol=1e-4)
+    # teacher-forced accounting (oracle/parity.py, as the 256^2 north-star tests): the oracle
+    # fed the device's z_hat / y_hat slices, so a flip in slice i is not blamed on slice i+1;
+    # every flip must sit at a near-tie of the measured fp32 noise floor
+    from oracle import parity
+    from rgbac.models._latent import debug_views
+    sd = {k: v.detach().cpu() for k, v in net.state_dict().items()}
+    dev_out = (out[0].cpu(),) + tuple(t.item() for t in out[1:])
+    rep = parity.north_star_report(sd, "rgb", x, a, debug_views(dbg), dev_out)
+    print(f"config4 teacher-forced: flips {rep['flips']} (near-tie {rep['near_tie_flips']}, far "
+          f"{rep['far_flips']}), per slice {rep['per_slice_flips']}, z flips "
+          f"{rep.get('z_flips')}, noise floor {rep['noise_floor']:.2e}, max flip |dd| "
+          f"{rep['max_flip_dd']:.2e}, bits(unflipped) rel {rep['bits_unflipped_rel']:.2e}, "
+          f"dPSNR {rep['tf_d_psnr_db']}, dMS-SSIM {rep['tf_d_ms_ssim']}, "
+          f"max|dx_hat| {rep['tf_max_abs_dx_hat']:.2e}")
+    assert rep["noise_floor"] < 1e-3
+    assert rep["far_flips"] == 0 and rep.get("z_far_flips", 0) == 0
+    assert rep["bits_unflipped_rel"] < 1e-5
+    assert rep["tf_d_psnr_db"] is None or rep["tf_d_psnr_db"] < 1e-4
+    assert rep["tf_d_ms_ssim"] < 1e-4
     # x_hat: fp32 noise everywhere except around the few flipped symbols (a flip moves
     # y_hat by 1 in one latent, i.e. a decoder receptive field of ~100 px)
     xs = out[0][:, :, ::mg.XHAT_STRIDE, ::mg.XHAT_STRIDE].cpu().numpy()

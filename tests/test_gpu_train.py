@@ -319,6 +319,44 @@ def test_winattn_core_bwd_explicit_mask():
         assert nrel(part.cpu(), bias.grad) < 1e-5, ws
 
 
+@pytest.mark.parametrize("ws,C", [(8, 192), (4, 80)])
+@pytest.mark.parametrize("kind", ["half", "rand"])
+def test_winattn_core_bwd_shift_alpha_vs_torch(ws, C, kind):
+    """The MFMA attention-core backward with the Swin shift (region mask of -100,
+    masked_win_attention.py:194-216) AND alpha window dropping (windows judged on the rolled
+    alpha, dropped windows contribute 0: :178-190,235-236), f32, against a torch autograd
+    restatement built from the oracle's window helpers -- so a shared region-id or
+    mask-indexing bug of the kernel pair cannot pass."""
+    g = _gen(91 + ws + len(kind))
+    B, H, W, heads = 2, 16, 24, 8
+    shift, N, d = ws // 2, ws * ws, C // heads
+    qkv = torch.randn((B, H, W, 3 * C), generator=g)
+    dout = torch.randn((B, H, W, C), generator=g)
+    dense = torch.randn((heads, N, N), generator=g) * 0.5
+    al = _alpha(kind, B, H, W, g)[:, 0].contiguous()
+    groups = -(-(B * (H // ws) * (W // ws)) // (64 // N))
+    dq, part = _attn_core_bwd(torch.float32, qkv.cuda(), dense.cuda(), dout.cuda(), al.cuda(),
+                              C, ws, shift, min(groups, 64))
+    x = qkv.clone().requires_grad_(True)
+    bias = dense.clone().requires_grad_(True)
+    xs = torch.roll(x, shifts=(-shift, -shift), dims=(1, 2))
+    a_s = torch.roll(al, shifts=(-shift, -shift), dims=(1, 2)).unsqueeze(-1)
+    win = ref.window_partition(xs, ws).reshape(-1, N, 3, heads, d).permute(2, 0, 3, 1, 4)
+    keep = ref.window_partition(a_s, ws).sum(dim=(1, 2, 3)) != 0
+    assert 0 < int(keep.sum()) < keep.numel()             # both kinds of window present
+    reg = ref.window_partition(ref._region_ids(B, H, W, ws, shift), ws).reshape(-1, N)
+    diff = reg.unsqueeze(1) - reg.unsqueeze(2)
+    rmask = torch.where(diff != 0, -100.0, 0.0)
+    s = (win[0] * d ** -0.5) @ win[1].transpose(-1, -2) + bias + rmask.unsqueeze(1)
+    o = s.softmax(-1) @ win[2]                            # (nWin, heads, N, d)
+    o = o * keep.view(-1, 1, 1, 1)
+    o = o.transpose(1, 2).reshape(-1, ws, ws, C)
+    y = torch.roll(ref.window_reverse(o, ws, H, W), shifts=(shift, shift), dims=(1, 2))
+    y.backward(dout)
+    assert nrel(dq.cpu(), x.grad) < 1e-5
+    assert nrel(part.cpu(), bias.grad) < 1e-5
+
+
 def test_gaussian_slice_grads():
     from rgbac import autograd as ag
     rt = _rt()
@@ -648,3 +686,67 @@ def test_channel_copy_multi(dtype):
             assert torch.equal(p.grad[..., :c], gy[..., off:off + c])
             assert not p.grad[..., c:].any()
             off += c
+
+
+def test_reference_loop_torch_adam_clip_matches_adam_clamp():
+    """The reference's own, unchanged optimizer loop (trainRGB.py:187-198: optimizer.zero_grad();
+    rd_loss.backward(); clip_gradient(optimizer, 5) -- param.grad.data.clamp_ per element;
+    torch.optim.Adam(lr 1e-4).step()) over the HIP codec, against rgbac.optim.AdamClamp (the
+    fused drop-in of INTEGRATION.md §2), 2 steps, fp32, fixed noise: the clamped gradients are
+    bit-identical in both steps (the optimizer does not touch the backward: the training packs
+    are re-gathered from the parameters every step, torch.optim.Adam's in-place updates
+    included) and the parameters agree to fp32 rounding of the Adam arithmetic."""
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    from rgbac.optim import AdamClamp
+    torch.manual_seed(234)
+    base = AutoEncoder().train()
+    g = _gen(64)
+    B, H, W = 2, 64, 64
+    x = (torch.randint(0, 256, (B, 3, H, W), generator=g).float() / 255).cuda()
+    a = torch.ones((B, 1, H, W)).cuda()
+    a[1, :, :, : W // 2] = 0
+    x = torch.where(a > 0, x, a)
+    me = [t.cuda() for t in ref.supply_mask(a.cpu())]
+    nz = (torch.rand((B, 1, 1, 192), generator=g) - 0.5).cuda()
+    ny = (torch.rand((B, 8, 8, 80), generator=g) - 0.5).cuda()
+
+    def clip_gradient(optimizer, grad_clip):                 # trainRGB.py:190-194
+        for group in optimizer.param_groups:
+            for param in group["params"]:
+                if param.grad is not None:
+                    param.grad.data.clamp_(-grad_clip, grad_clip)
+
+    nets = []
+    for _ in range(2):
+        n = AutoEncoder().cuda().train()
+        n.load_state_dict(base.state_dict())
+        nets.append(n)
+    opt_t = torch.optim.Adam(nets[0].parameters(), lr=1e-4)
+    opt_c = AdamClamp(nets[1].parameters(), lr=1e-4, clip=5.0)
+    grads_t, grads_c = [], []
+    for _ in range(2):
+        out = nets[0](x, a, a, *me[:4], noise_z=nz, noise_y=ny)
+        rd_loss = 4096.0 * out[1] + out[2]
+        opt_t.zero_grad()
+        rd_loss.backward()
+        clip_gradient(opt_t, 5)
+        grads_t.append(torch.cat([p.grad.reshape(-1) if p.grad is not None else
+                                  torch.zeros(p.numel(), device=p.device)
+                                  for p in nets[0].parameters()]).clone())
+        opt_t.step()
+        out = nets[1](x, a, a, *me[:4], noise_z=nz, noise_y=ny)
+        opt_c.zero_grad()
+        (4096.0 * out[1] + out[2]).backward()
+        opt_c.step()                                         # clamps flat_grad in place
+        grads_c.append(opt_c.flat_grad.clone())
+    torch.cuda.synchronize()
+    for s in range(2):
+        assert torch.equal(grads_t[s], grads_c[s]), (s, rel(grads_t[s], grads_c[s]))
+    pt = torch.cat([p.detach().reshape(-1) for p in nets[0].parameters()])
+    pc = torch.cat([p.detach().reshape(-1) for p in nets[1].parameters()])
+    p0 = torch.cat([p.detach().reshape(-1) for p in base.parameters()]).cuda()
+    step = (pt - p0).abs().max().item()
+    err = (pt - pc).abs().max().item()
+    print(f"torch.optim.Adam vs AdamClamp after 2 steps: max |dp| {err:.3e}, max step {step:.3e}")
+    assert step > 1e-5                                       # the parameters did move
+    assert err <= 1e-3 * step, (err, step)
