@@ -456,8 +456,9 @@ def capture_train(step, opt, dev, no_graph, before=None):
 def dp_train_record(args, world, rank, dev, dist):
     """BASELINE config 5 inside the driver's own scaling command: the trainRGB.py step
     (forward + backward of 4096*mse + bpp, clamp(+-5), Adam) at 16 images per rank, 256^2, bf16,
-    data-parallel over the ranks of THIS run -- bucketed RCCL all-reduce of the 34 M fp32
-    gradients launched from post-accumulate-grad hooks (rgbac.parallel.DataParallelTrainer),
+    data-parallel over the ranks of THIS run -- bucketed all-reduce of the 34 M fp32 gradients
+    (RCCL called directly, rgbac.parallel.RcclComm) launched from post-accumulate-grad hooks
+    (rgbac.parallel.DataParallelTrainer),
     the step captured in a HIP graph (RCCL collectives included) and replayed.  At world 1
     (plain ``python bench.py``) a one-rank RCCL process group is created and the buckets are
     forced on, so the 1-rank and N-rank numbers run the same code path: same backward, same
@@ -501,6 +502,7 @@ def dp_train_record(args, world, rank, dev, dist):
     torch.cuda.synchronize()
     nb = len(trainer.buckets.buckets)
     launched = trainer.buckets.launched_in_backward()
+    trainer_rccl = trainer.buckets.comm is not None
     graph_err = None
     try:
         run, graph, gout = capture_train(step, opt, dev, args.no_graph)
@@ -540,12 +542,12 @@ def dp_train_record(args, world, rank, dev, dist):
     finite = bool(torch.isfinite(loss_val).item())
     flat = opt.flat_grad
     for _ in range(2):
-        tdist.all_reduce(flat)
+        trainer.buckets.allreduce_all()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(5):
-        tdist.all_reduce(flat)
+        trainer.buckets.allreduce_all()
     e1.record()
     torch.cuda.synchronize()
     ar_ms = e0.elapsed_time(e1) / 5
@@ -569,7 +571,8 @@ def dp_train_record(args, world, rank, dev, dist):
             "value": round(n_ranks * B * S * S * args.dp_steps / elapsed / 1e6, 3), "unit": "MPix/s",
             "n_ranks": n_ranks, "global_batch": B * n_ranks, "steps": args.dp_steps,
             "warmup": args.dp_warmup, "ms_per_step": round(elapsed / args.dp_steps * 1e3, 3),
-            "backend": "nccl (RCCL)", "hip_graph": graph_err is None and not args.no_graph,
+            "backend": "RCCL (direct ncclAllReduce on a comm stream, csrc/comm.cpp)"
+            if trainer_rccl else "torch.distributed", "hip_graph": graph_err is None and not args.no_graph,
             "graph_error": graph_err, "buckets": nb, "buckets_launched_in_backward": launched,
             "exposed_allreduce_ms": None if exposed is None else round(exposed, 4),
             "allreduce_ms": round(ar_ms, 4), "gradient_bytes": grad_bytes,

@@ -2410,7 +2410,16 @@ __device__ __forceinline__ void patch_epilogue(const ConvShared& s, const ConvGr
 //     v_mfma_f32_16x16x32_bf16 from (TN + TM) ds_read_b128 per k-step;
 //   * every per-stage index is carried incrementally (no integer division in the loop);
 //   * CONVT_S2: phases run one after another (9, 6, 6, 4 taps); the epilogue of a phase
-//     runs while the next phase's first stages are already in flight.
+//     runs while the next phase's first stages are already in flight;
+//   * the 5x5 stride-2 conv (Analysis x2 / x3, TransformRGB.py:55-58): polyphase -- with
+//     u = 2y + ky - 2 = 2(y + dy) + qy, the conv is the sum over the four input phases
+//     P_q[i][j] = in[2i + qy][2j + qx] of stride-1 convs with (3 - qy) x (3 - qx) taps
+//     (dy, dx in -1..1, kernel tap (2 dy + qy + 2, 2 dx + qx + 2)), so the M grid is the
+//     output grid and a group (phase, chunk) stages the phase image's (TH+2) x 18 patch --
+//     every input pixel is fetched once per tile (plus the halo) instead of once per tap,
+//     the im2col tiles' 3.3x fetch.  The weights are the plain CONV packing (k = tap *
+//     cin_pad + ci over the 25 taps), walked phase by phase; the four phases accumulate
+//     into one tile and the epilogue runs once.
 template <int TH, int BN, int WGM, int WGN, int NBUF>
 __global__ void __launch_bounds__(512) conv_patch_kernel(const ConvArgsDev args) {
   using T = bf16_t;
@@ -2454,7 +2463,8 @@ __global__ void __launch_bounds__(512) conv_patch_kernel(const ConvArgsDev args)
   if (n0 >= g.cout) return;
   const int y0 = tyi * TH, x0 = txi * TW;
   const bool convt = s.mode == RGBAC_CONVT_S2;
-  const int nph = convt ? 4 : 1;
+  const bool s2 = s.mode == RGBAC_CONV && s.sy == 2;     // polyphase 5x5 stride-2 conv
+  const int nph = (convt || s2) ? 4 : 1;
   const int in_h = s.in_h, in_w = s.in_w, cin_pad = g.cin_pad;
   const int nck = (cin_pad + 63) >> 6;
   const int send0 = g.send0, send1 = g.send1, send2 = g.send2;
@@ -2464,7 +2474,7 @@ __global__ void __launch_bounds__(512) conv_patch_kernel(const ConvArgsDev args)
   const int sld0 = (int)g.sld0, sld1 = (int)g.sld1, sld2 = (int)g.sld2;
   // groups (phase, chunk); group sizes 9 (conv) or 9, 6, 6, 4 (convT phases)
   const int ngroups = nph * nck;
-  const int ns = convt ? nck * 25 : nck * 9;
+  const int ns = nph == 4 ? nck * 25 : nck * 9;
 
   // ---- per-lane DMA geometry (constant through the K loop)
   const int lrow = lane >> 3;
@@ -2477,8 +2487,11 @@ __global__ void __launch_bounds__(512) conv_patch_kernel(const ConvArgsDev args)
     alds[i] = q * 64;
     aoff[i] = (uint32_t)(((n0 + row) * g.k_pad + ((lane & 7) ^ (row & 7)) * 8) * 2);
   }
+  // patch piece of a lane: pixel (r / PW, r % PW) of the (TH+2) x 18 patch, channel chunk c;
+  // pmask bit q: the pixel exists in phase q (s2; bit 0 only otherwise), ppix: its pixel
+  // index in phase 0 (s2: the phase-q pixel is ppix + qy * in_w + qx)
   int ppix[PQ], plds[PQ], pch[PQ];
-  bool pok[PQ];
+  unsigned pmask[PQ];
 #pragma unroll
   for (int i = 0; i < PQ; ++i) {
     const int q = min(wave + NW * i, PPIECE - 1);
@@ -2487,18 +2500,34 @@ __global__ void __launch_bounds__(512) conv_patch_kernel(const ConvArgsDev args)
     plds[i] = q * 64;
     pch[i] = c * 8;
     const int py = r / PW, px = r - (r / PW) * PW;
-    const int iy = y0 - 1 + py, ix = x0 - 1 + px;
-    pok[i] = r < PR && c < 8 && (unsigned)iy < (unsigned)in_h && (unsigned)ix < (unsigned)in_w;
-    ppix[i] = pok[i] ? (b * in_h + iy) * in_w + ix : 0;
+    const bool rc_ok = r < PR && c < 8;
+    if (s2) {
+      const int iy = 2 * (y0 - 1 + py), ix = 2 * (x0 - 1 + px);
+      unsigned m = 0;
+#pragma unroll
+      for (int ph = 0; ph < 4; ++ph)
+        if (rc_ok && (unsigned)(iy + (ph >> 1)) < (unsigned)in_h &&
+            (unsigned)(ix + (ph & 1)) < (unsigned)in_w)
+          m |= 1u << ph;
+      pmask[i] = m;
+      ppix[i] = m ? (b * in_h + iy) * in_w + ix : 0;
+    } else {
+      const int iy = y0 - 1 + py, ix = x0 - 1 + px;
+      const bool ok = rc_ok && (unsigned)iy < (unsigned)in_h && (unsigned)ix < (unsigned)in_w;
+      pmask[i] = ok ? 1u : 0u;
+      ppix[i] = ok ? (b * in_h + iy) * in_w + ix : 0;
+    }
   }
   const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lptr_t)smem);
   const uint32_t lpatch = lbase + NBUF * WSTAGE * 16;
   const size_t phstride = (size_t)g.rows * g.k_pad * 2;     // bytes per convT phase
   const char* const wbase = reinterpret_cast<const char*>(g.w);
 
-#define PATCH_ISSUE(grp_, ck_)                                                                \
+#define PATCH_ISSUE(grp_, ck_, ph_)                                                           \
   do {                                                                                        \
     const uint32_t lpb = lpatch + (uint32_t)(((grp_) & 1) * PSTAGE * 16);                     \
+    const int pbit = s2 ? (ph_) : 0;                                                          \
+    const int pdel = s2 ? ((ph_) >> 1) * in_w + ((ph_) & 1) : 0;                              \
 _Pragma("unroll")                                                                             \
     for (int i = 0; i < PQ; ++i) {                                                            \
       const int ch = ((ck_) << 6) + pch[i];                                                   \
@@ -2506,41 +2535,50 @@ _Pragma("unroll")                                                               
       const char* src = in0 ? sp0 : (in1 ? sp1 : sp2);                                        \
       const int sld = in0 ? sld0 : (in1 ? sld1 : sld2);                                       \
       const int cs = ch - (in0 ? 0 : (in1 ? send0 : send1));                                  \
-      const bool ok = pok[i] & (ch < send2);                                                  \
-      const unsigned off = ((unsigned)ppix[i] * (unsigned)sld + (unsigned)cs) * 2u;           \
+      const bool ok = ((pmask[i] >> pbit) & 1u) && (ch < send2);                              \
+      const unsigned off = ((unsigned)(ppix[i] + pdel) * (unsigned)sld + (unsigned)cs) * 2u;  \
       const void* gp = ok ? (const void*)(src + off) : (const void*)g_zero_page;              \
       dma16_l(gp, lpb + plds[i] * 16);                                                        \
     }                                                                                         \
   } while (0)
 
   // issue-side state: stage weight address, tap / chunk / phase counters, group index
-  int itap = 0, intap = 9, ick = 0, iph = 0, igrp = 0;
+  int itap = 0, intap = 9, ick = 0, iph = 0, igrp = 0, itx = 0, itw = 3;
   const char* wph = wbase;                        // current phase's packed weights
   const char* wst = wbase;                        // current stage's weight column
   const int tapstep = cin_pad * 2;                // bytes from one tap's column to the next
 
+  // s2: the group's taps (ty, tx) are kernel taps (2 ty + qy, 2 tx + qx) of the plain 5x5
+  // packing: +2 taps along a row, +10 - 2 (tw - 1) taps to the next row's first
 #define STAGE_ISSUE(st_)                                                                      \
   do {                                                                                        \
     const uint32_t lst = lbase + (uint32_t)(((st_) % NBUF) * WSTAGE * 16);                    \
 _Pragma("unroll")                                                                             \
     for (int i = 0; i < NAW; ++i) dma16_s(wst, aoff[i], lst + alds[i] * 16);                  \
     if (itap == RT && igrp + 1 < ngroups) {      /* the next group's patch rides here */     \
-      const int nck_ = ick + 1 == nck ? 0 : ick + 1;                                          \
-      PATCH_ISSUE(igrp + 1, nck_);                                                            \
+      const bool last_ck = ick + 1 == nck;                                                    \
+      PATCH_ISSUE(igrp + 1, last_ck ? 0 : ick + 1, last_ck ? iph + 1 : iph);                 \
     }                                                                                         \
-    wst += tapstep;                                                                           \
+    if (s2) {                                                                                 \
+      if (++itx == itw) { itx = 0; wst += (10 - 2 * (itw - 1)) * tapstep; }                   \
+      else wst += 2 * tapstep;                                                                \
+    } else {                                                                                  \
+      wst += tapstep;                                                                         \
+    }                                                                                         \
     if (++itap == intap) {                                                                    \
-      itap = 0; ++igrp;                                                                       \
+      itap = 0; itx = 0; ++igrp;                                                              \
       if (++ick == nck) {                                                                     \
         ick = 0; ++iph;                                                                       \
-        wph += phstride;                                                                      \
-        intap = (3 - (iph >> 1)) * (3 - (iph & 1));                                           \
+        if (!s2) wph += phstride;                                                             \
+        itw = 3 - (iph & 1);                                                                  \
+        intap = (3 - (iph >> 1)) * itw;                                                       \
       }                                                                                       \
-      wst = wph + (ick << 7);                                                                 \
+      wst = s2 ? wbase + (((iph >> 1) * 5 + (iph & 1)) * tapstep) + (ick << 7)                \
+               : wph + (ick << 7);                                                            \
     }                                                                                         \
   } while (0)
 
-  PATCH_ISSUE(0, 0);
+  PATCH_ISSUE(0, 0, 0);
 #pragma unroll
   for (int st = 0; st < NBUF - 1; ++st)
     if (st < ns) STAGE_ISSUE(st);
@@ -2607,16 +2645,18 @@ _Pragma("unroll")                                                               
     if (ctap == cntap) {                          // end of a (phase, chunk) group
       ctap = 0; ctx = 0; ++cgrp;
       toff = convt ? (2 * PW + 2) * RSC : 0;
-      if (++cck == nck) {                         // end of a phase: epilogue
+      if (++cck == nck) {                         // end of a phase: epilogue (s2: the last)
         cck = 0;
-        int nn[TN];
+        if (!s2 || cph == 3) {
+          int nn[TN];
 #pragma unroll
-        for (int j = 0; j < TN; ++j) nn[j] = n0 + wn * TN * 16 + j * 16 + fq * 4;
-        patch_epilogue<TN, TM>(s, g, cph, b, y0 + wm * TM, x0, fr, nn, acc);
+          for (int j = 0; j < TN; ++j) nn[j] = n0 + wn * TN * 16 + j * 16 + fq * 4;
+          patch_epilogue<TN, TM>(s, g, s2 ? 0 : cph, b, y0 + wm * TM, x0, fr, nn, acc);
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
+          for (int j = 0; j < TN; ++j)
 #pragma unroll
-          for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int i = 0; i < TM; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
         ++cph;
         ctw = 3 - (cph & 1);
         cntap = (3 - (cph >> 1)) * ctw;
@@ -3375,10 +3415,13 @@ extern "C" int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroup
                       a->act != RGBAC_ACT_GAUSS &&
                       (a->mode == RGBAC_CONVT_S2 ||
                        (a->ksize == 3 && a->stride == 1 &&
-                        (a->mode == RGBAC_CONV || a->mode == RGBAC_SUBPEL2))) &&
+                        (a->mode == RGBAC_CONV || a->mode == RGBAC_SUBPEL2)) ||
+                       (a->mode == RGBAC_CONV && a->ksize == 5 && a->stride == 2 &&
+                        !fpatch_tile(a->tile))) &&
                       s.Wm % 16 == 0 && s.Hm % th == 0,
-                  "the patch tiles need bf16, ksplit 1, a 3x3 stride-1 conv/subpel or the 5x5/s2 "
-                  "convT, the M grid a multiple of 16 wide and of the tile height high");
+                  "the patch tiles need bf16, ksplit 1, a 3x3 stride-1 conv/subpel, the 5x5/s2 "
+                  "convT or (conv_patch_kernel tiles) the 5x5/s2 conv, the M grid a multiple of "
+                  "16 wide and of the tile height high");
     RGBAC_REQUIRE((long long)a->batch * a->in_h * a->in_w < (1ll << 24),
                   "patch tiles address sources of < 2^24 pixels");
     for (int i = 0; i < ngroups; ++i)

@@ -164,6 +164,11 @@ SIGNATURES = {
     "rgbac_rans_encoder_create": [ctypes.POINTER(ctypes.c_void_p)],
     "rgbac_rans_encoder_destroy": [_VP],
     "rgbac_rans_encoder_put": [_VP, _VP, _VP, _I64, _VP, _I32, _VP, _VP, _I32],
+    "rgbac_comm_load": [ctypes.c_char_p],
+    "rgbac_comm_unique_id": [_VP],
+    "rgbac_comm_init": [_VP, _I32, _I32, _I32, ctypes.POINTER(ctypes.c_void_p)],
+    "rgbac_comm_allreduce_sum": [_VP, _I32, _VP, _I64, _VP],
+    "rgbac_comm_destroy": [_VP],
     "rgbac_rans_encoder_bound": [_VP],
     "rgbac_rans_encoder_flush": [_VP, _VP, _I64, ctypes.POINTER(ctypes.c_int64)],
     "rgbac_rans_decoder_init": [ctypes.POINTER(RansDecoderState), _VP, _I64],

@@ -30,18 +30,76 @@ parameters that never notify sit in a tail bucket reduced in ``finish()``.
 Steps from then on issue the same collectives in the same order on every rank,
 so a step can be captured in a HIP graph (RCCL collectives are stream-ordered).
 """
+import ctypes
+import os
+
 import torch
 import torch.distributed as dist
+
+from . import _lib
+
+
+class RcclComm:
+    """In-place sum all-reduce through RCCL called directly (csrc/comm.cpp: the librccl.so
+    torch itself loaded, one ncclAllReduce per call), on a communication stream of its own:
+    ``allreduce(t)`` makes that stream wait for the current (compute) stream, enqueues the
+    collective there and returns an event; ``wait(ev)`` makes the current stream wait for it.
+    Every step is stream-ordered, so a bucket all-reduce issued from a backward hook overlaps
+    the rest of backward, and the whole step captures into a HIP graph -- no ProcessGroup
+    work object or watchdog thread is involved.  torch.distributed only bootstraps it: rank
+    0's 128-byte unique id is broadcast over ``group`` once."""
+
+    _cache = {}
+
+    @classmethod
+    def get(cls, device, group=None):
+        key = (id(group), device.index, dist.get_world_size(group), dist.get_rank(group))
+        c = cls._cache.get(key)
+        if c is None:
+            c = cls._cache[key] = cls(device, group)
+        return c
+
+    def __init__(self, device, group=None):
+        lib = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+        _lib.call("rgbac_comm_load", lib.encode())
+        self.world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            _lib.call("rgbac_comm_unique_id", ctypes.c_void_p(uid.data_ptr()))
+        if self.world > 1:
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            u = uid.to(device) if dist.get_backend(group) == "nccl" else uid
+            dist.broadcast(u, src=src, group=group)
+            uid = u.cpu()
+        self.comm = ctypes.c_void_p()
+        _lib.call("rgbac_comm_init", ctypes.c_void_p(uid.data_ptr()), self.world, rank,
+                  device.index, ctypes.byref(self.comm))
+        self.device = device
+        self.stream = torch.cuda.Stream(device)
+
+    def allreduce(self, t):
+        cur = torch.cuda.current_stream(t.device)
+        self.stream.wait_stream(cur)
+        _lib.call("rgbac_comm_allreduce_sum", self.comm, _lib.dtype_code(t.dtype), t.data_ptr(),
+                  t.numel(), self.stream.cuda_stream)
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        return ev
+
+    def wait(self, ev):
+        torch.cuda.current_stream(self.device).wait_event(ev)
 
 
 class GradBuckets:
     """Bucketed all-reduce of the flat gradient buffer, launched from the parameters'
     post-accumulate-grad hooks."""
 
-    def __init__(self, params, flat_grad, bucket_bytes=25 << 20, group=None):
+    def __init__(self, params, flat_grad, bucket_bytes=25 << 20, group=None, comm=None):
         self.params = list(params)
         self.flat = flat_grad
         self.group = group
+        self.comm = comm                   # RcclComm, or None: torch.distributed.all_reduce
         self.world = dist.get_world_size(group)
         # param i occupies [off_i, off_i + n_i) of the flat buffer (AdamClamp layout)
         self.offs, off = [], 0
@@ -122,9 +180,26 @@ class GradBuckets:
         if self.skip:
             self.works[b] = []
             return
+        if self.comm is not None:
+            self.works[b] = [self.comm.allreduce(self.flat[lo:hi]) for lo, hi in self.buckets[b][0]]
+            return
         self.works[b] = [dist.all_reduce(self.flat[lo:hi], op=dist.ReduceOp.SUM,
                                          group=self.group, async_op=True)
                          for lo, hi in self.buckets[b][0]]
+
+    def _wait(self, w):
+        if self.comm is not None:
+            self.comm.wait(w)
+        else:
+            w.wait()
+
+    def allreduce_all(self):
+        """The whole flat buffer through the same collective path, outside any step (the
+        bench's standalone all-reduce time)."""
+        if self.comm is not None:
+            self.comm.wait(self.comm.allreduce(self.flat))
+        else:
+            dist.all_reduce(self.flat, op=dist.ReduceOp.SUM, group=self.group)
 
     def begin(self):
         """Call before loss.backward()."""
@@ -148,7 +223,7 @@ class GradBuckets:
                 self._launch(b)
         for ws in self.works:
             for w in ws:
-                w.wait()
+                self._wait(w)
         if not self.learned:
             # every rank must cut the same buckets (else ranks would issue all-reduces of
             # different ranges and counts): every rank takes part, whatever it counted
@@ -172,19 +247,25 @@ class DataParallelTrainer:
     Buckets exist whenever a process group is up with more than one rank, or with
     ``force_buckets`` at any world size (world 1 then runs the real RCCL path: the hooks
     issue single-rank all-reduces, and the parameters stay bit-identical to the plain
-    step).  ``comm_events``: an optional list receiving, per step, a pair of timing events
+    step).  With an RCCL ("nccl") group the buckets go through RcclComm (``rccl=False``:
+    torch.distributed.all_reduce instead, as with gloo).  ``comm_events``: an optional list receiving, per step, a pair of timing events
     recorded on the compute stream at the end of backward and after the last bucket has been
     waited for -- the all-reduce time backward did not hide.  Pass ``external=True`` events
     (``make_comm_events``) when the step is captured in a HIP graph."""
 
-    def __init__(self, net, optimizer, bucket_bytes=25 << 20, force_buckets=False, group=None):
+    def __init__(self, net, optimizer, bucket_bytes=25 << 20, force_buckets=False, group=None,
+                 rccl=None):
         self.net, self.opt = net, optimizer
         self.buckets = None
         self.comm_events = None
         if dist.is_available() and dist.is_initialized() and \
                 (force_buckets or dist.get_world_size(group) > 1):
-            self.buckets = GradBuckets(optimizer.params, optimizer.flat_grad, bucket_bytes,
-                                       group=group)
+            flat = optimizer.flat_grad
+            if rccl is None:               # RCCL directly whenever the group is RCCL's
+                rccl = flat.is_cuda and dist.get_backend(group) == "nccl"
+            comm = RcclComm.get(flat.device, group) if rccl else None
+            self.buckets = GradBuckets(optimizer.params, flat, bucket_bytes, group=group,
+                                       comm=comm)
 
     @staticmethod
     def make_comm_events(external=False):

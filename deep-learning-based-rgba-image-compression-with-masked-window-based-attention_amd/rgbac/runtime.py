@@ -212,10 +212,14 @@ def _patch_tiles(preps):
     a = preps[0].a
     if a.dtype != _lib.BF16 or a.square_input or a.act == ACT["gauss"]:
         return []
+    s2 = a.mode == CONV and a.ksize == 5 and a.stride == 2
     if a.mode == CONVT_S2:
         hm, wm = a.in_h, a.in_w
     elif a.ksize == 3 and a.stride == 1 and a.mode in (CONV, SUBPEL2):
         hm, wm = a.in_h, a.in_w
+    elif s2:
+        # the polyphase strided conv (csrc/conv.hip conv_patch_kernel): the output grid
+        hm, wm = a.out_h, a.out_w
     else:
         return []
     if wm % 16 or a.batch * a.in_h * a.in_w >= (1 << 24):
@@ -227,8 +231,8 @@ def _patch_tiles(preps):
         if all(p.pk.cout_pad >= -(-p.pk.cout // bn) * bn for p in preps):
             out.append(t)
     # fragment-streamed tiles: PackedConv weights only (the training packs are re-gathered
-    # every step in the plain layout) and the whole patch in LDS
-    if all(isinstance(p.pk, PackedConv) for p in preps):
+    # every step in the plain layout) and the whole patch in LDS; no strided conv
+    if not s2 and all(isinstance(p.pk, PackedConv) for p in preps):
         c32 = max(round_up(p.pk.cin_pad, 32) for p in preps)
         for t, (th, bn) in FPATCH_SIG.items():
             if hm % th or (th + 2) * 18 * (c32 // 8 + 2) * 16 > 160 * 1024:

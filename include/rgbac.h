@@ -546,6 +546,18 @@ int rgbac_avgpool2(int planes, int h, int w, const float* x, float* y, void* str
 int rgbac_msssim_combine(int levels, int batch, const float* mcs, const float* ssim_last,
                          const float* weights, float* per_image, float* mean, void* stream);
 
+/* Data-parallel gradient exchange (csrc/comm.cpp; BASELINE config 5 -- the reference trains
+ * on one GPU, DataParallel is commented out at trainRGB.py:374, so no reference interface is
+ * replaced: this is the all-reduce of rgbac/parallel.py's gradient buckets).  RCCL is called
+ * directly on the caller's stream (capturable in a HIP graph); the library is the librccl.so
+ * PyTorch loaded, dlopen'ed by rgbac_comm_load.  The unique id is 128 bytes (rank 0 makes it,
+ * the host side broadcasts it).  rgbac_comm_allreduce_sum: in place, sum, fp32 or bf16. */
+int rgbac_comm_load(const char* librccl_path);
+int rgbac_comm_unique_id(void* id_out);
+int rgbac_comm_init(const void* id, int world, int rank, int device, void** comm);
+int rgbac_comm_allreduce_sum(void* comm, int dtype, void* buf, int64_t count, void* stream);
+int rgbac_comm_destroy(void* comm);
+
 /* Host-side range-ANS coder (csrc/rans.cpp), byte-compatible with compressai.ans:
  * replaces BufferedRansEncoder.encode_with_indexes/flush (:334,:367-368), RansDecoder
  * set_stream/decode_stream (:387-388,:401) and the EntropyModel compress/decompress coders.

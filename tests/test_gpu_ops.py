@@ -639,14 +639,17 @@ PATCH_CASES = [
     ("subpel", 192, 192, 8, 16), ("subpel", 192, 12, 16, 16),
     # the hyperprior's 16x16-grid convs (8..10 k-steps per tap: K-split tiles 51 / 52)
     ("conv", 256, 288, 16, 16), ("subpel", 288, 80, 16, 16), ("conv", 320, 288, 16, 16),
+    # the polyphase 5x5 stride-2 conv (Analysis x2 / x3): H, W = the input size
+    ("conv_s2", 192, 192, 32, 32), ("conv_s2", 120, 192, 48, 32), ("conv_s2", 40, 64, 16, 64),
 ]
 
 
 @pytest.mark.parametrize("mode,cin,cout,H,W", PATCH_CASES)
 def test_conv_patch_tiles(device, mode, cin, cout, H, W):
-    """conv_patch_kernel (tiles 36..41, bf16): ConvTranspose 5x5/s2 (four phases from one
-    staged patch), 3x3 convs (incl. three concatenated sources and a partial last 64-channel
-    chunk) and subpel convs, with GELU / residual epilogues, against PyTorch fp32 on the
+    """conv_patch_kernel (tiles 36..41, 48, 49, bf16): ConvTranspose 5x5/s2 (four phases from
+    one staged patch), 3x3 convs (incl. three concatenated sources and a partial last
+    64-channel chunk), subpel convs and the polyphase 5x5 stride-2 conv (four input phases
+    accumulated into one tile), with GELU / residual epilogues, against PyTorch fp32 on the
     same bf16-rounded operands (tolerance: bf16 output rounding, 1e-2 of the max)."""
     rt = _rt()
     from rgbac.layers.TransformRGB import prep_conv, prep_subpel
@@ -657,14 +660,16 @@ def test_conv_patch_tiles(device, mode, cin, cout, H, W):
         m = nn.ConvTranspose2d(cin, cout, 5, stride=2, padding=2, output_padding=1)
     elif mode == "conv":
         m = nn.Conv2d(cin, cout, 3, padding=1)
+    elif mode == "conv_s2":
+        m = nn.Conv2d(cin, cout, 5, stride=2, padding=2)
     else:
         m = subpel_conv3x3(cin, cout, 2)
     with torch.no_grad():
         for p in m.parameters():
             p.copy_(p.to(torch.bfloat16).float())
     x = torch.randn((B, cin, H, W), generator=g).to(torch.bfloat16).float()
-    r = torch.randn((B, cout, H * (1 if mode == "conv" else 2), W * (1 if mode == "conv" else 2)),
-                    generator=g).to(torch.bfloat16).float()
+    f = {"conv": 1.0, "conv_s2": 0.5}.get(mode, 2.0)
+    r = torch.randn((B, cout, int(H * f), int(W * f)), generator=g).to(torch.bfloat16).float()
     if mode == "convt" and cout <= 4:
         mode = "convt_small"                       # runs as conv3x3 + PixelShuffle (SUBPEL2)
     if mode in ("subpel", "convt_small"):
@@ -676,7 +681,7 @@ def test_conv_patch_tiles(device, mode, cin, cout, H, W):
     m = m.to(device)
     outs = {}
     with torch.no_grad():
-        if mode == "conv" and cin == 120:           # three sources: 80 + 32 + 8 channels
+        if mode in ("conv", "conv_s2") and cin == 120:   # three sources: 80 + 32 + 8 channels
             fs = [rt.to_nhwc(xd[:, a:b], dt) for a, b in ((0, 80), (80, 112), (112, 120))]
             srcs = [f.src() for f in fs]
         else:

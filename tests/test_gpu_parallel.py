@@ -182,6 +182,7 @@ def _nccl_world1_worker(q):
             opt1 = AdamClamp(net1.parameters(), lr=1e-4).use_device_step()
             tr1 = DataParallelTrainer(net1, opt1, bucket_bytes=4 << 20, force_buckets=True)
             assert tr1.buckets is not None
+            assert tr1.buckets.comm is not None              # RCCL called directly
             _step(net1, tr1, x, a, nz, ny)                       # learning step
             out["launched1"] = tr1.buckets.launched_in_backward()
             say("learning step done")
@@ -214,10 +215,10 @@ def _nccl_world1_worker(q):
 
 def test_dp_nccl_world1_buckets_bitexact(device):
     """the config-5 code path on RCCL -- buckets forced on at world 1 so
-    the post-accumulate-grad hooks issue async RCCL all-reduces during backward (direct
-    weight-gradient adds kept on: the same backward as the 1-GPU step), eager and captured
-    in a HIP graph; the parameters equal the plain step's bit for bit (a one-rank SUM is the
-    identity and the 1/world scale is 1)."""
+    the post-accumulate-grad hooks issue RCCL all-reduces (ncclAllReduce on the comm stream,
+    rgbac.parallel.RcclComm) during backward (direct weight-gradient adds kept on: the same
+    backward as the 1-GPU step), eager and captured in a HIP graph; the parameters equal the
+    plain step's bit for bit (a one-rank SUM is the identity and the 1/world scale is 1)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     p = ctx.Process(target=_nccl_world1_worker, args=(q,))
