@@ -147,6 +147,63 @@ __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlockArgs a) 
   const int win = w >> 2, tt = w & 3;                  // its window and token tile in it
   WB_T(0);
 
+  // ---- weight streams (pieces past the end repeat the last one: same bytes to the same
+  // place, so every wave issues as many)
+  auto dma_wq = [&](int p) {
+#pragma unroll
+    for (int i = 0; i < WQ_W; ++i) {
+      int f = w + 8 * i;
+      if (f >= WQF) f = WQF - 1;
+      wb_dma16(a.wq + ((size_t)(p * WQF + f) * 64 + lane) * 8, lds0 + L_WQ + f * 1024);
+    }
+  };
+  auto dma_wp = [&](int u) {
+#pragma unroll
+    for (int i = 0; i < WP_W; ++i) {
+      int f = w + 8 * i;
+      if (f >= WPF) f = WPF - 1;
+      wb_dma16(a.wp + ((size_t)(u * WPF + f) * 64 + lane) * 8, lds0 + L_WP + f * 1024);
+    }
+  };
+  // pair 0's qkv weights are requested first thing: they depend on nothing, and the first
+  // pair's MFMAs wait for them (the proj weights of pairs 0-1 stream behind pair 0; a
+  // workgroup's weight stream, 288 KiB, is what bounds it: every CU pulls its own copy at
+  // ~12 B/cycle, MI355X_MICROARCH.md prologue-burst row)
+  dma_wq(0);
+
+  // ---- this wave's x tile as MFMA fragments: X[ks] = tokens tok0+n, k-chunk 4ks+qq; the
+  // lane's pixel is derived here (the same map as the gather below), so the loads go out
+  // before the first barrier instead of behind the alpha gather's round trip
+  uint4 X[6];
+  {
+    const int gw = blockIdx.x * 2 + win;
+    int pix = -1;
+    if (gw < total) {
+      const int b = gw / (nwx * nwy);
+      const int rem = gw - b * nwx * nwy;
+      const int wy = rem / nwx, wx = rem - wy * nwx;
+      const int lt = 16 * tt + n;
+      int oy = wy * WS + (lt >> 3) + shift; if (oy >= H) oy -= H;
+      int ox = wx * WS + (lt & 7) + shift; if (ox >= W) ox -= W;
+      pix = (b * H + oy) * W + ox;
+    }
+    const bf16_t* row = a.x + (long long)(pix < 0 ? 0 : pix) * a.ldx;
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks)
+      X[ks] = pix < 0 ? make_uint4(0, 0, 0, 0) : *reinterpret_cast<const uint4*>(row + 32 * ks + 8 * qq);
+  }
+
+  // ---- tables (in log2 units: softmax runs on exp2): global reads issued before the gather
+  float* tb = reinterpret_cast<float*>(sm + L_TB);
+  for (int e = tid; e < 225 * 8; e += 512) {           // table [225][8] -> [var][8][225]
+    const int idx = e >> 3, hd = e & 7;
+    const float v = a.table[e];
+    tb[hd * 225 + idx] = v * LOG2E;
+    tb[8 * 225 + hd * 225 + idx] = (v + -100.0f) * LOG2E;   // the shift mask's -100 folded in
+  }
+  float* bq = reinterpret_cast<float*>(sm + L_BQ);
+  for (int e = tid; e < 192; e += 512) bq[e] = a.bproj[e];
+
   // ---- window gather: token -> pixel (cyclic shift folded in), shifted-frame region id
   if (tid < 2) act_s[tid] = a.masked ? 0 : 1;
   __syncthreads();
@@ -171,7 +228,9 @@ __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlockArgs a) 
   __syncthreads();
   const bool act = act_s[win] != 0 && pix_s[tok0] >= 0;         // wave-uniform
   if (act_s[0] == 0 && act_s[1] == 0) {
-    // both windows transparent: out = x on their tokens
+    // both windows transparent: out = x on their tokens.  The weight DMA issued above lands
+    // in this workgroup's LDS: it must complete before the workgroup exits.
+    wb_wait_all();
     for (int e = tid; e < TOK * (C / 8); e += 512) {
       const int t = e / (C / 8), c8 = e - t * (C / 8);
       const int pix = pix_s[t];
@@ -180,50 +239,6 @@ __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlockArgs a) 
             *reinterpret_cast<const uint4*>(a.x + (long long)pix * a.ldx + 8 * c8);
     }
     return;
-  }
-
-  // ---- weight streams (pieces past the end repeat the last one: same bytes to the same
-  // place, so every wave issues as many)
-  auto dma_wq = [&](int p) {
-#pragma unroll
-    for (int i = 0; i < WQ_W; ++i) {
-      int f = w + 8 * i;
-      if (f >= WQF) f = WQF - 1;
-      wb_dma16(a.wq + ((size_t)(p * WQF + f) * 64 + lane) * 8, lds0 + L_WQ + f * 1024);
-    }
-  };
-  auto dma_wp = [&](int u) {
-#pragma unroll
-    for (int i = 0; i < WP_W; ++i) {
-      int f = w + 8 * i;
-      if (f >= WPF) f = WPF - 1;
-      wb_dma16(a.wp + ((size_t)(u * WPF + f) * 64 + lane) * 8, lds0 + L_WP + f * 1024);
-    }
-  };
-  // only pair 0's qkv weights before the first barrier: the proj weights of pairs 0-1 stream
-  // behind pair 0 (a workgroup's weight stream, 288 KiB, is what bounds it: every CU pulls
-  // its own copy at ~12 B/cycle, MI355X_MICROARCH.md prologue-burst row)
-  dma_wq(0);
-
-  // ---- tables (in log2 units: softmax runs on exp2)
-  float* tb = reinterpret_cast<float*>(sm + L_TB);
-  for (int e = tid; e < 225 * 8; e += 512) {           // table [225][8] -> [var][8][225]
-    const int idx = e >> 3, hd = e & 7;
-    const float v = a.table[e];
-    tb[hd * 225 + idx] = v * LOG2E;
-    tb[8 * 225 + hd * 225 + idx] = (v + -100.0f) * LOG2E;   // the shift mask's -100 folded in
-  }
-  float* bq = reinterpret_cast<float*>(sm + L_BQ);
-  for (int e = tid; e < 192; e += 512) bq[e] = a.bproj[e];
-
-  // ---- this wave's x tile as MFMA fragments: X[ks] = tokens tok0+n, k-chunk 4ks+qq
-  uint4 X[6];
-  {
-    const int pix = pix_s[tok0 + n];
-    const bf16_t* row = a.x + (long long)(pix < 0 ? 0 : pix) * a.ldx;
-#pragma unroll
-    for (int ks = 0; ks < 6; ++ks)
-      X[ks] = pix < 0 ? make_uint4(0, 0, 0, 0) : *reinterpret_cast<const uint4*>(row + 32 * ks + 8 * qq);
   }
 
   // ---- per-lane relative-position-bias offsets (head-invariant; +900 h per head), into the

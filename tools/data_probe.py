@@ -1,6 +1,8 @@
 """Time the batched augmentation launch (rgbac/data.py) on COCO-sized sources resident in HBM,
 and the reference-style CPU transform (torch CPU crop+interpolate+flip, oracle/data_ref.py)
-on the same items.  Prints one JSON line."""
+on the same items.  Prints one JSON line.  ``--pipeline``: the whole input pipeline of a DP
+step (worker-side PNG decode + crop, main-process collate + H2D + augment launch) at 16 and
+128 images."""
 import json
 import os
 import random
@@ -59,5 +61,54 @@ def main(B=8, iters=50):
                       "cpu_ms_per_batch": round(cpu_ms, 2), "cpu_threads": torch.get_num_threads()}))
 
 
+def pipeline(per_rank=16, ranks=8, n_png=32, iters=20):
+    """The whole input pipeline of a DP step at BASELINE config 5 (16 images per rank, 128 per
+    step on 8 GPUs): worker side = COCOP3MDataset.__getitem__ (PNG decode + parameter draw +
+    crop) per item on one core, on synthetic 640x480 / 427x640 RGBA PNGs (random pixels:
+    they compress worse than photos, so decode is pessimistic); main process = collate_rgba
+    (pinned) + augment_packed (one H2D copy + one launch) per rank batch.  Prints one JSON line
+    with the rates against the training step's need."""
+    import tempfile
+    from PIL import Image
+    g = np.random.default_rng(1)
+    tmp = tempfile.mkdtemp(prefix="rgbac_png_")
+    shapes = [(480, 640), (427, 640), (640, 480), (500, 375)]
+    for k in range(n_png):
+        h, w = shapes[k % 4]
+        a = g.integers(0, 256, size=(h, w, 4), dtype=np.uint8)
+        a[..., 3] = np.where(g.random((h, w)) < 0.3, 0, 255)
+        Image.fromarray(a, "RGBA").save(os.path.join(tmp, f"{k:04d}.png"))
+    ds = data.COCOP3MDataset(coco_path=tmp, p3m_path=tmp + "_none")
+    t0 = time.perf_counter()
+    items = [ds[k % len(ds)] for k in range(n_png * 2)]
+    worker_ms = (time.perf_counter() - t0) * 1e3 / len(items)
+    dev = torch.device("cuda:0")
+    res = {"png_items": len(items), "worker_ms_per_item_1core": round(worker_ms, 3)}
+    for B in (per_rank, per_rank * ranks):
+        batch_items = [items[k % len(items)] for k in range(B)]
+        data.collate_rgba(batch_items)          # warm-up (torch's first CPU copy pays a one-off)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            batch = data.collate_rgba(batch_items)
+        collate_ms = (time.perf_counter() - t0) * 1e3 / iters
+        batch = {k: v.pin_memory() for k, v in batch.items()}
+        for _ in range(3):
+            data.augment_packed(batch, device=dev)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            out = data.augment_packed(batch, device=dev)
+        torch.cuda.synchronize()
+        main_ms = (time.perf_counter() - t0) * 1e3 / iters
+        res[f"B{B}"] = {"collate_ms": round(collate_ms, 3), "h2d_augment_ms": round(main_ms, 3),
+                        "main_process_img_per_s": round(B / (collate_ms + main_ms) * 1e3, 1)}
+    res["need_img_per_s_per_rank"] = "16 per training step: 16 / 25 ms = 640 img/s (config 3 graph step)"
+    res["workers_needed_per_rank"] = round(640 * worker_ms / 1e3, 2)
+    print(json.dumps(res))
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["--pipeline"]:
+        pipeline()
+    else:
+        main()
