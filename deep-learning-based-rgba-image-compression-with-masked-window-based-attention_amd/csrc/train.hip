@@ -497,18 +497,27 @@ __device__ __forceinline__ void wg_wait_ring(int after) {
   }
 }
 
-template <int TN, int KT, int WR>
-__global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
-  constexpr int BN = 32 * TN, BK = 32 * KT;
+// WGN x WGK waves (2 x 2: 256 threads, the original layout; 2 x 4: 512 threads), each owning a
+// (16 TN) x (16 KT) block of the BN x BK tile.  The 512-thread 128 x 256 tile (TN = KT = 4)
+// moves 48 KiB per 64-pixel stage for 4.2 MFLOP -- twice the MFMAs per DMA piece and per L2
+// byte of the 64 x 128 tile, whose per-stage DMA issue and address VALU (8.4 VALU + 7.6 SALU
+// per MFMA, 45 % of wave cycles issuing: PMC on the slice-stack shape) bounded it.
+template <int TN, int KT, int WR, int WGN = 2, int WGK = 2>
+__global__ void __launch_bounds__(64 * WGN * WGK) wgrad_ring_kernel(const WgradDev a) {
+  constexpr int NW = WGN * WGK, NTH = 64 * NW;
+  constexpr int BN = 16 * TN * WGN, BK = 16 * KT * WGK;
   constexpr int RSG = BN * 2, RSS = BK * 2;       // LDS row bytes (G: BN channels, S: BK k)
+  static_assert(RSG == 128 || RSG % 256 == 0, "G rows: 128 B or multiples of 256 B (swizzle)");
+  static_assert(RSS == 128 || RSS % 256 == 0, "S rows: 128 B or multiples of 256 B (swizzle)");
   constexpr int GB = 64 * RSG, SB = 64 * RSS;     // stage image bytes
-  constexpr int CRS = RSS / 16;                   // 16-B chunks per S row (8 or 16)
-  constexpr int RPS = 64 / CRS;                   // S rows per 1-KiB piece (8 or 4)
+  constexpr int CRS = RSS / 16;                   // 16-B chunks per S row (8, 16 or 32)
+  constexpr int RPS = 64 / CRS;                   // S rows per 1-KiB piece (8, 4 or 2)
   constexpr int CRG = RSG / 16, RPG = 64 / CRG;   // the same for G rows
-  constexpr int PG = GB / 1024 / 4, PS = SB / 1024 / 4;   // pieces per wave per stage (G, S)
+  constexpr int PG = GB / 1024 / NW, PS = SB / 1024 / NW;   // pieces per wave per stage
+  static_assert(PG * NW * 1024 == GB && PS * NW * 1024 == SB, "whole pieces per wave");
   constexpr int PW = PG + PS;
   __shared__ __attribute__((aligned(16))) unsigned char ring[WR * (GB + SB)];
-  __shared__ float bred[256 / BN][BN];
+  __shared__ float bred[NTH / BN][BN];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -533,12 +542,14 @@ __global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
   // 128-B rows: chunk c of row r at c ^ (2 r1 + 4 r3); 256-B rows: c ^ 2 (r&3 + 4 r3)
   // (r_i = bit i of r): conflict-free transposed reads, and rows r + 4 h + 32 kk keep r's
   // swizzle (only row bits 0, 1, 3 enter it)
+  // (rows of >= 256 B: a row is a multiple of 64 banks, so the 256-B-row swizzle -- chunk XORs
+  // below 16 -- spreads the 8 rows of a transposed read over all banks for any such length)
   auto swzG = [](int r) {
-    if constexpr (BN == 64) return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1);
+    if constexpr (RSG == 128) return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1);
     else return 2 * ((r & 3) + 4 * ((r >> 3) & 1));
   };
   auto swzS = [](int r) {
-    if constexpr (BK == 64) return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1);
+    if constexpr (RSS == 128) return 2 * ((r >> 1) & 1) + 4 * ((r >> 3) & 1);
     else return 2 * ((r & 3) + 4 * ((r >> 3) & 1));
   };
 
@@ -548,7 +559,7 @@ __global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
   bool gok[PG];
 #pragma unroll
   for (int j = 0; j < PG; ++j) {
-    const int q = wave + 4 * j;                   // G piece = rows RPG q .. RPG q + RPG - 1
+    const int q = wave + NW * j;                  // G piece = rows RPG q .. RPG q + RPG - 1
     grow[j] = RPG * q + lane / CRG;
     const int c = (lane % CRG) ^ swzG(grow[j]);
     const int n = n0 + 8 * c;
@@ -560,7 +571,7 @@ __global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
   bool sok[PS];
 #pragma unroll
   for (int j = 0; j < PS; ++j) {
-    const int q = wave + 4 * j;                   // S piece = rows RPS q .. RPS q + RPS - 1
+    const int q = wave + NW * j;                  // S piece = rows RPS q .. RPS q + RPS - 1
     srow[j] = RPS * q + lane / CRS;
     const int c = (lane % CRS) ^ swzS(srow[j]);
     const int k = k0 + 8 * c;
@@ -613,7 +624,7 @@ __global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
 #pragma unroll
     for (int j = 0; j < PG; ++j) {
       const bool ok = gok[j] && mb + grow[j] < mend;
-      wg_dma16(ok ? (const void*)gp[j] : zp, lg + (uint32_t)((wave + 4 * j) * 1024));
+      wg_dma16(ok ? (const void*)gp[j] : zp, lg + (uint32_t)((wave + NW * j) * 1024));
       gp[j] += gstep;
     }
 #pragma unroll
@@ -629,7 +640,7 @@ __global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
         src = ok ? (const void*)(ssrc[j] + (size_t)((pb[j] * a.in_h + iy) * a.in_w + ix) * sld[j])
                  : zp;
       }
-      wg_dma16(src, ls + (uint32_t)((wave + 4 * j) * 1024));
+      wg_dma16(src, ls + (uint32_t)((wave + NW * j) * 1024));
       if (!pdirect) {                             // advance to the next stage's pixel
         px[j] += adx;
         py[j] += ady;
@@ -645,7 +656,7 @@ __global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
 #pragma unroll
     for (int j = 0; j < KT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bacc = 0.0f;
-  const int wn = wave >> 1, wk = wave & 1;
+  const int wn = wave / WGK, wk = wave % WGK;
   const int fi = lane & 15, fq = lane >> 4;
   int aoff[TN], boff[KT];                         // per-lane fragment read offsets (bytes)
   {
@@ -672,7 +683,7 @@ __global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
     const unsigned char* Gs = ring + (it % WR) * (GB + SB);
     const unsigned char* Ss = Gs + GB;
     if (do_bias) {                                // G column sums: row groups x BN channels
-      constexpr int NRG = 256 / BN, RPR = 64 / NRG;
+      constexpr int NRG = NTH / BN, RPR = 64 / NRG;
       const int c = tid % BN, rg = tid / BN;
 #pragma unroll 4
       for (int r = RPR * rg; r < RPR * rg + RPR; ++r)
@@ -718,7 +729,7 @@ __global__ void __launch_bounds__(256) wgrad_ring_kernel(const WgradDev a) {
         if (k < a.k_pad && n < a.n_pad) P[(size_t)n * a.k_pad + k] = acc[tn][tk][r];
       }
   if (do_bias) {
-    constexpr int NRG = 256 / BN;
+    constexpr int NRG = NTH / BN;
     bred[tid / BN][tid % BN] = bacc;
     __syncthreads();
     if (tid < BN && n0 + tid < a.n_pad) {
@@ -1865,6 +1876,15 @@ extern "C" int rgbac_act_bwd(int dtype, int act, float act_param, int64_t npix, 
   return check_launch("act_bwd_kernel");
 }
 
+// RGBAC_WGRAD_BIG=0: keep the 64 x 128 tile on the wide shapes (A/B switch)
+static bool wgrad_big_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("RGBAC_WGRAD_BIG");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 extern "C" int rgbac_conv_wgrad(const rgbac_wgrad_args* a, void* stream) {
   RGBAC_REQUIRE(a != nullptr, "null args");
   RGBAC_REQUIRE(a->dtype == RGBAC_F32 || a->dtype == RGBAC_BF16, "dtype");
@@ -1909,9 +1929,13 @@ extern "C" int rgbac_conv_wgrad(const rgbac_wgrad_args* a, void* stream) {
   d.part = a->partial;
   d.bpart = a->bias_partial;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  // 64 x 128 tiles when K is wide (8 MFMAs per k-step per wave on 12 transposed reads)
+  // 64 x 128 tiles when K is wide (8 MFMAs per k-step per wave on 12 transposed reads);
+  // 128 x 256 tiles (512 threads) when N and K are both wide (rgbac.autograd.wgrad_tile mirrors
+  // this rule to size the pixel split)
   const bool wide = a->dtype == RGBAC_BF16 && a->k_pad >= 512;
+  const bool big = wide && !a->square_input && a->n_pad >= 128 && wgrad_big_enabled();
   dim3 grid(wide ? (a->k_pad + 127) / 128 : a->k_pad / 64, a->n_pad / 64, a->nsplit);
+  if (big) grid = dim3((a->k_pad + 255) / 256, (a->n_pad + 127) / 128, a->nsplit);
   // bf16 without the squared input: the LDS-DMA ring kernel (RGBAC_WGRAD_RING=0: the
   // register-staged kernel, A/B switch)
   static const bool ring_env = [] {
@@ -1921,7 +1945,9 @@ extern "C" int rgbac_conv_wgrad(const rgbac_wgrad_args* a, void* stream) {
   if (a->dtype == RGBAC_BF16 && !a->square_input && ring_env) {
     // (128 x 128 tiles, wgrad_ring_kernel<4, 4, 3>: one workgroup per CU -- measured no faster
     // on the slice-stack shapes and -4 % on the training step, so not dispatched)
-    if (wide) {
+    if (big) {
+      hipLaunchKernelGGL((wgrad_ring_kernel<4, 4, 3, 2, 4>), grid, dim3(512), 0, st, d);
+    } else if (wide) {
       hipLaunchKernelGGL((wgrad_ring_kernel<2, 4, 3>), grid, dim3(256), 0, st, d);
     } else {
       hipLaunchKernelGGL((wgrad_ring_kernel<2, 2, 4>), grid, dim3(256), 0, st, d);

@@ -256,10 +256,23 @@ def train_conv_of(m, kind, wshape, stride, segs, device):
 _SLAB_FLOATS = 16 << 20         # cap of nsplit * n_pad * k_pad (64 MiB of fp32 partials)
 
 
-def _nsplit(tiles, M, slab):
-    """Pixel splits: enough workgroups to fill the chip (~1024), each split >= 512 pixels,
-    and the fp32 partial slabs bounded (their write + reduce read is pure overhead)."""
-    want = max(1, -(-1024 // tiles))
+WGRAD_BIG = os.environ.get("RGBAC_WGRAD_BIG", "1") != "0"
+
+
+def wgrad_tile(dtype, n_pad, k_pad, square):
+    """(output tiles per pixel split, workgroups wanted in flight) of rgbac_conv_wgrad -- the
+    tile rule of csrc/train.hip: 128 x 256 tiles (512 threads, one workgroup per CU) when bf16,
+    no squared input, n_pad >= 128 and k_pad >= 512; otherwise counted in 64 x 64 units with
+    ~1024 workgroups wanted (the 64 x 64 / 64 x 128 tiles run two workgroups per CU)."""
+    if dtype == torch.bfloat16 and not square and n_pad >= 128 and k_pad >= 512 and WGRAD_BIG:
+        return -(-k_pad // 256) * -(-n_pad // 128), 256
+    return (k_pad // 64) * (n_pad // 64), 1024
+
+
+def _nsplit(tiles, M, slab, target=1024):
+    """Pixel splits: enough workgroups to fill the chip (``target``), each split >= 512
+    pixels, and the fp32 partial slabs bounded (their write + reduce read is pure overhead)."""
+    want = max(1, -(-target // tiles))
     cap = max(1, _SLAB_FLOATS // slab)
     return int(max(1, min(want, -(-M // 512), cap, 1024)))
 
@@ -272,8 +285,8 @@ def wgrad(G, S, ksize, stride, pad, square, k_pad, fmap, numel, nbias=0, bias_fr
     dev = G.t.device
     n_pad = round_up(G.ldc, 64)
     M = G.B * G.H * G.W
-    tiles = (k_pad // 64) * (n_pad // 64)
-    ns = _nsplit(tiles, M, n_pad * k_pad)
+    tiles, target = wgrad_tile(G.t.dtype, n_pad, k_pad, square)
+    ns = _nsplit(tiles, M, n_pad * k_pad, target)
     part = torch.empty(ns * n_pad * k_pad, dtype=_F32, device=dev)
     bpart = None
     if nbias and bias_from_g:

@@ -750,3 +750,54 @@ def test_reference_loop_torch_adam_clip_matches_adam_clamp():
     print(f"torch.optim.Adam vs AdamClamp after 2 steps: max |dp| {err:.3e}, max step {step:.3e}")
     assert step > 1e-5                                       # the parameters did move
     assert err <= 1e-3 * step, (err, step)
+
+
+@pytest.mark.parametrize("cin,cout,k,stride,hw,nsrc", [
+    (224, 128, 3, 1, 16, 2),      # slice-stack conv, two sources: the 128 x 256 tile
+    (96, 192, 3, 1, 16, 1),       # n_pad 192: a half-filled second N tile
+    (192, 192, 5, 2, 32, 1),      # Analysis 5x5/s2 (stride-2 S pieces)
+    (120, 224, 3, 1, 8, 3),       # three sources, ragged K tile (k_pad 1088)
+    (96, 96, 3, 1, 16, 1),        # 96 output channels: n_pad 128, partly empty N tile
+])
+def test_wgrad_wide_tiles_vs_torch(cin, cout, k, stride, hw, nsrc):
+    """rgbac.autograd.wgrad on the shapes the 512-thread 128 x 256 weight-gradient tile takes
+    (bf16, n_pad >= 128, k_pad >= 512; csrc/train.hip wgrad_ring_kernel<4, 4, 3, 2, 4>) and
+    their bias sums, against torch.nn.grad.conv2d_weight in fp32 on the same bf16-valued
+    operands (only the fp32 summation order differs: 1e-4 norm-wise)."""
+    from rgbac import autograd as ag
+    rt = _rt()
+    g = _gen(cin + cout + k + hw + nsrc)
+    B = 4
+    ho = hw // stride
+    x = torch.randn((B, cin, hw, hw), generator=g).bfloat16().float()
+    gy = torch.randn((B, cout, ho, ho), generator=g).bfloat16().float()
+    dev = torch.device("cuda")
+    if nsrc == 1:
+        cuts = [(0, cin)]
+    elif nsrc == 2:
+        cuts = [(0, 80), (80, cin)]
+    else:
+        cuts = [(0, 80), (80, 112), (112, cin)]
+    S = [rt.to_nhwc(x[:, a:b].to(dev), torch.bfloat16) for a, b in cuts]
+    G = rt.to_nhwc(gy.to(dev), torch.bfloat16)
+    n_pad = rt.round_up(G.ldc, 64)
+    cin_pad = sum(f.ldc for f in S)
+    k_pad = rt.round_up(k * k * cin_pad, 64)
+    tiles, target = ag.wgrad_tile(torch.bfloat16, n_pad, k_pad, False)
+    assert target == 256, "the shape must take the wide tile"
+    # slab slot (n, tap, channel of the concatenated padded sources) -> dense (n, c, ky, kx)
+    fmap = torch.full((n_pad, k_pad), -1, dtype=torch.int32)
+    pos, off = [], 0
+    for f, (a, b) in zip(S, cuts):
+        pos.extend(range(off, off + (b - a)))
+        off += f.ldc
+    for n in range(cout):
+        for tap in range(k * k):
+            for c, pc in enumerate(pos):
+                fmap[n, tap * cin_pad + pc] = ((n * cin + c) * k + tap // k) * k + tap % k
+    numel = cout * cin * k * k
+    dw, db = ag.wgrad(G, S, k, stride, k // 2, False, k_pad, fmap.to(dev), numel, nbias=cout)
+    torch.cuda.synchronize()
+    want = torch.nn.grad.conv2d_weight(x, (cout, cin, k, k), gy, stride=stride, padding=k // 2)
+    assert nrel(dw.view(cout, cin, k, k), want) < 1e-4
+    assert nrel(db, gy.sum(dim=(0, 2, 3))) < 1e-4
