@@ -100,6 +100,29 @@ __device__ __forceinline__ float gelu_fast(float x) {
 }
 
 
+// GELU'(v) = Phi(v) + v phi(v) with the Abramowitz & Stegun 7.1.26 erfc of the forward's
+// gelu_fast (|erf error| <= 1.5e-7; exp(-v^2/2) shared by both terms): ~15 instructions
+// instead of erfcf + expf.  bf16 only (the f32 parity path keeps erfcf).
+__device__ __forceinline__ float gelu_grad_fast(float v) {
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752440f, fabsf(v), 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = __builtin_amdgcn_exp2f(v * v * -0.72134752044448170368f);   // exp(-v^2/2)
+  const float q = p * t * e;                     // erfc(|v| / sqrt 2)
+  const float cdf = v >= 0.0f ? fmaf(-0.5f, q, 1.0f) : 0.5f * q;
+  return fmaf(0.39894228040143267794f * v, e, cdf);
+}
+
+// exact GELU'(v) = Phi(v) + v phi(v) (erfcf + expf; the same expression as train.hip's
+// t_cdf(v) + v * t_phi(v)): the f32 parity path
+__device__ __forceinline__ float gelu_grad_exact(float v) {
+  return 0.5f * erfcf(-0.70710678118654752440f * v) +
+         v * (0.39894228040143267794f * expf(-0.5f * v * v));
+}
+
+
 // Lane exchanges without an LDS round trip (gfx950 v_permlane16_swap / v_permlane32_swap;
 // __shfl_xor is a ds_bpermute).  With the same value in both operands the swap returns
 // {the lower row's / half's value, the upper one's} on both lanes of a pair.

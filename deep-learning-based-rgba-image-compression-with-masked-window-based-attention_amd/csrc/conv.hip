@@ -162,6 +162,20 @@ __device__ __forceinline__ void load_res(const void* ptr, long long ld, long lon
   }
 }
 
+// Input gradient through the producer's activation (ACT_DGELU / ACT_DLRELU, res0 = the
+// producer's pre-activation z): acc * act'(z), the activation backward folded into the
+// consumer's input-gradient conv (rgbac.autograd deferred activations).  Same arithmetic as
+// train.hip's act_bwd on dy = acc: the fast derivative for bf16, the exact one for f32.
+template <typename T>
+__device__ __forceinline__ float dact_apply(int act, float p, float acc, float z) {
+  if (act == RGBAC_ACT_DGELU)
+    return acc * (sizeof(T) == 4 ? gelu_grad_exact(z) : gelu_grad_fast(z));
+  return z > 0.0f ? acc : acc * p;
+}
+__host__ __device__ __forceinline__ bool is_dact(int act) {
+  return act == RGBAC_ACT_DGELU || act == RGBAC_ACT_DLRELU;
+}
+
 template <typename T>
 __device__ __forceinline__ void epilogue4_body(const ConvShared& s, const ConvGroup& g,
                                                long long opix, int n, float (&v)[4]);
@@ -249,7 +263,9 @@ __device__ __forceinline__ void epilogue4_fin(const ConvShared& s, const ConvGro
   const float (&r1)[4] = in.r1;
 #pragma unroll
   for (int r = 0; r < 4; ++r)
-    v[r] = s.act == RGBAC_ACT_SQBWD ? r0[r] + 2.0f * r1[r] * v[r] : v[r] + r0[r];
+    v[r] = s.act == RGBAC_ACT_SQBWD ? r0[r] + 2.0f * r1[r] * v[r]
+           : is_dact(s.act)         ? dact_apply<T>(s.act, s.act_param, v[r], r0[r])
+                                    : v[r] + r0[r];
   if (g.zout) {
     T* z = reinterpret_cast<T*>(g.zout) + opix * g.zld + g.out_coff + n;
     if (n + 3 < g.cout) {
@@ -409,7 +425,9 @@ __device__ __forceinline__ void epilogue_row(const ConvShared& s, const ConvGrou
       float zv[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        zv[r] = s.act == RGBAC_ACT_SQBWD ? r0[j][r] + 2.0f * r1[j][r] * vv[r] : vv[r] + r0[j][r];
+        zv[r] = s.act == RGBAC_ACT_SQBWD ? r0[j][r] + 2.0f * r1[j][r] * vv[r]
+                : is_dact(s.act)         ? dact_apply<T>(s.act, s.act_param, vv[r], r0[j][r])
+                                         : vv[r] + r0[j][r];
       T* z = reinterpret_cast<T*>(g.zout) + opix * g.zld + g.out_coff + nn[j];
       if (nn[j] + 3 < g.cout) {
         Elem<T>::st4(z, zv);
@@ -421,7 +439,9 @@ __device__ __forceinline__ void epilogue_row(const ConvShared& s, const ConvGrou
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float x = s.act == RGBAC_ACT_SQBWD ? r0[j][r] + 2.0f * r1[j][r] * vv[r] : vv[r] + r0[j][r];
+      float x = s.act == RGBAC_ACT_SQBWD ? r0[j][r] + 2.0f * r1[j][r] * vv[r]
+                : is_dact(s.act)         ? dact_apply<T>(s.act, s.act_param, vv[r], r0[j][r])
+                                         : vv[r] + r0[j][r];
       switch (s.act) {
         case RGBAC_ACT_GELU: x = gelu_t<T>(x); break;
         case RGBAC_ACT_RELU: x = x > 0.f ? x : 0.f; break;
@@ -2332,7 +2352,9 @@ __device__ __forceinline__ void patch_epi(const ConvShared& s, const ConvGroup& 
           float t[4];
           Elem<T>::ld4(r0 + opix * ld0 + nn[j], t);
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[j][r] += t[r];
+          for (int r = 0; r < 4; ++r)
+            v[j][r] = ACT == RGBAC_ACT_DGELU ? dact_apply<T>(s.act, s.act_param, v[j][r], t[r])
+                                             : v[j][r] + t[r];
         }
     }
     if constexpr (ACT == RGBAC_ACT_GELU) {
@@ -2377,6 +2399,8 @@ __device__ __forceinline__ void patch_epilogue(const ConvShared& s, const ConvGr
     patch_epi<TN, TM, RGBAC_ACT_GELU>(s, g, ph, b, yrow0, x0 + fr, nn, acc, pbias);
   } else if (lean && s.act == RGBAC_ACT_RELU) {
     patch_epi<TN, TM, RGBAC_ACT_RELU>(s, g, ph, b, yrow0, x0 + fr, nn, acc, pbias);
+  } else if (lean && is_dact(s.act)) {     // both folded activation backwards (s.act)
+    patch_epi<TN, TM, RGBAC_ACT_DGELU>(s, g, ph, b, yrow0, x0 + fr, nn, acc, pbias);
   } else {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -3246,6 +3270,10 @@ static int fill_group(const rgbac_conv_args* a, int ntaps_max, ConvGroup& g) {
                 "zout needs zout_ldc % 4 == 0 and no GAUSS epilogue");
   RGBAC_REQUIRE(a->act != RGBAC_ACT_SQBWD || (a->res0 && a->res1 && !a->bias),
                 "SQBWD needs res0 (direct gradient), res1 (x) and no bias");
+  RGBAC_REQUIRE(!is_dact(a->act) || (a->res0 && !a->res1 && !a->res2 && !a->bias && !a->zout &&
+                                      a->mode != RGBAC_SUBPEL2 && !a->square_input),
+                "DGELU / DLRELU need res0 (the producer's pre-activation) and no bias, res1, res2, "
+                "zout, subpel store or squared input");
   g.zout = a->zout;
   g.zld = a->zout_ldc;
   g.cnt = a->tile_counters;
@@ -3309,7 +3337,7 @@ extern "C" int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroup
   RGBAC_REQUIRE(a->batch > 0 && a->in_h > 0 && a->in_w > 0, "bad input shape");
   RGBAC_REQUIRE(a->tile >= 0 && a->tile < kNumTiles, "tile index out of range");
   RGBAC_REQUIRE(a->ksplit >= 1 && a->ksplit <= 64, "ksplit must be 1..64");
-  RGBAC_REQUIRE(a->act >= RGBAC_ACT_NONE && a->act <= RGBAC_ACT_SQBWD, "act");
+  RGBAC_REQUIRE(a->act >= RGBAC_ACT_NONE && a->act <= RGBAC_ACT_DLRELU, "act");
   for (int i = 1; i < ngroups; ++i) {
     const rgbac_conv_args* b = &args[i];
     RGBAC_REQUIRE(b->dtype == a->dtype && b->mode == a->mode && b->batch == a->batch &&

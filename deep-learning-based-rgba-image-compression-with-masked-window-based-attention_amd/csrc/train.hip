@@ -51,21 +51,6 @@ __device__ __forceinline__ long long ediv(long long e, int d, double rd, int& re
 // (GATE: y = r1*sigmoid(v); GDN: y = r1/sqrt(v); IGDN: y = r1*sqrt(v)).
 // Channels [C, ld) of the outputs are written as zeros.  One thread per group of
 // 4 channels of a pixel (vector loads/stores; all leading dims are multiples of 4).
-// GELU'(v) = Phi(v) + v phi(v) with the Abramowitz & Stegun 7.1.26 erfc of the forward's
-// gelu_fast (|erf error| <= 1.5e-7; exp(-v^2/2) shared by both terms): ~15 instructions
-// instead of erfcf + expf.  bf16 only (the f32 parity path keeps erfcf).
-__device__ __forceinline__ float gelu_grad_fast(float v) {
-  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f * 0.70710678118654752440f, fabsf(v), 1.0f));
-  float p = fmaf(1.061405429f, t, -1.453152027f);
-  p = fmaf(p, t, 1.421413741f);
-  p = fmaf(p, t, -0.284496736f);
-  p = fmaf(p, t, 0.254829592f);
-  const float e = __builtin_amdgcn_exp2f(v * v * -0.72134752044448170368f);   // exp(-v^2/2)
-  const float q = p * t * e;                     // erfc(|v| / sqrt 2)
-  const float cdf = v >= 0.0f ? fmaf(-0.5f, q, 1.0f) : 0.5f * q;
-  return fmaf(0.39894228040143267794f * v, e, cdf);
-}
-
 template <bool FAST>
 __device__ __forceinline__ void act_bwd1(int act, float slope, float g, float v, float a,
                                          bool on, float& gz, float& gr) {
@@ -737,6 +722,203 @@ __global__ void __launch_bounds__(64 * WGN * WGK) wgrad_ring_kernel(const WgradD
 #pragma unroll
       for (int g2 = 1; g2 < NRG; ++g2) sum += bred[g2][tid];
       a.bpart[(size_t)split * a.n_pad + n0 + tid] = sum;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Patch weight gradient for the narrow-output 3x3 convs (bf16, stride 1, pad 1, one source,
+// <= 32 output channels: the DSE's 32 -> 32 convs at full resolution, the slice stacks'
+// 128 -> 8 / 16 tails).  The ring kernel's im2col stages re-read each source pixel once per
+// tap (9x the source bytes through L2 -> LDS) and pads N to a 64-wide tile (2-8x the MFMAs);
+// here a workgroup stages one 8 x 32-pixel output patch of G and its 10 x 34 source halo
+// (one 32-channel block) ONCE per patch by LDS-DMA, and every tap reads the halo at a shifted
+// row: the 32 pixels of one output row segment are 32 consecutive halo rows.
+//   LDS rows are pixels of 64 B (32 channels); 16-B chunk c of row r sits at c ^ 2*bit3(r),
+//   which keeps the transposed fragment reads (rows base + 8q + {0..3}, +4) of every
+//   32-lane half on 64 distinct banks for ANY base row (exhaustively checked offline), so the
+//   tap shift costs no conflicts.
+//   The 18 (tap, 16-channel half) pairs of the block are dealt to the 4 waves (5/5/4/4); each
+//   wave runs all 8 row segments of the patch for its pairs and both 16-channel n tiles, so the
+//   accumulators never cross waves: each lane stores its own slab elements.
+//   Double-buffered over the workgroup's run of patches (m_chunk = patches per split); the
+//   slab layout [split][n_pad][k_pad], k = tap * cin_pad + channel, is the ring kernel's, so
+//   wgrad_reduce is unchanged.
+constexpr int kWpTH = 8, kWpTW = 32, kWpPW = kWpTW + 2;
+constexpr int kWpSRows = (kWpTH + 2) * kWpPW;          // 340 staged source pixels
+constexpr int kWpSPieces = (kWpSRows + 15) / 16;       // 22 one-KiB pieces of 16 rows
+constexpr int kWpGPieces = kWpTH * kWpTW / 16;         // 16
+constexpr int kWpBuf = (kWpSPieces + kWpGPieces) * 1024;
+
+__device__ __forceinline__ int wp_swz(int r) { return 2 * ((r >> 3) & 1); }
+
+template <int NT>
+__global__ void __launch_bounds__(256) wgrad_patch_kernel(const WgradDev a) {
+  __shared__ __attribute__((aligned(16))) unsigned char ring[2 * kWpBuf];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // XCD-contiguous (channel block fastest, split): the channel blocks of one split read the
+  // same G patches from one L2
+  int cb, split;
+  {
+    const int nwg = gridDim.x * gridDim.y;
+    int t = blockIdx.x + gridDim.x * blockIdx.y;
+    const int xcd = t & 7, q = nwg >> 3, r = nwg & 7;
+    t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (t >> 3);
+    cb = t % gridDim.x;
+    split = t / gridDim.x;
+  }
+  const int H = a.Hg, W = a.Wg;
+  const int pw = W / kWpTW, ppi = pw * (H / kWpTH);
+  const int P = a.M / (kWpTH * kWpTW);
+  const int pbeg = split * a.m_chunk;
+  const int pend = min(pbeg + a.m_chunk, P);
+  const bool do_bias = a.bpart && cb == 0;
+  const void* const zp = (const void*)g_wgrad_zero;
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(wg_lptr_t)ring);
+
+  // ---- per-lane DMA geometry (fixed over the patches)
+  constexpr int PSW = (kWpSPieces + 3) / 4, PGW = kWpGPieces / 4;
+  const int nps = (kWpSPieces - wave + 3) / 4;          // this wave's S pieces (6 or 5)
+  int s_rel[PSW], s_i[PSW], s_j[PSW], s_c[PSW];
+  bool s_on[PSW];
+  const int choff = (cb * 32) * 2;
+#pragma unroll
+  for (int j = 0; j < PSW; ++j) {
+    const int q = wave + 4 * j;                         // S piece = halo rows 16 q .. 16 q + 15
+    const int R = 16 * q + (lane >> 2);
+    s_c[j] = ((lane & 3) ^ wp_swz(R)) * 16;             // the global chunk this lane fetches
+    s_i[j] = R / kWpPW;
+    s_j[j] = R - s_i[j] * kWpPW;
+    s_on[j] = q < kWpSPieces && R < kWpSRows;
+    s_rel[j] = (s_i[j] - 1) * W + (s_j[j] - 1);         // pixel offset from the patch origin
+  }
+  int g_rel[PGW], g_c[PGW];
+  bool g_on[PGW];
+#pragma unroll
+  for (int j = 0; j < PGW; ++j) {
+    const int R = 16 * (wave + 4 * j) + (lane >> 2);
+    const int c = (lane & 3) ^ wp_swz(R);
+    g_rel[j] = (R >> 5) * W + (R & 31);
+    g_on[j] = 8 * c < a.gch;
+    g_c[j] = c * 16;
+  }
+  const char* const sbase = reinterpret_cast<const char*>(a.sp0) + choff;
+  const long long sld2 = a.sld0 * 2, ldg2 = a.ldg * 2;
+  const char* const gbase = reinterpret_cast<const char*>(a.g);
+
+  auto issue = [&](int p, int buf) {
+    const int b = p / ppi, rem = p - b * ppi;
+    const int y0 = (rem / pw) * kWpTH, x0 = (rem - (rem / pw) * pw) * kWpTW;
+    const long long pix0 = ((long long)b * H + y0) * W + x0;
+    const uint32_t ls = lbase + (uint32_t)(buf * kWpBuf);
+    const uint32_t lg = ls + kWpSPieces * 1024;
+#pragma unroll
+    for (int j = 0; j < PSW; ++j) {
+      if (j < nps) {
+        const int y = y0 + s_i[j] - 1, x = x0 + s_j[j] - 1;
+        const bool ok = s_on[j] && (unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W;
+        wg_dma16(ok ? (const void*)(sbase + (pix0 + s_rel[j]) * sld2 + s_c[j]) : zp,
+                 ls + (uint32_t)((wave + 4 * j) * 1024));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < PGW; ++j)
+      wg_dma16(g_on[j] ? (const void*)(gbase + (pix0 + g_rel[j]) * ldg2 + g_c[j]) : zp,
+               lg + (uint32_t)((wave + 4 * j) * 1024));
+  };
+
+  // ---- this wave's (tap, channel half) pairs: e = wave + 4 i < 18
+  f32x4 acc[5][NT];
+#pragma unroll
+  for (int i = 0; i < 5; ++i)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc = 0.0f;
+  const int fi = lane & 15, fq = lane >> 4, cq = fi & 3;
+  const int ra0 = 8 * fq + (fi >> 2);
+  int aoff[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) aoff[t] = ra0 * 64 + 16 * ((2 * t + (cq >> 1)) ^ wp_swz(ra0)) + 8 * (cq & 1);
+
+  if (pbeg < pend) issue(pbeg, 0);
+  for (int p = pbeg, it = 0; p < pend; ++p, ++it) {
+    const int buf = it & 1;
+    if (p + 1 < pend) {
+      issue(p + 1, buf ^ 1);
+      if (nps == PSW) wg_wait_vm<PSW + PGW>();
+      else wg_wait_vm<PSW - 1 + PGW>();
+    } else {
+      wg_wait_vm<0>();
+    }
+    __syncthreads();                                     // patch p landed for every wave
+    const unsigned char* Ss = ring + buf * kWpBuf;
+    const unsigned char* Gs = Ss + kWpSPieces * 1024;
+    if (do_bias) {                                       // G column sums: 8 row groups x 32
+      const int c = tid & 31, rg = tid >> 5;
+#pragma unroll 4
+      for (int r = 32 * rg; r < 32 * rg + 32; ++r)
+        bacc += bf2f(*reinterpret_cast<const uint16_t*>(
+            Gs + r * 64 + 16 * ((c >> 3) ^ wp_swz(r)) + (c & 7) * 2));
+    }
+#pragma unroll 1
+    for (int yy = 0; yy < kWpTH; ++yy) {
+      uint4 A[NT];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const unsigned char* q = Gs + aoff[t] + yy * 32 * 64;
+        const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)q);
+        const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)(q + 4 * 64));
+        const uint2 u0 = __builtin_bit_cast(uint2, a0), u1 = __builtin_bit_cast(uint2, a1);
+        A[t] = make_uint4(u0.x, u0.y, u1.x, u1.y);
+      }
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const int e = wave + 4 * i;
+        if (e < 18) {                                    // wave-uniform
+          const int tap = e >> 1, u = e & 1;
+          const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+          const int r0 = (yy + ky) * kWpPW + kx + ra0, r1 = r0 + 4;
+          const int ch = 2 * u + (cq >> 1);
+          const v4s b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4s_ptr)(Ss + r0 * 64 + 16 * (ch ^ wp_swz(r0)) + 8 * (cq & 1)));
+          const v4s b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4s_ptr)(Ss + r1 * 64 + 16 * (ch ^ wp_swz(r1)) + 8 * (cq & 1)));
+          const uint2 u0 = __builtin_bit_cast(uint2, b0), u1 = __builtin_bit_cast(uint2, b1);
+          const uint4 B = make_uint4(u0.x, u0.y, u1.x, u1.y);
+#pragma unroll
+          for (int t = 0; t < NT; ++t) mma_step<bf16_t>(acc[i][t], A[t], B);
+        }
+      }
+    }
+    __syncthreads();                                     // buf free for patch p + 2
+  }
+  // slab: lane holds D[n = 16 t + 4 fq + r][channel = 16 u + fi] of pair (tap, u)
+  float* Pp = a.part + (size_t)split * a.n_pad * a.k_pad;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int e = wave + 4 * i;
+    if (e < 18) {
+      const int tap = e >> 1, u = e & 1;
+      const int k = tap * a.cin_pad + cb * 32 + 16 * u + fi;
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = 16 * t + 4 * fq + r;
+          if (n < a.gch) Pp[(size_t)n * a.k_pad + k] = acc[i][t][r];
+        }
+    }
+  }
+  if (do_bias) {
+    float* bred = reinterpret_cast<float*>(ring);        // [8][32], the buffers are free
+    bred[tid] = bacc;
+    __syncthreads();
+    if (tid < 32 && tid < a.gch) {
+      float s = bred[tid];
+#pragma unroll
+      for (int g2 = 1; g2 < 8; ++g2) s += bred[32 * g2 + tid];
+      a.bpart[(size_t)split * a.n_pad + tid] = s;
     }
   }
 }
@@ -1885,6 +2067,20 @@ static bool wgrad_big_enabled() {
   return on;
 }
 
+// The patch kernel's shapes (rgbac.autograd.wgrad_tile mirrors this rule to size the split):
+// bf16, 3x3 stride 1 pad 1, one source of whole 32-channel blocks, <= 32 output channels,
+// the grid 8-row x 32-column patches of the input grid.  RGBAC_WGRAD_PATCH=0 turns it off.
+static bool wgrad_patch_ok(const rgbac_wgrad_args* a) {
+  static const bool on = [] {
+    const char* e = getenv("RGBAC_WGRAD_PATCH");
+    return !(e && e[0] == '0');
+  }();
+  return on && a->dtype == RGBAC_BF16 && !a->square_input && a->ksize == 3 && a->stride == 1 &&
+         a->pad == 1 && a->nsrc == 1 && a->g_channels <= 32 && a->cin_pad % 32 == 0 &&
+         a->grid_w % kWpTW == 0 && a->grid_h % kWpTH == 0 && a->in_h == a->grid_h &&
+         a->in_w == a->grid_w;
+}
+
 extern "C" int rgbac_conv_wgrad(const rgbac_wgrad_args* a, void* stream) {
   RGBAC_REQUIRE(a != nullptr, "null args");
   RGBAC_REQUIRE(a->dtype == RGBAC_F32 || a->dtype == RGBAC_BF16, "dtype");
@@ -1942,6 +2138,17 @@ extern "C" int rgbac_conv_wgrad(const rgbac_wgrad_args* a, void* stream) {
     const char* e = getenv("RGBAC_WGRAD_RING");
     return !(e && e[0] == '0');
   }();
+  if (wgrad_patch_ok(a)) {
+    // patches of 8 x 32 output pixels; nsplit workgroups per 32-channel source block
+    const long long P = M / (kWpTH * kWpTW);
+    d.m_chunk = (int)((P + a->nsplit - 1) / a->nsplit);
+    const dim3 pgrid(a->cin_pad / 32, a->nsplit);
+    if (a->g_channels > 16)
+      hipLaunchKernelGGL((wgrad_patch_kernel<2>), pgrid, dim3(256), 0, st, d);
+    else
+      hipLaunchKernelGGL((wgrad_patch_kernel<1>), pgrid, dim3(256), 0, st, d);
+    return check_launch("wgrad_patch_kernel");
+  }
   if (a->dtype == RGBAC_BF16 && !a->square_input && ring_env) {
     // (128 x 128 tiles, wgrad_ring_kernel<4, 4, 3>: one workgroup per CU -- measured no faster
     // on the slice-stack shapes and -4 % on the training step, so not dispatched)

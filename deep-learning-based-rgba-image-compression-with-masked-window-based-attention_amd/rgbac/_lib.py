@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("RGBAC_LIB_PATH") or os.path.join(_HERE, "librgbac_hip
 
 F32, BF16 = 0, 1
 ACT = dict(none=0, gelu=1, relu=2, lrelu=3, tanh_half=4, gate=5, gdn=6, igdn=7, masksel=8,
-           gauss=9, sqbwd=10)
+           gauss=9, sqbwd=10, dgelu=11, dlrelu=12)
 CONV, CONVT_S2, SUBPEL2 = 0, 1, 2
 
 

@@ -269,6 +269,18 @@ def wgrad_tile(dtype, n_pad, k_pad, square):
     return (k_pad // 64) * (n_pad // 64), 1024
 
 
+WGRAD_PATCH = os.environ.get("RGBAC_WGRAD_PATCH", "1") != "0"
+
+
+def wgrad_patch_ok(dtype, gch, S, ksize, stride, pad, square, grid_h, grid_w):
+    """csrc/train.hip wgrad_patch_ok: the 8 x 32-pixel patch kernel's shapes (bf16, 3x3
+    stride 1 pad 1, one source of whole 32-channel blocks, <= 32 output channels)."""
+    s0 = S[0]
+    return (WGRAD_PATCH and dtype == torch.bfloat16 and not square and ksize == 3 and
+            stride == 1 and pad == 1 and len(S) == 1 and gch <= 32 and s0.ldc % 32 == 0 and
+            grid_w % 32 == 0 and grid_h % 8 == 0 and s0.H == grid_h and s0.W == grid_w)
+
+
 def _nsplit(tiles, M, slab, target=1024):
     """Pixel splits: enough workgroups to fill the chip (``target``), each split >= 512
     pixels, and the fp32 partial slabs bounded (their write + reduce read is pure overhead)."""
@@ -285,8 +297,14 @@ def wgrad(G, S, ksize, stride, pad, square, k_pad, fmap, numel, nbias=0, bias_fr
     dev = G.t.device
     n_pad = round_up(G.ldc, 64)
     M = G.B * G.H * G.W
-    tiles, target = wgrad_tile(G.t.dtype, n_pad, k_pad, square)
-    ns = _nsplit(tiles, M, n_pad * k_pad, target)
+    if wgrad_patch_ok(G.t.dtype, G.ldc, S, ksize, stride, pad, square, G.H, G.W):
+        # one workgroup per (32-channel block, run of 8 x 32-pixel patches): ~512 in flight
+        # (two per CU), each at least 2 patches so the double-buffered staging overlaps
+        tiles = S[0].ldc // 32
+        ns = int(max(1, min(-(-512 // tiles), M // 512, _SLAB_FLOATS // (n_pad * k_pad))))
+    else:
+        tiles, target = wgrad_tile(G.t.dtype, n_pad, k_pad, square)
+        ns = _nsplit(tiles, M, n_pad * k_pad, target)
     part = torch.empty(ns * n_pad * k_pad, dtype=_F32, device=dev)
     bpart = None
     if nbias and bias_from_g:
@@ -352,12 +370,35 @@ _NEEDS_Z = {"gelu", "relu", "lrelu", "tanh_half", "gate", "gdn", "igdn"}
 
 
 class ConvCall:
-    """Non-tensor description of one training conv (ctx of ConvFn)."""
-    __slots__ = ("tc", "src_C", "act", "act_param", "square")
+    """Non-tensor description of one training conv (ctx of ConvFn).  ``defer``: the conv
+    returns (z, act(z)) and leaves its activation backward to its consumer; ``src_act`` /
+    ``src_param``: this conv's source is such a deferred output -- its input-gradient conv
+    applies the producer's activation backward in its epilogue (DGELU / DLRELU)."""
+    __slots__ = ("tc", "src_C", "act", "act_param", "square", "defer", "src_act", "src_param")
 
-    def __init__(self, tc, src_C, act, act_param, square=False):
+    def __init__(self, tc, src_C, act, act_param, square=False, defer=False, src_act=None,
+                 src_param=0.0):
         self.tc, self.src_C, self.act, self.act_param = tc, list(src_C), act, act_param
-        self.square = square
+        self.square, self.defer, self.src_act, self.src_param = square, defer, src_act, src_param
+
+
+class ActFeat(Feat):
+    """Output of a deferred-activation conv (``conv_t(..., defer=True)``): ``t`` = act(z)
+    (not autograd-tracked), ``pre`` = z (tracked).  Only a single-source ``conv_t`` may
+    consume it: that conv routes the gradient to ``pre`` through its input-gradient
+    epilogue, so the act_bwd pass (dy and z read, dL/dz written) never runs."""
+    __slots__ = ("pre", "dact", "dparam")
+
+    def __init__(self, t, C, pre, dact, dparam):
+        super().__init__(t, C)
+        self.pre, self.dact, self.dparam = pre, dact, dparam
+
+
+# the DGELU epilogue takes act_bwd's bf16 derivative (the fast form); RGBAC_GELU_BWD_EXACT=1
+# (act_bwd's exact-erfc A/B switch) therefore also keeps the activation backward unfolded
+DEFER_ACT = (os.environ.get("RGBAC_DEFER_ACT", "1") != "0" and
+             os.environ.get("RGBAC_GELU_BWD_EXACT", "0") in ("", "0"))
+_DEFERRABLE = {"gelu": "dgelu", "relu": "dlrelu", "lrelu": "dlrelu"}
 
 
 def _act_bwd(act, slope, dy, z, r1, sel, C, want_r1):
@@ -389,7 +430,7 @@ def _direct_grad(p):
 
 class ConvFn(Function):
     @staticmethod
-    def forward(ctx, call, weight, bias, res0, res1, res2, sel, *srcs):
+    def forward(ctx, call, weight, bias, res0, res1, res2, sel, zsrc, *srcs):
         tc = call.tc
         dt = srcs[0].dtype
         feats = [Feat(t, c) for t, c in zip(srcs, call.src_C)]
@@ -419,24 +460,32 @@ class ConvFn(Function):
         ctx.has = (bias is not None, res0 is not None, res1 is not None, res2 is not None)
         ctx.shape = (f0.B, Ho, Wo, Cs)
         keep_r1 = res1 if call.act in ("gate", "gdn", "igdn") else None
-        ctx.save_for_backward(weight, None if z is None else z.t, keep_r1, sel, *srcs)
+        ctx.save_for_backward(weight, None if (z is None or call.defer) else z.t, keep_r1, sel,
+                              zsrc, *srcs)
         if sel is not None:
             ctx.mark_non_differentiable(sel)
+        if call.defer:
+            ctx.mark_non_differentiable(out.t)
+            ctx.set_materialize_grads(False)
+            return z.t, out.t
         return out.t
 
     @staticmethod
-    def backward(ctx, dy_t):
+    def backward(ctx, dy_t, *_):
         call = ctx.call
         tc = call.tc
-        weight, z_t, r1_t, sel, *srcs = ctx.saved_tensors
+        weight, z_t, r1_t, sel, zsrc, *srcs = ctx.saved_tensors
         has_b, has0, has1, has2 = ctx.has
         B, Ho, Wo, Cs = ctx.shape
+        assert dy_t is not None, "deferred-activation conv output without a consumer gradient"
         dy = Feat(dy_t.contiguous(), Cs)
         dt = dy.t.dtype
         act = call.act
         z = None if z_t is None else Feat(z_t, Cs)
         r1 = None if r1_t is None else Feat(r1_t, Cs)
-        if act == "none":
+        if act == "none" or call.defer:
+            # deferred: dy_t is already dL/dz (the consumer's input-gradient epilogue applied
+            # this conv's activation backward)
             dz, dr1 = dy, None
         else:
             dz, dr1 = _act_bwd(act, call.act_param, dy, z, r1, sel, Cs,
@@ -461,23 +510,33 @@ class ConvFn(Function):
         need = ctx.needs_input_grad
         # ---- input gradients (one grouped launch over the sources)
         g_srcs = [None] * len(srcs)
+        g_zsrc = None
         preps = []
         idxs = []
         for i, f in enumerate(feats):
-            if not need[7 + i]:
+            folded = call.src_act is not None and i == 0
+            if not (need[7] if folded else need[8 + i]):
                 continue
             pk = tc.bwd_pack(i, dt, weight.detach().contiguous())
             o = new_feat(f.B, f.H, f.W, f.C, dt, f.t.device)   # zero-filled iff padded
             if call.square:
                 preps.append(rt.prepare(pk, [G.src()], out=o, act="sqbwd", res0=dr1,
                                         res1=f, bias=False))
+            elif folded:
+                # dL/dz of the producer = (W^T G) * act'(z): its activation backward here
+                preps.append(rt.prepare(pk, [G.src()], out=o, act=call.src_act,
+                                        act_param=call.src_param, res0=Feat(zsrc, f.C),
+                                        bias=False))
             else:
                 preps.append(rt.prepare(pk, [G.src()], out=o, bias=False))
             idxs.append(i)
         if preps:
             outs = rt.launch(preps)
             for i, o in zip(idxs, outs):
-                g_srcs[i] = o.t
+                if call.src_act is not None and i == 0:
+                    g_zsrc = o.t
+                else:
+                    g_srcs[i] = o.t
         # ---- weight / bias gradients
         g_w = g_b = None
         if need[1] or (has_b and need[2]):
@@ -510,14 +569,27 @@ class ConvFn(Function):
             if not direct:
                 g_w = dw.view(weight.shape)
                 g_b = db
-        return (None, g_w, g_b, g_res0, g_res1, g_res2, None, *g_srcs)
+        return (None, g_w, g_b, g_res0, g_res1, g_res2, None, g_zsrc, *g_srcs)
 
 
 def conv_t(m, srcs, act="none", act_param=0.0, res0=None, res1=None, res2=None, sel=None,
-           kind=None, weight=None, bias=None, square=False):
-    """Training conv of module ``m`` over Feat sources -> Feat (autograd-tracked)."""
+           kind=None, weight=None, bias=None, square=False, defer=False):
+    """Training conv of module ``m`` over Feat sources -> Feat (autograd-tracked).
+    ``defer=True`` (GELU / (Leaky)ReLU, no post-activation residual): return an ActFeat whose
+    only consumer is the next single-source conv_t, which folds this activation's backward
+    into its input-gradient conv (RGBAC_DEFER_ACT=0 turns the folding off)."""
     import torch.nn as nn
     dev = srcs[0].t.device
+    src_act, src_param, zsrc = None, 0.0, None
+    if any(isinstance(f, ActFeat) for f in srcs):
+        assert len(srcs) == 1 and not square, "a deferred activation feeds one plain conv"
+        f = srcs[0]
+        src_act, zsrc = f.dact, f.pre
+        src_param = f.dparam
+    defer = defer and DEFER_ACT
+    if defer:
+        assert act in _DEFERRABLE and res1 is None and res2 is None and sel is None \
+            and not square and kind != "gdn", "deferrable: GELU / ReLU / LeakyReLU epilogue only"
     segs = [(f.C, f.ldc) for f in srcs]
     w = m.weight if weight is None else weight
     b = getattr(m, "bias", None) if bias is None else bias
@@ -531,14 +603,16 @@ def conv_t(m, srcs, act="none", act_param=0.0, res0=None, res1=None, res2=None, 
         stride = m.stride[0]
     wshape = tuple(w.shape) if w.dim() == 4 else (w.shape[0], w.shape[1], 1, 1)
     tc = train_conv_of(m, kind, wshape, stride, segs, dev)
-    call = ConvCall(tc, [f.C for f in srcs], act, act_param, square)
+    call = ConvCall(tc, [f.C for f in srcs], act, act_param, square, defer, src_act, src_param)
     w4 = w if w.dim() == 4 else w.reshape(wshape)
     out = ConvFn.apply(call, w4, b, None if res0 is None else res0.t,
                        None if res1 is None else res1.t, None if res2 is None else res2.t,
-                       sel, *[f.t for f in srcs])
-    if kind == "subpel":
-        return Feat(out, tc.cout // 4)
-    return Feat(out, tc.cout)
+                       sel, zsrc, *[f.t for f in srcs])
+    C = tc.cout // 4 if kind == "subpel" else tc.cout
+    if defer:
+        z_t, o_t = out
+        return ActFeat(o_t, C, z_t, _DEFERRABLE[act], act_param if act == "lrelu" else 0.0)
+    return Feat(out, C)
 
 
 # --------------------------------------------------------------------------

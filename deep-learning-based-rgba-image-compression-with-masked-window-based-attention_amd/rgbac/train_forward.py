@@ -35,8 +35,8 @@ def gdn_t(g, x):
 
 def residual_unit_t(u, x):
     """Masked_Attention.py:150-169."""
-    t = conv_t(u.conv[0], [x], act="gelu")
-    t = conv_t(u.conv[2], [t], act="gelu")
+    t = conv_t(u.conv[0], [x], act="gelu", defer=True)
+    t = conv_t(u.conv[2], [t], act="gelu", defer=True)
     return conv_t(u.conv[4], [t], act="gelu", res0=x)
 
 
@@ -95,7 +95,7 @@ def attention_block_t(blk, x, mask):
 
 def enhancement_t(e, x, post=None):
     act, slope = _act_of(e.relu)
-    t = conv_t(e.conv1, [x], act=act, act_param=slope)
+    t = conv_t(e.conv1, [x], act=act, act_param=slope, defer=act != "none")
     return conv_t(e.conv2, [t], res0=x, res2=post)
 
 
@@ -129,7 +129,8 @@ def synthesis_t(D, y, md2, md3):
 
 
 def _seq_t(seq, x):
-    """conv / GELU / ... / conv (the hyper transforms and slice stacks)."""
+    """conv / GELU / ... / conv (the hyper transforms and slice stacks).  A GELU followed by
+    another conv of the stack is deferred into that conv's input-gradient epilogue."""
     mods = list(seq)
     t = x
     i = 0
@@ -138,19 +139,21 @@ def _seq_t(seq, x):
         act = "none"
         if i + 1 < len(mods) and isinstance(mods[i + 1], nn.GELU):
             act = "gelu"
+        step = 2 if act != "none" else 1
+        defer = act != "none" and i + step < len(mods)
         if isinstance(m, nn.Sequential):            # compressai subpel_conv3x3
             assert isinstance(m[1], nn.PixelShuffle) and m[1].upscale_factor == 2
-            t = conv_t(m[0], [t], act=act, kind="subpel")
+            t = conv_t(m[0], [t], act=act, kind="subpel", defer=defer)
         else:
-            t = conv_t(m, [t], act=act)
-        i += 2 if act != "none" else 1
+            t = conv_t(m, [t], act=act, defer=defer)
+        i += step
     return t
 
 
 def resblock_t(b, x):
     """AutoEncoderMask_Journal.py:96-110: conv1x1+ReLU, conv3x3+ReLU, conv1x1, + x."""
-    t = conv_t(b.conv1, [x], act="relu")
-    t = conv_t(b.conv2, [t], act="relu")
+    t = conv_t(b.conv1, [x], act="relu", defer=True)
+    t = conv_t(b.conv2, [t], act="relu", defer=True)
     return conv_t(b.conv3, [t], res0=x)
 
 
@@ -223,8 +226,8 @@ def latent_t(model, y, training, noise_z=None, noise_y=None):
         hat, bits = ag.gauss_t(y, i * cs, mu, sc, nyi)
         lrp = model.lrp_transforms[i]
         lsup = ag.cat_t([ms, hat])
-        t = conv_t(lrp[0], [lsup], act="gelu")
-        t = conv_t(lrp[2], [t], act="gelu")
+        t = conv_t(lrp[0], [lsup], act="gelu", defer=True)
+        t = conv_t(lrp[2], [t], act="gelu", defer=True)
         yh.append(conv_t(lrp[4], [t], act="tanh_half", res1=hat))
         ybits = bits if ybits is None else ybits + bits
     return ag.cat_t(yh), ybits, zbits

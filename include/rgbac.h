@@ -59,6 +59,12 @@ enum rgbac_act {
                               (training) or NULL.  One N tile, ksplit 1.          */
   RGBAC_ACT_SQBWD = 10,    /* res0 + 2*res1*acc  (GDN input gradient: dL/dx =
                               dL/dy-direct + 2 x * (gamma'^T dL/dnorm); no bias)  */
+  RGBAC_ACT_DGELU = 11,    /* acc * GELU'(res0)  (input gradient of a conv whose
+                              input is GELU(res0): the producer's activation
+                              backward folded in; bf16: the A&S 7.1.26 derivative
+                              of rgbac_act_bwd, f32: exact; no bias, res1, res2) */
+  RGBAC_ACT_DLRELU = 12,   /* res0 > 0 ? acc : acc * act_param  (same, (Leaky)ReLU
+                              producer: act_param = its slope, 0 for ReLU)        */
 };
 
 enum rgbac_conv_mode {

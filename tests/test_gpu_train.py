@@ -801,3 +801,39 @@ def test_wgrad_wide_tiles_vs_torch(cin, cout, k, stride, hw, nsrc):
     want = torch.nn.grad.conv2d_weight(x, (cout, cin, k, k), gy, stride=stride, padding=k // 2)
     assert nrel(dw.view(cout, cin, k, k), want) < 1e-4
     assert nrel(db, gy.sum(dim=(0, 2, 3))) < 1e-4
+
+
+@pytest.mark.parametrize("cin,cout,h,w,B", [
+    (32, 32, 32, 64, 2),      # the DSE 32 -> 32 conv shape (two 16-channel n tiles)
+    (128, 8, 32, 32, 3),      # slice-stack tail 128 -> 8: one n tile, 4 channel blocks
+    (64, 16, 16, 32, 2),      # 16 outputs, patch-high grid (2 patches per image)
+    (32, 24, 8, 96, 1),       # ragged n tile (24), one patch row, three patches wide
+])
+def test_wgrad_patch_vs_torch(cin, cout, h, w, B):
+    """The patch weight-gradient kernel (csrc/train.hip wgrad_patch_kernel: 8 x 32 output
+    patches with their 10 x 34 source halo staged once, taps as shifted halo rows) and its bias
+    sums against torch.nn.grad.conv2d_weight in fp32 on the same bf16-valued operands,
+    including the zero-padded image borders of every patch (1e-4 norm-wise)."""
+    from rgbac import autograd as ag
+    rt = _rt()
+    g = _gen(cin + cout + h + w)
+    x = torch.randn((B, cin, h, w), generator=g).bfloat16().float()
+    gy = torch.randn((B, cout, h, w), generator=g).bfloat16().float()
+    dev = torch.device("cuda")
+    S = [rt.to_nhwc(x.to(dev), torch.bfloat16)]
+    G = rt.to_nhwc(gy.to(dev), torch.bfloat16)
+    assert ag.wgrad_patch_ok(torch.bfloat16, G.ldc, S, 3, 1, 1, False, h, w)
+    n_pad = rt.round_up(G.ldc, 64)
+    cin_pad = S[0].ldc
+    k_pad = rt.round_up(9 * cin_pad, 64)
+    fmap = torch.full((n_pad, k_pad), -1, dtype=torch.int32)
+    for n in range(cout):
+        for tap in range(9):
+            for c in range(cin):
+                fmap[n, tap * cin_pad + c] = ((n * cin + c) * 3 + tap // 3) * 3 + tap % 3
+    numel = cout * cin * 9
+    dw, db = ag.wgrad(G, S, 3, 1, 1, False, k_pad, fmap.to(dev), numel, nbias=cout)
+    torch.cuda.synchronize()
+    want = torch.nn.grad.conv2d_weight(x, (cout, cin, 3, 3), gy, stride=1, padding=1)
+    assert nrel(dw.view(cout, cin, 3, 3), want) < 1e-4
+    assert nrel(db, gy.sum(dim=(0, 2, 3))) < 1e-4
