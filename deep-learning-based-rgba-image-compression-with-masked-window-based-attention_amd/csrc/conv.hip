@@ -176,12 +176,12 @@ __host__ __device__ __forceinline__ bool is_dact(int act) {
   return act == RGBAC_ACT_DGELU || act == RGBAC_ACT_DLRELU;
 }
 
-template <typename T>
+template <typename T, bool DACT = true>
 __device__ __forceinline__ void epilogue4_body(const ConvShared& s, const ConvGroup& g,
                                                long long opix, int n, float (&v)[4]);
 
 // Bias + fused epilogue + store of channels n..n+3 of M-grid pixel m (phase ph).
-template <typename T>
+template <typename T, bool DACT = true>
 __device__ __forceinline__ void epilogue4(const ConvShared& s, const ConvGroup& g, int ph, int m,
                                           int n, float (&v)[4]) {
   const int t = udiv(m, s.Wm, s.rWm);
@@ -210,7 +210,7 @@ __device__ __forceinline__ void epilogue4(const ConvShared& s, const ConvGroup& 
     opix = (long long)(b * s.out_h + 2 * my + (ph >> 1)) * s.out_w + 2 * mx + (ph & 1);
   else
     opix = (long long)(b * s.out_h + my) * s.out_w + mx;
-  epilogue4_body<T>(s, g, opix, n, v);
+  epilogue4_body<T, DACT>(s, g, opix, n, v);
 }
 
 // Same for a stride-1 CONV whose output grid is the M grid (output pixel = m).
@@ -236,12 +236,14 @@ struct EpiIn {
   }
 };
 
-template <typename T>
+// DACT = false: an instantiation without the folded activation backward (ACT_DGELU /
+// ACT_DLRELU), for kernels at their register limit that run it in a separate instance
+template <typename T, bool DACT = true>
 __device__ __forceinline__ void epilogue4_fin(const ConvShared& s, const ConvGroup& g,
                                               long long opix, int n, float (&v)[4],
                                               const float (&bias)[4], const EpiIn& in);
 
-template <typename T>
+template <typename T, bool DACT>
 __device__ __forceinline__ void epilogue4_body(const ConvShared& s, const ConvGroup& g,
                                                long long opix, int n, float (&v)[4]) {
   EpiIn in;
@@ -249,10 +251,10 @@ __device__ __forceinline__ void epilogue4_body(const ConvShared& s, const ConvGr
   float bias[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) bias[r] = g.bias ? g.bias[n + r] : 0.0f;
-  epilogue4_fin<T>(s, g, opix, n, v, bias, in);
+  epilogue4_fin<T, DACT>(s, g, opix, n, v, bias, in);
 }
 
-template <typename T>
+template <typename T, bool DACT>
 __device__ __forceinline__ void epilogue4_fin(const ConvShared& s, const ConvGroup& g,
                                               long long opix, int n, float (&v)[4],
                                               const float (&bias)[4], const EpiIn& in) {
@@ -261,11 +263,14 @@ __device__ __forceinline__ void epilogue4_fin(const ConvShared& s, const ConvGro
   T* out = reinterpret_cast<T*>(g.out);
   const float (&r0)[4] = in.r0;
   const float (&r1)[4] = in.r1;
+  if (DACT && is_dact(s.act)) {              // uniform branch: keeps the derivative out of the
+#pragma unroll                        // other epilogues (no if-converted select per element)
+    for (int r = 0; r < 4; ++r) v[r] = dact_apply<T>(s.act, s.act_param, v[r], r0[r]);
+  } else {
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
-    v[r] = s.act == RGBAC_ACT_SQBWD ? r0[r] + 2.0f * r1[r] * v[r]
-           : is_dact(s.act)         ? dact_apply<T>(s.act, s.act_param, v[r], r0[r])
-                                    : v[r] + r0[r];
+    for (int r = 0; r < 4; ++r)
+      v[r] = s.act == RGBAC_ACT_SQBWD ? r0[r] + 2.0f * r1[r] * v[r] : v[r] + r0[r];
+  }
   if (g.zout) {
     T* z = reinterpret_cast<T*>(g.zout) + opix * g.zld + g.out_coff + n;
     if (n + 3 < g.cout) {
@@ -329,7 +334,7 @@ __device__ __forceinline__ void epilogue4_fin(const ConvShared& s, const ConvGro
 
 // conv_kernel epilogue of accumulator row i (pixel m, channels nn[j]..+3 for j < TN):
 // every residual load of the row is issued before any math/store.
-template <typename T, int TN, int TM>
+template <typename T, int TN, int TM, bool DACT = true>
 __device__ __forceinline__ void epilogue_tile_row(const ConvShared& s, const ConvGroup& g, int ph,
                                                   int m, const int (&nn)[TN],
                                                   const f32x4 (&acc)[TN][TM], int i) {
@@ -338,7 +343,7 @@ __device__ __forceinline__ void epilogue_tile_row(const ConvShared& s, const Con
     for (int j = 0; j < TN; ++j) {
       if (nn[j] >= g.cout) continue;
       float v[4] = {acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]};
-      epilogue4<T>(s, g, ph, m, nn[j], v);
+      epilogue4<T, DACT>(s, g, ph, m, nn[j], v);
     }
     return;
   }
@@ -363,7 +368,7 @@ __device__ __forceinline__ void epilogue_tile_row(const ConvShared& s, const Con
   for (int j = 0; j < TN; ++j) {
     if (nn[j] >= g.cout) continue;
     float v[4] = {acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]};
-    epilogue4_fin<T>(s, g, opix, nn[j], v, bias[j], in[j]);
+    epilogue4_fin<T, DACT>(s, g, opix, nn[j], v, bias[j], in[j]);
   }
 }
 
@@ -421,13 +426,24 @@ __device__ __forceinline__ void epilogue_row(const ConvShared& s, const ConvGrou
   for (int j = 0; j < TN; ++j) {
     if (nn[j] >= g.cout) continue;
     float* vv = v[j];
+    if (is_dact(s.act)) {             // uniform: the folded activation backward, no zout
+#pragma unroll
+      for (int r = 0; r < 4; ++r) vv[r] = dact_apply<T>(s.act, s.act_param, vv[r], r0[j][r]);
+      const long long base = opix * g.out_ldc + g.out_coff + nn[j];
+      if (nn[j] + 3 < g.cout) {
+        Elem<T>::st4(out + base, v[j]);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (nn[j] + r < g.cout) Elem<T>::st(out + base + r, vv[r]);
+      }
+      continue;
+    }
     if (g.zout) {
       float zv[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        zv[r] = s.act == RGBAC_ACT_SQBWD ? r0[j][r] + 2.0f * r1[j][r] * vv[r]
-                : is_dact(s.act)         ? dact_apply<T>(s.act, s.act_param, vv[r], r0[j][r])
-                                         : vv[r] + r0[j][r];
+        zv[r] = s.act == RGBAC_ACT_SQBWD ? r0[j][r] + 2.0f * r1[j][r] * vv[r] : vv[r] + r0[j][r];
       T* z = reinterpret_cast<T*>(g.zout) + opix * g.zld + g.out_coff + nn[j];
       if (nn[j] + 3 < g.cout) {
         Elem<T>::st4(z, zv);
@@ -439,9 +455,7 @@ __device__ __forceinline__ void epilogue_row(const ConvShared& s, const ConvGrou
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float x = s.act == RGBAC_ACT_SQBWD ? r0[j][r] + 2.0f * r1[j][r] * vv[r]
-                : is_dact(s.act)         ? dact_apply<T>(s.act, s.act_param, vv[r], r0[j][r])
-                                         : vv[r] + r0[j][r];
+      float x = s.act == RGBAC_ACT_SQBWD ? r0[j][r] + 2.0f * r1[j][r] * vv[r] : vv[r] + r0[j][r];
       switch (s.act) {
         case RGBAC_ACT_GELU: x = gelu_t<T>(x); break;
         case RGBAC_ACT_RELU: x = x > 0.f ? x : 0.f; break;
@@ -1748,7 +1762,7 @@ static void launch_smallk(const ConvArgsDev& d, int nks16, int max_cout, hipStre
 //     lane) is requested as one batch before the epilogue math: one memory latency per
 //     tile, not per column (<= 128 VGPRs: four waves per SIMD hide it).
 // Persistent grid; no barrier after the weight panel.
-template <int NKS>
+template <int NKS, bool DACT>
 __global__ void __launch_bounds__(512, 4) conv_pw_kernel(const ConvArgsDev args) {
   constexpr int NT = 12, BN = 192, NCH = 4 * NKS;  // 16-byte chunks per weight row
   static_assert(NCH % 8 == 0, "swizzle groups of 8 chunks");
@@ -1853,7 +1867,7 @@ __global__ void __launch_bounds__(512, 4) conv_pw_kernel(const ConvArgsDev args)
           in.on = sel_on;
           float v[4] = {acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
           const float bias[4] = {bl[n], bl[n + 1], bl[n + 2], bl[n + 3]};
-          epilogue4_fin<bf16_t>(s, g, (long long)m, n, v, bias, in);
+          epilogue4_fin<bf16_t, DACT>(s, g, (long long)m, n, v, bias, in);
         }
       }
     }
@@ -1861,9 +1875,11 @@ __global__ void __launch_bounds__(512, 4) conv_pw_kernel(const ConvArgsDev args)
 #undef PWW_LOAD
 }
 
-template <int NKS>
+// DACT: the instance with the folded activation backward (training input gradients); the
+// forward's instance leaves that epilogue out (the kernel sits at its 128-VGPR limit)
+template <int NKS, bool DACT>
 static void launch_pw_k(const ConvArgsDev& d, hipStream_t st) {
-  auto kern = conv_pw_kernel<NKS>;
+  auto kern = conv_pw_kernel<NKS, DACT>;
   constexpr size_t lds = (size_t)192 * 4 * NKS * 16;
   static bool attr = false;
   static int ncu = 0;
@@ -1887,9 +1903,15 @@ static void launch_pw_k(const ConvArgsDev& d, hipStream_t st) {
 }
 
 static void launch_pw(const ConvArgsDev& d, int cin_max, hipStream_t st) {
-  if (cin_max <= 64) launch_pw_k<2>(d, st);
-  else if (cin_max <= 128) launch_pw_k<4>(d, st);
-  else launch_pw_k<6>(d, st);
+  if (is_dact(d.s.act)) {
+    if (cin_max <= 64) launch_pw_k<2, true>(d, st);
+    else if (cin_max <= 128) launch_pw_k<4, true>(d, st);
+    else launch_pw_k<6, true>(d, st);
+    return;
+  }
+  if (cin_max <= 64) launch_pw_k<2, false>(d, st);
+  else if (cin_max <= 128) launch_pw_k<4, false>(d, st);
+  else launch_pw_k<6, false>(d, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -2066,7 +2088,7 @@ __global__ void __launch_bounds__(512) conv_npatch_kernel(const ConvArgsDev args
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int n = 16 * j + 4 * fq;
-        if (n < cout) epilogue4<T>(s, g, 0, m_e, n, v[j]);
+        if (n < cout) epilogue4<T, false>(s, g, 0, m_e, n, v[j]);
       }
     } else {
 #pragma unroll
@@ -2075,7 +2097,7 @@ __global__ void __launch_bounds__(512) conv_npatch_kernel(const ConvArgsDev args
         if (n < cout) {
           EpiIn in;
           in.template load<T>(g, s.act, (long long)m_e, n);
-          epilogue4_fin<T>(s, g, (long long)m_e, n, v[j], pb[j], in);
+          epilogue4_fin<T, false>(s, g, (long long)m_e, n, v[j], pb[j], in);
         }
       }
     }
@@ -2387,7 +2409,9 @@ __device__ __forceinline__ void patch_epi(const ConvShared& s, const ConvGroup& 
 // Dispatch of a patch kernel's phase epilogue: the lean form where it applies, else the
 // generic per-row epilogue (SUBPEL2 stores, zout, res1 activations, ragged cout).
 // ``pbias``: the lane's biases (bias[nn[j] + r]) loaded up front by the caller, or nullptr.
-template <int TN, int TM>
+// DACT = false: no folded activation backward (the forward instances; their register
+// allocation is the one measured before the training epilogues existed)
+template <int TN, int TM, bool DACT>
 __device__ __forceinline__ void patch_epilogue(const ConvShared& s, const ConvGroup& g, int ph,
                                                int b, int yrow0, int x0, int fr,
                                                const int (&nn)[TN], const f32x4 (&acc)[TN][TM],
@@ -2399,13 +2423,13 @@ __device__ __forceinline__ void patch_epilogue(const ConvShared& s, const ConvGr
     patch_epi<TN, TM, RGBAC_ACT_GELU>(s, g, ph, b, yrow0, x0 + fr, nn, acc, pbias);
   } else if (lean && s.act == RGBAC_ACT_RELU) {
     patch_epi<TN, TM, RGBAC_ACT_RELU>(s, g, ph, b, yrow0, x0 + fr, nn, acc, pbias);
-  } else if (lean && is_dact(s.act)) {     // both folded activation backwards (s.act)
+  } else if (DACT && lean && is_dact(s.act)) {     // both folded activation backwards
     patch_epi<TN, TM, RGBAC_ACT_DGELU>(s, g, ph, b, yrow0, x0 + fr, nn, acc, pbias);
   } else {
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
       const int m = (b * s.Hm + yrow0 + i) * s.Wm + x0 + fr;
-      epilogue_tile_row<bf16_t, TN, TM>(s, g, ph, m, nn, acc, i);
+      epilogue_tile_row<bf16_t, TN, TM, DACT>(s, g, ph, m, nn, acc, i);
     }
   }
 }
@@ -2444,7 +2468,7 @@ __device__ __forceinline__ void patch_epilogue(const ConvShared& s, const ConvGr
 //     the im2col tiles' 3.3x fetch.  The weights are the plain CONV packing (k = tap *
 //     cin_pad + ci over the 25 taps), walked phase by phase; the four phases accumulate
 //     into one tile and the epilogue runs once.
-template <int TH, int BN, int WGM, int WGN, int NBUF>
+template <int TH, int BN, int WGM, int WGN, int NBUF, bool DACT>
 __global__ void __launch_bounds__(512) conv_patch_kernel(const ConvArgsDev args) {
   using T = bf16_t;
   constexpr int NW = 8;
@@ -2675,7 +2699,7 @@ _Pragma("unroll")                                                               
           int nn[TN];
 #pragma unroll
           for (int j = 0; j < TN; ++j) nn[j] = n0 + wn * TN * 16 + j * 16 + fq * 4;
-          patch_epilogue<TN, TM>(s, g, s2 ? 0 : cph, b, y0 + wm * TM, x0, fr, nn, acc);
+          patch_epilogue<TN, TM, DACT>(s, g, s2 ? 0 : cph, b, y0 + wm * TM, x0, fr, nn, acc);
 #pragma unroll
           for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -2876,7 +2900,7 @@ __global__ void __launch_bounds__(64 * NW * KS) conv_fpatch_kernel(const ConvArg
     int nn[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) nn[j] = n0 + wave * TN * 16 + j * 16 + fq * 4;
-    patch_epilogue<TN, TM>(s, g, 0, b, y0, x0, fr, nn, acc, pbias);
+    patch_epilogue<TN, TM, false>(s, g, 0, b, y0, x0, fr, nn, acc, pbias);
     WG_T(3);
     return;
   }
@@ -2939,7 +2963,7 @@ _Pragma("unroll")                                                               
     int nn[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) nn[j] = n0 + wave * TN * 16 + j * 16 + fq * 4;
-    patch_epilogue<TN, TM>(s, g, ph, b, y0, x0, fr, nn, acc);
+    patch_epilogue<TN, TM, false>(s, g, ph, b, y0, x0, fr, nn, acc);
   }
 #undef FP_LOAD
 }
@@ -3146,16 +3170,26 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
       const int th = tc.bm / 16;
       const long long nsp = (long long)s.batch * (s.Hm / th) * (s.Wm / 16) * s.ngroups;
       dim3 grid((unsigned)nsp, (unsigned)((max_cout + tc.bn - 1) / tc.bn), 1);
-      switch (tile) {
-        case 36: hipLaunchKernelGGL((conv_patch_kernel<8, 192, 2, 4, 3>), grid, dim3(512), 0, st, d); break;
-        case 37: hipLaunchKernelGGL((conv_patch_kernel<8, 128, 2, 4, 3>), grid, dim3(512), 0, st, d); break;
-        case 38: hipLaunchKernelGGL((conv_patch_kernel<8, 96, 4, 2, 3>), grid, dim3(512), 0, st, d); break;
-        case 39: hipLaunchKernelGGL((conv_patch_kernel<8, 256, 2, 4, 3>), grid, dim3(512), 0, st, d); break;
-        case 40: hipLaunchKernelGGL((conv_patch_kernel<8, 192, 2, 4, 4>), grid, dim3(512), 0, st, d); break;
-        case 48: hipLaunchKernelGGL((conv_patch_kernel<8, 64, 4, 2, 4>), grid, dim3(512), 0, st, d); break;
-        case 49: hipLaunchKernelGGL((conv_patch_kernel<8, 128, 2, 4, 4>), grid, dim3(512), 0, st, d); break;
-        default: hipLaunchKernelGGL((conv_patch_kernel<8, 64, 4, 2, 3>), grid, dim3(512), 0, st, d); break;
+      // the folded activation backward (training input gradients) in instances of their own:
+      // the forward instances keep the register allocation they were tuned with (the shared
+      // epilogue code cost the 5x5/s2 patch kernels 37 % when compiled into them)
+#define PATCH_LAUNCH(DA)                                                                               \
+      switch (tile) {                                                                                  \
+        case 36: hipLaunchKernelGGL((conv_patch_kernel<8, 192, 2, 4, 3, DA>), grid, dim3(512), 0, st, d); break; \
+        case 37: hipLaunchKernelGGL((conv_patch_kernel<8, 128, 2, 4, 3, DA>), grid, dim3(512), 0, st, d); break; \
+        case 38: hipLaunchKernelGGL((conv_patch_kernel<8, 96, 4, 2, 3, DA>), grid, dim3(512), 0, st, d); break;  \
+        case 39: hipLaunchKernelGGL((conv_patch_kernel<8, 256, 2, 4, 3, DA>), grid, dim3(512), 0, st, d); break; \
+        case 40: hipLaunchKernelGGL((conv_patch_kernel<8, 192, 2, 4, 4, DA>), grid, dim3(512), 0, st, d); break; \
+        case 48: hipLaunchKernelGGL((conv_patch_kernel<8, 64, 4, 2, 4, DA>), grid, dim3(512), 0, st, d); break;  \
+        case 49: hipLaunchKernelGGL((conv_patch_kernel<8, 128, 2, 4, 4, DA>), grid, dim3(512), 0, st, d); break; \
+        default: hipLaunchKernelGGL((conv_patch_kernel<8, 64, 4, 2, 3, DA>), grid, dim3(512), 0, st, d); break;  \
       }
+      if (is_dact(s.act)) {
+        PATCH_LAUNCH(true)
+      } else {
+        PATCH_LAUNCH(false)
+      }
+#undef PATCH_LAUNCH
       return check_launch("conv_patch_kernel");
     } else {
       set_error("the patch tiles are bf16 only");
@@ -3271,9 +3305,10 @@ static int fill_group(const rgbac_conv_args* a, int ntaps_max, ConvGroup& g) {
   RGBAC_REQUIRE(a->act != RGBAC_ACT_SQBWD || (a->res0 && a->res1 && !a->bias),
                 "SQBWD needs res0 (direct gradient), res1 (x) and no bias");
   RGBAC_REQUIRE(!is_dact(a->act) || (a->res0 && !a->res1 && !a->res2 && !a->bias && !a->zout &&
-                                      a->mode != RGBAC_SUBPEL2 && !a->square_input),
+                                      a->mode != RGBAC_SUBPEL2 && !a->square_input &&
+                                      !fpatch_tile(a->tile) && a->tile != kTileNPatch),
                 "DGELU / DLRELU need res0 (the producer's pre-activation) and no bias, res1, res2, "
-                "zout, subpel store or squared input");
+                "zout, subpel store, squared input or fragment-major (forward-only) tile");
   g.zout = a->zout;
   g.zld = a->zout_ldc;
   g.cnt = a->tile_counters;

@@ -265,8 +265,14 @@ def wgrad_tile(dtype, n_pad, k_pad, square):
     no squared input, n_pad >= 128 and k_pad >= 512; otherwise counted in 64 x 64 units with
     ~1024 workgroups wanted (the 64 x 64 / 64 x 128 tiles run two workgroups per CU)."""
     if dtype == torch.bfloat16 and not square and n_pad >= 128 and k_pad >= 512 and WGRAD_BIG:
-        return -(-k_pad // 256) * -(-n_pad // 128), 256
-    return (k_pad // 64) * (n_pad // 64), 1024
+        return -(-k_pad // 256) * -(-n_pad // 128), _WG_TARGET_BIG
+    return (k_pad // 64) * (n_pad // 64), _WG_TARGET
+
+
+# workgroups wanted per weight-gradient launch (A/B knobs: fewer = fewer fp32 slabs to write
+# and reduce, more = more CUs busy)
+_WG_TARGET_BIG = int(os.environ.get("RGBAC_WGRAD_TARGET_BIG", "256"))
+_WG_TARGET = int(os.environ.get("RGBAC_WGRAD_TARGET", "1024"))
 
 
 WGRAD_PATCH = os.environ.get("RGBAC_WGRAD_PATCH", "1") != "0"

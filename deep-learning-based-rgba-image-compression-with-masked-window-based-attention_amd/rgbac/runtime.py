@@ -608,7 +608,8 @@ def kernel_name(tile, preps):
         c = fpatch_cpt(preps) if FPATCH_SIG[tile][0] == 4 else 0
         return "conv_fpatch_kernel<%d, %d, 4, 4%s>" % (FPATCH_SIG[tile] + (f", {c}" if c else "",))
     if tile in PATCH_SIG:
-        return "conv_patch_kernel<%d, %d, %d, %d, %d>" % PATCH_SIG[tile]
+        dact = "true" if preps[0].a.act in (ACT["dgelu"], ACT["dlrelu"]) else "false"
+        return "conv_patch_kernel<%d, %d, %d, %d, %d, %s>" % (PATCH_SIG[tile] + (dact,))
     if tile == TILE_WSTREAM:
         # the library's wave count choice (csrc/conv.hip launch_wstream)
         nks = max((p.a.ksize * p.a.ksize * p.a.cin_pad + 15) // 16 for p in preps)
@@ -620,7 +621,8 @@ def kernel_name(tile, preps):
     if tile == TILE_PW:
         cin = max(p.a.cin_pad for p in preps)
         # csrc/conv.hip launch_pw: 32-deep k-steps held in LDS (2 / 4 / 6)
-        return f"conv_pw_kernel<{2 if cin <= 64 else (4 if cin <= 128 else 6)}>"
+        dact = "true" if preps[0].a.act in (ACT["dgelu"], ACT["dlrelu"]) else "false"
+        return f"conv_pw_kernel<{2 if cin <= 64 else (4 if cin <= 128 else 6)}, {dact}>"
     if tile == TILE_SMALLK:
         cout = max(p.pk.cout for p in preps)
         nt = 1 if cout <= 32 else (2 if cout <= 64 else 3)
