@@ -100,6 +100,34 @@ __device__ __forceinline__ float gelu_fast(float x) {
 }
 
 
+// gelu_fast on two values with packed FP32 math (v_pk_fma_f32 / v_pk_mul_f32 do both halves in
+// one instruction; the rcp / exp stay per element): the same operations in the same order as
+// gelu_fast, so bit-identical to it, in 21 instructions per pair instead of 32.  The GELU
+// epilogues are VALU-bound (the residual unit's three epilogues were ~2/3 of its SIMD cycles).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu2_fast(f32x2 x) {
+  const f32x2 ax = {fabsf(x.x), fabsf(x.y)};
+  constexpr float c1 = 0.3275911f * 0.70710678118654752440f;
+  const f32x2 den = __builtin_elementwise_fma((f32x2){c1, c1}, ax, (f32x2){1.0f, 1.0f});
+  const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  f32x2 p = __builtin_elementwise_fma((f32x2){1.061405429f, 1.061405429f}, t,
+                                      (f32x2){-1.453152027f, -1.453152027f});
+  p = __builtin_elementwise_fma(p, t, (f32x2){1.421413741f, 1.421413741f});
+  p = __builtin_elementwise_fma(p, t, (f32x2){-0.284496736f, -0.284496736f});
+  p = __builtin_elementwise_fma(p, t, (f32x2){0.254829592f, 0.254829592f});
+  const f32x2 arg = (x * x) * (f32x2){-0.72134752044448170368f, -0.72134752044448170368f};
+  const f32x2 e = {__builtin_amdgcn_exp2f(arg.x), __builtin_amdgcn_exp2f(arg.y)};
+  const f32x2 q = (p * t) * e;
+  const f32x2 h = (f32x2){-0.5f, -0.5f} * ax;
+  const f32x2 m = {fmaxf(x.x, 0.0f), fmaxf(x.y, 0.0f)};
+  return __builtin_elementwise_fma(h, q, m);
+}
+// v[r] = gelu_fast(v[r]) for a quad, as two packed pairs
+__device__ __forceinline__ void gelu4_fast(float (&v)[4]) {
+  const f32x2 a = gelu2_fast((f32x2){v[0], v[1]}), b = gelu2_fast((f32x2){v[2], v[3]});
+  v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+}
+
 // GELU'(v) = Phi(v) + v phi(v) with the Abramowitz & Stegun 7.1.26 erfc of the forward's
 // gelu_fast (|erf error| <= 1.5e-7; exp(-v^2/2) shared by both terms): ~15 instructions
 // instead of erfcf + expf.  bf16 only (the f32 parity path keeps erfcf).

@@ -57,8 +57,8 @@ __device__ __forceinline__ void ru_act4(float (&v)[4], const f32x4& a, const flo
     v[0] = fmaxf(a[0] + b.x, 0.0f); v[1] = fmaxf(a[1] + b.y, 0.0f);
     v[2] = fmaxf(a[2] + b.z, 0.0f); v[3] = fmaxf(a[3] + b.w, 0.0f);
   } else {
-    v[0] = ru_gelu(a[0] + b.x); v[1] = ru_gelu(a[1] + b.y);
-    v[2] = ru_gelu(a[2] + b.z); v[3] = ru_gelu(a[3] + b.w);
+    v[0] = a[0] + b.x; v[1] = a[1] + b.y; v[2] = a[2] + b.z; v[3] = a[3] + b.w;
+    gelu4_fast(v);                                   // packed pairs (bit-identical to ru_gelu)
   }
 }
 
@@ -796,10 +796,7 @@ __global__ void __launch_bounds__(256, 2) ru_stream_kernel(const RuArgsDev args)
       v[1] = acc3[j][i][1] + bb.y + bf2f(rr.x >> 16);
       v[2] = acc3[j][i][2] + bb.z + bf2f(rr.y & 0xFFFF);
       v[3] = acc3[j][i][3] + bb.w + bf2f(rr.y >> 16);
-      if (!RB) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = ru_gelu(v[r]);
-      }
+      if (!RB) gelu4_fast(v);
       Elem<bf16_t>::st4(reinterpret_cast<bf16_t*>(OT + p * ORW + n * 2), v);
     }
   }
