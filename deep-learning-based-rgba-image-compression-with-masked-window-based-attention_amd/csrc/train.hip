@@ -923,6 +923,207 @@ __global__ void __launch_bounds__(256) wgrad_patch_kernel(const WgradDev a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// Polyphase weight gradient of the 5x5 stride-2 convs and ConvTransposes (bf16, pad 2, one
+// source, 32-channel source blocks x 64-channel output blocks): Analysis x2 / x3 and their
+// Synthesis ConvTranspose mirrors, 120 GFLOP per step at 64^2.  Through im2col the ring kernel
+// re-reads every source pixel ~6x per k tile and once per n tile (1.3 GB of L2 -> LDS traffic
+// per launch at 64^2 B16); here, as in the forward's polyphase patch conv, the source splits
+// into its 4 stride phases S_q[i][j] = S[2i + qy][2j + qx], and kernel tap (ky, kx) =
+// (2 ty + qy, 2 tx + qx) is a stride-1 tap (ty, tx) of phase q:
+//   dW[n][ky][kx][c] = sum_{o} G[o][n] * S_q[oy + ty - 1][ox + tx - 1][c].
+// A workgroup (8 waves) stages a 4 x 32-pixel G patch (64 channels) and the 4 phase halos
+// (6 x 34 pixels, 32 channels) once per patch by LDS-DMA (double-buffered, 136 KiB: one
+// workgroup per CU); the 50 (tap, 16-channel half) pairs are dealt to the waves (7 / 6 each),
+// every wave covering the 4 n tiles of the block, so accumulators (<= 28 tiles) stay in the
+// wave.  LDS rows: phase-halo pixels of 64 B, unswizzled (a pair's fragment address is then a
+// per-lane constant plus an immediate; 2-way bank conflicts on those reads), and G pixels of
+// 128 B (swizzle 2 bit1(r) ^ 4 bit3(r), conflict-free).  Slab layout as the ring kernel's.
+constexpr int kWsTH = 4, kWsTW = 32, kWsPW = kWsTW + 2;
+constexpr int kWsPRows = (kWsTH + 2) * kWsPW;          // 204 halo pixels per phase
+constexpr int kWsPPieces = (kWsPRows + 15) / 16;       // 13 one-KiB pieces per phase
+constexpr int kWsSPieces = 4 * kWsPPieces;             // 52
+constexpr int kWsGPieces = kWsTH * kWsTW * 128 / 1024; // 16 (128-B G rows)
+constexpr int kWsBuf = (kWsSPieces + kWsGPieces) * 1024;
+
+__device__ __forceinline__ int ws_swz128(int r) { return 2 * ((r >> 1) & 1) ^ 4 * ((r >> 3) & 1); }
+
+__global__ void __launch_bounds__(512) wgrad_s2_kernel(const WgradDev a) {
+  __shared__ __attribute__((aligned(16))) unsigned char ring[2 * kWsBuf];
+  constexpr int NW = 8;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int ncb = a.cin_pad / 32;
+  int cb, nb, split;
+  {
+    const int nwg = gridDim.x * gridDim.y;
+    int t = blockIdx.x + gridDim.x * blockIdx.y;
+    const int xcd = t & 7, q = nwg >> 3, r = nwg & 7;
+    t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (t >> 3);
+    const int blk = t % gridDim.x;
+    split = t / gridDim.x;
+    cb = blk % ncb;
+    nb = blk / ncb;
+  }
+  const int H = a.Hg, W = a.Wg, IH = a.in_h, IW = a.in_w;
+  const int pw = W / kWsTW, ppi = pw * (H / kWsTH);
+  const int P = a.M / (kWsTH * kWsTW);
+  const int pbeg = split * a.m_chunk;
+  const int pend = min(pbeg + a.m_chunk, P);
+  const bool do_bias = a.bpart && cb == 0;
+  const void* const zp = (const void*)g_wgrad_zero;
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(wg_lptr_t)ring);
+
+  // ---- DMA: S pieces q = wave + 8 j (< 52), G pieces q = wave + 8 j (< 16); the per-lane
+  // geometry is recomputed at each issue (a few VALU per patch) rather than held in registers
+  constexpr int PSW = (kWsSPieces + NW - 1) / NW, PGW = kWsGPieces / NW;   // 7, 2
+  const int nps = (kWsSPieces - wave + NW - 1) / NW;                       // 7 or 6
+  const char* const sbase = reinterpret_cast<const char*>(a.sp0) + cb * 64;
+  const long long sld2 = a.sld0 * 2, ldg2 = a.ldg * 2;
+  const char* const gbase = reinterpret_cast<const char*>(a.g);
+
+  auto issue = [&](int p, int buf) {
+    const int b = p / ppi, rem = p - b * ppi;
+    const int oy0 = (rem / pw) * kWsTH, ox0 = (rem - (rem / pw) * pw) * kWsTW;
+    const long long gpix0 = ((long long)b * H + oy0) * W + ox0;
+    const long long spix0 = ((long long)b * IH + 2 * oy0) * IW + 2 * ox0;
+    const uint32_t ls = lbase + (uint32_t)(buf * kWsBuf);
+    const uint32_t lg = ls + kWsSPieces * 1024;
+#pragma unroll
+    for (int j = 0; j < PSW; ++j) {
+      if (j < nps) {
+        const int q = wave + NW * j;
+        const int ph = q / kWsPPieces, pp = q - ph * kWsPPieces;
+        const int R = 16 * pp + (lane >> 2);            // row within the phase halo
+        const int i = R / kWsPW, jj = R - (R / kWsPW) * kWsPW;
+        // source pixel offset from (2 oy0, 2 ox0): rows 2 (i - 1) + qy, columns 2 (jj - 1) + qx
+        const int dy = 2 * (i - 1) + (ph >> 1), dx = 2 * (jj - 1) + (ph & 1);
+        const int sy = 2 * oy0 + dy, sx = 2 * ox0 + dx;
+        const bool ok = R < kWsPRows && (unsigned)sy < (unsigned)IH && (unsigned)sx < (unsigned)IW;
+        const int cs = (lane & 3) * 16;                // halo rows unswizzled (see below)
+        wg_dma16(ok ? (const void*)(sbase + (spix0 + (long long)dy * IW + dx) * sld2 + cs) : zp,
+                 ls + (uint32_t)(q * 1024));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < PGW; ++j) {
+      const int R = 8 * (wave + NW * j) + (lane >> 3);  // G pixel row of the patch
+      const int cg = nb * 64 + 8 * ((lane & 7) ^ ws_swz128(R));
+      const bool ok = cg < a.gch;
+      wg_dma16(ok ? (const void*)(gbase + (gpix0 + (R >> 5) * W + (R & 31)) * ldg2 + cg * 2) : zp,
+               lg + (uint32_t)((wave + NW * j) * 1024));
+    }
+  };
+
+  // ---- this wave's (tap, channel half) pairs e = wave + 8 i < 50, all 4 n tiles.  The halo
+  // rows are NOT swizzled (2-way bank conflicts on these reads) so that a pair's fragment
+  // address is one per-lane register (set once per patch) plus the row's immediate offset:
+  // the address arithmetic of a swizzled, shifted row cost ~5 VALU per MFMA (PMC).
+  constexpr int NPR = (50 + NW - 1) / NW;               // 7
+  const int npr = (50 - wave + NW - 1) / NW;            // 7 or 6 (wave-uniform)
+  f32x4 acc[NPR][4];
+#pragma unroll
+  for (int i = 0; i < NPR; ++i)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[i][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bacc = 0.0f;
+  const int fi = lane & 15, fq = lane >> 4, cq = fi & 3;
+  const int ra0 = 8 * fq + (fi >> 2);
+  int aoff[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+    aoff[t] = ra0 * 128 + 16 * ((2 * t + (cq >> 1)) ^ ws_swz128(ra0)) + 8 * (cq & 1);
+  int boff[NPR];                                         // relative to the S region of buffer 0
+#pragma unroll
+  for (int i = 0; i < NPR; ++i) {
+    const int e = min(wave + NW * i, 49);
+    const int tap = e >> 1, u = e & 1;
+    const int ky = tap / 5, kx = tap - 5 * (tap / 5);
+    const int ph = 2 * (ky & 1) + (kx & 1);
+    boff[i] = ph * (kWsPPieces * 1024) + ((ky >> 1) * kWsPW + (kx >> 1) + ra0) * 64 +
+              16 * (2 * u + (cq >> 1)) + 8 * (cq & 1);
+  }
+  const uint32_t rbase = (uint32_t)(size_t)(wg_lptr_t)ring;
+
+  if (pbeg < pend) issue(pbeg, 0);
+  for (int p = pbeg, it = 0; p < pend; ++p, ++it) {
+    const int buf = it & 1;
+    if (p + 1 < pend) {
+      issue(p + 1, buf ^ 1);
+      if (nps == PSW) wg_wait_vm<PSW + PGW>();
+      else wg_wait_vm<PSW - 1 + PGW>();
+    } else {
+      wg_wait_vm<0>();
+    }
+    __syncthreads();                                     // patch p landed for every wave
+    const unsigned char* Ss = ring + buf * kWsBuf;
+    const unsigned char* Gs = Ss + kWsSPieces * 1024;
+    if (do_bias) {                                       // G column sums: 8 row groups x 64
+      const int c = tid & 63, rg = tid >> 6;
+#pragma unroll 4
+      for (int r = 16 * rg; r < 16 * rg + 16; ++r)
+        bacc += bf2f(*reinterpret_cast<const uint16_t*>(
+            Gs + r * 128 + 16 * ((c >> 3) ^ ws_swz128(r)) + (c & 7) * 2));
+    }
+    uint32_t bp[NPR];
+#pragma unroll
+    for (int i = 0; i < NPR; ++i) bp[i] = rbase + (uint32_t)(buf * kWsBuf) + (uint32_t)boff[i];
+    const uint32_t gp = rbase + (uint32_t)(buf * kWsBuf + kWsSPieces * 1024);
+#pragma unroll
+    for (int yy = 0; yy < kWsTH; ++yy) {
+      uint4 A[4];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const lds_v4s_ptr q = (lds_v4s_ptr)(size_t)(gp + aoff[t] + yy * 32 * 128);
+        const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(q);
+        const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(q + 4 * 128 / 8);
+        const uint2 u0 = __builtin_bit_cast(uint2, a0), u1 = __builtin_bit_cast(uint2, a1);
+        A[t] = make_uint4(u0.x, u0.y, u1.x, u1.y);
+      }
+#pragma unroll
+      for (int i = 0; i < NPR; ++i) {
+        if (i < npr) {                                   // wave-uniform
+          const lds_v4s_ptr q = (lds_v4s_ptr)(size_t)(bp[i] + yy * kWsPW * 64);
+          const v4s b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(q);
+          const v4s b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(q + 4 * 64 / 8);
+          const uint2 u0 = __builtin_bit_cast(uint2, b0), u1 = __builtin_bit_cast(uint2, b1);
+          const uint4 B = make_uint4(u0.x, u0.y, u1.x, u1.y);
+#pragma unroll
+          for (int t = 0; t < 4; ++t) mma_step<bf16_t>(acc[i][t], A[t], B);
+        }
+      }
+    }
+    __syncthreads();                                     // buf free for patch p + 2
+  }
+  float* Pp = a.part + (size_t)split * a.n_pad * a.k_pad;
+#pragma unroll
+  for (int i = 0; i < NPR; ++i) {
+    const int e = wave + NW * i;
+    if (e < 50) {
+      const int tap = e >> 1, u = e & 1;
+      const int k = tap * a.cin_pad + cb * 32 + 16 * u + fi;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = nb * 64 + 16 * t + 4 * fq + r;
+          if (n < a.gch) Pp[(size_t)n * a.k_pad + k] = acc[i][t][r];
+        }
+    }
+  }
+  if (do_bias) {
+    float* bred = reinterpret_cast<float*>(ring);        // [8][64], the buffers are free
+    bred[tid] = bacc;
+    __syncthreads();
+    if (tid < 64 && nb * 64 + tid < a.gch) {
+      float s = bred[tid];
+#pragma unroll
+      for (int g2 = 1; g2 < 8; ++g2) s += bred[64 * g2 + tid];
+      a.bpart[(size_t)split * a.n_pad + nb * 64 + tid] = s;
+    }
+  }
+}
+
 // Slab reduction in the slab's own (coalesced) order: for slab position e (row n,
 // column k of the packed layout), dw[fmap[e]] = sum_s part[s][e] (fmap < 0: a pad
 // slot, skipped; every parameter element owns exactly one slot);
@@ -2081,6 +2282,19 @@ static bool wgrad_patch_ok(const rgbac_wgrad_args* a) {
          a->in_w == a->grid_w;
 }
 
+// The polyphase kernel's shapes (mirrored by rgbac.autograd.wgrad_s2_ok): bf16, 5x5 stride 2
+// pad 2, one source of whole 32-channel blocks, the output grid 4-row x 32-column patches of
+// half the input grid.  RGBAC_WGRAD_S2=0 turns it off.
+static bool wgrad_s2_ok(const rgbac_wgrad_args* a) {
+  static const bool on = [] {
+    const char* e = getenv("RGBAC_WGRAD_S2");
+    return !(e && e[0] == '0');
+  }();
+  return on && a->dtype == RGBAC_BF16 && !a->square_input && a->ksize == 5 && a->stride == 2 &&
+         a->pad == 2 && a->nsrc == 1 && a->cin_pad % 32 == 0 && a->grid_w % kWsTW == 0 &&
+         a->grid_h % kWsTH == 0 && a->in_h == 2 * a->grid_h && a->in_w == 2 * a->grid_w;
+}
+
 extern "C" int rgbac_conv_wgrad(const rgbac_wgrad_args* a, void* stream) {
   RGBAC_REQUIRE(a != nullptr, "null args");
   RGBAC_REQUIRE(a->dtype == RGBAC_F32 || a->dtype == RGBAC_BF16, "dtype");
@@ -2138,6 +2352,15 @@ extern "C" int rgbac_conv_wgrad(const rgbac_wgrad_args* a, void* stream) {
     const char* e = getenv("RGBAC_WGRAD_RING");
     return !(e && e[0] == '0');
   }();
+  if (wgrad_s2_ok(a)) {
+    // 4 x 32-pixel patches of the output grid; nsplit workgroups per (32-channel source block,
+    // 64-channel output block)
+    const long long P = M / (kWsTH * kWsTW);
+    d.m_chunk = (int)((P + a->nsplit - 1) / a->nsplit);
+    const dim3 sgrid((a->cin_pad / 32) * ((a->g_channels + 63) / 64), a->nsplit);
+    hipLaunchKernelGGL(wgrad_s2_kernel, sgrid, dim3(512), 0, st, d);
+    return check_launch("wgrad_s2_kernel");
+  }
   if (wgrad_patch_ok(a)) {
     // patches of 8 x 32 output pixels; nsplit workgroups per 32-channel source block
     const long long P = M / (kWpTH * kWpTW);

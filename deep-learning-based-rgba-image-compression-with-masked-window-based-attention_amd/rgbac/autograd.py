@@ -273,6 +273,7 @@ def wgrad_tile(dtype, n_pad, k_pad, square):
 # and reduce, more = more CUs busy)
 _WG_TARGET_BIG = int(os.environ.get("RGBAC_WGRAD_TARGET_BIG", "256"))
 _WG_TARGET = int(os.environ.get("RGBAC_WGRAD_TARGET", "1024"))
+_WG_CEIL = os.environ.get("RGBAC_WGRAD_CEIL", "0") == "1"
 
 
 WGRAD_PATCH = os.environ.get("RGBAC_WGRAD_PATCH", "1") != "0"
@@ -287,10 +288,23 @@ def wgrad_patch_ok(dtype, gch, S, ksize, stride, pad, square, grid_h, grid_w):
             grid_w % 32 == 0 and grid_h % 8 == 0 and s0.H == grid_h and s0.W == grid_w)
 
 
+WGRAD_S2 = os.environ.get("RGBAC_WGRAD_S2", "1") != "0"
+
+
+def wgrad_s2_ok(dtype, S, ksize, stride, pad, square, grid_h, grid_w):
+    """csrc/train.hip wgrad_s2_ok: the polyphase kernel's shapes (bf16, 5x5 stride 2 pad 2, one
+    source of whole 32-channel blocks, the grid 4 x 32-pixel patches of half the source)."""
+    s0 = S[0]
+    return (WGRAD_S2 and dtype == torch.bfloat16 and not square and ksize == 5 and
+            stride == 2 and pad == 2 and len(S) == 1 and s0.ldc % 32 == 0 and
+            grid_w % 32 == 0 and grid_h % 4 == 0 and s0.H == 2 * grid_h and s0.W == 2 * grid_w)
+
+
 def _nsplit(tiles, M, slab, target=1024):
     """Pixel splits: enough workgroups to fill the chip (``target``), each split >= 512
     pixels, and the fp32 partial slabs bounded (their write + reduce read is pure overhead)."""
-    want = max(1, -(-target // tiles))
+    # floor: never a nearly empty extra round of workgroups (RGBAC_WGRAD_CEIL=1: the ceiling, A/B)
+    want = max(1, -(-target // tiles) if _WG_CEIL else target // tiles)
     cap = max(1, _SLAB_FLOATS // slab)
     return int(max(1, min(want, -(-M // 512), cap, 1024)))
 
@@ -303,11 +317,17 @@ def wgrad(G, S, ksize, stride, pad, square, k_pad, fmap, numel, nbias=0, bias_fr
     dev = G.t.device
     n_pad = round_up(G.ldc, 64)
     M = G.B * G.H * G.W
-    if wgrad_patch_ok(G.t.dtype, G.ldc, S, ksize, stride, pad, square, G.H, G.W):
-        # one workgroup per (32-channel block, run of 8 x 32-pixel patches): ~512 in flight
+    if wgrad_s2_ok(G.t.dtype, S, ksize, stride, pad, square, G.H, G.W):
+        # one workgroup per CU (136 KiB of LDS): ~256 per launch over the (32-channel source
+        # block, 64-channel output block) pairs, each at least 2 patches of 4 x 32 pixels
+        # (floor: one workgroup more than the 256 CUs would run a second, nearly empty round)
+        tiles = (S[0].ldc // 32) * -(-G.ldc // 64)
+        ns = int(max(1, min(256 // tiles, M // 256, _SLAB_FLOATS // (n_pad * k_pad))))
+    elif wgrad_patch_ok(G.t.dtype, G.ldc, S, ksize, stride, pad, square, G.H, G.W):
+        # one workgroup per (32-channel block, run of 8 x 32-pixel patches): <= 512 in flight
         # (two per CU), each at least 2 patches so the double-buffered staging overlaps
         tiles = S[0].ldc // 32
-        ns = int(max(1, min(-(-512 // tiles), M // 512, _SLAB_FLOATS // (n_pad * k_pad))))
+        ns = int(max(1, min(512 // tiles, M // 512, _SLAB_FLOATS // (n_pad * k_pad))))
     else:
         tiles, target = wgrad_tile(G.t.dtype, n_pad, k_pad, square)
         ns = _nsplit(tiles, M, n_pad * k_pad, target)

@@ -804,6 +804,43 @@ def test_wgrad_wide_tiles_vs_torch(cin, cout, k, stride, hw, nsrc):
 
 
 @pytest.mark.parametrize("cin,cout,h,w,B", [
+    (64, 192, 8, 32, 2),      # Analysis x2 / x3 shape class: 3 output blocks, 2 source blocks
+    (32, 96, 4, 64, 3),       # ragged output block (96 = 64 + 32), one patch row per image
+    (96, 64, 12, 32, 1),      # three source blocks, three patch rows
+])
+def test_wgrad_s2_vs_torch(cin, cout, h, w, B):
+    """The polyphase weight-gradient kernel of the 5x5 stride-2 convs (csrc/train.hip
+    wgrad_s2_kernel: 4 stride phases of the source staged as halos, tap (ky, kx) = phase
+    (ky & 1, kx & 1) at shift (ky >> 1, kx >> 1)) and its bias sums against
+    torch.nn.grad.conv2d_weight in fp32 on the same bf16-valued operands, borders included
+    (1e-4 norm-wise)."""
+    from rgbac import autograd as ag
+    rt = _rt()
+    g = _gen(cin + cout + h + w + 5)
+    x = torch.randn((B, cin, 2 * h, 2 * w), generator=g).bfloat16().float()
+    gy = torch.randn((B, cout, h, w), generator=g).bfloat16().float()
+    dev = torch.device("cuda")
+    S = [rt.to_nhwc(x.to(dev), torch.bfloat16)]
+    G = rt.to_nhwc(gy.to(dev), torch.bfloat16)
+    assert ag.wgrad_s2_ok(torch.bfloat16, S, 5, 2, 2, False, h, w)
+    n_pad = rt.round_up(G.ldc, 64)
+    cin_pad = S[0].ldc
+    k_pad = rt.round_up(25 * cin_pad, 64)
+    n_i = torch.arange(cout).view(-1, 1, 1)
+    tap = torch.arange(25).view(1, -1, 1)
+    c_i = torch.arange(cin).view(1, 1, -1)
+    fmap = torch.full((n_pad, k_pad), -1, dtype=torch.int32)
+    fmap[:cout].view(-1)[(n_i * k_pad + tap * cin_pad + c_i).reshape(-1)] = \
+        (((n_i * cin + c_i) * 5 + tap // 5) * 5 + tap % 5).reshape(-1).int()
+    numel = cout * cin * 25
+    dw, db = ag.wgrad(G, S, 5, 2, 2, False, k_pad, fmap.to(dev), numel, nbias=cout)
+    torch.cuda.synchronize()
+    want = torch.nn.grad.conv2d_weight(x, (cout, cin, 5, 5), gy, stride=2, padding=2)
+    assert nrel(dw.view(cout, cin, 5, 5), want) < 1e-4
+    assert nrel(db, gy.sum(dim=(0, 2, 3))) < 1e-4
+
+
+@pytest.mark.parametrize("cin,cout,h,w,B", [
     (32, 32, 32, 64, 2),      # the DSE 32 -> 32 conv shape (two 16-channel n tiles)
     (128, 8, 32, 32, 3),      # slice-stack tail 128 -> 8: one n tile, 4 channel blocks
     (64, 16, 16, 32, 2),      # 16 outputs, patch-high grid (2 patches per image)

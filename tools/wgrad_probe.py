@@ -21,17 +21,20 @@ def main():
     ap.add_argument("--batch", type=int, default=16)
     ap.add_argument("--ksize", type=int, default=3)
     ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--stride", type=int, default=1, help="2: the source at twice --hw")
     a = ap.parse_args()
     from rgbac import runtime as rt
     from rgbac.autograd import wgrad
     dev = torch.device("cuda:0")
     G = rt.to_nhwc(torch.randn((a.batch, a.cout, a.hw, a.hw), device=dev), torch.bfloat16)
-    S = rt.to_nhwc(torch.randn((a.batch, a.cin, a.hw, a.hw), device=dev), torch.bfloat16)
+    sh = a.hw * a.stride
+    S = rt.to_nhwc(torch.randn((a.batch, a.cin, sh, sh), device=dev), torch.bfloat16)
     n_pad = rt.round_up(G.ldc, 64)
     k_pad = rt.round_up(a.ksize * a.ksize * S.ldc, 64)
     fmap = torch.arange(n_pad * k_pad, dtype=torch.int32, device=dev).view(n_pad, k_pad)
     numel = n_pad * k_pad
-    run = lambda: wgrad(G, [S], a.ksize, 1, a.ksize // 2, False, k_pad, fmap, numel)  # noqa: E731
+    run = lambda: wgrad(G, [S], a.ksize, a.stride, a.ksize // 2, False, k_pad, fmap,  # noqa: E731
+                        numel)
     run()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -42,7 +45,7 @@ def main():
     e1.synchronize()
     us = e0.elapsed_time(e1) / a.iters * 1e3
     flop = 2.0 * a.batch * a.hw * a.hw * a.cout * a.ksize * a.ksize * a.cin
-    print(f"wgrad k{a.ksize} {a.cin}->{a.cout} {a.hw}x{a.hw} B{a.batch}: {us:.1f} us "
+    print(f"wgrad k{a.ksize}s{a.stride} {a.cin}->{a.cout} {a.hw}x{a.hw} B{a.batch}: {us:.1f} us "
           f"(kernel + reduce), {flop / us / 1e6:.1f} TF/s")
 
 
