@@ -924,36 +924,43 @@ __global__ void __launch_bounds__(256) wgrad_patch_kernel(const WgradDev a) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Polyphase weight gradient of the 5x5 stride-2 convs and ConvTransposes (bf16, pad 2, one
-// source, 32-channel source blocks x 64-channel output blocks): Analysis x2 / x3 and their
-// Synthesis ConvTranspose mirrors, 120 GFLOP per step at 64^2.  Through im2col the ring kernel
-// re-reads every source pixel ~6x per k tile and once per n tile (1.3 GB of L2 -> LDS traffic
-// per launch at 64^2 B16); here, as in the forward's polyphase patch conv, the source splits
-// into its 4 stride phases S_q[i][j] = S[2i + qy][2j + qx], and kernel tap (ky, kx) =
-// (2 ty + qy, 2 tx + qx) is a stride-1 tap (ty, tx) of phase q:
-//   dW[n][ky][kx][c] = sum_{o} G[o][n] * S_q[oy + ty - 1][ox + tx - 1][c].
-// A workgroup (8 waves) stages a 4 x 32-pixel G patch (64 channels) and the 4 phase halos
-// (6 x 34 pixels, 32 channels) once per patch by LDS-DMA (double-buffered, 136 KiB: one
-// workgroup per CU); the 50 (tap, 16-channel half) pairs are dealt to the waves (7 / 6 each),
-// every wave covering the 4 n tiles of the block, so accumulators (<= 28 tiles) stay in the
-// wave.  LDS rows: phase-halo pixels of 64 B, unswizzled (a pair's fragment address is then a
-// per-lane constant plus an immediate; 2-way bank conflicts on those reads), and G pixels of
-// 128 B (swizzle 2 bit1(r) ^ 4 bit3(r), conflict-free).  Slab layout as the ring kernel's.
+// Halo-staged weight gradients (bf16, 32-channel source blocks x 64-channel output blocks, up
+// to three concatenated sources):
+//   STRIDE 2: the 5x5 stride-2 pad-2 convs and ConvTransposes (Analysis x2 / x3, their
+//     Synthesis mirrors; 120 GFLOP per step at 64^2).  Through im2col the ring kernel re-reads
+//     every source pixel ~6x per k tile and once per n tile (1.3 GB of L2 -> LDS traffic per
+//     launch at 64^2 B16); here, as in the forward's polyphase patch conv, the source splits
+//     into its 4 stride phases S_q[i][j] = S[2i + qy][2j + qx], and kernel tap (ky, kx) =
+//     (2 ty + qy, 2 tx + qx) is a stride-1 tap (ty, tx) of phase q:
+//       dW[n][ky][kx][c] = sum_o G[o][n] * S_q[oy + ty - 1][ox + tx - 1][c];
+//   STRIDE 1: the 3x3 pad-1 convs with more than 32 outputs (slice stacks, residual units,
+//     hyper convs): one phase, tap (ky, kx) at shift (ky, kx) of the halo.
+// A workgroup (8 waves) stages a 4 x 32-pixel G patch (64 channels) and the phase halos
+// (6 x 34 pixels, 32 channels) once per patch by LDS-DMA (double-buffered: 136 KiB for stride
+// 2, one workgroup per CU; 58 KiB for stride 1, two); the (tap, 16-channel half) pairs are
+// dealt to the waves, every wave covering the block's 4 n tiles, so accumulators stay in the
+// wave.  LDS rows: halo pixels of 64 B, unswizzled (a pair's fragment address is then a
+// per-lane constant plus an immediate -- the address arithmetic of a swizzled, shifted row cost
+// ~5 VALU per MFMA, PMC -- at the price of 2-way bank conflicts on those reads), and G pixels
+// of 128 B (swizzle 2 bit1(r) ^ 4 bit3(r), conflict-free).  Slab layout as the ring kernel's.
 constexpr int kWsTH = 4, kWsTW = 32, kWsPW = kWsTW + 2;
 constexpr int kWsPRows = (kWsTH + 2) * kWsPW;          // 204 halo pixels per phase
 constexpr int kWsPPieces = (kWsPRows + 15) / 16;       // 13 one-KiB pieces per phase
-constexpr int kWsSPieces = 4 * kWsPPieces;             // 52
 constexpr int kWsGPieces = kWsTH * kWsTW * 128 / 1024; // 16 (128-B G rows)
-constexpr int kWsBuf = (kWsSPieces + kWsGPieces) * 1024;
 
 __device__ __forceinline__ int ws_swz128(int r) { return 2 * ((r >> 1) & 1) ^ 4 * ((r >> 3) & 1); }
 
-__global__ void __launch_bounds__(512) wgrad_s2_kernel(const WgradDev a) {
-  __shared__ __attribute__((aligned(16))) unsigned char ring[2 * kWsBuf];
+template <int STRIDE>
+__global__ void __launch_bounds__(512) wgrad_halo_kernel(const WgradDev a) {
+  constexpr bool S2 = STRIDE == 2;
+  constexpr int NPH = S2 ? 4 : 1, KS = S2 ? 5 : 3, NTAP = KS * KS, NPAIR = 2 * NTAP;
+  constexpr int SPIECES = NPH * kWsPPieces;             // 52 | 13
+  constexpr int BUF = (SPIECES + kWsGPieces) * 1024;
+  __shared__ __attribute__((aligned(16))) unsigned char ring[2 * BUF];
   constexpr int NW = 8;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ncb = a.cin_pad / 32;
+  const int ncb = (a.cin_pad + 31) / 32;
   int cb, nb, split;
   {
     const int nwg = gridDim.x * gridDim.y;
@@ -974,21 +981,36 @@ __global__ void __launch_bounds__(512) wgrad_s2_kernel(const WgradDev a) {
   const void* const zp = (const void*)g_wgrad_zero;
   const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(wg_lptr_t)ring);
 
-  // ---- DMA: S pieces q = wave + 8 j (< 52), G pieces q = wave + 8 j (< 16); the per-lane
-  // geometry is recomputed at each issue (a few VALU per patch) rather than held in registers
-  constexpr int PSW = (kWsSPieces + NW - 1) / NW, PGW = kWsGPieces / NW;   // 7, 2
-  const int nps = (kWsSPieces - wave + NW - 1) / NW;                       // 7 or 6
-  const char* const sbase = reinterpret_cast<const char*>(a.sp0) + cb * 64;
-  const long long sld2 = a.sld0 * 2, ldg2 = a.ldg * 2;
+  // ---- DMA: S pieces q = wave + 8 j, G pieces q = wave + 8 j (< 16); the halo geometry is
+  // recomputed at each issue (a few VALU per patch) rather than held in registers.  This lane's
+  // 8-channel chunk of the block: its source (up to three concatenated) and channel offset.
+  constexpr int PSW = (SPIECES + NW - 1) / NW, PGW = kWsGPieces / NW;
+  const int nps = (SPIECES - wave + NW - 1) / NW;
+  const char* sbase;
+  long long sld2;
+  bool schan;
+  {
+    const int ch = cb * 32 + 8 * (lane & 3);
+    const void* sp;
+    long long ld;
+    int cs;
+    if (ch < a.send0) { sp = a.sp0; ld = a.sld0; cs = ch; }
+    else if (ch < a.send1) { sp = a.sp1; ld = a.sld1; cs = ch - a.send0; }
+    else { sp = a.sp2; ld = a.sld2; cs = ch - a.send1; }
+    schan = ch < a.send2;
+    sbase = reinterpret_cast<const char*>(sp) + (schan ? cs : 0) * 2;
+    sld2 = ld * 2;
+  }
+  const long long ldg2 = a.ldg * 2;
   const char* const gbase = reinterpret_cast<const char*>(a.g);
 
   auto issue = [&](int p, int buf) {
     const int b = p / ppi, rem = p - b * ppi;
     const int oy0 = (rem / pw) * kWsTH, ox0 = (rem - (rem / pw) * pw) * kWsTW;
     const long long gpix0 = ((long long)b * H + oy0) * W + ox0;
-    const long long spix0 = ((long long)b * IH + 2 * oy0) * IW + 2 * ox0;
-    const uint32_t ls = lbase + (uint32_t)(buf * kWsBuf);
-    const uint32_t lg = ls + kWsSPieces * 1024;
+    const long long spix0 = ((long long)b * IH + STRIDE * oy0) * IW + STRIDE * ox0;
+    const uint32_t ls = lbase + (uint32_t)(buf * BUF);
+    const uint32_t lg = ls + SPIECES * 1024;
 #pragma unroll
     for (int j = 0; j < PSW; ++j) {
       if (j < nps) {
@@ -996,12 +1018,12 @@ __global__ void __launch_bounds__(512) wgrad_s2_kernel(const WgradDev a) {
         const int ph = q / kWsPPieces, pp = q - ph * kWsPPieces;
         const int R = 16 * pp + (lane >> 2);            // row within the phase halo
         const int i = R / kWsPW, jj = R - (R / kWsPW) * kWsPW;
-        // source pixel offset from (2 oy0, 2 ox0): rows 2 (i - 1) + qy, columns 2 (jj - 1) + qx
-        const int dy = 2 * (i - 1) + (ph >> 1), dx = 2 * (jj - 1) + (ph & 1);
-        const int sy = 2 * oy0 + dy, sx = 2 * ox0 + dx;
-        const bool ok = R < kWsPRows && (unsigned)sy < (unsigned)IH && (unsigned)sx < (unsigned)IW;
-        const int cs = (lane & 3) * 16;                // halo rows unswizzled (see below)
-        wg_dma16(ok ? (const void*)(sbase + (spix0 + (long long)dy * IW + dx) * sld2 + cs) : zp,
+        // source pixel offset from (STRIDE oy0, STRIDE ox0): rows STRIDE (i - 1) + qy, ...
+        const int dy = STRIDE * (i - 1) + (ph >> 1), dx = STRIDE * (jj - 1) + (ph & 1);
+        const int sy = STRIDE * oy0 + dy, sx = STRIDE * ox0 + dx;
+        const bool ok = schan && R < kWsPRows && (unsigned)sy < (unsigned)IH &&
+                        (unsigned)sx < (unsigned)IW;
+        wg_dma16(ok ? (const void*)(sbase + (spix0 + (long long)dy * IW + dx) * sld2) : zp,
                  ls + (uint32_t)(q * 1024));
       }
     }
@@ -1015,12 +1037,9 @@ __global__ void __launch_bounds__(512) wgrad_s2_kernel(const WgradDev a) {
     }
   };
 
-  // ---- this wave's (tap, channel half) pairs e = wave + 8 i < 50, all 4 n tiles.  The halo
-  // rows are NOT swizzled (2-way bank conflicts on these reads) so that a pair's fragment
-  // address is one per-lane register (set once per patch) plus the row's immediate offset:
-  // the address arithmetic of a swizzled, shifted row cost ~5 VALU per MFMA (PMC).
-  constexpr int NPR = (50 + NW - 1) / NW;               // 7
-  const int npr = (50 - wave + NW - 1) / NW;            // 7 or 6 (wave-uniform)
+  // ---- this wave's (tap, channel half) pairs e = wave + 8 i < NPAIR, all 4 n tiles
+  constexpr int NPR = (NPAIR + NW - 1) / NW;            // 7 | 3
+  const int npr = (NPAIR - wave + NW - 1) / NW;         // wave-uniform
   f32x4 acc[NPR][4];
 #pragma unroll
   for (int i = 0; i < NPR; ++i)
@@ -1036,11 +1055,12 @@ __global__ void __launch_bounds__(512) wgrad_s2_kernel(const WgradDev a) {
   int boff[NPR];                                         // relative to the S region of buffer 0
 #pragma unroll
   for (int i = 0; i < NPR; ++i) {
-    const int e = min(wave + NW * i, 49);
+    const int e = min(wave + NW * i, NPAIR - 1);
     const int tap = e >> 1, u = e & 1;
-    const int ky = tap / 5, kx = tap - 5 * (tap / 5);
-    const int ph = 2 * (ky & 1) + (kx & 1);
-    boff[i] = ph * (kWsPPieces * 1024) + ((ky >> 1) * kWsPW + (kx >> 1) + ra0) * 64 +
+    const int ky = tap / KS, kx = tap - KS * (tap / KS);
+    const int ph = S2 ? 2 * (ky & 1) + (kx & 1) : 0;
+    const int sy = S2 ? ky >> 1 : ky, sx = S2 ? kx >> 1 : kx;
+    boff[i] = ph * (kWsPPieces * 1024) + (sy * kWsPW + sx + ra0) * 64 +
               16 * (2 * u + (cq >> 1)) + 8 * (cq & 1);
   }
   const uint32_t rbase = (uint32_t)(size_t)(wg_lptr_t)ring;
@@ -1056,8 +1076,7 @@ __global__ void __launch_bounds__(512) wgrad_s2_kernel(const WgradDev a) {
       wg_wait_vm<0>();
     }
     __syncthreads();                                     // patch p landed for every wave
-    const unsigned char* Ss = ring + buf * kWsBuf;
-    const unsigned char* Gs = Ss + kWsSPieces * 1024;
+    const unsigned char* Gs = ring + buf * BUF + SPIECES * 1024;
     if (do_bias) {                                       // G column sums: 8 row groups x 64
       const int c = tid & 63, rg = tid >> 6;
 #pragma unroll 4
@@ -1067,8 +1086,8 @@ __global__ void __launch_bounds__(512) wgrad_s2_kernel(const WgradDev a) {
     }
     uint32_t bp[NPR];
 #pragma unroll
-    for (int i = 0; i < NPR; ++i) bp[i] = rbase + (uint32_t)(buf * kWsBuf) + (uint32_t)boff[i];
-    const uint32_t gp = rbase + (uint32_t)(buf * kWsBuf + kWsSPieces * 1024);
+    for (int i = 0; i < NPR; ++i) bp[i] = rbase + (uint32_t)(buf * BUF) + (uint32_t)boff[i];
+    const uint32_t gp = rbase + (uint32_t)(buf * BUF + SPIECES * 1024);
 #pragma unroll
     for (int yy = 0; yy < kWsTH; ++yy) {
       uint4 A[4];
@@ -1099,9 +1118,9 @@ __global__ void __launch_bounds__(512) wgrad_s2_kernel(const WgradDev a) {
 #pragma unroll
   for (int i = 0; i < NPR; ++i) {
     const int e = wave + NW * i;
-    if (e < 50) {
-      const int tap = e >> 1, u = e & 1;
-      const int k = tap * a.cin_pad + cb * 32 + 16 * u + fi;
+    const int ch = cb * 32 + 16 * (e & 1) + fi;
+    if (e < NPAIR && ch < a.cin_pad) {
+      const int k = (e >> 1) * a.cin_pad + ch;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
@@ -2282,17 +2301,29 @@ static bool wgrad_patch_ok(const rgbac_wgrad_args* a) {
          a->in_w == a->grid_w;
 }
 
-// The polyphase kernel's shapes (mirrored by rgbac.autograd.wgrad_s2_ok): bf16, 5x5 stride 2
-// pad 2, one source of whole 32-channel blocks, the output grid 4-row x 32-column patches of
-// half the input grid.  RGBAC_WGRAD_S2=0 turns it off.
-static bool wgrad_s2_ok(const rgbac_wgrad_args* a) {
+// The halo kernel's shapes (mirrored by rgbac.autograd.wgrad_halo_ok): bf16, no squared input,
+// 5x5 stride 2 pad 2, or 3x3 stride 1 pad 1 with more than 32 outputs; the output grid 4-row x
+// 32-column patches of the input grid (of half of it, stride 2).  RGBAC_WGRAD_HALO=0 turns
+// it off (RGBAC_WGRAD_S2=0: the stride-2 shapes only).  Returns the stride, 0 = not eligible.
+static int wgrad_halo_ok(const rgbac_wgrad_args* a) {
   static const bool on = [] {
+    const char* e = getenv("RGBAC_WGRAD_HALO");
+    return !(e && e[0] == '0');
+  }();
+  static const bool on2 = [] {
     const char* e = getenv("RGBAC_WGRAD_S2");
     return !(e && e[0] == '0');
   }();
-  return on && a->dtype == RGBAC_BF16 && !a->square_input && a->ksize == 5 && a->stride == 2 &&
-         a->pad == 2 && a->nsrc == 1 && a->cin_pad % 32 == 0 && a->grid_w % kWsTW == 0 &&
-         a->grid_h % kWsTH == 0 && a->in_h == 2 * a->grid_h && a->in_w == 2 * a->grid_w;
+  if (!on || a->dtype != RGBAC_BF16 || a->square_input || a->grid_w % kWsTW != 0 ||
+      a->grid_h % kWsTH != 0)
+    return 0;
+  if (on2 && a->ksize == 5 && a->stride == 2 && a->pad == 2 && a->in_h == 2 * a->grid_h &&
+      a->in_w == 2 * a->grid_w)
+    return 2;
+  if (a->ksize == 3 && a->stride == 1 && a->pad == 1 && a->g_channels > 32 &&
+      a->in_h == a->grid_h && a->in_w == a->grid_w)
+    return 1;
+  return 0;
 }
 
 extern "C" int rgbac_conv_wgrad(const rgbac_wgrad_args* a, void* stream) {
@@ -2352,14 +2383,15 @@ extern "C" int rgbac_conv_wgrad(const rgbac_wgrad_args* a, void* stream) {
     const char* e = getenv("RGBAC_WGRAD_RING");
     return !(e && e[0] == '0');
   }();
-  if (wgrad_s2_ok(a)) {
+  if (const int hs = wgrad_halo_ok(a)) {
     // 4 x 32-pixel patches of the output grid; nsplit workgroups per (32-channel source block,
     // 64-channel output block)
     const long long P = M / (kWsTH * kWsTW);
     d.m_chunk = (int)((P + a->nsplit - 1) / a->nsplit);
-    const dim3 sgrid((a->cin_pad / 32) * ((a->g_channels + 63) / 64), a->nsplit);
-    hipLaunchKernelGGL(wgrad_s2_kernel, sgrid, dim3(512), 0, st, d);
-    return check_launch("wgrad_s2_kernel");
+    const dim3 sgrid(((a->cin_pad + 31) / 32) * ((a->g_channels + 63) / 64), a->nsplit);
+    if (hs == 2) hipLaunchKernelGGL(wgrad_halo_kernel<2>, sgrid, dim3(512), 0, st, d);
+    else hipLaunchKernelGGL(wgrad_halo_kernel<1>, sgrid, dim3(512), 0, st, d);
+    return check_launch("wgrad_halo_kernel");
   }
   if (wgrad_patch_ok(a)) {
     // patches of 8 x 32 output pixels; nsplit workgroups per 32-channel source block

@@ -288,16 +288,24 @@ def wgrad_patch_ok(dtype, gch, S, ksize, stride, pad, square, grid_h, grid_w):
             grid_w % 32 == 0 and grid_h % 8 == 0 and s0.H == grid_h and s0.W == grid_w)
 
 
+WGRAD_HALO = os.environ.get("RGBAC_WGRAD_HALO", "1") != "0"
 WGRAD_S2 = os.environ.get("RGBAC_WGRAD_S2", "1") != "0"
 
 
-def wgrad_s2_ok(dtype, S, ksize, stride, pad, square, grid_h, grid_w):
-    """csrc/train.hip wgrad_s2_ok: the polyphase kernel's shapes (bf16, 5x5 stride 2 pad 2, one
-    source of whole 32-channel blocks, the grid 4 x 32-pixel patches of half the source)."""
+def wgrad_halo_ok(dtype, gch, S, ksize, stride, pad, square, grid_h, grid_w):
+    """csrc/train.hip wgrad_halo_ok: 2 / 1 when the halo-staged kernel takes the shape (bf16;
+    5x5 stride 2 pad 2, or 3x3 stride 1 pad 1 with more than 32 outputs; the grid 4 x 32-pixel
+    patches of the source grid, or of half of it), else 0."""
     s0 = S[0]
-    return (WGRAD_S2 and dtype == torch.bfloat16 and not square and ksize == 5 and
-            stride == 2 and pad == 2 and len(S) == 1 and s0.ldc % 32 == 0 and
-            grid_w % 32 == 0 and grid_h % 4 == 0 and s0.H == 2 * grid_h and s0.W == 2 * grid_w)
+    if not (WGRAD_HALO and dtype == torch.bfloat16 and not square and grid_w % 32 == 0 and
+            grid_h % 4 == 0):
+        return 0
+    if (WGRAD_S2 and ksize == 5 and stride == 2 and pad == 2 and s0.H == 2 * grid_h and
+            s0.W == 2 * grid_w):
+        return 2
+    if ksize == 3 and stride == 1 and pad == 1 and gch > 32 and s0.H == grid_h and s0.W == grid_w:
+        return 1
+    return 0
 
 
 def _nsplit(tiles, M, slab, target=1024):
@@ -317,12 +325,14 @@ def wgrad(G, S, ksize, stride, pad, square, k_pad, fmap, numel, nbias=0, bias_fr
     dev = G.t.device
     n_pad = round_up(G.ldc, 64)
     M = G.B * G.H * G.W
-    if wgrad_s2_ok(G.t.dtype, S, ksize, stride, pad, square, G.H, G.W):
-        # one workgroup per CU (136 KiB of LDS): ~256 per launch over the (32-channel source
-        # block, 64-channel output block) pairs, each at least 2 patches of 4 x 32 pixels
-        # (floor: one workgroup more than the 256 CUs would run a second, nearly empty round)
-        tiles = (S[0].ldc // 32) * -(-G.ldc // 64)
-        ns = int(max(1, min(256 // tiles, M // 256, _SLAB_FLOATS // (n_pad * k_pad))))
+    hs = wgrad_halo_ok(G.t.dtype, G.ldc, S, ksize, stride, pad, square, G.H, G.W)
+    if hs:
+        # workgroups over (32-channel source block, 64-channel output block) pairs: one per CU
+        # for stride 2 (136 KiB of LDS), two for stride 1 (58 KiB); each at least 2 patches of
+        # 4 x 32 pixels (floor: a workgroup past a full round would run a nearly empty one)
+        tiles = -(-sum(f.ldc for f in S) // 32) * -(-G.ldc // 64)
+        ns = int(max(1, min((256 if hs == 2 else 512) // tiles, M // 256,
+                            _SLAB_FLOATS // (n_pad * k_pad))))
     elif wgrad_patch_ok(G.t.dtype, G.ldc, S, ksize, stride, pad, square, G.H, G.W):
         # one workgroup per (32-channel block, run of 8 x 32-pixel patches): <= 512 in flight
         # (two per CU), each at least 2 patches so the double-buffered staging overlaps

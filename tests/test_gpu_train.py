@@ -810,7 +810,7 @@ def test_wgrad_wide_tiles_vs_torch(cin, cout, k, stride, hw, nsrc):
 ])
 def test_wgrad_s2_vs_torch(cin, cout, h, w, B):
     """The polyphase weight-gradient kernel of the 5x5 stride-2 convs (csrc/train.hip
-    wgrad_s2_kernel: 4 stride phases of the source staged as halos, tap (ky, kx) = phase
+    wgrad_halo_kernel<2>: 4 stride phases of the source staged as halos, tap (ky, kx) = phase
     (ky & 1, kx & 1) at shift (ky >> 1, kx >> 1)) and its bias sums against
     torch.nn.grad.conv2d_weight in fp32 on the same bf16-valued operands, borders included
     (1e-4 norm-wise)."""
@@ -822,7 +822,7 @@ def test_wgrad_s2_vs_torch(cin, cout, h, w, B):
     dev = torch.device("cuda")
     S = [rt.to_nhwc(x.to(dev), torch.bfloat16)]
     G = rt.to_nhwc(gy.to(dev), torch.bfloat16)
-    assert ag.wgrad_s2_ok(torch.bfloat16, S, 5, 2, 2, False, h, w)
+    assert ag.wgrad_halo_ok(torch.bfloat16, G.ldc, S, 5, 2, 2, False, h, w) == 2
     n_pad = rt.round_up(G.ldc, 64)
     cin_pad = S[0].ldc
     k_pad = rt.round_up(25 * cin_pad, 64)
@@ -837,6 +837,50 @@ def test_wgrad_s2_vs_torch(cin, cout, h, w, B):
     torch.cuda.synchronize()
     want = torch.nn.grad.conv2d_weight(x, (cout, cin, 5, 5), gy, stride=2, padding=2)
     assert nrel(dw.view(cout, cin, 5, 5), want) < 1e-4
+    assert nrel(db, gy.sum(dim=(0, 2, 3))) < 1e-4
+
+
+@pytest.mark.parametrize("cuts,cout,h,w,B", [
+    ((96, 128), 128, 32, 32, 2),     # slice-stack conv over two concatenated sources (224 -> 128)
+    ((40,), 40, 32, 32, 2),          # 40 -> 40: partial source block, partial output block
+    ((80, 32, 8), 224, 8, 64, 1),    # three sources (a block straddles them), 4 output blocks
+    ((96,), 96, 4, 32, 3),           # one patch per image, n blocks 64 + 32
+])
+def test_wgrad_halo_s1_vs_torch(cuts, cout, h, w, B):
+    """The stride-1 halo weight-gradient kernel (csrc/train.hip wgrad_halo_kernel<1>: the
+    3x3 convs with more than 32 outputs; taps as shifted halo rows, up to three concatenated
+    sources, ragged channel blocks) and its bias sums against torch.nn.grad.conv2d_weight in
+    fp32 on the same bf16-valued operands (1e-4 norm-wise)."""
+    from rgbac import autograd as ag
+    rt = _rt()
+    cin = sum(cuts)
+    g = _gen(cin + cout + h + w + 7)
+    x = torch.randn((B, cin, h, w), generator=g).bfloat16().float()
+    gy = torch.randn((B, cout, h, w), generator=g).bfloat16().float()
+    dev = torch.device("cuda")
+    S, off = [], 0
+    for cc in cuts:
+        S.append(rt.to_nhwc(x[:, off:off + cc].to(dev), torch.bfloat16))
+        off += cc
+    G = rt.to_nhwc(gy.to(dev), torch.bfloat16)
+    assert ag.wgrad_halo_ok(torch.bfloat16, G.ldc, S, 3, 1, 1, False, h, w) == 1
+    n_pad = rt.round_up(G.ldc, 64)
+    cin_pad = sum(f.ldc for f in S)
+    k_pad = rt.round_up(9 * cin_pad, 64)
+    pos, o = [], 0
+    for f, cc in zip(S, cuts):
+        pos.extend(range(o, o + cc))
+        o += f.ldc
+    fmap = torch.full((n_pad, k_pad), -1, dtype=torch.int32)
+    for n in range(cout):
+        for tap in range(9):
+            for c, pc in enumerate(pos):
+                fmap[n, tap * cin_pad + pc] = ((n * cin + c) * 3 + tap // 3) * 3 + tap % 3
+    numel = cout * cin * 9
+    dw, db = ag.wgrad(G, S, 3, 1, 1, False, k_pad, fmap.to(dev), numel, nbias=cout)
+    torch.cuda.synchronize()
+    want = torch.nn.grad.conv2d_weight(x, (cout, cin, 3, 3), gy, stride=1, padding=1)
+    assert nrel(dw.view(cout, cin, 3, 3), want) < 1e-4
     assert nrel(db, gy.sum(dim=(0, 2, 3))) < 1e-4
 
 
