@@ -734,10 +734,10 @@ __global__ void __launch_bounds__(64 * WGN * WGK) wgrad_ring_kernel(const WgradD
 // here a workgroup stages one 8 x 32-pixel output patch of G and its 10 x 34 source halo
 // (one 32-channel block) ONCE per patch by LDS-DMA, and every tap reads the halo at a shifted
 // row: the 32 pixels of one output row segment are 32 consecutive halo rows.
-//   LDS rows are pixels of 64 B (32 channels); 16-B chunk c of row r sits at c ^ 2*bit3(r),
-//   which keeps the transposed fragment reads (rows base + 8q + {0..3}, +4) of every
-//   32-lane half on 64 distinct banks for ANY base row (exhaustively checked offline), so the
-//   tap shift costs no conflicts.
+//   LDS rows are pixels of 64 B (32 channels).  G rows: 16-B chunk c of row r at c ^ 2*bit3(r)
+//   (conflict-free transposed reads).  Halo rows are unswizzled: a (tap, half) pair's fragment
+//   address is then a per-lane register plus the row's immediate offset (a swizzled, shifted
+//   row cost ~5 VALU of address math per MFMA), for 2-way bank conflicts on those reads.
 //   The 18 (tap, 16-channel half) pairs of the block are dealt to the 4 waves (5/5/4/4); each
 //   wave runs all 8 row segments of the patch for its pairs and both 16-channel n tiles, so the
 //   accumulators never cross waves: each lane stores its own slab elements.
@@ -787,7 +787,7 @@ __global__ void __launch_bounds__(256) wgrad_patch_kernel(const WgradDev a) {
   for (int j = 0; j < PSW; ++j) {
     const int q = wave + 4 * j;                         // S piece = halo rows 16 q .. 16 q + 15
     const int R = 16 * q + (lane >> 2);
-    s_c[j] = ((lane & 3) ^ wp_swz(R)) * 16;             // the global chunk this lane fetches
+    s_c[j] = (lane & 3) * 16;                           // halo rows unswizzled (see below)
     s_i[j] = R / kWpPW;
     s_j[j] = R - s_i[j] * kWpPW;
     s_on[j] = q < kWpSPieces && R < kWpSRows;
@@ -840,6 +840,18 @@ __global__ void __launch_bounds__(256) wgrad_patch_kernel(const WgradDev a) {
   int aoff[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) aoff[t] = ra0 * 64 + 16 * ((2 * t + (cq >> 1)) ^ wp_swz(ra0)) + 8 * (cq & 1);
+  // per-lane fragment offsets of this wave's pairs (unswizzled halo rows: the address is this
+  // register plus the row's immediate, no per-read arithmetic)
+  const int npr = (18 - wave + 3) / 4;                  // 5 or 4 (wave-uniform)
+  int boff[5];
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int e = min(wave + 4 * i, 17);
+    const int tap = e >> 1, u = e & 1;
+    const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+    boff[i] = (ky * kWpPW + kx + ra0) * 64 + 16 * (2 * u + (cq >> 1)) + 8 * (cq & 1);
+  }
+  const uint32_t rbase = (uint32_t)(size_t)(wg_lptr_t)ring;
 
   if (pbeg < pend) issue(pbeg, 0);
   for (int p = pbeg, it = 0; p < pend; ++p, ++it) {
@@ -861,29 +873,27 @@ __global__ void __launch_bounds__(256) wgrad_patch_kernel(const WgradDev a) {
         bacc += bf2f(*reinterpret_cast<const uint16_t*>(
             Gs + r * 64 + 16 * ((c >> 3) ^ wp_swz(r)) + (c & 7) * 2));
     }
-#pragma unroll 1
+    uint32_t bp[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) bp[i] = rbase + (uint32_t)(buf * kWpBuf) + (uint32_t)boff[i];
+    const uint32_t gp = rbase + (uint32_t)(buf * kWpBuf + kWpSPieces * 1024);
+#pragma unroll 2
     for (int yy = 0; yy < kWpTH; ++yy) {
       uint4 A[NT];
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
-        const unsigned char* q = Gs + aoff[t] + yy * 32 * 64;
-        const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)q);
-        const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s_ptr)(q + 4 * 64));
+        const lds_v4s_ptr q = (lds_v4s_ptr)(size_t)(gp + aoff[t] + yy * 32 * 64);
+        const v4s a0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(q);
+        const v4s a1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(q + 4 * 64 / 8);
         const uint2 u0 = __builtin_bit_cast(uint2, a0), u1 = __builtin_bit_cast(uint2, a1);
         A[t] = make_uint4(u0.x, u0.y, u1.x, u1.y);
       }
 #pragma unroll
       for (int i = 0; i < 5; ++i) {
-        const int e = wave + 4 * i;
-        if (e < 18) {                                    // wave-uniform
-          const int tap = e >> 1, u = e & 1;
-          const int ky = tap / 3, kx = tap - 3 * (tap / 3);
-          const int r0 = (yy + ky) * kWpPW + kx + ra0, r1 = r0 + 4;
-          const int ch = 2 * u + (cq >> 1);
-          const v4s b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_v4s_ptr)(Ss + r0 * 64 + 16 * (ch ^ wp_swz(r0)) + 8 * (cq & 1)));
-          const v4s b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_v4s_ptr)(Ss + r1 * 64 + 16 * (ch ^ wp_swz(r1)) + 8 * (cq & 1)));
+        if (i < npr) {                                   // wave-uniform
+          const lds_v4s_ptr q = (lds_v4s_ptr)(size_t)(bp[i] + yy * kWpPW * 64);
+          const v4s b0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(q);
+          const v4s b1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(q + 4 * 64 / 8);
           const uint2 u0 = __builtin_bit_cast(uint2, b0), u1 = __builtin_bit_cast(uint2, b1);
           const uint4 B = make_uint4(u0.x, u0.y, u1.x, u1.y);
 #pragma unroll
