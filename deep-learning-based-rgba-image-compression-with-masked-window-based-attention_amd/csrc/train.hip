@@ -2094,7 +2094,7 @@ struct CopyTask {
   const void* src;
   void* dst;
   long long lds, ldd;                           // row strides, elements
-  int scoff, dcoff, C, vec;
+  int scoff, dcoff, C, vec, acc;                // acc: dst += src (one rounding)
 };
 struct CopyTasks { CopyTask t[16]; };
 
@@ -2110,8 +2110,26 @@ channel_copy_multi_kernel(long long npix, CopyTasks tasks) {
     for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
       int c;
       const long long p = ediv(e, cv, rc, c);
-      *reinterpret_cast<uint4*>(static_cast<T*>(k.dst) + p * k.ldd + k.dcoff + c * E) =
-          *reinterpret_cast<const uint4*>(static_cast<const T*>(k.src) + p * k.lds + k.scoff + c * E);
+      uint4* d = reinterpret_cast<uint4*>(static_cast<T*>(k.dst) + p * k.ldd + k.dcoff + c * E);
+      uint4 v = *reinterpret_cast<const uint4*>(static_cast<const T*>(k.src) + p * k.lds + k.scoff + c * E);
+      if (k.acc) {
+        const uint4 o = *d;
+        if constexpr (sizeof(T) == 2) {
+          const uint32_t a[4] = {o.x, o.y, o.z, o.w}, b[4] = {v.x, v.y, v.z, v.w};
+          uint32_t r[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            r[q] = pack_bf16x2(bf2f(a[q] & 0xFFFF) + bf2f(b[q] & 0xFFFF),
+                               bf2f(a[q] >> 16) + bf2f(b[q] >> 16));
+          v = make_uint4(r[0], r[1], r[2], r[3]);
+        } else {
+          v = make_uint4(__float_as_uint(__uint_as_float(o.x) + __uint_as_float(v.x)),
+                         __float_as_uint(__uint_as_float(o.y) + __uint_as_float(v.y)),
+                         __float_as_uint(__uint_as_float(o.z) + __uint_as_float(v.z)),
+                         __float_as_uint(__uint_as_float(o.w) + __uint_as_float(v.w)));
+        }
+      }
+      *d = v;
     }
   } else {
     const long long n = npix * k.C;
@@ -2119,8 +2137,16 @@ channel_copy_multi_kernel(long long npix, CopyTasks tasks) {
     for (long long e = blockIdx.x * 256ll + threadIdx.x; e < n; e += (long long)gridDim.x * 256) {
       int c;
       const long long p = ediv(e, k.C, rc, c);
-      static_cast<T*>(k.dst)[p * k.ldd + k.dcoff + c] =
-          static_cast<const T*>(k.src)[p * k.lds + k.scoff + c];
+      T* d = static_cast<T*>(k.dst) + p * k.ldd + k.dcoff + c;
+      const T s = static_cast<const T*>(k.src)[p * k.lds + k.scoff + c];
+      if (k.acc) {
+        if constexpr (sizeof(T) == 2)
+          *d = (T)f2bf(bf2f(*d) + bf2f(s));
+        else
+          *d = *d + s;
+      } else {
+        *d = s;
+      }
     }
   }
 }
@@ -2680,8 +2706,8 @@ extern "C" int rgbac_channel_copy(int dtype, int64_t npix, int channels, const v
   return check_launch("channel_copy_kernel");
 }
 
-extern "C" int rgbac_channel_copy_multi(int dtype, int64_t npix, int ntasks, const int64_t* desc,
-                                        void* stream) {
+static int copy_multi(int dtype, int64_t npix, int ntasks, const int64_t* desc, int nfield,
+                      void* stream) {
   RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
   RGBAC_REQUIRE(npix >= 0 && ntasks >= 1 && ntasks <= 16 && desc, "shape");
   if (npix == 0) return RGBAC_OK;
@@ -2689,8 +2715,9 @@ extern "C" int rgbac_channel_copy_multi(int dtype, int64_t npix, int ntasks, con
   CopyTasks tk;
   long long maxc = 0;
   for (int i = 0; i < ntasks; ++i) {
-    const int64_t* d = desc + 7 * i;          // src, lds, scoff, channels, dst, ldd, dcoff
+    const int64_t* d = desc + nfield * i;     // src, lds, scoff, channels, dst, ldd, dcoff[, acc]
     CopyTask& k = tk.t[i];
+    k.acc = nfield > 7 ? (int)d[7] : 0;
     k.src = reinterpret_cast<const void*>(d[0]);
     k.lds = d[1];
     k.scoff = (int)d[2];
@@ -2712,6 +2739,16 @@ extern "C" int rgbac_channel_copy_multi(int dtype, int64_t npix, int ntasks, con
   else
     hipLaunchKernelGGL(channel_copy_multi_kernel<uint16_t>, grid, dim3(256), 0, st, npix, tk);
   return check_launch("channel_copy_multi_kernel");
+}
+
+extern "C" int rgbac_channel_copy_multi(int dtype, int64_t npix, int ntasks, const int64_t* desc,
+                                        void* stream) {
+  return copy_multi(dtype, npix, ntasks, desc, 7, stream);
+}
+
+extern "C" int rgbac_channel_copy_multi_ex(int dtype, int64_t npix, int ntasks,
+                                           const int64_t* desc, void* stream) {
+  return copy_multi(dtype, npix, ntasks, desc, 8, stream);
 }
 
 extern "C" int rgbac_weight_gather(int dtype, int64_t n, const float* src, const int32_t* idx,

@@ -145,6 +145,7 @@ SIGNATURES = {
     "rgbac_pixel_shuffle": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _I64, _VP, _I64, _VP],
     "rgbac_channel_copy": [_I32, _I64, _I32, _VP, _I64, _I32, _VP, _I64, _I32, _VP],
     "rgbac_channel_copy_multi": [_I32, _I64, _I32, _VP, _VP],
+    "rgbac_channel_copy_multi_ex": [_I32, _I64, _I32, _VP, _VP],
     "rgbac_weight_gather": [_I32, _I64, _VP, _VP, _VP, _VP],
     "rgbac_weight_gather_multi": [_I32, _VP, _VP, _I64, _VP],
     "rgbac_colsum": [_I32, _I64, _I32, _VP, _I64, _I32, _VP, _VP],

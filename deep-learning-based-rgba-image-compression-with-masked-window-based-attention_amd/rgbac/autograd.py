@@ -410,12 +410,16 @@ class ConvCall:
     returns (z, act(z)) and leaves its activation backward to its consumer; ``src_act`` /
     ``src_param``: this conv's source is such a deferred output -- its input-gradient conv
     applies the producer's activation backward in its epilogue (DGELU / DLRELU)."""
-    __slots__ = ("tc", "src_C", "act", "act_param", "square", "defer", "src_act", "src_param")
+    __slots__ = ("tc", "src_C", "act", "act_param", "square", "defer", "src_act", "src_param",
+                 "sink", "src_sinks", "res_sinks", "zsink")
 
     def __init__(self, tc, src_C, act, act_param, square=False, defer=False, src_act=None,
                  src_param=0.0):
         self.tc, self.src_C, self.act, self.act_param = tc, list(src_C), act, act_param
         self.square, self.defer, self.src_act, self.src_param = square, defer, src_act, src_param
+        # gradient sinks: of this conv's output, of its sources / residual operands / folded
+        # producer (rgbac.autograd.Sink)
+        self.sink, self.src_sinks, self.res_sinks, self.zsink = None, (), (None,) * 3, None
 
 
 class ActFeat(Feat):
@@ -464,6 +468,48 @@ def _direct_grad(p):
     return g
 
 
+class Sink:
+    """Gradient buffer of one autograd-tracked training activation (a ConvFn / CatFn output).
+    Consumers that know the protocol (ConvFn sources and residual operands, CatFn parts) add
+    their gradient here and hand autograd None; the producer's backward takes the buffer (plus
+    whatever ordinary gradient autograd still delivers from other consumers).  A multiply-used
+    activation -- the slice supports used by up to 11 concatenations, every residual-unit and
+    attention-block input -- then costs no autograd add: the first deposit adopts the tensor,
+    later ones accumulate inside the input-gradient conv's epilogue (res0 = the buffer) or the
+    concatenation split's copy (rgbac_channel_copy_multi_ex).  autograd still runs the
+    producer after every consumer (its dependency count does not depend on the values)."""
+    __slots__ = ("buf", "own")
+
+    def __init__(self):
+        self.buf, self.own = None, False
+
+
+GRAD_SINKS = os.environ.get("RGBAC_GRAD_SINKS", "1") != "0"
+
+
+def _sink(t):
+    return getattr(t, "_rgbac_sink", None) if (GRAD_SINKS and t is not None) else None
+
+
+def _deposit(sink, g, own):
+    """sink += g.  own: g is a fresh tensor nobody else holds (adoptable, accumulable)."""
+    if sink.buf is None:
+        sink.buf, sink.own = g, own
+    elif sink.own:
+        sink.buf.add_(g)
+    else:
+        sink.buf, sink.own = sink.buf + g, True
+
+
+def _take(sink, g):
+    """The producer's output gradient: its sink plus the gradient autograd delivered."""
+    if sink is None or sink.buf is None:
+        return g
+    if g is None:
+        return sink.buf
+    return sink.buf + g
+
+
 class ConvFn(Function):
     @staticmethod
     def forward(ctx, call, weight, bias, res0, res1, res2, sel, zsrc, *srcs):
@@ -500,9 +546,9 @@ class ConvFn(Function):
                               zsrc, *srcs)
         if sel is not None:
             ctx.mark_non_differentiable(sel)
+        ctx.set_materialize_grads(False)
         if call.defer:
             ctx.mark_non_differentiable(out.t)
-            ctx.set_materialize_grads(False)
             return z.t, out.t
         return out.t
 
@@ -513,7 +559,9 @@ class ConvFn(Function):
         weight, z_t, r1_t, sel, zsrc, *srcs = ctx.saved_tensors
         has_b, has0, has1, has2 = ctx.has
         B, Ho, Wo, Cs = ctx.shape
-        assert dy_t is not None, "deferred-activation conv output without a consumer gradient"
+        dy_t = _take(call.sink, dy_t)
+        if dy_t is None:                              # no consumer contributed a gradient
+            return (None,) * (8 + len(srcs))
         dy = Feat(dy_t.contiguous(), Cs)
         dt = dy.t.dtype
         act = call.act
@@ -534,6 +582,19 @@ class ConvFn(Function):
             elif act in ("gate", "igdn", "gdn") and not call.square:
                 g_res1 = dr1.t
         g_res2 = dy.t if has2 else None
+        # residual gradients into their operands' sinks; a tensor is adopted by at most one
+        # sink, and dy (autograd's or this conv's own sink buffer) never
+        adopted = set()
+        res_g = [g_res0, g_res1, g_res2]
+        for j, sk in enumerate(call.res_sinks):
+            if sk is not None and res_g[j] is not None:
+                g = res_g[j]
+                own = g is not dy.t and id(g) not in adopted
+                if own:
+                    adopted.add(id(g))
+                _deposit(sk, g, own)
+                res_g[j] = None
+        g_res0, g_res1, g_res2 = res_g
         feats = [Feat(t, c) for t, c in zip(srcs, call.src_C)]
         # the conv's own output-gradient grid
         if tc.kind == "subpel":
@@ -549,27 +610,49 @@ class ConvFn(Function):
         g_zsrc = None
         preps = []
         idxs = []
+        sinks_in = []
         for i, f in enumerate(feats):
             folded = call.src_act is not None and i == 0
             if not (need[7] if folded else need[8 + i]):
                 continue
+            sk = call.zsink if folded else (call.src_sinks[i] if call.src_sinks else None)
             pk = tc.bwd_pack(i, dt, weight.detach().contiguous())
-            o = new_feat(f.B, f.H, f.W, f.C, dt, f.t.device)   # zero-filled iff padded
             if call.square:
+                o = new_feat(f.B, f.H, f.W, f.C, dt, f.t.device)   # zero-filled iff padded
                 preps.append(rt.prepare(pk, [G.src()], out=o, act="sqbwd", res0=dr1,
                                         res1=f, bias=False))
             elif folded:
                 # dL/dz of the producer = (W^T G) * act'(z): its activation backward here
+                o = new_feat(f.B, f.H, f.W, f.C, dt, f.t.device)
                 preps.append(rt.prepare(pk, [G.src()], out=o, act=call.src_act,
                                         act_param=call.src_param, res0=Feat(zsrc, f.C),
                                         bias=False))
+            elif sk is not None and sk.buf is not None:
+                # accumulate in the epilogue: out = W^T G + buffer (in place when the buffer
+                # is ours -- every element is read and written by the same lane -- and not an
+                # operand of this very launch)
+                prev = Feat(sk.buf, f.C)
+                inplace = sk.own and all(sk.buf is not t for t in (G.t, dz.t, dy.t))
+                o = prev if inplace else new_feat(f.B, f.H, f.W, f.C, dt, f.t.device)
+                preps.append(rt.prepare(pk, [G.src()], out=o, res0=prev, bias=False))
+                sk.buf, sk.own = o.t, True
+                sk = None                               # deposited by the launch itself
             else:
+                o = new_feat(f.B, f.H, f.W, f.C, dt, f.t.device)
                 preps.append(rt.prepare(pk, [G.src()], out=o, bias=False))
             idxs.append(i)
+            sinks_in.append(sk)
         if preps:
             outs = rt.launch(preps)
-            for i, o in zip(idxs, outs):
-                if call.src_act is not None and i == 0:
+            for i, o, sk in zip(idxs, outs, sinks_in):
+                folded = call.src_act is not None and i == 0
+                if folded or call.src_sinks:
+                    target = call.zsink if folded else call.src_sinks[i]
+                    if target is not None:
+                        if sk is not None:
+                            _deposit(sk, o.t, True)
+                        continue                          # (accumulated in place otherwise)
+                if folded:
                     g_zsrc = o.t
                 else:
                     g_srcs[i] = o.t
@@ -640,6 +723,11 @@ def conv_t(m, srcs, act="none", act_param=0.0, res0=None, res1=None, res2=None, 
     wshape = tuple(w.shape) if w.dim() == 4 else (w.shape[0], w.shape[1], 1, 1)
     tc = train_conv_of(m, kind, wshape, stride, segs, dev)
     call = ConvCall(tc, [f.C for f in srcs], act, act_param, square, defer, src_act, src_param)
+    if GRAD_SINKS:
+        call.sink = Sink()
+        call.src_sinks = tuple(None if isinstance(f, ActFeat) else _sink(f.t) for f in srcs)
+        call.res_sinks = tuple(None if r is None else _sink(r.t) for r in (res0, res1, res2))
+        call.zsink = _sink(zsrc)
     w4 = w if w.dim() == 4 else w.reshape(wshape)
     out = ConvFn.apply(call, w4, b, None if res0 is None else res0.t,
                        None if res1 is None else res1.t, None if res2 is None else res2.t,
@@ -647,7 +735,11 @@ def conv_t(m, srcs, act="none", act_param=0.0, res0=None, res1=None, res2=None, 
     C = tc.cout // 4 if kind == "subpel" else tc.cout
     if defer:
         z_t, o_t = out
+        if call.sink is not None:
+            z_t._rgbac_sink = call.sink
         return ActFeat(o_t, C, z_t, _DEFERRABLE[act], act_param if act == "lrelu" else 0.0)
+    if call.sink is not None:
+        out._rgbac_sink = call.sink
     return Feat(out, C)
 
 
@@ -745,9 +837,20 @@ def _copy(dst, dcoff, src, scoff, C):
 _CAT_MULTI = os.environ.get("RGBAC_CAT_MULTI", "1") != "0"
 
 
-def _copy_multi(pairs, npix):
+def _copy_multi(pairs, npix, accs=None):
     """[(dst Feat, dst channel offset, src Feat, src channel offset, channels)] -> one
-    rgbac_channel_copy_multi launch per 16 copies."""
+    rgbac_channel_copy_multi launch per 16 copies; ``accs``: per pair, add into dst instead."""
+    if accs is not None and any(accs):
+        for k in range(0, len(pairs), 16):
+            part, acc = pairs[k:k + 16], accs[k:k + 16]
+            desc = (ctypes.c_int64 * (8 * len(part)))()
+            for i, ((dst, dcoff, src, scoff, C), a) in enumerate(zip(part, acc)):
+                desc[8 * i: 8 * i + 8] = [src.ptr(), src.ldc, scoff, C, dst.ptr(), dst.ldc, dcoff,
+                                          1 if a else 0]
+            src0 = part[0][2]
+            _lib.call("rgbac_channel_copy_multi_ex", _lib.dtype_code(src0.t.dtype), npix,
+                      len(part), ctypes.addressof(desc), _lib.stream_ptr(src0.t.device))
+        return
     if not _CAT_MULTI:
         for dst, dcoff, src, scoff, C in pairs:
             _copy(dst, dcoff, src, scoff, C)
@@ -768,7 +871,8 @@ class CatFn(Function):
     likewise."""
 
     @staticmethod
-    def forward(ctx, Cs, *ts):
+    def forward(ctx, meta, *ts):
+        Cs, sink, part_sinks = meta
         fs = [Feat(t, c) for t, c in zip(ts, Cs)]
         f0 = fs[0]
         out = new_feat(f0.B, f0.H, f0.W, sum(Cs), f0.t.dtype, f0.t.device)
@@ -777,24 +881,42 @@ class CatFn(Function):
             pairs.append((out, off, f, 0, f.C))
             off += f.C
         _copy_multi(pairs, f0.B * f0.H * f0.W)
-        ctx.Cs = Cs
+        ctx.meta = meta
         ctx.shapes = [t.shape for t in ts]
+        ctx.set_materialize_grads(False)
         return out.t
 
     @staticmethod
     def backward(ctx, g):
-        g = Feat(g.contiguous(), sum(ctx.Cs))
-        outs, pairs = [], []
+        Cs, sink, part_sinks = ctx.meta
+        g = _take(sink, g)
+        if g is None:
+            return (None,) * (1 + len(Cs))
+        g = Feat(g.contiguous(), sum(Cs))
+        outs, pairs, accs = [], [], []
         off = 0
-        for c, shp in zip(ctx.Cs, ctx.shapes):
-            # the copy writes channels [0, c) of every pixel: only channel padding (ldc > c)
-            # needs the zero fill (the slice supports are unpadded: ~140 fills per step saved)
-            alloc = torch.empty if shp[-1] == c else torch.zeros
-            o = Feat(alloc(shp, dtype=g.t.dtype, device=g.t.device), c)
-            pairs.append((o, 0, g, off, c))
+        for c, shp, sk in zip(Cs, ctx.shapes, part_sinks):
+            if sk is not None and sk.buf is not None:
+                # add this part's slice into the producer's gradient buffer
+                if not sk.own:
+                    sk.buf, sk.own = sk.buf.clone(), True
+                pairs.append((Feat(sk.buf, c), 0, g, off, c))
+                accs.append(True)
+                outs.append(None)
+            else:
+                # the copy writes channels [0, c) of every pixel: only channel padding
+                # (ldc > c) needs the zero fill (the slice supports are unpadded)
+                alloc = torch.empty if shp[-1] == c else torch.zeros
+                o = Feat(alloc(shp, dtype=g.t.dtype, device=g.t.device), c)
+                pairs.append((o, 0, g, off, c))
+                accs.append(False)
+                if sk is not None:
+                    sk.buf, sk.own = o.t, True
+                    outs.append(None)
+                else:
+                    outs.append(o.t)
             off += c
-            outs.append(o.t)
-        _copy_multi(pairs, g.B * g.H * g.W)
+        _copy_multi(pairs, g.B * g.H * g.W, accs)
         return (None, *outs)
 
 
@@ -802,7 +924,12 @@ def cat_t(feats):
     if len(feats) == 1:
         return feats[0]
     Cs = [f.C for f in feats]
-    return Feat(CatFn.apply(Cs, *[f.t for f in feats]), sum(Cs))
+    sink = Sink() if GRAD_SINKS else None
+    part_sinks = tuple(_sink(f.t) for f in feats)
+    out = CatFn.apply((Cs, sink, part_sinks), *[f.t for f in feats])
+    if sink is not None:
+        out._rgbac_sink = sink
+    return Feat(out, sum(Cs))
 
 
 class SliceFn(Function):

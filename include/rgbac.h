@@ -398,6 +398,15 @@ int rgbac_channel_copy(int dtype, int64_t npix, int channels, const void* src, i
 int rgbac_channel_copy_multi(int dtype, int64_t npix, int ntasks, const int64_t* desc,
                              void* stream);
 
+/* rgbac_channel_copy_multi with an 8th descriptor field per task: accumulate (0 = copy,
+ * 1 = dst += src, rounded once to the element type).  The backward split of a concatenation
+ * adds each part's gradient slice straight into the gradient buffer its producer reads (the
+ * training step's activation-gradient sinks, rgbac/autograd.py), in place of a copy plus an
+ * autograd add (trainRGB.py:187 rd_loss.backward(): the slice supports of
+ * AutoEncoderRGB_Journal.py:249-262 are each used by up to 11 later concatenations).   */
+int rgbac_channel_copy_multi_ex(int dtype, int64_t npix, int ntasks, const int64_t* desc,
+                                void* stream);
+
 /* Weight repack through a cached index map: dst[i] = idx[i] >= 0 ? src[idx[i]] : 0
  * (src = fp32 PyTorch parameter, dst = packed [nphase][cout_pad][k_pad]).   */
 int rgbac_weight_gather(int dtype, int64_t n, const float* src, const int32_t* idx, void* dst,

@@ -679,13 +679,24 @@ def test_channel_copy_multi(dtype):
         assert torch.equal(cat.t[..., : cat.C], want)
         gy = torch.randn(cat.t.shape, generator=g).to(dtype).cuda()
         leaves = [p.t.requires_grad_(True) for p in parts]
-        out = ag.CatFn.apply(Cs, *leaves)
+        out = ag.CatFn.apply((Cs, None, (None,) * len(Cs)), *leaves)
         out.backward(gy)
         off = 0
         for p, c in zip(leaves, Cs):
             assert torch.equal(p.grad[..., :c], gy[..., off:off + c])
             assert not p.grad[..., c:].any()
             off += c
+    # accumulate mode (rgbac_channel_copy_multi_ex: a concatenation's backward split adding
+    # into gradient sinks): dst += src, one rounding to the element type, copies beside it
+    dst = [Feat(torch.randn((B, H, W, c), generator=g).to(dtype).cuda(), c) for c in (16, 8, 24)]
+    src = Feat(torch.randn((B, H, W, 48), generator=g).to(dtype).cuda(), 48)
+    want = [d.t.float() + src.t[..., o:o + d.C].float() for d, o in zip(dst, (0, 16, 24))]
+    want[1] = src.t[..., 16:24].float()
+    ag._copy_multi([(d, 0, src, o, d.C) for d, o in zip(dst, (0, 16, 24))], B * H * W,
+                   [True, False, True])
+    torch.cuda.synchronize()
+    for d, w in zip(dst, want):
+        assert torch.equal(d.t, w.to(dtype))
 
 
 def test_reference_loop_torch_adam_clip_matches_adam_clamp():
