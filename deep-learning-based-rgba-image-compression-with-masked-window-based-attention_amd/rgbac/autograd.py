@@ -75,6 +75,24 @@ class TPack:
         self.src = None                # (weight ptr, bias ptr) of the last refresh
         self.token = 0                 # == _PREFETCH[0]: re-gathered by this step's prefetch
         self.gen = -1                  # rt.PARAM_GEN at that prefetch (an optimizer step bumps it)
+        self.frag = self.fidx = None   # fragment-major copy (runtime.frag_weights layout)
+
+    def enable_frag(self):
+        """Also gather the fragment-major copy the conv_fpatch / conv_npatch tiles read
+        (runtime.frag_weights' layout, built here from the index map: the same permutation
+        of slots), refreshed with the plain pack every step -- so the training convs can take
+        the forward's fragment-streamed tiles."""
+        nph, rows, _ = self.idx.shape
+        taps = 9 if self.mode == CONVT_S2 else self.ksize * self.ksize
+        cp, c32 = self.cin_pad, round_up(self.cin_pad, 32)
+        w = self.idx[:, :, :taps * cp].reshape(nph, rows, taps, cp)
+        wt = torch.full((nph, rows, taps, c32), -1, dtype=torch.int32, device=self.idx.device)
+        wt[..., :cp] = w
+        nks = taps * c32 // 32
+        self.fidx = wt.reshape(nph, rows // 16, 16, nks, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
+        self.frag = torch.zeros(self.fidx.shape, dtype=self.w.dtype, device=self.idx.device)
+        self.src = None                # gather both at the next refresh
+        return self
 
     def refresh(self, weight, bias=None):
         # re-gathered every training step: the optimizer kernel updates parameters in
@@ -90,6 +108,10 @@ class TPack:
         dev = w.device
         _lib.call("rgbac_weight_gather", _lib.dtype_code(self.w.dtype), self.w.numel(),
                   w.data_ptr(), self.idx.data_ptr(), self.w.data_ptr(), _lib.stream_ptr(dev))
+        if self.frag is not None:
+            _lib.call("rgbac_weight_gather", _lib.dtype_code(self.frag.dtype), self.frag.numel(),
+                      w.data_ptr(), self.fidx.data_ptr(), self.frag.data_ptr(),
+                      _lib.stream_ptr(dev))
         if bias is not None:
             b = bias.detach()
             _lib.call("rgbac_weight_gather", _lib.F32, self.bias.numel(), b.data_ptr(),
@@ -131,8 +153,9 @@ def prefetch_packs(model):
         rows, blk0 = [], [0]
         for tp in packs:
             for dst, idx, sp, dt in ((tp.w, tp.idx, tp.src[0], _lib.dtype_code(tp.w.dtype)),
+                                     (tp.frag, tp.fidx, tp.src[0], _lib.dtype_code(tp.w.dtype)),
                                      (tp.bias, tp.bias_idx, tp.src[1], _lib.F32)):
-                if sp is None or idx is None or dst.numel() == 0:
+                if sp is None or idx is None or dst is None or dst.numel() == 0:
                     continue
                 n = dst.numel()
                 rows.append([sp, idx.data_ptr(), dst.data_ptr(), n, dt])
@@ -228,6 +251,8 @@ class TrainConv:
             pk, idx = self.fwd
             nb = self.cout if self.kind != "subpel" else pk.cout
             tp = TPack(pk, idx, dtype, self._bidx(pk, nb))
+            if _frag_eligible(tp):
+                tp.enable_frag()
             self._fw[dtype] = tp
         return tp.refresh(weight, bias)
 
@@ -236,8 +261,22 @@ class TrainConv:
         if tp is None:
             pk, idx = self.bwd[i]
             tp = TPack(pk, idx, dtype)
+            if _frag_eligible(tp):
+                tp.enable_frag()
             self._bw[(i, dtype)] = tp
         return tp.refresh(weight, None)
+
+
+# RGBAC_TRAIN_FRAG=0: training packs without the fragment-major copy (plain-layout tiles only)
+TRAIN_FRAG = os.environ.get("RGBAC_TRAIN_FRAG", "1") != "0"
+
+
+def _frag_eligible(tp):
+    """Packs the fragment-streamed tiles can take: bf16, 3x3 stride-1 conv / subpel conv, or
+    the 5x5/s2 ConvTranspose (runtime._patch_tiles, _npatch_ok)."""
+    return (TRAIN_FRAG and tp.w.dtype == torch.bfloat16 and
+            ((tp.mode in (CONV, SUBPEL2) and tp.ksize == 3 and tp.stride == 1) or
+             tp.mode == CONVT_S2))
 
 
 def train_conv_of(m, kind, wshape, stride, segs, device):

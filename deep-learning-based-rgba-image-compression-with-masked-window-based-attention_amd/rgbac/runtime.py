@@ -203,6 +203,13 @@ def frag_weights(pk):
     return fr
 
 
+def _has_frag(pk):
+    """A pack the fragment-streamed tiles can read: a forward PackedConv (its fragment-major
+    copy built once, frag_weights) or a training pack gathering one every step
+    (rgbac.autograd.TPack.enable_frag)."""
+    return isinstance(pk, PackedConv) or getattr(pk, "frag", None) is not None
+
+
 def _patch_tiles(preps):
     """Patch-resident tiles that apply to these (grouped) convs: bf16, the 5x5/s2 convT or a
     3x3 stride-1 conv/subpel, no squared input / GAUSS epilogue, M grid a multiple of 16 wide
@@ -232,7 +239,8 @@ def _patch_tiles(preps):
             out.append(t)
     # fragment-streamed tiles: PackedConv weights only (the training packs are re-gathered
     # every step in the plain layout) and the whole patch in LDS; no strided conv
-    if not s2 and all(isinstance(p.pk, PackedConv) for p in preps):
+    if not s2 and all(_has_frag(p.pk) for p in preps) and \
+            a.act not in (ACT["dgelu"], ACT["dlrelu"]):
         c32 = max(round_up(p.pk.cin_pad, 32) for p in preps)
         for t, (th, bn) in FPATCH_SIG.items():
             if hm % th or (th + 2) * 18 * (c32 // 8 + 2) * 16 > 160 * 1024:
@@ -570,6 +578,10 @@ def prepare(pk, srcs, out=None, out_coff=0, act="none", act_param=0.0, res0=None
     pr.nst = -(-taps * pk.cin_pad // (32 if dtype == torch.float32 else 64))
     pr.nks = -(-taps * pk.cin_pad // (16 if dtype == torch.float32 else 32))
     pr.key = f"{a.dtype}/{pk.mode}/{pk.ksize}/{pk.stride}/{B}x{H}x{W}/{pk.cin_pad}/{pk.cout}/{act == 'gauss'}"
+    if act in ("dgelu", "dlrelu"):
+        # the folded activation backward runs in other instances and not on the
+        # fragment-streamed tiles: its own choice
+        pr.key += "/dact"
     pr.flops = 2.0 * pr.mgrid * pk.cout * pk.cin * (25 if pk.mode == CONVT_S2 else taps)
     es = f0.t.element_size()
     pr.nbytes = es * (B * H * W * pk.cin + B * Ho * Wo * cstore) + pk.w.numel() * es
@@ -653,7 +665,7 @@ def _npatch_ok(preps):
             a.stride == 1 and a.in_w % 16 == 0 and a.in_h % 4 == 0 and
             a.batch * a.in_h * a.in_w < (1 << 24)):
         return False
-    if not all(isinstance(p.pk, PackedConv) for p in preps):
+    if not all(_has_frag(p.pk) for p in preps) or a.act in (ACT["dgelu"], ACT["dlrelu"]):
         return False
     for p in preps:
         if p.pk.cout > 32 or 6 * 18 * (round_up(p.pk.cin_pad, 32) // 8 + 2) * 16 > 128 * 1024:
@@ -852,9 +864,8 @@ def launch(preps, force=None):
         # count, the residual operands, the activation or the pack type, so the same key
         # can come from a conv the special tiles accept (e.g. TILE_PW tuned on a
         # one-source conv, handed a two-source one), or a fragment-streamed tile tuned on a
-        # forward PackedConv handed a training pack (TPack weights are re-gathered in the
-        # plain layout every step, a cached fragment-major copy would go stale) -- take the
-        # shape rule
+        # pack with a fragment-major copy handed one without it, or an input-gradient conv
+        # with the folded activation backward (not in those tiles) -- take the shape rule
         choice = _heuristic(p0.mgrid * p0.nphase * n, max(pr.pk.cout for pr in preps),
                             max(pr.nst for pr in preps))
     if gauss and not (choice[0] == TILE_WSTREAM and _wstream_ok(preps)) and \
