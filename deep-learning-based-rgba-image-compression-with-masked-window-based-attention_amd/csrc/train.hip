@@ -1222,6 +1222,61 @@ wgrad_reduce_wide_kernel(long long nslot, const int* __restrict__ fmap,
   }
 }
 
+// Up to 8 reductions in one launch (rgbac_wgrad_reduce_multi): task t owns blocks
+// [blk0[t], blk0[t + 1]); each block is wgrad_reduce_wide_kernel's 32 slots x 8 split groups.
+struct ReduceTask {
+  long long nslot, slab;
+  const int* fmap;
+  const float* part;
+  float* dw;
+  const float* bpart;
+  float* db;
+  int nsplit, nbias, n_pad, acc;
+};
+struct ReduceTasks {
+  ReduceTask t[8];
+  int blk0[9];
+  int ntask;
+};
+
+__global__ void __launch_bounds__(256) wgrad_reduce_multi_kernel(const ReduceTasks tasks) {
+  __shared__ float red[8][32];
+  int ti = 0;
+  while (ti + 1 < tasks.ntask && (int)blockIdx.x >= tasks.blk0[ti + 1]) ++ti;
+  const ReduceTask& k = tasks.t[ti];
+  const int sl = threadIdx.x & 31, sg = threadIdx.x >> 5;
+  const long long e = (long long)(blockIdx.x - tasks.blk0[ti]) * 32 + sl;
+  const long long total = k.nslot + k.nbias;
+  float acc = 0.0f;
+  if (e < total) {
+    const bool wslot = e < k.nslot;
+    if (!wslot || k.fmap[e] >= 0) {
+      const float* src = wslot ? k.part + e : k.bpart + (e - k.nslot);
+      const long long stride = wslot ? k.slab : (long long)k.n_pad;
+      int q = sg;
+      for (; q + 24 < k.nsplit; q += 32) {
+        const float v0 = src[q * stride], v1 = src[(q + 8) * stride];
+        const float v2 = src[(q + 16) * stride], v3 = src[(q + 24) * stride];
+        acc += v0; acc += v1; acc += v2; acc += v3;
+      }
+      for (; q < k.nsplit; q += 8) acc += src[q * stride];
+    }
+  }
+  red[sg][sl] = acc;
+  __syncthreads();
+  if (sg == 0 && e < total) {
+    float s = red[0][sl];
+#pragma unroll
+    for (int g = 1; g < 8; ++g) s += red[g][sl];
+    if (e < k.nslot) {
+      const int i = k.fmap[e];
+      if (i >= 0) k.dw[i] = k.acc ? k.dw[i] + s : s;
+    } else {
+      k.db[e - k.nslot] = k.acc ? k.db[e - k.nslot] + s : s;
+    }
+  }
+}
+
 // ------------------------------------------------------------------ attention core backward
 // Recomputes P = softmax(q k^T * scale + B + M) per window (fp32, same op order
 // as the VALU forward), then dV = P^T dO, dP = dO V^T, dS = P (dP - rowsum(P dP)),
@@ -2480,6 +2535,39 @@ extern "C" int rgbac_wgrad_reduce(int64_t nslot, const int32_t* fmap, const floa
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(grid_for(nslot + nbias)), dim3(256), 0, st, nslot,
                      fmap, partial, nsplit, slab, dw, nbias, bias_partial, n_pad, db, accumulate);
   return check_launch("wgrad_reduce_kernel");
+}
+
+extern "C" int rgbac_wgrad_reduce_multi(int ntasks, const int64_t* tasks, void* stream) {
+  RGBAC_REQUIRE(ntasks >= 1 && ntasks <= 8 && tasks, "1..8 tasks");
+  ReduceTasks tk{};
+  tk.ntask = ntasks;
+  tk.blk0[0] = 0;
+  for (int i = 0; i < ntasks; ++i) {
+    const int64_t* d = tasks + 11 * i;
+    ReduceTask& k = tk.t[i];
+    k.nslot = d[0];
+    k.fmap = reinterpret_cast<const int*>(d[1]);
+    k.part = reinterpret_cast<const float*>(d[2]);
+    k.nsplit = (int)d[3];
+    k.slab = d[4];
+    k.dw = reinterpret_cast<float*>(d[5]);
+    k.nbias = (int)d[6];
+    k.bpart = reinterpret_cast<const float*>(d[7]);
+    k.n_pad = (int)d[8];
+    k.db = reinterpret_cast<float*>(d[9]);
+    k.acc = (int)d[10];
+    RGBAC_REQUIRE(k.nslot >= 0 && k.nsplit >= 1 && k.slab > 0 && k.nslot <= k.slab, "shape");
+    RGBAC_REQUIRE((k.nslot == 0 || (k.fmap && k.part && k.dw)) &&
+                      (k.nbias == 0 || (k.bpart && k.db)), "null pointer");
+    RGBAC_REQUIRE(k.nbias <= k.n_pad, "nbias > n_pad");
+    const long long nb = (k.nslot + k.nbias + 31) / 32;
+    RGBAC_REQUIRE(tk.blk0[i] + nb < (1ll << 31), "too many blocks");
+    tk.blk0[i + 1] = tk.blk0[i] + (int)nb;
+  }
+  if (tk.blk0[ntasks] == 0) return RGBAC_OK;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(wgrad_reduce_multi_kernel, dim3((unsigned)tk.blk0[ntasks]), dim3(256), 0, st, tk);
+  return check_launch("wgrad_reduce_multi_kernel");
 }
 
 template <typename T, int WS, int DH>

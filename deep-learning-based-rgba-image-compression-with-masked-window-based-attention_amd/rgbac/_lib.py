@@ -129,6 +129,7 @@ SIGNATURES = {
                       _I64, _VP, _I64, _VP],
     "rgbac_conv_wgrad": [ctypes.POINTER(WgradArgs), _VP],
     "rgbac_wgrad_reduce": [_I64, _VP, _VP, _I32, _I64, _VP, _I32, _VP, _I32, _VP, _I32, _VP],
+    "rgbac_wgrad_reduce_multi": [_I32, _VP, _VP],
     "rgbac_winattn_core_bwd": [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _F, _VP,
                                _I64, _VP, _VP, _VP, _I64, _VP, _I64, _I32, _VP, _VP],
     "rgbac_winattn_core_bwd_ex": [_I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _I32, _F,

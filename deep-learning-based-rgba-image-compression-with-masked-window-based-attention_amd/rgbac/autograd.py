@@ -313,6 +313,7 @@ def wgrad_tile(dtype, n_pad, k_pad, square):
 _WG_TARGET_BIG = int(os.environ.get("RGBAC_WGRAD_TARGET_BIG", "256"))
 _WG_TARGET = int(os.environ.get("RGBAC_WGRAD_TARGET", "1024"))
 _WG_CEIL = os.environ.get("RGBAC_WGRAD_CEIL", "0") == "1"
+_HALO_WG = int(os.environ.get("RGBAC_WGRAD_HALO_WG", "512"))   # stride-1 halo kernel target
 
 
 WGRAD_PATCH = os.environ.get("RGBAC_WGRAD_PATCH", "1") != "0"
@@ -356,6 +357,57 @@ def _nsplit(tiles, M, slab, target=1024):
     return int(max(1, min(want, -(-M // 512), cap, 1024)))
 
 
+# Weight-gradient reductions that add into param.grad (DIRECT_GRAD) are queued and issued
+# eight at a time by rgbac_wgrad_reduce_multi -- a reduce launch is a few microseconds of
+# mostly fixed cost, ~195 per training step.  The queue is flushed when it is full, before any
+# reduction whose result autograd reads (not accumulated into .grad), at the end of the
+# backward pass (an engine callback), and by the data-parallel bucket hooks before they
+# all-reduce (rgbac.parallel).  Measured neutral on config 3 (49.30 vs 49.25 MPix/s: the
+# reductions are bound by their slab reads, not launch cost), so RGBAC_REDUCE_BATCH=1 opts in.
+REDUCE_BATCH = os.environ.get("RGBAC_REDUCE_BATCH", "0") == "1"   # measured neutral: off
+_PENDING = []                   # (task int64 x 11, keep-alive tensors)
+_PENDING_CB = [False]
+
+
+def flush_reductions():
+    """Issue every queued weight-gradient reduction (one launch per 8)."""
+    while _PENDING:
+        part = _PENDING[:8]
+        del _PENDING[:8]
+        desc = (ctypes.c_int64 * (11 * len(part)))()
+        for i, (task, _) in enumerate(part):
+            desc[11 * i: 11 * i + 11] = task
+        dev = part[0][1][0].device
+        _lib.call("rgbac_wgrad_reduce_multi", len(part), ctypes.addressof(desc),
+                  _lib.stream_ptr(dev))
+
+
+def _end_of_backward():
+    _PENDING_CB[0] = False
+    flush_reductions()
+
+
+def _reduce(nslot, fmap, part, nsplit, slab, dw, nbias, bpart, n_pad, db, acc, st):
+    if not (REDUCE_BATCH and acc):
+        flush_reductions()
+        _lib.call("rgbac_wgrad_reduce", nslot, None if fmap is None else fmap.data_ptr(),
+                  None if part is None else part.data_ptr(), nsplit, slab,
+                  None if dw is None else dw.data_ptr(), nbias,
+                  None if bpart is None else bpart.data_ptr(), n_pad,
+                  None if db is None else db.data_ptr(), 1 if acc else 0, st)
+        return
+    keep = [t for t in (part, bpart, fmap, dw, db) if t is not None]
+    task = [nslot, 0 if fmap is None else fmap.data_ptr(), 0 if part is None else part.data_ptr(),
+            nsplit, slab, 0 if dw is None else dw.data_ptr(), nbias,
+            0 if bpart is None else bpart.data_ptr(), n_pad, 0 if db is None else db.data_ptr(), 1]
+    _PENDING.append((task, keep))
+    if not _PENDING_CB[0]:
+        torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
+        _PENDING_CB[0] = True
+    if len(_PENDING) >= 8:
+        flush_reductions()
+
+
 def wgrad(G, S, ksize, stride, pad, square, k_pad, fmap, numel, nbias=0, bias_from_g=True,
           acc_dw=None, acc_db=None):
     """dW (fp32, flat param layout) and optional db from G (Feat on the M grid) and
@@ -370,7 +422,7 @@ def wgrad(G, S, ksize, stride, pad, square, k_pad, fmap, numel, nbias=0, bias_fr
         # for stride 2 (136 KiB of LDS), two for stride 1 (58 KiB); each at least 2 patches of
         # 4 x 32 pixels (floor: a workgroup past a full round would run a nearly empty one)
         tiles = -(-sum(f.ldc for f in S) // 32) * -(-G.ldc // 64)
-        ns = int(max(1, min((256 if hs == 2 else 512) // tiles, M // 256,
+        ns = int(max(1, min((256 if hs == 2 else _HALO_WG) // tiles, M // 256,
                             _SLAB_FLOATS // (n_pad * k_pad))))
     elif wgrad_patch_ok(G.t.dtype, G.ldc, S, ksize, stride, pad, square, G.H, G.W):
         # one workgroup per (32-channel block, run of 8 x 32-pixel patches): <= 512 in flight
@@ -415,10 +467,8 @@ def wgrad(G, S, ksize, stride, pad, square, k_pad, fmap, numel, nbias=0, bias_fr
     if nbias and not bias_from_g:
         raise ValueError("use colsum for biases not on G")
     nslot = min(fmap.shape[0], n_pad) * k_pad
-    _lib.call("rgbac_wgrad_reduce", nslot, fmap.data_ptr(), part.data_ptr(), ns,
-              n_pad * k_pad, dw.data_ptr(), nbias if bpart is not None else 0,
-              None if bpart is None else bpart.data_ptr(), n_pad,
-              None if db is None else db.data_ptr(), 1 if acc else 0, st)
+    _reduce(nslot, fmap, part, ns, n_pad * k_pad, dw, nbias if bpart is not None else 0, bpart,
+            n_pad, db, acc, st)
     return dw, db
 
 
@@ -433,8 +483,7 @@ def colsum(f, C, acc=None):
     _lib.call("rgbac_colsum", _lib.dtype_code(f.t.dtype), npix, C, f.ptr(), f.ldc, ns,
               part.data_ptr(), st)
     db = acc if acc is not None else torch.empty(C, dtype=_F32, device=dev)
-    _lib.call("rgbac_wgrad_reduce", 0, None, None, ns, 1, None, C, part.data_ptr(), C,
-              db.data_ptr(), 1 if acc is not None else 0, st)
+    _reduce(0, None, None, ns, 1, None, C, part, C, db, acc is not None, st)
     return db
 
 

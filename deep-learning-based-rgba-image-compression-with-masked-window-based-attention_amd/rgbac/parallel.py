@@ -177,6 +177,10 @@ class GradBuckets:
                                "the learning step (the autograd graph changed between steps)")
 
     def _launch(self, b):
+        # the weight-gradient reductions still queued by rgbac.autograd add into these
+        # gradients: issue them first (stream order then puts them before the collective)
+        from .autograd import flush_reductions
+        flush_reductions()
         if self.skip:
             self.works[b] = []
             return

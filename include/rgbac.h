@@ -325,6 +325,13 @@ int rgbac_wgrad_reduce(int64_t nslot, const int32_t* fmap, const float* partial,
                        int64_t slab, float* dw, int nbias, const float* bias_partial, int n_pad,
                        float* db, int accumulate, void* stream);
 
+/* Up to 8 rgbac_wgrad_reduce calls in one launch: tasks[11*t ..] = {nslot, fmap, partial,
+ * nsplit, slab, dw, nbias, bias_partial, n_pad, db, accumulate} as int64 (pointers as
+ * integers), each task the same fixed-order sum as rgbac_wgrad_reduce.  The training step
+ * queues the weight-gradient reductions that add straight into param.grad and issues them in
+ * batches (~195 reduce launches per step otherwise, each a few microseconds of fixed cost). */
+int rgbac_wgrad_reduce_multi(int ntasks, const int64_t* tasks, void* stream);
+
 /* Backward of rgbac_winattn_core: dqkv [B,H,W,>=3C] (dq, dk, dv; zero for
  * dropped windows) and per-block dense bias gradients bias_partial
  * [nblk][heads][N][N] (N = ws*ws), reduced by rgbac_relpos_bwd into the
