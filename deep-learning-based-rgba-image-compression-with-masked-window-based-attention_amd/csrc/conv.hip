@@ -1844,7 +1844,7 @@ __global__ void __launch_bounds__(512, 4) conv_pw_kernel(const ConvArgsDev args)
       }
       PWW_LOAD(bv[st], st, nrowp, nvalid);
     }
-    if (valid) {
+    if (valid && !g.res0 && !g.res2) {
       // res1 quads of the whole tile (raw bf16), all requested before any epilogue math
       uint2 e1[NT];
 #pragma unroll
@@ -1862,12 +1862,48 @@ __global__ void __launch_bounds__(512, 4) conv_pw_kernel(const ConvArgsDev args)
           for (int r = 0; r < 4; ++r) { in.r0[r] = 0.f; in.r2[r] = 0.f; }
           in.r1[0] = bf2f(e1[j].x & 0xFFFF); in.r1[1] = bf2f(e1[j].x >> 16);
           in.r1[2] = bf2f(e1[j].y & 0xFFFF); in.r1[3] = bf2f(e1[j].y >> 16);
-          if (g.res0) load_res<bf16_t>(g.res0, g.ld0, mm, n, cout, in.r0);
-          if (g.res2) load_res<bf16_t>(g.res2, g.ld2, mm, n, cout, in.r2);
           in.on = sel_on;
           float v[4] = {acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
           const float bias[4] = {bl[n], bl[n + 1], bl[n + 2], bl[n + 3]};
           epilogue4_fin<bf16_t, DACT>(s, g, (long long)m, n, v, bias, in);
+        }
+      }
+    } else if (valid) {
+      // with res0 / res2 (the gate's x, the training step's in-place gradient accumulation):
+      // every residual quad of a third of the tile requested before that third's math and
+      // stores -- the output may alias a residual, so a load behind a store waits for it, and
+      // loading per quad serialised one memory latency per quad (12 per tile)
+      const bf16_t* const R0 = reinterpret_cast<const bf16_t*>(g.res0);
+      const bf16_t* const R2 = reinterpret_cast<const bf16_t*>(g.res2);
+#pragma unroll
+      for (int h = 0; h < 3; ++h) {
+        constexpr int NH = NT / 3;
+        uint2 e0[NH], e1[NH], e2[NH];
+#pragma unroll
+        for (int jj = 0; jj < NH; ++jj) {
+          const int n = 16 * (NH * h + jj) + 4 * fq;
+          const bool on = n < cout;
+          e0[jj] = (R0 && on) ? *reinterpret_cast<const uint2*>(R0 + mm * g.ld0 + n) : make_uint2(0, 0);
+          e1[jj] = (R1 && on) ? *reinterpret_cast<const uint2*>(R1 + mm * g.ld1 + n) : make_uint2(0, 0);
+          e2[jj] = (R2 && on) ? *reinterpret_cast<const uint2*>(R2 + mm * g.ld2 + n) : make_uint2(0, 0);
+        }
+#pragma unroll
+        for (int jj = 0; jj < NH; ++jj) {
+          const int j = NH * h + jj;
+          const int n = 16 * j + 4 * fq;
+          if (n < cout) {
+            EpiIn in;
+            in.r0[0] = bf2f(e0[jj].x & 0xFFFF); in.r0[1] = bf2f(e0[jj].x >> 16);
+            in.r0[2] = bf2f(e0[jj].y & 0xFFFF); in.r0[3] = bf2f(e0[jj].y >> 16);
+            in.r1[0] = bf2f(e1[jj].x & 0xFFFF); in.r1[1] = bf2f(e1[jj].x >> 16);
+            in.r1[2] = bf2f(e1[jj].y & 0xFFFF); in.r1[3] = bf2f(e1[jj].y >> 16);
+            in.r2[0] = bf2f(e2[jj].x & 0xFFFF); in.r2[1] = bf2f(e2[jj].x >> 16);
+            in.r2[2] = bf2f(e2[jj].y & 0xFFFF); in.r2[3] = bf2f(e2[jj].y >> 16);
+            in.on = sel_on;
+            float v[4] = {acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
+            const float bias[4] = {bl[n], bl[n + 1], bl[n + 2], bl[n + 3]};
+            epilogue4_fin<bf16_t, DACT>(s, g, (long long)m, n, v, bias, in);
+          }
         }
       }
     }

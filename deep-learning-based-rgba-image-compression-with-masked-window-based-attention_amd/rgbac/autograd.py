@@ -566,10 +566,12 @@ class Sink:
     later ones accumulate inside the input-gradient conv's epilogue (res0 = the buffer) or the
     concatenation split's copy (rgbac_channel_copy_multi_ex).  autograd still runs the
     producer after every consumer (its dependency count does not depend on the values)."""
-    __slots__ = ("buf", "own")
+    __slots__ = ("buf", "own", "slices")
 
     def __init__(self):
-        self.buf, self.own = None, False
+        # slices: the buffer holds only disjoint channel slices written so far (GaussFn),
+        # so another slice may be written into it without an add
+        self.buf, self.own, self.slices = None, False, False
 
 
 GRAD_SINKS = os.environ.get("RGBAC_GRAD_SINKS", "1") != "0"
@@ -581,6 +583,7 @@ def _sink(t):
 
 def _deposit(sink, g, own):
     """sink += g.  own: g is a fresh tensor nobody else holds (adoptable, accumulable)."""
+    sink.slices = False
     if sink.buf is None:
         sink.buf, sink.own = g, own
     elif sink.own:
@@ -723,7 +726,7 @@ class ConvFn(Function):
                 inplace = sk.own and all(sk.buf is not t for t in (G.t, dz.t, dy.t))
                 o = prev if inplace else new_feat(f.B, f.H, f.W, f.C, dt, f.t.device)
                 preps.append(rt.prepare(pk, [G.src()], out=o, res0=prev, bias=False))
-                sk.buf, sk.own = o.t, True
+                sk.buf, sk.own, sk.slices = o.t, True, False
                 sk = None                               # deposited by the launch itself
             else:
                 o = new_feat(f.B, f.H, f.W, f.C, dt, f.t.device)
@@ -988,6 +991,7 @@ class CatFn(Function):
                 # add this part's slice into the producer's gradient buffer
                 if not sk.own:
                     sk.buf, sk.own = sk.buf.clone(), True
+                sk.slices = False
                 pairs.append((Feat(sk.buf, c), 0, g, off, c))
                 accs.append(True)
                 outs.append(None)
@@ -999,7 +1003,7 @@ class CatFn(Function):
                 pairs.append((o, 0, g, off, c))
                 accs.append(False)
                 if sk is not None:
-                    sk.buf, sk.own = o.t, True
+                    sk.buf, sk.own, sk.slices = o.t, True, False
                     outs.append(None)
                 else:
                     outs.append(o.t)
@@ -1098,7 +1102,7 @@ class GaussFn(Function):
     """One latent slice: (hat = ste_round(y - mu) + mu, sum of clamped bits)."""
 
     @staticmethod
-    def forward(ctx, y_t, Cy, coff, cs, mu_t, sc_t, noise):
+    def forward(ctx, y_t, Cy, coff, cs, mu_t, sc_t, noise, sinks=None):
         y = Feat(y_t, Cy)
         mu, sc = Feat(mu_t, cs), Feat(sc_t, cs)
         dev = y_t.device
@@ -1112,19 +1116,28 @@ class GaussFn(Function):
         bits = torch.empty(1, dtype=_F32, device=dev)
         _lib.call("rgbac_sum_partials", 1, nb, part.data_ptr(), bits.data_ptr(),
                   _lib.stream_ptr(dev))
-        ctx.meta = (Cy, coff, cs)
+        ctx.meta = (Cy, coff, cs, sinks)
         ctx.save_for_backward(y_t, mu_t, sc_t, noise)
+        ctx.set_materialize_grads(False)
         return hat.t, bits.reshape(())
 
     @staticmethod
     def backward(ctx, dhat, dbits):
-        Cy, coff, cs = ctx.meta
+        Cy, coff, cs, sinks = ctx.meta
+        ysink, hsink = sinks if sinks is not None else (None, None)
+        dhat = _take(hsink, dhat)
         y_t, mu_t, sc_t, noise = ctx.saved_tensors
         y = Feat(y_t, Cy)
         mu, sc = Feat(mu_t, cs), Feat(sc_t, cs)
         dev = y_t.device
         npix = y.B * y.H * y.W
-        dy = Feat(torch.zeros_like(y_t), Cy)
+        # dL/dy of this slice's channels: written straight into y's gradient sink while it
+        # holds only other slices' disjoint channels (the ten slices' backward run before
+        # y's other consumer); else into a zero-filled tensor as before
+        direct = ysink is not None and (ysink.buf is None or (ysink.slices and ysink.own))
+        if direct and ysink.buf is None:
+            ysink.buf, ysink.own, ysink.slices = torch.zeros_like(y_t), True, True
+        dy = Feat(ysink.buf if direct else torch.zeros_like(y_t), Cy)
         dmu = Feat(torch.zeros_like(mu_t), cs)
         dsc = Feat(torch.zeros_like(sc_t), cs)
         gb = (dbits if dbits is not None else torch.zeros((), device=dev)).float().reshape(1)
@@ -1133,12 +1146,24 @@ class GaussFn(Function):
                   mu.ptr(), mu.ldc, sc.ptr(), sc.ldc, _lib.ptr(noise), gb.data_ptr(),
                   None if dh is None else dh.ptr(), 0 if dh is None else dh.ldc, dy.ptr(coff),
                   dy.ldc, dmu.ptr(), dmu.ldc, dsc.ptr(), dsc.ldc, _lib.stream_ptr(dev))
-        return dy.t, None, None, None, dmu.t, dsc.t, None
+        if direct:
+            return None, None, None, None, dmu.t, dsc.t, None, None
+        if ysink is not None:
+            _deposit(ysink, dy.t, True)
+            return None, None, None, None, dmu.t, dsc.t, None, None
+        return dy.t, None, None, None, dmu.t, dsc.t, None, None
 
 
 def gauss_t(y, coff, mu, sc, noise):
-    """GaussianConditional + ste_round of y[..., coff:coff+cs] -> (hat Feat, bits scalar)."""
-    hat, bits = GaussFn.apply(y.t, y.C, coff, mu.C, mu.t, sc.t, noise)
+    """GaussianConditional + ste_round of y[..., coff:coff+cs] -> (hat Feat, bits scalar).
+    A gradient-sink consumer of y (its slice gradient goes into y's buffer) and producer of
+    hat (whose consumers -- the lrp support concatenation, the lrp update's residual --
+    deposit into hat's buffer)."""
+    ysink = _sink(y.t)
+    hsink = Sink() if GRAD_SINKS else None
+    hat, bits = GaussFn.apply(y.t, y.C, coff, mu.C, mu.t, sc.t, noise, (ysink, hsink))
+    if hsink is not None:
+        hat._rgbac_sink = hsink
     return Feat(hat, mu.C), bits
 
 
