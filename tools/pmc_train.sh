@@ -1,7 +1,7 @@
 # HBM traffic per dispatch of the training step's kernels (config 3): separate FETCH_SIZE and
 # WRITE_SIZE passes over bench.py --train (its eager attribution step between GPU spins),
 # summarised by tools/pmc_traffic.py; "wgrad_kernel" aggregates every weight-gradient kernel
-# (ring and register-staged forms), matching bench.py's launch label.  GPU only.
+# (ring, register-staged, patch and halo forms; not the split reductions), matching bench.py's launch label.  GPU only.
 export TMPDIR=/tmp
 set -e
 for C in FETCH_SIZE WRITE_SIZE; do
@@ -16,7 +16,7 @@ import json
 p = "gpurun_out/pmc_traffic_train.json"
 d = json.load(open(p))
 k = d["kernels"]
-sel = [v for n, v in k.items() if n.startswith("wgrad_ring_kernel") or n.startswith("wgrad_kernel<")]
+sel = [v for n, v in k.items() if n.startswith("wgrad_") and "reduce" not in n]
 nf = sum(v["dispatches_fetch_pass"] for v in sel)
 nw = sum(v["dispatches_write_pass"] for v in sel)
 fb = sum(v["fetch_bytes_per_dispatch"] * v["dispatches_fetch_pass"] for v in sel) / max(nf, 1)
