@@ -124,6 +124,11 @@ __device__ __forceinline__ f32x2 gelu2_fast(f32x2 x) {
 }
 // v[r] = gelu_fast(v[r]) for a quad, as two packed pairs
 __device__ __forceinline__ void gelu4_fast(float (&v)[4]) {
+#ifdef RGBAC_GELU_SCALAR
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = gelu_fast(v[r]);
+  return;
+#endif
   const f32x2 a = gelu2_fast((f32x2){v[0], v[1]}), b = gelu2_fast((f32x2){v[2], v[3]});
   v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
 }
