@@ -314,7 +314,7 @@ _WG_TARGET_BIG = int(os.environ.get("RGBAC_WGRAD_TARGET_BIG", "256"))
 _WG_TARGET = int(os.environ.get("RGBAC_WGRAD_TARGET", "1024"))
 _WG_CEIL = os.environ.get("RGBAC_WGRAD_CEIL", "0") == "1"
 _HALO_WG = int(os.environ.get("RGBAC_WGRAD_HALO_WG", "512"))   # stride-1 halo kernel target
-_PATCH_PIX = int(os.environ.get("RGBAC_WGRAD_PATCH_PIX", "512"))  # min pixels per patch workgroup
+_PATCH_PIX = int(os.environ.get("RGBAC_WGRAD_PATCH_PIX", "256"))  # min pixels per patch workgroup
 
 
 WGRAD_PATCH = os.environ.get("RGBAC_WGRAD_PATCH", "1") != "0"
@@ -427,7 +427,8 @@ def wgrad(G, S, ksize, stride, pad, square, k_pad, fmap, numel, nbias=0, bias_fr
                             _SLAB_FLOATS // (n_pad * k_pad))))
     elif wgrad_patch_ok(G.t.dtype, G.ldc, S, ksize, stride, pad, square, G.H, G.W):
         # one workgroup per (32-channel block, run of 8 x 32-pixel patches): <= 512 in flight
-        # (two per CU), each at least 2 patches so the double-buffered staging overlaps
+        # (two per CU); small grids (32^2 latents) take one patch per workgroup -- more
+        # workgroups beat the double-buffered staging overlap there (RGBAC_WGRAD_PATCH_PIX A/B)
         tiles = S[0].ldc // 32
         ns = int(max(1, min(512 // tiles, M // _PATCH_PIX, _SLAB_FLOATS // (n_pad * k_pad))))
     else:
