@@ -1455,21 +1455,46 @@ __global__ void __launch_bounds__(256) conv3x3_c32_kernel(const ConvArgsDev args
   const int ty = t % ty_n;
   const int b = t / ty_n;
   const int y0 = ty * TS, x0 = tx * TS;
+  // every global load of the staging is issued before the first LDS store (fully unrolled
+  // register staging): one memory latency per workgroup, not one per loop iteration (the
+  // strided loops compiled to load / vmcnt(0) / ds_write chains)
+  constexpr int NWL = (32 * 36 + 255) / 256, NXL = (NH * 4 + 255) / 256;
   const T* wsrc = reinterpret_cast<const T*>(g.w);
-  for (int e = tid; e < 32 * 36; e += 256) {
-    const int r = e / 36, c = e - r * 36;
-    Ws[r * 36 + (c ^ ((r >> 1) & 3))] =
-        *reinterpret_cast<const uint4*>(wsrc + (size_t)r * g.k_pad + c * 8);
-  }
   const T* xsrc = reinterpret_cast<const T*>(g.sp0);
-  for (int e = tid; e < NH * 4; e += 256) {
+  uint4 wv[NWL], xv[NXL];
+  // (branch-free: a thread past the end takes the last slot's clamped index, loading and
+  // storing the same value as its owner -- no exec-masked block for the compiler to sink the
+  // loads into, which would split them into separately waited groups again)
+#pragma unroll
+  for (int u = 0; u < NWL; ++u) {
+    const int e = min(tid + 256 * u, 32 * 36 - 1);
+    const int r = e / 36, c = e - r * 36;
+    wv[u] = *reinterpret_cast<const uint4*>(wsrc + (size_t)r * g.k_pad + c * 8);
+  }
+  bool xin[NXL];
+#pragma unroll
+  for (int u = 0; u < NXL; ++u) {
+    const int e = min(tid + 256 * u, NH * 4 - 1);
     const int hr = e >> 2, c = e & 3;
     const int hy = hr / HS, hx = hr - hy * HS;
     const int iy = y0 + hy - 1, ix = x0 + hx - 1;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (iy >= 0 && iy < s.in_h && ix >= 0 && ix < s.in_w)
-      v = *reinterpret_cast<const uint4*>(xsrc + ((long long)(b * s.in_h + iy) * s.in_w + ix) * g.sld0 + c * 8);
-    if (s.square) v = square_chunk<T>(v);
+    xin[u] = iy >= 0 && iy < s.in_h && ix >= 0 && ix < s.in_w;
+    const int cy = min(max(iy, 0), s.in_h - 1), cx = min(max(ix, 0), s.in_w - 1);
+    xv[u] = *reinterpret_cast<const uint4*>(xsrc + ((long long)(b * s.in_h + cy) * s.in_w + cx) * g.sld0 + c * 8);
+  }
+#pragma unroll
+  for (int u = 0; u < NWL; ++u) {
+    const int e = min(tid + 256 * u, 32 * 36 - 1);
+    const int r = e / 36, c = e - r * 36;
+    Ws[r * 36 + (c ^ ((r >> 1) & 3))] = wv[u];
+  }
+  const bool sq = s.square;
+#pragma unroll
+  for (int u = 0; u < NXL; ++u) {
+    const int e = min(tid + 256 * u, NH * 4 - 1);
+    const int hr = e >> 2, c = e & 3;
+    uint4 v = xin[u] ? xv[u] : make_uint4(0, 0, 0, 0);
+    if (sq) v = square_chunk<T>(v);
     Xs[hr * 4 + (c ^ ((hr >> 1) & 3))] = v;
   }
   __syncthreads();

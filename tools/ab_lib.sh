@@ -1,16 +1,22 @@
-# Same-box A/B of two builds of the library: the default librgbac_hip.so (B) against
-# RGBAC_LIB_PATH=$BASE (A), config-2 bench lines interleaved (differences of ~1 % are below
-# the box-to-box spread, so only same-box pairs are compared).  Optional TESTK: a -k filter
-# of GPU tests run on B first.
+#!/bin/bash
+# A/B of two library builds on one box: the working tree's librgbac_hip.so against
+# rgbac/librgbac_hip_prev.so, interleaved; config 3 (with per-layer tables) and config 2.
+# Usage: TAG=x TESTS="tests/test_gpu_ops.py -k spatial" bash tools/ab_lib.sh
 export TMPDIR=/tmp
 set -e
 mkdir -p gpurun_out
-TAG=${TAG:-ab}
-BASE=${BASE:-deep-learning-based-rgba-image-compression-with-masked-window-based-attention_amd/rgbac/librgbac_base.so}
-if [ -n "$TESTK" ]; then
-  timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 100 --timeout-method thread -k "$TESTK" > gpurun_out/${TAG}_tests.log 2>&1
+P=deep-learning-based-rgba-image-compression-with-masked-window-based-attention_amd/rgbac/librgbac_hip_prev.so
+T=${TAG:-ab}
+if [ -n "$TESTS" ]; then
+  timeout -k 10 600 python -u -m pytest $TESTS -x -q --timeout 200 --timeout-method thread > gpurun_out/ab_${T}_tests.log 2>&1
 fi
-for i in 1 2 3; do
-  env $A_ENV RGBAC_LIB_PATH=$BASE timeout -k 10 200 python bench.py --no-dp-train --no-cpu-baseline --no-parity-mode > gpurun_out/${TAG}_A$i.json 2>> gpurun_out/${TAG}.err
-  timeout -k 10 200 python bench.py --no-dp-train --no-cpu-baseline --no-parity-mode > gpurun_out/${TAG}_B$i.json 2>> gpurun_out/${TAG}.err
+for i in 1 2; do
+  L1=""; L2=""
+  if [ $i = 2 ]; then L1="--layers gpurun_out/ab_${T}_c3_new_layers.txt"; L2="--layers gpurun_out/ab_${T}_c3_old_layers.txt"; fi
+  timeout -k 10 300 python -u bench.py --train --steps 10 --no-cpu-baseline $L1 > gpurun_out/ab_${T}_c3_new$i.json 2> gpurun_out/ab_${T}_c3_new$i.err
+  RGBAC_LIB_PATH=$P timeout -k 10 300 python -u bench.py --train --steps 10 --no-cpu-baseline $L2 > gpurun_out/ab_${T}_c3_old$i.json 2> gpurun_out/ab_${T}_c3_old$i.err
+done
+for i in 1 2; do
+  timeout -k 10 300 python -u bench.py --steps 20 --no-cpu-baseline --no-dp-train > gpurun_out/ab_${T}_c2_new$i.json 2> gpurun_out/ab_${T}_c2_new$i.err
+  RGBAC_LIB_PATH=$P timeout -k 10 300 python -u bench.py --steps 20 --no-cpu-baseline --no-dp-train > gpurun_out/ab_${T}_c2_old$i.json 2> gpurun_out/ab_${T}_c2_old$i.err
 done
