@@ -1440,7 +1440,7 @@ __global__ void __launch_bounds__(256) conv_direct_kernel(const ConvArgsDev args
 // Both LDS images use slot = chunk ^ ((row >> 1) & 3), conflict-free for the
 // ds_read_b128 lane groups of the fragment reads.  bf16 only.
 template <typename T>
-__global__ void __launch_bounds__(256) conv3x3_c32_kernel(const ConvArgsDev args) {
+__global__ void __launch_bounds__(256, 4) conv3x3_c32_kernel(const ConvArgsDev args) {
   constexpr int TS = 16, HS = TS + 2, NH = HS * HS;
   __shared__ __attribute__((aligned(16))) uint4 Xs[NH * 4];
   __shared__ __attribute__((aligned(16))) uint4 Ws[32 * 36];
@@ -1520,15 +1520,36 @@ __global__ void __launch_bounds__(256) conv3x3_c32_kernel(const ConvArgsDev args
       for (int j = 0; j < 2; ++j) mma_step<T>(acc[j][i], A[j], B);
     }
   }
+  // stride-1 CONV: output pixel = m.  The residual / bias operands of two rows' quads are
+  // requested before their stores (the output may alias a residual -- the training path's
+  // in-place gradient accumulation -- and a load issued behind a store waits for it)
+  float bias[2][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int m = (b * s.Hm + y0 + wave * 4 + i) * s.Wm + x0 + fr;
+  for (int j = 0; j < 2; ++j) {
+    const int n = 16 * j + fq * 4;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = 16 * j + fq * 4;
-      if (n >= g.cout) continue;
-      float v[4] = {acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]};
-      epilogue4<T>(s, g, 0, m, n, v);
+    for (int r = 0; r < 4; ++r) bias[j][r] = (g.bias && n < g.cout) ? g.bias[n + r] : 0.0f;
+  }
+#pragma unroll
+  for (int i0 = 0; i0 < 4; i0 += 2) {
+    EpiIn in[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = (b * s.Hm + y0 + wave * 4 + i0 + i) * s.Wm + x0 + fr;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        if (16 * j + fq * 4 < g.cout) in[i][j].template load<T>(g, s.act, (long long)m, 16 * j + fq * 4);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = (b * s.Hm + y0 + wave * 4 + i0 + i) * s.Wm + x0 + fr;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = 16 * j + fq * 4;
+        if (n >= g.cout) continue;
+        float v[4] = {acc[j][i0 + i][0], acc[j][i0 + i][1], acc[j][i0 + i][2], acc[j][i0 + i][3]};
+        epilogue4_fin<T>(s, g, (long long)m, n, v, bias[j], in[i][j]);
+      }
     }
   }
 }
