@@ -470,7 +470,7 @@ def dp_train_record(args, world, rank, dev, dist):
     from rgbac.layers.SupplyMask import mask_pyramid
     from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
     from rgbac.optim import AdamClamp
-    from rgbac.parallel import DataParallelTrainer
+    from rgbac.parallel import CommWatchdog, DataParallelTrainer, RcclComm
     from rgbac import runtime as rt
     own_group = False
     if not tdist.is_initialized():
@@ -503,6 +503,11 @@ def dp_train_record(args, world, rank, dev, dist):
     nb = len(trainer.buckets.buckets)
     launched = trainer.buckets.launched_in_backward()
     trainer_rccl = trainer.buckets.comm is not None
+    # failure detection: a dead peer leaves every survivor blocked in a replay; the watchdog
+    # aborts the communicator and exits non-zero once an armed stretch overruns its deadline
+    wd = CommWatchdog(trainer.buckets.comm, timeout_s=240.0).start() if trainer_rccl else None
+    if wd is not None:
+        wd.arm()
     graph_err = None
     try:
         run, graph, gout = capture_train(step, opt, dev, args.no_graph)
@@ -557,10 +562,15 @@ def dp_train_record(args, world, rank, dev, dist):
     exposed, ar_ms = t.tolist()
     exposed = None if exposed < 0 else exposed
     n_ranks = tdist.get_world_size()
+    rccl_ranks = trainer.buckets.comm.count() if trainer_rccl else None
+    if wd is not None:
+        wd.disarm()
+        wd.stop()
     grad_bytes = flat.numel() * flat.element_size()
     trainer.buckets.remove()
     del run, graph, gout, net, opt, trainer
     if own_group:
+        RcclComm.close_all()
         tdist.destroy_process_group()
     if rank != 0:
         return None
@@ -569,7 +579,7 @@ def dp_train_record(args, world, rank, dev, dist):
             "same code path at every world size: bucketed RCCL all-reduce launched from "
             "post-accumulate-grad hooks during backward, step captured in a HIP graph",
             "value": round(n_ranks * B * S * S * args.dp_steps / elapsed / 1e6, 3), "unit": "MPix/s",
-            "n_ranks": n_ranks, "global_batch": B * n_ranks, "steps": args.dp_steps,
+            "n_ranks": n_ranks, "rccl_ranks": rccl_ranks, "global_batch": B * n_ranks, "steps": args.dp_steps,
             "warmup": args.dp_warmup, "ms_per_step": round(elapsed / args.dp_steps * 1e3, 3),
             "backend": "RCCL (direct ncclAllReduce on a comm stream, csrc/comm.cpp)"
             if trainer_rccl else "torch.distributed", "hip_graph": graph_err is None and not args.no_graph,

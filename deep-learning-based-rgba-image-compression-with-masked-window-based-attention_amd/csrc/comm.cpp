@@ -30,6 +30,9 @@ struct Rccl {
   decltype(&ncclAllReduce) all_reduce = nullptr;
   decltype(&ncclCommDestroy) comm_destroy = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
+  decltype(&ncclCommCount) comm_count = nullptr;
+  decltype(&ncclCommGetAsyncError) async_error = nullptr;
+  decltype(&ncclCommAbort) comm_abort = nullptr;
 };
 
 Rccl g_rccl;
@@ -58,8 +61,11 @@ extern "C" int rgbac_comm_load(const char* librccl_path) {
   r.all_reduce = reinterpret_cast<decltype(r.all_reduce)>(dlsym(h, "ncclAllReduce"));
   r.comm_destroy = reinterpret_cast<decltype(r.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
   r.error_string = reinterpret_cast<decltype(r.error_string)>(dlsym(h, "ncclGetErrorString"));
+  r.comm_count = reinterpret_cast<decltype(r.comm_count)>(dlsym(h, "ncclCommCount"));
+  r.async_error = reinterpret_cast<decltype(r.async_error)>(dlsym(h, "ncclCommGetAsyncError"));
+  r.comm_abort = reinterpret_cast<decltype(r.comm_abort)>(dlsym(h, "ncclCommAbort"));
   if (!r.get_unique_id || !r.comm_init_rank || !r.all_reduce || !r.comm_destroy ||
-      !r.error_string) {
+      !r.error_string || !r.comm_count || !r.async_error || !r.comm_abort) {
     dlclose(h);
     rgbac::set_error("rgbac_comm_load: the library lacks an NCCL entry point");
     return RGBAC_E_ARG;
@@ -114,5 +120,39 @@ extern "C" int rgbac_comm_destroy(void* comm) {
   if (!comm) return RGBAC_OK;
   const ncclResult_t r = g_rccl.comm_destroy(reinterpret_cast<ncclComm_t>(comm));
   if (r != ncclSuccess) return nccl_fail("ncclCommDestroy", r);
+  return RGBAC_OK;
+}
+
+// Ranks the communicator itself spans (ncclCommCount): what a multi-GPU bench line reports as
+// the world RCCL saw, independent of torch.distributed's view.
+extern "C" int rgbac_comm_count(void* comm, int* count) {
+  RGBAC_REQUIRE(g_rccl.handle && comm, "no communicator");
+  RGBAC_REQUIRE(count != nullptr, "null count");
+  const ncclResult_t r = g_rccl.comm_count(reinterpret_cast<ncclComm_t>(comm), count);
+  if (r != ncclSuccess) return nccl_fail("ncclCommCount", r);
+  return RGBAC_OK;
+}
+
+// Asynchronous error state of the communicator (ncclCommGetAsyncError): *err = 0 while healthy,
+// else the ncclResult_t code (a peer died, a network / xGMI failure).  Polled from a host thread
+// between steps (rgbac.parallel.CommWatchdog); a collective that can never complete otherwise
+// blocks its stream -- and every rank's graph replay -- forever.
+extern "C" int rgbac_comm_async_error(void* comm, int* err) {
+  RGBAC_REQUIRE(g_rccl.handle && comm, "no communicator");
+  RGBAC_REQUIRE(err != nullptr, "null error out");
+  ncclResult_t a = ncclSuccess;
+  const ncclResult_t r = g_rccl.async_error(reinterpret_cast<ncclComm_t>(comm), &a);
+  if (r != ncclSuccess) return nccl_fail("ncclCommGetAsyncError", r);
+  *err = (int)a;
+  return RGBAC_OK;
+}
+
+// Abort the communicator (ncclCommAbort): kernels of pending collectives are released and the
+// handle is freed.  The host then exits the process non-zero; nothing here restarts anything.
+extern "C" int rgbac_comm_abort(void* comm) {
+  RGBAC_REQUIRE(g_rccl.handle, "rgbac_comm_load first");
+  if (!comm) return RGBAC_OK;
+  const ncclResult_t r = g_rccl.comm_abort(reinterpret_cast<ncclComm_t>(comm));
+  if (r != ncclSuccess) return nccl_fail("ncclCommAbort", r);
   return RGBAC_OK;
 }

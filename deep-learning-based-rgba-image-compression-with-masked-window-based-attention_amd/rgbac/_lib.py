@@ -171,6 +171,9 @@ SIGNATURES = {
     "rgbac_comm_init": [_VP, _I32, _I32, _I32, ctypes.POINTER(ctypes.c_void_p)],
     "rgbac_comm_allreduce_sum": [_VP, _I32, _VP, _I64, _VP],
     "rgbac_comm_destroy": [_VP],
+    "rgbac_comm_count": [_VP, ctypes.POINTER(ctypes.c_int)],
+    "rgbac_comm_async_error": [_VP, ctypes.POINTER(ctypes.c_int)],
+    "rgbac_comm_abort": [_VP],
     "rgbac_rans_encoder_bound": [_VP],
     "rgbac_rans_encoder_flush": [_VP, _VP, _I64, ctypes.POINTER(ctypes.c_int64)],
     "rgbac_rans_decoder_init": [ctypes.POINTER(RansDecoderState), _VP, _I64],

@@ -30,8 +30,12 @@ parameters that never notify sit in a tail bucket reduced in ``finish()``.
 Steps from then on issue the same collectives in the same order on every rank,
 so a step can be captured in a HIP graph (RCCL collectives are stream-ordered).
 """
+import atexit
 import ctypes
 import os
+import sys
+import threading
+import time
 
 import torch
 import torch.distributed as dist
@@ -47,17 +51,31 @@ class RcclComm:
     Every step is stream-ordered, so a bucket all-reduce issued from a backward hook overlaps
     the rest of backward, and the whole step captures into a HIP graph -- no ProcessGroup
     work object or watchdog thread is involved.  torch.distributed only bootstraps it: rank
-    0's 128-byte unique id is broadcast over ``group`` once."""
+    0's 128-byte unique id is broadcast over ``group`` once.
+
+    Communicators are cached per (group, device); the cache holds the group object itself, so
+    a destroyed-and-recreated group can never be matched to a stale communicator by a recycled
+    ``id``.  ``close()`` destroys one (``abort()`` aborts it), and every live one is destroyed
+    at interpreter exit."""
 
     _cache = {}
 
     @classmethod
     def get(cls, device, group=None):
-        key = (id(group), device.index, dist.get_world_size(group), dist.get_rank(group))
-        c = cls._cache.get(key)
-        if c is None:
-            c = cls._cache[key] = cls(device, group)
+        gk = group if group is not None else dist.group.WORLD
+        key = (id(gk), device.index, dist.get_world_size(group), dist.get_rank(group))
+        ent = cls._cache.get(key)
+        if ent is not None and ent[0] is gk and ent[1].comm is not None:
+            return ent[1]
+        c = cls(device, group)
+        cls._cache[key] = (gk, c)
         return c
+
+    @classmethod
+    def close_all(cls):
+        for _, c in list(cls._cache.values()):
+            c.close()
+        cls._cache.clear()
 
     def __init__(self, device, group=None):
         lib = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
@@ -89,6 +107,114 @@ class RcclComm:
 
     def wait(self, ev):
         torch.cuda.current_stream(self.device).wait_event(ev)
+
+    def count(self):
+        """Ranks the communicator itself spans (ncclCommCount)."""
+        n = ctypes.c_int(0)
+        _lib.call("rgbac_comm_count", self.comm, ctypes.byref(n))
+        return n.value
+
+    def async_error(self):
+        """0 while healthy, else RCCL's asynchronous error code (ncclCommGetAsyncError)."""
+        e = ctypes.c_int(0)
+        _lib.call("rgbac_comm_async_error", self.comm, ctypes.byref(e))
+        return e.value
+
+    def abort(self):
+        if self.comm is not None and self.comm.value:
+            _lib.call("rgbac_comm_abort", self.comm)
+        self.comm = None
+
+    def close(self):
+        if self.comm is not None and self.comm.value:
+            _lib.call("rgbac_comm_destroy", self.comm)
+        self.comm = None
+
+
+atexit.register(RcclComm.close_all)
+
+
+class CommWatchdog:
+    """Failure detection for the direct-RCCL step.  A collective whose peer died never
+    completes: the surviving ranks would block inside a graph replay forever (there is no
+    ProcessGroup watchdog on this path).  A host thread polls ``comm.async_error()`` every
+    ``poll_s`` and, while a step is armed, its completion event; on an asynchronous error, or
+    when an armed step has not completed ``timeout_s`` after ``arm()``, it aborts the
+    communicator and ends the process with ``exit_code`` (``os._exit``: no Python teardown
+    that could itself block on the GPU).  It never restarts or re-executes anything.
+
+    ``comm`` needs ``async_error()`` and ``abort()``; ``exit_fn`` and ``clock`` are
+    injectable (tests run it against a stub communicator on the CPU)."""
+
+    def __init__(self, comm, timeout_s=300.0, poll_s=0.5, exit_code=3, exit_fn=None,
+                 clock=None, log=None):
+        self.comm, self.timeout_s, self.poll_s, self.exit_code = comm, timeout_s, poll_s, exit_code
+        self.exit_fn = exit_fn if exit_fn is not None else os._exit
+        self.clock = clock if clock is not None else time.monotonic
+        self.log = log if log is not None else (lambda m: print(m, file=sys.stderr, flush=True))
+        self._lock = threading.Lock()
+        self._deadline = None
+        self._done = None                  # callable -> True once the armed step completed
+        self.fired = None                  # reason string once it fired
+        self._stop = threading.Event()
+        self._thread = None
+
+    def start(self):
+        if self._thread is None:
+            self._thread = threading.Thread(target=self._run, name="rgbac-comm-watchdog",
+                                            daemon=True)
+            self._thread.start()
+        return self
+
+    def stop(self):
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+
+    def arm(self, done=None):
+        """A step was enqueued; ``done()`` (e.g. a recorded event's ``query``) says when it has
+        completed.  ``done=None``: the caller disarms explicitly."""
+        with self._lock:
+            self._deadline = self.clock() + self.timeout_s
+            self._done = done
+
+    def disarm(self):
+        with self._lock:
+            self._deadline = None
+            self._done = None
+
+    def check(self):
+        """One poll (the thread's body; callable directly).  Returns the reason it fired, or
+        None."""
+        if self.fired is not None:
+            return self.fired
+        reason = None
+        err = self.comm.async_error()
+        if err:
+            reason = f"RCCL asynchronous error {err}"
+        else:
+            with self._lock:
+                dl, done = self._deadline, self._done
+            if dl is not None:
+                if done is not None and done():
+                    self.disarm()
+                elif self.clock() > dl:
+                    reason = f"step not complete {self.timeout_s:.1f} s after it was enqueued"
+        if reason is not None:
+            self.fired = reason
+            self.log(f"rgbac.parallel: {reason}; aborting the communicator and exiting "
+                     f"with status {self.exit_code}")
+            try:
+                self.comm.abort()
+            finally:
+                self.exit_fn(self.exit_code)
+        return reason
+
+    def _run(self):
+        while not self._stop.wait(self.poll_s):
+            if self.check() is not None:
+                return
 
 
 class GradBuckets:
@@ -222,6 +348,18 @@ class GradBuckets:
         everything in the learning step), wait for every bucket (stream-ordered: the
         current stream waits for RCCL's); returns 1/world."""
         self.active = False
+        if self.learned:
+            # every rank must issue the same collectives in the same order: a non-tail bucket
+            # that did not complete its learned count during backward would be launched here,
+            # after buckets another rank may already have sent -- mismatched RCCL calls (a
+            # silent hang or a sum over different ranges).  Refuse before launching anything.
+            short = [b for b in range(len(self.buckets))
+                     if b != self.tail and (self.works[b] is None or self.pending[b] != 0)]
+            if short or self.count != self.expect:
+                raise RuntimeError(
+                    "rgbac.parallel: gradient notifications differ from the learning step "
+                    f"(buckets {short} incomplete at the end of backward): the autograd graph "
+                    "changed between steps")
         for b in range(len(self.buckets)):
             if self.works[b] is None:
                 self._launch(b)
@@ -261,13 +399,24 @@ class DataParallelTrainer:
                  rccl=None):
         self.net, self.opt = net, optimizer
         self.buckets = None
+        self.comm = None
         self.comm_events = None
+        self.watchdog = None
         if dist.is_available() and dist.is_initialized() and \
                 (force_buckets or dist.get_world_size(group) > 1):
             flat = optimizer.flat_grad
             if rccl is None:               # RCCL directly whenever the group is RCCL's
                 rccl = flat.is_cuda and dist.get_backend(group) == "nccl"
-            comm = RcclComm.get(flat.device, group) if rccl else None
+            comm = None
+            if rccl:
+                try:
+                    comm = RcclComm.get(flat.device, group)
+                except (RuntimeError, OSError) as e:
+                    # no usable librccl.so (or its init failed): torch.distributed's own
+                    # all_reduce over the same group, bucketed the same way
+                    print(f"rgbac.parallel: direct RCCL unavailable ({e}); using "
+                          "torch.distributed.all_reduce", file=sys.stderr, flush=True)
+            self.comm = comm
             self.buckets = GradBuckets(optimizer.params, flat, bucket_bytes, group=group,
                                        comm=comm)
 

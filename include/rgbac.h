@@ -579,6 +579,14 @@ int rgbac_comm_unique_id(void* id_out);
 int rgbac_comm_init(const void* id, int world, int rank, int device, void** comm);
 int rgbac_comm_allreduce_sum(void* comm, int dtype, void* buf, int64_t count, void* stream);
 int rgbac_comm_destroy(void* comm);
+/* Health and size of a communicator: rgbac_comm_count -> ranks RCCL itself spans
+ * (ncclCommCount); rgbac_comm_async_error -> *err = 0 healthy, else the ncclResult_t of an
+ * asynchronous failure (ncclCommGetAsyncError); rgbac_comm_abort releases pending collectives
+ * and frees the handle (ncclCommAbort) -- the host then exits non-zero
+ * (rgbac.parallel.CommWatchdog), it never restarts a process that touched the GPU. */
+int rgbac_comm_count(void* comm, int* count);
+int rgbac_comm_async_error(void* comm, int* err);
+int rgbac_comm_abort(void* comm);
 
 /* Host-side range-ANS coder (csrc/rans.cpp), byte-compatible with compressai.ans:
  * replaces BufferedRansEncoder.encode_with_indexes/flush (:334,:367-368), RansDecoder
