@@ -40,6 +40,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "conv_common.h"
 
 namespace rgbac {
 
@@ -58,529 +59,6 @@ __device__ unsigned long long g_wg_t[16384][4];
 #else
 #define WG_T(k) do {} while (0)
 #endif
-
-constexpr int kMaxGroups = 10;
-
-struct ConvGroup {                  // per-group operands
-  const void* sp0; const void* sp1; const void* sp2;
-  long long sld0, sld1, sld2;
-  const void* w;
-  const float* bias;
-  void* out;
-  const void* res0; const void* res1; const void* res2;
-  long long ld0, ld1, ld2, out_ldc;
-  const uint8_t* sel;
-  float* ws;                        // split-K slabs [ksplit][nphase][M][cout16]
-  const float* aux0;                // GAUSS: noise [M][cout/2] or NULL
-  float* aux1;                      // GAUSS: likelihood out [M][cout/2] or NULL
-  double* partial;                  // GAUSS: bits per M-tile block
-  void* zout;                       // training: pre-activation store (or NULL)
-  long long zld;
-  int* cnt;                         // split-K tickets (in-launch reduction) or NULL
-  int send0, send1, send2;          // cumulative channel ends
-  int cin_pad, k_pad, cout, rows, cout16, out_coff;
-};
-
-struct ConvShared {
-  double rWm, rHm;                  // 1/Wm, 1/Hm for divide-free pixel decode
-  int mode, batch, in_h, in_w, Hm, Wm, out_h, out_w, M, sy;
-  int ksize, pad;
-  int act; float act_param; int square;
-  int ksplit, nphase, ngroups;
-  int remap;                        // 1: XCD-aware block order (env RGBAC_XCD_REMAP=0 disables)
-};
-
-struct ConvArgsDev {
-  ConvShared s;
-  ConvGroup g[kMaxGroups];
-};
-
-__device__ uint4 g_zero_page[64];
-   // zero source for padding taps (static, never written)
-
-// n / d for 0 <= n < 2^31 via a double reciprocal and one correction step
-// (|n*rd - n/d| < 2^-21, so the truncated quotient is off by at most one).
-__device__ __forceinline__ int udiv(int n, int d, double rd) {
-  int q = (int)((double)n * rd);
-  const int r = n - q * d;
-  if (r < 0) --q;
-  else if (r >= d) ++q;
-  return q;
-}
-
-__device__ __forceinline__ float gelu_f(float v) {
-  return 0.5f * v * (1.0f + erff(v * 0.70710678118654752440f));
-}
-// exact erf GELU for fp32 (parity mode), the branch-free form for bf16 outputs
-template <typename T> __device__ __forceinline__ float gelu_t(float v);
-template <> __device__ __forceinline__ float gelu_t<float>(float v) { return gelu_f(v); }
-template <> __device__ __forceinline__ float gelu_t<bf16_t>(float v) { return gelu_fast(v); }
-__device__ __forceinline__ float sigmoid_f(float v) { return 1.0f / (1.0f + expf(-v)); }
-// GDN / IGDN output x / sqrt(n), x * sqrt(n): IEEE sqrt + divide in the fp32 parity mode,
-// the hardware rsq / sqrt (~1 ulp fp32) where the result is stored as bf16
-template <typename T> __device__ __forceinline__ float gdn_t(float x, float n);
-template <> __device__ __forceinline__ float gdn_t<float>(float x, float n) { return x / sqrtf(n); }
-template <> __device__ __forceinline__ float gdn_t<bf16_t>(float x, float n) {
-  return x * __builtin_amdgcn_rsqf(n);
-}
-template <typename T> __device__ __forceinline__ float igdn_t(float x, float n);
-template <> __device__ __forceinline__ float igdn_t<float>(float x, float n) { return x * sqrtf(n); }
-template <> __device__ __forceinline__ float igdn_t<bf16_t>(float x, float n) {
-  return x * __builtin_amdgcn_sqrtf(n);
-}
-__device__ __forceinline__ float std_cum_f(float t) {
-  return 0.5f * erfcf(-0.70710678118654752440f * t);
-}
-
-template <typename T>
-__device__ __forceinline__ uint4 square_chunk(uint4 v);
-template <>
-__device__ __forceinline__ uint4 square_chunk<float>(uint4 v) {
-  float a = __uint_as_float(v.x), b = __uint_as_float(v.y);
-  float c = __uint_as_float(v.z), d = __uint_as_float(v.w);
-  return make_uint4(__float_as_uint(a * a), __float_as_uint(b * b),
-                    __float_as_uint(c * c), __float_as_uint(d * d));
-}
-__device__ __forceinline__ uint32_t sq_pair(uint32_t w) {
-  float lo = bf2f(w & 0xFFFF), hi = bf2f(w >> 16);
-  return (uint32_t)f2bf(lo * lo) | ((uint32_t)f2bf(hi * hi) << 16);
-}
-template <>
-__device__ __forceinline__ uint4 square_chunk<bf16_t>(uint4 v) {
-  return make_uint4(sq_pair(v.x), sq_pair(v.y), sq_pair(v.z), sq_pair(v.w));
-}
-
-template <typename T>
-__device__ __forceinline__ void load_res(const void* ptr, long long ld, long long opix, int n,
-                                         int cout, float (&v)[4]) {
-  const T* r = reinterpret_cast<const T*>(ptr) + opix * ld + n;
-  if (n + 3 < cout) {
-    Elem<T>::ld4(r, v);
-  } else {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = (n + q < cout) ? Elem<T>::ld(r + q) : 0.0f;
-  }
-}
-
-// Input gradient through the producer's activation (ACT_DGELU / ACT_DLRELU, res0 = the
-// producer's pre-activation z): acc * act'(z), the activation backward folded into the
-// consumer's input-gradient conv (rgbac.autograd deferred activations).  Same arithmetic as
-// train.hip's act_bwd on dy = acc: the fast derivative for bf16, the exact one for f32.
-template <typename T>
-__device__ __forceinline__ float dact_apply(int act, float p, float acc, float z) {
-  if (act == RGBAC_ACT_DGELU)
-    return acc * (sizeof(T) == 4 ? gelu_grad_exact(z) : gelu_grad_fast(z));
-  return z > 0.0f ? acc : acc * p;
-}
-__host__ __device__ __forceinline__ bool is_dact(int act) {
-  return act == RGBAC_ACT_DGELU || act == RGBAC_ACT_DLRELU;
-}
-
-template <typename T, bool DACT = true>
-__device__ __forceinline__ void epilogue4_body(const ConvShared& s, const ConvGroup& g,
-                                               long long opix, int n, float (&v)[4]);
-
-// Bias + fused epilogue + store of channels n..n+3 of M-grid pixel m (phase ph).
-template <typename T, bool DACT = true>
-__device__ __forceinline__ void epilogue4(const ConvShared& s, const ConvGroup& g, int ph, int m,
-                                          int n, float (&v)[4]) {
-  const int t = udiv(m, s.Wm, s.rWm);
-  const int mx = m - t * s.Wm;
-  const int b = udiv(t, s.Hm, s.rHm);
-  const int my = t - b * s.Hm;
-  T* out = reinterpret_cast<T*>(g.out);
-  if (s.mode == RGBAC_SUBPEL2) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] += (g.bias ? g.bias[n + r] : 0.0f);
-    // conv channel n+r = 4*cc + 2*ii + jj -> pixel (2my+ii, 2mx+jj), channel cc
-    const int cc = n >> 2;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float x = v[r];
-      const int oy = 2 * my + (r >> 1), ox = 2 * mx + (r & 1);
-      const long long op = (long long)(b * s.out_h + oy) * s.out_w + ox;
-      if (g.zout) Elem<T>::st(reinterpret_cast<T*>(g.zout) + op * g.zld + g.out_coff + cc, x);
-      if (s.act == RGBAC_ACT_GELU) x = gelu_t<T>(x);
-      Elem<T>::st(out + op * g.out_ldc + g.out_coff + cc, x);
-    }
-    return;
-  }
-  long long opix;
-  if (s.mode == RGBAC_CONVT_S2)
-    opix = (long long)(b * s.out_h + 2 * my + (ph >> 1)) * s.out_w + 2 * mx + (ph & 1);
-  else
-    opix = (long long)(b * s.out_h + my) * s.out_w + mx;
-  epilogue4_body<T, DACT>(s, g, opix, n, v);
-}
-
-// Same for a stride-1 CONV whose output grid is the M grid (output pixel = m).
-template <typename T>
-__device__ __forceinline__ void epilogue4_at(const ConvShared& s, const ConvGroup& g, int m, int n,
-                                             float (&v)[4]) {
-  epilogue4_body<T>(s, g, (long long)m, n, v);
-}
-
-// Operands the epilogue reads from memory, loaded ahead of the math so several quads'
-// loads can be in flight together (EpiIn::load, then epilogue4_fin).
-struct EpiIn {
-  float r0[4], r1[4], r2[4];
-  bool on;
-  template <typename T>
-  __device__ __forceinline__ void load(const ConvGroup& g, int act, long long opix, int n) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) { r0[r] = 0.f; r1[r] = 0.f; r2[r] = 0.f; }
-    if (g.res0) load_res<T>(g.res0, g.ld0, opix, n, g.cout, r0);
-    if (g.res1) load_res<T>(g.res1, g.ld1, opix, n, g.cout, r1);
-    if (g.res2) load_res<T>(g.res2, g.ld2, opix, n, g.cout, r2);
-    on = act == RGBAC_ACT_MASKSEL ? g.sel[opix] != 0 : true;
-  }
-};
-
-// DACT = false: an instantiation without the folded activation backward (ACT_DGELU /
-// ACT_DLRELU), for kernels at their register limit that run it in a separate instance
-template <typename T, bool DACT = true>
-__device__ __forceinline__ void epilogue4_fin(const ConvShared& s, const ConvGroup& g,
-                                              long long opix, int n, float (&v)[4],
-                                              const float (&bias)[4], const EpiIn& in);
-
-template <typename T, bool DACT>
-__device__ __forceinline__ void epilogue4_body(const ConvShared& s, const ConvGroup& g,
-                                               long long opix, int n, float (&v)[4]) {
-  EpiIn in;
-  in.template load<T>(g, s.act, opix, n);
-  float bias[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) bias[r] = g.bias ? g.bias[n + r] : 0.0f;
-  epilogue4_fin<T, DACT>(s, g, opix, n, v, bias, in);
-}
-
-template <typename T, bool DACT>
-__device__ __forceinline__ void epilogue4_fin(const ConvShared& s, const ConvGroup& g,
-                                              long long opix, int n, float (&v)[4],
-                                              const float (&bias)[4], const EpiIn& in) {
-#pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] += bias[r];
-  T* out = reinterpret_cast<T*>(g.out);
-  const float (&r0)[4] = in.r0;
-  const float (&r1)[4] = in.r1;
-  if (DACT && is_dact(s.act)) {              // uniform branch: keeps the derivative out of the
-#pragma unroll                        // other epilogues (no if-converted select per element)
-    for (int r = 0; r < 4; ++r) v[r] = dact_apply<T>(s.act, s.act_param, v[r], r0[r]);
-  } else {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      v[r] = s.act == RGBAC_ACT_SQBWD ? r0[r] + 2.0f * r1[r] * v[r] : v[r] + r0[r];
-  }
-  if (g.zout) {
-    T* z = reinterpret_cast<T*>(g.zout) + opix * g.zld + g.out_coff + n;
-    if (n + 3 < g.cout) {
-      Elem<T>::st4(z, v);
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (n + r < g.cout) Elem<T>::st(z + r, v[r]);
-    }
-  }
-  switch (s.act) {
-    case RGBAC_ACT_GELU:
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = gelu_t<T>(v[r]);
-      break;
-    case RGBAC_ACT_RELU:
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
-      break;
-    case RGBAC_ACT_LRELU:
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : v[r] * s.act_param;
-      break;
-    case RGBAC_ACT_TANH_HALF:
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = r1[r] + 0.5f * tanhf(v[r]);
-      break;
-    case RGBAC_ACT_GATE:
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = r1[r] * sigmoid_f(v[r]);
-      break;
-    case RGBAC_ACT_GDN:
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = gdn_t<T>(r1[r], v[r]);
-      break;
-    case RGBAC_ACT_IGDN:
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = igdn_t<T>(r1[r], v[r]);
-      break;
-    case RGBAC_ACT_MASKSEL: {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = in.on ? r1[r] + v[r] : r1[r];
-      break;
-    }
-    default:
-      break;
-  }
-  if (g.res2) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] += in.r2[r];
-  }
-  const long long base = opix * g.out_ldc + g.out_coff + n;
-  if (n + 3 < g.cout) {
-    Elem<T>::st4(out + base, v);
-  } else {
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (n + r < g.cout) Elem<T>::st(out + base + r, v[r]);
-  }
-}
-
-// conv_kernel epilogue of accumulator row i (pixel m, channels nn[j]..+3 for j < TN):
-// every residual load of the row is issued before any math/store.
-template <typename T, int TN, int TM, bool DACT = true>
-__device__ __forceinline__ void epilogue_tile_row(const ConvShared& s, const ConvGroup& g, int ph,
-                                                  int m, const int (&nn)[TN],
-                                                  const f32x4 (&acc)[TN][TM], int i) {
-  if (s.mode == RGBAC_SUBPEL2) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      if (nn[j] >= g.cout) continue;
-      float v[4] = {acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]};
-      epilogue4<T, DACT>(s, g, ph, m, nn[j], v);
-    }
-    return;
-  }
-  const int t = udiv(m, s.Wm, s.rWm);
-  const int mx = m - t * s.Wm;
-  const int b = udiv(t, s.Hm, s.rHm);
-  const int my = t - b * s.Hm;
-  long long opix;
-  if (s.mode == RGBAC_CONVT_S2)
-    opix = (long long)(b * s.out_h + 2 * my + (ph >> 1)) * s.out_w + 2 * mx + (ph & 1);
-  else
-    opix = (long long)(b * s.out_h + my) * s.out_w + mx;
-  EpiIn in[TN];
-  float bias[TN][4];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    if (nn[j] < g.cout) in[j].template load<T>(g, s.act, opix, nn[j]);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bias[j][r] = (g.bias && nn[j] < g.cout) ? g.bias[nn[j] + r] : 0.0f;
-  }
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    if (nn[j] >= g.cout) continue;
-    float v[4] = {acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]};
-    epilogue4_fin<T, DACT>(s, g, opix, nn[j], v, bias[j], in[j]);
-  }
-}
-
-// Epilogue of one pixel row held by a lane: channels nn[j]..nn[j]+3 for j < TN.
-// The pixel index is decoded once and every residual load of the row is issued
-// before any store (stores could alias later loads in program order otherwise,
-// which serialises one memory latency per 16x16 tile).
-template <typename T, int TN>
-__device__ __forceinline__ void epilogue_row(const ConvShared& s, const ConvGroup& g, int ph, int m,
-                                             const int (&nn)[TN], float (&v)[TN][4]) {
-  const int t = udiv(m, s.Wm, s.rWm);
-  const int mx = m - t * s.Wm;
-  const int b = udiv(t, s.Hm, s.rHm);
-  const int my = t - b * s.Hm;
-#pragma unroll
-  for (int j = 0; j < TN; ++j)
-    if (nn[j] < g.cout)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[j][r] += (g.bias ? g.bias[nn[j] + r] : 0.0f);
-  T* out = reinterpret_cast<T*>(g.out);
-  if (s.mode == RGBAC_SUBPEL2) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      if (nn[j] >= g.cout) continue;
-      const int cc = nn[j] >> 2;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float x = v[j][r];
-        const int oy = 2 * my + (r >> 1), ox = 2 * mx + (r & 1);
-        const long long op = (long long)(b * s.out_h + oy) * s.out_w + ox;
-        if (g.zout) Elem<T>::st(reinterpret_cast<T*>(g.zout) + op * g.zld + g.out_coff + cc, x);
-        if (s.act == RGBAC_ACT_GELU) x = gelu_t<T>(x);
-        Elem<T>::st(out + op * g.out_ldc + g.out_coff + cc, x);
-      }
-    }
-    return;
-  }
-  long long opix;
-  if (s.mode == RGBAC_CONVT_S2)
-    opix = (long long)(b * s.out_h + 2 * my + (ph >> 1)) * s.out_w + 2 * mx + (ph & 1);
-  else
-    opix = (long long)(b * s.out_h + my) * s.out_w + mx;
-  float r0[TN][4], r1[TN][4], r2[TN][4];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) r0[j][r] = r1[j][r] = r2[j][r] = 0.0f;
-    if (nn[j] >= g.cout) continue;
-    if (g.res0) load_res<T>(g.res0, g.ld0, opix, nn[j], g.cout, r0[j]);
-    if (g.res1) load_res<T>(g.res1, g.ld1, opix, nn[j], g.cout, r1[j]);
-    if (g.res2) load_res<T>(g.res2, g.ld2, opix, nn[j], g.cout, r2[j]);
-  }
-  const bool on = s.act != RGBAC_ACT_MASKSEL || g.sel[opix] != 0;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    if (nn[j] >= g.cout) continue;
-    float* vv = v[j];
-    if (is_dact(s.act)) {             // uniform: the folded activation backward, no zout
-#pragma unroll
-      for (int r = 0; r < 4; ++r) vv[r] = dact_apply<T>(s.act, s.act_param, vv[r], r0[j][r]);
-      const long long base = opix * g.out_ldc + g.out_coff + nn[j];
-      if (nn[j] + 3 < g.cout) {
-        Elem<T>::st4(out + base, v[j]);
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (nn[j] + r < g.cout) Elem<T>::st(out + base + r, vv[r]);
-      }
-      continue;
-    }
-    if (g.zout) {
-      float zv[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        zv[r] = s.act == RGBAC_ACT_SQBWD ? r0[j][r] + 2.0f * r1[j][r] * vv[r] : vv[r] + r0[j][r];
-      T* z = reinterpret_cast<T*>(g.zout) + opix * g.zld + g.out_coff + nn[j];
-      if (nn[j] + 3 < g.cout) {
-        Elem<T>::st4(z, zv);
-      } else {
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (nn[j] + r < g.cout) Elem<T>::st(z + r, zv[r]);
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float x = s.act == RGBAC_ACT_SQBWD ? r0[j][r] + 2.0f * r1[j][r] * vv[r] : vv[r] + r0[j][r];
-      switch (s.act) {
-        case RGBAC_ACT_GELU: x = gelu_t<T>(x); break;
-        case RGBAC_ACT_RELU: x = x > 0.f ? x : 0.f; break;
-        case RGBAC_ACT_LRELU: x = x > 0.f ? x : x * s.act_param; break;
-        case RGBAC_ACT_TANH_HALF: x = r1[j][r] + 0.5f * tanhf(x); break;
-        case RGBAC_ACT_GATE: x = r1[j][r] * sigmoid_f(x); break;
-        case RGBAC_ACT_GDN: x = gdn_t<T>(r1[j][r], x); break;
-        case RGBAC_ACT_IGDN: x = igdn_t<T>(r1[j][r], x); break;
-        case RGBAC_ACT_MASKSEL: x = on ? r1[j][r] + x : r1[j][r]; break;
-        default: break;
-      }
-      vv[r] = x + r2[j][r];
-    }
-    const long long base = opix * g.out_ldc + g.out_coff + nn[j];
-    if (nn[j] + 3 < g.cout) {
-      Elem<T>::st4(out + base, v[j]);
-    } else {
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if (nn[j] + r < g.cout) Elem<T>::st(out + base + r, vv[r]);
-    }
-  }
-}
-
-// GaussianConditional + ste_round on a (mu | sigma) conv output (ACT_GAUSS):
-//   hat = round(y - mu) + mu -> out;  v = |(train ? y + noise : hat) - mu|;
-//   lik = max(Phi((.5-v)/s) - Phi((-.5-v)/s), 1e-9), s = max(sigma, .11);
-//   returns clamp(-log(lik + 1e-10)/ln2, 0, 50)   (AutoEncoderRGB_Journal.py:255-257,280)
-template <typename T>
-__device__ __forceinline__ float gauss_elem(const ConvGroup& g, int m, int c, int nch, float mu,
-                                            float sg) {
-  const float yv = Elem<T>::ld(reinterpret_cast<const T*>(g.res1) + (long long)m * g.ld1 + c);
-  const float hat = rintf(yv - mu) + mu;
-  Elem<T>::st(reinterpret_cast<T*>(g.out) + (long long)m * g.out_ldc + g.out_coff + c, hat);
-  const float xin = g.aux0 ? yv + g.aux0[(long long)m * nch + c] : hat;
-  const float v = fabsf(xin - mu);
-  const float sc = fmaxf(sg, 0.11f);
-  const float lik = fmaxf(std_cum_f((0.5f - v) / sc) - std_cum_f((-0.5f - v) / sc), 1e-9f);
-  if (g.aux1) g.aux1[(long long)m * nch + c] = lik;
-  const float bits = (-1.0f * logf(lik + 1e-10f)) / 0.69314718055994530942f;
-  return fminf(fmaxf(bits, 0.0f), 50.0f);
-}
-
-// gauss_elem with y (res1) already loaded by the caller
-template <typename T>
-__device__ __forceinline__ float gauss_elem_y(const ConvGroup& g, int m, int c, int nch, float mu,
-                                              float sg, float yv) {
-  const float hat = rintf(yv - mu) + mu;
-  Elem<T>::st(reinterpret_cast<T*>(g.out) + (long long)m * g.out_ldc + g.out_coff + c, hat);
-  const float xin = g.aux0 ? yv + g.aux0[(long long)m * nch + c] : hat;
-  const float v = fabsf(xin - mu);
-  const float sc = fmaxf(sg, 0.11f);
-  const float lik = fmaxf(std_cum_f((0.5f - v) / sc) - std_cum_f((-0.5f - v) / sc), 1e-9f);
-  if (g.aux1) g.aux1[(long long)m * nch + c] = lik;
-  const float bits = (-1.0f * logf(lik + 1e-10f)) / 0.69314718055994530942f;
-  return fminf(fmaxf(bits, 0.0f), 50.0f);
-}
-
-typedef __attribute__((address_space(3))) void* lptr_t;
-
-// One LDS-DMA piece: each lane moves 16 bytes from its own global address to
-// lds_block + 16*lane.  Issued from inline asm so hipcc neither counts it nor
-// inserts its own vmcnt(0) before later ds_reads; every wait on it is the
-// kernel's explicit counted s_waitcnt (M0 saved/restored inside the statement).
-__device__ __forceinline__ void dma16(const void* src, uint4* lds_block) {
-  const uint32_t lds = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lptr_t)lds_block);
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(lds)
-      : "memory");
-}
-
-// The same with a wave-uniform base address and a per-lane 32-bit byte offset (the SADDR
-// form: no per-lane 64-bit address arithmetic).
-__device__ __forceinline__ void dma16_s(const void* sbase, uint32_t voff, uint32_t lds) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, %2\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(sbase), "s"(lds)
-      : "memory");
-}
-// dma16 with a precomputed wave-uniform LDS byte address (no per-call generic->LDS cast).
-__device__ __forceinline__ void dma16_l(const void* src, uint32_t lds) {
-  uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %2\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(src), "s"(lds)
-      : "memory");
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm() {
-  static_assert(N >= 0 && N <= 63, "vmcnt range");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-struct KDec { int ci, tap, ty, tx; };      // a lane's (channel, tap) position in K
-
-// Retire the oldest ring stage when `after` stages (LW DMA pieces each) were issued
-// behind it: vmcnt(LW * min(after, D)), D = the ring's steady-state look-ahead.
-template <int LW, int D>
-__device__ __forceinline__ void wait_ring(int after) {
-  if constexpr (D <= 0) {
-    wait_vm<0>();
-  } else {
-    if (after >= D) wait_vm<LW * D>();
-    else wait_ring<LW, D - 1>(after);
-  }
-}
 
 // BM x BN tile, 4 waves laid out WGM (along m) x WGN (along n), NBUF-stage ring of
 // K stages of KSM x 128 bytes per row (KSM = 2: half the barriers and ring bookkeeping per
@@ -1957,6 +1435,172 @@ __global__ void __launch_bounds__(512, 4) conv_pw_kernel(const ConvArgsDev args)
 #undef PWW_LOAD
 }
 
+// Pointwise kernel, forward form (bf16; 1x1 stride-1 conv, one source, cin_pad <= 32 * NKS,
+// cout <= 192, cout % 8 == 0; epilogues without zout / folded activation backward): the
+// GDN / IGDN norm pools and the attention blocks' output gate (layers/GDN.py:64-94,
+// layers/Masked_Attention.py:182-189).  At 64^2 x B8 the whole launch is 128 pixels per CU:
+// conv_pw_kernel spent it in three dependent memory round trips per wave (weight panel +
+// input, then the epilogue's res1 quads after the MFMAs, then the stores), ~21 us for ~25 MB
+// (PMC: 62 % of wave cycles waiting).  Here:
+//   * each wave's 16-pixel input tile lands in its own LDS slot by LDS-DMA (16-byte chunk c
+//     of pixel row r at slot c ^ (r & 7)), in the same request burst as the weight panel and
+//     the tile's residual quads (res0 / res2, and res1 unless it IS the input): one memory
+//     latency before the MFMAs, none after them;
+//   * GDN / IGDN (res1 == the input, square_input): the x quads of the epilogue are read from
+//     the LDS tile the MFMAs consumed -- the input is read from memory once, not twice;
+//   * the next tile's input DMA and residual loads are issued right after this tile's
+//     fragments have been consumed, so they overlap its epilogue and stores.
+// One 512-thread workgroup per CU (weights 72 KiB + 8 x 6 KiB tiles), persistent over tiles.
+template <int NKS>
+__global__ void __launch_bounds__(512, 2) conv_pw2_kernel(const ConvArgsDev args) {
+  constexpr int NT = 12, BN = 192, NCH = 4 * NKS, NW = 8, TS = 24;   // TS: tile row chunks
+  static_assert(NCH % 8 == 0 && NCH <= TS, "swizzle groups of 8 chunks");
+  constexpr int NPIECE = BN * NCH / 64;            // 1-KiB LDS-DMA pieces of the panel
+  constexpr int XP = 16 * TS / 64;                 // pieces of one 16-pixel tile (6)
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];
+  __shared__ float bl[BN];
+  const ConvShared& s = args.s;
+  const ConvGroup& g = args.g[blockIdx.z];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nchunk = g.cin_pad >> 3;               // real 8-channel chunks of K
+  const int Mtot = s.M, act = s.act, cout = g.cout;
+  const int ld = (int)g.sld0;
+  const bool sq_in = s.square != 0;
+  const bool xl = g.res1 == g.sp0 && g.ld1 == g.sld0;   // epilogue x from the LDS tile
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lptr_t)lds);
+  const uint32_t xbase = lbase + (uint32_t)(BN * NCH + wave * 16 * TS) * 16u;
+  const uint4* const Xl = lds + BN * NCH + wave * 16 * TS;
+  {
+    const bf16_t* wbase = reinterpret_cast<const bf16_t*>(g.w);
+    for (int p = wave; p < NPIECE; p += NW) {
+      const int d = p * 64 + lane;
+      const int row = d / NCH, slot = d - (d / NCH) * NCH;
+      const int ch = slot ^ (row & 7);
+      const bool ok = row < g.rows && ch < nchunk;
+      dma16_l(ok ? (const void*)(wbase + (size_t)row * g.k_pad + ch * 8) : (const void*)g_zero_page,
+              lbase + p * 1024);
+    }
+  }
+  for (int e = tid; e < BN; e += 64 * NW) bl[e] = (g.bias && e < cout) ? g.bias[e] : 0.0f;
+
+  const char* const src = reinterpret_cast<const char*>(g.sp0);
+  const bf16_t* const R0 = reinterpret_cast<const bf16_t*>(g.res0);
+  const bf16_t* const R1 = xl ? nullptr : reinterpret_cast<const bf16_t*>(g.res1);
+  const bf16_t* const R2 = reinterpret_cast<const bf16_t*>(g.res2);
+  const int ntile = (Mtot + 15) / 16;
+  const int tstride = gridDim.x * NW;
+  int tile = blockIdx.x * NW + wave;
+
+  // input tile -> this wave's LDS slot (rows past M and padding chunks read the zero page)
+#define PW2_DMA(t_)                                                                           \
+  do {                                                                                        \
+    _Pragma("unroll")                                                                         \
+    for (int p_ = 0; p_ < XP; ++p_) {                                                         \
+      const int d_ = p_ * 64 + lane;                                                          \
+      const int row_ = d_ / TS, slot_ = d_ - (d_ / TS) * TS;                                  \
+      const int ch_ = slot_ ^ (row_ & 7);                                                     \
+      const int m_ = (t_) * 16 + row_;                                                        \
+      const bool ok_ = m_ < Mtot && ch_ < nchunk;                                             \
+      dma16_l(ok_ ? (const void*)(src + ((size_t)m_ * ld + ch_ * 8) * 2)                      \
+                  : (const void*)g_zero_page, xbase + p_ * 1024);                             \
+    }                                                                                         \
+  } while (0)
+  // the tile's residual quads (channels 16 j + 4 fq .. + 3 of pixel fr), raw bf16
+#define PW2_RES(t_, e0_, e1_, e2_)                                                            \
+  do {                                                                                        \
+    const int m_ = (t_) * 16 + fr;                                                            \
+    const bool v_ = m_ < Mtot;                                                                \
+    const long long mm_ = v_ ? m_ : 0;                                                        \
+    _Pragma("unroll")                                                                         \
+    for (int j_ = 0; j_ < NT; ++j_) {                                                         \
+      const int n_ = 16 * j_ + 4 * fq;                                                        \
+      const bool on_ = v_ && n_ < cout;                                                       \
+      e0_[j_] = (R0 && on_) ? *reinterpret_cast<const uint2*>(R0 + mm_ * g.ld0 + n_) : make_uint2(0, 0); \
+      e1_[j_] = (R1 && on_) ? *reinterpret_cast<const uint2*>(R1 + mm_ * g.ld1 + n_) : make_uint2(0, 0); \
+      e2_[j_] = (R2 && on_) ? *reinterpret_cast<const uint2*>(R2 + mm_ * g.ld2 + n_) : make_uint2(0, 0); \
+    }                                                                                         \
+  } while (0)
+
+  uint2 e0[NT], e1[NT], e2[NT];
+  if (tile < ntile) {
+    PW2_DMA(tile);
+    PW2_RES(tile, e0, e1, e2);
+  }
+  wait_vm<0>();
+  __syncthreads();
+  bf16_t* const out = reinterpret_cast<bf16_t*>(g.out);
+  for (; tile < ntile; tile += tstride) {
+    f32x4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int st = 0; st < NKS; ++st) {
+      uint4 b = Xl[fr * TS + ((4 * st + fq) ^ (fr & 7))];
+      if (sq_in) b = square_chunk<bf16_t>(b);
+      const int slot = (4 * st + fq) ^ (fr & 7);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) mma_step<bf16_t>(acc[j], lds[(16 * j + fr) * NCH + slot], b);
+    }
+    if (xl) {                                      // GDN / IGDN: x quads from the LDS tile
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int c = 2 * j + (fq >> 1);
+        e1[j] = *reinterpret_cast<const uint2*>(
+            reinterpret_cast<const char*>(Xl + fr * TS + (c ^ (fr & 7))) + 8 * (fq & 1));
+      }
+    }
+    // this tile's operands are in registers: the next tile's requests go out now
+    const int m = tile * 16 + fr;
+    const bool valid = m < Mtot;
+    const bool sel_on = act == RGBAC_ACT_MASKSEL ? (valid && g.sel[m] != 0) : true;
+    uint2 c0[NT], c1[NT], c2[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) { c0[j] = e0[j]; c1[j] = e1[j]; c2[j] = e2[j]; }
+    const int nt = tile + tstride;
+    if (nt < ntile) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // tile reads done before the DMA
+      PW2_DMA(nt);
+      PW2_RES(nt, e0, e1, e2);
+    }
+    if (valid) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = 16 * j + 4 * fq;
+        if (n < cout) {
+          float v[4] = {acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
+          float r0[4] = {bf2f(c0[j].x & 0xFFFF), bf2f(c0[j].x >> 16), bf2f(c0[j].y & 0xFFFF),
+                         bf2f(c0[j].y >> 16)};
+          float r1[4] = {bf2f(c1[j].x & 0xFFFF), bf2f(c1[j].x >> 16), bf2f(c1[j].y & 0xFFFF),
+                         bf2f(c1[j].y >> 16)};
+          float r2[4] = {bf2f(c2[j].x & 0xFFFF), bf2f(c2[j].x >> 16), bf2f(c2[j].y & 0xFFFF),
+                         bf2f(c2[j].y >> 16)};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float x = v[r] + bl[n + r] + r0[r];
+            switch (act) {
+              case RGBAC_ACT_GELU: x = gelu_fast(x); break;
+              case RGBAC_ACT_RELU: x = x > 0.f ? x : 0.f; break;
+              case RGBAC_ACT_LRELU: x = x > 0.f ? x : x * s.act_param; break;
+              case RGBAC_ACT_GATE: x = r1[r] * sigmoid_f(x); break;
+              case RGBAC_ACT_GDN: x = gdn_t<bf16_t>(r1[r], x); break;
+              case RGBAC_ACT_IGDN: x = igdn_t<bf16_t>(r1[r], x); break;
+              case RGBAC_ACT_MASKSEL: x = sel_on ? r1[r] + x : r1[r]; break;
+              default: break;
+            }
+            v[r] = x + r2[r];
+          }
+          Elem<bf16_t>::st4(out + (long long)m * g.out_ldc + g.out_coff + n, v);
+        }
+      }
+    }
+    if (nt < ntile) wait_vm<0>();
+  }
+#undef PW2_DMA
+#undef PW2_RES
+}
+
 // DACT: the instance with the folded activation backward (training input gradients); the
 // forward's instance leaves that epilogue out (the kernel sits at its 128-VGPR limit)
 template <int NKS, bool DACT>
@@ -1984,7 +1628,61 @@ static void launch_pw_k(const ConvArgsDev& d, hipStream_t st) {
   hipLaunchKernelGGL(kern, dim3(gx, 1, nz), dim3(512), lds, st, d);
 }
 
+template <int NKS>
+static void launch_pw2_k(const ConvArgsDev& d, hipStream_t st) {
+  auto kern = conv_pw2_kernel<NKS>;
+  constexpr size_t lds = ((size_t)192 * 4 * NKS + 8 * 16 * 24) * 16;
+  static bool attr = false;
+  static int ncu = 0;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu < 1) ncu = 256;
+    (void)hipGetLastError();
+    attr = true;
+  }
+  const int nz = d.s.ngroups;
+  const int ntile = (d.s.M + 15) / 16;
+  int gx = (ncu + nz - 1) / nz;
+  const int need = (ntile + 7) / 8;
+  if (gx > need) gx = need;
+  if (gx < 1) gx = 1;
+  hipLaunchKernelGGL(kern, dim3(gx, 1, nz), dim3(512), lds, st, d);
+}
+
+// conv_pw2_kernel's preconditions (the rest -- one source, 1x1, cin/cout <= 192 -- are the
+// pointwise tile's own); RGBAC_PW2=0 keeps conv_pw_kernel (A/B switch)
+static bool pw2_ok(const ConvArgsDev& d) {
+  static const bool on = [] {
+    const char* e = getenv("RGBAC_PW2");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || is_dact(d.s.act) || d.s.act == RGBAC_ACT_TANH_HALF || d.s.act == RGBAC_ACT_SQBWD ||
+      d.s.act == RGBAC_ACT_GAUSS || d.s.mode != RGBAC_CONV)
+    return false;
+  // one 16-pixel tile per wave at most (8 waves x one workgroup per CU): a single round of
+  // latency-bound work, where its one request burst wins; with several tiles per wave
+  // (128^2 IGDN) conv_pw_kernel's two workgroups per CU stream better (measured 43.8 vs 45.6 us)
+  if ((long long)(d.s.M + 15) / 16 * d.s.ngroups > 8LL * 256) return false;
+  for (int i = 0; i < d.s.ngroups; ++i) {
+    const ConvGroup& g = d.g[i];
+    if (g.zout || g.cout % 8 || g.out_coff % 8 || g.out_ldc % 8 || g.cout > 192 ||
+        (g.res0 && g.ld0 % 4) || (g.res1 && g.ld1 % 4) || (g.res2 && g.ld2 % 4))
+      return false;
+  }
+  return true;
+}
+
 static void launch_pw(const ConvArgsDev& d, int cin_max, hipStream_t st) {
+  if (pw2_ok(d)) {
+    if (cin_max <= 64) launch_pw2_k<2>(d, st);
+    else if (cin_max <= 128) launch_pw2_k<4>(d, st);
+    else launch_pw2_k<6>(d, st);
+    return;
+  }
   if (is_dact(d.s.act)) {
     if (cin_max <= 64) launch_pw_k<2, true>(d, st);
     else if (cin_max <= 128) launch_pw_k<4, true>(d, st);
@@ -3349,7 +3047,7 @@ splitk_epilogue:
   return RGBAC_OK;
 }
 
-static int fill_group(const rgbac_conv_args* a, int ntaps_max, ConvGroup& g) {
+int fill_group(const rgbac_conv_args* a, int ntaps_max, ConvGroup& g) {
   RGBAC_REQUIRE(a->nsrc >= 1 && a->nsrc <= 3, "nsrc must be 1..3");
   RGBAC_REQUIRE(a->weight && a->out, "null weight/out");
   RGBAC_REQUIRE(a->ksplit == 1 || a->workspace, "split-K needs a workspace");
