@@ -1753,18 +1753,9 @@ __global__ void __launch_bounds__(512) conv_npatch_kernel(const ConvArgsDev args
     for (int r = 0; r < 4; ++r) yv[r] = Elem<T>::ld(yr + r);
   }
 
-  // ---- weight ring prologue: this wave's k-steps [k0, k1) of the fragment-major copy
   const uint4* const wf = reinterpret_cast<const uint4*>(g.w);
   uint4 ring[R][TN];
   int lks = k0;
-#pragma unroll
-  for (int u = 0; u < R; ++u) {
-    if (lks < k1) {
-#pragma unroll
-      for (int j = 0; j < TN; ++j) ring[u][j] = wf[((size_t)j * nks + lks) * 64 + lane];
-    }
-    ++lks;
-  }
 
   // ---- stage the input patch (as conv_fpatch_kernel): flat uint4 f -> (row, chunk)
   {
@@ -1792,7 +1783,27 @@ __global__ void __launch_bounds__(512) conv_npatch_kernel(const ConvArgsDev args
                                  (unsigned)cs) * 2u : 0u;
       dma16_l(ok ? (const void*)(src + off) : (const void*)g_zero_page, lbase + (pc << 10));
     }
-    wait_vm<0>();
+    // weight ring prologue (this wave's k-steps [k0, k1) of the fragment-major copy) behind
+    // the patch pieces, left in flight: the counted wait retires only the patch (in-order
+    // returns), not the ring
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      if (lks < k1) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) ring[u][j] = wf[((size_t)j * nks + lks) * 64 + lane];
+      }
+      ++lks;
+    }
+    const int nring = (k1 - k0 < R ? k1 - k0 : R) * TN;    // loads just issued (wave-uniform)
+    switch (nring) {
+      case 8: wait_vm<8>(); break;
+      case 6: wait_vm<6>(); break;
+      case 4: wait_vm<4>(); break;
+      case 3: wait_vm<3>(); break;
+      case 2: wait_vm<2>(); break;
+      case 1: wait_vm<1>(); break;
+      default: wait_vm<0>(); break;
+    }
     __syncthreads();
   }
   WG_T(1);
@@ -2588,10 +2599,6 @@ __global__ void __launch_bounds__(64 * NW * KS) conv_fpatch_kernel(const ConvArg
 #pragma unroll
     for (int j = 0; j < TN; ++j)
       wj[j] = wf + ((size_t)(ntile0 + j) * NKSC + kp * NKSP) * 64 + lane;
-#pragma unroll
-    for (int u = 0; u < RC; ++u)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) cring[u][j] = wj[j][u * 64];
   }
 
   // ---- stage the whole patch: flat uint4 index f -> (row, chunk), zero page outside
@@ -2620,7 +2627,19 @@ __global__ void __launch_bounds__(64 * NW * KS) conv_fpatch_kernel(const ConvArg
                                  (unsigned)cs) * 2u : 0u;
       dma16_l(ok ? (const void*)(src + off) : (const void*)g_zero_page, lbase + (pc << 10));
     }
-    wait_vm<0>();
+    if constexpr (CPT > 0) {
+      // the weight ring is requested BEHIND the patch pieces and left in flight: the wait
+      // below retires only the older requests (loads return in order), so the workgroup
+      // waits for its patch, not for the whole ring prologue (the per-workgroup probe's
+      // 3.4-4.8 us "stage" phase of the slice-chain convs was mostly that prologue)
+#pragma unroll
+      for (int u = 0; u < RC; ++u)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) cring[u][j] = wj[j][u * 64];
+      wait_vm<RC * TN>();
+    } else {
+      wait_vm<0>();
+    }
     __syncthreads();
   }
   WG_T(1);

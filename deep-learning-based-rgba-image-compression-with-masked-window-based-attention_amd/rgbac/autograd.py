@@ -389,7 +389,10 @@ def _end_of_backward():
 
 
 def _reduce(nslot, fmap, part, nsplit, slab, dw, nbias, bpart, n_pad, db, acc, st):
-    if not (REDUCE_BATCH and acc):
+    # queued reductions are flushed by a callback of the running backward pass: outside one
+    # (a weight gradient computed directly, e.g. a test or a custom loop) there is no engine
+    # to run the callback, so the reduction goes out immediately
+    if not (REDUCE_BATCH and acc) or torch._C._current_graph_task_id() < 0:
         flush_reductions()
         _lib.call("rgbac_wgrad_reduce", nslot, None if fmap is None else fmap.data_ptr(),
                   None if part is None else part.data_ptr(), nsplit, slab,
@@ -704,6 +707,7 @@ class ConvFn(Function):
         preps = []
         idxs = []
         sinks_in = []
+        targeted = set()            # sinks this launch already accumulates into in place
         for i, f in enumerate(feats):
             folded = call.src_act is not None and i == 0
             if not (need[7] if folded else need[8 + i]):
@@ -720,10 +724,14 @@ class ConvFn(Function):
                 preps.append(rt.prepare(pk, [G.src()], out=o, act=call.src_act,
                                         act_param=call.src_param, res0=Feat(zsrc, f.C),
                                         bias=False))
-            elif sk is not None and sk.buf is not None:
+            elif sk is not None and sk.buf is not None and id(sk) not in targeted:
                 # accumulate in the epilogue: out = W^T G + buffer (in place when the buffer
                 # is ours -- every element is read and written by the same lane -- and not an
-                # operand of this very launch)
+                # operand of this very launch).  Only ONE group of a launch may target a sink:
+                # a tensor used as two sources of one conv would otherwise have two groups
+                # read-modify-write the same buffer concurrently; later ones take the plain
+                # branch (fresh output, deposited after the launch)
+                targeted.add(id(sk))
                 prev = Feat(sk.buf, f.C)
                 inplace = sk.own and all(sk.buf is not t for t in (G.t, dz.t, dy.t))
                 o = prev if inplace else new_feat(f.B, f.H, f.W, f.C, dt, f.t.device)

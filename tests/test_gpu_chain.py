@@ -101,3 +101,57 @@ def test_chain_alpha_bitexact(device):
     assert int(rt.LAST_CHAIN[0][-1].item()) == 0
     assert torch.equal(got[0], ref[0])
     assert got[2].item() == ref[2].item()
+
+
+def test_chain_stage_outputs_bitexact(device):
+    """Every stage output of one recorded slice loop (the same Prepared records and buffers):
+    chain launch vs one launch per stage -- localises a mismatch to its stage and group."""
+    import bench
+    from rgbac import runtime as rt
+    from rgbac.layers.SupplyMask import mask_pyramid
+    from rgbac.models import _latent
+    net = bench.rgb_net().to(device).set_compute_dtype(torch.bfloat16)
+    x, a = bench.synth_inputs(2, 128, 128, seed=3)
+    x, a = x.to(device), a.to(device)
+    _, me = mask_pyramid(a, 4)
+    rec = {}
+    orig = _latent._slice_waves
+
+    def spy(*args):
+        with rt.chain_recording() as ch:
+            orig(*args)
+        rec["ch"], rec["ypart"] = ch, args[18]
+    prev = rt.CHAIN
+    rt.CHAIN = False
+    _latent._slice_waves = spy
+    try:
+        with torch.no_grad():
+            net(x, a, a, *me)
+    finally:
+        _latent._slice_waves = orig
+        rt.CHAIN = prev
+    ch, ypart = rec["ch"], rec["ypart"]
+    # the written channels of every stage output (an output may be a channel slice of YH)
+    views = [pr.out.t[..., pr.a.out_coff:pr.a.out_coff + (pr.pk.cout // 2 if pr.a.act == rt.ACT["gauss"]
+                                                          else pr.pk.cout)]
+             for st in ch.stages for pr in st]
+    for v in views:
+        v.zero_()
+    torch.cuda.synchronize()
+    ch.launch_each()
+    torch.cuda.synchronize()
+    ref = [v.clone() for v in views]
+    ref_bits = ypart.clone()
+    for v in views:
+        v.fill_(float("nan"))
+    ypart.zero_()
+    assert ch.run()
+    torch.cuda.synchronize()
+    assert int(rt.LAST_CHAIN[0][-1].item()) == 0
+    k = 0
+    for si, st in enumerate(ch.stages):
+        for gi, pr in enumerate(st):
+            same = torch.equal(views[k].view(torch.int16), ref[k].view(torch.int16))
+            assert same, (si, gi, pr.desc, (views[k].float() - ref[k].float()).abs().max().item())
+            k += 1
+    assert torch.equal(ypart, ref_bits), (ypart.sum().item(), ref_bits.sum().item())

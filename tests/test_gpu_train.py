@@ -929,3 +929,101 @@ def test_wgrad_patch_vs_torch(cin, cout, h, w, B):
     want = torch.nn.grad.conv2d_weight(x, (cout, cin, 3, 3), gy, stride=1, padding=1)
     assert nrel(dw.view(cout, cin, 3, 3), want) < 1e-4
     assert nrel(db, gy.sum(dim=(0, 2, 3))) < 1e-4
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("act,slope", [("gelu", 0.0), ("relu", 0.0), ("lrelu", 0.2)])
+@pytest.mark.parametrize("defer", [True, False])
+def test_deferred_act_chain_and_shared_sink(act, slope, defer, dtype):
+    """Training graph pieces the model relies on, against torch fp32 autograd:
+    * a two-conv chain whose first activation is deferred (its backward folded into the
+      second conv's input-gradient epilogue, ACT_DGELU / ACT_DLRELU; LeakyReLU with a nonzero
+      slope) or not (RGBAC_DEFER_ACT=0 path);
+    * a multiply-consumed activation y (gradient sink): one conv reads y TWICE as its two
+      sources (built first, so its backward runs after the other consumer's deposit: the
+      in-place accumulation path, only one group of the launch may take it) and another conv
+      reads it once."""
+    rt = _rt()
+    from rgbac import autograd as ag
+    g = _gen(zlib.crc32(f"chain/{act}/{defer}".encode()) % 100000)
+    rnd = (lambda t: t.to(torch.bfloat16).float()) if dtype == torch.bfloat16 else (lambda t: t)
+    m1, m2 = nn.Conv2d(16, 24, 3, padding=1), nn.Conv2d(24, 16, 3, padding=1)
+    m3, m4 = nn.Conv2d(48, 8, 3, padding=1), nn.Conv2d(24, 8, 1)
+    for m in (m1, m2, m3, m4):
+        with torch.no_grad():
+            for p in m.parameters():
+                p.copy_(rnd(torch.randn(p.shape, generator=g) * 0.2))
+    B, H, W = 2, 8, 12
+    x = rnd(torch.randn((B, 16, H, W), generator=g)).requires_grad_(True)
+    f = {"gelu": F.gelu, "relu": F.relu, "lrelu": lambda t: F.leaky_relu(t, slope)}[act]
+    # torch reference
+    h = f(m1(x))
+    c = m2(h)                                   # chain: act(m1 x) -> m2
+    y = F.gelu(m1(x))                           # shared activation (not deferred)
+    z2 = m3(torch.cat([y, y], 1))
+    z1 = m4(y)
+    gs = [torch.randn(t.shape, generator=g) for t in (c, z2, z1)]
+    (c * gs[0]).sum().backward(retain_graph=True)
+    ((z2 * gs[1]).sum() + (z1 * gs[2]).sum()).backward()
+    want_x = x.grad.clone()
+    want_p = {f"m{i + 1}.{k}": p.grad.clone() for i, m in enumerate((m1, m2, m3, m4))
+              for k, p in m.named_parameters()}
+
+    ms = [m.cuda() for m in (nn.Conv2d(16, 24, 3, padding=1), nn.Conv2d(24, 16, 3, padding=1),
+                             nn.Conv2d(48, 8, 3, padding=1), nn.Conv2d(24, 8, 1))]
+    for mg, m in zip(ms, (m1, m2, m3, m4)):
+        mg.load_state_dict(m.state_dict())
+    prev = ag.DEFER_ACT
+    ag.DEFER_ACT = defer
+    try:
+        fx = _leaf(x.detach(), dtype)
+        hf = ag.conv_t(ms[0], [fx], act=act, act_param=slope, defer=True)
+        cf = ag.conv_t(ms[1], [hf])
+        yf = ag.conv_t(ms[0], [fx], act="gelu")   # a ConvFn output: it carries a sink
+        z2f = ag.conv_t(ms[2], [yf, yf])        # built first: backward after z1's deposit
+        z1f = ag.conv_t(ms[3], [yf])
+        loss = sum((t.t * rt.to_nhwc(gg.cuda(), dtype).t).float().sum()
+                   for t, gg in ((cf, gs[0]), (z2f, gs[1]), (z1f, gs[2])))
+        loss.backward()
+    finally:
+        ag.DEFER_ACT = prev
+    tol, err = (1e-4, rel) if dtype == torch.float32 else (3e-2, nrel)
+    assert err(_nchw_grad(fx), want_x) < tol
+    pg = {f"m{i + 1}.{k}": p.grad for i, m in enumerate(ms) for k, p in m.named_parameters()}
+    for k, w in want_p.items():
+        assert err(pg[k], w) < tol, k
+
+
+def test_reduce_batch_matches_immediate_reductions():
+    """RGBAC_REDUCE_BATCH (weight-gradient slab reductions queued and issued eight per launch,
+    flushed at the end of backward): the AdamClamp flat gradient equals the one-launch-per-
+    reduction path bit for bit (same fixed summation order), bf16 B=2 64^2 training step.
+    Outside a backward pass the reduction goes out immediately (no engine callback)."""
+    from rgbac import autograd as ag
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    from rgbac.optim import AdamClamp
+    g = _gen(71)
+    B, H, W = 2, 64, 64
+    x = (torch.randint(0, 256, (B, 3, H, W), generator=g).float() / 255).cuda()
+    a = torch.ones((B, 1, H, W)).cuda()
+    me = [t.cuda() for t in ref.supply_mask(a.cpu())]
+    nz = (torch.rand((B, 1, 1, 192), generator=g) - 0.5).cuda()
+    ny = (torch.rand((B, 8, 8, 80), generator=g) - 0.5).cuda()
+    torch.manual_seed(234)
+    net = AutoEncoder().cuda().train().set_compute_dtype(torch.bfloat16)
+    opt = AdamClamp(net.parameters(), lr=1e-4, clip=5.0)
+    grads = {}
+    prev = ag.REDUCE_BATCH
+    try:
+        for mode in (False, True, False):
+            ag.REDUCE_BATCH = mode
+            opt.zero_grad()
+            o = net(x, a, a, *me[:4], noise_z=nz, noise_y=ny)
+            (4096 * o[1] + o[2]).backward()
+            torch.cuda.synchronize()
+            assert not ag._PENDING, "queued reductions left after backward"
+            grads.setdefault(mode, []).append(opt.flat_grad.clone())
+    finally:
+        ag.REDUCE_BATCH = prev
+    assert torch.equal(grads[False][0], grads[False][1])      # the step is deterministic
+    assert torch.equal(grads[True][0], grads[False][0])
