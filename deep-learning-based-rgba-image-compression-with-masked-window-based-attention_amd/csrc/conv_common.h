@@ -1,4 +1,4 @@
-// Shared by the implicit-GEMM convolution translation units (conv.hip, chain.hip): the
+// Shared by the implicit-GEMM convolution translation units (conv.hip): the
 // device-side launch descriptors (ConvArgsDev), the fused-epilogue helpers and the LDS-DMA /
 // wait primitives.  Everything here is inline or has internal linkage (each TU holds its own
 // zero page), so the TUs compile independently.
@@ -533,9 +533,5 @@ __device__ __forceinline__ void wait_ring(int after) {
 
 // rgbac_conv_args -> the device-side group descriptor (validates the group; conv.hip)
 int fill_group(const rgbac_conv_args* a, int ntaps_max, ConvGroup& g);
-
-#ifndef RGBAC_CHAIN_RC1
-#define RGBAC_CHAIN_RC1 24   // chain engine wide-item weight ring depth at TN 1 (TN 2: half)
-#endif
 
 }  // namespace rgbac

@@ -166,10 +166,6 @@ SIGNATURES = {
     "rgbac_rans_encoder_create": [ctypes.POINTER(ctypes.c_void_p)],
     "rgbac_rans_encoder_destroy": [_VP],
     "rgbac_rans_encoder_put": [_VP, _VP, _VP, _I64, _VP, _I32, _VP, _VP, _I32],
-    "rgbac_chain_desc_size": [],
-    "rgbac_chain_counter_words": [_I32, _I32, _I32],
-    "rgbac_chain_build": [_VP, _VP, _I32, _VP],
-    "rgbac_chain_launch": [_VP, _I32, _I32, _I32, _I32, _VP, _VP],
     "rgbac_comm_load": [ctypes.c_char_p],
     "rgbac_comm_unique_id": [_VP],
     "rgbac_comm_init": [_VP, _I32, _I32, _I32, ctypes.POINTER(ctypes.c_void_p)],
@@ -184,8 +180,7 @@ SIGNATURES = {
     "rgbac_rans_decode": [ctypes.POINTER(RansDecoderState), _VP, _I64, _VP, _I32, _VP, _VP, _I32,
                           _VP],
 }
-_RESTYPE = {"rgbac_last_error": ctypes.c_char_p, "rgbac_rans_encoder_bound": ctypes.c_int64,
-            "rgbac_chain_counter_words": ctypes.c_int64}
+_RESTYPE = {"rgbac_last_error": ctypes.c_char_p, "rgbac_rans_encoder_bound": ctypes.c_int64}
 
 _lib = None
 

@@ -185,21 +185,9 @@ def latent_path(model, y, training=False, noise_z=None, noise_y=None, debug=None
                            for i in range(p0c, ns)])
                 ev_cc.record(side)
     waited = set()
-    # bf16 inference: the whole slice loop as one persistent launch (rt.Chain, csrc/chain.hip)
-    use_chain = (rt.CHAIN and not pre_ok and not training and debug is None and
-                 dt == torch.bfloat16 and not torch.is_grad_enabled() and
-                 h % 4 == 0 and w % 16 == 0)
-    rec = rt.chain_recording() if use_chain else None
-    ch = rec.__enter__() if rec is not None else None
-    try:
-        _slice_waves(model, waves, y, YH, means, scales, Cm, cs, B, h, w, dt, dev, training,
-                     noise_y, debug, liks, musig, ypart, pre_ok, p0c, p0l, waited,
-                     (main, ev_cc, ev_lrp, Pm, Ps, Plrp) if pre_ok else None)
-    finally:
-        if rec is not None:
-            rec.__exit__(None, None, None)
-    if ch is not None and not ch.run():
-        ch.launch_each()
+    _slice_waves(model, waves, y, YH, means, scales, Cm, cs, B, h, w, dt, dev, training,
+                 noise_y, debug, liks, musig, ypart, pre_ok, p0c, p0l, waited,
+                 (main, ev_cc, ev_lrp, Pm, Ps, Plrp) if pre_ok else None)
     if pre_ok:
         main.wait_stream(side)                 # join the side stream (graph capture needs it)
     if debug is not None:
@@ -210,7 +198,8 @@ def latent_path(model, y, training=False, noise_z=None, noise_y=None, debug=None
 
 def _slice_waves(model, waves, y, YH, means, scales, Cm, cs, B, h, w, dt, dev, training,
                  noise_y, debug, liks, musig, ypart, pre_ok, p0c, p0l, waited, side):
-    """The slice waves of latent_path (launched, or recorded as chain stages)."""
+    """The slice waves of latent_path: per wave the cc stacks, the (mu | sigma) Gaussian
+    launch and the lrp stacks (grouped launches)."""
     msup = model.max_support_slices
     Wc = model.cc_mean_transforms[0][0].out_channels
     Wl = model.lrp_transforms[0][0].out_channels

@@ -746,104 +746,9 @@ def _flush_buffer(dev):
     return buf
 
 
-# ---- slice-chain engine (csrc/chain.hip): a recorded list of grouped 3x3 convs run as ONE
-# persistent launch.  Inside ``chain_recording()`` launch() records its (grouped) convs as a
-# stage instead of launching them -- prepare() has already allocated every output, so each
-# stage's buffers exist when the chain is launched -- and ``Chain.run()`` launches the whole
-# list.  Measured SLOWER than one launch per stage (config 2: 1,778 us for the 36 stages vs
-# ~600 us launched): one 12-wave workgroup per CU walks its items one at a time,
-# so nothing overlaps an item's staging / K loop / epilogue latencies the way several resident
-# workgroups per CU do in the per-stage launches.  Opt-in: RGBAC_CHAIN=1.
-CHAIN = os.environ.get("RGBAC_CHAIN", "0") == "1"
-_RECORD = [None]
-_CHAIN_TABLES = {}          # descriptor-table bytes -> (pinned host copy, device copy)
-LAST_CHAIN = [None]         # counters of the most recent chain launch (tests read its error word)
-_CHAIN_ARENA = [None, 0]    # pinned host arena for descriptor tables, next free offset
-
-
-def _chain_arena():
-    if _CHAIN_ARENA[0] is None:
-        _CHAIN_ARENA[0] = torch.zeros(32 << 20, dtype=torch.uint8).pin_memory()
-    return _CHAIN_ARENA[0]
-
-
-class Chain:
-    def __init__(self):
-        self.stages = []
-
-    def run(self):
-        """Launch the recorded stages as one chain_kernel; False (nothing launched) if a stage
-        is outside the engine's envelope -- the caller then launches them one by one."""
-        if not self.stages:
-            return True
-        dev = self.stages[0][0].out.t.device
-        args = [pr for st in self.stages for pr in st]
-        arr = (_lib.ConvArgs * len(args))()
-        for i, pr in enumerate(args):
-            arr[i] = pr.a
-            arr[i].tile, arr[i].ksplit, arr[i].workspace, arr[i].tile_counters = 0, 1, None, None
-            arr[i].weight = frag_weights(pr.pk).data_ptr()
-        ng = (ctypes.c_int32 * len(self.stages))(*[len(st) for st in self.stages])
-        dsz = _lib.load().rgbac_chain_desc_size()
-        host = (ctypes.c_uint8 * (dsz * len(self.stages)))()
-        lib = _lib.load()
-        if lib.rgbac_chain_build(ctypes.addressof(arr), ctypes.addressof(ng), len(self.stages),
-                                 ctypes.addressof(host)) != 0:
-            return False
-        key = bytes(host)
-        ent = _CHAIN_TABLES.get(key)
-        if ent is None:
-            # the table goes up from a slot of a pinned arena allocated outside any capture
-            # (a memcpy node under graph capture reads that host memory at every replay, so a
-            # slot is never reused); one device copy per distinct table
-            arena = _chain_arena()
-            off = _CHAIN_ARENA[1]
-            if off + len(key) > arena.numel():
-                raise RuntimeError("rgbac: chain descriptor arena exhausted")
-            _CHAIN_ARENA[1] = (off + len(key) + 255) & ~255
-            h = arena[off:off + len(key)]
-            h.copy_(torch.frombuffer(bytearray(key), dtype=torch.uint8))
-            d = torch.empty(len(key), dtype=torch.uint8, device=dev)
-            d.copy_(h, non_blocking=True)
-            ent = _CHAIN_TABLES[key] = (h, d)
-        a0 = args[0].a
-        words = lib.rgbac_chain_counter_words(len(self.stages), a0.batch, a0.in_h)
-        cnt = torch.empty(words, dtype=torch.int32, device=dev)
-        LAST_CHAIN[0] = cnt
-
-        def run():
-            _lib.call("rgbac_chain_launch", ent[1].data_ptr(), len(self.stages), a0.batch,
-                      a0.in_h, a0.in_w, cnt.data_ptr(), _lib.stream_ptr(dev))
-        if PROFILER is None:
-            run()
-        else:
-            PROFILER.wrap("chain_kernel", sum(pr.flops for pr in args),
-                          sum(pr.nbytes for pr in args), run,
-                          f"chain_kernel {len(self.stages)} stages {a0.batch}x{a0.in_h}x{a0.in_w}")
-        return True
-
-    def launch_each(self):
-        for st in self.stages:
-            launch(st)
-
-
-@contextlib.contextmanager
-def chain_recording():
-    """Record launch() calls as chain stages (see Chain)."""
-    ch = Chain()
-    prev, _RECORD[0] = _RECORD[0], ch
-    try:
-        yield ch
-    finally:
-        _RECORD[0] = prev
-
-
 def launch(preps, force=None):
     """Launch prepared convs (same geometry) as ONE grouped kernel; returns their outputs.
     ``force``: (tile, ksplit) to use instead of the tuned / heuristic choice."""
-    if _RECORD[0] is not None and force is None:
-        _RECORD[0].stages.append(list(preps))
-        return [pr.out for pr in preps]
     n = len(preps)
     p0 = preps[0]
     dev = p0.out.t.device

@@ -568,26 +568,6 @@ int rgbac_avgpool2(int planes, int h, int w, const float* x, float* y, void* str
 int rgbac_msssim_combine(int levels, int batch, const float* mcs, const float* ssim_last,
                          const float* weights, float* per_image, float* mean, void* stream);
 
-/* Slice-chain engine (csrc/chain.hip): a list of dependent grouped 3x3 stride-1 bf16 convs
- * on one latent grid -- the channel-conditional slice loop of
- * models/AutoEncoderRGB_Journal.py:240-266 / AutoEncoderMask_Journal.py:268-298 (cc_mean /
- * cc_scale stacks, (mu | sigma) + GaussianConditional + STE (ACT_GAUSS), lrp stacks ending in
- * the tanh update (ACT_TANH_HALF)) -- run as ONE persistent launch.  Stage s is the
- * stage_ngroups[s] consecutive records of `args` (the rgbac_conv2d_grouped contract: shared
- * geometry and activation; `weight` is the FRAGMENT-MAJOR copy; tile / ksplit / workspace are
- * ignored).  rgbac_chain_build validates the stages and writes nstages descriptors of
- * rgbac_chain_desc_size() bytes each into host_table (no GPU work); the caller copies the
- * table to device memory and passes it to rgbac_chain_launch together with an int32
- * workspace of rgbac_chain_counter_words() words (zeroed by the launch itself; its last word
- * is the give-up flag: nonzero if a dependency wait timed out).  Outputs are bit-identical to
- * launching the stages one by one through rgbac_conv2d_grouped. */
-int rgbac_chain_desc_size(void);
-int64_t rgbac_chain_counter_words(int32_t nstages, int32_t batch, int32_t h);
-int rgbac_chain_build(const rgbac_conv_args* args, const int32_t* stage_ngroups,
-                      int32_t nstages, void* host_table);
-int rgbac_chain_launch(const void* dev_table, int32_t nstages, int32_t batch, int32_t h,
-                       int32_t w, int32_t* counters, void* stream);
-
 /* Data-parallel gradient exchange (csrc/comm.cpp; BASELINE config 5 -- the reference trains
  * on one GPU, DataParallel is commented out at trainRGB.py:374, so no reference interface is
  * replaced: this is the all-reduce of rgbac/parallel.py's gradient buckets).  RCCL is called
