@@ -1451,6 +1451,41 @@ __global__ void __launch_bounds__(512, 4) conv_pw_kernel(const ConvArgsDev args)
 //   * the next tile's input DMA and residual loads are issued right after this tile's
 //     fragments have been consumed, so they overlap its epilogue and stores.
 // One 512-thread workgroup per CU (weights 72 KiB + 8 x 6 KiB tiles), persistent over tiles.
+// conv_pw2_kernel's epilogue for one pixel row (channels 16 j + 4 fq .. + 3), ACT fixed at
+// compile time (-1: no activation):
+// v = acc + bias + res0, act, + res2, bf16 store
+template <int NT, int ACT>
+__device__ __forceinline__ void pw2_epi(bf16_t* orow, const f32x4 (&acc)[NT], const float* bl,
+                                        const uint2 (&c0)[NT], const uint2 (&c1)[NT],
+                                        const uint2 (&c2)[NT], int fq, int cout, bool sel_on,
+                                        float act_param) {
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int n = 16 * j + 4 * fq;
+    if (n >= cout) continue;
+    const float r0[4] = {bf2f(c0[j].x & 0xFFFF), bf2f(c0[j].x >> 16), bf2f(c0[j].y & 0xFFFF),
+                         bf2f(c0[j].y >> 16)};
+    const float r1[4] = {bf2f(c1[j].x & 0xFFFF), bf2f(c1[j].x >> 16), bf2f(c1[j].y & 0xFFFF),
+                         bf2f(c1[j].y >> 16)};
+    const float r2[4] = {bf2f(c2[j].x & 0xFFFF), bf2f(c2[j].x >> 16), bf2f(c2[j].y & 0xFFFF),
+                         bf2f(c2[j].y >> 16)};
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float x = acc[j][r] + bl[n + r] + r0[r];
+      if constexpr (ACT == RGBAC_ACT_GDN) x = gdn_t<bf16_t>(r1[r], x);
+      else if constexpr (ACT == RGBAC_ACT_IGDN) x = igdn_t<bf16_t>(r1[r], x);
+      else if constexpr (ACT == RGBAC_ACT_GATE) x = r1[r] * sigmoid_f(x);
+      else if constexpr (ACT == RGBAC_ACT_GELU) x = gelu_fast(x);
+      else if constexpr (ACT == RGBAC_ACT_MASKSEL) x = sel_on ? r1[r] + x : r1[r];
+      else if constexpr (ACT == RGBAC_ACT_RELU) x = x > 0.f ? x : 0.f;
+      else if constexpr (ACT == RGBAC_ACT_LRELU) x = x > 0.f ? x : x * act_param;
+      v[r] = x + r2[r];
+    }
+    Elem<bf16_t>::st4(orow + n, v);
+  }
+}
+
 template <int NKS>
 __global__ void __launch_bounds__(512, 2) conv_pw2_kernel(const ConvArgsDev args) {
   constexpr int NT = 12, BN = 192, NCH = 4 * NKS, NW = 8, TS = 24;   // TS: tile row chunks
@@ -1565,34 +1600,18 @@ __global__ void __launch_bounds__(512, 2) conv_pw2_kernel(const ConvArgsDev args
       PW2_RES(nt, e0, e1, e2);
     }
     if (valid) {
-#pragma unroll
-      for (int j = 0; j < NT; ++j) {
-        const int n = 16 * j + 4 * fq;
-        if (n < cout) {
-          float v[4] = {acc[j][0], acc[j][1], acc[j][2], acc[j][3]};
-          float r0[4] = {bf2f(c0[j].x & 0xFFFF), bf2f(c0[j].x >> 16), bf2f(c0[j].y & 0xFFFF),
-                         bf2f(c0[j].y >> 16)};
-          float r1[4] = {bf2f(c1[j].x & 0xFFFF), bf2f(c1[j].x >> 16), bf2f(c1[j].y & 0xFFFF),
-                         bf2f(c1[j].y >> 16)};
-          float r2[4] = {bf2f(c2[j].x & 0xFFFF), bf2f(c2[j].x >> 16), bf2f(c2[j].y & 0xFFFF),
-                         bf2f(c2[j].y >> 16)};
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            float x = v[r] + bl[n + r] + r0[r];
-            switch (act) {
-              case RGBAC_ACT_GELU: x = gelu_fast(x); break;
-              case RGBAC_ACT_RELU: x = x > 0.f ? x : 0.f; break;
-              case RGBAC_ACT_LRELU: x = x > 0.f ? x : x * s.act_param; break;
-              case RGBAC_ACT_GATE: x = r1[r] * sigmoid_f(x); break;
-              case RGBAC_ACT_GDN: x = gdn_t<bf16_t>(r1[r], x); break;
-              case RGBAC_ACT_IGDN: x = igdn_t<bf16_t>(r1[r], x); break;
-              case RGBAC_ACT_MASKSEL: x = sel_on ? r1[r] + x : r1[r]; break;
-              default: break;
-            }
-            v[r] = x + r2[r];
-          }
-          Elem<bf16_t>::st4(out + (long long)m * g.out_ldc + g.out_coff + n, v);
-        }
+      bf16_t* const orow = out + (long long)m * g.out_ldc + g.out_coff;
+      // one compile-time epilogue per activation (a per-element switch compiled to scalar
+      // compare-and-branch chains: ~3,000 SALU per wave)
+      switch (act) {
+        case RGBAC_ACT_GDN: pw2_epi<NT, RGBAC_ACT_GDN>(orow, acc, bl, c0, c1, c2, fq, cout, sel_on, s.act_param); break;
+        case RGBAC_ACT_IGDN: pw2_epi<NT, RGBAC_ACT_IGDN>(orow, acc, bl, c0, c1, c2, fq, cout, sel_on, s.act_param); break;
+        case RGBAC_ACT_GATE: pw2_epi<NT, RGBAC_ACT_GATE>(orow, acc, bl, c0, c1, c2, fq, cout, sel_on, s.act_param); break;
+        case RGBAC_ACT_GELU: pw2_epi<NT, RGBAC_ACT_GELU>(orow, acc, bl, c0, c1, c2, fq, cout, sel_on, s.act_param); break;
+        case RGBAC_ACT_MASKSEL: pw2_epi<NT, RGBAC_ACT_MASKSEL>(orow, acc, bl, c0, c1, c2, fq, cout, sel_on, s.act_param); break;
+        case RGBAC_ACT_RELU: pw2_epi<NT, RGBAC_ACT_RELU>(orow, acc, bl, c0, c1, c2, fq, cout, sel_on, s.act_param); break;
+        case RGBAC_ACT_LRELU: pw2_epi<NT, RGBAC_ACT_LRELU>(orow, acc, bl, c0, c1, c2, fq, cout, sel_on, s.act_param); break;
+        default: pw2_epi<NT, -1>(orow, acc, bl, c0, c1, c2, fq, cout, sel_on, s.act_param); break;
       }
     }
     if (nt < ntile) wait_vm<0>();
@@ -1663,10 +1682,13 @@ static bool pw2_ok(const ConvArgsDev& d) {
   if (!on || is_dact(d.s.act) || d.s.act == RGBAC_ACT_TANH_HALF || d.s.act == RGBAC_ACT_SQBWD ||
       d.s.act == RGBAC_ACT_GAUSS || d.s.mode != RGBAC_CONV)
     return false;
-  // one 16-pixel tile per wave at most (8 waves x one workgroup per CU): a single round of
-  // latency-bound work, where its one request burst wins; with several tiles per wave
-  // (128^2 IGDN) conv_pw_kernel's two workgroups per CU stream better (measured 43.8 vs 45.6 us)
-  if ((long long)(d.s.M + 15) / 16 * d.s.ngroups > 8LL * 256) return false;
+  // (multi-tile launches too: with the compile-time epilogue the 128^2 IGDN takes 38.0 us
+  // here vs 44.5 us on conv_pw_kernel, same box; RGBAC_PW2_ALL=0 keeps those on the old one)
+  static const bool all = [] {
+    const char* e = getenv("RGBAC_PW2_ALL");
+    return !(e && e[0] == '0');
+  }();
+  if (!all && (long long)(d.s.M + 15) / 16 * d.s.ngroups > 8LL * 256) return false;
   for (int i = 0; i < d.s.ngroups; ++i) {
     const ConvGroup& g = d.g[i];
     if (g.zout || g.cout % 8 || g.out_coff % 8 || g.out_ldc % 8 || g.cout > 192 ||

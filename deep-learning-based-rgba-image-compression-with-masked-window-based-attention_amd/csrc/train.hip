@@ -2223,6 +2223,7 @@ gather_kernel(long long n, const float* __restrict__ src, const int* __restrict_
 // blocks [blk0[t], blk0[t+1]) cover its elements, 2048 per block; a block finds its task by
 // binary search over blk0.
 constexpr int kGatherChunk = 2048;
+constexpr long long kGatherCopy16 = 16;   // task dtype: 16-byte chunk copy (rgbac.h)
 // the bf16 path covers a block's chunk as 256 threads x 8 elements
 static_assert(kGatherChunk == 256 * 8, "gather_multi_kernel: bf16 chunk = 256 threads x 8");
 __global__ void __launch_bounds__(256)
@@ -2239,6 +2240,19 @@ gather_multi_kernel(int ntask, const long long* __restrict__ tasks,
   const int* idx = reinterpret_cast<const int*>(tk[1]);
   const long long n = tk[3];
   const long long e0 = (b - blk0[lo]) * kGatherChunk;
+  if (tk[4] == kGatherCopy16) {
+    // 16-byte chunk copy through a chunk map: the fragment-major training packs are a
+    // permutation of 8-element runs of the plain pack written by the previous launch (L2 /
+    // MALL-hot bf16 rows), not a second element gather from the fp32 parameter
+    const uint4* s4 = reinterpret_cast<const uint4*>(tk[0]);
+    uint4* d4 = reinterpret_cast<uint4*>(tk[2]);
+#pragma unroll
+    for (int r = 0; r < kGatherChunk / 256; ++r) {
+      const long long e = e0 + r * 256 + threadIdx.x;
+      if (e < n) { const int j = idx[e]; d4[e] = j >= 0 ? s4[j] : make_uint4(0, 0, 0, 0); }
+    }
+    return;
+  }
   if (tk[4] == RGBAC_F32) {
     float* dst = reinterpret_cast<float*>(tk[2]);
 #pragma unroll

@@ -76,6 +76,7 @@ class TPack:
         self.token = 0                 # == _PREFETCH[0]: re-gathered by this step's prefetch
         self.gen = -1                  # rt.PARAM_GEN at that prefetch (an optimizer step bumps it)
         self.frag = self.fidx = None   # fragment-major copy (runtime.frag_weights layout)
+        self.fcmap = None              # frag 16-byte chunk -> plain-pack chunk (prefetch_packs)
 
     def enable_frag(self):
         """Also gather the fragment-major copy the conv_fpatch / conv_npatch tiles read
@@ -91,6 +92,15 @@ class TPack:
         nks = taps * c32 // 32
         self.fidx = wt.reshape(nph, rows // 16, 16, nks, 4, 8).permute(0, 1, 3, 4, 2, 5).contiguous()
         self.frag = torch.zeros(self.fidx.shape, dtype=self.w.dtype, device=self.idx.device)
+        # the same permutation applied to the PLAIN pack's positions: every 8-element run of
+        # the fragment-major copy is one 16-byte chunk of the plain pack (cin_pad and k_pad are
+        # multiples of 8), so prefetch_packs copies chunks from the just-gathered plain pack
+        pos = torch.arange(self.idx.numel(), dtype=torch.int64, device=self.idx.device)
+        pw = pos.reshape(nph, rows, -1)[:, :, :taps * cp].reshape(nph, rows, taps, cp)
+        pt = torch.full((nph, rows, taps, c32), -1, dtype=torch.int64, device=self.idx.device)
+        pt[..., :cp] = pw
+        first = pt.reshape(nph, rows // 16, 16, nks, 4, 8).permute(0, 1, 3, 4, 2, 5)[..., 0]
+        self.fcmap = torch.where(first >= 0, first // 8, -1).to(torch.int32).contiguous().reshape(-1)
         self.src = None                # gather both at the next refresh
         return self
 
@@ -120,6 +130,7 @@ class TPack:
 
 
 PREFETCH = os.environ.get("RGBAC_PACK_PREFETCH", "1") != "0"
+_GATHER_COPY16 = 16          # rgbac_weight_gather_multi task dtype: 16-byte chunk copy
 _PREFETCH = [1]              # current prefetch token (TPack.token == it: gathered this step)
 _TASKS = {}
 
@@ -150,24 +161,34 @@ def prefetch_packs(model):
     if ent is None or ent[0] != key:
         if torch.cuda.is_current_stream_capturing():
             return                     # no host->device table upload inside a graph capture
-        rows, blk0 = [], [0]
+        # launch 1: the plain packs and biases, gathered from the fp32 parameters; launch 2:
+        # the fragment-major copies as 16-byte chunk copies of the plain packs (bf16 rows
+        # just written) -- one element gather from the parameters per packed weight, not two
+        rows, blk0, crows, cblk0 = [], [0], [], [0]
         for tp in packs:
             for dst, idx, sp, dt in ((tp.w, tp.idx, tp.src[0], _lib.dtype_code(tp.w.dtype)),
-                                     (tp.frag, tp.fidx, tp.src[0], _lib.dtype_code(tp.w.dtype)),
                                      (tp.bias, tp.bias_idx, tp.src[1], _lib.F32)):
                 if sp is None or idx is None or dst is None or dst.numel() == 0:
                     continue
                 n = dst.numel()
                 rows.append([sp, idx.data_ptr(), dst.data_ptr(), n, dt])
                 blk0.append(blk0[-1] + -(-n // 2048))
+            if tp.frag is not None and tp.frag.numel():
+                n = tp.fcmap.numel()
+                crows.append([tp.w.data_ptr(), tp.fcmap.data_ptr(), tp.frag.data_ptr(), n,
+                              _GATHER_COPY16])
+                cblk0.append(cblk0[-1] + -(-n // 2048))
         dev = packs[0].w.device
-        tasks = torch.tensor(rows, dtype=torch.int64, device=dev)
-        b0 = torch.tensor(blk0, dtype=torch.int64, device=dev)
-        ent = (key, tasks, b0, len(rows), blk0[-1])
+        launches = []
+        for rr, bb in ((rows, blk0), (crows, cblk0)):
+            if rr:
+                launches.append((torch.tensor(rr, dtype=torch.int64, device=dev),
+                                 torch.tensor(bb, dtype=torch.int64, device=dev), len(rr), bb[-1]))
+        ent = (key, launches)
         _TASKS[id(model)] = ent
-    _, tasks, b0, ntask, nblk = ent
-    _lib.call("rgbac_weight_gather_multi", ntask, tasks.data_ptr(), b0.data_ptr(), nblk,
-              _lib.stream_ptr(tasks.device))
+    for tasks, b0, ntask, nblk in ent[1]:
+        _lib.call("rgbac_weight_gather_multi", ntask, tasks.data_ptr(), b0.data_ptr(), nblk,
+                  _lib.stream_ptr(tasks.device))
     for tp in packs:
         tp.token, tp.gen = _PREFETCH[0], rt.PARAM_GEN
 

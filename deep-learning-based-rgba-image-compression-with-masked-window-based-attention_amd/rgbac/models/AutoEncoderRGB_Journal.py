@@ -180,14 +180,28 @@ class AutoEncoder(_CompressionModelMixin, nn.Module):
         dt = self.compute_dtype
         with torch.no_grad():
             x = input.contiguous().float()
+            # reconmask = round(reconmask*255)/255 ; md1..md4 = DecMakeMask(reconmask)  (:212-215):
+            # only the decoder reads md, so the pyramid runs on a side stream beside the
+            # encoder and the entropy model (its launch is one latency-bound round of 128
+            # workgroups, ~18 us on the critical path otherwise)
+            main, side = rt.side_streams(x.device)
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                _, md = mask_pyramid(reconmask, 4, round255=True)
+            for t in md:
+                t.record_stream(main)
             xf = rt.to_nhwc(x, dt)
-            # reconmask = round(reconmask*255)/255 ; md1..md4 = DecMakeMask(reconmask)  (:212-215)
-            _, md = mask_pyramid(reconmask, 4, round255=True)
             y = self.Encoder.nhwc(xf, me2, me3)                                  # :217
             yh, ypart, zpart = latent_path(self, y, self.training, noise_z, noise_y, debug)
+            main.wait_stream(side)
             xh = self.Decoder.nhwc(yh, md[1], md[2])                              # :273
+            # x_hat's NCHW copy beside the loss / bits reduction
+            side.wait_stream(main)
+            with torch.cuda.stream(side):
+                x_hat = rt.to_nchw(xh)
+            x_hat.record_stream(main)
             out = finalize(0, x, xh, mask.contiguous().float(), ypart, zpart)    # :280-295
-            x_hat = rt.to_nchw(xh)
+            main.wait_stream(side)
         if debug is not None:
             debug.update(y=y)
         return x_hat, out[0], out[1], out[2], out[3]

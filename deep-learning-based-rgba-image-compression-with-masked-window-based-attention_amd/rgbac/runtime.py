@@ -266,6 +266,23 @@ WINBLOCK_FUSED = os.environ.get("RGBAC_WINBLOCK", "1") != "0"  # ws-8 attention 
 WINBLOCK4_FUSED = os.environ.get("RGBAC_WINBLOCK4", "1") != "0"  # ws-4 / C-80 block, 1 launch
 
 
+_SIDE_STREAMS = {}
+SIDE = os.environ.get("RGBAC_SIDE_STREAMS", "1") != "0"     # A/B switch
+
+
+def side_streams(dev):
+    """(current stream, this device's side stream) for independent work forked off the
+    current stream and joined back (graph-capturable: event waits).  RGBAC_SIDE_STREAMS=0:
+    the side stream IS the current stream (no fork)."""
+    cur = torch.cuda.current_stream(dev)
+    if not SIDE:
+        return cur, cur
+    st = _SIDE_STREAMS.get(dev)
+    if st is None:
+        st = _SIDE_STREAMS[dev] = torch.cuda.Stream(device=dev)
+    return cur, st
+
+
 def pick_cout_pad(cout):
     """Packed weight rows per phase: every tile's N blocks stay inside the buffer."""
     return round_up(cout, 128)

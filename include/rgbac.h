@@ -422,7 +422,9 @@ int rgbac_weight_gather(int dtype, int64_t n, const float* src, const int32_t* i
 /* Many rgbac_weight_gather calls in one launch: tasks[5*t ..] = {src (const
  * float*), idx (const int32_t*), dst, n, dtype} as int64 in DEVICE memory;
  * task t owns blocks [blk0[t], blk0[t+1]) of 2048 elements (blk0 in device
- * memory, ntask + 1 entries, blk0[ntask] = nblk).                           */
+ * memory, ntask + 1 entries, blk0[ntask] = nblk).  dtype 16: a 16-byte chunk
+ * copy -- src / dst are arrays of 16-byte chunks, n counts chunks, idx[i] is
+ * the source chunk (< 0: zeros); a block owns 2048 chunks.                  */
 int rgbac_weight_gather_multi(int ntask, const int64_t* tasks, const int64_t* blk0, int64_t nblk,
                               void* stream);
 /* Per-channel sums over pixels into partial[nsplit][channels] (bias grads). */

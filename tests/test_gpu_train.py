@@ -1027,3 +1027,41 @@ def test_reduce_batch_matches_immediate_reductions():
         ag.REDUCE_BATCH = prev
     assert torch.equal(grads[False][0], grads[False][1])      # the step is deterministic
     assert torch.equal(grads[True][0], grads[False][0])
+
+
+def test_prefetch_frag_packs_equal_element_gather():
+    """prefetch_packs' two launches (plain packs + biases gathered from the fp32 parameters,
+    then the fragment-major copies as 16-byte chunk copies of the plain packs) give every
+    fragment-major training pack the same bits as a direct element gather through its own
+    index map (TPack.fidx), after a parameter update too."""
+    from rgbac import _lib
+    from rgbac import autograd as ag
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    g = _gen(72)
+    B, H, W = 2, 64, 64
+    x = (torch.randint(0, 256, (B, 3, H, W), generator=g).float() / 255).cuda()
+    a = torch.ones((B, 1, H, W)).cuda()
+    me = [t.cuda() for t in ref.supply_mask(a.cpu())]
+    torch.manual_seed(234)
+    net = AutoEncoder().cuda().train().set_compute_dtype(torch.bfloat16)
+    for step in range(3):
+        o = net(x, a, a, *me[:4])
+        (4096 * o[1] + o[2]).backward()
+        with torch.no_grad():
+            for p in net.parameters():
+                p.add_(torch.randn_like(p) * 1e-3)     # parameters move between steps
+    ag.prefetch_packs(net)
+    torch.cuda.synchronize()
+    n = 0
+    for m in net.modules():
+        for tc in m.__dict__.get("_rgbac_train", {}).values():
+            for tp in list(tc._fw.values()) + list(tc._bw.values()):
+                if tp.frag is None or tp.src is None:
+                    continue
+                want = torch.empty_like(tp.frag)
+                _lib.call("rgbac_weight_gather", _lib.dtype_code(want.dtype), want.numel(),
+                          tp.src[0], tp.fidx.data_ptr(), want.data_ptr(), _lib.stream_ptr())
+                torch.cuda.synchronize()
+                assert torch.equal(want.view(torch.int16), tp.frag.view(torch.int16))
+                n += 1
+    assert n > 10

@@ -57,7 +57,7 @@ def main():
         nbytes = B * H * H * C * 2 * (4 if kind == "gate" else 2)
         rows.append(f"{kind:5s} {H:4d}^2  {us:7.2f} us  {nbytes / us / 1e3:7.1f} GB/s (algorithmic "
                     f"{nbytes / 1e6:.1f} MB)")
-    tag = os.environ.get("RGBAC_PW2", "1")
+    tag = os.environ.get("RGBAC_PW2", "1") + ("all" if os.environ.get("RGBAC_PW2_ALL") == "1" else "")
     for r in rows:
         print(f"PW2={tag} {r}", flush=True)
 
