@@ -1452,13 +1452,14 @@ __global__ void __launch_bounds__(512, 4) conv_pw_kernel(const ConvArgsDev args)
 //     fragments have been consumed, so they overlap its epilogue and stores.
 // One 512-thread workgroup per CU (weights 72 KiB + 8 x 6 KiB tiles), persistent over tiles.
 // conv_pw2_kernel's epilogue for one pixel row (channels 16 j + 4 fq .. + 3), ACT fixed at
-// compile time (-1: no activation):
-// v = acc + bias + res0, act, + res2, bf16 store
+// compile time (-1: no activation), epilogue4_fin's order: v = acc + bias; the folded
+// activation backward (DGELU / DLRELU: v * act'(res0)) or v = SQBWD ? res0 + 2 res1 v :
+// v + res0; the pre-activation to zout (training forward); act; + res2; bf16 store.
 template <int NT, int ACT>
-__device__ __forceinline__ void pw2_epi(bf16_t* orow, const f32x4 (&acc)[NT], const float* bl,
-                                        const uint2 (&c0)[NT], const uint2 (&c1)[NT],
-                                        const uint2 (&c2)[NT], int fq, int cout, bool sel_on,
-                                        float act_param) {
+__device__ __forceinline__ void pw2_epi(bf16_t* orow, bf16_t* zrow, const f32x4 (&acc)[NT],
+                                        const float* bl, const uint2 (&c0)[NT],
+                                        const uint2 (&c1)[NT], const uint2 (&c2)[NT], int fq,
+                                        int cout, bool sel_on, float act_param) {
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     const int n = 16 * j + 4 * fq;
@@ -1472,7 +1473,19 @@ __device__ __forceinline__ void pw2_epi(bf16_t* orow, const f32x4 (&acc)[NT], co
     float v[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float x = acc[j][r] + bl[n + r] + r0[r];
+      float x = acc[j][r] + bl[n + r];
+      if constexpr (ACT == RGBAC_ACT_DGELU || ACT == RGBAC_ACT_DLRELU)
+        x = dact_apply<bf16_t>(ACT, act_param, x, r0[r]);
+      else if constexpr (ACT == RGBAC_ACT_SQBWD)
+        x = r0[r] + 2.0f * r1[r] * x;
+      else
+        x = x + r0[r];
+      v[r] = x;
+    }
+    if (zrow) Elem<bf16_t>::st4(zrow + n, v);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float x = v[r];
       if constexpr (ACT == RGBAC_ACT_GDN) x = gdn_t<bf16_t>(r1[r], x);
       else if constexpr (ACT == RGBAC_ACT_IGDN) x = igdn_t<bf16_t>(r1[r], x);
       else if constexpr (ACT == RGBAC_ACT_GATE) x = r1[r] * sigmoid_f(x);
@@ -1601,18 +1614,25 @@ __global__ void __launch_bounds__(512, 2) conv_pw2_kernel(const ConvArgsDev args
     }
     if (valid) {
       bf16_t* const orow = out + (long long)m * g.out_ldc + g.out_coff;
+      bf16_t* const zrow = g.zout ? reinterpret_cast<bf16_t*>(g.zout) + (long long)m * g.zld +
+                                        g.out_coff : nullptr;
       // one compile-time epilogue per activation (a per-element switch compiled to scalar
       // compare-and-branch chains: ~3,000 SALU per wave)
+#define PW2_EPI(A) pw2_epi<NT, A>(orow, zrow, acc, bl, c0, c1, c2, fq, cout, sel_on, s.act_param)
       switch (act) {
-        case RGBAC_ACT_GDN: pw2_epi<NT, RGBAC_ACT_GDN>(orow, acc, bl, c0, c1, c2, fq, cout, sel_on, s.act_param); break;
-        case RGBAC_ACT_IGDN: pw2_epi<NT, RGBAC_ACT_IGDN>(orow, acc, bl, c0, c1, c2, fq, cout, sel_on, s.act_param); break;
-        case RGBAC_ACT_GATE: pw2_epi<NT, RGBAC_ACT_GATE>(orow, acc, bl, c0, c1, c2, fq, cout, sel_on, s.act_param); break;
-        case RGBAC_ACT_GELU: pw2_epi<NT, RGBAC_ACT_GELU>(orow, acc, bl, c0, c1, c2, fq, cout, sel_on, s.act_param); break;
-        case RGBAC_ACT_MASKSEL: pw2_epi<NT, RGBAC_ACT_MASKSEL>(orow, acc, bl, c0, c1, c2, fq, cout, sel_on, s.act_param); break;
-        case RGBAC_ACT_RELU: pw2_epi<NT, RGBAC_ACT_RELU>(orow, acc, bl, c0, c1, c2, fq, cout, sel_on, s.act_param); break;
-        case RGBAC_ACT_LRELU: pw2_epi<NT, RGBAC_ACT_LRELU>(orow, acc, bl, c0, c1, c2, fq, cout, sel_on, s.act_param); break;
-        default: pw2_epi<NT, -1>(orow, acc, bl, c0, c1, c2, fq, cout, sel_on, s.act_param); break;
+        case RGBAC_ACT_GDN: PW2_EPI(RGBAC_ACT_GDN); break;
+        case RGBAC_ACT_IGDN: PW2_EPI(RGBAC_ACT_IGDN); break;
+        case RGBAC_ACT_GATE: PW2_EPI(RGBAC_ACT_GATE); break;
+        case RGBAC_ACT_GELU: PW2_EPI(RGBAC_ACT_GELU); break;
+        case RGBAC_ACT_MASKSEL: PW2_EPI(RGBAC_ACT_MASKSEL); break;
+        case RGBAC_ACT_RELU: PW2_EPI(RGBAC_ACT_RELU); break;
+        case RGBAC_ACT_LRELU: PW2_EPI(RGBAC_ACT_LRELU); break;
+        case RGBAC_ACT_SQBWD: PW2_EPI(RGBAC_ACT_SQBWD); break;
+        case RGBAC_ACT_DGELU: PW2_EPI(RGBAC_ACT_DGELU); break;
+        case RGBAC_ACT_DLRELU: PW2_EPI(RGBAC_ACT_DLRELU); break;
+        default: PW2_EPI(-1); break;
       }
+#undef PW2_EPI      }
     }
     if (nt < ntile) wait_vm<0>();
   }
@@ -1679,8 +1699,8 @@ static bool pw2_ok(const ConvArgsDev& d) {
     const char* e = getenv("RGBAC_PW2");
     return !(e && e[0] == '0');
   }();
-  if (!on || is_dact(d.s.act) || d.s.act == RGBAC_ACT_TANH_HALF || d.s.act == RGBAC_ACT_SQBWD ||
-      d.s.act == RGBAC_ACT_GAUSS || d.s.mode != RGBAC_CONV)
+  if (!on || d.s.act == RGBAC_ACT_TANH_HALF || d.s.act == RGBAC_ACT_GAUSS ||
+      d.s.mode != RGBAC_CONV)
     return false;
   // (multi-tile launches too: with the compile-time epilogue the 128^2 IGDN takes 38.0 us
   // here vs 44.5 us on conv_pw_kernel, same box; RGBAC_PW2_ALL=0 keeps those on the old one)
@@ -1691,7 +1711,7 @@ static bool pw2_ok(const ConvArgsDev& d) {
   if (!all && (long long)(d.s.M + 15) / 16 * d.s.ngroups > 8LL * 256) return false;
   for (int i = 0; i < d.s.ngroups; ++i) {
     const ConvGroup& g = d.g[i];
-    if (g.zout || g.cout % 8 || g.out_coff % 8 || g.out_ldc % 8 || g.cout > 192 ||
+    if ((g.zout && g.zld % 4) || g.cout % 8 || g.out_coff % 8 || g.out_ldc % 8 || g.cout > 192 ||
         (g.res0 && g.ld0 % 4) || (g.res1 && g.ld1 % 4) || (g.res2 && g.ld2 % 4))
       return false;
   }

@@ -480,10 +480,23 @@ def wgrad(G, S, ksize, stride, pad, square, k_pad, fmap, numel, nbias=0, bias_fr
     a.partial = part.data_ptr()
     a.bias_partial = None if bpart is None else bpart.data_ptr()
     st = _stream(G.t)
-    rt.timed("wgrad_kernel", 2.0 * M * G.ldc * ksize * ksize * cin,
+    # the launched form's rocprof name (the C side's choice, restated), so the bench's
+    # per-kernel table and training roofline keep the forms apart
+    if hs:
+        kname = f"wgrad_halo_kernel<{hs}>"
+    elif wgrad_patch_ok(G.t.dtype, G.ldc, S, ksize, stride, pad, square, G.H, G.W):
+        kname = f"wgrad_patch_kernel<{2 if G.ldc > 16 else 1}>"
+    elif G.t.dtype == torch.bfloat16 and not square and n_pad >= 128 and k_pad >= 512 and \
+            WGRAD_BIG:
+        kname = "wgrad_ring_kernel<4, 4, 3, 2, 4>"
+    elif G.t.dtype == torch.bfloat16 and not square:
+        kname = "wgrad_ring_kernel"
+    else:
+        kname = "wgrad_kernel"
+    rt.timed(kname, 2.0 * M * G.ldc * ksize * ksize * cin,
              G.t.element_size() * M * (G.ldc + cin * ksize * ksize // max(1, stride * stride)),
              lambda: _lib.call("rgbac_conv_wgrad", ctypes.byref(a), st),
-             f"wgrad_kernel k{ksize}s{stride} G{G.ldc}@{G.H}x{G.W} S{cin}@{s0.H}x{s0.W} "
+             f"{kname} k{ksize}s{stride} G{G.ldc}@{G.H}x{G.W} S{cin}@{s0.H}x{s0.W} "
              f"B{G.B} split{ns}{' sq' if square else ''}")
     acc = acc_dw is not None
     dw = acc_dw if acc else torch.empty(numel, dtype=_F32, device=dev)

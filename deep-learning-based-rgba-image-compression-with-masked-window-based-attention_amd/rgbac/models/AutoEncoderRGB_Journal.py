@@ -181,9 +181,8 @@ class AutoEncoder(_CompressionModelMixin, nn.Module):
         with torch.no_grad():
             x = input.contiguous().float()
             # reconmask = round(reconmask*255)/255 ; md1..md4 = DecMakeMask(reconmask)  (:212-215):
-            # only the decoder reads md, so the pyramid runs on a side stream beside the
-            # encoder and the entropy model (its launch is one latency-bound round of 128
-            # workgroups, ~18 us on the critical path otherwise)
+            # only the decoder reads md, so the pyramid may run on a side stream beside the
+            # encoder (rt.side_streams; off by default: the fork / join measured slower)
             main, side = rt.side_streams(x.device)
             side.wait_stream(main)
             with torch.cuda.stream(side):

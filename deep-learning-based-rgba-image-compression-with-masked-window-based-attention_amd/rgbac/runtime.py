@@ -267,7 +267,10 @@ WINBLOCK4_FUSED = os.environ.get("RGBAC_WINBLOCK4", "1") != "0"  # ws-4 / C-80 b
 
 
 _SIDE_STREAMS = {}
-SIDE = os.environ.get("RGBAC_SIDE_STREAMS", "1") != "0"     # A/B switch
+# measured slower on the config-2 forward graph (same box, interleaved: 1,796 / 1,794 us with the
+# decoder's mask pyramid and x_hat conversion forked off vs 1,772 / 1,775 us without; the
+# event waits of the fork / join cost more than the hidden ~18 us): opt-in
+SIDE = os.environ.get("RGBAC_SIDE_STREAMS", "0") == "1"
 
 
 def side_streams(dev):

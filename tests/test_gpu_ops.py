@@ -441,7 +441,10 @@ def test_conv_smallk_tile(device, cin, cout, k, s, act):
 @pytest.mark.parametrize("cin,cout,kind", [(192, 192, "gelu"), (3, 32, "none"), (32, 3, "none"),
                                            (80, 40, "gelu"), (96, 80, "none"), (192, 100, "relu"),
                                            (192, 192, "gdn"), (192, 192, "igdn"), (80, 80, "igdn"),
-                                           (192, 192, "gate"), (192, 192, "masksel")])
+                                           (192, 192, "gate"), (192, 192, "masksel"),
+                                           (192, 192, "gdn_zout"), (192, 192, "sqbwd"),
+                                           (192, 192, "dgelu"), (96, 96, "dlrelu"),
+                                           (192, 192, "gelu_zout")])
 def test_conv_pw_tile(device, cin, cout, kind):
     """The full-width pointwise tile (54, bf16): every output channel of a 16-pixel tile in one
     wave, the res1 operand prefetched.  Against the small-K tile on the model's 1x1 epilogues
@@ -471,9 +474,23 @@ def test_conv_pw_tile(device, cin, cout, kind):
         rt.FORCE = (tile, 1)
         try:
             with torch.no_grad():
-                if kind in ("gdn", "igdn"):
+                zo = None
+                if kind.endswith("_zout"):
+                    zo = rt.new_feat(B, H, W, cout, dt, device)
+                if kind in ("gdn", "igdn", "gdn_zout"):
                     pk = rt.packed(md, dt, [(cin, rt.round_up(cin, 8))])
-                    o = rt.conv(pk, [fx.src()], square=True, act=kind, res1=fx)
+                    o = rt.conv(pk, [fx.src()], square=True, act=kind.split("_")[0], res1=fx,
+                                zout=zo)
+                elif kind == "gelu_zout":
+                    pk = rt.packed(md, dt, [(cin, rt.round_up(cin, 8))])
+                    o = rt.conv(pk, [fx.src()], act="gelu", res0=fr, zout=zo)
+                elif kind == "sqbwd":              # GDN input gradient: res0 + 2 x (W^T g)
+                    pk = rt.packed(md, dt, [(cin, rt.round_up(cin, 8))])
+                    o = rt.conv(pk, [fx.src()], act="sqbwd", res0=fr, res1=fa, bias=False)
+                elif kind in ("dgelu", "dlrelu"):  # folded activation backward, res0 = z
+                    pk = rt.packed(md, dt, [(cin, rt.round_up(cin, 8))])
+                    o = rt.conv(pk, [fx.src()], act=kind, act_param=0.2 if kind == "dlrelu" else 0.0,
+                                res0=fa, bias=False)
                 elif kind == "gate":
                     pk = rt.packed(md, dt, [(cin, rt.round_up(cin, 8))])
                     o = rt.conv(pk, [fx.src()], act="gate", res1=fa, res2=fr)
@@ -483,9 +500,13 @@ def test_conv_pw_tile(device, cin, cout, kind):
                 else:
                     o = run_conv(md, [fx.src()], act=kind, res0=fr)
             outs[tile] = rt.to_nchw(o).float().cpu()
+            if zo is not None:
+                outs[(tile, "z")] = rt.to_nchw(zo).float().cpu()
         finally:
             rt.FORCE = None
     assert rel(outs[rt.TILE_PW], outs[rt.TILE_SMALLK]) < 1e-2, kind
+    if kind.endswith("_zout"):
+        assert rel(outs[(rt.TILE_PW, "z")], outs[(rt.TILE_SMALLK, "z")]) < 1e-2, kind
     if kind in ("gelu", "none", "relu"):
         f = {"gelu": F.gelu, "relu": F.relu, "none": lambda t: t}[kind]
         xb = x.to(dt).float()
