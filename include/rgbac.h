@@ -192,6 +192,58 @@ int rgbac_winattn_core_ex(int dtype, int batch, int h, int w, int channels,
                           const float* bias, void* out, int64_t ldo, uint8_t* sel,
                           const float* amask, int amask_nw, int hpb, void* stream);
 
+/* Slice-chain conv with the chain's narrow tail conv folded in (bf16 inference; csrc/fold.hip).
+ * The slice stacks of models/AutoEncoderRGB_Journal.py:240-264 end in narrow 128 -> 8 3x3
+ * convs (cc_mean_transforms[i][4] -> mu, lrp_transforms[i][4] -> the tanh update) whose
+ * 8 output channels are the LAST 8 input channels of the next wide conv: lrp_transforms[i][0]
+ * reads [means, y_hat_<i, y_hat_i^pre] (:260-262, y_hat_i^pre = round(y_i - mu_i) + mu_i,
+ * :255-257) and cc_*_transforms[i+1][0] reads [means|scales, y_hat_<=i] (:241-252).  Each
+ * workgroup of this launch recomputes the narrow conv for its own (4+2) x (16+2) patch
+ * (K split over its 4 waves, from a (4+4) x (16+4) halo of the narrow conv's 128-channel
+ * input in LDS) and writes the 8 values straight into its patch of the wide conv's input:
+ *   RGBAC_FOLD_GAUSS: value = rint(y - mu) + mu,  mu = conv(pin) + pbias,  aux = y_i
+ *   RGBAC_FOLD_TANH:  value = aux + 0.5 * tanh(conv(pin) + pbias),        aux = pre_i
+ * (zero outside the image: the wide conv's padding).  The wide conv (3x3 stride 1, GELU) then
+ * runs on [src0, src1, value] with its fragment-major pack (see rgbac_conv_args.tile).
+ * Groups with ``writer`` also store the folded value of their own pixels to ``put`` (GAUSS:
+ * y_hat_i^pre, the lrp residual; TANH: y_hat_i into the decoder input) and, GAUSS, the fp32
+ * mu to ``mu`` (read back by rgbac_gauss_bits): with several groups folding the same narrow
+ * conv exactly one of them is the writer. */
+enum rgbac_fold_mode { RGBAC_FOLD_GAUSS = 1, RGBAC_FOLD_TANH = 2 };
+typedef struct rgbac_fold_group {
+  rgbac_src src[2];            /* wide-conv input channels [0, c0) (src[1].channels may be 0) */
+  int32_t c0;                  /* folded channels [c0, c0 + 8); c0 + 8 = the pack's cin_pad */
+  int32_t cout;                /* wide-conv output channels (multiple of 4)                 */
+  const void* weight;          /* fragment-major copy of the wide conv's pack, bf16         */
+  const float* bias;
+  void* out; int64_t out_ldc; int32_t out_coff; int32_t writer;
+  const void* pin; int64_t pin_ldc;          /* narrow conv input: 128 channels, NHWC    */
+  const void* pweight;         /* fragment-major copy of the narrow conv's pack (128 -> 8)   */
+  const float* pbias;          /* >= 16 entries (the pack's zero-padded bias)                */
+  const void* aux; int64_t aux_ldc;          /* GAUSS: y_i; TANH: y_hat_i^pre (8 ch)     */
+  float* mu; int64_t mu_ldc;                 /* GAUSS writer: fp32 mu out                */
+  void* put; int64_t put_ldc;                /* writer: the folded value, 8 channels     */
+} rgbac_fold_group;
+/* ngroups in 1..12 share batch / h / w (h % 4 == 0, w % 16 == 0), the mode and ceil((c0 + 8)
+ * / 32) (3 or 4); bn = 64 or 128 output channels per workgroup. */
+int rgbac_conv_fold(const rgbac_fold_group* groups, int ngroups, int batch, int h, int w,
+                    int mode, int bn, void* stream);
+
+/* The bits of slices whose quantisation ran folded (RGBAC_FOLD_GAUSS): per group the sigma
+ * conv (cc_scale_transforms[i][4], 128 -> 8, 3x3) over ``pin`` and the GaussianConditional
+ * likelihood of y_hat = rint(y - mu) + mu with the stored mu (as rgbac_gaussian_slice,
+ * eval mode); partial[t] = the fp64 bits of 64-pixel tile t (4 x 16 pixels, tiles in
+ * (batch, row, column) order). */
+typedef struct rgbac_bits_group {
+  const void* pin; int64_t pin_ldc;
+  const void* pweight; const float* pbias;
+  const void* y; int64_t y_ldc;
+  const float* mu; int64_t mu_ldc;
+  double* partial;
+} rgbac_bits_group;
+int rgbac_gauss_bits(const rgbac_bits_group* groups, int ngroups, int batch, int h, int w,
+                     void* stream);
+
 /* compressai GaussianConditional.forward + ste_round for one channel slice
  * (models/AutoEncoderRGB_Journal.py:255-257, bits :280):
  *   out_hat = round(y - mu) + mu   (torch.round: half to even)

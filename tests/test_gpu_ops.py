@@ -461,7 +461,7 @@ def test_conv_pw_tile(device, cin, cout, kind):
     dt = torch.bfloat16
     m = nn.Conv2d(cin, cout, 1)
     with torch.no_grad():
-        if kind in ("gdn", "igdn"):
+        if kind in ("gdn", "igdn", "gdn_zout"):
             m.weight.copy_(0.1 * torch.rand(cout, cin, 1, 1, generator=g))
             m.bias.copy_(0.5 + torch.rand(cout, generator=g))
     md = m.to(device)
