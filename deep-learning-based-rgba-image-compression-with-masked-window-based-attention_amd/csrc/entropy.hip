@@ -133,7 +133,10 @@ eb_forward_kernel(long long n, int C, const T* __restrict__ z, long long ldz,
 template <typename T>
 __global__ void __launch_bounds__(256)
 mse_partial_kernel(int mode, int cx, int HW, const float* __restrict__ x, const T* __restrict__ xh,
-                   long long ldh, const float* __restrict__ mask, double* __restrict__ part) {
+                   long long ldh, const float* __restrict__ mask, double* __restrict__ part,
+                   float* __restrict__ xo, int vec) {
+  // xo (or null): x_hat's fp32 NCHW copy, written from the same reads (rgbac_finalize_ex).
+  // vec (cx <= 4, vector-aligned rows): the pixel's channels arrive in one vector load.
   __shared__ double red[4];
   const int b = blockIdx.y;
   double se = 0.0, cnt = 0.0;
@@ -141,11 +144,20 @@ mse_partial_kernel(int mode, int cx, int HW, const float* __restrict__ x, const 
     const long long pix = (long long)b * HW + p;
     float m = 1.0f;
     if (mode == 0) m = mask[pix] > 0.0f ? 1.0f : 0.0f;
-    for (int c = 0; c < cx; ++c) {
+    auto term = [&](int c, float hv) {
       const float xv = x[((long long)b * cx + c) * HW + p];
-      const float hv = Elem<T>::ld(xh + pix * ldh + c);
+      if (xo) xo[((long long)b * cx + c) * HW + p] = hv;
       const float dlt = mode == 0 ? (xv * m - hv * m) : (hv - xv);
       se += (double)(dlt * dlt);
+    };
+    if (vec) {
+      float hq[4];
+      Elem<T>::ld4(xh + pix * ldh, hq);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (c < cx) term(c, hq[c]);
+    } else {
+      for (int c = 0; c < cx; ++c) term(c, Elem<T>::ld(xh + pix * ldh + c));
     }
     cnt += (double)(m * cx);
   }
@@ -255,8 +267,9 @@ __global__ void __launch_bounds__(256) pyramid_kernel(int batch, int H, int W,
                                                       const float* __restrict__ alpha,
                                                       int round255, float* __restrict__ rounded,
                                                       PyrOuts outs) {
-  constexpr int TP = 64 >> L;                          // last-level tile: 32 / 16 / 8 / 4
-  constexpr int N0 = (TP + 1) * (1 << L) - 1;          // level-0 region side (65 .. 79)
+  constexpr int TP = 32 >> L;                          // last-level tile: 16 / 8 / 4 / 2
+  constexpr int N0 = (TP + 1) * (1 << L) - 1;          // level-0 region side (33 .. 47)
+  constexpr int NL0 = (N0 * N0 + 255) / 256;           // level-0 elements per thread
   extern __shared__ float pyr[];
   float* bufA = pyr;
   float* bufB = pyr + N0 * N0;
@@ -273,18 +286,29 @@ __global__ void __launch_bounds__(256) pyramid_kernel(int batch, int H, int W,
   const int s0 = 1 << L;
   const int ry = ty * TP * s0 - (s0 - 1), rx = tx * TP * s0 - (s0 - 1);
   const float* ab = alpha + (long long)b * H * W;
-  for (int e = threadIdx.x; e < N0 * N0; e += 256) {
+  // every load of the thread first (one memory round trip, not NL0 dependent ones), then the
+  // rounding, the owned-core stores and the LDS image
+  float v0[NL0];
+#pragma unroll
+  for (int k = 0; k < NL0; ++k) {
+    const int e = threadIdx.x + 256 * k;
     const int i = e / N0, j = e - (e / N0) * N0;
     const int y = ry + i, x = rx + j;
-    float v = 0.0f;
-    if (y >= 0 && y < H && x >= 0 && x < W) {
-      v = ab[(long long)y * W + x];
-      if (round255) {
-        v = rintf(v * 255.0f) / 255.0f;
-        // core rows / cols of level 0 owned by this tile
-        if (i >= s0 - 1 && i < s0 - 1 + TP * s0 && j >= s0 - 1 && j < s0 - 1 + TP * s0)
-          rounded[((long long)b * H + y) * W + x] = v;
-      }
+    const bool in = e < N0 * N0 && y >= 0 && y < H && x >= 0 && x < W;
+    v0[k] = in ? ab[(long long)y * W + x] : 0.0f;
+  }
+#pragma unroll
+  for (int k = 0; k < NL0; ++k) {
+    const int e = threadIdx.x + 256 * k;
+    if (e >= N0 * N0) break;
+    const int i = e / N0, j = e - (e / N0) * N0;
+    const int y = ry + i, x = rx + j;
+    float v = v0[k];
+    if (round255 && y >= 0 && y < H && x >= 0 && x < W) {
+      v = rintf(v * 255.0f) / 255.0f;
+      // core rows / cols of level 0 owned by this tile
+      if (i >= s0 - 1 && i < s0 - 1 + TP * s0 && j >= s0 - 1 && j < s0 - 1 + TP * s0)
+        rounded[((long long)b * H + y) * W + x] = v;
     }
     bufA[e] = v;
   }
@@ -342,6 +366,63 @@ __global__ void nhwc_to_nchw_kernel(int batch, int C, int HW, const T* __restric
     const int c = (int)(t % C);
     const int b = (int)(t / C);
     dst[i] = Elem<T>::ld(src + ((long long)b * HW + p) * ldc + c);
+  }
+}
+
+// One thread per (pixel, 16-byte chunk of the NHWC row): the reads of a channel plane are
+// coalesced over consecutive pixels, the row chunk goes out as one 16-byte store, and the
+// indices are 32-bit (the grid-stride form above divides 64-bit indices per element).
+template <typename T>
+__global__ void __launch_bounds__(256) nchw_to_nhwc_chunk_kernel(int n, int nck, int C, int HW,
+                                                                 const float* __restrict__ src,
+                                                                 T* __restrict__ dst, int ldc) {
+  constexpr int E = Elem<T>::EPV;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int pix = i / nck, ck = i - (i / nck) * nck;
+  const int b = pix / HW, p = pix - (pix / HW) * HW;
+  float v[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int c = ck * E + e;
+    v[e] = c < C ? src[((long long)b * C + c) * HW + p] : 0.0f;
+  }
+  T* o = dst + (long long)pix * ldc + ck * E;
+  if constexpr (E == 8) {
+    uint4 q;
+    q.x = pack_bf16x2(v[0], v[1]); q.y = pack_bf16x2(v[2], v[3]);
+    q.z = pack_bf16x2(v[4], v[5]); q.w = pack_bf16x2(v[6], v[7]);
+    *reinterpret_cast<uint4*>(o) = q;
+  } else {
+    *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+// One thread per pixel: its NHWC row read in 16-byte chunks, each channel written to its plane
+// (coalesced over consecutive pixels).
+template <typename T>
+__global__ void __launch_bounds__(256) nhwc_to_nchw_px_kernel(int npix, int C, int HW,
+                                                              const T* __restrict__ src, int ldc,
+                                                              float* __restrict__ dst) {
+  constexpr int E = Elem<T>::EPV;
+  const int pix = blockIdx.x * 256 + threadIdx.x;
+  if (pix >= npix) return;
+  const int b = pix / HW, p = pix - (pix / HW) * HW;
+  const T* row = src + (long long)pix * ldc;
+  for (int c0 = 0; c0 < C; c0 += E) {
+    const uint4 q = *reinterpret_cast<const uint4*>(row + c0);
+    float v[E];
+    if constexpr (E == 8) {
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { v[2 * k] = bf2f(w[k] & 0xFFFF); v[2 * k + 1] = bf2f(w[k] >> 16); }
+    } else {
+      v[0] = __uint_as_float(q.x); v[1] = __uint_as_float(q.y);
+      v[2] = __uint_as_float(q.z); v[3] = __uint_as_float(q.w);
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e)
+      if (c0 + e < C) dst[((long long)b * C + c0 + e) * HW + p] = v[e];
   }
 }
 
@@ -403,20 +484,32 @@ extern "C" int rgbac_finalize(int dtype, int mode, int batch, int cx, int h, int
                               const void* x_hat, int64_t ldh, const float* mask,
                               const double* ybits, int ny, const double* zbits, int nz,
                               double* scratch, float* out, void* stream) {
+  return rgbac_finalize_ex(dtype, mode, batch, cx, h, w, x, x_hat, ldh, mask, ybits, ny, zbits,
+                           nz, scratch, out, nullptr, stream);
+}
+
+extern "C" int rgbac_finalize_ex(int dtype, int mode, int batch, int cx, int h, int w,
+                                 const float* x, const void* x_hat, int64_t ldh,
+                                 const float* mask, const double* ybits, int ny,
+                                 const double* zbits, int nz, double* scratch, float* out,
+                                 float* x_hat_nchw, void* stream) {
   RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
   RGBAC_REQUIRE(mode == 0 || mode == 1, "mode");
   RGBAC_REQUIRE(batch > 0 && cx > 0 && h > 0 && w > 0, "shape");
   RGBAC_REQUIRE(x && x_hat && scratch && out && ybits && zbits, "null pointer");
   RGBAC_REQUIRE(mode == 1 || mask, "masked mse needs the mask");
+  RGBAC_REQUIRE(ldh >= cx, "ldh");
+  const int vec = cx <= 4 && ldh % 4 == 0 &&
+                  ((uintptr_t)x_hat % (dtype == RGBAC_F32 ? 16 : 8)) == 0;
   const int HW = h * w;
   const int nblk = 64;  // scratch must hold batch * 64 * 2 doubles
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (dtype == RGBAC_F32)
     hipLaunchKernelGGL(mse_partial_kernel<float>, dim3(nblk, batch), dim3(256), 0, st, mode, cx,
-                       HW, x, (const float*)x_hat, ldh, mask, scratch);
+                       HW, x, (const float*)x_hat, ldh, mask, scratch, x_hat_nchw, vec);
   else
     hipLaunchKernelGGL(mse_partial_kernel<bf16_t>, dim3(nblk, batch), dim3(256), 0, st, mode, cx,
-                       HW, x, (const bf16_t*)x_hat, ldh, mask, scratch);
+                       HW, x, (const bf16_t*)x_hat, ldh, mask, scratch, x_hat_nchw, vec);
   int rc = check_launch("mse_partial_kernel");
   if (rc) return rc;
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, st, mode, batch, nblk,
@@ -440,7 +533,7 @@ extern "C" int rgbac_mask_pyramid(int batch, int h, int w, const float* alpha, i
     for (int l = 0; l < levels; ++l) po.p[l] = outs[l];
     int hl = h, wl = w;
     for (int l = 0; l < levels; ++l) { hl = (hl - 1) / 2 + 1; wl = (wl - 1) / 2 + 1; }
-    const int tp = 64 >> levels;
+    const int tp = 32 >> levels;
     const long long nblk = (long long)batch * ((hl + tp - 1) / tp) * ((wl + tp - 1) / tp);
     RGBAC_REQUIRE(nblk < (1ll << 31), "too many pyramid tiles");
     const int n0 = (tp + 1) * (1 << levels) - 1;
@@ -483,6 +576,18 @@ extern "C" int rgbac_nchw_to_nhwc(int dtype, int batch, int c, int h, int w, con
   RGBAC_REQUIRE(batch > 0 && c > 0 && h > 0 && w > 0 && ldc >= c && src && dst, "shape");
   const long long n = (long long)batch * h * w * ldc;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int E = dtype == RGBAC_F32 ? 4 : 8;
+  if (ldc % E == 0 && ((uintptr_t)dst & 15) == 0 && n / E < (1ll << 31) - 256) {
+    const int nck = (int)(ldc / E), nn = (int)(n / E);
+    const dim3 grid((unsigned)((nn + 255) / 256));
+    if (dtype == RGBAC_F32)
+      hipLaunchKernelGGL(nchw_to_nhwc_chunk_kernel<float>, grid, dim3(256), 0, st, nn, nck, c,
+                         h * w, src, (float*)dst, (int)ldc);
+    else
+      hipLaunchKernelGGL(nchw_to_nhwc_chunk_kernel<bf16_t>, grid, dim3(256), 0, st, nn, nck, c,
+                         h * w, src, (bf16_t*)dst, (int)ldc);
+    return check_launch("nchw_to_nhwc_chunk_kernel");
+  }
   if (dtype == RGBAC_F32)
     hipLaunchKernelGGL(nchw_to_nhwc_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, batch, c,
                        h * w, src, (float*)dst, ldc);
@@ -498,6 +603,19 @@ extern "C" int rgbac_nhwc_to_nchw(int dtype, int batch, int c, int h, int w, con
   RGBAC_REQUIRE(batch > 0 && c > 0 && h > 0 && w > 0 && ldc >= c && src && dst, "shape");
   const long long n = (long long)batch * h * w * c;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int E = dtype == RGBAC_F32 ? 4 : 8;
+  const long long npix = (long long)batch * h * w;
+  if (ldc % E == 0 && ((uintptr_t)src & 15) == 0 && npix < (1ll << 31) - 256 &&
+      npix * ldc < (1ll << 40)) {
+    const dim3 grid((unsigned)((npix + 255) / 256));
+    if (dtype == RGBAC_F32)
+      hipLaunchKernelGGL(nhwc_to_nchw_px_kernel<float>, grid, dim3(256), 0, st, (int)npix, c,
+                         h * w, (const float*)src, (int)ldc, dst);
+    else
+      hipLaunchKernelGGL(nhwc_to_nchw_px_kernel<bf16_t>, grid, dim3(256), 0, st, (int)npix, c,
+                         h * w, (const bf16_t*)src, (int)ldc, dst);
+    return check_launch("nhwc_to_nchw_px_kernel");
+  }
   if (dtype == RGBAC_F32)
     hipLaunchKernelGGL(nhwc_to_nchw_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, batch, c,
                        h * w, (const float*)src, ldc, dst);

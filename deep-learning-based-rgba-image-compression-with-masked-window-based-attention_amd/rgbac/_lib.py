@@ -139,6 +139,8 @@ SIGNATURES = {
     "rgbac_reduce_blocks": [_I64],
     "rgbac_finalize": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP, _VP, _I32,
                        _VP, _I32, _VP, _VP, _VP],
+    "rgbac_finalize_ex": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP, _VP, _I32,
+                          _VP, _I32, _VP, _VP, _VP, _VP],
     "rgbac_mask_pyramid": [_I32, _I32, _I32, _VP, _I32, _VP, _I32, _VP, _VP],
     "rgbac_nchw_to_nhwc": [_I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP],
     "rgbac_nhwc_to_nchw": [_I32, _I32, _I32, _I32, _I32, _VP, _I64, _VP, _VP],

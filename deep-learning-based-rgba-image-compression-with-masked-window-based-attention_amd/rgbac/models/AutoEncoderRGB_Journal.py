@@ -113,16 +113,17 @@ def _hyper_analysis(M):
                          conv3x3(224, 192, stride=2))
 
 
-def finalize(mode, x, x_hat, mask, ypart, zpart):
-    """rgbac_finalize -> fp32 [mse, bpp, y_bpp, z_bpp] on device."""
+def finalize(mode, x, x_hat, mask, ypart, zpart, x_hat_nchw=None):
+    """rgbac_finalize_ex -> fp32 [mse, bpp, y_bpp, z_bpp] on device; with ``x_hat_nchw`` (fp32
+    [B, cx, H, W]) the same pass also writes x_hat's NCHW copy."""
     B, cx, H, W = x.shape
     dev = x.device
     scratch = torch.empty(B * 64 * 2, dtype=torch.float64, device=dev)
     out = torch.empty(4, dtype=torch.float32, device=dev)
-    _lib.call("rgbac_finalize", _lib.dtype_code(x_hat.t.dtype), mode, B, cx, H, W,
+    _lib.call("rgbac_finalize_ex", _lib.dtype_code(x_hat.t.dtype), mode, B, cx, H, W,
               x.data_ptr(), x_hat.ptr(), x_hat.ldc, _lib.ptr(mask), ypart.data_ptr(),
               ypart.numel(), zpart.data_ptr(), zpart.numel(), scratch.data_ptr(),
-              out.data_ptr(), _lib.stream_ptr(dev))
+              out.data_ptr(), _lib.ptr(x_hat_nchw), _lib.stream_ptr(dev))
     return out
 
 
@@ -194,13 +195,10 @@ class AutoEncoder(_CompressionModelMixin, nn.Module):
             yh, ypart, zpart = latent_path(self, y, self.training, noise_z, noise_y, debug)
             main.wait_stream(side)
             xh = self.Decoder.nhwc(yh, md[1], md[2])                              # :273
-            # x_hat's NCHW copy beside the loss / bits reduction
-            side.wait_stream(main)
-            with torch.cuda.stream(side):
-                x_hat = rt.to_nchw(xh)
-            x_hat.record_stream(main)
-            out = finalize(0, x, xh, mask.contiguous().float(), ypart, zpart)    # :280-295
-            main.wait_stream(side)
+            # x_hat's NCHW copy written by the loss pass itself (one read of x_hat)
+            x_hat = torch.empty((B, xh.C, H, W), dtype=torch.float32, device=x.device)
+            out = finalize(0, x, xh, mask.contiguous().float(), ypart, zpart,     # :280-295
+                           x_hat_nchw=x_hat)
         if debug is not None:
             debug.update(y=y)
         return x_hat, out[0], out[1], out[2], out[3]

@@ -282,6 +282,14 @@ int rgbac_finalize(int dtype, int mode, int batch, int cx, int h, int w,
                    const float* mask, const double* ybits, int ny,
                    const double* zbits, int nz, double* scratch, float* out,
                    void* stream);
+/* The same, also writing x_hat's fp32 NCHW copy [B,cx,H,W] (the forward's returned x_hat,
+ * otherwise a separate rgbac_nhwc_to_nchw) from the reads the MSE pass makes anyway;
+ * x_hat_nchw may be NULL (== rgbac_finalize). */
+int rgbac_finalize_ex(int dtype, int mode, int batch, int cx, int h, int w,
+                      const float* x, const void* x_hat, int64_t ldh,
+                      const float* mask, const double* ybits, int ny,
+                      const double* zbits, int nz, double* scratch, float* out,
+                      float* x_hat_nchw, void* stream);
 
 /* SupplyMaskToTransform (layers/SupplyMask.py:11-18): ``levels`` successive
  * AvgPool2d(3, s2, p1, count_include_pad) of fp32 [B,H,W]; if round255, the

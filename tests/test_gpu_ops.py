@@ -729,3 +729,49 @@ def test_conv_patch_tiles(device, mode, cin, cout, H, W):
     for t, got in outs.items():
         assert got.shape == want.shape
         assert rel(got, want) < 1e-2, (t, rel(got, want))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("C,ldc", [(3, 8), (3, 16), (80, 80), (13, 24)])
+def test_layout_conversions(device, dtype, C, ldc):
+    """rgbac_nchw_to_nhwc / rgbac_nhwc_to_nchw (the per-chunk / per-pixel kernels): exact round
+    trip of dtype-representable values, zero padding channels, ragged pixel counts."""
+    rt = _rt()
+    g = _gen(77 + C + ldc)
+    B, H, W = 3, 17, 23
+    x = torch.randn((B, C, H, W), generator=g).to(dtype).float().to(device)
+    f = rt.to_nhwc(x, dtype, ldc=ldc)
+    assert f.ldc == ldc
+    t = f.t.float()
+    assert torch.equal(t[..., :C].permute(0, 3, 1, 2), x)
+    assert (t[..., C:] == 0).all()
+    back = rt.to_nchw(f)
+    assert torch.equal(back, x)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_finalize_writes_xhat_nchw(device, dtype):
+    """rgbac_finalize_ex: the x_hat NCHW copy it writes equals rgbac_nhwc_to_nchw, and the
+    loss / bpp scalars equal rgbac_finalize's (same pass, same order)."""
+    rt = _rt()
+    from rgbac import _lib
+    from rgbac.models.AutoEncoderRGB_Journal import finalize
+    g = _gen(5)
+    B, H, W = 2, 32, 48
+    x = torch.rand((B, 3, H, W), generator=g).to(device)
+    xh = rt.to_nhwc(torch.rand((B, 3, H, W), generator=g).to(device), dtype)
+    mask = (torch.rand((B, 1, H, W), generator=g) > 0.3).float().to(device)
+    yp = torch.rand(64, generator=g, dtype=torch.float64).to(device)
+    zp = torch.rand(16, generator=g, dtype=torch.float64).to(device)
+    xo = torch.full((B, 3, H, W), 5.0, device=device)
+    a = finalize(0, x, xh, mask, yp, zp, x_hat_nchw=xo)
+    scratch = torch.empty(B * 64 * 2, dtype=torch.float64, device=device)
+    b = torch.empty(4, dtype=torch.float32, device=device)
+    _lib.call("rgbac_finalize", _lib.dtype_code(dtype), 0, B, 3, H, W, x.data_ptr(), xh.ptr(),
+              xh.ldc, mask.data_ptr(), yp.data_ptr(), yp.numel(), zp.data_ptr(), zp.numel(),
+              scratch.data_ptr(), b.data_ptr(), _lib.stream_ptr(device))
+    assert torch.equal(a, b)
+    assert torch.equal(xo, rt.to_nchw(xh))
+    m = (mask > 0).float()
+    want = (((x * m - xo * m) ** 2).sum((1, 2, 3)) / (3 * m.sum((1, 2, 3))).clamp_min(1)).mean()
+    assert abs(a[0].item() - want.item()) <= 1e-5 * max(want.item(), 1e-6)

@@ -32,6 +32,11 @@ SHAPES = [
     ("hs 256->288 g2 16x16", [256], 288, 3, 16, 16, 8, 2, "conv"),
     ("hs subpel 288->80 g2 16x16", [288], 80, 3, 16, 16, 8, 2, "subpel"),
     ("ha 320->288 16x16", [320], 288, 3, 16, 16, 8, 1, "conv"),
+    # the strided analysis / synthesis convs (5x5 stride 2; TransformRGB.py:57-58, 83-84)
+    ("5x5s2 E.x2 192 128^2", [192], 192, 5, 128, 128, 8, 1, "s2"),
+    ("5x5s2 E.x3 192 64^2", [192], 192, 5, 64, 64, 8, 1, "s2"),
+    ("5x5s2 D.x2 convT 192 32^2", [192], 192, 5, 32, 32, 8, 1, "convT"),
+    ("5x5s2 D.x3 convT 192 64^2", [192], 192, 5, 64, 64, 8, 1, "convT"),
 ]
 
 
@@ -48,8 +53,15 @@ def main():
         preps = []
         for gi in range(G):
             torch.manual_seed(gi)
-            m = (subpel_conv3x3(sum(cins), cout, 2) if kind == "subpel"
-                 else nn.Conv2d(sum(cins), cout, k, padding=k // 2)).to(dev)
+            if kind == "subpel":
+                m = subpel_conv3x3(sum(cins), cout, 2)
+            elif kind == "convT":
+                m = nn.ConvTranspose2d(sum(cins), cout, k, stride=2, padding=k // 2,
+                                       output_padding=1)
+            else:
+                m = nn.Conv2d(sum(cins), cout, k, stride=2 if kind == "s2" else 1,
+                              padding=k // 2)
+            m = m.to(dev)
             if kind in ("gdn", "igdn"):
                 with torch.no_grad():
                     m.weight.uniform_(0, 0.01)
