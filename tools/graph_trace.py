@@ -30,7 +30,8 @@ def run(args):
         with torch.no_grad():
             return net(x, a, a, *me)
     from rgbac import runtime as rt
-    cache = os.path.join(ROOT, "profiles", f"tune_fwd_bf16_b{args.batch}_{args.size}.json")
+    cache = os.environ.get("RGBAC_TUNE_CACHE") or os.path.join(
+        ROOT, "profiles", f"tune_fwd_bf16_b{args.batch}_{args.size}.json")
     if os.path.exists(cache):
         rt.load_tune_cache(cache)        # no autotuning dispatches in the trace
     step()
