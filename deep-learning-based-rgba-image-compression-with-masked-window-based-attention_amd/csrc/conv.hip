@@ -1758,12 +1758,21 @@ __global__ void __launch_bounds__(512) conv_npatch_kernel(const ConvArgsDev args
   __shared__ double wsum[TM];
   WG_T(0);
   const ConvShared& s = args.s;
-  const ConvGroup& g = args.g[blockIdx.z];
+  int tsp = blockIdx.x, gi = blockIdx.z;         // spatial tile (the GAUSS partial's slot), group
+  {
+    int sp, g_, nb_;
+    if (s.remap == 2 && xcd_spatial(blockIdx.x + gridDim.x * blockIdx.z, gridDim.x, gridDim.z, 1,
+                                    sp, g_, nb_)) {
+      tsp = sp;
+      gi = g_;
+    }
+  }
+  const ConvGroup& g = args.g[gi];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
   const int txn = s.Wm / TW, tyn = s.Hm / TH;
-  int t = blockIdx.x;
+  int t = tsp;
   const int txi = t % txn; t /= txn;
   const int tyi = t % tyn;
   const int b = t / tyn;
@@ -1939,7 +1948,7 @@ __global__ void __launch_bounds__(512) conv_npatch_kernel(const ConvArgsDev args
     for (int o = 32; o > 0; o >>= 1) bits += __shfl_xor(bits, o);
     if (wave < TM && lane == 0) wsum[wave] = bits;
     __syncthreads();
-    if (tid == 0) g.partial[blockIdx.x] = ((wsum[0] + wsum[1]) + wsum[2]) + wsum[3];
+    if (tid == 0) g.partial[tsp] = ((wsum[0] + wsum[1]) + wsum[2]) + wsum[3];
   }
   WG_T(3);
 }
@@ -2588,15 +2597,23 @@ __global__ void __launch_bounds__(64 * NW * KS) conv_fpatch_kernel(const ConvArg
   {
     const int nwg = gridDim.x * gridDim.y;
     int t = blockIdx.x + gridDim.x * blockIdx.y;
-    if (s.remap) {                               // XCD-contiguous runs, N tile fastest
-      const int xcd = t & 7, q = nwg >> 3, r = nwg & 7;
-      t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (t >> 3);
+    const int S = txn * tyn * s.batch;
+    int sp;
+    if (s.remap == 2 && xcd_spatial(t, S, gridDim.x / S, gridDim.y, sp, gi, nblk)) {
+      txi = sp % txn; sp /= txn;
+      tyi = sp % tyn;
+      b = sp / tyn;
+    } else {
+      if (s.remap) {                             // XCD-contiguous runs, N tile fastest
+        const int xcd = t & 7, q = nwg >> 3, r = nwg & 7;
+        t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (t >> 3);
+      }
+      nblk = t % gridDim.y; t /= gridDim.y;
+      txi = t % txn; t /= txn;
+      tyi = t % tyn; t /= tyn;
+      b = t % s.batch;
+      gi = t / s.batch;
     }
-    nblk = t % gridDim.y; t /= gridDim.y;
-    txi = t % txn; t /= txn;
-    tyi = t % tyn; t /= tyn;
-    b = t % s.batch;
-    gi = t / s.batch;
   }
   const ConvGroup& g = args.g[gi];
   const int n0 = nblk * BN;
@@ -3272,7 +3289,7 @@ extern "C" int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroup
   s.ngroups = ngroups;
   static const int remap_env = [] {
     const char* e = getenv("RGBAC_XCD_REMAP");
-    return (e && e[0] == '0') ? 0 : 1;
+    return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
   }();
   s.remap = remap_env;
   if (a->tile == kTileNPatch) {
