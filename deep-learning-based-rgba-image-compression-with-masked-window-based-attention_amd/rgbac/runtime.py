@@ -628,6 +628,26 @@ _TILE_SIG = {0: "128, 128, 2, 2, 2", 1: "128, 64, 4, 1, 3", 2: "64, 64, 2, 2, 3"
 _SMALLK_NKS = {1: 1, 2: 2, 3: 3, 4: 4, 5: 5, 6: 6, 7: 8, 8: 8, 9: 12, 10: 12, 11: 12, 12: 12}
 
 
+_PW2_ON = os.environ.get("RGBAC_PW2", "1") != "0"
+_PW2_ALL = os.environ.get("RGBAC_PW2_ALL", "1") != "0"
+
+
+def _pw2_admits(preps):
+    """Host mirror of csrc/conv.hip pw2_ok (which pointwise kernel a TILE_PW launch runs)."""
+    a0 = preps[0].a
+    if not _PW2_ON or a0.act in (ACT["tanh_half"], ACT["gauss"]) or a0.mode != CONV:
+        return False
+    if not _PW2_ALL and -(-preps[0].mgrid // 16) * len(preps) > 8 * 256:
+        return False
+    for p in preps:
+        a = p.a
+        if (a.zout and a.zout_ldc % 4) or a.cout % 8 or a.out_coff % 8 or a.out_ldc % 8 or \
+                a.cout > 192 or (a.res0 and a.res0_ldc % 4) or (a.res1 and a.res1_ldc % 4) or \
+                (a.res2 and a.res2_ldc % 4):
+            return False
+    return True
+
+
 def kernel_name(tile, preps):
     """rocprofv3-style name (namespace and argument list stripped) of a conv launch."""
     dt = "float" if preps[0].a.dtype == 0 else "bf16_t"
@@ -652,9 +672,13 @@ def kernel_name(tile, preps):
         return f"conv_npatch_kernel<{2 if max(p.pk.cout for p in preps) > 16 else 1}>"
     if tile == TILE_PW:
         cin = max(p.a.cin_pad for p in preps)
-        # csrc/conv.hip launch_pw: 32-deep k-steps held in LDS (2 / 4 / 6)
+        nks = 2 if cin <= 64 else (4 if cin <= 128 else 6)
+        # csrc/conv.hip launch_pw: conv_pw2_kernel where pw2_ok admits the launch, else
+        # conv_pw_kernel (32-deep k-steps held in LDS: 2 / 4 / 6)
+        if _pw2_admits(preps):
+            return f"conv_pw2_kernel<{nks}>"
         dact = "true" if preps[0].a.act in (ACT["dgelu"], ACT["dlrelu"]) else "false"
-        return f"conv_pw_kernel<{2 if cin <= 64 else (4 if cin <= 128 else 6)}, {dact}>"
+        return f"conv_pw_kernel<{nks}, {dact}>"
     if tile == TILE_SMALLK:
         cout = max(p.pk.cout for p in preps)
         nt = 1 if cout <= 32 else (2 if cout <= 64 else 3)
