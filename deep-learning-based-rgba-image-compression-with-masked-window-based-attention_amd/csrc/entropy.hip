@@ -480,6 +480,12 @@ extern "C" int rgbac_eb_forward(int dtype, int64_t npix, int channels, const voi
   return check_launch("eb_forward_kernel");
 }
 
+extern "C" int rgbac_finalize_blocks(int h, int w) {
+  const long long hw = (long long)h * w;
+  long long n = (hw + 1023) / 1024;
+  return (int)(n < 64 ? 64 : (n > 1024 ? 1024 : n));
+}
+
 extern "C" int rgbac_finalize(int dtype, int mode, int batch, int cx, int h, int w, const float* x,
                               const void* x_hat, int64_t ldh, const float* mask,
                               const double* ybits, int ny, const double* zbits, int nz,
@@ -502,7 +508,10 @@ extern "C" int rgbac_finalize_ex(int dtype, int mode, int batch, int cx, int h, 
   const int vec = cx <= 4 && ldh % 4 == 0 &&
                   ((uintptr_t)x_hat % (dtype == RGBAC_F32 ? 16 : 8)) == 0;
   const int HW = h * w;
-  const int nblk = 64;  // scratch must hold batch * 64 * 2 doubles
+  // scratch holds batch * nblk * 2 doubles (rgbac_finalize_blocks): <= 4 pixels per thread, so
+  // the large frames' MSE pass is not a long dependent loop per thread (1024^2: 64 -> 1024
+  // blocks per image)
+  const int nblk = rgbac_finalize_blocks(h, w);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (dtype == RGBAC_F32)
     hipLaunchKernelGGL(mse_partial_kernel<float>, dim3(nblk, batch), dim3(256), 0, st, mode, cx,

@@ -2726,10 +2726,11 @@ extern "C" int rgbac_mse_bwd(int dtype, int mode, int batch, int cx, int h, int 
   RGBAC_REQUIRE(mode == 0 || mode == 1, "mode");
   RGBAC_REQUIRE(batch > 0 && cx > 0 && h > 0 && w > 0 && lddx >= cx, "shape");
   RGBAC_REQUIRE(x && x_hat && gmse && dx_hat && (mode == 1 || (mask && scratch)), "null pointer");
+  const int nblk = rgbac_finalize_blocks(h, w);   // the forward's scratch layout
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   dim3 grid(64, batch);
 #define K_(T, ...)                                                                              \
-  hipLaunchKernelGGL(mse_bwd_kernel<T>, grid, dim3(256), 0, st, mode, batch, cx, h * w, 64, x,   \
+  hipLaunchKernelGGL(mse_bwd_kernel<T>, grid, dim3(256), 0, st, mode, batch, cx, h * w, nblk, x,   \
                      (const T*)x_hat, ldh, mask, scratch, gmse, (T*)dx_hat, lddx)
   RGBAC_DT_DISPATCH(dtype, K_, 0);
 #undef K_

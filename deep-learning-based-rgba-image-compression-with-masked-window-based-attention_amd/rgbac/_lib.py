@@ -139,6 +139,7 @@ SIGNATURES = {
     "rgbac_reduce_blocks": [_I64],
     "rgbac_finalize": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP, _VP, _I32,
                        _VP, _I32, _VP, _VP, _VP],
+    "rgbac_finalize_blocks": [_I32, _I32],
     "rgbac_finalize_ex": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP, _VP, _I32,
                           _VP, _I32, _VP, _VP, _VP, _VP],
     "rgbac_mask_pyramid": [_I32, _I32, _I32, _VP, _I32, _VP, _I32, _VP, _VP],
@@ -241,6 +242,11 @@ def call(name, *args):
         msg = lib.rgbac_last_error().decode(errors="replace")
         raise RuntimeError(f"{name} failed ({rc}): {msg}")
     return rc
+
+
+def finalize_scratch_doubles(batch, h, w):
+    """Doubles of the rgbac_finalize / rgbac_finalize_ex scratch (rgbac_finalize_blocks)."""
+    return batch * load().rgbac_finalize_blocks(h, w) * 2
 
 
 def stream_ptr(device=None):

@@ -1259,7 +1259,8 @@ class MSEFn(Function):
         xh = Feat(xh_t, C)
         dev = xh_t.device
         B, cx, H, W = x.shape
-        scratch = torch.empty(B * 64 * 2, dtype=torch.float64, device=dev)
+        scratch = torch.empty(_lib.finalize_scratch_doubles(B, H, W), dtype=torch.float64,
+                              device=dev)
         zero = torch.zeros(1, dtype=torch.float64, device=dev)
         out = torch.empty(4, dtype=_F32, device=dev)
         _lib.call("rgbac_finalize", _lib.dtype_code(xh_t.dtype), mode, B, cx, H, W, x.data_ptr(),

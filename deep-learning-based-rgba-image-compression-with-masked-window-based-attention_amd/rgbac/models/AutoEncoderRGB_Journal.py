@@ -118,7 +118,8 @@ def finalize(mode, x, x_hat, mask, ypart, zpart, x_hat_nchw=None):
     [B, cx, H, W]) the same pass also writes x_hat's NCHW copy."""
     B, cx, H, W = x.shape
     dev = x.device
-    scratch = torch.empty(B * 64 * 2, dtype=torch.float64, device=dev)
+    scratch = torch.empty(_lib.finalize_scratch_doubles(B, H, W), dtype=torch.float64,
+                          device=dev)
     out = torch.empty(4, dtype=torch.float32, device=dev)
     _lib.call("rgbac_finalize_ex", _lib.dtype_code(x_hat.t.dtype), mode, B, cx, H, W,
               x.data_ptr(), x_hat.ptr(), x_hat.ldc, _lib.ptr(mask), ypart.data_ptr(),

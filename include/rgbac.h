@@ -282,6 +282,10 @@ int rgbac_finalize(int dtype, int mode, int batch, int cx, int h, int w,
                    const float* mask, const double* ybits, int ny,
                    const double* zbits, int nz, double* scratch, float* out,
                    void* stream);
+/* Partial-sum blocks per image of the MSE pass: ``scratch`` of rgbac_finalize /
+ * rgbac_finalize_ex must hold batch * rgbac_finalize_blocks(h, w) * 2 doubles
+ * (min(1024, max(64, ceil(h * w / 1024)))). */
+int rgbac_finalize_blocks(int h, int w);
 /* The same, also writing x_hat's fp32 NCHW copy [B,cx,H,W] (the forward's returned x_hat,
  * otherwise a separate rgbac_nhwc_to_nchw) from the reads the MSE pass makes anyway;
  * x_hat_nchw may be NULL (== rgbac_finalize). */

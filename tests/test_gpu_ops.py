@@ -765,7 +765,7 @@ def test_finalize_writes_xhat_nchw(device, dtype):
     zp = torch.rand(16, generator=g, dtype=torch.float64).to(device)
     xo = torch.full((B, 3, H, W), 5.0, device=device)
     a = finalize(0, x, xh, mask, yp, zp, x_hat_nchw=xo)
-    scratch = torch.empty(B * 64 * 2, dtype=torch.float64, device=device)
+    scratch = torch.empty(_lib.finalize_scratch_doubles(B, H, W), dtype=torch.float64, device=device)
     b = torch.empty(4, dtype=torch.float32, device=device)
     _lib.call("rgbac_finalize", _lib.dtype_code(dtype), 0, B, 3, H, W, x.data_ptr(), xh.ptr(),
               xh.ldc, mask.data_ptr(), yp.data_ptr(), yp.numel(), zp.data_ptr(), zp.numel(),
