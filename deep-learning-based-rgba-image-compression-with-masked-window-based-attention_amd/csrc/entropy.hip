@@ -169,24 +169,43 @@ mse_partial_kernel(int mode, int cx, int HW, const float* __restrict__ x, const 
   }
 }
 
-__global__ void __launch_bounds__(256)
+constexpr int kFinWaves = 16;   // finalize_kernel: one 1024-thread block
+
+__global__ void __launch_bounds__(64 * kFinWaves)
 finalize_kernel(int mode, int batch, int nblk, double npix, const double* __restrict__ part,
                 const double* __restrict__ yb, int ny, const double* __restrict__ zb, int nz,
                 float* __restrict__ out) {
-  // One block; every reduction is a wave reduction (shuffles, no barrier) and the four waves'
+  // One block; every reduction is a wave reduction (shuffles, no barrier) and the waves'
   // results meet once in LDS, combined in wave order (fixed order: deterministic).  Wave w owns
-  // images w, w + 4, ...  (The block-wide form spent two barriers per image and bits term.)
-  __shared__ double wred[4][5];
+  // images w, w + 16, ...  The bits partials are summed four independent chains per thread
+  // (their loads in flight together: a single dependent chain over the 1024^2 frame's 20k
+  // partials was 37 us of load latencies), the chains then added in a fixed order.
+  constexpr int NT = 64 * kFinWaves;
+  __shared__ double wred[kFinWaves][5];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  double ys = 0.0, zs = 0.0;
-  for (int i = threadIdx.x; i < ny; i += 256) ys += yb[i];
-  for (int i = threadIdx.x; i < nz; i += 256) zs += zb[i];
+  double ya[4] = {0.0, 0.0, 0.0, 0.0}, za[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int i0 = threadIdx.x; i0 < ny; i0 += 4 * NT) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * NT;
+      ya[u] += i < ny ? yb[i] : 0.0;
+    }
+  }
+  for (int i0 = threadIdx.x; i0 < nz; i0 += 4 * NT) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * NT;
+      za[u] += i < nz ? zb[i] : 0.0;
+    }
+  }
+  double ys = (ya[0] + ya[1]) + (ya[2] + ya[3]);
+  double zs = (za[0] + za[1]) + (za[2] + za[3]);
   for (int o = 32; o > 0; o >>= 1) {
     ys += __shfl_xor(ys, o);
     zs += __shfl_xor(zs, o);
   }
   double mse_acc = 0.0, se_all = 0.0, cnt_all = 0.0;
-  for (int b = wave; b < batch; b += 4) {
+  for (int b = wave; b < batch; b += kFinWaves) {
     double se = 0.0, cnt = 0.0;
     for (int i = lane; i < nblk; i += 64) {
       se += part[((size_t)b * nblk + i) * 2 + 0];
@@ -210,7 +229,10 @@ finalize_kernel(int mode, int batch, int nblk, double npix, const double* __rest
   if (threadIdx.x == 0) {
     double t[5];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) t[k] = ((wred[0][k] + wred[1][k]) + wred[2][k]) + wred[3][k];
+    for (int k = 0; k < 5; ++k) {
+      t[k] = 0.0;
+      for (int w = 0; w < kFinWaves; ++w) t[k] += wred[w][k];
+    }
     float mse;
     if (mode == 0)
       mse = (float)(t[2] / batch);
@@ -521,7 +543,7 @@ extern "C" int rgbac_finalize_ex(int dtype, int mode, int batch, int cx, int h, 
                        HW, x, (const bf16_t*)x_hat, ldh, mask, scratch, x_hat_nchw, vec);
   int rc = check_launch("mse_partial_kernel");
   if (rc) return rc;
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, st, mode, batch, nblk,
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64 * kFinWaves), 0, st, mode, batch, nblk,
                      (double)batch * HW, scratch, ybits, ny, zbits, nz, out);
   return check_launch("finalize_kernel");
 }
