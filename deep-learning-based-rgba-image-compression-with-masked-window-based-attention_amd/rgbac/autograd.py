@@ -391,8 +391,29 @@ _PENDING = []                   # (task int64 x 11, keep-alive tensors)
 _PENDING_CB = [False]
 
 
+# Weight-gradient reductions that add into param.grad on a SIDE stream (RGBAC_SIDE_REDUCE=1):
+# the slab reads of layer L's reduction then run beside layer L-1's input-gradient convs, which
+# are the backward's critical path.  The side stream forks from the stream the backward node
+# runs on; that stream waits for the side stream again (the join) before anything reads the
+# gradients: in rgbac.parallel's bucket hooks (flush_reductions) and at the end of the backward
+# pass (an engine callback).  The slabs stay referenced until the join.
+SIDE_REDUCE = os.environ.get("RGBAC_SIDE_REDUCE", "0") == "1"
+_SIDE = {}                      # device -> side stream
+_SIDE_MAIN = {}                 # device -> the stream the side stream forked from
+_SIDE_KEEP = []
+
+
+def join_side():
+    """Make each forking stream wait for its side stream's reductions; release their slabs."""
+    for dev, main in list(_SIDE_MAIN.items()):
+        main.wait_stream(_SIDE[dev])
+    _SIDE_MAIN.clear()
+    _SIDE_KEEP.clear()
+
+
 def flush_reductions():
     """Issue every queued weight-gradient reduction (one launch per 8)."""
+    join_side()
     while _PENDING:
         part = _PENDING[:8]
         del _PENDING[:8]
@@ -409,10 +430,36 @@ def _end_of_backward():
     flush_reductions()
 
 
+def _side_reduce(args, keep):
+    dev = keep[0].device
+    main = torch.cuda.current_stream(dev)
+    side = _SIDE.get(dev)
+    if side is None:
+        side = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    prev = _SIDE_MAIN.get(dev)
+    if prev is not None and prev != main:
+        join_side()                # a different forking stream: join the first one's work
+    _SIDE_MAIN[dev] = main
+    side.wait_stream(main)
+    _lib.call("rgbac_wgrad_reduce", *args, side.cuda_stream)
+    _SIDE_KEEP.extend(keep)
+    if not _PENDING_CB[0]:
+        torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
+        _PENDING_CB[0] = True
+
+
 def _reduce(nslot, fmap, part, nsplit, slab, dw, nbias, bpart, n_pad, db, acc, st):
     # queued reductions are flushed by a callback of the running backward pass: outside one
     # (a weight gradient computed directly, e.g. a test or a custom loop) there is no engine
     # to run the callback, so the reduction goes out immediately
+    if SIDE_REDUCE and acc and torch._C._current_graph_task_id() >= 0:
+        _side_reduce((nslot, None if fmap is None else fmap.data_ptr(),
+                      None if part is None else part.data_ptr(), nsplit, slab,
+                      None if dw is None else dw.data_ptr(), nbias,
+                      None if bpart is None else bpart.data_ptr(), n_pad,
+                      None if db is None else db.data_ptr(), 1),
+                     [t for t in (part, bpart, fmap, dw, db) if t is not None])
+        return
     if not (REDUCE_BATCH and acc) or torch._C._current_graph_task_id() < 0:
         flush_reductions()
         _lib.call("rgbac_wgrad_reduce", nslot, None if fmap is None else fmap.data_ptr(),

@@ -210,3 +210,33 @@ def test_stream_unit_matches_chunk_ring_kernel(device, kind):
         frac = ((a - b).abs() > scale * 2.0 ** -8).float().mean().item()
         print(f"kind {kind}: max diff {(a - b).abs().max().item() / scale:.2e}, > 1 ulp {frac:.1e}")
         assert frac <= 1e-3, frac
+
+
+@pytest.mark.parametrize("mode", ["1", "2"])
+@pytest.mark.parametrize("kind,B,H,W", [(0, 2, 32, 64), (1, 2, 32, 64), (0, 1, 24, 48), (1, 1, 8, 16)])
+def test_half_tile_unit_matches_stream_kernel(device, monkeypatch, mode, kind, B, H, W):
+    """ru_half_kernel (8 x 8 tiles: RGBAC_RU_HALF=1 one per workgroup at four workgroups per CU,
+    =2 two neighbouring tiles per workgroup with the second's x fetched during the first) against
+    ru_stream_kernel (8 x 16 tiles) on the same C = 192 units: the same GEMM order per output
+    and the same bf16 rounding points, so the two agree to 1 bf16 ulp of the output range at
+    99.9 % of the elements (image borders included: 8 x 16 has a single tile)."""
+    from rgbac import runtime as rt
+    from rgbac.layers import Masked_Attention as MA
+    from rgbac.models import AutoEncoderMask_Journal as AM
+    torch.manual_seed(41 + kind)
+    mods = [(MA.ResidualUnit(192) if kind == 0 else AM.ResBlock(192)).cuda() for _ in range(2)]
+    units = [((m.conv[0], m.conv[2], m.conv[4]) if kind == 0 else (m.conv1, m.conv2, m.conv3))
+             for m in mods]
+    xs = [rt.to_nhwc(torch.randn((B, 192, H, W), device="cuda"), torch.bfloat16) for _ in mods]
+    with torch.no_grad():
+        monkeypatch.setenv("RGBAC_RU_HALF", "0")
+        base = [rt.to_nchw(o).float() for o in MA.run_bottlenecks_fused(list(zip(units, xs)), kind)]
+        monkeypatch.setenv("RGBAC_RU_HALF", mode)
+        got = [rt.to_nchw(o).float() for o in MA.run_bottlenecks_fused(list(zip(units, xs)), kind)]
+        torch.cuda.synchronize()
+    for a, b in zip(got, base):
+        scale = b.abs().max().item()
+        frac = ((a - b).abs() > scale * 2.0 ** -8).float().mean().item()
+        print(f"kind {kind} {B}x{H}x{W}: max diff {(a - b).abs().max().item() / scale:.2e}, "
+              f"> 1 ulp {frac:.1e}")
+        assert frac <= 1e-3, frac

@@ -1029,6 +1029,58 @@ def test_reduce_batch_matches_immediate_reductions():
     assert torch.equal(grads[True][0], grads[False][0])
 
 
+def test_side_reduce_matches_in_stream_reductions():
+    """RGBAC_SIDE_REDUCE (the weight-gradient reductions that add into param.grad run on a side
+    stream forked from the backward's stream and joined at the end of backward): the AdamClamp
+    flat gradient equals the in-stream path bit for bit (same kernels, same order), eager and
+    in a captured HIP graph (fork / join inside the capture), bf16 B=2 64^2 training step."""
+    from rgbac import autograd as ag
+    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    from rgbac.optim import AdamClamp
+    g = _gen(73)
+    B, H, W = 2, 64, 64
+    x = (torch.randint(0, 256, (B, 3, H, W), generator=g).float() / 255).cuda()
+    a = torch.ones((B, 1, H, W)).cuda()
+    me = [t.cuda() for t in ref.supply_mask(a.cpu())]
+    nz = (torch.rand((B, 1, 1, 192), generator=g) - 0.5).cuda()
+    ny = (torch.rand((B, 8, 8, 80), generator=g) - 0.5).cuda()
+    torch.manual_seed(234)
+    net = AutoEncoder().cuda().train().set_compute_dtype(torch.bfloat16)
+    opt = AdamClamp(net.parameters(), lr=1e-4, clip=5.0)
+
+    def step():
+        opt.zero_grad()
+        o = net(x, a, a, *me[:4], noise_z=nz, noise_y=ny)
+        (4096 * o[1] + o[2]).backward()
+
+    grads = {}
+    prev = ag.SIDE_REDUCE
+    try:
+        for mode in (False, True):
+            ag.SIDE_REDUCE = mode
+            step()
+            torch.cuda.synchronize()
+            assert not ag._SIDE_MAIN and not ag._SIDE_KEEP, "side stream not joined"
+            grads[mode] = opt.flat_grad.clone()
+        assert torch.equal(grads[True], grads[False])
+        ag.SIDE_REDUCE = True
+        cap = torch.cuda.Stream()
+        cap.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cap):
+            step()
+        torch.cuda.current_stream().wait_stream(cap)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step()
+        opt.flat_grad.fill_(float("nan"))
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(opt.flat_grad, grads[False])
+        del graph
+    finally:
+        ag.SIDE_REDUCE = prev
+
+
 def test_prefetch_frag_packs_equal_element_gather():
     """prefetch_packs' two launches (plain packs + biases gathered from the fp32 parameters,
     then the fragment-major copies as 16-byte chunk copies of the plain packs) give every
