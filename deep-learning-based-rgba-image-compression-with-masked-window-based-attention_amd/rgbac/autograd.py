@@ -397,10 +397,14 @@ _PENDING_CB = [False]
 # runs on; that stream waits for the side stream again (the join) before anything reads the
 # gradients: in rgbac.parallel's bucket hooks (flush_reductions) and at the end of the backward
 # pass (an engine callback).  The slabs stay referenced until the join.
-SIDE_REDUCE = os.environ.get("RGBAC_SIDE_REDUCE", "0") == "1"
+# RGBAC_SIDE_REDUCE=2 also moves the weight-gradient kernel itself there (it reads the output
+# gradient and the saved inputs, which then stay referenced until the join as well).
+SIDE_REDUCE = os.environ.get("RGBAC_SIDE_REDUCE", "0") in ("1", "2")
+SIDE_WGRAD = os.environ.get("RGBAC_SIDE_REDUCE", "0") == "2"
 _SIDE = {}                      # device -> side stream
 _SIDE_MAIN = {}                 # device -> the stream the side stream forked from
 _SIDE_KEEP = []
+_SIDE_READS = set()             # storages the side stream's pending weight-gradient kernels read
 
 
 def join_side():
@@ -409,6 +413,15 @@ def join_side():
         main.wait_stream(_SIDE[dev])
     _SIDE_MAIN.clear()
     _SIDE_KEEP.clear()
+    _SIDE_READS.clear()
+
+
+def _side_guard(t):
+    """Before ``t`` is written in place (a gradient sink accumulating): join the side stream if
+    a pending weight-gradient kernel there reads t's storage -- e.g. a residual unit's output
+    gradient, adopted by the unit input's sink and later accumulated into in place."""
+    if _SIDE_READS and t is not None and t.untyped_storage().data_ptr() in _SIDE_READS:
+        join_side()
 
 
 def flush_reductions():
@@ -430,8 +443,9 @@ def _end_of_backward():
     flush_reductions()
 
 
-def _side_reduce(args, keep):
-    dev = keep[0].device
+def _fork_side(dev, keep):
+    """The side stream of ``dev``, made to wait for the current stream; ``keep`` stays
+    referenced until the join."""
     main = torch.cuda.current_stream(dev)
     side = _SIDE.get(dev)
     if side is None:
@@ -441,11 +455,16 @@ def _side_reduce(args, keep):
         join_side()                # a different forking stream: join the first one's work
     _SIDE_MAIN[dev] = main
     side.wait_stream(main)
-    _lib.call("rgbac_wgrad_reduce", *args, side.cuda_stream)
     _SIDE_KEEP.extend(keep)
     if not _PENDING_CB[0]:
         torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
         _PENDING_CB[0] = True
+    return side
+
+
+def _side_reduce(args, keep):
+    side = _fork_side(keep[0].device, keep)
+    _lib.call("rgbac_wgrad_reduce", *args, side.cuda_stream)
 
 
 def _reduce(nslot, fmap, part, nsplit, slab, dw, nbias, bpart, n_pad, db, acc, st):
@@ -527,6 +546,11 @@ def wgrad(G, S, ksize, stride, pad, square, k_pad, fmap, numel, nbias=0, bias_fr
     a.partial = part.data_ptr()
     a.bias_partial = None if bpart is None else bpart.data_ptr()
     st = _stream(G.t)
+    if (SIDE_WGRAD and acc_dw is not None and rt.PROFILER is None and
+            torch._C._current_graph_task_id() >= 0):
+        st = _fork_side(dev, [G.t, part] + [f.t for f in S] +
+                        ([] if bpart is None else [bpart])).cuda_stream
+        _SIDE_READS.update(t.untyped_storage().data_ptr() for t in [G.t] + [f.t for f in S])
     # the launched form's rocprof name (the C side's choice, restated), so the bench's
     # per-kernel table and training roofline keep the forms apart
     if hs:
@@ -673,6 +697,7 @@ def _deposit(sink, g, own):
     if sink.buf is None:
         sink.buf, sink.own = g, own
     elif sink.own:
+        _side_guard(sink.buf)
         sink.buf.add_(g)
     else:
         sink.buf, sink.own = sink.buf + g, True
@@ -815,6 +840,8 @@ class ConvFn(Function):
                 targeted.add(id(sk))
                 prev = Feat(sk.buf, f.C)
                 inplace = sk.own and all(sk.buf is not t for t in (G.t, dz.t, dy.t))
+                if inplace:
+                    _side_guard(sk.buf)
                 o = prev if inplace else new_feat(f.B, f.H, f.W, f.C, dt, f.t.device)
                 preps.append(rt.prepare(pk, [G.src()], out=o, res0=prev, bias=False))
                 sk.buf, sk.own, sk.slices = o.t, True, False
@@ -1082,6 +1109,7 @@ class CatFn(Function):
                 # add this part's slice into the producer's gradient buffer
                 if not sk.own:
                     sk.buf, sk.own = sk.buf.clone(), True
+                _side_guard(sk.buf)
                 sk.slices = False
                 pairs.append((Feat(sk.buf, c), 0, g, off, c))
                 accs.append(True)
@@ -1228,6 +1256,8 @@ class GaussFn(Function):
         direct = ysink is not None and (ysink.buf is None or (ysink.slices and ysink.own))
         if direct and ysink.buf is None:
             ysink.buf, ysink.own, ysink.slices = torch.zeros_like(y_t), True, True
+        if direct:
+            _side_guard(ysink.buf)
         dy = Feat(ysink.buf if direct else torch.zeros_like(y_t), Cy)
         dmu = Feat(torch.zeros_like(mu_t), cs)
         dsc = Feat(torch.zeros_like(sc_t), cs)

@@ -1030,8 +1030,9 @@ def test_reduce_batch_matches_immediate_reductions():
 
 
 def test_side_reduce_matches_in_stream_reductions():
-    """RGBAC_SIDE_REDUCE (the weight-gradient reductions that add into param.grad run on a side
-    stream forked from the backward's stream and joined at the end of backward): the AdamClamp
+    """RGBAC_SIDE_REDUCE=1 (the weight-gradient reductions that add into param.grad run on a side
+    stream forked from the backward's stream and joined at the end of backward) and =2 (the
+    weight-gradient kernels too): the AdamClamp
     flat gradient equals the in-stream path bit for bit (same kernels, same order), eager and
     in a captured HIP graph (fork / join inside the capture), bf16 B=2 64^2 training step."""
     from rgbac import autograd as ag
@@ -1054,31 +1055,40 @@ def test_side_reduce_matches_in_stream_reductions():
         (4096 * o[1] + o[2]).backward()
 
     grads = {}
-    prev = ag.SIDE_REDUCE
+    prev = ag.SIDE_REDUCE, ag.SIDE_WGRAD
     try:
-        for mode in (False, True):
-            ag.SIDE_REDUCE = mode
+        for mode in (0, 1, 2):
+            ag.SIDE_REDUCE, ag.SIDE_WGRAD = mode >= 1, mode == 2
             step()
             torch.cuda.synchronize()
             assert not ag._SIDE_MAIN and not ag._SIDE_KEEP, "side stream not joined"
             grads[mode] = opt.flat_grad.clone()
-        assert torch.equal(grads[True], grads[False])
-        ag.SIDE_REDUCE = True
-        cap = torch.cuda.Stream()
-        cap.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(cap):
-            step()
-        torch.cuda.current_stream().wait_stream(cap)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            step()
-        opt.flat_grad.fill_(float("nan"))
-        graph.replay()
-        torch.cuda.synchronize()
-        assert torch.equal(opt.flat_grad, grads[False])
-        del graph
+        assert torch.equal(grads[1], grads[0])
+        assert torch.equal(grads[2], grads[0])
+        names = {id(p): n for n, p in net.named_parameters()}
+        for mode in (0, 1, 2):
+            ag.SIDE_REDUCE, ag.SIDE_WGRAD = mode >= 1, mode == 2
+            cap = torch.cuda.Stream()
+            cap.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(cap):
+                step()
+            torch.cuda.current_stream().wait_stream(cap)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                step()
+            bad = []
+            for rep in range(3):
+                opt.flat_grad.fill_(float("nan"))
+                graph.replay()
+                torch.cuda.synchronize()
+                for p, (off, k) in zip(opt.params, opt.offsets):
+                    d = (opt.flat_grad[off:off + k] - grads[0][off:off + k]).abs().max().item()
+                    if not d == 0.0:
+                        bad.append((rep, names.get(id(p)), d))
+            del graph
+            assert not bad, (mode, bad[:12])
     finally:
-        ag.SIDE_REDUCE = prev
+        ag.SIDE_REDUCE, ag.SIDE_WGRAD = prev
 
 
 def test_prefetch_frag_packs_equal_element_gather():
