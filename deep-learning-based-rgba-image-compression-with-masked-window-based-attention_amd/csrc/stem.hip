@@ -33,6 +33,12 @@ constexpr int kW1Chunks = 2 * kStemKS1 + 1;   // 16-byte chunks per W1 row (26 +
 constexpr int kW2Chunks = kStemC / 8;     // 24
 
 typedef __attribute__((ext_vector_type(16))) float f32x16_s;
+// waves per workgroup: two per SIMD, so one wave's VALU epilogues (bias / GDN B fragments /
+// rsqrt) issue beside the other wave's MFMAs (at one wave per SIMD they serialised)
+#ifndef RGBAC_STEM_NW
+#define RGBAC_STEM_NW 8
+#endif
+constexpr int kStemNW = RGBAC_STEM_NW;
 
 __device__ uint4 g_stem_zero[64];           // source of the W1 rows' padding chunk
 
@@ -55,7 +61,7 @@ __device__ __forceinline__ int w2_slot(int row, int chunk) {
 }
 
 
-__global__ void __launch_bounds__(256, 1)
+__global__ void __launch_bounds__(kStemNW * 64, 1)
 stem_gdn_kernel(int batch, int in_h, int in_w, const bf16_t* __restrict__ x, int x_ldc,
                 const bf16_t* __restrict__ w1, int w1_kpad, const float* __restrict__ b1,
                 const bf16_t* __restrict__ w2, int w2_kpad, const float* __restrict__ beta,
@@ -75,7 +81,7 @@ stem_gdn_kernel(int batch, int in_h, int in_w, const bf16_t* __restrict__ x, int
         (uint32_t)(size_t)(__attribute__((address_space(3))) void*)W2s);
     constexpr int P1 = kStemC * kW1Chunks / 64, P2 = kStemC * kW2Chunks / 64;
     static_assert(P1 * 64 == kStemC * kW1Chunks && P2 * 64 == kStemC * kW2Chunks, "whole pieces");
-    for (int p = wave; p < P1 + P2; p += 4) {
+    for (int p = wave; p < P1 + P2; p += kStemNW) {
       if (p < P1) {
         const int e = p * 64 + lane, r = e / kW1Chunks, ch = e - r * kW1Chunks;
         stem_dma16(ch < kW1Chunks - 1 ? (const void*)(w1 + (size_t)r * w1_kpad + ch * 8)
@@ -96,7 +102,7 @@ stem_gdn_kernel(int batch, int in_h, int in_w, const bf16_t* __restrict__ x, int
   const int Ho = (in_h + 1) / 2, Wo = (in_w + 1) / 2;
   const int M = batch * Ho * Wo;
   const int ntile = (M + 31) / 32;
-  const int tstride = gridDim.x * 4;
+  const int tstride = gridDim.x * kStemNW;
   // XCD-contiguous tile runs: the hardware deals block b to XCD b mod 8, so with the plain
   // order the 4 x 32-pixel tiles of one output row and its neighbour rows -- whose 5x5/s2
   // windows share input rows -- land on 8 different L2s and every L2 fetches the shared rows
@@ -132,26 +138,25 @@ stem_gdn_kernel(int batch, int in_h, int in_w, const bf16_t* __restrict__ x, int
     pb = t2 / Ho;
     return valid;
   };
-  uint4 bv[kStemKS1];
-  {
-    int pb, oy, ox;
-    const bool v = decode(vb * 4 + wave, pb, oy, ox);
-#pragma unroll
-    for (int ks = 0; ks < kStemKS1; ++ks) bv[ks] = load_b(ks, pb, oy, ox, v);
-  }
-  // the panels and the first tile's im2col fragments, one wait
+  // the panels, one wait
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  for (int tile = vb * 4 + wave; tile < ntile; tile += tstride) {
+  for (int tile = vb * kStemNW + wave; tile < ntile; tile += tstride) {
     const int m = tile * 32 + r32;
     const bool valid = m < M;
+    // this tile's im2col fragments (register budget at two waves per SIMD: no cross-tile
+    // prefetch; the SIMD's other wave computes while these are in flight)
+    uint4 bv[kStemKS1];
+    {
+      int pb, oy, ox;
+      const bool v = decode(tile, pb, oy, ox);
+#pragma unroll
+      for (int ks = 0; ks < kStemKS1; ++ks) bv[ks] = load_b(ks, pb, oy, ox, v);
+    }
 
     // ---- stem conv
     f32x16_s acc[kStemNT];
-#pragma unroll
-    for (int t = 0; t < kStemNT; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
+    const f32x16_s zero16 = {};
     // A fragments one k-step ahead: k-step ks + 1's LDS reads are in flight under k-step ks's
     // six MFMAs (the scheduling barrier keeps the compiler from hoisting all 78 and spilling)
     uint4 an[kStemNT];
@@ -170,17 +175,10 @@ stem_gdn_kernel(int batch, int in_h, int in_w, const bf16_t* __restrict__ x, int
 #pragma unroll
       for (int t = 0; t < kStemNT; ++t)
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[t]), bb,
-                                                         acc[t], 0, 0, 0);
+                                                         ks ? acc[t] : zero16, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
 
-    // the next tile's im2col fragments load while this tile's GDN runs
-    {
-      int pb, oy, ox;
-      const bool v = decode(tile + tstride, pb, oy, ox);
-#pragma unroll
-      for (int ks = 0; ks < kStemKS1; ++ks) bv[ks] = load_b(ks, pb, oy, ox, v);
-    }
 
     // ---- y = bf16(acc + b1), kept packed per channel quad (channels 32t + 8g + 4h + r)
     uint32_t ypk[kStemNT][4][2];
@@ -199,10 +197,6 @@ stem_gdn_kernel(int batch, int in_h, int in_w, const bf16_t* __restrict__ x, int
     };
 
     // ---- GDN norm pool: norm[n][px] = sum_j gamma'[n][j] * y[j][px]^2 on MFMA
-#pragma unroll
-    for (int t = 0; t < kStemNT; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
     uint4 wn[kStemNT];
 #pragma unroll
     for (int t = 0; t < kStemNT; ++t) wn[t] = W2s[w2_slot(32 * t + r32, h)];
@@ -238,7 +232,7 @@ stem_gdn_kernel(int batch, int in_h, int in_w, const bf16_t* __restrict__ x, int
 #pragma unroll
       for (int t = 0; t < kStemNT; ++t)
         acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a[t]), bb,
-                                                         acc[t], 0, 0, 0);
+                                                         ks ? acc[t] : zero16, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
 
@@ -288,14 +282,14 @@ extern "C" int rgbac_stem_gdn(int batch, int in_h, int in_w, const void* x, int6
   static int ncu = 0;
   if (ncu == 0) {
     int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (ncu < 1) ncu = 256;
   }
   const long long ntile = (M + 31) / 32;
-  long long g = (ntile + 3) / 4;
+  long long g = (ntile + kStemNW - 1) / kStemNW;
   if (g > ncu) g = ncu;
-  hipLaunchKernelGGL(stem_gdn_kernel, dim3((unsigned)g), dim3(256), 0,
+  hipLaunchKernelGGL(stem_gdn_kernel, dim3((unsigned)g), dim3(kStemNW * 64), 0,
                      reinterpret_cast<hipStream_t>(stream), batch, in_h, in_w,
                      reinterpret_cast<const bf16_t*>(x), (int)x_ldc,
                      reinterpret_cast<const bf16_t*>(w1), w1_kpad, b1,
