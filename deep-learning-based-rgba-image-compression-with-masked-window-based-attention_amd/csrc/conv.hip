@@ -1719,6 +1719,10 @@ static bool pw2_ok(const ConvArgsDev& d) {
 }
 
 static void launch_pw(const ConvArgsDev& d, int cin_max, hipStream_t st) {
+  if (pw3_ok(d, cin_max)) {                        // GDN / IGDN forward: pw3.hip
+    launch_pw3(d, st);
+    return;
+  }
   if (pw2_ok(d)) {
     if (cin_max <= 64) launch_pw2_k<2>(d, st);
     else if (cin_max <= 128) launch_pw2_k<4>(d, st);

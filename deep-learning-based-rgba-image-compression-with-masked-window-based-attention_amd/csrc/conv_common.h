@@ -463,6 +463,10 @@ __device__ __forceinline__ float gauss_elem_y(const ConvGroup& g, int m, int c, 
   return fminf(fmaxf(bits, 0.0f), 50.0f);
 }
 
+// the two-deep pointwise GDN / IGDN forward (pw3.hip), dispatched by conv.hip's launch_pw
+bool pw3_ok(const ConvArgsDev& d, int cin_max);
+void launch_pw3(const ConvArgsDev& d, hipStream_t st);
+
 typedef __attribute__((address_space(3))) void* lptr_t;
 
 // One LDS-DMA piece: each lane moves 16 bytes from its own global address to

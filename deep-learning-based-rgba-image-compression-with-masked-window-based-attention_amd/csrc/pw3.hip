@@ -1,0 +1,180 @@
+// Pointwise GDN / IGDN forward with a two-deep input pipeline (conv_pw3_kernel).
+// Reference: layers/GDN.py:64-94 -- out = x / sqrt(beta' + gamma' . x^2) (IGDN: * sqrt), the
+// norm pool a 1x1 conv over bf16(x^2).
+//
+// conv_pw2_kernel (conv.hip) keeps ONE 16-pixel input tile per wave in LDS: the next tile's
+// LDS-DMA goes out after this tile's MFMAs and has to land before the next MFMAs start, so a
+// wave has at most one tile in flight and waits one memory latency per tile.  On the
+// multi-round launches (the 256^2 and 512^2 GDN / IGDN of config 4: 16-64 tiles per wave) that
+// latency, not HBM or the MFMAs, set the time (2.66 TB/s on the 512^2 IGDN).  Here each wave
+// owns TWO tile slots: tile k+2's DMA is issued while tile k computes, and the wait before
+// tile k+1 retires only the DMA issued one iteration earlier (counted vmcnt: the epilogue's
+// stores and the newest DMA stay in flight).  The residual-register sets of conv_pw2_kernel
+// (res0 / res1 / res2 quads, double-buffered) are gone: the only epilogue operand, x, comes
+// from the LDS tile the MFMAs consumed.  Six waves (two slots of 6 KiB each + the 72 KiB
+// weight panel = 144 KiB of LDS).
+//
+// Same MFMA order, the same bf16(x^2) B fragments and the same epilogue arithmetic as
+// conv_pw2_kernel's GDN / IGDN instance, so the two are bit-identical.
+#include <cstdlib>
+
+#include "common.h"
+#include "conv_common.h"
+
+namespace rgbac {
+
+constexpr int kPw3Waves = 6;
+
+template <int NKS, int ACT>
+__global__ void __launch_bounds__(64 * kPw3Waves, 1) conv_pw3_kernel(const ConvArgsDev args) {
+  constexpr int NT = 12, BN = 192, NCH = 4 * NKS, NW = kPw3Waves, TS = 24;
+  static_assert(NCH % 8 == 0 && NCH <= TS, "swizzle groups of 8 chunks");
+  constexpr int NPIECE = BN * NCH / 64;            // 1-KiB LDS-DMA pieces of the panel
+  constexpr int XP = 16 * TS / 64;                 // pieces of one 16-pixel tile (6)
+  constexpr int XS = 16 * TS;                      // uint4 slots of one tile
+  extern __shared__ __attribute__((aligned(16))) uint4 lds[];
+  __shared__ float bl[BN];
+  const ConvShared& s = args.s;
+  const ConvGroup& g = args.g[blockIdx.z];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int nchunk = g.cin_pad >> 3;
+  const int Mtot = s.M;
+  const int ld = (int)g.sld0;
+  const uint32_t lbase = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(lptr_t)lds);
+  const uint32_t xbase = lbase + (uint32_t)(BN * NCH + wave * 2 * XS) * 16u;
+  const uint4* const X0 = lds + BN * NCH + wave * 2 * XS;
+  {
+    const bf16_t* wbase = reinterpret_cast<const bf16_t*>(g.w);
+    for (int p = wave; p < NPIECE; p += NW) {
+      const int d = p * 64 + lane;
+      const int row = d / NCH, slot = d - (d / NCH) * NCH;
+      const int ch = slot ^ (row & 7);
+      const bool ok = row < g.rows && ch < nchunk;
+      dma16_l(ok ? (const void*)(wbase + (size_t)row * g.k_pad + ch * 8) : (const void*)g_zero_page,
+              lbase + p * 1024);
+    }
+  }
+  for (int e = tid; e < BN; e += 64 * NW) bl[e] = g.bias ? g.bias[e] : 0.0f;
+
+  const char* const src = reinterpret_cast<const char*>(g.sp0);
+  const int ntile = (Mtot + 15) / 16;
+  const int tstride = gridDim.x * NW;
+  int tile = blockIdx.x * NW + wave;
+
+  // tile t_ -> slot sl_ of this wave (rows past M and padding chunks read the zero page);
+  // always XP pieces, so the counted waits below are exact
+  auto dma_tile = [&](int t_, int sl_) {
+#pragma unroll
+    for (int p = 0; p < XP; ++p) {
+      const int d = p * 64 + lane;
+      const int row = d / TS, slot = d - (d / TS) * TS;
+      const int ch = slot ^ (row & 7);
+      const int m = t_ * 16 + row;
+      const bool ok = m < Mtot && ch < nchunk;
+      dma16_l(ok ? (const void*)(src + ((size_t)m * ld + ch * 8) * 2) : (const void*)g_zero_page,
+              xbase + (uint32_t)(sl_ * XS * 16) + p * 1024);
+    }
+  };
+  dma_tile(tile, 0);
+  dma_tile(tile + tstride, 1);
+  wait_vm<XP>();                                   // the panel and slot 0 (slot 1 in flight)
+  __syncthreads();
+  bf16_t* const out = reinterpret_cast<bf16_t*>(g.out);
+  for (int k = 0; tile < ntile; tile += tstride, ++k) {
+    // slot k & 1 holds tile k: its DMA was issued two iterations back (or in the prologue);
+    // younger than it are that iteration's stores (NT), the next DMA (XP) and the last
+    // iteration's stores (NT)
+    if (k == 1) wait_vm<XP + NT>();
+    else if (k > 1) wait_vm<2 * NT + XP>();
+    const uint4* const Xl = X0 + (k & 1) * XS;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int st = 0; st < NKS; ++st) {
+      const int slot = (4 * st + fq) ^ (fr & 7);
+      const uint4 b = square_chunk<bf16_t>(Xl[fr * TS + slot]);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) mma_step<bf16_t>(acc[j], lds[(16 * j + fr) * NCH + slot], b);
+    }
+    uint2 xq[NT];                                  // the epilogue's x quads, from the same tile
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int c = 2 * j + (fq >> 1);
+      xq[j] = *reinterpret_cast<const uint2*>(
+          reinterpret_cast<const char*>(Xl + fr * TS + (c ^ (fr & 7))) + 8 * (fq & 1));
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // slot reads done before its refill
+    dma_tile(tile + 2 * tstride, k & 1);
+    const int m = tile * 16 + fr;
+    if (m < Mtot) {
+      bf16_t* const orow = out + (long long)m * g.out_ldc + g.out_coff;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = 16 * j + 4 * fq;
+        const float x4[4] = {bf2f(xq[j].x & 0xFFFF), bf2f(xq[j].x >> 16), bf2f(xq[j].y & 0xFFFF),
+                             bf2f(xq[j].y >> 16)};
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float nrm = acc[j][r] + bl[n + r];
+          v[r] = ACT == RGBAC_ACT_GDN ? gdn_t<bf16_t>(x4[r], nrm) : igdn_t<bf16_t>(x4[r], nrm);
+        }
+        Elem<bf16_t>::st4(orow + n, v);
+      }
+    }
+  }
+  wait_vm<0>();                                    // no DMA may land after the workgroup ends
+}
+
+// conv_pw3_kernel's shapes: the bf16 GDN / IGDN norm pool -- one source whose x is also the
+// epilogue's (square input, res1 == the input), 192 outputs, no other residual, no
+// pre-activation store.  RGBAC_PW3=0 keeps conv_pw2_kernel (A/B switch).
+bool pw3_ok(const ConvArgsDev& d, int cin_max) {
+  const char* e = getenv("RGBAC_PW3");              // read per launch (tests switch it)
+  const bool on = !(e && e[0] == '0');
+  if (!on || (d.s.act != RGBAC_ACT_GDN && d.s.act != RGBAC_ACT_IGDN) || !d.s.square ||
+      d.s.mode != RGBAC_CONV || cin_max <= 128 || cin_max > 192)
+    return false;
+  for (int i = 0; i < d.s.ngroups; ++i) {
+    const ConvGroup& g = d.g[i];
+    if (g.res1 != g.sp0 || g.ld1 != g.sld0 || g.res0 || g.res2 || g.zout || g.cout != 192 ||
+        g.rows < 192 || g.out_coff % 8 || g.out_ldc % 8 || g.sld0 % 8 || g.k_pad < g.cin_pad)
+      return false;
+  }
+  return true;
+}
+
+template <int ACT>
+static void launch_pw3_k(const ConvArgsDev& d, hipStream_t st) {
+  auto kern = conv_pw3_kernel<6, ACT>;
+  constexpr size_t lds = ((size_t)192 * 24 + (size_t)kPw3Waves * 2 * 16 * 24) * 16;
+  static bool attr = false;
+  static int ncu = 0;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (ncu < 1) ncu = 256;
+    (void)hipGetLastError();
+    attr = true;
+  }
+  const int nz = d.s.ngroups;
+  const int ntile = (d.s.M + 15) / 16;
+  int gx = (ncu + nz - 1) / nz;
+  const int need = (ntile + kPw3Waves - 1) / kPw3Waves;
+  if (gx > need) gx = need;
+  if (gx < 1) gx = 1;
+  hipLaunchKernelGGL(kern, dim3(gx, 1, nz), dim3(64 * kPw3Waves), lds, st, d);
+}
+
+void launch_pw3(const ConvArgsDev& d, hipStream_t st) {
+  if (d.s.act == RGBAC_ACT_GDN) launch_pw3_k<RGBAC_ACT_GDN>(d, st);
+  else launch_pw3_k<RGBAC_ACT_IGDN>(d, st);
+}
+
+}  // namespace rgbac

@@ -648,6 +648,26 @@ def _pw2_admits(preps):
     return True
 
 
+_PW3_ON = os.environ.get("RGBAC_PW3", "1") != "0"
+
+
+def _pw3_admits(preps):
+    """Host mirror of csrc/pw3.hip pw3_ok: the two-deep GDN / IGDN forward kernel."""
+    a0 = preps[0].a
+    if not _PW3_ON or a0.act not in (ACT["gdn"], ACT["igdn"]) or not a0.square_input or \
+            a0.mode != CONV:
+        return False
+    if not 128 < max(p.a.cin_pad for p in preps) <= 192:
+        return False
+    for p in preps:
+        a = p.a
+        if a.res1 != a.src[0].ptr or a.res1_ldc != a.src[0].ldc or a.res0 or a.res2 or \
+                a.zout or a.cout != 192 or a.out_coff % 8 or a.out_ldc % 8 or \
+                a.src[0].ldc % 8 or a.k_pad < a.cin_pad:
+            return False
+    return True
+
+
 def kernel_name(tile, preps):
     """rocprofv3-style name (namespace and argument list stripped) of a conv launch."""
     dt = "float" if preps[0].a.dtype == 0 else "bf16_t"
@@ -675,6 +695,8 @@ def kernel_name(tile, preps):
         nks = 2 if cin <= 64 else (4 if cin <= 128 else 6)
         # csrc/conv.hip launch_pw: conv_pw2_kernel where pw2_ok admits the launch, else
         # conv_pw_kernel (32-deep k-steps held in LDS: 2 / 4 / 6)
+        if _pw3_admits(preps):
+            return f"conv_pw3_kernel<6, {preps[0].a.act}>"
         if _pw2_admits(preps):
             return f"conv_pw2_kernel<{nks}>"
         dact = "true" if preps[0].a.act in (ACT["dgelu"], ACT["dlrelu"]) else "false"

@@ -438,6 +438,42 @@ def test_conv_smallk_tile(device, cin, cout, k, s, act):
         rt.FORCE = None
 
 
+@pytest.mark.parametrize("kind", ["gdn", "igdn"])
+@pytest.mark.parametrize("B,H,W", [(3, 46, 70), (8, 128, 128), (1, 4, 4), (2, 64, 64)])
+def test_pw3_matches_pw2(device, monkeypatch, kind, B, H, W):
+    """conv_pw3_kernel (csrc/pw3.hip: the GDN / IGDN norm pool with two input tiles in flight
+    per wave) against conv_pw2_kernel (RGBAC_PW3=0) on the same launch: the same MFMA order and
+    epilogue arithmetic, so bit-identical -- ragged (a partial last tile), one tile, and 8192
+    tiles (up to six per wave: every slot of the two-deep ring refilled several times)."""
+    rt = _rt()
+    g = _gen(77 + B * H)
+    dt = torch.bfloat16
+    m = nn.Conv2d(192, 192, 1)
+    with torch.no_grad():
+        m.weight.copy_(0.1 * torch.rand(192, 192, 1, 1, generator=g))
+        m.bias.copy_(0.5 + torch.rand(192, generator=g))
+    md = m.to(device)
+    fx = rt.to_nhwc(torch.randn((B, 192, H, W), generator=g).to(device), dt)
+    pk = rt.packed(md, dt, [(192, 192)])
+    outs = {}
+    rt.FORCE = (rt.TILE_PW, 1)
+    try:
+        for mode in ("0", "1"):
+            monkeypatch.setenv("RGBAC_PW3", mode)
+            with torch.no_grad():
+                o = rt.conv(pk, [fx.src()], square=True, act=kind, res1=fx)
+            torch.cuda.synchronize()
+            outs[mode] = o.t.clone()
+    finally:
+        rt.FORCE = None
+    assert torch.equal(outs["1"].view(torch.int16), outs["0"].view(torch.int16))
+    ref = rt.to_nchw(fx).float()
+    with torch.no_grad():
+        nrm = F.conv2d(ref.bfloat16().float() ** 2, md.weight.bfloat16().float(), md.bias.float())
+        want = ref * (torch.rsqrt(nrm) if kind == "gdn" else torch.sqrt(nrm))
+    assert rel(rt.to_nchw(rt.Feat(outs["1"], 192)).float(), want) < 2e-2
+
+
 @pytest.mark.parametrize("cin,cout,kind", [(192, 192, "gelu"), (3, 32, "none"), (32, 3, "none"),
                                            (80, 40, "gelu"), (96, 80, "none"), (192, 100, "relu"),
                                            (192, 192, "gdn"), (192, 192, "igdn"), (80, 80, "igdn"),
