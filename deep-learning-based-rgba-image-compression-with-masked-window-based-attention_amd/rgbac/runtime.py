@@ -654,16 +654,21 @@ _PW3_ON = os.environ.get("RGBAC_PW3", "1") != "0"
 def _pw3_admits(preps):
     """Host mirror of csrc/pw3.hip pw3_ok: the two-deep GDN / IGDN forward kernel."""
     a0 = preps[0].a
-    if not _PW3_ON or a0.act not in (ACT["gdn"], ACT["igdn"]) or not a0.square_input or \
-            a0.mode != CONV:
+    gate = a0.act == ACT["gate"] and preps[0].mgrid >= 8192 * 16
+    if not _PW3_ON or (a0.act not in (ACT["gdn"], ACT["igdn"]) and not gate) or \
+            bool(a0.square_input) == gate or a0.mode != CONV:
         return False
     if not 128 < max(p.a.cin_pad for p in preps) <= 192:
         return False
     for p in preps:
         a = p.a
-        if a.res1 != a.src[0].ptr or a.res1_ldc != a.src[0].ldc or a.res0 or a.res2 or \
-                a.zout or a.cout != 192 or a.out_coff % 8 or a.out_ldc % 8 or \
+        if a.res0 or a.zout or a.cout != 192 or a.out_coff % 8 or a.out_ldc % 8 or \
                 a.src[0].ldc % 8 or a.k_pad < a.cin_pad:
+            return False
+        if gate:
+            if not a.res1 or not a.res2 or a.res1_ldc % 4 or a.res2_ldc % 4:
+                return False
+        elif a.res1 != a.src[0].ptr or a.res1_ldc != a.src[0].ldc or a.res2:
             return False
     return True
 

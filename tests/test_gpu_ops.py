@@ -438,13 +438,16 @@ def test_conv_smallk_tile(device, cin, cout, k, s, act):
         rt.FORCE = None
 
 
-@pytest.mark.parametrize("kind", ["gdn", "igdn"])
+@pytest.mark.parametrize("kind", ["gdn", "igdn", "gate"])
 @pytest.mark.parametrize("B,H,W", [(3, 46, 70), (8, 128, 128), (1, 4, 4), (2, 64, 64)])
 def test_pw3_matches_pw2(device, monkeypatch, kind, B, H, W):
-    """conv_pw3_kernel (csrc/pw3.hip: the GDN / IGDN norm pool with two input tiles in flight
-    per wave) against conv_pw2_kernel (RGBAC_PW3=0) on the same launch: the same MFMA order and
-    epilogue arithmetic, so bit-identical -- ragged (a partial last tile), one tile, and 8192
-    tiles (up to six per wave: every slot of the two-deep ring refilled several times)."""
+    """conv_pw3_kernel (csrc/pw3.hip: the GDN / IGDN norm pool and the attention gate with two
+    input tiles in flight per wave) against conv_pw2_kernel (RGBAC_PW3=0) on the same launch:
+    the same MFMA order and epilogue arithmetic, so GDN / IGDN are bit-identical (the gate up to
+    multiply-add contraction; the gate takes pw3 from 8192 tiles on, i.e. here only at 8 x 128^2)
+    -- ragged (a partial last tile), one tile, and 8192 tiles (up to
+    six per wave: every slot of the two-deep ring refilled several times); and against fp32
+    torch on the same bf16 operands."""
     rt = _rt()
     g = _gen(77 + B * H)
     dt = torch.bfloat16
@@ -454,6 +457,8 @@ def test_pw3_matches_pw2(device, monkeypatch, kind, B, H, W):
         m.bias.copy_(0.5 + torch.rand(192, generator=g))
     md = m.to(device)
     fx = rt.to_nhwc(torch.randn((B, 192, H, W), generator=g).to(device), dt)
+    fa = rt.to_nhwc(torch.randn((B, 192, H, W), generator=g).to(device), dt)
+    fr = rt.to_nhwc(torch.randn((B, 192, H, W), generator=g).to(device), dt)
     pk = rt.packed(md, dt, [(192, 192)])
     outs = {}
     rt.FORCE = (rt.TILE_PW, 1)
@@ -461,16 +466,34 @@ def test_pw3_matches_pw2(device, monkeypatch, kind, B, H, W):
         for mode in ("0", "1"):
             monkeypatch.setenv("RGBAC_PW3", mode)
             with torch.no_grad():
-                o = rt.conv(pk, [fx.src()], square=True, act=kind, res1=fx)
+                if kind == "gate":                 # a * sigmoid(W x + b) + r
+                    o = rt.conv(pk, [fx.src()], act="gate", res1=fa, res2=fr)
+                else:
+                    o = rt.conv(pk, [fx.src()], square=True, act=kind, res1=fx)
             torch.cuda.synchronize()
             outs[mode] = o.t.clone()
     finally:
         rt.FORCE = None
-    assert torch.equal(outs["1"].view(torch.int16), outs["0"].view(torch.int16))
+    same = outs["1"].view(torch.int16) == outs["0"].view(torch.int16)
+    d = (outs["1"].float() - outs["0"].float()).abs()
+    print(f"{kind} {B}x{H}x{W}: {int((~same).sum())} of {same.numel()} differ, max {d.max().item():.3g}")
+    if kind == "gate":
+        # a * sigmoid(z) + r: the two compilations contract the multiply-add differently, so
+        # a few elements (8 of 25 M at 8 x 128^2) round differently -- by at most one bf16 ulp
+        # of the operands' scale (a result near zero is a cancellation of a * s and r)
+        assert d.max().item() <= 2.0 ** -8 * outs["0"].float().abs().max().item()
+        assert (~same).float().mean().item() < 1e-5
+    else:
+        assert same.all()
     ref = rt.to_nchw(fx).float()
     with torch.no_grad():
-        nrm = F.conv2d(ref.bfloat16().float() ** 2, md.weight.bfloat16().float(), md.bias.float())
-        want = ref * (torch.rsqrt(nrm) if kind == "gdn" else torch.sqrt(nrm))
+        if kind == "gate":
+            z = F.conv2d(ref, md.weight.bfloat16().float(), md.bias.float())
+            want = rt.to_nchw(fa).float() * torch.sigmoid(z) + rt.to_nchw(fr).float()
+        else:
+            nrm = F.conv2d(ref.bfloat16().float() ** 2, md.weight.bfloat16().float(),
+                           md.bias.float())
+            want = ref * (torch.rsqrt(nrm) if kind == "gdn" else torch.sqrt(nrm))
     assert rel(rt.to_nchw(rt.Feat(outs["1"], 192)).float(), want) < 2e-2
 
 
