@@ -347,8 +347,8 @@ __global__ void __launch_bounds__(256, OCC) ru_fused_kernel(const RuArgsDev args
 //   stage 2: T2 = act(W2 (*) T1 + b2), 48 rows x K 9 taps x 64 (40 real)
 //   stage 3: y  = [GELU](W3 T2 + b3 + x), 80 rows x K 64 (40 real)
 // T1 / T2 pixels are 128-B rows (64 channels, 40..63 zero), chunk c at slot c ^ (p & 7).
-// LDS 73 KiB weights + 22 KiB maps: one workgroup per CU, 4 waves; per wave 18 + 54 + 10
-// MFMAs.  Three launches (and two HBM round trips of the 40-channel maps) become one.
+// LDS 73 KiB weights + 22 KiB maps: one workgroup per CU, 4 waves, persistent over tiles (at
+// config 4's 128^2 latent, 8 tiles per workgroup); per wave and tile 18 + 54 + 10 MFMAs.  Three launches (and two HBM round trips of the 40-channel maps) become one.
 typedef __attribute__((address_space(3))) void* ru_lptr_t;
 // one LDS-DMA piece: each lane moves 16 bytes from src to lds + 16 * lane (M0 saved / restored;
 // waited for by an explicit s_waitcnt)
@@ -381,11 +381,7 @@ __global__ void __launch_bounds__(256, 1) ru_small_kernel(const RuArgsDev args) 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n = lane & 15, q = lane >> 4;
   const int tx_n = args.W / 8, ty_n = args.H / 8;
-  int t = blockIdx.x;
-  const int tx = t % tx_n; t /= tx_n;
-  const int ty = t % ty_n;
-  const int b = t / ty_n;
-  const int y0 = ty * 8, x0 = tx * 8;
+  const int ntiles = args.batch * tx_n * ty_n;
 
   // weights: the three fragment-major packs (1 KiB per fragment) land in LDS by LDS-DMA, one
   // piece per wave instruction with no wait in between -- the register-staged copy loop it
@@ -409,119 +405,157 @@ __global__ void __launch_bounds__(256, 1) ru_small_kernel(const RuArgsDev args) 
   }
   // stage-1 input fragments straight from HBM: halo pixel 16f + n, channels 32ks + 8q
   constexpr int F1 = 2;                                  // fragments w, w + 4 (< 7)
-  uint4 xb[F1][3];
-  bool xin[F1];
-#pragma unroll
-  for (int i = 0; i < F1; ++i) {
-    const int hp = 16 * (wave + 4 * i) + n;
-    const int hy = hp / HX, hx = hp - hy * HX;
-    const int iy = y0 + hy - 1, ix = x0 + hx - 1;
-    xin[i] = hp < NH && iy >= 0 && iy < args.H && ix >= 0 && ix < args.W;
-    const bf16_t* row = g.x + ((long long)(b * args.H + (xin[i] ? iy : 0)) * args.W +
-                               (xin[i] ? ix : 0)) * g.ldx;
-#pragma unroll
-    for (int ks = 0; ks < 3; ++ks) {
-      const int c8 = 4 * ks + q;                         // 8-channel chunk (10 real)
-      xb[i][ks] = (xin[i] && c8 < 10) ? *reinterpret_cast<const uint4*>(row + 8 * c8)
-                                      : make_uint4(0, 0, 0, 0);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this wave's weight pieces landed
-  __syncthreads();
-
-  // ================= stage 1
-  {
-    f32x4 acc[3][F1];
-#pragma unroll
-    for (int tt = 0; tt < 3; ++tt)
-#pragma unroll
-      for (int i = 0; i < F1; ++i) acc[tt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 3; ++ks)
-#pragma unroll
-      for (int tt = 0; tt < 3; ++tt) {
-        const uint4 a = Ws[(tt * 3 + ks) * 64 + lane];
-#pragma unroll
-        for (int i = 0; i < F1; ++i)
-          if (wave + 4 * i < 7) mma_step<bf16_t>(acc[tt][i], a, xb[i][ks]);
-      }
+  uint4 xb[F1][3], xn[F1][3];
+  bool xin[F1], xinn[F1];
+  uint2 rx[5], rxn[5];                                   // stage 3's residual quads
+  const int p = 16 * wave + n, py = p >> 3, px = p & 7;  // this lane's stage-2 / 3 pixel
+  auto load_x = [&](int tt, uint4 (&dst)[F1][3], bool (&in)[F1], uint2 (&rd)[5]) {
+    const int tx = tt % tx_n, ty = (tt / tx_n) % ty_n, b = tt / (tx_n * ty_n);
 #pragma unroll
     for (int i = 0; i < F1; ++i) {
       const int hp = 16 * (wave + 4 * i) + n;
-      if (wave + 4 * i >= 7) continue;
+      const int hy = hp / HX, hx = hp - hy * HX;
+      const int iy = ty * 8 + hy - 1, ix = tx * 8 + hx - 1;
+      in[i] = hp < NH && iy >= 0 && iy < args.H && ix >= 0 && ix < args.W;
+      const bf16_t* row = g.x + ((long long)(b * args.H + (in[i] ? iy : 0)) * args.W +
+                                 (in[i] ? ix : 0)) * g.ldx;
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) {
+        const int c8 = 4 * ks + q;                       // 8-channel chunk (10 real)
+        dst[i][ks] = (in[i] && c8 < 10) ? *reinterpret_cast<const uint4*>(row + 8 * c8)
+                                        : make_uint4(0, 0, 0, 0);
+      }
+    }
+    const bf16_t* xr = g.x + ((long long)(b * args.H + ty * 8 + py) * args.W + tx * 8 + px) * g.ldx;
+#pragma unroll
+    for (int tt2 = 0; tt2 < 5; ++tt2) rd[tt2] = *reinterpret_cast<const uint2*>(xr + 16 * tt2 + 4 * q);
+  };
+  int t = blockIdx.x;
+  if (t >= ntiles) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (no DMA may land after the exit)
+    return;
+  }
+  load_x(t, xb, xin, rx);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this wave's weight pieces landed
+  __syncthreads();
+
+  // persistent over tiles (the 73 KiB of weights staged once per workgroup, not per tile): the
+  // next tile's stage-1 fragments load while this tile runs stages 2 and 3.  T1 is rewritten
+  // only after every wave passed the barrier behind stage 2 (its last reader); T2 rows are
+  // wave-private.
+  for (;;) {
+    const int tx = t % tx_n, ty = (t / tx_n) % ty_n, b = t / (tx_n * ty_n);
+    const int y0 = ty * 8, x0 = tx * 8;
+    const int tnext = t + gridDim.x;
+
+    // ================= stage 1
+    {
+      f32x4 acc[3][F1];
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt)
+#pragma unroll
+        for (int i = 0; i < F1; ++i) acc[tt][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks)
+#pragma unroll
+        for (int tt = 0; tt < 3; ++tt) {
+          const uint4 a = Ws[(tt * 3 + ks) * 64 + lane];
+#pragma unroll
+          for (int i = 0; i < F1; ++i)
+            if (wave + 4 * i < 7) mma_step<bf16_t>(acc[tt][i], a, xb[i][ks]);
+        }
+      if (tnext < ntiles) load_x(tnext, xn, xinn, rxn);         // consumed: the next tile's go out
+#pragma unroll
+      for (int i = 0; i < F1; ++i) {
+        const int hp = 16 * (wave + 4 * i) + n;
+        if (wave + 4 * i >= 7) continue;
+#pragma unroll
+        for (int tt = 0; tt < 3; ++tt) {
+          const int c0 = 16 * tt + 4 * q;
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = xin[i] ? ru_act<RB>(acc[tt][i][r] + bs[c0 + r]) : 0.0f;
+          *reinterpret_cast<uint2*>(reinterpret_cast<unsigned char*>(T1) + hp * 128 +
+                                    (((c0 >> 3) ^ (hp & 7)) << 4) + 2 * (c0 & 7)) =
+              make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+        }
+      }
+    }
+    __syncthreads();
+
+    // ================= stage 2 (wave w: output pixels 16w .. 16w+15 = rows 2w, 2w+1)
+    {
+      f32x4 acc[3];
+#pragma unroll
+      for (int tt = 0; tt < 3; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 18; ++kk) {
+        const int tap = kk >> 1, c8 = 4 * (kk & 1) + q;
+        const int hp = (py + tap / 3) * HX + px + tap % 3;
+        const uint4 bv = T1[hp * 8 + (c8 ^ (hp & 7))];
+#pragma unroll
+        for (int tt = 0; tt < 3; ++tt)
+          mma_step<bf16_t>(acc[tt], Ws[(W1F + tt * 18 + kk) * 64 + lane], bv);
+      }
 #pragma unroll
       for (int tt = 0; tt < 3; ++tt) {
         const int c0 = 16 * tt + 4 * q;
         float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = xin[i] ? ru_act<RB>(acc[tt][i][r] + bs[c0 + r]) : 0.0f;
-        *reinterpret_cast<uint2*>(reinterpret_cast<unsigned char*>(T1) + hp * 128 +
-                                  (((c0 >> 3) ^ (hp & 7)) << 4) + 2 * (c0 & 7)) =
+        for (int r = 0; r < 4; ++r) v[r] = ru_act<RB>(acc[tt][r] + bs[48 + c0 + r]);
+        *reinterpret_cast<uint2*>(reinterpret_cast<unsigned char*>(T2) + p * 128 +
+                                  (((c0 >> 3) ^ (p & 7)) << 4) + 2 * (c0 & 7)) =
             make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
       }
     }
-  }
-  __syncthreads();
-
-  // ================= stage 2 (wave w: output pixels 16w .. 16w+15 = rows 2w, 2w+1)
-  const int p = 16 * wave + n, py = p >> 3, px = p & 7;
-  {
-    f32x4 acc[3];
+    __syncthreads();                                       // (T2 rows are wave-private: a
+                                                           //  wave reads only its own pixels)
+    // ================= stage 3: y = [GELU](W3 T2 + b3 + x)
+    {
+      f32x4 acc[5];
 #pragma unroll
-    for (int tt = 0; tt < 3; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int tt = 0; tt < 5; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int kk = 0; kk < 18; ++kk) {
-      const int tap = kk >> 1, c8 = 4 * (kk & 1) + q;
-      const int hp = (py + tap / 3) * HX + px + tap % 3;
-      const uint4 bv = T1[hp * 8 + (c8 ^ (hp & 7))];
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c8 = 4 * ks + q;
+        const uint4 bv = T2[p * 8 + (c8 ^ (p & 7))];
 #pragma unroll
-      for (int tt = 0; tt < 3; ++tt)
-        mma_step<bf16_t>(acc[tt], Ws[(W1F + tt * 18 + kk) * 64 + lane], bv);
-    }
-#pragma unroll
-    for (int tt = 0; tt < 3; ++tt) {
-      const int c0 = 16 * tt + 4 * q;
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = ru_act<RB>(acc[tt][r] + bs[48 + c0 + r]);
-      *reinterpret_cast<uint2*>(reinterpret_cast<unsigned char*>(T2) + p * 128 +
-                                (((c0 >> 3) ^ (p & 7)) << 4) + 2 * (c0 & 7)) =
-          make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
-    }
-  }
-  __syncthreads();                                       // (T2 rows are wave-private: a
-                                                         //  wave reads only its own pixels)
-  // ================= stage 3: y = [GELU](W3 T2 + b3 + x)
-  {
-    f32x4 acc[5];
-#pragma unroll
-    for (int tt = 0; tt < 5; ++tt) acc[tt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int c8 = 4 * ks + q;
-      const uint4 bv = T2[p * 8 + (c8 ^ (p & 7))];
-#pragma unroll
-      for (int tt = 0; tt < 5; ++tt)
-        mma_step<bf16_t>(acc[tt], Ws[(W1F + W2F + tt * 2 + ks) * 64 + lane], bv);
-    }
-    const int gy = y0 + py, gx = x0 + px;
-    const long long pix = (long long)(b * args.H + gy) * args.W + gx;
-    const bf16_t* xr = g.x + pix * g.ldx;
-    bf16_t* orow = g.out + pix * g.ldo;
-    float res[5][4];
-#pragma unroll
-    for (int tt = 0; tt < 5; ++tt) Elem<bf16_t>::ld4(xr + 16 * tt + 4 * q, res[tt]);
-#pragma unroll
-    for (int tt = 0; tt < 5; ++tt) {
-      const int c0 = 16 * tt + 4 * q;
-      float v[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float t3 = acc[tt][r] + bs[96 + c0 + r] + res[tt][r];
-        v[r] = RB ? t3 : ru_gelu(t3);
+        for (int tt = 0; tt < 5; ++tt)
+          mma_step<bf16_t>(acc[tt], Ws[(W1F + W2F + tt * 2 + ks) * 64 + lane], bv);
       }
-      Elem<bf16_t>::st4(orow + c0, v);
+      const int gy = y0 + py, gx = x0 + px;
+      const long long pix = (long long)(b * args.H + gy) * args.W + gx;
+      bf16_t* orow = g.out + pix * g.ldo;
+      float res[5][4];                                   // (prefetched with the x fragments)
+#pragma unroll
+      for (int tt = 0; tt < 5; ++tt) {
+        res[tt][0] = bf2f(rx[tt].x & 0xFFFF);
+        res[tt][1] = bf2f(rx[tt].x >> 16);
+        res[tt][2] = bf2f(rx[tt].y & 0xFFFF);
+        res[tt][3] = bf2f(rx[tt].y >> 16);
+      }
+#pragma unroll
+      for (int tt = 0; tt < 5; ++tt) {
+        const int c0 = 16 * tt + 4 * q;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float t3 = acc[tt][r] + bs[96 + c0 + r] + res[tt][r];
+          v[r] = RB ? t3 : ru_gelu(t3);
+        }
+        Elem<bf16_t>::st4(orow + c0, v);
+      }
     }
+    if (tnext >= ntiles) break;
+    t = tnext;
+#pragma unroll
+    for (int i = 0; i < F1; ++i) {
+      xin[i] = xinn[i];
+#pragma unroll
+      for (int ks = 0; ks < 3; ++ks) xb[i][ks] = xn[i][ks];
+    }
+#pragma unroll
+    for (int tt = 0; tt < 5; ++tt) rx[tt] = rxn[tt];
   }
 }
 
@@ -1119,8 +1153,19 @@ extern "C" int rgbac_residual_unit_ex(const rgbac_ru_args* args, int ngroups, in
   if (a->channels == 80) {
     const long long tiles = (long long)a->batch * (a->h / 8) * (a->w / 8);
     RGBAC_REQUIRE(tiles < (1ll << 31), "too many tiles");
-    if (kind) hipLaunchKernelGGL(ru_small_kernel<1>, dim3((unsigned)tiles, 1, ngroups), dim3(256), 0, st, d);
-    else hipLaunchKernelGGL(ru_small_kernel<0>, dim3((unsigned)tiles, 1, ngroups), dim3(256), 0, st, d);
+    // one workgroup per CU over all groups (a workgroup stages its group's weights once)
+    static int ncu = 0;
+    if (ncu == 0) {
+      int dev = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      if (ncu < 1) ncu = 256;
+    }
+    long long gx = ncu / ngroups;
+    if (gx < 1) gx = 1;
+    if (gx > tiles) gx = tiles;
+    if (kind) hipLaunchKernelGGL(ru_small_kernel<1>, dim3((unsigned)gx, 1, ngroups), dim3(256), 0, st, d);
+    else hipLaunchKernelGGL(ru_small_kernel<0>, dim3((unsigned)gx, 1, ngroups), dim3(256), 0, st, d);
     return check_launch("ru_small_kernel");
   }
   if (a->w1_kpad == 0) {                             // fragment-major packs: streamed kernel
