@@ -46,22 +46,6 @@ def main():
         with torch.no_grad():
             return net(x, a, a, *me)
 
-    # ---- record every launch's key and prepared convs (one eager forward)
-    seen = {}
-    orig_launch = rt.launch
-
-    def rec_launch(preps, force=None):
-        key = f"{preps[0].key}/g{len(preps)}"
-        if key not in seen and force is None and preps[0].a.act != rt.ACT["gauss"]:
-            seen[key] = preps
-        return orig_launch(preps, force=force)
-    rt.launch = rec_launch
-    step()
-    torch.cuda.synchronize()
-    rt.launch = orig_launch
-    print(f"{len(seen)} launch shapes", flush=True)
-
-    # ---- cold timing of each shape's candidates (the tuner's method)
     flush = torch.zeros(16 << 20, device=dev)
 
     def cands_of(preps):
@@ -78,15 +62,24 @@ def main():
             c.append((rt.TILE_NPATCH, 1))
         return c
 
+    # ---- cold timing of each shape's candidates (the tuner's method) INSIDE one eager forward,
+    # at the launch itself while its operands are live: a recorded launch replayed after the
+    # forward would write through pointers the allocator has since handed to other tensors.
+    # A launch that accumulates into its output in place (res0 == out) is not timed; the
+    # launch's own choice runs last, so the forward's values are those of a normal forward.
     short = {}
-    with torch.no_grad():
-        for key, preps in seen.items():
+    orig_launch = rt.launch
+
+    def tune_launch(preps, force=None):
+        key = f"{preps[0].key}/g{len(preps)}"
+        inplace = any(p.a.res0 and p.a.res0 == p.a.out for p in preps)
+        if (key not in short and force is None and preps[0].a.act != rt.ACT["gauss"] and
+                not inplace):
             res = []
             for c in cands_of(preps):
                 try:
                     orig_launch(preps, force=c)
-                    torch.cuda.synchronize()
-                except RuntimeError:
+                except RuntimeError:               # preconditions refused (nothing launched)
                     continue
                 us = 0.0
                 for _ in range(3):
@@ -101,10 +94,13 @@ def main():
                 res.append((us, tuple(c)))
             res.sort()
             cur = tuple(rt._tune_cache.get(key, ()))
-            alts = [c for _, c in res[:args.top] if c != cur]
-            short[key] = alts
-    seen.clear()
+            short[key] = [c for _, c in res[:args.top] if c != cur]
+        return orig_launch(preps, force=force)
+    rt.launch = tune_launch
+    step()
     torch.cuda.synchronize()
+    rt.launch = orig_launch
+    print(f"{len(short)} launch shapes", flush=True)
 
     # ---- in-graph comparison, one key at a time (interleaved replays)
     def capture():
