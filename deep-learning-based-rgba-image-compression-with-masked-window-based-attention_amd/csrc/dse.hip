@@ -28,6 +28,8 @@
 // MFMA v_mfma_f32_16x16x32_bf16 with A = weights (16 output channels x one tap's 32
 // input channels), B = 16 pixels x 32 channels: each lane ends with 4 consecutive
 // channels of one pixel.  Per 16x32 tile: conv1 40.5 fragments x 2 x 9, conv2 32 x 2 x 9.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace rgbac {
@@ -39,8 +41,6 @@ constexpr int IH = TY + 4, UH = TY + 2;                      // In / U rows
 constexpr int NIV = IH * RS;                                 // 720 In pixels
 constexpr int NUF = (UH * RS + 15) / 16;                     // 41 conv1 fragments (648 px)
 constexpr int NI = NUF * 16 + 2 * RS + 2 + 6;                // In slots incl. conv1 overrun
-constexpr int NTH = 512;
-constexpr int PRE = (NIV * 4 + NTH - 1) / NTH;               // 6 In chunks per thread
 constexpr int WBYTES = 2 * 2 * 9 * 64 * 16;                  // 36864
 constexpr int IBASE = WBYTES;
 constexpr int UBASE = IBASE + NI * 64;                       // In: 47104 B
@@ -64,9 +64,17 @@ __device__ __forceinline__ uint4 lds16(const unsigned char* base, int off) {
   return *reinterpret_cast<const uint4*>(base + off);
 }
 
-template <int MODE, int CIN>
-__global__ void __launch_bounds__(dse::NTH) dse_block_kernel(const DseArgsDev a) {
+// NW waves: 8 (two per SIMD; conv1 / conv2 weight fragments read from LDS per tap) or 4 (one
+// per SIMD, 512 registers: conv1's 18 weight fragments held in registers for the whole launch,
+// each wave 10 conv1 fragments and 4 output rows -- a quarter less LDS traffic per tile;
+// RGBAC_DSE_WAVES=4)
+template <int MODE, int CIN, int NW>
+__global__ void __launch_bounds__(64 * NW) dse_block_kernel(const DseArgsDev a) {
   using namespace dse;
+  constexpr int NTH = 64 * NW;
+  constexpr int PRE = (NIV * 4 + NTH - 1) / NTH;             // In chunks per thread (6 / 12)
+  constexpr int FST = 1024 * NW;                              // byte step between a wave's fragments
+  constexpr int RPW = 16 / NW;                                // conv2 output rows per wave
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ float bb1[32], bb2[32];
 
@@ -126,7 +134,7 @@ __global__ void __launch_bounds__(dse::NTH) dse_block_kernel(const DseArgsDev a)
     o1[t] = IBASE + (16 * wave + x) * 64 + ((q ^ ((x >> 1) & 3)) << 4);
 #pragma unroll
     for (int par = 0; par < 2; ++par)
-      o2[par][t] = UBASE + (2 * RS * wave + x) * 64 + ((q ^ ((2 * par + (x >> 1)) & 3)) << 4);
+      o2[par][t] = UBASE + (RPW * RS * wave + x) * 64 + ((q ^ ((2 * par + (x >> 1)) & 3)) << 4);
   }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -134,10 +142,10 @@ __global__ void __launch_bounds__(dse::NTH) dse_block_kernel(const DseArgsDev a)
     ow[j] = UBASE + (16 * wave + n16) * 64 + ((c ^ ((n16 >> 1) & 3)) << 4) + 8 * (q & 1);
 #pragma unroll
     for (int par = 0; par < 2; ++par)
-      orr[par][j] = IBASE + (2 * RS * wave + 2 * RS + n16 + 2) * 64 +
+      orr[par][j] = IBASE + (RPW * RS * wave + 2 * RS + n16 + 2) * 64 +
                     ((c ^ ((2 * par + ((n16 + 2) >> 1)) & 3)) << 4) + 8 * (q & 1);
   }
-  // In fill: chunk c = tid & 3 of pixels p = tid/4 + 128 r -> LDS at ofill + 8192 r
+  // In fill: chunk c = tid & 3 of pixels p = tid/4 + (NTH/4) r -> LDS at ofill + 16 NTH r
   const int ofill = IBASE + (tid >> 2) * 64 + (((tid & 3) ^ ((tid >> 3) & 3)) << 4);
   // conv1 extra fragment 40 (pixels 640..655): waves 0 and 1, one 16-channel half each;
   // its offsets are this wave's fragment-0 offsets moved from pixel 16*wave to 640
@@ -150,7 +158,7 @@ __global__ void __launch_bounds__(dse::NTH) dse_block_kernel(const DseArgsDev a)
     const int b = tt / ty_n;
 #pragma unroll
     for (int r = 0; r < PRE; ++r) {
-      const int p = (tid >> 2) + 128 * r;
+      const int p = (tid >> 2) + (NTH / 4) * r;
       const int py = p / RS, px = p - py * RS;
       const int gy = ty * TY - 2 + py, gx = tx * TX - 2 + px;
       uint4 v = make_uint4(0, 0, 0, 0);
@@ -169,7 +177,7 @@ __global__ void __launch_bounds__(dse::NTH) dse_block_kernel(const DseArgsDev a)
   auto store_in = [&](const uint4 (&pre)[PRE]) {
 #pragma unroll
     for (int r = 0; r < PRE; ++r) {
-      if ((tid >> 2) + 128 * r >= NIV) continue;
+      if ((tid >> 2) + (NTH / 4) * r >= NIV) continue;
       uint4 v = pre[r];
       if (MODE == FIRST) {
         // f = in_conv(x) (bf16 weights and input, fp32 sum, + bias, stored bf16); 0 outside
@@ -189,7 +197,7 @@ __global__ void __launch_bounds__(dse::NTH) dse_block_kernel(const DseArgsDev a)
         v = make_uint4(pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]),
                        pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7]));
       }
-      *reinterpret_cast<uint4*>(smem + ofill + 8192 * r) = v;
+      *reinterpret_cast<uint4*>(smem + ofill + 16 * NTH * r) = v;
     }
   };
 
@@ -199,6 +207,15 @@ __global__ void __launch_bounds__(dse::NTH) dse_block_kernel(const DseArgsDev a)
   load_in(t, pre);
   __syncthreads();                                     // weights + biases visible
   store_in(pre);
+  // NW 4: conv1's weight fragments (2 channel halves x 9 taps) in registers for the launch
+  uint4 W1r[NW == 4 ? 2 : 1][NW == 4 ? 9 : 1];
+  if constexpr (NW == 4) {
+#pragma unroll
+    for (int tp = 0; tp < 9; ++tp) {
+      W1r[0][tp] = lds16(smem, ((0 * 9 + tp) * 64 + lane) * 16);
+      W1r[1][tp] = lds16(smem, ((1 * 9 + tp) * 64 + lane) * 16);
+    }
+  }
 
   for (; t < ntiles; t += gridDim.x) {
     int tt = t;
@@ -211,7 +228,7 @@ __global__ void __launch_bounds__(dse::NTH) dse_block_kernel(const DseArgsDev a)
 
     // ================= conv1 + act -> U (zero outside the image)
     {
-      constexpr int NF = 5;                            // + fragment 40 (half) on waves 0, 1
+      constexpr int NF = 40 / NW;                      // + fragment 40 (half) on waves 0, 1
       const bool extra = wave < 2;
       f32x4 acc[NF][2], accx;
 #pragma unroll
@@ -220,10 +237,15 @@ __global__ void __launch_bounds__(dse::NTH) dse_block_kernel(const DseArgsDev a)
       const int ax = extra ? wave : 0;                 // the extra fragment's channel half
       uint4 A[2][2], B[2][NF], BX[2], AX[2];
       auto load = [&](int tp, int sb) {
-        A[sb][0] = lds16(smem, ((0 * 9 + tp) * 64 + lane) * 16);
-        A[sb][1] = lds16(smem, ((1 * 9 + tp) * 64 + lane) * 16);
+        if constexpr (NW == 4) {
+          A[sb][0] = W1r[0][tp];
+          A[sb][1] = W1r[1][tp];
+        } else {
+          A[sb][0] = lds16(smem, ((0 * 9 + tp) * 64 + lane) * 16);
+          A[sb][1] = lds16(smem, ((1 * 9 + tp) * 64 + lane) * 16);
+        }
 #pragma unroll
-        for (int i = 0; i < NF; ++i) B[sb][i] = lds16(smem, o1[tp] + 8192 * i);
+        for (int i = 0; i < NF; ++i) B[sb][i] = lds16(smem, o1[tp] + FST * i);
         if (extra) {
           BX[sb] = lds16(smem, o1[tp] + xoff);
           AX[sb] = ax ? A[sb][1] : A[sb][0];
@@ -265,23 +287,24 @@ __global__ void __launch_bounds__(dse::NTH) dse_block_kernel(const DseArgsDev a)
 #pragma unroll
       for (int i = 0; i < NF; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) emit(acc[i][j], j, wave + 8 * i, ow[j] + 8192 * i);
+        for (int j = 0; j < 2; ++j) emit(acc[i][j], j, wave + NW * i, ow[j] + FST * i);
       if (extra) emit(accx, ax, NUF - 1, (ax ? ow[1] : ow[0]) + xoff);
     }
     __syncthreads();                                   // U complete
 
     // ================= conv2 + bias + residual (+ f, out_conv, identity) -> HBM
     {
-      f32x4 acc[4][2];
+      constexpr int NF2 = 2 * RPW;                     // output fragments per wave (4 / 8)
+      f32x4 acc[NF2][2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-      uint4 A[2][2], B[2][4];
+      for (int i = 0; i < NF2; ++i) acc[i][0] = acc[i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      uint4 A[2][2], B[2][NF2];
       auto load = [&](int tp, int sb) {
         A[sb][0] = lds16(smem, ((2 * 9 + tp) * 64 + lane) * 16);
         A[sb][1] = lds16(smem, ((3 * 9 + tp) * 64 + lane) * 16);
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
-          B[sb][i] = lds16(smem, o2[i >> 1][tp] + 64 * (RS * (i >> 1) + 16 * (i & 1)));
+        for (int i = 0; i < NF2; ++i)
+          B[sb][i] = lds16(smem, o2[(i >> 1) & 1][tp] + 64 * (RS * (i >> 1) + 16 * (i & 1)));
       };
       load(0, 0);
 #pragma unroll
@@ -289,7 +312,7 @@ __global__ void __launch_bounds__(dse::NTH) dse_block_kernel(const DseArgsDev a)
         const int sb = tp & 1;
         if (tp < 8) load(tp + 1, sb ^ 1);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
+        for (int i = 0; i < NF2; ++i) {
           mma_step<bf16_t>(acc[i][0], A[sb][0], B[sb][i]);
           mma_step<bf16_t>(acc[i][1], A[sb][1], B[sb][i]);
         }
@@ -297,8 +320,8 @@ __global__ void __launch_bounds__(dse::NTH) dse_block_kernel(const DseArgsDev a)
       }
       const long long pix0 = (long long)(b * H + y0) * W + x0;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int oy = 2 * wave + (i >> 1), ox = 16 * (i & 1) + n16;
+      for (int i = 0; i < NF2; ++i) {
+        const int oy = RPW * wave + (i >> 1), ox = 16 * (i & 1) + n16;
         const bool inside = y0 + oy < H && x0 + ox < W;
         const long long pix = pix0 + (long long)oy * W + ox;
         float v[2][4];
@@ -306,7 +329,7 @@ __global__ void __launch_bounds__(dse::NTH) dse_block_kernel(const DseArgsDev a)
         for (int j = 0; j < 2; ++j) {
           const int c0 = 16 * j + 4 * q;
           const uint2 rv = *reinterpret_cast<const uint2*>(
-              smem + orr[i >> 1][j] + 64 * (RS * (i >> 1) + 16 * (i & 1)));
+              smem + orr[(i >> 1) & 1][j] + 64 * (RS * (i >> 1) + 16 * (i & 1)));
           const float r4[4] = {bf2f(rv.x & 0xFFFF), bf2f(rv.x >> 16), bf2f(rv.y & 0xFFFF),
                                bf2f(rv.y >> 16)};
 #pragma unroll
@@ -400,8 +423,8 @@ extern "C" int rgbac_dse_block(int mode, int batch, int h, int w, int cin, float
   static int ncu = 0;
   if (ncu == 0) {
     int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (ncu < 1) ncu = 256;
   }
   const long long ntiles = (long long)batch * ((h + dse::TY - 1) / dse::TY) * ((w + dse::TX - 1) / dse::TX);
@@ -410,16 +433,22 @@ extern "C" int rgbac_dse_block(int mode, int batch, int h, int w, int cin, float
   const size_t lds = dse::LDS;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int key = mode == 1 ? 10 : mode * 100 + cin;
+  const char* wenv = getenv("RGBAC_DSE_WAVES");      // read per call (tests switch it)
+  const bool w4 = wenv && wenv[0] == '4';
   switch (key) {
-#define RGBAC_DSE(M_, C_)                                                                       \
-  case (M_ == 1 ? 10 : M_ * 100 + C_): {                                                      \
+#define RGBAC_DSE_NW(M_, C_, NW_)                                                               \
+  {                                                                                             \
     static bool attr = false;                                                                   \
     if (!attr) {                                                                                \
-      hipFuncSetAttribute(reinterpret_cast<const void*>(dse_block_kernel<M_, C_>),              \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                \
+      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(dse_block_kernel<M_, C_, NW_>),   \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);          \
       attr = true;                                                                              \
     }                                                                                           \
-    hipLaunchKernelGGL((dse_block_kernel<M_, C_>), dim3(grid), dim3(dse::NTH), lds, st, d);     \
+    hipLaunchKernelGGL((dse_block_kernel<M_, C_, NW_>), dim3(grid), dim3(64 * NW_), lds, st, d); \
+  }
+#define RGBAC_DSE(M_, C_)                                                                       \
+  case (M_ == 1 ? 10 : M_ * 100 + C_): {                                                      \
+    if (w4) RGBAC_DSE_NW(M_, C_, 4) else RGBAC_DSE_NW(M_, C_, 8)                                \
     break;                                                                                      \
   }
     RGBAC_DSE(0, 1)
@@ -428,6 +457,7 @@ extern "C" int rgbac_dse_block(int mode, int batch, int h, int w, int cin, float
     RGBAC_DSE(2, 1)
     RGBAC_DSE(2, 3)
 #undef RGBAC_DSE
+#undef RGBAC_DSE_NW
     default:
       RGBAC_REQUIRE(false, "DSE input channels must be 1 or 3");
   }

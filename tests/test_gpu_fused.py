@@ -63,6 +63,27 @@ def test_dse_fused_matches_unfused_and_oracle(device, kind, B, H, W):
     assert frac <= 1e-3, frac
 
 
+@pytest.mark.parametrize("kind,B,H,W", [("rgb", 2, 64, 96), ("rgb", 1, 40, 50),
+                                        ("mask", 1, 17, 33), ("rgb", 2, 256, 256)])
+def test_dse_four_wave_kernel_matches(device, monkeypatch, kind, B, H, W):
+    """dse_block_kernel<.., 4> (RGBAC_DSE_WAVES=4: one wave per SIMD, conv1's weight fragments
+    in registers, 10 conv1 fragments and 4 output rows per wave) against the 8-wave kernel:
+    the same MFMAs per fragment in the same order, so bit-identical outputs."""
+    from rgbac import runtime as rt
+    from rgbac.layers.TransformRGB import dse_fused
+    m = _dse(kind, 7)
+    C = 3 if kind == "rgb" else 1
+    x = torch.rand((B, C, H, W), generator=torch.Generator().manual_seed(5)).cuda()
+    outs = {}
+    with torch.no_grad():
+        f = rt.to_nhwc(x, torch.bfloat16)
+        for w in ("8", "4"):
+            monkeypatch.setenv("RGBAC_DSE_WAVES", w)
+            outs[w] = dse_fused(m, f).t.clone()
+        torch.cuda.synchronize()
+    assert torch.equal(outs["4"].view(torch.int16), outs["8"].view(torch.int16))
+
+
 def test_dse_module_forward_uses_fused_path(device):
     """DSE.forward under no_grad at bf16 goes through rgbac_dse_block (3 launches)."""
     from rgbac import runtime as rt
