@@ -369,16 +369,21 @@ constexpr int W1F = 9, W2F = 54, W3F = 10;            // fragments per matrix
 constexpr int HY = 10, HX = 10, NH = 100, NHP = 112;  // halo pixels (7 fragments)
 }  // namespace rus
 
-template <int RB>
-__global__ void __launch_bounds__(256, 1) ru_small_kernel(const RuArgsDev args) {
+// NHALF = 2 (multi-round launches): two 4-wave halves each run their own tile over the shared
+// weights -- two waves per SIMD instead of one (T1 / T2 per half: 117 KiB of LDS)
+template <int RB, int NHALF>
+__global__ void __launch_bounds__(256 * NHALF, 1) ru_small_kernel(const RuArgsDev args) {
   using namespace rus;
   __shared__ __attribute__((aligned(16))) uint4 Ws[(W1F + W2F + W3F) * 64];
-  __shared__ __attribute__((aligned(16))) uint4 T1[NHP * 8];
-  __shared__ __attribute__((aligned(16))) uint4 T2[64 * 8];
+  __shared__ __attribute__((aligned(16))) uint4 T1s[NHALF * NHP * 8];
+  __shared__ __attribute__((aligned(16))) uint4 T2s[NHALF * 64 * 8];
   __shared__ float bs[48 + 48 + 80];
   const RuGroup& g = args.g[blockIdx.z];
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int half = wave_all >> 2, wave = wave_all & 3;
+  uint4* const T1 = T1s + half * NHP * 8;
+  uint4* const T2 = T2s + half * 64 * 8;
   const int n = lane & 15, q = lane >> 4;
   const int tx_n = args.W / 8, ty_n = args.H / 8;
   const int ntiles = args.batch * tx_n * ty_n;
@@ -388,17 +393,17 @@ __global__ void __launch_bounds__(256, 1) ru_small_kernel(const RuArgsDev args) 
   // replaces waited for an L2 round trip every few of its 18 iterations
   {
     const uint32_t lws = __builtin_amdgcn_readfirstlane((uint32_t)(size_t)(ru_lptr_t)Ws);
-    for (int pc = wave; pc < W1F + W2F + W3F; pc += 4) {
+    for (int pc = wave_all; pc < W1F + W2F + W3F; pc += 4 * NHALF) {
       const uint4* src = pc < W1F ? reinterpret_cast<const uint4*>(g.w1) + pc * 64
                        : pc < W1F + W2F ? reinterpret_cast<const uint4*>(g.w2) + (pc - W1F) * 64
                        : reinterpret_cast<const uint4*>(g.w3) + (pc - W1F - W2F) * 64;
       ru_dma16(src + lane, lws + (uint32_t)pc * 1024u);
     }
   }
-  for (int e = tid; e < 48 + 48 + 80; e += 256)
+  for (int e = tid; e < 48 + 48 + 80; e += 256 * NHALF)
     bs[e] = e < 48 ? g.b1[e] : e < 96 ? g.b2[e - 48] : g.b3[e - 96];
   // zero channels 48..63 (chunks 6, 7) of T1 / T2: the stage-2 / stage-3 K padding
-  for (int e = tid; e < (NHP + 64) * 2; e += 256) {
+  for (int e = tid & 255; e < (NHP + 64) * 2; e += 256) {
     const int p = e >> 1, c = 6 + (e & 1);
     if (p < NHP) T1[p * 8 + (c ^ (p & 7))] = make_uint4(0, 0, 0, 0);
     else T2[(p - NHP) * 8 + (c ^ ((p - NHP) & 7))] = make_uint4(0, 0, 0, 0);
@@ -430,12 +435,15 @@ __global__ void __launch_bounds__(256, 1) ru_small_kernel(const RuArgsDev args) 
 #pragma unroll
     for (int tt2 = 0; tt2 < 5; ++tt2) rd[tt2] = *reinterpret_cast<const uint2*>(xr + 16 * tt2 + 4 * q);
   };
-  int t = blockIdx.x;
-  if (t >= ntiles) {
+  // half h runs tiles blockIdx.x + h grid, + NHALF grid, ...; a half past the last tile
+  // computes a clamped tile and stores nothing (both halves meet at every barrier)
+  const int stride = NHALF * (int)gridDim.x;
+  int t = blockIdx.x + half * (int)gridDim.x;
+  if ((int)blockIdx.x >= ntiles) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (no DMA may land after the exit)
     return;
   }
-  load_x(t, xb, xin, rx);
+  load_x(t < ntiles ? t : ntiles - 1, xb, xin, rx);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // this wave's weight pieces landed
   __syncthreads();
 
@@ -444,9 +452,11 @@ __global__ void __launch_bounds__(256, 1) ru_small_kernel(const RuArgsDev args) 
   // only after every wave passed the barrier behind stage 2 (its last reader); T2 rows are
   // wave-private.
   for (;;) {
-    const int tx = t % tx_n, ty = (t / tx_n) % ty_n, b = t / (tx_n * ty_n);
+    const bool valid = t < ntiles;
+    const int tc = valid ? t : ntiles - 1;
+    const int tx = tc % tx_n, ty = (tc / tx_n) % ty_n, b = tc / (tx_n * ty_n);
     const int y0 = ty * 8, x0 = tx * 8;
-    const int tnext = t + gridDim.x;
+    const int tnext = t + stride;
 
     // ================= stage 1
     {
@@ -543,10 +553,10 @@ __global__ void __launch_bounds__(256, 1) ru_small_kernel(const RuArgsDev args) 
           const float t3 = acc[tt][r] + bs[96 + c0 + r] + res[tt][r];
           v[r] = RB ? t3 : ru_gelu(t3);
         }
-        Elem<bf16_t>::st4(orow + c0, v);
+        if (valid) Elem<bf16_t>::st4(orow + c0, v);
       }
     }
-    if (tnext >= ntiles) break;
+    if (tnext - half * (int)gridDim.x >= ntiles) break;   // (the first half's next tile)
     t = tnext;
 #pragma unroll
     for (int i = 0; i < F1; ++i) {
@@ -1163,9 +1173,18 @@ extern "C" int rgbac_residual_unit_ex(const rgbac_ru_args* args, int ngroups, in
     }
     long long gx = ncu / ngroups;
     if (gx < 1) gx = 1;
-    if (gx > tiles) gx = tiles;
-    if (kind) hipLaunchKernelGGL(ru_small_kernel<1>, dim3((unsigned)gx, 1, ngroups), dim3(256), 0, st, d);
-    else hipLaunchKernelGGL(ru_small_kernel<0>, dim3((unsigned)gx, 1, ngroups), dim3(256), 0, st, d);
+    const char* dual_env = getenv("RGBAC_RU_SMALL_DUAL");
+    // multi-round launches only (=2 forces it: A/B)
+    const bool dual = (tiles > gx && !(dual_env && dual_env[0] == '0')) || (dual_env && dual_env[0] == '2');
+    if (dual) {
+      if (gx > (tiles + 1) / 2) gx = (tiles + 1) / 2;
+      if (kind) hipLaunchKernelGGL((ru_small_kernel<1, 2>), dim3((unsigned)gx, 1, ngroups), dim3(512), 0, st, d);
+      else hipLaunchKernelGGL((ru_small_kernel<0, 2>), dim3((unsigned)gx, 1, ngroups), dim3(512), 0, st, d);
+    } else {
+      if (gx > tiles) gx = tiles;
+      if (kind) hipLaunchKernelGGL((ru_small_kernel<1, 1>), dim3((unsigned)gx, 1, ngroups), dim3(256), 0, st, d);
+      else hipLaunchKernelGGL((ru_small_kernel<0, 1>), dim3((unsigned)gx, 1, ngroups), dim3(256), 0, st, d);
+    }
     return check_launch("ru_small_kernel");
   }
   if (a->w1_kpad == 0) {                             // fragment-major packs: streamed kernel

@@ -261,3 +261,27 @@ def test_half_tile_unit_matches_stream_kernel(device, monkeypatch, mode, kind, B
         print(f"kind {kind} {B}x{H}x{W}: max diff {(a - b).abs().max().item() / scale:.2e}, "
               f"> 1 ulp {frac:.1e}")
         assert frac <= 1e-3, frac
+
+
+@pytest.mark.parametrize("kind,B,H,W", [("ru", 1, 72, 136), ("rb", 1, 72, 136), ("ru", 4, 128, 128)])
+def test_small_unit_two_tile_matches_one_tile(device, monkeypatch, kind, B, H, W):
+    """ru_small_kernel<RB, 2> (multi-round C = 80 launches: two 4-wave halves per workgroup, each
+    on its own tile over the shared LDS weights) against the one-tile form
+    (RGBAC_RU_SMALL_DUAL=0) on two grouped units: identical per-tile arithmetic, so bit-identical;
+    9 x 17 = 153 tiles leave the last workgroup's second half without a tile."""
+    from rgbac import runtime as rt
+    from rgbac.layers import Masked_Attention as MA
+    from rgbac.models import AutoEncoderMask_Journal as AM
+    torch.manual_seed(51)
+    mods = [(MA.ResidualUnit(80) if kind == "ru" else AM.ResBlock(80)).cuda() for _ in range(2)]
+    g = torch.Generator().manual_seed(52)
+    xs = [rt.to_nhwc(torch.randn((B, 80, H, W), generator=g).cuda(), torch.bfloat16) for _ in mods]
+    run = MA.run_residual_units if kind == "ru" else AM.run_resblocks
+    outs = {}
+    with torch.no_grad():
+        for mode in ("0", "1"):
+            monkeypatch.setenv("RGBAC_RU_SMALL_DUAL", mode)
+            outs[mode] = [o.t.clone() for o in run(list(zip(mods, xs)))]
+        torch.cuda.synchronize()
+    for a, b in zip(outs["1"], outs["0"]):
+        assert torch.equal(a.view(torch.int16), b.view(torch.int16))
