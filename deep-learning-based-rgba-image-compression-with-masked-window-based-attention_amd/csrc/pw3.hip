@@ -13,8 +13,8 @@
 // (res0 / res1 / res2 quads, double-buffered) are gone: the only epilogue operand, x, comes
 // from the LDS tile the MFMAs consumed.  The attention gate (a * sigmoid(W b + bias) + x,
 // layers/Masked_Attention.py:182-189) loads its a / x quads into registers one tile ahead,
-// issued before each tile DMA so the counted waits stay exact.  Six waves (two slots of 6 KiB each + the 72 KiB
-// weight panel = 144 KiB of LDS).
+// issued behind each tile DMA.  Seven waves (two slots of 6 KiB each + the 72 KiB weight
+// panel = 156 KiB of LDS).
 //
 // Same MFMA order, the same bf16(x^2) B fragments and the same epilogue arithmetic as
 // conv_pw2_kernel's GDN / IGDN instance, so the two are bit-identical.
@@ -25,7 +25,11 @@
 
 namespace rgbac {
 
-constexpr int kPw3Waves = 6;
+#ifndef RGBAC_PW3_WAVES
+#define RGBAC_PW3_WAVES 7
+#endif
+// waves per workgroup: 7 x two 6 KiB slots + the 72 KiB panel = 156 KiB of LDS
+constexpr int kPw3Waves = RGBAC_PW3_WAVES;
 
 template <int NKS, int ACT>
 __global__ void __launch_bounds__(64 * kPw3Waves, 1) conv_pw3_kernel(const ConvArgsDev args) {
