@@ -613,9 +613,15 @@ __device__ unsigned long long g_ru_w[8192][2];     // wall clock (100 MHz) at st
 #define RU_T(k) do {} while (0)
 #endif
 
-template <int RB>
-__global__ void __launch_bounds__(256, 2) ru_stream_kernel(const RuArgsDev args) {
+// TYV = 8: 8 x 16 tiles, 4 waves, two workgroups per CU.  TYV = 16 (RGBAC_RU_TILE16=1): 16 x 16
+// tiles, 8 waves, one workgroup per CU -- the same pixels per CU with each weight fragment
+// streamed once per CU instead of twice and 1.27x halo instead of 1.41x.
+template <int RB, int TYV>
+__global__ void __launch_bounds__(32 * TYV, TYV == 8 ? 2 : 1) ru_stream_kernel(const RuArgsDev args) {
   using namespace rsw;
+  constexpr int TY = TYV, NH = (TYV + 2) * HX;      // (shadow rsw's 8-row values)
+  constexpr int NW = TYV / 2, NTH = 64 * NW;        // waves: stage 1 takes 3 halo m tiles each
+  constexpr int NHP = NW * 48;
   constexpr int R2 = RB ? 6 : RGBAC_RU_R2;         // stage-2 ring (ReLU variant: register fit)
   // T1 | T2; after stage 3's MFMAs the same bytes stage the output tile (128 x 400-B rows)
   // (T1 padded to NHP = 192 rows: the stage-1 epilogue of wave 3 stores its 12 rows past the
@@ -625,7 +631,7 @@ __global__ void __launch_bounds__(256, 2) ru_stream_kernel(const RuArgsDev args)
   unsigned char* const T2 = lds + NHP * TROW;
   unsigned char* const OT = lds;
   static_assert(TY * TX * ORW <= NHP * TROW + TY * TX * TROW, "output staging fits");
-  static_assert(NHP >= 4 * 48, "every wave's 3 halo m tiles have rows");
+  static_assert(NHP >= NH, "every halo row has a T1 row");
   // biases in LDS: an epilogue's bias read is then an LDS read (lgkmcnt), not a global load
   // whose vmcnt wait would also drain the next stage's weight prefetch
   __shared__ __attribute__((aligned(16))) float bs[96 + 96 + 192];
@@ -652,7 +658,7 @@ __global__ void __launch_bounds__(256, 2) ru_stream_kernel(const RuArgsDev args)
     for (int i = 0; i < args.stagger; ++i) __builtin_amdgcn_s_sleep(16);
   // ================= stage 1
   RU_T(0);
-  for (int e = tid; e < 384; e += 256) bs[e] = e < 96 ? g.b1[e] : e < 192 ? g.b2[e - 96] : g.b3[e - 192];
+  for (int e = tid; e < 384; e += NTH) bs[e] = e < 96 ? g.b1[e] : e < 192 ? g.b2[e - 96] : g.b3[e - 192];
   const uint4* const W1 = reinterpret_cast<const uint4*>(g.w1) + lane;
   uint4 w1r[R1][6];
 #pragma unroll
@@ -697,7 +703,7 @@ __global__ void __launch_bounds__(256, 2) ru_stream_kernel(const RuArgsDev args)
   }
   RU_T(1);
   // stage-2 weights for the first R2 k-steps, in flight during the stage-1 epilogue
-  const int wn = wave >> 1, wm = wave & 1;
+  const int wn = wave / (NW / 2), wm = wave % (NW / 2);   // channel half, 4-row group
   const uint4* const W2 = reinterpret_cast<const uint4*>(g.w2) + lane + (size_t)(3 * wn) * NK2 * 64;
   uint4 w2r[R2][3];
 #pragma unroll
@@ -847,8 +853,8 @@ __global__ void __launch_bounds__(256, 2) ru_stream_kernel(const RuArgsDev args)
   __syncthreads();
   // whole 16-B chunks, consecutive lanes on consecutive chunks of a pixel's 384 bytes
 #pragma unroll
-  for (int u = 0; u < TY * TX * 24 / 256; ++u) {
-    const int c = tid + 256 * u, p = c / 24, q = c - (c / 24) * 24;
+  for (int u = 0; u < TY * TX * 24 / NTH; ++u) {
+    const int c = tid + NTH * u, p = c / 24, q = c - (c / 24) * 24;
     const long long pix = (long long)(b * args.H + y0 + p / TX) * args.W + x0 + p % TX;
     *reinterpret_cast<uint4*>(g.out + pix * g.ldo + q * 8) =
         *reinterpret_cast<const uint4*>(OT + p * ORW + q * 16);
@@ -1213,8 +1219,15 @@ extern "C" int rgbac_residual_unit_ex(const rgbac_ru_args* args, int ngroups, in
       else hipLaunchKernelGGL((ru_half_kernel<0, 2>), dim3(t8, 1, ngroups), dim3(256), 0, st, d);
       return check_launch("ru_half_kernel");
     }
-    if (kind) hipLaunchKernelGGL(ru_stream_kernel<1>, dim3((unsigned)tiles, 1, ngroups), dim3(256), 0, st, d);
-    else hipLaunchKernelGGL(ru_stream_kernel<0>, dim3((unsigned)tiles, 1, ngroups), dim3(256), 0, st, d);
+    const char* t16_env = getenv("RGBAC_RU_TILE16");  // read per call (tests switch it)
+    if (t16_env && t16_env[0] == '1' && a->h % 16 == 0) {
+      const unsigned t16 = (unsigned)(tiles / 2);
+      if (kind) hipLaunchKernelGGL((ru_stream_kernel<1, 16>), dim3(t16, 1, ngroups), dim3(512), 0, st, d);
+      else hipLaunchKernelGGL((ru_stream_kernel<0, 16>), dim3(t16, 1, ngroups), dim3(512), 0, st, d);
+      return check_launch("ru_stream_kernel");
+    }
+    if (kind) hipLaunchKernelGGL((ru_stream_kernel<1, 8>), dim3((unsigned)tiles, 1, ngroups), dim3(256), 0, st, d);
+    else hipLaunchKernelGGL((ru_stream_kernel<0, 8>), dim3((unsigned)tiles, 1, ngroups), dim3(256), 0, st, d);
     return check_launch("ru_stream_kernel");
   }
   static const int wide_env = [] {

@@ -159,8 +159,20 @@ def run_bottlenecks_fused(units, kind):
         outs.append(o)
     npix = x0.B * x0.H * x0.W
     flops = 2.0 * npix * len(units) * (C * C // 2 * 2 + 9 * (C // 2) ** 2)
-    kname = (f"ru_small_kernel<{kind}>" if C == 80 else f"ru_stream_kernel<{kind}>" if stream
-             else f"ru_fused_kernel<{C}, {C // 2}>")
+    # the launched template's rocprof name (csrc/fused.hip rgbac_residual_unit_ex's choice,
+    # restated): C 80 takes two tiles per workgroup on multi-round launches, C 192 the 16-row
+    # tile under RGBAC_RU_TILE16=1
+    if C == 80:
+        tiles = x0.B * (x0.H // 8) * (x0.W // 8)
+        ncu = torch.cuda.get_device_properties(x0.t.device).multi_processor_count
+        dual_env = os.environ.get("RGBAC_RU_SMALL_DUAL", "")
+        dual = (tiles > max(1, ncu // len(units)) and dual_env != "0") or dual_env == "2"
+        kname = f"ru_small_kernel<{kind}, {2 if dual else 1}>"
+    elif stream:
+        t16 = os.environ.get("RGBAC_RU_TILE16", "") == "1" and x0.H % 16 == 0
+        kname = f"ru_stream_kernel<{kind}, {16 if t16 else 8}>"
+    else:
+        kname = f"ru_fused_kernel<{C}, {C // 2}>"
     rt.timed(kname, flops, 2 * npix * len(units) * 2 * C,
              lambda: _lib.call("rgbac_residual_unit_ex", ctypes.addressof(arr), len(units), kind,
                                _lib.stream_ptr(x0.t.device)),

@@ -285,3 +285,26 @@ def test_small_unit_two_tile_matches_one_tile(device, monkeypatch, kind, B, H, W
         torch.cuda.synchronize()
     for a, b in zip(outs["1"], outs["0"]):
         assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+
+
+@pytest.mark.parametrize("kind,B,H,W", [(0, 2, 32, 64), (1, 2, 32, 64), (0, 1, 16, 16), (1, 1, 48, 32)])
+def test_stream_unit_16_row_tile_matches(device, monkeypatch, kind, B, H, W):
+    """ru_stream_kernel<RB, 16> (RGBAC_RU_TILE16=1: 16 x 16 tiles, 8 waves, one workgroup per
+    CU) against the 8 x 16 tile: the same GEMM order per output and the same bf16 rounding
+    points, so bit-identical (image borders included: 16 x 16 is a single tile)."""
+    from rgbac import runtime as rt
+    from rgbac.layers import Masked_Attention as MA
+    from rgbac.models import AutoEncoderMask_Journal as AM
+    torch.manual_seed(61 + kind)
+    mods = [(MA.ResidualUnit(192) if kind == 0 else AM.ResBlock(192)).cuda() for _ in range(2)]
+    units = [((m.conv[0], m.conv[2], m.conv[4]) if kind == 0 else (m.conv1, m.conv2, m.conv3))
+             for m in mods]
+    xs = [rt.to_nhwc(torch.randn((B, 192, H, W), device="cuda"), torch.bfloat16) for _ in mods]
+    outs = {}
+    with torch.no_grad():
+        for mode in ("0", "1"):
+            monkeypatch.setenv("RGBAC_RU_TILE16", mode)
+            outs[mode] = [o.t.clone() for o in MA.run_bottlenecks_fused(list(zip(units, xs)), kind)]
+        torch.cuda.synchronize()
+    for a, b in zip(outs["1"], outs["0"]):
+        assert torch.equal(a.view(torch.int16), b.view(torch.int16))
