@@ -112,7 +112,10 @@ __global__ void __launch_bounds__(64 * kPw3Waves, 1) conv_pw3_kernel(const ConvA
                   uint2 (&vr)[NT]) {
     // slot k & 1 holds tile k: its DMA was issued two iterations back (or in the prologue);
     // younger than it are that iteration's stores (NT), the next DMA (XP) and the last
-    // iteration's stores (NT)
+    // iteration's stores (NT).  The counts are lower bounds that hold for any codegen: the DMA
+    // is always XP pieces (asm), and the NT quad stores of a lane are 8-byte stores 32 bytes
+    // apart (nothing to merge; a split store only adds younger operations, i.e. waits more);
+    // every iteration has a valid lane (fr = 0), so no store block is skipped
     // (GATE: plus the 2 NT quad loads of the next tile issued behind each tile DMA; past
     // vmcnt's 63 the wait also retires some older quad loads, which the epilogue before
     // already needed)
