@@ -164,6 +164,41 @@ def test_tile_candidates():
     assert ks > 1                                       # tiny grids split K
 
 
+def test_pw3_admission_mirror():
+    """rgbac.runtime._pw3_admits (the host mirror of csrc/pw3.hip pw3_ok, which names the
+    pointwise kernel in the bench tables): GDN / IGDN with x as the epilogue operand and 192
+    channels; the gate only with both operands and from 8,192 tiles on; never a pre-activation
+    store, a res0 operand or a 96-channel input."""
+    import types
+    from rgbac import _lib
+    from rgbac import runtime as rt
+
+    def prep(act, cin=192, cout=192, square=True, res1="x", res2=False, res0=False, zout=False,
+             mgrid=8 * 64 * 64):
+        a = _lib.ConvArgs()
+        a.mode, a.act, a.square_input = rt.CONV, rt.ACT[act], 1 if square else 0
+        a.cin_pad, a.k_pad, a.cout, a.out_ldc, a.out_coff = cin, cin, cout, cout, 0
+        a.src[0].ptr, a.src[0].ldc = 4096, cin
+        a.res1 = 4096 if res1 == "x" else (8192 if res1 else None)
+        a.res1_ldc = cin if res1 == "x" else cout
+        a.res2, a.res2_ldc = (12288 if res2 else None), cout
+        a.res0, a.zout = (16384 if res0 else None), (20480 if zout else None)
+        return types.SimpleNamespace(a=a, mgrid=mgrid)
+
+    assert rt._pw3_admits([prep("gdn")]) and rt._pw3_admits([prep("igdn")])
+    assert rt._pw3_admits([prep("gdn"), prep("gdn")])
+    assert not rt._pw3_admits([prep("gdn", zout=True)])
+    assert not rt._pw3_admits([prep("gdn", res0=True)])
+    assert not rt._pw3_admits([prep("gdn", cin=96)])
+    assert not rt._pw3_admits([prep("gdn", cout=96)])
+    assert not rt._pw3_admits([prep("gdn", res1="a")])          # x must be the epilogue operand
+    gate = dict(square=False, res1="a", res2=True)
+    assert not rt._pw3_admits([prep("gate", **gate)])           # 2,048 tiles: stays on pw2
+    assert rt._pw3_admits([prep("gate", mgrid=8 * 128 * 128, **gate)])
+    assert not rt._pw3_admits([prep("gate", mgrid=8 * 128 * 128, square=False, res1="a")])
+    assert not rt._pw3_admits([prep("gelu", square=False, res1=None)])
+
+
 def test_state_dict_layout_matches_reference_names():
     """Key names/shapes the reference's checkpoints use."""
     from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
