@@ -438,6 +438,48 @@ def test_conv_smallk_tile(device, cin, cout, k, s, act):
         rt.FORCE = None
 
 
+@pytest.mark.parametrize("kind", ["igdn", "gate"])
+def test_pw3_grouped_matches_pw2(device, monkeypatch, kind):
+    """conv_pw3_kernel on a grouped launch (three convs of one geometry in one dispatch,
+    blockIdx.z = group; 8 x 128^2 so the gate takes pw3 too) against conv_pw2_kernel: each
+    group's output equal to pw2's (GDN-family bit for bit, the gate within one bf16 ulp of the
+    operands' scale), and no group writing another's output."""
+    rt = _rt()
+    g = _gen(91)
+    dt = torch.bfloat16
+    B, H, W = 8, 128, 128
+    preps_in = []
+    for i in range(3):
+        m = nn.Conv2d(192, 192, 1)
+        with torch.no_grad():
+            m.weight.copy_(0.1 * torch.rand(192, 192, 1, 1, generator=g))
+            m.bias.copy_(0.5 + torch.rand(192, generator=g))
+        fx = rt.to_nhwc(torch.randn((B, 192, H, W), generator=g).to(device), dt)
+        fa = rt.to_nhwc(torch.randn((B, 192, H, W), generator=g).to(device), dt)
+        fr = rt.to_nhwc(torch.randn((B, 192, H, W), generator=g).to(device), dt)
+        preps_in.append((rt.packed(m.to(device), dt, [(192, 192)]), fx, fa, fr))
+    outs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("RGBAC_PW3", mode)
+        with torch.no_grad():
+            preps = []
+            for pk, fx, fa, fr in preps_in:
+                if kind == "gate":
+                    preps.append(rt.prepare(pk, [fx.src()], act="gate", res1=fa, res2=fr))
+                else:
+                    preps.append(rt.prepare(pk, [fx.src()], square=True, act=kind, res1=fx))
+            o = rt.launch(preps, force=(rt.TILE_PW, 1))
+        torch.cuda.synchronize()
+        outs[mode] = [f.t.clone() for f in o]
+    for a, b in zip(outs["1"], outs["0"]):
+        if kind == "gate":
+            d = (a.float() - b.float()).abs()
+            assert d.max().item() <= 2.0 ** -8 * b.float().abs().max().item()
+            assert (a != b).float().mean().item() < 1e-5
+        else:
+            assert torch.equal(a.view(torch.int16), b.view(torch.int16))
+
+
 @pytest.mark.parametrize("kind", ["gdn", "igdn", "gate"])
 @pytest.mark.parametrize("B,H,W", [(3, 46, 70), (8, 128, 128), (1, 4, 4), (2, 64, 64)])
 def test_pw3_matches_pw2(device, monkeypatch, kind, B, H, W):
