@@ -194,6 +194,10 @@ SIGNATURES = {
     "rgbac_ssim_level": [_I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _F, _F, _VP, _VP, _VP, _VP],
     "rgbac_avgpool2": [_I32, _I32, _I32, _VP, _VP, _VP],
     "rgbac_msssim_combine": [_I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP],
+    "rgbac_masked_apply": [_I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP, _VP],
+    "rgbac_masked_ssim_level": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _F, _F,
+                                _VP, _VP, _VP, _VP],
+    "rgbac_masked_msssim_combine": [_I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP, _VP],
     "rgbac_pmf_to_quantized_cdf": [_VP, _I32, _I32, _VP],
     "rgbac_rans_encoder_create": [ctypes.POINTER(ctypes.c_void_p)],
     "rgbac_rans_encoder_destroy": [_VP],

@@ -634,6 +634,28 @@ int rgbac_avgpool2(int planes, int h, int w, const float* x, float* y, void* str
 int rgbac_msssim_combine(int levels, int batch, const float* mcs, const float* ssim_last,
                          const float* weights, float* per_image, float* mean, void* stream);
 
+/* Masked MS-SSIM / SSIM (csrc/msssim.hip), replaces metrics/masked_ms_ssim_torch.py:56-265.
+ * fp32 NCHW planes; the mask has 1 (broadcast over the channels) or C channels.
+ * rgbac_masked_apply: one level's start (:246-248): mask_out = (mask > 0), x_out = x * it,
+ *   y_out = y * it (mask_out shaped like mask).
+ * rgbac_masked_ssim_level: _ssim (:56-118) on x, y with the binary level mask: VALID ssim / cs
+ *   maps, kept where mask NEAREST-resized to (h-ws+1, w-ws+1) is nonzero (:103-105);
+ *   ssim_out[b*C+c], cs_out[b*C+c] = masked sums / (count + 1e-10) (:115-116);
+ *   partials: caller scratch of batch*channels*ceil((h-ws+1)/16)*ceil((w-ws+1)/16)*3 floats.
+ * rgbac_masked_msssim_combine: v[b,c] = prod_{l<L-1} relu(mcs[l][b,c])^w[l] *
+ *   relu(ssim_last[b,c])^w[L-1] (:252-260); per_image[b] = mean_c v, mean = mean_{b,c} v
+ *   (:262-265); either output may be NULL; mcs may be NULL when levels == 1. */
+int rgbac_masked_apply(int batch, int channels, int mask_channels, int h, int w, const float* x,
+                       const float* y, const float* mask, float* x_out, float* y_out,
+                       float* mask_out, void* stream);
+int rgbac_masked_ssim_level(int batch, int channels, int mask_channels, int h, int w,
+                            int win_size, const float* x, const float* y, const float* mask,
+                            const float* win, float c1, float c2, float* partials,
+                            float* ssim_out, float* cs_out, void* stream);
+int rgbac_masked_msssim_combine(int levels, int batch, int channels, const float* mcs,
+                                const float* ssim_last, const float* weights, float* per_image,
+                                float* mean, void* stream);
+
 /* Data-parallel gradient exchange (csrc/comm.cpp; BASELINE config 5 -- the reference trains
  * on one GPU, DataParallel is commented out at trainRGB.py:374, so no reference interface is
  * replaced: this is the all-reduce of rgbac/parallel.py's gradient buckets).  RCCL is called

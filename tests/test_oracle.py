@@ -192,6 +192,44 @@ def test_ms_ssim_oracle_known_answers():
     assert abs(s.item() - want) < 1e-3 and abs(cs.item() - 1.0) < 1e-3
 
 
+def test_masked_ms_ssim_oracle_known_answers():
+    """masked_ms_ssim_torch.py: an all-ones mask keeps every valid pixel, so a level's masked
+    per-channel mean is the plain map mean (:115-116); X = Y scores 1 under any mask that keeps
+    pixels at every level; an all-zero mask scores 0 (0 / (0 + 1e-10), relu, 0 ** w)."""
+    from oracle import ref_metrics as rm
+    g = torch.Generator().manual_seed(6)
+    X = torch.rand((2, 1, 48, 56), generator=g)
+    Y = torch.clamp(X + 0.1 * torch.randn(X.shape, generator=g), 0, 1)
+    win = rm.fspecial_gauss_1d(11, 1.5).repeat(1, 1, 1, 1)
+    s0, c0 = rm.ssim_level(X, Y, win, 1.0)
+    s1, c1 = rm.masked_ssim_level(X, Y, torch.ones_like(X), win, 1.0)
+    assert (s1[:, 0] - s0).abs().max() < 1e-5 and (c1[:, 0] - c0).abs().max() < 1e-5
+    X = torch.rand((2, 3, 176, 192), generator=g)
+    m = torch.ones((2, 1, 176, 192))
+    m[:, :, 120:, 150:] = 0         # the coarsest level's 1x2 valid map still samples a kept pixel
+    assert abs(rm.masked_ms_ssim(X, X, m, data_range=1.0).item() - 1.0) < 1e-5
+    assert rm.masked_ms_ssim(X, X * 0.5, torch.zeros_like(m), data_range=1.0).item() == 0.0
+
+
+@pytest.mark.parametrize("hw", [(161, 177), (80, 96), (40, 45), (20, 23), (10, 12), (5, 6)])
+@pytest.mark.parametrize("ws", [7, 11])
+def test_masked_nearest_index_matches_interpolate(hw, ws):
+    """csrc/msssim.hip masked_ssim_tile_kernel samples the level mask at
+    min(floor(float32(o) * float32(in / out)), in - 1); that must be the source pixel
+    F.interpolate(mode='nearest') (torchvision's NEAREST resize, :104) picks."""
+    H, W = hw
+    if H < ws or W < ws:
+        pytest.skip("smaller than the window")
+    Ho, Wo = H - ws + 1, W - ws + 1
+    idx = torch.arange(H * W, dtype=torch.float32).reshape(1, 1, H, W)
+    got = F.interpolate(idx, size=(Ho, Wo), mode="nearest")[0, 0].long()
+    sh, sw = np.float32(H) / np.float32(Ho), np.float32(W) / np.float32(Wo)
+    ys = np.minimum(np.floor(np.arange(Ho, dtype=np.float32) * sh).astype(np.int64), H - 1)
+    xs = np.minimum(np.floor(np.arange(Wo, dtype=np.float32) * sw).astype(np.int64), W - 1)
+    want = torch.from_numpy(ys[:, None] * W + xs[None, :])
+    assert torch.equal(got, want)
+
+
 def test_teacher_forcing_with_own_latents_is_identity():
     """oracle/parity.py: forcing the oracle's OWN z_hat / y_hat reproduces its free-running
     forward exactly, and the accounting of a forward against itself finds no flip."""
