@@ -285,3 +285,22 @@ def test_bench_gpus_flag_spawns_ranks(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4"])
     with pytest.raises(SystemExit):
         bench.main()
+
+
+def test_masked_ms_ssim_argument_checks():
+    """rgbac.metrics.masked_ms_ssim_torch: the reference's shape / window errors
+    (masked_ms_ssim_torch.py:148-165, :207-228) and the mask's shape are checked before any
+    launch, and CPU tensors fail loudly (no CPU fallback)."""
+    from rgbac.metrics.masked_ms_ssim_torch import ms_ssim, ssim
+    X = torch.rand((1, 3, 192, 192))
+    M = torch.ones((1, 1, 192, 192))
+    with pytest.raises(ValueError, match="same dimensions"):
+        ms_ssim(X, X[:, :, :100], M)
+    with pytest.raises(ValueError, match="odd"):
+        ssim(X, X, M, win_size=10)
+    with pytest.raises(ValueError, match="mask"):
+        ms_ssim(X, X, torch.ones((1, 2, 192, 192)))
+    with pytest.raises(ValueError, match="4-d"):
+        ms_ssim(X[0], X[0], M)
+    with pytest.raises(RuntimeError, match="GPU"):
+        ms_ssim(X, X, M)
