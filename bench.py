@@ -496,76 +496,99 @@ def dp_train_record(args, world, rank, dev, dist):
         trainer.step(loss)
         return loss.detach()
 
-    step()                                              # learning step of the buckets
-    for _ in range(max(0, args.dp_warmup - 1)):
-        step()
-    torch.cuda.synchronize()
-    nb = len(trainer.buckets.buckets)
-    launched = trainer.buckets.launched_in_backward()
     trainer_rccl = trainer.buckets.comm is not None
-    # failure detection: a dead peer leaves every survivor blocked in a replay; the watchdog
-    # aborts the communicator and exits non-zero once an armed stretch overruns its deadline
+    # failure detection: a dead peer leaves every survivor blocked in a collective; the
+    # watchdog aborts the communicator and exits non-zero once an armed stretch overruns its
+    # deadline.  Armed per stretch (learning step and warmup included), the deadline scaled
+    # to the stretch's steps; stopped on every exit path
     wd = CommWatchdog(trainer.buckets.comm, timeout_s=240.0).start() if trainer_rccl else None
-    if wd is not None:
-        wd.arm()
-    graph_err = None
+
+    class _armed:
+        def __init__(self, nsteps):
+            self.n = nsteps
+
+        def __enter__(self):
+            if wd is not None:
+                wd.timeout_s = 120.0 + 10.0 * self.n
+                wd.arm()
+
+        def __exit__(self, *exc):
+            if wd is not None:
+                if exc[0] is None:
+                    torch.cuda.synchronize()
+                wd.disarm()
+            return False
+
     try:
-        run, graph, gout = capture_train(step, opt, dev, args.no_graph)
-    except RuntimeError as e:                           # recorded, the eager step is timed
-        graph_err = f"{type(e).__name__}: {str(e)[:200]}"
-        run, graph, gout = step, None, None
-    for _ in range(2):
-        run()
-    torch.cuda.synchronize()
-    elapsed = time_steps(run, args.dp_steps, dist, dev)
-    # exposed all-reduce time = what backward did not hide: the same step captured once more
-    # with the bucket all-reduces left out (GradBuckets.skip), the two graphs replayed in
-    # alternation, HIP events around the replays on the replaying stream (timing events
-    # cannot be recorded inside a capture on ROCm).  Measured after the timed loop: the
-    # comm-free replays update each rank's replica with its own gradient only.
-    exposed = None
-    if graph is not None:
-        trainer.buckets.skip = True
-        try:
-            run_nc, graph_nc, _ = capture_train(step, opt, dev, False)
-        finally:
-            trainer.buckets.skip = False
-        t_dp, t_nc = [], []
-        for _ in range(4):
-            for fn, acc in ((run, t_dp), (run_nc, t_nc)):
-                e0 = torch.cuda.Event(enable_timing=True)
-                e1 = torch.cuda.Event(enable_timing=True)
-                e0.record()
-                for _ in range(3):
-                    fn()
-                e1.record()
-                e1.synchronize()
-                acc.append(e0.elapsed_time(e1) / 3)
-        exposed = max(0.0, min(t_dp) - min(t_nc))
-        del run_nc, graph_nc
-    loss_val = run()
-    finite = bool(torch.isfinite(loss_val).item())
-    flat = opt.flat_grad
-    for _ in range(2):
-        trainer.buckets.allreduce_all()
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(5):
-        trainer.buckets.allreduce_all()
-    e1.record()
-    torch.cuda.synchronize()
-    ar_ms = e0.elapsed_time(e1) / 5
-    t = torch.tensor([-1.0 if exposed is None else exposed, ar_ms], device=dev,
-                     dtype=torch.float64)
-    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-    exposed, ar_ms = t.tolist()
-    exposed = None if exposed < 0 else exposed
-    n_ranks = tdist.get_world_size()
-    rccl_ranks = trainer.buckets.comm.count() if trainer_rccl else None
-    if wd is not None:
-        wd.disarm()
-        wd.stop()
+        with _armed(max(1, args.dp_warmup)):
+            step()                                      # learning step of the buckets
+            for _ in range(max(0, args.dp_warmup - 1)):
+                step()
+        nb = len(trainer.buckets.buckets)
+        launched = trainer.buckets.launched_in_backward()
+        graph_err = None
+        with _armed(4):
+            try:
+                run, graph, gout = capture_train(step, opt, dev, args.no_graph)
+            except RuntimeError as e:                   # recorded, the eager step is timed
+                graph_err = f"{type(e).__name__}: {str(e)[:200]}"
+                run, graph, gout = step, None, None
+            for _ in range(2):
+                run()
+        with _armed(args.dp_steps):
+            elapsed = time_steps(run, args.dp_steps, dist, dev)
+        # exposed all-reduce time = what backward did not hide: the same step captured once
+        # more with the bucket all-reduces left out (GradBuckets.skip), the two graphs replayed
+        # in alternation, HIP events around the replays on the replaying stream (timing events
+        # cannot be recorded inside a capture on ROCm).  Measured after the timed loop: the
+        # comm-free replays update each rank's replica with its own gradient only.  At world 1
+        # the all-reduce moves nothing over xGMI, so no overlap is reported there.
+        exposed = None
+        n_ranks = tdist.get_world_size()
+        if graph is not None and n_ranks > 1:
+            with _armed(30):
+                trainer.buckets.skip = True
+                try:
+                    run_nc, graph_nc, _ = capture_train(step, opt, dev, False)
+                finally:
+                    trainer.buckets.skip = False
+                t_dp, t_nc = [], []
+                for _ in range(4):
+                    for fn, acc in ((run, t_dp), (run_nc, t_nc)):
+                        e0 = torch.cuda.Event(enable_timing=True)
+                        e1 = torch.cuda.Event(enable_timing=True)
+                        e0.record()
+                        for _ in range(3):
+                            fn()
+                        e1.record()
+                        e1.synchronize()
+                        acc.append(e0.elapsed_time(e1) / 3)
+                exposed = max(0.0, min(t_dp) - min(t_nc))
+                del run_nc, graph_nc
+        with _armed(10):
+            loss_val = run()
+            finite = bool(torch.isfinite(loss_val).item())
+            flat = opt.flat_grad
+            for _ in range(2):
+                trainer.buckets.allreduce_all()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(5):
+                trainer.buckets.allreduce_all()
+            e1.record()
+            torch.cuda.synchronize()
+            ar_ms = e0.elapsed_time(e1) / 5
+            t = torch.tensor([-1.0 if exposed is None else exposed, ar_ms], device=dev,
+                             dtype=torch.float64)
+            tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        exposed, ar_ms = t.tolist()
+        exposed = None if exposed < 0 else exposed
+        rccl_ranks = trainer.buckets.comm.count() if trainer_rccl else None
+    finally:
+        if wd is not None:
+            wd.disarm()
+            wd.stop()
     grad_bytes = flat.numel() * flat.element_size()
     trainer.buckets.remove()
     del run, graph, gout, net, opt, trainer

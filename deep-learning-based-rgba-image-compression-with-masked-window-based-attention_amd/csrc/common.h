@@ -185,6 +185,29 @@ int check_launch(const char* what);
     }                                                              \
   } while (0)
 
+// Per-device launch facts, cached per device id (a process may drive several GPUs):
+// the CU count, and the dynamic-LDS opt-in of a kernel above 64 KiB (one call per device).
+inline int device_cus() {
+  static int cus[64] = {0};
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (dev < 0 || dev >= 64) dev = 0;
+  if (cus[dev] == 0) {
+    int n = 0;
+    (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    cus[dev] = n > 0 ? n : 256;
+  }
+  return cus[dev];
+}
+inline void lds_optin(const void* kern, int bytes, unsigned long long* done_mask) {
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  const unsigned long long bit = 1ull << (dev & 63);
+  if (*done_mask & bit) return;
+  (void)hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+  *done_mask |= bit;
+}
+
 constexpr int kReduceThreads = 256;
 constexpr int kReduceMaxBlocks = 1024;
 inline int reduce_blocks(int64_t n) {

@@ -1762,15 +1762,7 @@ __global__ void __launch_bounds__(512) conv_npatch_kernel(const ConvArgsDev args
   __shared__ double wsum[TM];
   WG_T(0);
   const ConvShared& s = args.s;
-  int tsp = blockIdx.x, gi = blockIdx.z;         // spatial tile (the GAUSS partial's slot), group
-  {
-    int sp, g_, nb_;
-    if (s.remap == 2 && xcd_spatial(blockIdx.x + gridDim.x * blockIdx.z, gridDim.x, gridDim.z, 1,
-                                    sp, g_, nb_)) {
-      tsp = sp;
-      gi = g_;
-    }
-  }
+  const int tsp = blockIdx.x, gi = blockIdx.z;   // spatial tile (the GAUSS partial's slot), group
   const ConvGroup& g = args.g[gi];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2601,23 +2593,15 @@ __global__ void __launch_bounds__(64 * NW * KS) conv_fpatch_kernel(const ConvArg
   {
     const int nwg = gridDim.x * gridDim.y;
     int t = blockIdx.x + gridDim.x * blockIdx.y;
-    const int S = txn * tyn * s.batch;
-    int sp;
-    if (s.remap == 2 && xcd_spatial(t, S, gridDim.x / S, gridDim.y, sp, gi, nblk)) {
-      txi = sp % txn; sp /= txn;
-      tyi = sp % tyn;
-      b = sp / tyn;
-    } else {
-      if (s.remap) {                             // XCD-contiguous runs, N tile fastest
-        const int xcd = t & 7, q = nwg >> 3, r = nwg & 7;
-        t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (t >> 3);
-      }
-      nblk = t % gridDim.y; t /= gridDim.y;
-      txi = t % txn; t /= txn;
-      tyi = t % tyn; t /= tyn;
-      b = t % s.batch;
-      gi = t / s.batch;
+    if (s.remap) {                               // XCD-contiguous runs, N tile fastest
+      const int xcd = t & 7, q = nwg >> 3, r = nwg & 7;
+      t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (t >> 3);
     }
+    nblk = t % gridDim.y; t /= gridDim.y;
+    txi = t % txn; t /= txn;
+    tyi = t % tyn; t /= tyn;
+    b = t % s.batch;
+    gi = t / s.batch;
   }
   const ConvGroup& g = args.g[gi];
   const int n0 = nblk * BN;
@@ -3293,7 +3277,7 @@ extern "C" int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroup
   s.ngroups = ngroups;
   static const int remap_env = [] {
     const char* e = getenv("RGBAC_XCD_REMAP");
-    return (e && e[0] == '0') ? 0 : (e && e[0] == '2') ? 2 : 1;
+    return (e && e[0] == '0') ? 0 : 1;
   }();
   s.remap = remap_env;
   if (a->tile == kTileNPatch) {

@@ -35,8 +35,8 @@ struct ConvShared {
   int ksize, pad;
   int act; float act_param; int square;
   int ksplit, nphase, ngroups;
-  int remap;                        // XCD-aware block order: 1 contiguous runs, 2 spatial-major
-                                    // (patch kernels); env RGBAC_XCD_REMAP=0|1|2
+  int remap;                        // XCD-aware block order: 1 contiguous runs (env
+                                    // RGBAC_XCD_REMAP=0: plain order)
 };
 
 struct ConvArgsDev {
@@ -535,23 +535,6 @@ __device__ __forceinline__ void wait_ring(int after) {
   }
 }
 
-
-// Spatial-major XCD placement (remap 2, the patch kernels): XCD x runs spatial tiles
-// [x S/8, (x+1) S/8) of every group and N tile.  A chain of launches over the same tile grid
-// -- the slice stacks, whatever their group and N-tile counts -- then keeps each tile on one
-// XCD, whose L2 still holds what the previous launch wrote there (at B 8 on the 32 x 32 latent
-// each XCD owns one image).  lin: linear workgroup id (dealt round-robin to the 8 XCDs).
-// False when S is not a multiple of 8 (callers keep their other order).
-__device__ __forceinline__ bool xcd_spatial(int lin, int S, int G, int NB, int& sp, int& gi,
-                                            int& nb) {
-  if (S & 7) return false;
-  const int xcd = lin & 7;
-  int j = lin >> 3;
-  nb = j % NB; j /= NB;
-  gi = j % G; j /= G;
-  sp = xcd * (S >> 3) + j;
-  return true;
-}
 
 // rgbac_conv_args -> the device-side group descriptor (validates the group; conv.hip)
 int fill_group(const rgbac_conv_args* a, int ntaps_max, ConvGroup& g);

@@ -64,13 +64,12 @@ __device__ __forceinline__ uint4 lds16(const unsigned char* base, int off) {
   return *reinterpret_cast<const uint4*>(base + off);
 }
 
-// NW waves: 8 (two per SIMD; conv1 / conv2 weight fragments read from LDS per tap) or 4 (one
-// per SIMD, 512 registers: conv1's 18 weight fragments held in registers for the whole launch,
-// each wave 10 conv1 fragments and 4 output rows -- a quarter less LDS traffic per tile;
-// RGBAC_DSE_WAVES=4)
-template <int MODE, int CIN, int NW>
-__global__ void __launch_bounds__(64 * NW) dse_block_kernel(const DseArgsDev a) {
+// 8 waves, two per SIMD; conv1 / conv2 weight fragments read from LDS per tap.  (A 4-wave form
+// holding conv1's weights in registers measured 20-40 % slower and was removed)
+template <int MODE, int CIN>
+__global__ void __launch_bounds__(512) dse_block_kernel(const DseArgsDev a) {
   using namespace dse;
+  constexpr int NW = 8;
   constexpr int NTH = 64 * NW;
   constexpr int PRE = (NIV * 4 + NTH - 1) / NTH;             // In chunks per thread (6 / 12)
   constexpr int FST = 1024 * NW;                              // byte step between a wave's fragments
@@ -207,15 +206,6 @@ __global__ void __launch_bounds__(64 * NW) dse_block_kernel(const DseArgsDev a) 
   load_in(t, pre);
   __syncthreads();                                     // weights + biases visible
   store_in(pre);
-  // NW 4: conv1's weight fragments (2 channel halves x 9 taps) in registers for the launch
-  uint4 W1r[NW == 4 ? 2 : 1][NW == 4 ? 9 : 1];
-  if constexpr (NW == 4) {
-#pragma unroll
-    for (int tp = 0; tp < 9; ++tp) {
-      W1r[0][tp] = lds16(smem, ((0 * 9 + tp) * 64 + lane) * 16);
-      W1r[1][tp] = lds16(smem, ((1 * 9 + tp) * 64 + lane) * 16);
-    }
-  }
 
   for (; t < ntiles; t += gridDim.x) {
     int tt = t;
@@ -237,13 +227,8 @@ __global__ void __launch_bounds__(64 * NW) dse_block_kernel(const DseArgsDev a) 
       const int ax = extra ? wave : 0;                 // the extra fragment's channel half
       uint4 A[2][2], B[2][NF], BX[2], AX[2];
       auto load = [&](int tp, int sb) {
-        if constexpr (NW == 4) {
-          A[sb][0] = W1r[0][tp];
-          A[sb][1] = W1r[1][tp];
-        } else {
-          A[sb][0] = lds16(smem, ((0 * 9 + tp) * 64 + lane) * 16);
-          A[sb][1] = lds16(smem, ((1 * 9 + tp) * 64 + lane) * 16);
-        }
+        A[sb][0] = lds16(smem, ((0 * 9 + tp) * 64 + lane) * 16);
+        A[sb][1] = lds16(smem, ((1 * 9 + tp) * 64 + lane) * 16);
 #pragma unroll
         for (int i = 0; i < NF; ++i) B[sb][i] = lds16(smem, o1[tp] + FST * i);
         if (extra) {
@@ -420,35 +405,19 @@ extern "C" int rgbac_dse_block(int mode, int batch, int h, int w, int cin, float
   d.w2 = reinterpret_cast<const bf16_t*>(w2); d.kp2 = kp2; d.b2 = b2;
   d.w_out = reinterpret_cast<const bf16_t*>(w_out); d.kp_out = kp_out; d.b_out = b_out;
   d.out = reinterpret_cast<bf16_t*>(out); d.ldo = ldo;
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu < 1) ncu = 256;
-  }
+  const int ncu = device_cus();
   const long long ntiles = (long long)batch * ((h + dse::TY - 1) / dse::TY) * ((w + dse::TX - 1) / dse::TX);
   RGBAC_REQUIRE(ntiles < (1LL << 30), "too many tiles");
   const int grid = (int)(ntiles < ncu ? ntiles : ncu);
   const size_t lds = dse::LDS;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int key = mode == 1 ? 10 : mode * 100 + cin;
-  const char* wenv = getenv("RGBAC_DSE_WAVES");      // read per call (tests switch it)
-  const bool w4 = wenv && wenv[0] == '4';
   switch (key) {
-#define RGBAC_DSE_NW(M_, C_, NW_)                                                               \
-  {                                                                                             \
-    static bool attr = false;                                                                   \
-    if (!attr) {                                                                                \
-      (void)hipFuncSetAttribute(reinterpret_cast<const void*>(dse_block_kernel<M_, C_, NW_>),   \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);          \
-      attr = true;                                                                              \
-    }                                                                                           \
-    hipLaunchKernelGGL((dse_block_kernel<M_, C_, NW_>), dim3(grid), dim3(64 * NW_), lds, st, d); \
-  }
 #define RGBAC_DSE(M_, C_)                                                                       \
   case (M_ == 1 ? 10 : M_ * 100 + C_): {                                                      \
-    if (w4) RGBAC_DSE_NW(M_, C_, 4) else RGBAC_DSE_NW(M_, C_, 8)                                \
+    static unsigned long long attr = 0;                                                         \
+    lds_optin(reinterpret_cast<const void*>(dse_block_kernel<M_, C_>), (int)lds, &attr);       \
+    hipLaunchKernelGGL((dse_block_kernel<M_, C_>), dim3(grid), dim3(512), lds, st, d);          \
     break;                                                                                      \
   }
     RGBAC_DSE(0, 1)
@@ -457,7 +426,6 @@ extern "C" int rgbac_dse_block(int mode, int batch, int h, int w, int cin, float
     RGBAC_DSE(2, 1)
     RGBAC_DSE(2, 3)
 #undef RGBAC_DSE
-#undef RGBAC_DSE_NW
     default:
       RGBAC_REQUIRE(false, "DSE input channels must be 1 or 3");
   }

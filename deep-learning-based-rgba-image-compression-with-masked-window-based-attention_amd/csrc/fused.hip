@@ -613,9 +613,9 @@ __device__ unsigned long long g_ru_w[8192][2];     // wall clock (100 MHz) at st
 #define RU_T(k) do {} while (0)
 #endif
 
-// TYV = 8: 8 x 16 tiles, 4 waves, two workgroups per CU.  TYV = 16 (RGBAC_RU_TILE16=1): 16 x 16
-// tiles, 8 waves, one workgroup per CU -- the same pixels per CU with each weight fragment
-// streamed once per CU instead of twice and 1.27x halo instead of 1.41x.
+// TYV = 8: 8 x 16 tiles, 4 waves, two workgroups per CU (the launched form).  16 x 16 tiles at
+// one 8-wave workgroup per CU measured 4-5 % slower and were removed, as were
+// 8 x 8 half tiles (14k).
 template <int RB, int TYV>
 __global__ void __launch_bounds__(32 * TYV, TYV == 8 ? 2 : 1) ru_stream_kernel(const RuArgsDev args) {
   using namespace rsw;
@@ -863,252 +863,6 @@ __global__ void __launch_bounds__(32 * TYV, TYV == 8 ? 2 : 1) ru_stream_kernel(c
 }
 #undef RU_T
 
-// ---------------------------------------------------------------------------------------
-// The C = 192 bottleneck on HALF-size tiles (ru_half_kernel): ru_stream_kernel's three GEMMs
-// per 8 x 8 output tile, sized to run FOUR workgroups per CU (<= 128 VGPRs, 38 KB of LDS)
-// instead of two.  At the benchmark's batch every ru_stream launch is one round of workgroups
-// whose time is one workgroup's dependency chain (a B 4 launch takes 70 % of a B 8 one,
-// DESIGN.md section 14j); half the pixels per workgroup halves each chain and four waves per
-// SIMD hide more of each wave's latencies, for 11 % more stage-1 halo work (100 halo pixels
-// per 64 instead of 180 per 128).
-//   stage 1: T1 = act(W1 x + b1) on the 10 x 10 halo: 7 m tiles of 16 halo pixels (waves
-//            0..2 two, wave 3 one), the 6 N tiles in two halves of 3 (register budget); the
-//            x fragments stay in registers for both halves
-//   stage 2: T2 = act(W2 (*) T1 + b2): waves = 2 channel halves x 2 pixel halves (32 pixels =
-//            2 m tiles of two 8-pixel rows), 27 k-steps of 3 x 2 MFMAs
-//   stage 3: y = [GELU](W3 T2 + b3 + x): 3 k-steps of 6 x 2 MFMAs; output staged over the
-//            dead T1 + T2 for whole 16-byte stores
-namespace rsh {
-constexpr int T = 8, HX = 10, NH = 100, NHP = 112;
-constexpr int TROW = 208, ORW = 400;
-constexpr int NK1 = 6, NK2 = 27, NK3 = 3;
-constexpr int R1 = 2, R2 = 4, R3 = 2;
-constexpr int T1B = NHP * TROW, T2B = T * T * TROW;           // 23296 + 13312
-static_assert(T * T * ORW <= T1B + T2B, "output staging fits over T1 + T2");
-}  // namespace rsh
-
-template <int RB, int NT>
-__global__ void __launch_bounds__(256, 4 / NT) ru_half_kernel(const RuArgsDev args) {
-  using namespace rsh;
-  __shared__ __attribute__((aligned(16))) unsigned char lds[T1B + T2B];
-  unsigned char* const T1 = lds;
-  unsigned char* const T2 = lds + T1B;
-  unsigned char* const OT = lds;
-  __shared__ __attribute__((aligned(16))) float bs[96 + 96 + 192];
-  const RuGroup& g = args.g[blockIdx.z];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int fr = lane & 15, fq = lane >> 4;
-  const int tx_n = args.W / T, ty_n = args.H / T;
-  int t0 = blockIdx.x;
-  {                                                // XCD-contiguous runs of neighbouring tiles
-    const int nwg = gridDim.x, xcd = t0 & 7, q = nwg >> 3, r = nwg & 7;
-    t0 = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (t0 >> 3);
-  }
-  t0 *= NT;                                        // this workgroup's NT neighbouring tiles
-
-  for (int e = tid; e < 384; e += 256) bs[e] = e < 96 ? g.b1[e] : e < 192 ? g.b2[e - 96] : g.b3[e - 192];
-  const int nm = wave < 3 ? 2 : 1;                 // this wave's halo m tiles (wave-uniform)
-  const int wn = wave >> 1, wm = wave & 1;
-  const int prow = (lane & 15) >> 3, pcol = lane & 7;
-  int hp[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) hp[i] = 16 * (2 * wave + i) + fr;
-  bool xin[2];
-  uint4 xb[NK1][2];
-  // x fragments of tile tt's halo (k-step-major issue order); also sets xin for its epilogue
-  auto load_x = [&](int tt) {
-    const int tx = tt % tx_n, ty = (tt / tx_n) % ty_n, b = tt / (tx_n * ty_n);
-    unsigned xoff[2];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int hy = hp[i] / HX, hx = hp[i] - (hp[i] / HX) * HX;
-      const int iy = ty * T + hy - 1, ix = tx * T + hx - 1;
-      xin[i] = i < nm && hp[i] < NH && iy >= 0 && iy < args.H && ix >= 0 && ix < args.W;
-      xoff[i] = (unsigned)(((b * args.H + (xin[i] ? iy : 0)) * args.W + (xin[i] ? ix : 0)) * g.ldx +
-                           fq * 8);
-    }
-#pragma unroll
-    for (int ks = 0; ks < NK1; ++ks)
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        xb[ks][i] = xin[i] ? *reinterpret_cast<const uint4*>(g.x + xoff[i] + ks * 32)
-                           : make_uint4(0, 0, 0, 0);
-  };
-  load_x(t0);
-  __syncthreads();                                 // bs visible
-
-#pragma unroll 1
-  for (int s = 0; s < NT; ++s) {
-    const int tt = t0 + s;
-    const int tx = tt % tx_n, ty = (tt / tx_n) % ty_n, b = tt / (tx_n * ty_n);
-    const int y0 = ty * T, x0 = tx * T;
-    // weight fragment pointers re-formed per tile from an opaque lane index: the loads are
-    // loop-invariant, and hoisting all of them out of the tile loop would need 540 registers
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    const uint4* const W1 = reinterpret_cast<const uint4*>(g.w1) + ln;
-    const uint4* const W2 = reinterpret_cast<const uint4*>(g.w2) + ln + (size_t)(3 * wn) * NK2 * 64;
-    const uint4* const W3 = reinterpret_cast<const uint4*>(g.w3) + ln + (size_t)(6 * wn) * NK3 * 64;
-    // ================= stage 1
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      uint4 w1r[R1][3];
-#pragma unroll
-      for (int u = 0; u < R1; ++u)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) w1r[u][j] = W1[((3 * half + j) * NK1 + u) * 64];
-      f32x4 acc1[3][2];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) acc1[j][0] = acc1[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < NK1; ++ks) {
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-          mma_step<bf16_t>(acc1[j][0], w1r[ks % R1][j], xb[ks][0]);
-          if (nm > 1) mma_step<bf16_t>(acc1[j][1], w1r[ks % R1][j], xb[ks][1]);
-        }
-        if (ks + R1 < NK1) {
-#pragma unroll
-          for (int j = 0; j < 3; ++j) w1r[ks % R1][j] = W1[((3 * half + j) * NK1 + ks + R1) * 64];
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 3; ++j) {
-        const int n = 16 * (3 * half + j) + 4 * fq;
-        const float4 bb = *reinterpret_cast<const float4*>(bs + n);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          if (i >= nm) break;
-          float v[4];
-          ru_act4<RB>(v, acc1[j][i], bb);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = xin[i] ? v[r] : 0.0f;
-          Elem<bf16_t>::st4(reinterpret_cast<bf16_t*>(&T1[hp[i] * TROW + n * 2]), v);
-        }
-      }
-    }
-    // stage-2 weights for the first R2 k-steps
-    uint4 w2r[R2][3];
-#pragma unroll
-    for (int u = 0; u < R2; ++u)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) w2r[u][j] = W2[(j * NK2 + u) * 64];
-    __syncthreads();                               // T1 complete
-
-    // ================= stage 2: m tile i = tile rows 4 wm + 2 i, +1 (lanes fr < 8 / >= 8)
-    f32x4 acc2[3][2];
-#pragma unroll
-    for (int j = 0; j < 3; ++j) acc2[j][0] = acc2[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const unsigned char* const t1l = T1 + ((4 * wm + prow) * HX + pcol) * TROW + fq * 16;
-#pragma unroll
-    for (int ks = 0; ks < NK2; ++ks) {
-      const int tap = ks / 3, c = ks % 3;
-      const int off = ((tap / 3) * HX + tap % 3) * TROW + c * 64;
-      uint4 bv[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) bv[i] = *reinterpret_cast<const uint4*>(t1l + i * 2 * HX * TROW + off);
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) mma_step<bf16_t>(acc2[j][i], w2r[ks % R2][j], bv[i]);
-      if (ks + R2 < NK2) {
-#pragma unroll
-        for (int j = 0; j < 3; ++j) w2r[ks % R2][j] = W2[(j * NK2 + ks + R2) * 64];
-      }
-      asm volatile("" ::: "memory");
-    }
-    // stage-3 weights, then (NT > 1) the residual and the NEXT tile's x fragments: issued in
-    // that order, so each wait below is on loads older than the prefetch (vmcnt counts in
-    // issue order) and the prefetch lands behind this tile's stage-2 epilogue and stage 3
-    constexpr int R3E = NT > 1 ? NK3 : R3;
-    uint4 w3r[R3E][6];
-#pragma unroll
-    for (int u = 0; u < R3E; ++u)
-#pragma unroll
-      for (int j = 0; j < 6; ++j) w3r[u][j] = W3[(j * NK3 + u) * 64];
-    uint2 res[2][6];
-    auto load_res = [&]() {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const bf16_t* xr = g.x + (unsigned)(((b * args.H + y0 + 4 * wm + 2 * i + prow) * args.W +
-                                             x0 + pcol) * g.ldx + 96 * wn + 4 * fq);
-#pragma unroll
-        for (int j = 0; j < 6; ++j) res[i][j] = *reinterpret_cast<const uint2*>(xr + 16 * j);
-      }
-    };
-    if constexpr (NT > 1) {
-      load_res();
-      if (s + 1 < NT) load_x(tt + 1);
-    }
-#pragma unroll
-    for (int j = 0; j < 3; ++j) {
-      const int n = 48 * wn + 16 * j + 4 * fq;
-      const float4 bb = *reinterpret_cast<const float4*>(bs + 96 + n);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int p = (4 * wm + 2 * i + prow) * T + pcol;
-        float v[4];
-        ru_act4<RB>(v, acc2[j][i], bb);
-        Elem<bf16_t>::st4(reinterpret_cast<bf16_t*>(&T2[p * TROW + n * 2]), v);
-      }
-    }
-    __syncthreads();                               // T2 complete
-
-    // ================= stage 3
-    f32x4 acc3[6][2];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) acc3[j][0] = acc3[j][1] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const unsigned char* const t2l = T2 + ((4 * wm + prow) * T + pcol) * TROW + fq * 16;
-#pragma unroll
-    for (int ks = 0; ks < NK3; ++ks) {
-      uint4 bv[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) bv[i] = *reinterpret_cast<const uint4*>(t2l + i * 2 * T * TROW + ks * 64);
-#pragma unroll
-      for (int j = 0; j < 6; ++j)
-#pragma unroll
-        for (int i = 0; i < 2; ++i) mma_step<bf16_t>(acc3[j][i], w3r[ks % R3E][j], bv[i]);
-      if (ks + R3E < NK3) {
-#pragma unroll
-        for (int j = 0; j < 6; ++j) w3r[ks % R3E][j] = W3[(j * NK3 + ks + R3E) * 64];
-      }
-    }
-    if constexpr (NT == 1) load_res();             // (after the MFMAs: register budget)
-    float4 b3v[6];
-#pragma unroll
-    for (int j = 0; j < 6; ++j) b3v[j] = *reinterpret_cast<const float4*>(bs + 192 + 96 * wn + 16 * j + 4 * fq);
-    __syncthreads();                               // every wave is done reading T2
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int p = (4 * wm + 2 * i + prow) * T + pcol;
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        const int n = 96 * wn + 16 * j + 4 * fq;
-        const float4 bb = b3v[j];
-        const uint2 rr = res[i][j];
-        float v[4];
-        v[0] = acc3[j][i][0] + bb.x + bf2f(rr.x & 0xFFFF);
-        v[1] = acc3[j][i][1] + bb.y + bf2f(rr.x >> 16);
-        v[2] = acc3[j][i][2] + bb.z + bf2f(rr.y & 0xFFFF);
-        v[3] = acc3[j][i][3] + bb.w + bf2f(rr.y >> 16);
-        if (!RB) gelu4_fast(v);
-        Elem<bf16_t>::st4(reinterpret_cast<bf16_t*>(OT + p * ORW + n * 2), v);
-      }
-    }
-    __syncthreads();
-    // whole 16-byte chunks, consecutive lanes on consecutive chunks of a pixel's 384 bytes
-#pragma unroll
-    for (int u = 0; u < T * T * 24 / 256; ++u) {
-      const int c = tid + 256 * u, p = c / 24, q = c - (c / 24) * 24;
-      const long long pix = (long long)(b * args.H + y0 + p / T) * args.W + x0 + p % T;
-      *reinterpret_cast<uint4*>(g.out + pix * g.ldo + q * 8) =
-          *reinterpret_cast<const uint4*>(OT + p * ORW + q * 16);
-    }
-    if (s + 1 < NT) __syncthreads();               // OT read out before the next T1
-  }
-}
-
 }  // namespace rgbac
 
 using namespace rgbac;
@@ -1206,26 +960,6 @@ extern "C" int rgbac_residual_unit_ex(const rgbac_ru_args* args, int ngroups, in
     for (int i = 0; i < ngroups; ++i)
       RGBAC_REQUIRE((long long)a->batch * a->h * a->w * args[i].x_ldc < (1ll << 31),
                     "the streamed unit addresses x with 32-bit element offsets");
-    const char* half_env = getenv("RGBAC_RU_HALF");  // read per call (tests switch it)
-    if (half_env && half_env[0] == '1') {            // 8 x 8 tiles, four workgroups per CU
-      const unsigned t8 = (unsigned)(tiles * 2);
-      if (kind) hipLaunchKernelGGL((ru_half_kernel<1, 1>), dim3(t8, 1, ngroups), dim3(256), 0, st, d);
-      else hipLaunchKernelGGL((ru_half_kernel<0, 1>), dim3(t8, 1, ngroups), dim3(256), 0, st, d);
-      return check_launch("ru_half_kernel");
-    }
-    if (half_env && half_env[0] == '2') {            // two 8 x 8 tiles per workgroup, pipelined
-      const unsigned t8 = (unsigned)tiles;
-      if (kind) hipLaunchKernelGGL((ru_half_kernel<1, 2>), dim3(t8, 1, ngroups), dim3(256), 0, st, d);
-      else hipLaunchKernelGGL((ru_half_kernel<0, 2>), dim3(t8, 1, ngroups), dim3(256), 0, st, d);
-      return check_launch("ru_half_kernel");
-    }
-    const char* t16_env = getenv("RGBAC_RU_TILE16");  // read per call (tests switch it)
-    if (t16_env && t16_env[0] == '1' && a->h % 16 == 0) {
-      const unsigned t16 = (unsigned)(tiles / 2);
-      if (kind) hipLaunchKernelGGL((ru_stream_kernel<1, 16>), dim3(t16, 1, ngroups), dim3(512), 0, st, d);
-      else hipLaunchKernelGGL((ru_stream_kernel<0, 16>), dim3(t16, 1, ngroups), dim3(512), 0, st, d);
-      return check_launch("ru_stream_kernel");
-    }
     if (kind) hipLaunchKernelGGL((ru_stream_kernel<1, 8>), dim3((unsigned)tiles, 1, ngroups), dim3(256), 0, st, d);
     else hipLaunchKernelGGL((ru_stream_kernel<0, 8>), dim3((unsigned)tiles, 1, ngroups), dim3(256), 0, st, d);
     return check_launch("ru_stream_kernel");

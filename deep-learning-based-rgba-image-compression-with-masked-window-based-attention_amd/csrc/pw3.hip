@@ -215,18 +215,9 @@ template <int ACT>
 static void launch_pw3_k(const ConvArgsDev& d, hipStream_t st) {
   auto kern = conv_pw3_kernel<6, ACT>;
   constexpr size_t lds = ((size_t)192 * 24 + (size_t)kPw3Waves * 2 * 16 * 24) * 16;
-  static bool attr = false;
-  static int ncu = 0;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu < 1) ncu = 256;
-    (void)hipGetLastError();
-    attr = true;
-  }
+  static unsigned long long attr = 0;                 // per device (lds_optin, common.h)
+  lds_optin((const void*)kern, (int)lds, &attr);
+  const int ncu = device_cus();
   const int nz = d.s.ngroups;
   const int ntile = (d.s.M + 15) / 16;
   int gx = (ncu + nz - 1) / nz;

@@ -35,7 +35,9 @@
 // V^T [2 win][3 channel tiles][2 key pairs] 12 KiB | relative-position bias [table,
 // table - 100 (the shift mask folded in)][8 heads][225] fp32 | proj bias -> 136,000 B.
 // All fragment images are lane-major (16 B per lane): conflict-free ds_read/write_b128.
+#include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 
@@ -128,7 +130,7 @@ __device__ unsigned long long g_wb_w[8192][2];     // wall clock (100 MHz) at st
 #define WB_T(k) do {} while (0)
 #endif
 
-__global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlockArgs a) {
+__global__ void __launch_bounds__(512, 1) winblock_v2_kernel(const WinBlockArgs a) {
   using namespace wb;
   constexpr float LOG2E = 1.4426950408889634f;
   extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
@@ -452,6 +454,554 @@ __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlockArgs a) 
 
 
 // ---------------------------------------------------------------------------------------
+// Round 6: the ws-8 block as persistent kernels over the ACTIVE windows.
+//
+// winblock_v2_kernel (round 3, kept for the A/B until it is removed) runs one 8-wave workgroup
+// per window PAIR and streams all four head pairs' weights (288 KiB) through its LDS for those
+// 128 tokens: a 42k-cycle chain per workgroup, one round of workgroups at config 2 (DESIGN
+// 12c).  Here:
+//   winflag_kernel   one wave per window: flag = alpha non-zero anywhere in the (shifted)
+//                    window (remove_zero_windows, :38-47), no host sync;
+//   winblock_kernel  one workgroup per (head pair, slot), persistent: the pair's 54 KiB qkv
+//                    panel stays in LDS; a block scan of the flags deals active window r to
+//                    slot r % slots (device-side compaction), and the workgroup walks its
+//                    windows two at a time -- 8 waves, token tile w & 3, role w >> 2 (0: q^T
+//                    tiles 0-2 + k^T tiles 0-1, 1: k^T tile 2 + v tiles 0-2), so every qkv
+//                    weight fragment read from LDS feeds two MFMAs and each SIMD (waves w,
+//                    w + 4) issues 108 of the pair's 432 qkv MFMAs; x fragments arrive by
+//                    LDS-DMA (the next pair's during this pair's attention); K, V^T and the
+//                    head-1 q^T fragments cross waves through LDS; wave (head w >> 2, query
+//                    tile w & 3) runs S^T = K Q^T, the softmax and O^T = V^T P^T in registers
+//                    and stores O^T (bf16) to the window's slot of the workspace.  Inactive
+//                    windows are copied out = x (MASKSEL, :236-240) by the workgroups in
+//                    inactive-rank order; pair 0's workgroups publish the compacted list;
+//   winproj_kernel   persistent over that list: out = x + Wp O^T + b for every token of an
+//                    active window, the 72 KiB proj panel resident, each window's O^T
+//                    fragments LDS-DMA'd one window ahead.
+// The four workgroups of a slot have the same blockIdx & 7, so they sit on one XCD and share
+// the windows' x in L2.  Every product, rounding point and accumulation order is
+// winblock_v2_kernel's (O^T is rounded to bf16 exactly where that kernel rounds it before the
+// proj), so the two paths are bit-identical.
+namespace wb3 {
+constexpr int WQF = 54, WPF = 72;
+// winblock_kernel
+constexpr int L_WQ = 0;                                // the pair's qkv fragments
+constexpr int L_X = L_WQ + WQF * 1024;                 // 55296: x [win 2][token tile 4][k-step 6]
+constexpr int L_K = L_X + 48 * 1024;                   // 104448: K [win 2][head 2][key tile 4]
+constexpr int L_V = L_K + 16 * 1024;                   // 120832: V^T [win 2][channel tile 3][key pair 2]
+constexpr int L_Q = L_V + 12 * 1024;                   // 133120: q^T [win 2][head 2][token tile 4]
+constexpr int L_TB = L_Q + 16 * 1024;                  // 149504: bias [var 2][head 2][225] fp32
+constexpr int L_BQ = L_TB + 2 * 2 * 225 * 4;           // 153104: [bq 48 | bk 48 | bv 48] (1 KiB piece)
+constexpr int L_LA = L_BQ + 1024;                      // 154128: this workgroup's active windows
+constexpr int MAXA = 256;
+constexpr int L_LC = L_LA + MAXA * 2;                  // 154640: its inactive windows
+constexpr int MAXC = 64;
+constexpr int L_MS = L_LC + MAXC * 2;                  // 154768: scan partials [8]
+constexpr int LDS_A = L_MS + 64;                       // 154832
+static_assert(LDS_A <= 160 * 1024, "LDS");
+// prologue staging, free until the first x DMA: the launch's flags at L_X (8 KiB), the raw
+// table [225][8] (padded to 8 KiB) at L_X + 8 KiB
+// winproj_kernel
+constexpr int P_WP = 0;                                // all proj fragments [u][m][s]
+constexpr int P_O = P_WP + WPF * 1024;                 // 73728: O^T [buf 2][token tile 4][k-step 6]
+constexpr int P_BP = P_O + 48 * 1024;                  // 122880: bproj (1 KiB piece)
+constexpr int LDS_B = P_BP + 1024;                     // 123904
+constexpr int CHUNK = 8192;                            // windows per launch: 16 flags per thread
+constexpr int OSLOT = 4 * 6 * 64 * 2;                  // 8-byte words of one window's O^T (24 KiB)
+}  // namespace wb3
+
+struct WinBlock3Args {
+  int batch, H, W, shift, masked;
+  int w0, nwc, slots, chunk;             // window range of this launch; workgroups per pair
+  float scale;
+  const bf16_t* x; long long ldx;
+  const float* alpha;                    // (B, H, W) fp32 (masked; winflag_kernel only)
+  uint8_t* flags;                        // [windows]: alpha non-zero somewhere in the window
+  const bf16_t* wq;                      // [4 pairs][54][64 lanes][8]
+  const float* bias;                     // [5][256]: bproj | pair p: bq, bk, bv (48 each)
+  const bf16_t* wp;                      // [2][12][3][64][8] (permuted k)
+  const float* table;                    // relative_position_bias_table [225][8], padded to 2048
+  bf16_t* out; long long ldo;
+  unsigned long long* oscr;              // [windows][4 token tiles][6 k-steps][64 lanes][2]
+  int* alist;                            // [windows]: active rank -> window (per launch at w0)
+  int* acount;                           // [launches]: active windows of the launch
+};
+
+// per-window alpha flags: one wave per window, the 64 alpha values of its (shifted) pixels
+__global__ void __launch_bounds__(256) winflag_kernel(const WinBlock3Args a) {
+  const int lane = threadIdx.x & 63;
+  const int win = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int nwx = a.W >> 3, nwimg = nwx * (a.H >> 3);
+  if (win >= a.batch * nwimg) return;
+  const int b = win / nwimg, rem = win - b * nwimg;
+  const int wy = rem / nwx, wx = rem - wy * nwx;
+  int oy = wy * 8 + (lane >> 3) + a.shift; if (oy >= a.H) oy -= a.H;
+  int ox = wx * 8 + (lane & 7) + a.shift; if (ox >= a.W) ox -= a.W;
+  const bool act = __any(a.alpha[((long long)b * a.H + oy) * a.W + ox] != 0.0f);
+  if (lane == 0) a.flags[win] = act ? 1 : 0;
+}
+
+__device__ __forceinline__ int wb_win_pix(int wg, int lt, int H, int W, int nwx, int nwimg,
+                                          int shift) {               // token lt of window wg
+  const int b = wg / nwimg, rem = wg - b * nwimg;
+  const int wy = rem / nwx, wx = rem - wy * nwx;
+  int oy = wy * 8 + (lt >> 3) + shift; if (oy >= H) oy -= H;
+  int ox = wx * 8 + (lt & 7) + shift; if (ox >= W) ox -= W;
+  return (b * H + oy) * W + ox;
+}
+
+__global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlock3Args a) {
+  using namespace wb3;
+  constexpr float LOG2E = 1.4426950408889634f;
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = lane & 15, qq = lane >> 4;
+  const int g = blockIdx.x, slots = a.slots, G = 4 * slots;
+  const int p = (g >> 3) & 3;                          // head pair
+  const int slot = ((g >> 5) << 3) | (g & 7);          // a slot's four pair workgroups: one XCD
+  const int H = a.H, W = a.W, shift = a.shift;
+  const int nwx = W >> 3, nwimg = nwx * (H >> 3);
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) void*)sm;
+  const int tt = w & 3, hr = w >> 2;                   // token tile; role and attention head
+  WB_T(0);
+
+  // ---- prologue DMA: three staging pieces per wave (flags, raw table, the pair's biases),
+  // then the pair's qkv panel (pieces past the end repeat the last one: same bytes, same place)
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    int k = w + 8 * i;
+    if (k > 16) k = 16;
+    const void* src;
+    int dst;
+    if (k < 8) { src = a.flags + a.w0 + k * 1024 + lane * 16; dst = L_X + k * 1024; }
+    else if (k < 16) { src = a.table + (k - 8) * 256 + lane * 4; dst = L_X + 8192 + (k - 8) * 1024; }
+    else { src = a.bias + 256 * (1 + p) + lane * 4; dst = L_BQ; }
+    wb_dma16(src, lds0 + dst);
+  }
+  const bf16_t* wqp = a.wq + (size_t)p * WQF * 512;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    int f = w + 8 * i;
+    if (f >= WQF) f = WQF - 1;
+    wb_dma16(wqp + ((size_t)f * 64 + lane) * 8, lds0 + L_WQ + f * 1024);
+  }
+  wb_wait_vm<7>();                                     // the staging pieces landed
+  __syncthreads();
+
+  // ---- this workgroup's windows: block scan of the active flags (16 windows per thread)
+  short* const la = reinterpret_cast<short*>(sm + L_LA);
+  short* const lc = reinterpret_cast<short*>(sm + L_LC);
+  int* const ms = reinterpret_cast<int*>(sm + L_MS);
+  const int nwc = a.nwc;
+  unsigned bits = 0;
+  {
+    const uint4 fv = *reinterpret_cast<const uint4*>(sm + L_X + 16 * tid);
+    const uint32_t fw[4] = {fv.x, fv.y, fv.z, fv.w};
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const bool on = 16 * tid + e < nwc && (!a.masked || ((fw[e >> 2] >> (8 * (e & 3))) & 0xFFu) != 0);
+      bits |= (on ? 1u : 0u) << e;
+    }
+  }
+  const int cntv = __popc(bits);
+  int inc = cntv;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(inc, d);
+    if (lane >= d) inc += y;
+  }
+  if (lane == 63) ms[w] = inc;
+  {                                                    // table [225][8] -> [var][head][225]
+    const float* raw = reinterpret_cast<const float*>(sm + L_X + 8192);
+    float* tb = reinterpret_cast<float*>(sm + L_TB);
+    for (int e = tid; e < 2 * 225; e += 512) {
+      const int hh = e >= 225 ? 1 : 0, idx = e - 225 * hh;
+      const float v = raw[idx * 8 + 2 * p + hh];
+      tb[hh * 225 + idx] = v * LOG2E;
+      tb[2 * 225 + hh * 225 + idx] = (v + -100.0f) * LOG2E;   // the shift mask's -100 folded in
+    }
+  }
+  __syncthreads();
+  int nact = 0, before = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int v = ms[i];
+    nact += v;
+    before += i < w ? v : 0;
+  }
+  {
+    const int r = before + inc - cntv;                 // active windows before 16 tid
+    int rq = r / slots, rm = r - rq * slots;
+    const int q0 = min(16 * tid, nwc) - r;             // inactive windows before 16 tid
+    int iq = q0 / G, im = q0 - iq * G;
+    for (int e = 0; e < 16; ++e) {
+      const int idx = 16 * tid + e;
+      if (idx >= nwc) break;
+      if ((bits >> e) & 1u) {
+        if (rm == slot) la[rq] = (short)idx;
+        if (g == 0) a.alist[a.w0 + rq * slots + rm] = a.w0 + idx;   // the compacted list
+        if (++rm == slots) { rm = 0; ++rq; }
+      } else {
+        if (im == g) lc[iq] = (short)idx;
+        if (++im == G) { im = 0; ++iq; }
+      }
+    }
+  }
+  if (g == 0 && tid == 0) a.acount[a.chunk] = nact;
+  const int nmine = nact > slot ? (nact - 1 - slot) / slots + 1 : 0;
+  const int ninact = nwc - nact;
+  const int ncopy = ninact > g ? (ninact - 1 - g) / G + 1 : 0;
+  const int npair = (nmine + 1) >> 1;
+  __syncthreads();                                     // lists visible; the staging area free
+  WB_T(1);
+
+  // x of windows (wa, wb) as fragment images [win][tt][ks] by LDS-DMA: 48 pieces, 6 per wave
+  // (piece k: window k / 24, token tile (k / 6) & 3, k-step k % 6; lane (n, qq) fetches token
+  // 16 tt + n, channels 32 ks + 8 qq ..)
+  auto dma_x = [&](int wa, int wb) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) {
+      const int k = w + 8 * i;
+      const int wi = k / 24, t4 = (k / 6) & 3, ks = k % 6;
+      const int pix = wb_win_pix(wi ? wb : wa, 16 * t4 + n, H, W, nwx, nwimg, shift);
+      wb_dma16(a.x + (long long)pix * a.ldx + 32 * ks + 8 * qq, lds0 + L_X + k * 1024);
+    }
+  };
+  if (npair > 0) dma_x(a.w0 + la[0], a.w0 + la[nmine > 1 ? 1 : 0]);
+  wb_wait_all();                                       // qkv panel and the first windows' x
+  __syncthreads();
+
+  // relative-position-bias offsets of this lane's S^T elements (key 16 kt + 4 qq + r, query
+  // 16 tt + n) in this wave's head's table: idx(kt, r) = idx(3, 3) + 30 (3 - kt) + 3 - r, so
+  // one base per lane plus immediates; cut bit 4 kt + r selects the "- 100" copy where the
+  // shift mask separates query and key
+  const int iq = 16 * tt + n;
+  const int tbase = L_TB + hr * 900 +
+                    4 * (((iq >> 3) - 6 - (qq >> 1) + 7) * 15 + ((iq & 7) - 4 * (qq & 1) - 3 + 7));
+  auto make_cut = [&](int wg) -> unsigned {
+    if (shift == 0) return 0u;
+    const int rem = wg % nwimg;
+    const int wy = rem / nwx, wx = rem - wy * nwx;
+    auto rid = [&](int t) {
+      const int r = wy * 8 + (t >> 3), c = wx * 8 + (t & 7);
+      return 3 * (r < H - 8 ? 0 : (r < H - shift ? 1 : 2)) + (c < W - 8 ? 0 : (c < W - shift ? 1 : 2));
+    };
+    const int qrid = rid(iq);
+    unsigned m = 0;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) m |= (rid(16 * kt + 4 * qq + r) != qrid ? 1u : 0u) << (4 * kt + r);
+    return m;
+  };
+  WB_T(2);
+
+  const float qscale = a.scale * LOG2E;                // q * scale, in log2 units
+  const uint32_t lo8 = n < 8 ? 0xFFFFFFFFu : 0u;       // lane holds channel row < 8 of a tile
+  const uint32_t qlo = qq < 2 ? 0xFFFFFFFFu : 0u;      // lane's accumulator rows are < 8
+  const float* bqs = reinterpret_cast<const float*>(sm + L_BQ);
+
+  // q^T, k^T, v of the pair's heads for this wave's 16 tokens of NWIN windows: every weight
+  // fragment read once, used for each window
+  auto gemm = [&](auto nw_c) {
+    constexpr int NWIN = decltype(nw_c)::value;
+    if (hr == 0) {
+      f32x4 aq[NWIN][3], ak[NWIN][2];
+#pragma unroll
+      for (int v = 0; v < NWIN; ++v) {
+#pragma unroll
+        for (int t = 0; t < 3; ++t) aq[v][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 2; ++t) ak[v][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int ks = 0; ks < 6; ++ks) {
+        uint4 X[NWIN];
+#pragma unroll
+        for (int v = 0; v < NWIN; ++v)
+          X[v] = *reinterpret_cast<const uint4*>(sm + L_X + ((v * 4 + tt) * 6 + ks) * 1024 + lane * 16);
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const uint4 f = *reinterpret_cast<const uint4*>(sm + L_WQ + (t * 6 + ks) * 1024 + lane * 16);
+#pragma unroll
+          for (int v = 0; v < NWIN; ++v) mma_step<bf16_t>(aq[v][t], f, X[v]);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const uint4 f = *reinterpret_cast<const uint4*>(sm + L_WQ + (18 + t * 6 + ks) * 1024 + lane * 16);
+#pragma unroll
+          for (int v = 0; v < NWIN; ++v) mma_step<bf16_t>(ak[v][t], f, X[v]);
+        }
+      }
+      float4 bq4[3], bk4[2];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) bq4[t] = *reinterpret_cast<const float4*>(bqs + 16 * t + 4 * qq);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) bk4[t] = *reinterpret_cast<const float4*>(bqs + 48 + 16 * t + 4 * qq);
+#pragma unroll
+      for (int v = 0; v < NWIN; ++v) {
+        uint2 q2[3], k2[2];
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+          q2[t] = make_uint2(pack_bf16x2((aq[v][t][0] + bq4[t].x) * qscale, (aq[v][t][1] + bq4[t].y) * qscale),
+                             pack_bf16x2((aq[v][t][2] + bq4[t].z) * qscale, (aq[v][t][3] + bq4[t].w) * qscale));
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          k2[t] = make_uint2(pack_bf16x2(ak[v][t][0] + bk4[t].x, ak[v][t][1] + bk4[t].y),
+                             pack_bf16x2(ak[v][t][2] + bk4[t].z, ak[v][t][3] + bk4[t].w));
+        // head 2p: channels 0..23 = tile 0 + rows 0..7 of tile 1; head 2p+1: rows 8..15 of
+        // tile 1 + tile 2.  Zeroing the other head's rows in q alone cuts them from q . k.
+        *reinterpret_cast<uint4*>(sm + L_Q + (v * 8 + tt) * 1024 + lane * 16) =
+            make_uint4(q2[0].x, q2[0].y, q2[1].x & qlo, q2[1].y & qlo);
+        *reinterpret_cast<uint4*>(sm + L_Q + (v * 8 + 4 + tt) * 1024 + lane * 16) =
+            make_uint4(q2[1].x & ~qlo, q2[1].y & ~qlo, q2[2].x, q2[2].y);
+        *reinterpret_cast<uint4*>(sm + L_K + ((v * 2 + 0) * 4 + tt) * 1024 + lane * 16) = cat2(k2[0], k2[1]);
+        *reinterpret_cast<uint2*>(sm + L_K + ((v * 2 + 1) * 4 + tt) * 1024 + lane * 16) = k2[1];
+      }
+    } else {
+      f32x4 ak2[NWIN], av[NWIN][3];
+#pragma unroll
+      for (int v = 0; v < NWIN; ++v) {
+        ak2[v] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < 3; ++t) av[v][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int ks = 0; ks < 6; ++ks) {
+        uint4 X[NWIN];
+#pragma unroll
+        for (int v = 0; v < NWIN; ++v)
+          X[v] = *reinterpret_cast<const uint4*>(sm + L_X + ((v * 4 + tt) * 6 + ks) * 1024 + lane * 16);
+        {
+          const uint4 f = *reinterpret_cast<const uint4*>(sm + L_WQ + (30 + ks) * 1024 + lane * 16);
+#pragma unroll
+          for (int v = 0; v < NWIN; ++v) mma_step<bf16_t>(ak2[v], f, X[v]);
+        }
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+          const uint4 f = *reinterpret_cast<const uint4*>(sm + L_WQ + (36 + t * 6 + ks) * 1024 + lane * 16);
+#pragma unroll
+          for (int v = 0; v < NWIN; ++v) mma_step<bf16_t>(av[v][t], X[v], f);
+        }
+      }
+      const float4 bk4 = *reinterpret_cast<const float4*>(bqs + 48 + 32 + 4 * qq);
+      float bv[3];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) bv[t] = bqs[96 + 16 * t + n];
+#pragma unroll
+      for (int v = 0; v < NWIN; ++v) {
+        *reinterpret_cast<uint2*>(sm + L_K + ((v * 2 + 1) * 4 + tt) * 1024 + lane * 16 + 8) =
+            make_uint2(pack_bf16x2(ak2[v][0] + bk4.x, ak2[v][1] + bk4.y),
+                       pack_bf16x2(ak2[v][2] + bk4.z, ak2[v][3] + bk4.w));
+        // V^T (channels x keys): this token tile is one half of key pair tt >> 1
+#pragma unroll
+        for (int t = 0; t < 3; ++t)
+          *reinterpret_cast<uint2*>(sm + L_V + ((v * 3 + t) * 2 + (tt >> 1)) * 1024 + lane * 16 + 8 * (tt & 1)) =
+              make_uint2(pack_bf16x2(av[v][t][0] + bv[t], av[v][t][1] + bv[t]),
+                         pack_bf16x2(av[v][t][2] + bv[t], av[v][t][3] + bv[t]));
+      }
+    }
+  };
+
+  // attention of head 2p + hr, query tile tt, window slot v (global window wg): O^T to the
+  // window's slot of the workspace (channel tile 3p + c is half (3p + c) & 1 of the proj's
+  // k-step (3p + c) >> 1)
+  auto attend = [&](int v, int wg) {
+    const uint4 qf = *reinterpret_cast<const uint4*>(sm + L_Q + (v * 8 + hr * 4 + tt) * 1024 + lane * 16);
+    const unsigned cutm = make_cut(wg);
+    f32x4 s[4];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt) {
+      const uint4 kf = *reinterpret_cast<const uint4*>(sm + L_K + ((v * 2 + hr) * 4 + kt) * 1024 + lane * 16);
+      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      mma_step<bf16_t>(s[kt], kf, qf);
+    }
+    // + B_rel + shift mask, softmax over the 64 keys (lane + lanes ^16, ^32, ^48)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int off = tbase + 4 * (30 * (3 - kt) + 3 - r) + (((cutm >> (4 * kt + r)) & 1u) ? 1800 : 0);
+        const float val = s[kt][r] + *reinterpret_cast<const float*>(sm + off);
+        s[kt][r] = val;
+        mx = fmaxf(mx, val);
+      }
+    mx = pair16_max(mx);
+    mx = pair32_max(mx);
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float ex = __builtin_amdgcn_exp2f(s[kt][r] - mx);
+        s[kt][r] = ex;
+        sum += ex;
+      }
+    sum = pair16_sum(sum);
+    sum = pair32_sum(sum);
+    const float inv = __builtin_amdgcn_rcpf(sum);
+    uint4 pf[2];                                       // P^T key pairs (0,1), (2,3)
+#pragma unroll
+    for (int kp = 0; kp < 2; ++kp) {
+      f32x4 a0 = s[2 * kp], a1 = s[2 * kp + 1];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { a0[r] *= inv; a1[r] *= inv; }
+      pf[kp] = cat2(pk4(a0), pk4(a1));
+    }
+    uint2* dst = reinterpret_cast<uint2*>(a.oscr + (size_t)wg * OSLOT);
+#pragma unroll
+    for (int ci = 0; ci < 2; ++ci) {
+      const int c = hr + ci;
+      f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kp = 0; kp < 2; ++kp) {
+        uint4 vf = *reinterpret_cast<const uint4*>(sm + L_V + ((v * 3 + c) * 2 + kp) * 1024 + lane * 16);
+        if (c == 1) {
+          const uint32_t keep = hr == 0 ? lo8 : ~lo8;
+          vf.x &= keep; vf.y &= keep; vf.z &= keep; vf.w &= keep;
+        }
+        mma_step<bf16_t>(o, vf, pf[kp]);
+      }
+      const int ct = 3 * p + c;
+      if (c != 1 || (hr == 0 ? qq < 2 : qq >= 2))
+        dst[((tt * 6 + (ct >> 1)) * 64 + lane) * 2 + (ct & 1)] = pk4(o);
+    }
+  };
+
+  for (int i = 0; i < npair; ++i) {
+    const bool two = 2 * i + 1 < nmine;               // wave-uniform
+    const int wa = a.w0 + la[2 * i], wb = two ? a.w0 + la[2 * i + 1] : wa;
+    if (two) gemm(std::integral_constant<int, 2>{});
+    else gemm(std::integral_constant<int, 1>{});
+    WB_T(3 + 4 * (i < 2 ? i : 2));
+    __syncthreads();                                   // K / V^T / q^T visible; x free
+    WB_T(4 + 4 * (i < 2 ? i : 2));
+    if (i + 1 < npair) {
+      const int nb = 2 * i + 3 < nmine ? 2 * i + 3 : 2 * i + 2;
+      dma_x(a.w0 + la[2 * i + 2], a.w0 + la[nb]);
+    }
+    attend(0, wa);
+    if (two) attend(1, wb);
+    WB_T(5 + 4 * (i < 2 ? i : 2));
+    wb_wait_all();                                     // the next windows' x landed
+    __syncthreads();                                   // exchange free; x visible
+    WB_T(6 + 4 * (i < 2 ? i : 2));
+  }
+  WB_T(15);
+
+  // ---- inactive windows: out = x (MASKSEL, :236-240), 64 tokens x 24 chunks of 16 bytes
+  for (int c = 0; c < ncopy; ++c) {
+    const int wg = a.w0 + lc[c];
+    const int e0 = tid, e1 = tid + 512, e2 = tid + 1024;
+    const int t0 = e0 / 24, t1 = e1 / 24, t2 = e2 / 24;
+    const long long p0 = wb_win_pix(wg, t0, H, W, nwx, nwimg, shift);
+    const long long p1 = wb_win_pix(wg, t1, H, W, nwx, nwimg, shift);
+    const long long p2 = wb_win_pix(wg, t2, H, W, nwx, nwimg, shift);
+    const int c0 = 8 * (e0 - 24 * t0), c1 = 8 * (e1 - 24 * t1), c2 = 8 * (e2 - 24 * t2);
+    const uint4 v0 = *reinterpret_cast<const uint4*>(a.x + p0 * a.ldx + c0);
+    const uint4 v1 = *reinterpret_cast<const uint4*>(a.x + p1 * a.ldx + c1);
+    const uint4 v2 = *reinterpret_cast<const uint4*>(a.x + p2 * a.ldx + c2);
+    *reinterpret_cast<uint4*>(a.out + p0 * a.ldo + c0) = v0;
+    *reinterpret_cast<uint4*>(a.out + p1 * a.ldo + c1) = v1;
+    *reinterpret_cast<uint4*>(a.out + p2 * a.ldo + c2) = v2;
+  }
+  wb_wait_all();                                       // no LDS-DMA in flight at exit
+  WB_T(17);
+}
+
+// out = x + Wp O^T + b over the launch's active windows (winblock_kernel's compacted list),
+// the proj panel resident; 8 waves: token tiles 2tp, 2tp + 1 (tp = w & 1) x output channel
+// tiles 3mg .. 3mg + 2 (mg = w >> 1), 36 MFMAs each, k-steps in winblock_v2_kernel's order
+__global__ void __launch_bounds__(512, 1) winproj_kernel(const WinBlock3Args a) {
+  using namespace wb3;
+  extern __shared__ __attribute__((aligned(16))) unsigned char sm[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n = lane & 15, qq = lane >> 4;
+  const int H = a.H, W = a.W, shift = a.shift;
+  const int nwx = W >> 3, nwimg = nwx * (H >> 3);
+  const uint32_t lds0 = (uint32_t)(size_t)(__attribute__((address_space(3))) void*)sm;
+  const int tp = w & 1, mg = w >> 1;
+  const int nact = a.acount[a.chunk];
+  const int G = gridDim.x;
+  // O^T of window wg into buffer b: 24 pieces [tt][ks], 3 per wave
+  auto dma_o = [&](int wg, int b) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int k = w + 8 * i;
+      wb_dma16(a.oscr + (size_t)wg * OSLOT + (size_t)(k * 64 + lane) * 2, lds0 + P_O + (b * 24 + k) * 1024);
+    }
+  };
+  uint2 xr[2][3];
+  auto load_res = [&](int wg) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bf16_t* xrow = a.x + (long long)wb_win_pix(wg, 16 * (2 * tp + u) + n, H, W, nwx, nwimg, shift) * a.ldx;
+#pragma unroll
+      for (int mi = 0; mi < 3; ++mi)
+        xr[u][mi] = *reinterpret_cast<const uint2*>(xrow + 16 * (3 * mg + mi) + 4 * qq);
+    }
+  };
+  int r = blockIdx.x;
+  int wg = r < nact ? a.alist[a.w0 + r] : 0;
+  if (r < nact) dma_o(wg, 0);
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const int f = w + 8 * i;
+    wb_dma16(a.wp + ((size_t)f * 64 + lane) * 8, lds0 + P_WP + f * 1024);
+  }
+  wb_dma16(a.bias + lane * 4, lds0 + P_BP);
+  if (r < nact) load_res(wg);
+  wb_wait_all();
+  __syncthreads();
+  const float* bp = reinterpret_cast<const float*>(sm + P_BP);
+  for (int it = 0; r < nact; ++it, r += G) {
+    const int b = it & 1;
+    const int rn = r + G;
+    const int wgn = rn < nact ? a.alist[a.w0 + rn] : 0;
+    if (rn < nact) dma_o(wgn, b ^ 1);                 // the next window's O^T, in flight
+    f32x4 acc[2][3];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int mi = 0; mi < 3; ++mi) acc[u][mi] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 6; ++ks) {
+      uint4 ob[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        ob[u] = *reinterpret_cast<const uint4*>(sm + P_O + (b * 24 + (2 * tp + u) * 6 + ks) * 1024 + lane * 16);
+#pragma unroll
+      for (int mi = 0; mi < 3; ++mi) {
+        const int f = ((ks / 3) * 12 + 3 * mg + mi) * 3 + ks % 3;
+        const uint4 wf = *reinterpret_cast<const uint4*>(sm + P_WP + f * 1024 + lane * 16);
+#pragma unroll
+        for (int u = 0; u < 2; ++u) mma_step<bf16_t>(acc[u][mi], wf, ob[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      bf16_t* orow = a.out + (long long)wb_win_pix(wg, 16 * (2 * tp + u) + n, H, W, nwx, nwimg, shift) * a.ldo;
+#pragma unroll
+      for (int mi = 0; mi < 3; ++mi) {
+        const int c0 = 16 * (3 * mg + mi) + 4 * qq;
+        const uint2 xv = xr[u][mi];
+        float v[4] = {bf2f(xv.x & 0xFFFF), bf2f(xv.x >> 16), bf2f(xv.y & 0xFFFF), bf2f(xv.y >> 16)};
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr) v[rr] += acc[u][mi][rr] + bp[c0 + rr];
+        *reinterpret_cast<uint2*>(orow + c0) = make_uint2(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]));
+      }
+    }
+    if (rn < nact) load_res(wgn);
+    wg = wgn;
+    wb_wait_all();                                     // next O^T and x landed, stores drained
+    __syncthreads();                                   // buffer b free, b ^ 1 visible
+  }
+}
+
+// ---------------------------------------------------------------------------------------
 // The same block at ws 4, C 80, 8 heads of 10 (the 1/16-resolution attention blocks,
 // TransformRGB.py:63,80): a window is 16 tokens = ONE 16-token tile, so each wave owns a
 // whole window and nothing crosses waves.  q^T, k^T (channels x tokens) and v (tokens x
@@ -668,7 +1218,7 @@ extern "C" int rgbac_debug_wb_times(unsigned long long* host, int nblocks) {
 }
 #endif
 
-extern "C" int rgbac_winattn_block(int batch, int h, int w, int shift, int masked, float scale,
+extern "C" int rgbac_winattn_block_v2(int batch, int h, int w, int shift, int masked, float scale,
                                    const void* x, int64_t ldx, const float* alpha,
                                    const void* wq_packed, const float* bqkv,
                                    const void* wp_packed, const float* bproj, const float* table,
@@ -691,13 +1241,100 @@ extern "C" int rgbac_winattn_block(int batch, int h, int w, int shift, int maske
   d.out = reinterpret_cast<bf16_t*>(out); d.ldo = ldo;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(winblock_kernel),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(winblock_v2_kernel),
                         hipFuncAttributeMaxDynamicSharedMemorySize, wb::LDS);
     attr = true;
   }
   const dim3 grid((int)((windows + 1) / 2));
-  hipLaunchKernelGGL(winblock_kernel, grid, dim3(512), wb::LDS, reinterpret_cast<hipStream_t>(stream), d);
-  return check_launch("winblock_kernel");
+  hipLaunchKernelGGL(winblock_v2_kernel, grid, dim3(512), wb::LDS, reinterpret_cast<hipStream_t>(stream), d);
+  return check_launch("winblock_v2_kernel");
+}
+
+namespace {
+struct Wb3Layout {
+  long long flags, alist, acount, oscr, total;
+};
+Wb3Layout wb3_layout(long long nwin) {
+  auto up = [](long long v, long long m) { return (v + m - 1) / m * m; };
+  Wb3Layout l;
+  l.flags = 0;
+  l.alist = up(nwin, wb3::CHUNK);
+  l.acount = l.alist + up(nwin * 4, 256);
+  l.oscr = l.acount + up((nwin + wb3::CHUNK - 1) / wb3::CHUNK * 4, 256);
+  l.total = l.oscr + nwin * (long long)wb3::OSLOT * 8;
+  return l;
+}
+}  // namespace
+
+extern "C" int64_t rgbac_winattn_block_workspace(int batch, int h, int w) {
+  if (batch <= 0 || h <= 0 || w <= 0 || h % 8 || w % 8) return -1;
+  return wb3_layout((long long)batch * (h / 8) * (w / 8)).total;
+}
+
+extern "C" int rgbac_winattn_block(int batch, int h, int w, int shift, int masked, float scale,
+                                   const void* x, int64_t ldx, const float* alpha,
+                                   const void* wq_packed, const float* bias_pack,
+                                   const void* wp_packed, const float* table_pad, void* out,
+                                   int64_t ldo, void* work, int64_t work_bytes, void* stream) {
+  RGBAC_REQUIRE(batch > 0 && h > 0 && w > 0 && h % 8 == 0 && w % 8 == 0,
+                "H and W must be positive multiples of the window size 8");
+  RGBAC_REQUIRE(shift >= 0 && shift < 8, "0 <= shift < 8");
+  RGBAC_REQUIRE(x && out && wq_packed && bias_pack && wp_packed && table_pad && work, "null pointer");
+  RGBAC_REQUIRE(!masked || alpha, "masked attention needs alpha");
+  RGBAC_REQUIRE(ldx >= 192 && ldo >= 192 && ldx % 8 == 0 && ldo % 8 == 0, "strides");
+  RGBAC_REQUIRE(((uintptr_t)x % 16) == 0 && ((uintptr_t)out % 16) == 0 &&
+                    ((uintptr_t)wq_packed % 16) == 0 && ((uintptr_t)wp_packed % 16) == 0 &&
+                    ((uintptr_t)bias_pack % 16) == 0 && ((uintptr_t)table_pad % 16) == 0 &&
+                    ((uintptr_t)work % 256) == 0,
+                "16-byte aligned operands, 256-byte aligned workspace");
+  RGBAC_REQUIRE(x != out, "out must not alias x");
+  const long long nwin = (long long)batch * (h / 8) * (w / 8);
+  RGBAC_REQUIRE((long long)batch * h * w < (1LL << 31), "pixel index must fit in 31 bits");
+  const Wb3Layout lay = wb3_layout(nwin);
+  RGBAC_REQUIRE(work_bytes >= lay.total, "workspace smaller than rgbac_winattn_block_workspace()");
+  unsigned char* wk = static_cast<unsigned char*>(work);
+  WinBlock3Args d;
+  d.batch = batch; d.H = h; d.W = w; d.shift = shift; d.masked = masked; d.scale = scale;
+  d.x = reinterpret_cast<const bf16_t*>(x); d.ldx = ldx; d.alpha = alpha;
+  d.flags = wk + lay.flags;
+  d.wq = reinterpret_cast<const bf16_t*>(wq_packed); d.bias = bias_pack;
+  d.wp = reinterpret_cast<const bf16_t*>(wp_packed); d.table = table_pad;
+  d.out = reinterpret_cast<bf16_t*>(out); d.ldo = ldo;
+  d.oscr = reinterpret_cast<unsigned long long*>(wk + lay.oscr);
+  d.alist = reinterpret_cast<int*>(wk + lay.alist);
+  d.acount = reinterpret_cast<int*>(wk + lay.acount);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (masked) {
+    const long long blocks = (nwin + 3) / 4;
+    RGBAC_REQUIRE(blocks < (1LL << 31), "too many windows");
+    hipLaunchKernelGGL(winflag_kernel, dim3((unsigned)blocks), dim3(256), 0, st, d);
+    const int rc = check_launch("winflag_kernel");
+    if (rc) return rc;
+  }
+  static unsigned long long attr_a = 0, attr_b = 0;
+  lds_optin(reinterpret_cast<const void*>(winblock_kernel), wb3::LDS_A, &attr_a);
+  lds_optin(reinterpret_cast<const void*>(winproj_kernel), wb3::LDS_B, &attr_b);
+  // slots per head pair: a quarter of the CUs (one workgroup per CU), a multiple of 8 so a
+  // slot's four pair workgroups share blockIdx & 7
+  const int ncu = device_cus();
+  int slots = (ncu / 4) & ~7;
+  if (slots < 8) slots = 8;
+  int chunk = 0;
+  for (long long w0 = 0; w0 < nwin; w0 += wb3::CHUNK, ++chunk) {
+    const int nwc = (int)std::min<long long>(wb3::CHUNK, nwin - w0);
+    const int s = std::min(slots, (nwc + 7) / 8 * 8);
+    // list capacities: ceil(nwc / s) active and ceil(nwc / 4s) inactive windows per workgroup
+    RGBAC_REQUIRE((nwc + s - 1) / s <= wb3::MAXA && (nwc + 4 * s - 1) / (4 * s) <= wb3::MAXC,
+                  "window lists exceed the workgroup's capacity");
+    d.w0 = (int)w0; d.nwc = nwc; d.slots = s; d.chunk = chunk;
+    hipLaunchKernelGGL(winblock_kernel, dim3(4 * s), dim3(512), wb3::LDS_A, st, d);
+    int rc = check_launch("winblock_kernel");
+    if (rc) return rc;
+    hipLaunchKernelGGL(winproj_kernel, dim3(std::min(ncu, nwc)), dim3(512), wb3::LDS_B, st, d);
+    rc = check_launch("winproj_kernel");
+    if (rc) return rc;
+  }
+  return RGBAC_OK;
 }
 
 extern "C" int rgbac_winattn_block_ws4(int batch, int h, int w, int shift, int masked, float scale,

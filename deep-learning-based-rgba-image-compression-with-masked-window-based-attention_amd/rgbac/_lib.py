@@ -17,7 +17,6 @@ F32, BF16 = 0, 1
 ACT = dict(none=0, gelu=1, relu=2, lrelu=3, tanh_half=4, gate=5, gdn=6, igdn=7, masksel=8,
            gauss=9, sqbwd=10, dgelu=11, dlrelu=12)
 CONV, CONVT_S2, SUBPEL2 = 0, 1, 2
-FOLD_GAUSS, FOLD_TANH = 1, 2
 
 
 class Src(ctypes.Structure):
@@ -47,32 +46,6 @@ class ConvArgs(ctypes.Structure):
         ("aux0", ctypes.c_void_p), ("aux1", ctypes.c_void_p), ("partial", ctypes.c_void_p),
         ("zout", ctypes.c_void_p), ("zout_ldc", ctypes.c_int64),
         ("tile_counters", ctypes.c_void_p),
-    ]
-
-
-class FoldGroup(ctypes.Structure):
-    """rgbac_fold_group"""
-    _fields_ = [
-        ("src", Src * 2), ("c0", ctypes.c_int32), ("cout", ctypes.c_int32),
-        ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p),
-        ("out", ctypes.c_void_p), ("out_ldc", ctypes.c_int64),
-        ("out_coff", ctypes.c_int32), ("writer", ctypes.c_int32),
-        ("pin", ctypes.c_void_p), ("pin_ldc", ctypes.c_int64),
-        ("pweight", ctypes.c_void_p), ("pbias", ctypes.c_void_p),
-        ("aux", ctypes.c_void_p), ("aux_ldc", ctypes.c_int64),
-        ("mu", ctypes.c_void_p), ("mu_ldc", ctypes.c_int64),
-        ("put", ctypes.c_void_p), ("put_ldc", ctypes.c_int64),
-    ]
-
-
-class BitsGroup(ctypes.Structure):
-    """rgbac_bits_group"""
-    _fields_ = [
-        ("pin", ctypes.c_void_p), ("pin_ldc", ctypes.c_int64),
-        ("pweight", ctypes.c_void_p), ("pbias", ctypes.c_void_p),
-        ("y", ctypes.c_void_p), ("y_ldc", ctypes.c_int64),
-        ("mu", ctypes.c_void_p), ("mu_ldc", ctypes.c_int64),
-        ("partial", ctypes.c_void_p),
     ]
 
 
@@ -123,8 +96,6 @@ SIGNATURES = {
     "rgbac_conv2d_grouped": [ctypes.c_void_p, _I32, _VP],
     "rgbac_conv2d_grouped_part": [ctypes.c_void_p, _I32, _I32, _VP],
     "rgbac_conv_max_groups": [],
-    "rgbac_conv_fold": [_VP, _I32, _I32, _I32, _I32, _I32, _I32, _VP],
-    "rgbac_gauss_bits": [_VP, _I32, _I32, _I32, _I32, _VP],
     "rgbac_timer_create": [ctypes.POINTER(ctypes.c_void_p)],
     "rgbac_timer_record": [_VP, _VP],
     "rgbac_timer_elapsed_ms": [_VP, _VP, ctypes.POINTER(ctypes.c_float)],
@@ -150,7 +121,12 @@ SIGNATURES = {
     "rgbac_stem_gdn": [_I32, _I32, _I32, _VP, _I64, _VP, _I32, _VP, _VP, _I32, _VP, _I32, _VP,
                        _I64, _VP],
     "rgbac_winattn_block": [_I32, _I32, _I32, _I32, _I32, _F, _VP, _I64, _VP, _VP, _VP, _VP, _VP,
-                            _VP, _VP, _I64, _VP],
+                            _VP, _I64, _VP, _I64, _VP],
+    "rgbac_winattn_block_workspace": [_I32, _I32, _I32],
+    "rgbac_gdn_reparam": [_I32, _I32, _VP, _VP, _F, _F, _F, _VP, _VP, _VP],
+    "rgbac_gdn_reparam_bwd": [_I32, _I32, _VP, _VP, _F, _F, _VP, _VP, _VP, _VP, _I32, _VP],
+    "rgbac_winattn_block_v2": [_I32, _I32, _I32, _I32, _I32, _F, _VP, _I64, _VP, _VP, _VP, _VP, _VP,
+                               _VP, _VP, _I64, _VP],
     "rgbac_winattn_block_ws4": [_I32, _I32, _I32, _I32, _I32, _F, _VP, _I64, _VP, _VP, _VP, _VP,
                                 _VP, _VP, _VP, _I64, _VP],
     "rgbac_rgba_augment": [_I32, _VP, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP],
@@ -216,7 +192,8 @@ SIGNATURES = {
     "rgbac_rans_decode": [ctypes.POINTER(RansDecoderState), _VP, _I64, _VP, _I32, _VP, _VP, _I32,
                           _VP],
 }
-_RESTYPE = {"rgbac_last_error": ctypes.c_char_p, "rgbac_rans_encoder_bound": ctypes.c_int64}
+_RESTYPE = {"rgbac_last_error": ctypes.c_char_p, "rgbac_rans_encoder_bound": ctypes.c_int64,
+            "rgbac_winattn_block_workspace": ctypes.c_int64}
 
 _lib = None
 

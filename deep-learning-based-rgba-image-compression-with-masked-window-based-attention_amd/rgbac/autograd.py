@@ -391,42 +391,8 @@ _PENDING = []                   # (task int64 x 11, keep-alive tensors)
 _PENDING_CB = [False]
 
 
-# Weight-gradient reductions that add into param.grad on a SIDE stream (RGBAC_SIDE_REDUCE=1):
-# the slab reads of layer L's reduction then run beside layer L-1's input-gradient convs, which
-# are the backward's critical path.  The side stream forks from the stream the backward node
-# runs on; that stream waits for the side stream again (the join) before anything reads the
-# gradients: in rgbac.parallel's bucket hooks (flush_reductions) and at the end of the backward
-# pass (an engine callback).  The slabs stay referenced until the join.
-# RGBAC_SIDE_REDUCE=2 also moves the weight-gradient kernel itself there (it reads the output
-# gradient and the saved inputs, which then stay referenced until the join as well).
-SIDE_REDUCE = os.environ.get("RGBAC_SIDE_REDUCE", "0") in ("1", "2")
-SIDE_WGRAD = os.environ.get("RGBAC_SIDE_REDUCE", "0") == "2"
-_SIDE = {}                      # device -> side stream
-_SIDE_MAIN = {}                 # device -> the stream the side stream forked from
-_SIDE_KEEP = []
-_SIDE_READS = set()             # storages the side stream's pending weight-gradient kernels read
-
-
-def join_side():
-    """Make each forking stream wait for its side stream's reductions; release their slabs."""
-    for dev, main in list(_SIDE_MAIN.items()):
-        main.wait_stream(_SIDE[dev])
-    _SIDE_MAIN.clear()
-    _SIDE_KEEP.clear()
-    _SIDE_READS.clear()
-
-
-def _side_guard(t):
-    """Before ``t`` is written in place (a gradient sink accumulating): join the side stream if
-    a pending weight-gradient kernel there reads t's storage -- e.g. a residual unit's output
-    gradient, adopted by the unit input's sink and later accumulated into in place."""
-    if _SIDE_READS and t is not None and t.untyped_storage().data_ptr() in _SIDE_READS:
-        join_side()
-
-
 def flush_reductions():
     """Issue every queued weight-gradient reduction (one launch per 8)."""
-    join_side()
     while _PENDING:
         part = _PENDING[:8]
         del _PENDING[:8]
@@ -443,42 +409,10 @@ def _end_of_backward():
     flush_reductions()
 
 
-def _fork_side(dev, keep):
-    """The side stream of ``dev``, made to wait for the current stream; ``keep`` stays
-    referenced until the join."""
-    main = torch.cuda.current_stream(dev)
-    side = _SIDE.get(dev)
-    if side is None:
-        side = _SIDE[dev] = torch.cuda.Stream(device=dev)
-    prev = _SIDE_MAIN.get(dev)
-    if prev is not None and prev != main:
-        join_side()                # a different forking stream: join the first one's work
-    _SIDE_MAIN[dev] = main
-    side.wait_stream(main)
-    _SIDE_KEEP.extend(keep)
-    if not _PENDING_CB[0]:
-        torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
-        _PENDING_CB[0] = True
-    return side
-
-
-def _side_reduce(args, keep):
-    side = _fork_side(keep[0].device, keep)
-    _lib.call("rgbac_wgrad_reduce", *args, side.cuda_stream)
-
-
 def _reduce(nslot, fmap, part, nsplit, slab, dw, nbias, bpart, n_pad, db, acc, st):
     # queued reductions are flushed by a callback of the running backward pass: outside one
     # (a weight gradient computed directly, e.g. a test or a custom loop) there is no engine
     # to run the callback, so the reduction goes out immediately
-    if SIDE_REDUCE and acc and torch._C._current_graph_task_id() >= 0:
-        _side_reduce((nslot, None if fmap is None else fmap.data_ptr(),
-                      None if part is None else part.data_ptr(), nsplit, slab,
-                      None if dw is None else dw.data_ptr(), nbias,
-                      None if bpart is None else bpart.data_ptr(), n_pad,
-                      None if db is None else db.data_ptr(), 1),
-                     [t for t in (part, bpart, fmap, dw, db) if t is not None])
-        return
     if not (REDUCE_BATCH and acc) or torch._C._current_graph_task_id() < 0:
         flush_reductions()
         _lib.call("rgbac_wgrad_reduce", nslot, None if fmap is None else fmap.data_ptr(),
@@ -546,11 +480,6 @@ def wgrad(G, S, ksize, stride, pad, square, k_pad, fmap, numel, nbias=0, bias_fr
     a.partial = part.data_ptr()
     a.bias_partial = None if bpart is None else bpart.data_ptr()
     st = _stream(G.t)
-    if (SIDE_WGRAD and acc_dw is not None and rt.PROFILER is None and
-            torch._C._current_graph_task_id() >= 0):
-        st = _fork_side(dev, [G.t, part] + [f.t for f in S] +
-                        ([] if bpart is None else [bpart])).cuda_stream
-        _SIDE_READS.update(t.untyped_storage().data_ptr() for t in [G.t] + [f.t for f in S])
     # the launched form's rocprof name (the C side's choice, restated), so the bench's
     # per-kernel table and training roofline keep the forms apart
     if hs:
@@ -666,6 +595,45 @@ def _direct_grad(p):
     return g
 
 
+class GdnReparamFn(torch.autograd.Function):
+    """GDN / IGDN beta' = LowerBound(beta, beta_bound)^2 - pedestal and gamma' likewise
+    (layers/GDN.py:9-23, 71-78) as one HIP launch forward (rgbac_gdn_reparam) and one
+    backward (rgbac_gdn_reparam_bwd, LowerBound's pass-through rule), bit-identical to the
+    torch graph of the reference's LowerBound Function, ``** 2`` and ``- pedestal``.  With an
+    attached fp32 .grad (AdamClamp) the backward adds into it and hands autograd None (as the
+    conv weight gradients do, DIRECT_GRAD)."""
+
+    @staticmethod
+    def forward(ctx, beta, gamma, beta_bound, gamma_bound, pedestal):
+        b, g = beta.detach(), gamma.detach()
+        assert b.dtype == _F32 and g.dtype == _F32 and b.is_contiguous() and g.is_contiguous()
+        bo, go = torch.empty_like(b), torch.empty_like(g)
+        _lib.call("rgbac_gdn_reparam", b.numel(), g.numel(), b.data_ptr(), g.data_ptr(),
+                  float(beta_bound), float(gamma_bound), float(pedestal), bo.data_ptr(),
+                  go.data_ptr(), _lib.stream_ptr(b.device))
+        ctx.save_for_backward(beta, gamma)
+        ctx.bounds = (float(beta_bound), float(gamma_bound))
+        return bo, go
+
+    @staticmethod
+    def backward(ctx, dbo, dgo):
+        beta, gamma = ctx.saved_tensors
+        need_b, need_g = ctx.needs_input_grad[0], ctx.needs_input_grad[1]
+        acc_b = _direct_grad(beta) if need_b else None
+        acc_g = _direct_grad(gamma) if need_g else None
+        direct = acc_b is not None and acc_g is not None
+        db = acc_b if direct else torch.empty_like(beta)
+        dg = acc_g if direct else torch.empty_like(gamma)
+        dbo = None if dbo is None else dbo.contiguous()
+        dgo = None if dgo is None else dgo.contiguous()
+        _lib.call("rgbac_gdn_reparam_bwd", beta.numel(), gamma.numel(), beta.data_ptr(),
+                  gamma.data_ptr(), ctx.bounds[0], ctx.bounds[1], _lib.ptr(dbo), _lib.ptr(dgo),
+                  db.data_ptr(), dg.data_ptr(), 1 if direct else 0, _lib.stream_ptr(beta.device))
+        if direct:
+            return None, None, None, None, None
+        return (db if need_b else None), (dg if need_g else None), None, None, None
+
+
 class Sink:
     """Gradient buffer of one autograd-tracked training activation (a ConvFn / CatFn output).
     Consumers that know the protocol (ConvFn sources and residual operands, CatFn parts) add
@@ -697,7 +665,6 @@ def _deposit(sink, g, own):
     if sink.buf is None:
         sink.buf, sink.own = g, own
     elif sink.own:
-        _side_guard(sink.buf)
         sink.buf.add_(g)
     else:
         sink.buf, sink.own = sink.buf + g, True
@@ -840,8 +807,6 @@ class ConvFn(Function):
                 targeted.add(id(sk))
                 prev = Feat(sk.buf, f.C)
                 inplace = sk.own and all(sk.buf is not t for t in (G.t, dz.t, dy.t))
-                if inplace:
-                    _side_guard(sk.buf)
                 o = prev if inplace else new_feat(f.B, f.H, f.W, f.C, dt, f.t.device)
                 preps.append(rt.prepare(pk, [G.src()], out=o, res0=prev, bias=False))
                 sk.buf, sk.own, sk.slices = o.t, True, False
@@ -1109,7 +1074,6 @@ class CatFn(Function):
                 # add this part's slice into the producer's gradient buffer
                 if not sk.own:
                     sk.buf, sk.own = sk.buf.clone(), True
-                _side_guard(sk.buf)
                 sk.slices = False
                 pairs.append((Feat(sk.buf, c), 0, g, off, c))
                 accs.append(True)
@@ -1256,8 +1220,6 @@ class GaussFn(Function):
         direct = ysink is not None and (ysink.buf is None or (ysink.slices and ysink.own))
         if direct and ysink.buf is None:
             ysink.buf, ysink.own, ysink.slices = torch.zeros_like(y_t), True, True
-        if direct:
-            _side_guard(ysink.buf)
         dy = Feat(ysink.buf if direct else torch.zeros_like(y_t), Cy)
         dmu = Feat(torch.zeros_like(mu_t), cs)
         dsc = Feat(torch.zeros_like(sc_t), cs)

@@ -49,7 +49,13 @@ class GDN(nn.Module):
         self.gamma = nn.Parameter(torch.sqrt(g))
 
     def effective_params(self):
-        """Reparametrised (beta', gamma') exactly as GDN.py:71-78 computes them (fp32)."""
+        """Reparametrised (beta', gamma') exactly as GDN.py:71-78 computes them (fp32): on the
+        GPU one HIP launch each way (rgbac.autograd.GdnReparamFn, bit-identical to the torch
+        graph below, which CPU tensors keep)."""
+        if self.beta.is_cuda and self.gamma.is_cuda:
+            from ..autograd import GdnReparamFn
+            return GdnReparamFn.apply(self.beta, self.gamma, self.beta_bound, self.gamma_bound,
+                                      self.pedestal)
         beta = LowerBound.apply(self.beta, self.beta_bound) ** 2 - self.pedestal
         gamma = LowerBound.apply(self.gamma, self.gamma_bound) ** 2 - self.pedestal
         return beta, gamma

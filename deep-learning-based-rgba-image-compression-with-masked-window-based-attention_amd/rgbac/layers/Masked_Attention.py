@@ -160,8 +160,7 @@ def run_bottlenecks_fused(units, kind):
     npix = x0.B * x0.H * x0.W
     flops = 2.0 * npix * len(units) * (C * C // 2 * 2 + 9 * (C // 2) ** 2)
     # the launched template's rocprof name (csrc/fused.hip rgbac_residual_unit_ex's choice,
-    # restated): C 80 takes two tiles per workgroup on multi-round launches, C 192 the 16-row
-    # tile under RGBAC_RU_TILE16=1
+    # restated): C 80 takes two tiles per workgroup on multi-round launches
     if C == 80:
         tiles = x0.B * (x0.H // 8) * (x0.W // 8)
         ncu = torch.cuda.get_device_properties(x0.t.device).multi_processor_count
@@ -169,8 +168,7 @@ def run_bottlenecks_fused(units, kind):
         dual = (tiles > max(1, ncu // len(units)) and dual_env != "0") or dual_env == "2"
         kname = f"ru_small_kernel<{kind}, {2 if dual else 1}>"
     elif stream:
-        t16 = os.environ.get("RGBAC_RU_TILE16", "") == "1" and x0.H % 16 == 0
-        kname = f"ru_stream_kernel<{kind}, {16 if t16 else 8}>"
+        kname = f"ru_stream_kernel<{kind}, 8>"
     else:
         kname = f"ru_fused_kernel<{C}, {C // 2}>"
     rt.timed(kname, flops, 2 * npix * len(units) * 2 * C,

@@ -127,7 +127,9 @@ class WindowAttention(nn.Module):
         2p, 2p+1: 3 x 3 16-row tiles x 6 32-deep k-steps), wp [2][12][3][64][8]: proj input
         channels 96u .. 96u + 95 (head pairs 2u, 2u + 1) as 3 k-steps in the kernel's
         accumulator-operand order -- element e of lane l in k-step s is input channel
-        96u + 32s + 4(l >> 4) + (e & 3) + 16(e >> 2).
+        96u + 32s + 4(l >> 4) + (e & 3) + 16(e >> 2); biases as one fp32 [5][256] pack (bproj |
+        per head pair: the q, k, v bias rows of its two heads) and the bias table zero-padded
+        to 2048 floats (the kernel stages whole 1 KiB pieces).
         ws 4 / C 80 (rgbac_winattn_block_ws4): wq [15 tiles][3 k-steps][64][8] (k >= 80 zero),
         wp [5][5][64][4] 16x16x16 fragments (lane l: row 16m + (l & 15), input channels
         16kt + 4(l >> 4) .. +3) in a 13 KiB buffer (the kernel DMAs whole KiB)."""
@@ -156,6 +158,20 @@ class WindowAttention(nn.Module):
                     colp = (96 * u + 32 * s + 4 * (l4 >> 4) + (e & 3) +
                             16 * (e >> 2)).expand(2, 12, 3, 64, 8)
                     wp = Wp[rowp, colp].to(torch.bfloat16).contiguous()
+                    bq = self.qkv.bias.float()
+                    bias = torch.zeros((5, 256), dtype=torch.float32, device=dev)
+                    bias[0, :192] = self.proj.bias.float()
+                    for pr in range(4):
+                        for part in range(3):
+                            bias[1 + pr, 48 * part:48 * part + 48] = bq[192 * part + 48 * pr:
+                                                                      192 * part + 48 * pr + 48]
+                    table = torch.zeros(2048, dtype=torch.float32, device=dev)
+                    table[:225 * 8] = self.relative_position_bias_table.float().reshape(-1)
+                    ent = (wq, bias, wp, None, table, self.qkv.bias.float().contiguous(),
+                           self.proj.bias.float().contiguous(),
+                           self.relative_position_bias_table.float().contiguous())
+                    self.__dict__["_rgbac_block"] = (key, ent)
+                    return ent
                 else:
                     C = self.dim
                     t, ks = ar(3 * C // 16).view(-1, 1, 1, 1), ar(3).view(1, 3, 1, 1)
@@ -188,26 +204,56 @@ class WindowAttention(nn.Module):
         return (ws == 4 and self.dim == 80 and x.H % 4 == 0 and x.W % 4 == 0 and
                 rt.WINBLOCK4_FUSED)
 
+    def block_workspace(self, B, H, W, device):
+        """Device workspace of the ws-8 block (rgbac_winattn_block_workspace bytes): per-window
+        arrival counters (zero here, and left zero by every launch), alpha flags and the O^T
+        hand-off slots.  Kept per module and device, grown when a larger frame comes."""
+        need = int(_lib.load().rgbac_winattn_block_workspace(B, H, W))
+        if need < 0:
+            raise RuntimeError(f"rgbac_winattn_block_workspace({B}, {H}, {W}) failed")
+        cache = self.__dict__.setdefault("_rgbac_ws", {})
+        buf = cache.get(device)
+        if buf is None or buf.numel() < need:
+            buf = torch.zeros(need, dtype=torch.uint8, device=device)
+            cache[device] = buf
+        return buf
+
     def run_block(self, x, alpha, shift, masked):
         """The whole block (qkv + attention + proj + MASKSEL residual) as one
-        rgbac_winattn_block(_ws4) launch: x + attn(x) on active windows, x elsewhere."""
-        wq, bqkv, wp, bproj, table = self.block_packs()
+        rgbac_winattn_block(_ws4) call: x + attn(x) on active windows, x elsewhere."""
+        packs = self.block_packs()
         out = rt.new_feat(x.B, x.H, x.W, x.C, x.t.dtype, x.t.device)
         if masked:
             alpha = alpha.contiguous().float()
         npix = x.B * x.H * x.W
         C, ws = self.dim, self.window_size[0]
-        fn = "rgbac_winattn_block" if ws == 8 else "rgbac_winattn_block_ws4"
-        kname = "winblock_kernel" if ws == 8 else "winblock4_kernel"
+        scale = float(torch.tensor(self.scale, dtype=torch.float32))
+        aptr = _lib.ptr(alpha) if masked else None
+        stream = _lib.stream_ptr(x.t.device)
+        if ws == 8 and os.environ.get("RGBAC_WINBLOCK_V2", "") == "1":
+            wq, _, wp, _, _, bqkv, bproj, table = packs
+            kname = "winblock_v2_kernel"
+            run = lambda: _lib.call(
+                "rgbac_winattn_block_v2", x.B, x.H, x.W, shift, 1 if masked else 0, scale,
+                x.ptr(), x.ldc, aptr, wq.data_ptr(), bqkv.data_ptr(), wp.data_ptr(),
+                bproj.data_ptr(), table.data_ptr(), out.ptr(), out.ldc, stream)
+        elif ws == 8:
+            wq, bias, wp, _, table = packs[:5]
+            work = self.block_workspace(x.B, x.H, x.W, x.t.device)
+            kname = "winblock_kernel"
+            run = lambda: _lib.call(
+                "rgbac_winattn_block", x.B, x.H, x.W, shift, 1 if masked else 0, scale,
+                x.ptr(), x.ldc, aptr, wq.data_ptr(), bias.data_ptr(), wp.data_ptr(),
+                table.data_ptr(), out.ptr(), out.ldc, work.data_ptr(), work.numel(), stream)
+        else:
+            wq, bqkv, wp, bproj, table = packs
+            kname = "winblock4_kernel"
+            run = lambda: _lib.call(
+                "rgbac_winattn_block_ws4", x.B, x.H, x.W, shift, 1 if masked else 0, scale,
+                x.ptr(), x.ldc, aptr, wq.data_ptr(), bqkv.data_ptr(), wp.data_ptr(),
+                bproj.data_ptr(), table.data_ptr(), out.ptr(), out.ldc, stream)
         rt.timed(kname, 2.0 * npix * (3 * C * C + 2 * ws * ws * C + C * C),
-                 2.0 * npix * 2 * x.ldc,
-                 lambda: _lib.call(
-                     fn, x.B, x.H, x.W, shift, 1 if masked else 0,
-                     float(torch.tensor(self.scale, dtype=torch.float32)), x.ptr(), x.ldc,
-                     _lib.ptr(alpha) if masked else None, wq.data_ptr(), bqkv.data_ptr(),
-                     wp.data_ptr(), bproj.data_ptr(), table.data_ptr(), out.ptr(), out.ldc,
-                     _lib.stream_ptr(x.t.device)),
-                 f"{kname} ws{ws} C{C} {x.H}x{x.W} B{x.B} shift{shift}")
+                 2.0 * npix * 2 * x.ldc, run, f"{kname} ws{ws} C{C} {x.H}x{x.W} B{x.B} shift{shift}")
         return out
 
     def run_nhwc(self, x, alpha, shift, masked, residual=True, amask=None):

@@ -12,7 +12,6 @@ forward builds an autograd graph whose backward is HIP (rgbac/train_forward.py);
 under torch.no_grad() it runs the fused, grouped inference path.
 """
 import math
-import os
 
 import torch
 import torch.nn as nn
@@ -52,28 +51,6 @@ def reconstruct_error(input, output, input_mask, output_mask=None):
 class GeometryError(RuntimeError, ValueError):
     """Input size the reference's forward cannot process either (RuntimeError like the
     reference's own failure, ValueError for callers of round 1's API)."""
-
-
-# bf16 inference: the batch runs as BATCH_SPLIT equal parts, each on its own stream, part k's
-# encoder released when part k-1's encoder is done.  The slice chain of the latent path is a
-# string of latency-bound launches that leave most of every CU idle, so part k's chain runs
-# beside part k+1's encoder and part k-1's decoder (throughput-bound work) instead of after
-# them.  Every image goes through the same kernels either way; mse / bpp are the means of the
-# parts' values (equal parts: the batch mean of the per-image terms).  "1": one pass.
-# Measured (interleaved A/B of the config-2 graph, DESIGN.md section 14j): 2 parts 2,510 /
-# 2,495 us and 4 parts 4,312 / 4,210 us against 1,723 / 1,734 us in one pass -- at B 4 most
-# launches take 70-100 % of their B 8 time, so the overlap cannot pay for the doubled launch
-# count.  Opt-in.
-BATCH_SPLIT = int(os.environ.get("RGBAC_BATCH_SPLIT", "1"))
-_SPLIT_STREAMS = {}
-
-
-def _split_streams(dev, n):
-    st = _SPLIT_STREAMS.get(dev, [])
-    if len(st) < n:
-        st = st + [torch.cuda.Stream(device=dev) for _ in range(n - len(st))]
-        _SPLIT_STREAMS[dev] = st
-    return st[:n]
 
 
 def check_geometry(H, W):
@@ -203,12 +180,6 @@ class AutoEncoder(_CompressionModelMixin, nn.Module):
             from ..train_forward import rgb_forward_train
             return rgb_forward_train(self, input, mask, reconmask, me2, me3, noise_z, noise_y)
         dt = self.compute_dtype
-        n = BATCH_SPLIT
-        if n > 1 and dt == torch.bfloat16 and debug is None and not self.training and \
-                B % n == 0 and B >= n:
-            with torch.no_grad():
-                return self._forward_split(input.contiguous().float(), mask, reconmask, me2, me3,
-                                           n)
         with torch.no_grad():
             x = input.contiguous().float()
             # reconmask = round(reconmask*255)/255 ; md1..md4 = DecMakeMask(reconmask)  (:212-215):
@@ -231,34 +202,4 @@ class AutoEncoder(_CompressionModelMixin, nn.Module):
                            x_hat_nchw=x_hat)
         if debug is not None:
             debug.update(y=y)
-        return x_hat, out[0], out[1], out[2], out[3]
-
-    def _forward_split(self, x, mask, reconmask, me2, me3, n):
-        """forward() over n equal batch parts on n streams (see BATCH_SPLIT)."""
-        B, _, H, W = x.shape
-        dev, dt, h = x.device, self.compute_dtype, B // n
-        main = torch.cuda.current_stream(dev)
-        mask = mask.contiguous().float()
-        reconmask = reconmask.contiguous()
-        x_hat = torch.empty((B, 3, H, W), dtype=torch.float32, device=dev)
-        outs, prev = [], None
-        for k, st in enumerate(_split_streams(dev, n)):
-            st.wait_stream(main)
-            if prev is not None:
-                st.wait_event(prev)                 # part k's encoder after part k-1's
-            sl = slice(k * h, (k + 1) * h)
-            with torch.cuda.stream(st):
-                _, md = mask_pyramid(reconmask[sl], 4, round255=True)
-                y = self.Encoder.nhwc(rt.to_nhwc(x[sl], dt), me2[sl], me3[sl])   # :217
-                prev = torch.cuda.Event()
-                prev.record(st)
-                yh, ypart, zpart = latent_path(self, y, False)
-                xh = self.Decoder.nhwc(yh, md[1], md[2])                          # :273
-                outs.append(finalize(0, x[sl], xh, mask[sl], ypart, zpart,        # :280-295
-                                     x_hat_nchw=x_hat[sl]))
-        for st in _split_streams(dev, n):
-            main.wait_stream(st)
-        for o in outs:
-            o.record_stream(main)
-        out = torch.stack(outs).mean(0)
         return x_hat, out[0], out[1], out[2], out[3]

@@ -187,12 +187,9 @@ def latent_path(model, y, training=False, noise_z=None, noise_y=None, debug=None
                            for i in range(p0c, ns)])
                 ev_cc.record(side)
     waited = set()
-    if not pre_ok and _fold_ok(model, y, Cm, cs, dt, training, debug):
-        _fold_waves(model, waves, y, YH, means, scales, Cm, cs, B, h, w, dt, dev, ypart)
-    else:
-        _slice_waves(model, waves, y, YH, means, scales, Cm, cs, B, h, w, dt, dev, training,
-                     noise_y, debug, liks, musig, ypart, pre_ok, p0c, p0l, waited,
-                     (main, ev_cc, ev_lrp, Pm, Ps, Plrp) if pre_ok else None)
+    _slice_waves(model, waves, y, YH, means, scales, Cm, cs, B, h, w, dt, dev, training,
+                 noise_y, debug, liks, musig, ypart, pre_ok, p0c, p0l, waited,
+                 (main, ev_cc, ev_lrp, Pm, Ps, Plrp) if pre_ok else None)
     if pre_ok:
         main.wait_stream(side)                 # join the side stream (graph capture needs it)
     if debug is not None:
@@ -280,184 +277,6 @@ def _slice_waves(model, waves, y, YH, means, scales, Cm, cs, B, h, w, dt, dev, t
         rt.launch([prep_conv(model.lrp_transforms[i][4], [l2[j].src()], out=YH,
                              out_coff=i * cs, act="tanh_half", res1=pres[j])
                    for j, i in enumerate(wave)])
-
-
-# bf16 inference: the chain's narrow tail convs folded into the next wide conv
-# (csrc/fold.hip, rgbac_conv_fold):
-#   * mu_i + the quantisation into lrp_transforms[i][0] (whose last input channels are
-#     y_hat_i^pre = round(y_i - mu_i) + mu_i); the folded slices' bits in one
-#     rgbac_gauss_bits launch after the chain;
-#   * lrp_transforms[i][4] into the next wave's cc_*_transforms[.][0] (whose last input channels
-#     are y_hat_i).
-# Measured in the forward graph (interleaved same-box A/B): the
-# quantisation fold saves 2.4-4.5 us per one-slice wave against 10 us for the deferred bits
-# launch, and loses 6 us on the five-slice wave; the tanh fold saves 0-3 us on the one-slice
-# waves and loses 33 us on the five-slice wave (each of its 20 workgroups per tile recomputes
-# the same narrow conv).  The chain's kernel sum was within noise either way (574-576 us folded
-# vs 563-578 us unfolded), so the fold is opt-in: RGBAC_FOLD=1 (quantisation, one-slice
-# waves), + RGBAC_FOLD_TANH=1, + RGBAC_FOLD_WIDE=1 (the five-slice wave too).
-FOLD = os.environ.get("RGBAC_FOLD", "0") == "1"
-FOLD_TANH = os.environ.get("RGBAC_FOLD_TANH", "0") == "1"
-FOLD_WIDE = os.environ.get("RGBAC_FOLD_WIDE", "0") == "1"     # also the multi-slice waves
-# output channels per workgroup of the folded launches (the tiles the unfolded convs tuned
-# to: 64 for the one-group lrp convs, 128 for the grouped ones)
-FOLD_BN_ONE = int(os.environ.get("RGBAC_FOLD_BN1", "64"))
-FOLD_BN_MANY = int(os.environ.get("RGBAC_FOLD_BNG", "128"))
-
-
-def _fold_ok(model, y, Cm, cs, dt, training, debug):
-    """The folded chain applies: bf16 inference without parity tooling, 8-channel slices, the
-    narrow convs 3x3 128 -> 8, and every folded wide conv with 72..128 input channels."""
-    if not FOLD or training or debug is not None or dt != torch.bfloat16 or \
-            torch.is_grad_enabled() or cs != 8 or y.H % 4 or y.W % 16:
-        return False
-    ns, msup = model.num_slices, model.max_support_slices
-    for i in range(ns):
-        for st in (model.cc_mean_transforms[i], model.cc_scale_transforms[i],
-                   model.lrp_transforms[i]):
-            if st[2].out_channels != 128 or st[4].in_channels != 128 or \
-                    st[4].out_channels != cs or st[4].kernel_size[0] != 3 or \
-                    st[0].kernel_size[0] != 3:
-                return False
-        n = cs * min(i, msup)
-        if not (72 <= Cm + n + cs <= 128 and (n == 0 or 72 <= Cm + n <= 128)):
-            return False
-    return True
-
-
-def _narrow_pack(m, dt):
-    pk = rt.packed(m, dt, [(m.in_channels, m.in_channels)])
-    return rt.frag_weights(pk), pk.bias
-
-
-def _fold_group(wide, srcs, c0, out, pin, narrow, aux, put=None, mu=None):
-    """rgbac_fold_group of the wide conv ``wide`` over ``srcs`` (the unfolded conv's sources:
-    the last one is the folded 8 channels) with the narrow conv ``narrow`` over ``pin``."""
-    dt = out.t.dtype
-    pk = rt.packed(wide, dt, rt.segs_of(*srcs))
-    assert pk.cin_pad == c0 + 8, (pk.cin_pad, c0)
-    g = _lib.FoldGroup()
-    real = [(f, off, n) for f, off, n in srcs[:-1] if n > 0]
-    for k, (f, off, n) in enumerate(real):
-        g.src[k].ptr, g.src[k].ldc, g.src[k].channels = f.ptr(off), f.ldc, n
-    g.c0, g.cout = c0, wide.out_channels
-    g.weight, g.bias = rt.frag_weights(pk).data_ptr(), pk.bias.data_ptr()
-    g.out, g.out_ldc, g.out_coff = out.ptr(), out.ldc, 0
-    g.pin, g.pin_ldc = pin.ptr(), pin.ldc
-    pw, pb = _narrow_pack(narrow, dt)
-    g.pweight, g.pbias = pw.data_ptr(), pb.data_ptr()
-    g.aux, g.aux_ldc = aux[0].ptr(aux[1]), aux[0].ldc
-    if put is not None:
-        g.writer = 1
-        g.put, g.put_ldc = put[0].ptr(put[1]), put[0].ldc
-        if mu is not None:
-            g.mu, g.mu_ldc = mu[0].data_ptr() + 4 * mu[1], mu[0].shape[-1]
-    return g
-
-
-def _fold_launch(groups, mode, bn, B, h, w, dev, name):
-    arr = (_lib.FoldGroup * len(groups))(*groups)
-    flops = 0.0
-    for g in groups:
-        flops += 2.0 * B * h * w * 9 * ((g.c0 + 8) * g.cout + 128 * 8)
-    rt.timed(name, flops, 0.0, lambda: _lib.call(
-        "rgbac_conv_fold", ctypes.cast(arr, ctypes.c_void_p), len(groups), B, h, w, mode, bn,
-        _lib.stream_ptr(dev)))
-
-
-def _fold_waves(model, waves, y, YH, means, scales, Cm, cs, B, h, w, dt, dev, ypart):
-    """The slice waves of latent_path with narrow tails folded (see FOLD): per wave cc1 (the
-    previous wave's lrp3 folded in where FOLD_TANH takes it), cc2, the (mu | sigma) GAUSS launch
-    or, folded, nothing (lrp1 quantises), lrp1, lrp2, lrp3 unless the next cc1 folds it; then
-    the bits of the folded slices."""
-    msup, ns = model.max_support_slices, model.num_slices
-    Wc = model.cc_mean_transforms[0][0].out_channels
-    Wl = model.lrp_transforms[0][0].out_channels
-    MU = torch.empty((B, h, w, ns * cs), dtype=torch.float32, device=dev)
-    folded = []                     # (slice, t2 of its cc_scale stack) quantised by a fold
-    prev = None                     # (slice, l2, pre) whose lrp3 the next cc1 folds
-    for wi, wave in enumerate(waves):
-        sup = [cs * min(i, msup) for i in wave]
-        k = len(wave)
-        if prev is None:
-            t1 = rt.launch(
-                [prep_conv(model.cc_mean_transforms[i][0], [means.src(), YH.src(0, n)],
-                           act="gelu") for i, n in zip(wave, sup)] +
-                [prep_conv(model.cc_scale_transforms[i][0], [scales.src(), YH.src(0, n)],
-                           act="gelu") for i, n in zip(wave, sup)])
-        else:
-            pi, pl2, ppre = prev
-            t1, groups = [], []
-            for stack, base in ((model.cc_mean_transforms, means),
-                                (model.cc_scale_transforms, scales)):
-                for i, n in zip(wave, sup):
-                    o = rt.new_feat(B, h, w, Wc, dt, dev)
-                    t1.append(o)
-                    groups.append(_fold_group(
-                        stack[i][0], [base.src(), YH.src(0, n - cs), YH.src(n - cs, cs)],
-                        Cm + n - cs, o, pl2, model.lrp_transforms[pi][4], (ppre, 0),
-                        put=(YH, pi * cs) if not groups else None))
-            _fold_launch(groups, _lib.FOLD_TANH, FOLD_BN_MANY if len(groups) > 1 else
-                         FOLD_BN_ONE, B, h, w, dev, "conv_fold_kernel")
-        t2 = rt.launch(
-            [prep_conv(model.cc_mean_transforms[i][2], [t1[j].src()], act="gelu")
-             for j, i in enumerate(wave)] +
-            [prep_conv(model.cc_scale_transforms[i][2], [t1[k + j].src()], act="gelu")
-             for j, i in enumerate(wave)])
-        pres = [rt.new_feat(B, h, w, cs, dt, dev) for _ in wave]
-        if k == 1 or FOLD_WIDE:
-            # lrp1 with mu_i and the quantisation folded: y_hat_i^pre lands in pres[j]
-            l1, groups = [], []
-            for j, (i, n) in enumerate(zip(wave, sup)):
-                o = rt.new_feat(B, h, w, Wl, dt, dev)
-                l1.append(o)
-                groups.append(_fold_group(
-                    model.lrp_transforms[i][0], [means.src(), YH.src(0, n), pres[j].src()],
-                    Cm + n, o, t2[j], model.cc_mean_transforms[i][4], (y, i * cs),
-                    put=(pres[j], 0), mu=(MU, i * cs)))
-                folded.append((i, t2[k + j]))
-            _fold_launch(groups, _lib.FOLD_GAUSS, FOLD_BN_MANY if k > 1 else FOLD_BN_ONE,
-                         B, h, w, dev, "conv_fold_kernel")
-        else:
-            rt.launch([rt.prepare(_musigma_pack(model.cc_mean_transforms[i][4],
-                                                model.cc_scale_transforms[i][4], dt, t2[j].ldc),
-                                  [t2[j].src(), t2[k + j].src()], out=pres[j], act="gauss",
-                                  res1=(y, i * cs), partial=ypart[i])
-                       for j, i in enumerate(wave)])
-            l1 = rt.launch([prep_conv(model.lrp_transforms[i][0],
-                                      [means.src(), YH.src(0, n), pres[j].src()], act="gelu")
-                            for j, (i, n) in enumerate(zip(wave, sup))])
-        l2 = rt.launch([prep_conv(model.lrp_transforms[i][2], [l1[j].src()], act="gelu")
-                        for j, i in enumerate(wave)])
-        # lrp3: folded into the next wave's cc1 when this wave is one slice whose y_hat is the
-        # last channel slice of every next-wave support
-        nxt = waves[wi + 1] if wi + 1 < len(waves) else None
-        if FOLD_TANH and nxt is not None and k == 1 and (len(nxt) == 1 or FOLD_WIDE) and \
-                all(cs * min(i, msup) == cs * (wave[0] + 1) for i in nxt):
-            prev = (wave[0], l2[0], pres[0])
-        else:
-            prev = None
-            rt.launch([prep_conv(model.lrp_transforms[i][4], [l2[j].src()], out=YH,
-                                 out_coff=i * cs, act="tanh_half", res1=pres[j])
-                       for j, i in enumerate(wave)])
-    # the folded slices' bits: sigma conv + likelihood with the stored mu (one launch)
-    groups = []
-    for i, f in folded:
-        g = _lib.BitsGroup()
-        g.pin, g.pin_ldc = f.ptr(), f.ldc
-        pw, pb = _narrow_pack(model.cc_scale_transforms[i][4], dt)
-        g.pweight, g.pbias = pw.data_ptr(), pb.data_ptr()
-        g.y, g.y_ldc = y.ptr(i * cs), y.ldc
-        g.mu, g.mu_ldc = MU.data_ptr() + 4 * i * cs, MU.shape[-1]
-        g.partial = ypart[i].data_ptr()
-        groups.append(g)
-    for g0 in range(0, len(groups), 12):
-        part = groups[g0:g0 + 12]
-        arr = (_lib.BitsGroup * len(part))(*part)
-        rt.timed("gauss_bits_kernel", 2.0 * B * h * w * 9 * 128 * 8 * len(part), 0.0,
-                 lambda arr=arr, n=len(part): _lib.call(
-                     "rgbac_gauss_bits", ctypes.cast(arr, ctypes.c_void_p), n, B, h, w,
-                     _lib.stream_ptr(dev)))
 
 
 def debug_views(debug):

@@ -67,6 +67,14 @@ class RcclComm:
         ent = cls._cache.get(key)
         if ent is not None and ent[0] is gk and ent[1].comm is not None:
             return ent[1]
+        if ent is not None:
+            # a stale entry (the group was destroyed and re-created, or the communicator was
+            # aborted): release its communicator before replacing it
+            try:
+                ent[1].close()
+            except RuntimeError:
+                pass
+            del cls._cache[key]
         c = cls(device, group)
         cls._cache[key] = (gk, c)
         return c
@@ -78,10 +86,22 @@ class RcclComm:
         cls._cache.clear()
 
     def __init__(self, device, group=None):
-        lib = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
-        _lib.call("rgbac_comm_load", lib.encode())
+        self.comm = None
+        self.watchdogs = []
         self.world = dist.get_world_size(group)
         rank = dist.get_rank(group)
+        # every rank loads and checks librccl.so BEFORE the unique id goes out, and the group
+        # agrees on the outcome: one rank failing alone would otherwise fall back to
+        # torch.distributed while its peers block in the broadcast or in ncclCommInitRank
+        lib = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+        err = None
+        try:
+            _lib.call("rgbac_comm_load", lib.encode())
+        except (RuntimeError, OSError) as e:
+            err = e
+        if not group_all_ok(err is None, device, group):
+            raise RuntimeError(f"direct RCCL unavailable on some rank "
+                               f"({err if err is not None else 'a peer failed to load it'})")
         uid = torch.zeros(128, dtype=torch.uint8)
         if rank == 0:
             _lib.call("rgbac_comm_unique_id", ctypes.c_void_p(uid.data_ptr()))
@@ -90,9 +110,21 @@ class RcclComm:
             u = uid.to(device) if dist.get_backend(group) == "nccl" else uid
             dist.broadcast(u, src=src, group=group)
             uid = u.cpu()
-        self.comm = ctypes.c_void_p()
-        _lib.call("rgbac_comm_init", ctypes.c_void_p(uid.data_ptr()), self.world, rank,
-                  device.index, ctypes.byref(self.comm))
+        comm = ctypes.c_void_p()
+        err = None
+        try:
+            _lib.call("rgbac_comm_init", ctypes.c_void_p(uid.data_ptr()), self.world, rank,
+                      device.index, ctypes.byref(comm))
+        except RuntimeError as e:
+            err = e
+        # an init that returned an error on one rank: every rank gives the path up together
+        ok = group_all_ok(err is None, device, group)
+        if not ok:
+            if err is None and comm.value:
+                _lib.call("rgbac_comm_destroy", comm)
+            raise RuntimeError(f"RCCL communicator init failed on some rank "
+                               f"({err if err is not None else 'a peer failed'})")
+        self.comm = comm
         self.device = device
         self.stream = torch.cuda.Stream(device)
 
@@ -120,15 +152,37 @@ class RcclComm:
         _lib.call("rgbac_comm_async_error", self.comm, ctypes.byref(e))
         return e.value
 
+    def _stop_watchdogs(self):
+        me = threading.current_thread()
+        for wd in self.watchdogs:
+            if wd._thread is not me:           # (a watchdog aborting from its own thread)
+                wd.stop()
+        self.watchdogs = []
+
     def abort(self):
+        self._stop_watchdogs()
         if self.comm is not None and self.comm.value:
             _lib.call("rgbac_comm_abort", self.comm)
         self.comm = None
 
     def close(self):
+        """Destroy the communicator; every watchdog attached to it is stopped first, so none
+        polls a destroyed communicator."""
+        self._stop_watchdogs()
         if self.comm is not None and self.comm.value:
             _lib.call("rgbac_comm_destroy", self.comm)
         self.comm = None
+
+
+def group_all_ok(ok, device, group=None):
+    """MIN-reduce a success flag over ``group`` (a CUDA tensor for an RCCL group, CPU for
+    gloo): True only when every rank passed ``ok=True``."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return bool(ok)
+    dev = device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
 
 
 atexit.register(RcclComm.close_all)
@@ -160,6 +214,9 @@ class CommWatchdog:
         self._thread = None
 
     def start(self):
+        ws = getattr(self.comm, "watchdogs", None)
+        if ws is not None and self not in ws:
+            ws.append(self)                # the communicator's close() / abort() stops it
         if self._thread is None:
             self._thread = threading.Thread(target=self._run, name="rgbac-comm-watchdog",
                                             daemon=True)
@@ -168,9 +225,9 @@ class CommWatchdog:
 
     def stop(self):
         self._stop.set()
-        if self._thread is not None:
+        if self._thread is not None and self._thread is not threading.current_thread():
             self._thread.join()
-            self._thread = None
+        self._thread = None
 
     def arm(self, done=None):
         """A step was enqueued; ``done()`` (e.g. a recorded event's ``query``) says when it has
@@ -189,6 +246,8 @@ class CommWatchdog:
         None."""
         if self.fired is not None:
             return self.fired
+        if getattr(self.comm, "comm", True) is None:
+            return None                    # the communicator was closed: nothing to watch
         reason = None
         err = self.comm.async_error()
         if err:
@@ -213,6 +272,8 @@ class CommWatchdog:
 
     def _run(self):
         while not self._stop.wait(self.poll_s):
+            if getattr(self.comm, "comm", True) is None:
+                return                     # closed: stop quietly
             if self.check() is not None:
                 return
 
@@ -396,7 +457,7 @@ class DataParallelTrainer:
     (``make_comm_events``) when the step is captured in a HIP graph."""
 
     def __init__(self, net, optimizer, bucket_bytes=25 << 20, force_buckets=False, group=None,
-                 rccl=None):
+                 rccl=None, watchdog_s=None):
         self.net, self.opt = net, optimizer
         self.buckets = None
         self.comm = None
@@ -419,6 +480,11 @@ class DataParallelTrainer:
             self.comm = comm
             self.buckets = GradBuckets(optimizer.params, flat, bucket_bytes, group=group,
                                        comm=comm)
+            if comm is not None and watchdog_s:
+                # opt-in failure detection for eager steps (the direct-RCCL path has no
+                # ProcessGroup watchdog): each step arms it until the step's completion event
+                # fires.  A caller replaying a captured step arms it around each replay.
+                self.watchdog = CommWatchdog(comm, timeout_s=float(watchdog_s)).start()
 
     @staticmethod
     def make_comm_events(external=False):
@@ -442,3 +508,7 @@ class DataParallelTrainer:
                 if isinstance(self.comm_events, list):
                     self.comm_events.append(ev)
         self.opt.step()
+        if self.watchdog is not None and not torch.cuda.is_current_stream_capturing():
+            done = torch.cuda.Event()
+            done.record()
+            self.watchdog.arm(done=done.query)

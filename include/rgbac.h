@@ -192,58 +192,6 @@ int rgbac_winattn_core_ex(int dtype, int batch, int h, int w, int channels,
                           const float* bias, void* out, int64_t ldo, uint8_t* sel,
                           const float* amask, int amask_nw, int hpb, void* stream);
 
-/* Slice-chain conv with the chain's narrow tail conv folded in (bf16 inference; csrc/fold.hip).
- * The slice stacks of models/AutoEncoderRGB_Journal.py:240-264 end in narrow 128 -> 8 3x3
- * convs (cc_mean_transforms[i][4] -> mu, lrp_transforms[i][4] -> the tanh update) whose
- * 8 output channels are the LAST 8 input channels of the next wide conv: lrp_transforms[i][0]
- * reads [means, y_hat_<i, y_hat_i^pre] (:260-262, y_hat_i^pre = round(y_i - mu_i) + mu_i,
- * :255-257) and cc_*_transforms[i+1][0] reads [means|scales, y_hat_<=i] (:241-252).  Each
- * workgroup of this launch recomputes the narrow conv for its own (4+2) x (16+2) patch
- * (K split over its 4 waves, from a (4+4) x (16+4) halo of the narrow conv's 128-channel
- * input in LDS) and writes the 8 values straight into its patch of the wide conv's input:
- *   RGBAC_FOLD_GAUSS: value = rint(y - mu) + mu,  mu = conv(pin) + pbias,  aux = y_i
- *   RGBAC_FOLD_TANH:  value = aux + 0.5 * tanh(conv(pin) + pbias),        aux = pre_i
- * (zero outside the image: the wide conv's padding).  The wide conv (3x3 stride 1, GELU) then
- * runs on [src0, src1, value] with its fragment-major pack (see rgbac_conv_args.tile).
- * Groups with ``writer`` also store the folded value of their own pixels to ``put`` (GAUSS:
- * y_hat_i^pre, the lrp residual; TANH: y_hat_i into the decoder input) and, GAUSS, the fp32
- * mu to ``mu`` (read back by rgbac_gauss_bits): with several groups folding the same narrow
- * conv exactly one of them is the writer. */
-enum rgbac_fold_mode { RGBAC_FOLD_GAUSS = 1, RGBAC_FOLD_TANH = 2 };
-typedef struct rgbac_fold_group {
-  rgbac_src src[2];            /* wide-conv input channels [0, c0) (src[1].channels may be 0) */
-  int32_t c0;                  /* folded channels [c0, c0 + 8); c0 + 8 = the pack's cin_pad */
-  int32_t cout;                /* wide-conv output channels (multiple of 4)                 */
-  const void* weight;          /* fragment-major copy of the wide conv's pack, bf16         */
-  const float* bias;
-  void* out; int64_t out_ldc; int32_t out_coff; int32_t writer;
-  const void* pin; int64_t pin_ldc;          /* narrow conv input: 128 channels, NHWC    */
-  const void* pweight;         /* fragment-major copy of the narrow conv's pack (128 -> 8)   */
-  const float* pbias;          /* >= 16 entries (the pack's zero-padded bias)                */
-  const void* aux; int64_t aux_ldc;          /* GAUSS: y_i; TANH: y_hat_i^pre (8 ch)     */
-  float* mu; int64_t mu_ldc;                 /* GAUSS writer: fp32 mu out                */
-  void* put; int64_t put_ldc;                /* writer: the folded value, 8 channels     */
-} rgbac_fold_group;
-/* ngroups in 1..12 share batch / h / w (h % 4 == 0, w % 16 == 0), the mode and ceil((c0 + 8)
- * / 32) (3 or 4); bn = 64 or 128 output channels per workgroup. */
-int rgbac_conv_fold(const rgbac_fold_group* groups, int ngroups, int batch, int h, int w,
-                    int mode, int bn, void* stream);
-
-/* The bits of slices whose quantisation ran folded (RGBAC_FOLD_GAUSS): per group the sigma
- * conv (cc_scale_transforms[i][4], 128 -> 8, 3x3) over ``pin`` and the GaussianConditional
- * likelihood of y_hat = rint(y - mu) + mu with the stored mu (as rgbac_gaussian_slice,
- * eval mode); partial[t] = the fp64 bits of 64-pixel tile t (4 x 16 pixels, tiles in
- * (batch, row, column) order). */
-typedef struct rgbac_bits_group {
-  const void* pin; int64_t pin_ldc;
-  const void* pweight; const float* pbias;
-  const void* y; int64_t y_ldc;
-  const float* mu; int64_t mu_ldc;
-  double* partial;
-} rgbac_bits_group;
-int rgbac_gauss_bits(const rgbac_bits_group* groups, int ngroups, int batch, int h, int w,
-                     void* stream);
-
 /* compressai GaussianConditional.forward + ste_round for one channel slice
  * (models/AutoEncoderRGB_Journal.py:255-257, bits :280):
  *   out_hat = round(y - mu) + mu   (torch.round: half to even)
@@ -520,23 +468,52 @@ int rgbac_stem_gdn(int batch, int in_h, int in_w, const void* x, int64_t x_ldc, 
 int rgbac_rgba_augment(int batch, const void* descs, int out_h, int out_w, int antialias,
                        float* masked, float* alpha, float* img, float* rgba, void* stream);
 
+/* GDN / IGDN parameter reparametrisation (reference: layers/GDN.py:9-23 LowerBound, :71-78),
+ * fp32, nb beta and ng gamma elements in one launch:
+ *   beta_out = max(beta, beta_bound)^2 - pedestal,  gamma_out = max(gamma, gamma_bound)^2 - pedestal
+ * and its backward: g2 = d_out * (2 max(p, bound)), passed where p >= bound or g2 < 0,
+ * stored to dbeta / dgamma (accumulate == 0) or added into them (accumulate == 1; a null
+ * d_out is a zero gradient).  Uncontracted, op for op torch's arithmetic. */
+int rgbac_gdn_reparam(int nb, int ng, const float* beta, const float* gamma, float beta_bound,
+                      float gamma_bound, float pedestal, float* beta_out, float* gamma_out,
+                      void* stream);
+int rgbac_gdn_reparam_bwd(int nb, int ng, const float* beta, const float* gamma,
+                          float beta_bound, float gamma_bound, const float* dbeta_out,
+                          const float* dgamma_out, float* dbeta, float* dgamma, int accumulate,
+                          void* stream);
+
 /* Fused masked shifted-window attention block, bf16, window 8, C = 192, 8 heads
  * (reference: layers/masked_win_attention.py:96-131 WindowAttention.forward, :169-251
  * WinBasedAttention.forward).  out = x + proj(attn(x)) on windows whose alpha is non-zero
  * anywhere (all windows when masked == 0), out = x elsewhere; the cyclic shift, window
  * partition / drop / reverse, the shifted-frame region mask and the relative position bias
- * are index math inside the kernel.  x, out: NHWC bf16 [batch][h][w][ld] (h, w multiples of
- * 8, out != x); alpha: fp32 [batch][h][w] (masked only); wq_packed / wp_packed: the
- * fragment-major qkv / proj packs of WindowAttention.block_packs() (wq [4][54][64][8]; wp
- * [2][12][3][64][8] in the kernel's accumulator-operand k order: element e of lane l in
- * k-step s of pair-pair u is input channel 96u + 32s + 4(l >> 4) + (e & 3) + 16(e >> 2));
- * bqkv [576], bproj [192]
- * fp32; table: relative_position_bias_table [225][8] fp32.  Replaces the qkv GEMM,
- * rgbac_winattn_core_ex and the MASKSEL proj GEMM of one WinBasedAttention call. */
+ * are index math inside the kernels.  x, out: NHWC bf16 [batch][h][w][ld] (h, w multiples of
+ * 8, out != x, 16-byte aligned); alpha: fp32 [batch][h][w] (masked only); wq_packed /
+ * wp_packed: the fragment-major qkv / proj packs of WindowAttention.block_packs() (wq
+ * [4][54][64][8]; wp [2][12][3][64][8] in the kernel's accumulator-operand k order: element e
+ * of lane l in k-step s of pair-pair u is input channel 96u + 32s + 4(l >> 4) + (e & 3) +
+ * 16(e >> 2)); bias_pack: fp32 [5][256] = bproj (192) | per head pair p: qkv.bias rows
+ * 48p.., 192 + 48p.., 384 + 48p.. (48 each), zero padded; table_pad: relative_position_bias_table
+ * [225][8] fp32 zero-padded to 2048 floats.  work: device workspace of at least
+ * rgbac_winattn_block_workspace(batch, h, w) bytes, 256-byte aligned (no initial contents
+ * needed).  Launches per 8,192 windows: one flag pass (masked only, once), the persistent
+ * head-pair kernel (qkv + attention of one head pair over a share of the active windows, O
+ * to the workspace, inactive windows copied) and the proj kernel over the compacted active
+ * windows.  Replaces the qkv GEMM, rgbac_winattn_core_ex and the MASKSEL proj GEMM of one
+ * WinBasedAttention call. */
+int64_t rgbac_winattn_block_workspace(int batch, int h, int w);
 int rgbac_winattn_block(int batch, int h, int w, int shift, int masked, float scale,
                         const void* x, int64_t ldx, const float* alpha, const void* wq_packed,
-                        const float* bqkv, const void* wp_packed, const float* bproj,
-                        const float* table, void* out, int64_t ldo, void* stream);
+                        const float* bias_pack, const void* wp_packed, const float* table_pad,
+                        void* out, int64_t ldo, void* work, int64_t work_bytes, void* stream);
+
+/* The round-3 single-kernel form of the same block (winblock_v2_kernel: one workgroup per
+ * window pair streaming all four head pairs' weights), kept for the A/B against
+ * rgbac_winattn_block until it is measured out: bqkv [576], bproj [192], table [225][8]. */
+int rgbac_winattn_block_v2(int batch, int h, int w, int shift, int masked, float scale,
+                           const void* x, int64_t ldx, const float* alpha, const void* wq_packed,
+                           const float* bqkv, const void* wp_packed, const float* bproj,
+                           const float* table, void* out, int64_t ldo, void* stream);
 
 /* The same block at window 4, C = 80, 8 heads of 10 (the 1/16-resolution attention blocks,
  * layers/TransformRGB.py:63,80): one wave per window, every product after the qkv GEMM in

@@ -128,3 +128,69 @@ def test_buckets_refuse_changed_graph(world1):
     with pytest.raises(RuntimeError, match="autograd graph changed"):
         gb.finish()
     gb.remove()
+
+
+class ClosableComm(StubComm):
+    """A stub with RcclComm's close protocol: ``comm`` is None once closed, and close()
+    stops every attached watchdog first."""
+
+    def __init__(self):
+        super().__init__()
+        self.comm = object()
+        self.watchdogs = []
+        self.polls = 0
+
+    def async_error(self):
+        assert self.comm is not None, "polled a closed communicator"
+        self.polls += 1
+        return 0
+
+    def close(self):
+        for wd in self.watchdogs:
+            wd.stop()
+        self.watchdogs = []
+        self.comm = None
+
+
+def test_close_stops_attached_watchdog():
+    comm, clock, exits = ClosableComm(), Clock(), []
+    wd = _dog(comm, clock, exits).start()
+    assert comm.watchdogs == [wd]
+    deadline = 200
+    while comm.polls == 0 and deadline:
+        threading.Event().wait(0.01)
+        deadline -= 1
+    comm.close()
+    assert wd._thread is None
+    assert wd.check() is None and exits == []        # a closed communicator is not polled
+
+
+def _agree_worker(rank, world, port, out):
+    import os
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rgbac.parallel import group_all_ok
+        out.put((rank, group_all_ok(True, torch.device("cpu")),
+                 group_all_ok(rank != 1, torch.device("cpu"))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_group_agrees_on_a_failure_gloo():
+    """One rank failing (e.g. librccl.so missing there) makes every rank give the direct RCCL
+    path up together (rgbac.parallel.group_all_ok, gloo world 2)."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_agree_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert res == [(0, True, False), (1, True, False)]

@@ -63,27 +63,6 @@ def test_dse_fused_matches_unfused_and_oracle(device, kind, B, H, W):
     assert frac <= 1e-3, frac
 
 
-@pytest.mark.parametrize("kind,B,H,W", [("rgb", 2, 64, 96), ("rgb", 1, 40, 50),
-                                        ("mask", 1, 17, 33), ("rgb", 2, 256, 256)])
-def test_dse_four_wave_kernel_matches(device, monkeypatch, kind, B, H, W):
-    """dse_block_kernel<.., 4> (RGBAC_DSE_WAVES=4: one wave per SIMD, conv1's weight fragments
-    in registers, 10 conv1 fragments and 4 output rows per wave) against the 8-wave kernel:
-    the same MFMAs per fragment in the same order, so bit-identical outputs."""
-    from rgbac import runtime as rt
-    from rgbac.layers.TransformRGB import dse_fused
-    m = _dse(kind, 7)
-    C = 3 if kind == "rgb" else 1
-    x = torch.rand((B, C, H, W), generator=torch.Generator().manual_seed(5)).cuda()
-    outs = {}
-    with torch.no_grad():
-        f = rt.to_nhwc(x, torch.bfloat16)
-        for w in ("8", "4"):
-            monkeypatch.setenv("RGBAC_DSE_WAVES", w)
-            outs[w] = dse_fused(m, f).t.clone()
-        torch.cuda.synchronize()
-    assert torch.equal(outs["4"].view(torch.int16), outs["8"].view(torch.int16))
-
-
 def test_dse_module_forward_uses_fused_path(device):
     """DSE.forward under no_grad at bf16 goes through rgbac_dse_block (3 launches)."""
     from rgbac import runtime as rt
@@ -154,6 +133,59 @@ def test_winattn_block_fused_matches_unfused_and_oracle(device, C, ws, B, H, W, 
     if masked and shift == 0 and H >= 4 * ws:                # transparent windows: exactly x
         xb = rt.to_nchw(f).float().cpu()
         assert torch.equal(got[:, :, ws:H // 2, ws:W // 2], xb[:, :, ws:H // 2, ws:W // 2])
+
+
+# The head-pair ws-8 block (round 6): per-window flags (winflag_kernel), device-side
+# compaction and one head pair per persistent workgroup (winblock_kernel), the proj over the
+# compacted list (winproj_kernel).  It keeps every product and rounding point of the round-3
+# kernel (winblock_v2_kernel), so the two are compared bit for bit, over repeated calls on one
+# workspace.  B 3 at 512^2 (12,288 windows) spans two launches of at most 8,192 windows.
+@pytest.mark.parametrize("B,H,W,shift,alpha_kind", [
+    (8, 64, 64, 0, "bench"), (2, 64, 64, 4, "quarter"), (1, 32, 48, 0, "ones"),
+    (1, 24, 40, 4, "quarter"), (2, 16, 16, 0, "zeros"), (1, 8, 8, 0, "one_pixel"),
+    (3, 8, 24, 0, "unmasked"), (3, 512, 512, 0, "quarter"), (4, 256, 256, 4, "bench")])
+def test_winblock_head_pair_kernel_bit_identical(device, B, H, W, shift, alpha_kind):
+    import os
+    from rgbac import runtime as rt
+    from rgbac.layers.masked_win_attention import WinBasedAttention
+    torch.manual_seed(21)
+    m = WinBasedAttention(192, 8, 8, shift).cuda().eval()
+    with torch.no_grad():
+        m.attn.relative_position_bias_table.normal_(0, 0.5)
+        m.attn.qkv.bias.normal_(0, 0.2)
+        m.attn.proj.bias.normal_(0, 0.2)
+    m.masked = alpha_kind != "unmasked"
+    g = torch.Generator().manual_seed(22)
+    x = torch.randn((B, 192, H, W), generator=g)
+    alpha = torch.ones((B, 1, H, W))
+    if alpha_kind == "quarter":
+        alpha[:, :, : H // 2, : W // 2] = 0
+    elif alpha_kind == "zeros":
+        alpha.zero_()
+    elif alpha_kind == "one_pixel":
+        alpha.zero_()
+        alpha[0, 0, 5, 2] = 0.25
+    elif alpha_kind == "bench":                       # ones / half / ellipse / all-zero cycle
+        yy, xx = torch.meshgrid(torch.linspace(-1, 1, H), torch.linspace(-1, 1, W), indexing="ij")
+        for b in range(B):
+            k = b % 4
+            alpha[b, 0] = (1.0 if k == 0 else 0.5 if k == 1 else
+                           ((xx / 0.8) ** 2 + (yy / 0.6) ** 2 <= 1).float() if k == 2 else 0.0)
+    xg, ag = x.cuda(), alpha.cuda()
+    with torch.no_grad():
+        f = rt.to_nhwc(xg, torch.bfloat16)
+        outs = []
+        for _ in range(3):                            # repeated calls on one workspace
+            outs.append(rt.to_nchw(m.attn.run_block(f, ag, shift, m.masked)).float())
+        os.environ["RGBAC_WINBLOCK_V2"] = "1"
+        try:
+            ref_out = rt.to_nchw(m.attn.run_block(f, ag, shift, m.masked)).float()
+        finally:
+            os.environ.pop("RGBAC_WINBLOCK_V2", None)
+    for o in outs:
+        assert torch.equal(o, ref_out), (o - ref_out).abs().max().item()
+    if alpha_kind == "zeros":
+        assert torch.equal(outs[0], rt.to_nchw(f).float())
 
 
 # ---------------------------------------------------------------------------------------
@@ -233,36 +265,6 @@ def test_stream_unit_matches_chunk_ring_kernel(device, kind):
         assert frac <= 1e-3, frac
 
 
-@pytest.mark.parametrize("mode", ["1", "2"])
-@pytest.mark.parametrize("kind,B,H,W", [(0, 2, 32, 64), (1, 2, 32, 64), (0, 1, 24, 48), (1, 1, 8, 16)])
-def test_half_tile_unit_matches_stream_kernel(device, monkeypatch, mode, kind, B, H, W):
-    """ru_half_kernel (8 x 8 tiles: RGBAC_RU_HALF=1 one per workgroup at four workgroups per CU,
-    =2 two neighbouring tiles per workgroup with the second's x fetched during the first) against
-    ru_stream_kernel (8 x 16 tiles) on the same C = 192 units: the same GEMM order per output
-    and the same bf16 rounding points, so the two agree to 1 bf16 ulp of the output range at
-    99.9 % of the elements (image borders included: 8 x 16 has a single tile)."""
-    from rgbac import runtime as rt
-    from rgbac.layers import Masked_Attention as MA
-    from rgbac.models import AutoEncoderMask_Journal as AM
-    torch.manual_seed(41 + kind)
-    mods = [(MA.ResidualUnit(192) if kind == 0 else AM.ResBlock(192)).cuda() for _ in range(2)]
-    units = [((m.conv[0], m.conv[2], m.conv[4]) if kind == 0 else (m.conv1, m.conv2, m.conv3))
-             for m in mods]
-    xs = [rt.to_nhwc(torch.randn((B, 192, H, W), device="cuda"), torch.bfloat16) for _ in mods]
-    with torch.no_grad():
-        monkeypatch.setenv("RGBAC_RU_HALF", "0")
-        base = [rt.to_nchw(o).float() for o in MA.run_bottlenecks_fused(list(zip(units, xs)), kind)]
-        monkeypatch.setenv("RGBAC_RU_HALF", mode)
-        got = [rt.to_nchw(o).float() for o in MA.run_bottlenecks_fused(list(zip(units, xs)), kind)]
-        torch.cuda.synchronize()
-    for a, b in zip(got, base):
-        scale = b.abs().max().item()
-        frac = ((a - b).abs() > scale * 2.0 ** -8).float().mean().item()
-        print(f"kind {kind} {B}x{H}x{W}: max diff {(a - b).abs().max().item() / scale:.2e}, "
-              f"> 1 ulp {frac:.1e}")
-        assert frac <= 1e-3, frac
-
-
 @pytest.mark.parametrize("kind,B,H,W", [("ru", 1, 72, 136), ("rb", 1, 72, 136), ("ru", 4, 128, 128)])
 def test_small_unit_two_tile_matches_one_tile(device, monkeypatch, kind, B, H, W):
     """ru_small_kernel<RB, 2> (multi-round C = 80 launches: two 4-wave halves per workgroup, each
@@ -287,24 +289,3 @@ def test_small_unit_two_tile_matches_one_tile(device, monkeypatch, kind, B, H, W
         assert torch.equal(a.view(torch.int16), b.view(torch.int16))
 
 
-@pytest.mark.parametrize("kind,B,H,W", [(0, 2, 32, 64), (1, 2, 32, 64), (0, 1, 16, 16), (1, 1, 48, 32)])
-def test_stream_unit_16_row_tile_matches(device, monkeypatch, kind, B, H, W):
-    """ru_stream_kernel<RB, 16> (RGBAC_RU_TILE16=1: 16 x 16 tiles, 8 waves, one workgroup per
-    CU) against the 8 x 16 tile: the same GEMM order per output and the same bf16 rounding
-    points, so bit-identical (image borders included: 16 x 16 is a single tile)."""
-    from rgbac import runtime as rt
-    from rgbac.layers import Masked_Attention as MA
-    from rgbac.models import AutoEncoderMask_Journal as AM
-    torch.manual_seed(61 + kind)
-    mods = [(MA.ResidualUnit(192) if kind == 0 else AM.ResBlock(192)).cuda() for _ in range(2)]
-    units = [((m.conv[0], m.conv[2], m.conv[4]) if kind == 0 else (m.conv1, m.conv2, m.conv3))
-             for m in mods]
-    xs = [rt.to_nhwc(torch.randn((B, 192, H, W), device="cuda"), torch.bfloat16) for _ in mods]
-    outs = {}
-    with torch.no_grad():
-        for mode in ("0", "1"):
-            monkeypatch.setenv("RGBAC_RU_TILE16", mode)
-            outs[mode] = [o.t.clone() for o in MA.run_bottlenecks_fused(list(zip(units, xs)), kind)]
-        torch.cuda.synchronize()
-    for a, b in zip(outs["1"], outs["0"]):
-        assert torch.equal(a.view(torch.int16), b.view(torch.int16))

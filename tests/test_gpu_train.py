@@ -1029,68 +1029,6 @@ def test_reduce_batch_matches_immediate_reductions():
     assert torch.equal(grads[True][0], grads[False][0])
 
 
-def test_side_reduce_matches_in_stream_reductions():
-    """RGBAC_SIDE_REDUCE=1 (the weight-gradient reductions that add into param.grad run on a side
-    stream forked from the backward's stream and joined at the end of backward) and =2 (the
-    weight-gradient kernels too): the AdamClamp
-    flat gradient equals the in-stream path bit for bit (same kernels, same order), eager and
-    in a captured HIP graph (fork / join inside the capture), bf16 B=2 64^2 training step."""
-    from rgbac import autograd as ag
-    from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
-    from rgbac.optim import AdamClamp
-    g = _gen(73)
-    B, H, W = 2, 64, 64
-    x = (torch.randint(0, 256, (B, 3, H, W), generator=g).float() / 255).cuda()
-    a = torch.ones((B, 1, H, W)).cuda()
-    me = [t.cuda() for t in ref.supply_mask(a.cpu())]
-    nz = (torch.rand((B, 1, 1, 192), generator=g) - 0.5).cuda()
-    ny = (torch.rand((B, 8, 8, 80), generator=g) - 0.5).cuda()
-    torch.manual_seed(234)
-    net = AutoEncoder().cuda().train().set_compute_dtype(torch.bfloat16)
-    opt = AdamClamp(net.parameters(), lr=1e-4, clip=5.0)
-
-    def step():
-        opt.zero_grad()
-        o = net(x, a, a, *me[:4], noise_z=nz, noise_y=ny)
-        (4096 * o[1] + o[2]).backward()
-
-    grads = {}
-    prev = ag.SIDE_REDUCE, ag.SIDE_WGRAD
-    try:
-        for mode in (0, 1, 2):
-            ag.SIDE_REDUCE, ag.SIDE_WGRAD = mode >= 1, mode == 2
-            step()
-            torch.cuda.synchronize()
-            assert not ag._SIDE_MAIN and not ag._SIDE_KEEP, "side stream not joined"
-            grads[mode] = opt.flat_grad.clone()
-        assert torch.equal(grads[1], grads[0])
-        assert torch.equal(grads[2], grads[0])
-        names = {id(p): n for n, p in net.named_parameters()}
-        for mode in (0, 1, 2):
-            ag.SIDE_REDUCE, ag.SIDE_WGRAD = mode >= 1, mode == 2
-            cap = torch.cuda.Stream()
-            cap.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(cap):
-                step()
-            torch.cuda.current_stream().wait_stream(cap)
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                step()
-            bad = []
-            for rep in range(3):
-                opt.flat_grad.fill_(float("nan"))
-                graph.replay()
-                torch.cuda.synchronize()
-                for p, (off, k) in zip(opt.params, opt.offsets):
-                    d = (opt.flat_grad[off:off + k] - grads[0][off:off + k]).abs().max().item()
-                    if not d == 0.0:
-                        bad.append((rep, names.get(id(p)), d))
-            del graph
-            assert not bad, (mode, bad[:12])
-    finally:
-        ag.SIDE_REDUCE, ag.SIDE_WGRAD = prev
-
-
 def test_prefetch_frag_packs_equal_element_gather():
     """prefetch_packs' two launches (plain packs + biases gathered from the fp32 parameters,
     then the fragment-major copies as 16-byte chunk copies of the plain packs) give every
@@ -1127,3 +1065,40 @@ def test_prefetch_frag_packs_equal_element_gather():
                 assert torch.equal(want.view(torch.int16), tp.frag.view(torch.int16))
                 n += 1
     assert n > 10
+
+
+def test_gdn_reparam_fn_bit_identical_to_torch_lowerbound():
+    """rgbac.autograd.GdnReparamFn (one HIP launch each way) against the reference's torch
+    graph LowerBound(p, bound) ** 2 - pedestal (layers/GDN.py:9-23, 71-78): forward values and
+    parameter gradients bit-identical, with parameters below their bounds and gradients of
+    both signs (LowerBound's pass-through rule), stored and added into an attached .grad."""
+    from rgbac.autograd import GdnReparamFn
+    from rgbac.layers.GDN import GDN, LowerBound
+    torch.manual_seed(5)
+    g = GDN(96).cuda()
+    with torch.no_grad():
+        g.beta.copy_(torch.rand(96) * 2e-3)                    # some below beta_bound (~1e-3)
+        g.gamma.copy_(torch.randn(96, 96).abs() * 1e-3 - 2e-4)  # some below gamma_bound
+    db_out = torch.randn(96, device="cuda")
+    dg_out = torch.randn(96, 96, device="cuda")
+
+    def torch_path(beta, gamma):
+        b = LowerBound.apply(beta, g.beta_bound) ** 2 - g.pedestal
+        gm = LowerBound.apply(gamma, g.gamma_bound) ** 2 - g.pedestal
+        return b, gm
+
+    for direct in (False, True):
+        res = {}
+        for name, fn in (("torch", torch_path),
+                         ("hip", lambda b, gm: GdnReparamFn.apply(b, gm, g.beta_bound,
+                                                                  g.gamma_bound, g.pedestal))):
+            beta = g.beta.detach().clone().requires_grad_(True)
+            gamma = g.gamma.detach().clone().requires_grad_(True)
+            if direct:
+                beta.grad = torch.full_like(beta, 0.25)
+                gamma.grad = torch.full_like(gamma, -0.5)
+            b, gm = fn(beta, gamma)
+            torch.autograd.backward([b, gm], [db_out, dg_out])
+            res[name] = (b.detach(), gm.detach(), beta.grad.clone(), gamma.grad.clone())
+        for t, h in zip(res["torch"], res["hip"]):
+            assert torch.equal(t, h), (direct, (t - h).abs().max().item())
