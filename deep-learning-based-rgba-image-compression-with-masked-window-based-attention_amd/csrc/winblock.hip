@@ -64,10 +64,10 @@ struct WinBlockArgs {
   const bf16_t* x; long long ldx;
   const float* alpha;                    // (B, H, W) fp32 when masked
   const bf16_t* wq;                      // [4 pairs][54][64 lanes][8]
-  const float* bqkv;                     // [576]
+  const float* bqkv;                     // [576] (ws 4) | the ws-8 bias pack [5][256]
   const bf16_t* wp;                      // [2 pair pairs][12 m][3 k-steps][64][8] (permuted k)
-  const float* bproj;                    // [192]
-  const float* table;                    // relative_position_bias_table [225][8]
+  const float* bproj;                    // [80] (ws 4) | the ws-8 bias pack (row 0 = bproj)
+  const float* table;                    // [49][8] (ws 4) | the ws-8 per-pair pack [4][1024]
   bf16_t* out; long long ldo;
 };
 
@@ -195,16 +195,17 @@ __global__ void __launch_bounds__(512, 1) winblock_v2_kernel(const WinBlockArgs 
       X[ks] = pix < 0 ? make_uint4(0, 0, 0, 0) : *reinterpret_cast<const uint4*>(row + 32 * ks + 8 * qq);
   }
 
-  // ---- tables (in log2 units: softmax runs on exp2): global reads issued before the gather
+  // ---- tables (in log2 units: softmax runs on exp2; the host's per-pair pack [var][head][225],
+  // the shift mask's -100 folded into var 1) -> [var][8 heads][225]: global reads issued before
+  // the gather
   float* tb = reinterpret_cast<float*>(sm + L_TB);
-  for (int e = tid; e < 225 * 8; e += 512) {           // table [225][8] -> [var][8][225]
-    const int idx = e >> 3, hd = e & 7;
-    const float v = a.table[e];
-    tb[hd * 225 + idx] = v * LOG2E;
-    tb[8 * 225 + hd * 225 + idx] = (v + -100.0f) * LOG2E;   // the shift mask's -100 folded in
+  for (int e = tid; e < 2 * 8 * 225; e += 512) {
+    const int var = e >= 8 * 225 ? 1 : 0, rem = e - 8 * 225 * var;
+    const int hd = rem / 225, idx = rem - 225 * hd;
+    tb[e] = a.table[(hd >> 1) * 1024 + var * 450 + (hd & 1) * 225 + idx];
   }
   float* bq = reinterpret_cast<float*>(sm + L_BQ);
-  for (int e = tid; e < 192; e += 512) bq[e] = a.bproj[e];
+  for (int e = tid; e < 192; e += 512) bq[e] = a.bproj[e];   // the bias pack's row 0
 
   // ---- window gather: token -> pixel (cyclic shift folded in), shifted-frame region id
   if (tid < 2) act_s[tid] = a.masked ? 0 : 1;
@@ -294,9 +295,9 @@ __global__ void __launch_bounds__(512, 1) winblock_v2_kernel(const WinBlockArgs 
       float bv[3];
 #pragma unroll
       for (int t = 0; t < 3; ++t) {
-        bq4[t] = *reinterpret_cast<const float4*>(a.bqkv + 48 * p + 16 * t + 4 * qq);
-        bk4[t] = *reinterpret_cast<const float4*>(a.bqkv + 192 + 48 * p + 16 * t + 4 * qq);
-        bv[t] = a.bqkv[384 + 48 * p + 16 * t + n];
+        bq4[t] = *reinterpret_cast<const float4*>(a.bqkv + 256 * (1 + p) + 16 * t + 4 * qq);
+        bk4[t] = *reinterpret_cast<const float4*>(a.bqkv + 256 * (1 + p) + 48 + 16 * t + 4 * qq);
+        bv[t] = a.bqkv[256 * (1 + p) + 96 + 16 * t + n];
       }
 #pragma unroll
       for (int ks = 0; ks < 6; ++ks) {
@@ -490,17 +491,16 @@ constexpr int L_X = L_WQ + WQF * 1024;                 // 55296: x [win 2][token
 constexpr int L_K = L_X + 48 * 1024;                   // 104448: K [win 2][head 2][key tile 4]
 constexpr int L_V = L_K + 16 * 1024;                   // 120832: V^T [win 2][channel tile 3][key pair 2]
 constexpr int L_Q = L_V + 12 * 1024;                   // 133120: q^T [win 2][head 2][token tile 4]
-constexpr int L_TB = L_Q + 16 * 1024;                  // 149504: bias [var 2][head 2][225] fp32
-constexpr int L_BQ = L_TB + 2 * 2 * 225 * 4;           // 153104: [bq 48 | bk 48 | bv 48] (1 KiB piece)
-constexpr int L_LA = L_BQ + 1024;                      // 154128: this workgroup's active windows
+constexpr int L_TB = L_Q + 16 * 1024;                  // 149504: bias [var 2][head 2][225] fp32 (4 KiB)
+constexpr int L_BQ = L_TB + 4 * 1024;                  // 153600: [bq 48 | bk 48 | bv 48] (1 KiB piece)
+constexpr int L_LA = L_BQ + 1024;                      // 154624: this workgroup's active windows
 constexpr int MAXA = 256;
-constexpr int L_LC = L_LA + MAXA * 2;                  // 154640: its inactive windows
+constexpr int L_LC = L_LA + MAXA * 2;                  // 155136: its inactive windows
 constexpr int MAXC = 64;
-constexpr int L_MS = L_LC + MAXC * 2;                  // 154768: scan partials [8]
-constexpr int LDS_A = L_MS + 64;                       // 154832
+constexpr int L_MS = L_LC + MAXC * 2;                  // 155264: scan partials [8]
+constexpr int LDS_A = L_MS + 64;                       // 155328
 static_assert(LDS_A <= 160 * 1024, "LDS");
-// prologue staging, free until the first x DMA: the launch's flags at L_X (8 KiB), the raw
-// table [225][8] (padded to 8 KiB) at L_X + 8 KiB
+// prologue staging, free until the first x DMA: the launch's flags at L_X (<= 8 KiB)
 // winproj_kernel
 constexpr int P_WP = 0;                                // all proj fragments [u][m][s]
 constexpr int P_O = P_WP + WPF * 1024;                 // 73728: O^T [buf 2][token tile 4][k-step 6]
@@ -520,7 +520,7 @@ struct WinBlock3Args {
   const bf16_t* wq;                      // [4 pairs][54][64 lanes][8]
   const float* bias;                     // [5][256]: bproj | pair p: bq, bk, bv (48 each)
   const bf16_t* wp;                      // [2][12][3][64][8] (permuted k)
-  const float* table;                    // relative_position_bias_table [225][8], padded to 2048
+  const float* table;                    // [4 pairs][1024]: [var 2][head 2][225] in log2 units
   bf16_t* out; long long ldo;
   unsigned long long* oscr;              // [windows][4 token tiles][6 k-steps][64 lanes][2]
   int* alist;                            // [windows]: active rank -> window (per launch at w0)
@@ -566,24 +566,30 @@ __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlock3Args a)
   const int tt = w & 3, hr = w >> 2;                   // token tile; role and attention head
   WB_T(0);
 
-  // ---- prologue DMA: three staging pieces per wave (flags, raw table, the pair's biases),
-  // then the pair's qkv panel (pieces past the end repeat the last one: same bytes, same place)
+  // ---- prologue DMA, two staging pieces per wave (the launch's flags, the pair's bias table
+  // and biases), then the pair's qkv panel.  Pieces past the end repeat the last one (same
+  // bytes, same place).  The panel pieces start at a per-slot rotation: the 32 workgroups of
+  // an XCD would otherwise request the same lines in the same order (one L2 channel at a time).
+  const int nflag = (a.nwc + 1023) >> 10;              // 1 KiB flag pieces of this launch
 #pragma unroll
-  for (int i = 0; i < 3; ++i) {
+  for (int i = 0; i < 2; ++i) {
     int k = w + 8 * i;
-    if (k > 16) k = 16;
+    if (k > nflag + 4) k = nflag + 4;
     const void* src;
     int dst;
-    if (k < 8) { src = a.flags + a.w0 + k * 1024 + lane * 16; dst = L_X + k * 1024; }
-    else if (k < 16) { src = a.table + (k - 8) * 256 + lane * 4; dst = L_X + 8192 + (k - 8) * 1024; }
+    if (k < nflag) { src = a.flags + a.w0 + k * 1024 + lane * 16; dst = L_X + k * 1024; }
+    else if (k < nflag + 4) { src = a.table + 1024 * p + (k - nflag) * 256 + lane * 4; dst = L_TB + (k - nflag) * 1024; }
     else { src = a.bias + 256 * (1 + p) + lane * 4; dst = L_BQ; }
     wb_dma16(src, lds0 + dst);
   }
   const bf16_t* wqp = a.wq + (size_t)p * WQF * 512;
+  const int rot = ((g >> 5) * 7) % WQF;
 #pragma unroll
   for (int i = 0; i < 7; ++i) {
     int f = w + 8 * i;
     if (f >= WQF) f = WQF - 1;
+    f += rot;
+    if (f >= WQF) f -= WQF;
     wb_dma16(wqp + ((size_t)f * 64 + lane) * 8, lds0 + L_WQ + f * 1024);
   }
   wb_wait_vm<7>();                                     // the staging pieces landed
@@ -612,16 +618,6 @@ __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlock3Args a)
     if (lane >= d) inc += y;
   }
   if (lane == 63) ms[w] = inc;
-  {                                                    // table [225][8] -> [var][head][225]
-    const float* raw = reinterpret_cast<const float*>(sm + L_X + 8192);
-    float* tb = reinterpret_cast<float*>(sm + L_TB);
-    for (int e = tid; e < 2 * 225; e += 512) {
-      const int hh = e >= 225 ? 1 : 0, idx = e - 225 * hh;
-      const float v = raw[idx * 8 + 2 * p + hh];
-      tb[hh * 225 + idx] = v * LOG2E;
-      tb[2 * 225 + hh * 225 + idx] = (v + -100.0f) * LOG2E;   // the shift mask's -100 folded in
-    }
-  }
   __syncthreads();
   int nact = 0, before = 0;
 #pragma unroll
@@ -672,13 +668,19 @@ __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlock3Args a)
   wb_wait_all();                                       // qkv panel and the first windows' x
   __syncthreads();
 
-  // relative-position-bias offsets of this lane's S^T elements (key 16 kt + 4 qq + r, query
-  // 16 tt + n) in this wave's head's table: idx(kt, r) = idx(3, 3) + 30 (3 - kt) + 3 - r, so
-  // one base per lane plus immediates; cut bit 4 kt + r selects the "- 100" copy where the
-  // shift mask separates query and key
+  // relative-position bias of this lane's S^T elements (key 16 kt + 4 qq + r, query 16 tt + n)
+  // for this wave's head, held in registers for the launch: idx(kt, r) = idx(3, 3) +
+  // 30 (3 - kt) + 3 - r; the "- 100" copy (bcut) where the shift mask separates query and key
   const int iq = 16 * tt + n;
   const int tbase = L_TB + hr * 900 +
                     4 * (((iq >> 3) - 6 - (qq >> 1) + 7) * 15 + ((iq & 7) - 4 * (qq & 1) - 3 + 7));
+  float breg[16], bcut[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int off = tbase + 4 * (30 * (3 - (e >> 2)) + 3 - (e & 3));
+    breg[e] = *reinterpret_cast<const float*>(sm + off);
+    bcut[e] = shift > 0 ? *reinterpret_cast<const float*>(sm + off + 1800) : 0.0f;
+  }
   auto make_cut = [&](int wg) -> unsigned {
     if (shift == 0) return 0u;
     const int rem = wg % nwimg;
@@ -804,70 +806,113 @@ __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlock3Args a)
     }
   };
 
-  // attention of head 2p + hr, query tile tt, window slot v (global window wg): O^T to the
-  // window's slot of the workspace (channel tile 3p + c is half (3p + c) & 1 of the proj's
-  // k-step (3p + c) >> 1)
-  auto attend = [&](int v, int wg) {
-    const uint4 qf = *reinterpret_cast<const uint4*>(sm + L_Q + (v * 8 + hr * 4 + tt) * 1024 + lane * 16);
-    const unsigned cutm = make_cut(wg);
-    f32x4 s[4];
+  // attention of head 2p + hr, query tile tt, for NWIN windows (global windows wg[v]) phase by
+  // phase, so the windows' independent chains interleave: O^T to each window's slot of the
+  // workspace (channel tile 3p + c is half (3p + c) & 1 of the proj's k-step (3p + c) >> 1);
+  // two store instructions per window
+  auto attend = [&](auto nw_c, int wg0, int wg1) {
+    constexpr int NWIN = decltype(nw_c)::value;
+    const int wgv[2] = {wg0, wg1};
+    f32x4 s[NWIN][4];
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt) {
-      const uint4 kf = *reinterpret_cast<const uint4*>(sm + L_K + ((v * 2 + hr) * 4 + kt) * 1024 + lane * 16);
-      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      mma_step<bf16_t>(s[kt], kf, qf);
+    for (int v = 0; v < NWIN; ++v) {
+      const uint4 qf = *reinterpret_cast<const uint4*>(sm + L_Q + (v * 8 + hr * 4 + tt) * 1024 + lane * 16);
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt) {
+        const uint4 kf = *reinterpret_cast<const uint4*>(sm + L_K + ((v * 2 + hr) * 4 + kt) * 1024 + lane * 16);
+        s[v][kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        mma_step<bf16_t>(s[v][kt], kf, qf);
+      }
     }
+    unsigned cutm[NWIN];
+#pragma unroll
+    for (int v = 0; v < NWIN; ++v) cutm[v] = make_cut(wgv[v]);
     // + B_rel + shift mask, softmax over the 64 keys (lane + lanes ^16, ^32, ^48)
-    float mx = -INFINITY;
+    float mx[NWIN], sum[NWIN];
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
+    for (int v = 0; v < NWIN; ++v) {
+      mx[v] = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int off = tbase + 4 * (30 * (3 - kt) + 3 - r) + (((cutm >> (4 * kt + r)) & 1u) ? 1800 : 0);
-        const float val = s[kt][r] + *reinterpret_cast<const float*>(sm + off);
-        s[kt][r] = val;
-        mx = fmaxf(mx, val);
-      }
-    mx = pair16_max(mx);
-    mx = pair32_max(mx);
-    float sum = 0.f;
+      for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float ex = __builtin_amdgcn_exp2f(s[kt][r] - mx);
-        s[kt][r] = ex;
-        sum += ex;
-      }
-    sum = pair16_sum(sum);
-    sum = pair32_sum(sum);
-    const float inv = __builtin_amdgcn_rcpf(sum);
-    uint4 pf[2];                                       // P^T key pairs (0,1), (2,3)
-#pragma unroll
-    for (int kp = 0; kp < 2; ++kp) {
-      f32x4 a0 = s[2 * kp], a1 = s[2 * kp + 1];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) { a0[r] *= inv; a1[r] *= inv; }
-      pf[kp] = cat2(pk4(a0), pk4(a1));
+        for (int r = 0; r < 4; ++r) {
+          const float val = s[v][kt][r] + (((cutm[v] >> (4 * kt + r)) & 1u) ? bcut[4 * kt + r] : breg[4 * kt + r]);
+          s[v][kt][r] = val;
+          mx[v] = fmaxf(mx[v], val);
+        }
     }
-    uint2* dst = reinterpret_cast<uint2*>(a.oscr + (size_t)wg * OSLOT);
 #pragma unroll
-    for (int ci = 0; ci < 2; ++ci) {
-      const int c = hr + ci;
-      f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int v = 0; v < NWIN; ++v) mx[v] = pair16_max(mx[v]);
+#pragma unroll
+    for (int v = 0; v < NWIN; ++v) mx[v] = pair32_max(mx[v]);
+#pragma unroll
+    for (int v = 0; v < NWIN; ++v) {
+      sum[v] = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float ex = __builtin_amdgcn_exp2f(s[v][kt][r] - mx[v]);
+          s[v][kt][r] = ex;
+          sum[v] += ex;
+        }
+    }
+#pragma unroll
+    for (int v = 0; v < NWIN; ++v) sum[v] = pair16_sum(sum[v]);
+#pragma unroll
+    for (int v = 0; v < NWIN; ++v) sum[v] = pair32_sum(sum[v]);
+#pragma unroll
+    for (int v = 0; v < NWIN; ++v) {
+      const float inv = __builtin_amdgcn_rcpf(sum[v]);
+      uint4 pf[2];                                     // P^T key pairs (0,1), (2,3)
 #pragma unroll
       for (int kp = 0; kp < 2; ++kp) {
-        uint4 vf = *reinterpret_cast<const uint4*>(sm + L_V + ((v * 3 + c) * 2 + kp) * 1024 + lane * 16);
-        if (c == 1) {
-          const uint32_t keep = hr == 0 ? lo8 : ~lo8;
-          vf.x &= keep; vf.y &= keep; vf.z &= keep; vf.w &= keep;
-        }
-        mma_step<bf16_t>(o, vf, pf[kp]);
+        f32x4 a0 = s[v][2 * kp], a1 = s[v][2 * kp + 1];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) { a0[r] *= inv; a1[r] *= inv; }
+        pf[kp] = cat2(pk4(a0), pk4(a1));
       }
-      const int ct = 3 * p + c;
-      if (c != 1 || (hr == 0 ? qq < 2 : qq >= 2))
-        dst[((tt * 6 + (ct >> 1)) * 64 + lane) * 2 + (ct & 1)] = pk4(o);
+      uint2* dst = reinterpret_cast<uint2*>(a.oscr + (size_t)wgv[v] * OSLOT);
+#pragma unroll
+      for (int ci = 0; ci < 2; ++ci) {
+        const int c = hr + ci;
+        f32x4 o = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kp = 0; kp < 2; ++kp) {
+          uint4 vf = *reinterpret_cast<const uint4*>(sm + L_V + ((v * 3 + c) * 2 + kp) * 1024 + lane * 16);
+          if (c == 1) {
+            const uint32_t keep = hr == 0 ? lo8 : ~lo8;
+            vf.x &= keep; vf.y &= keep; vf.z &= keep; vf.w &= keep;
+          }
+          mma_step<bf16_t>(o, vf, pf[kp]);
+        }
+        const int ct = 3 * p + c;
+        if (c != 1 || (hr == 0 ? qq < 2 : qq >= 2))
+          dst[((tt * 6 + (ct >> 1)) * 64 + lane) * 2 + (ct & 1)] = pk4(o);
+      }
     }
+  };
+
+  // inactive windows: out = x (MASKSEL, :236-240), 64 tokens x 24 chunks of 16 bytes, 3 per
+  // thread; one window per pair iteration rides under the attention (loads after the exchange
+  // barrier, stores after the attention), the rest follow the loop
+  uint4 cv0, cv1, cv2;
+  long long cp0 = 0, cp1 = 0, cp2 = 0;
+  const int ce0 = tid, ce1 = tid + 512, ce2 = tid + 1024;
+  const int ct0 = ce0 / 24, ct1 = ce1 / 24, ct2 = ce2 / 24;
+  const int cc0 = 8 * (ce0 - 24 * ct0), cc1 = 8 * (ce1 - 24 * ct1), cc2 = 8 * (ce2 - 24 * ct2);
+  auto copy_load = [&](int wg) {
+    cp0 = wb_win_pix(wg, ct0, H, W, nwx, nwimg, shift);
+    cp1 = wb_win_pix(wg, ct1, H, W, nwx, nwimg, shift);
+    cp2 = wb_win_pix(wg, ct2, H, W, nwx, nwimg, shift);
+    cv0 = *reinterpret_cast<const uint4*>(a.x + cp0 * a.ldx + cc0);
+    cv1 = *reinterpret_cast<const uint4*>(a.x + cp1 * a.ldx + cc1);
+    cv2 = *reinterpret_cast<const uint4*>(a.x + cp2 * a.ldx + cc2);
+  };
+  auto copy_store = [&]() {
+    *reinterpret_cast<uint4*>(a.out + cp0 * a.ldo + cc0) = cv0;
+    *reinterpret_cast<uint4*>(a.out + cp1 * a.ldo + cc1) = cv1;
+    *reinterpret_cast<uint4*>(a.out + cp2 * a.ldo + cc2) = cv2;
   };
 
   for (int i = 0; i < npair; ++i) {
@@ -882,30 +927,33 @@ __global__ void __launch_bounds__(512, 1) winblock_kernel(const WinBlock3Args a)
       const int nb = 2 * i + 3 < nmine ? 2 * i + 3 : 2 * i + 2;
       dma_x(a.w0 + la[2 * i + 2], a.w0 + la[nb]);
     }
-    attend(0, wa);
-    if (two) attend(1, wb);
+    const bool cp = i < ncopy;                         // wave-uniform
+    if (cp) copy_load(a.w0 + lc[i]);
+    if (two) attend(std::integral_constant<int, 2>{}, wa, wb);
+    else attend(std::integral_constant<int, 1>{}, wa, wa);
+    if (cp) copy_store();
     WB_T(5 + 4 * (i < 2 ? i : 2));
-    wb_wait_all();                                     // the next windows' x landed
+    // the next windows' x landed (the O^T stores issued after it may still be in flight:
+    // two store instructions per window)
+    if (two) wb_wait_vm<4>();
+    else wb_wait_vm<2>();
     __syncthreads();                                   // exchange free; x visible
     WB_T(6 + 4 * (i < 2 ? i : 2));
   }
   WB_T(15);
 
-  // ---- inactive windows: out = x (MASKSEL, :236-240), 64 tokens x 24 chunks of 16 bytes
-  for (int c = 0; c < ncopy; ++c) {
-    const int wg = a.w0 + lc[c];
-    const int e0 = tid, e1 = tid + 512, e2 = tid + 1024;
-    const int t0 = e0 / 24, t1 = e1 / 24, t2 = e2 / 24;
-    const long long p0 = wb_win_pix(wg, t0, H, W, nwx, nwimg, shift);
-    const long long p1 = wb_win_pix(wg, t1, H, W, nwx, nwimg, shift);
-    const long long p2 = wb_win_pix(wg, t2, H, W, nwx, nwimg, shift);
-    const int c0 = 8 * (e0 - 24 * t0), c1 = 8 * (e1 - 24 * t1), c2 = 8 * (e2 - 24 * t2);
-    const uint4 v0 = *reinterpret_cast<const uint4*>(a.x + p0 * a.ldx + c0);
-    const uint4 v1 = *reinterpret_cast<const uint4*>(a.x + p1 * a.ldx + c1);
-    const uint4 v2 = *reinterpret_cast<const uint4*>(a.x + p2 * a.ldx + c2);
-    *reinterpret_cast<uint4*>(a.out + p0 * a.ldo + c0) = v0;
-    *reinterpret_cast<uint4*>(a.out + p1 * a.ldo + c1) = v1;
-    *reinterpret_cast<uint4*>(a.out + p2 * a.ldo + c2) = v2;
+  // the inactive windows left: two at a time (six loads in flight per thread)
+  for (int c = npair; c < ncopy; c += 2) {
+    copy_load(a.w0 + lc[c]);
+    if (c + 1 < ncopy) {
+      const uint4 a0 = cv0, a1 = cv1, a2 = cv2;
+      const long long q0 = cp0, q1 = cp1, q2 = cp2;
+      copy_load(a.w0 + lc[c + 1]);
+      *reinterpret_cast<uint4*>(a.out + q0 * a.ldo + cc0) = a0;
+      *reinterpret_cast<uint4*>(a.out + q1 * a.ldo + cc1) = a1;
+      *reinterpret_cast<uint4*>(a.out + q2 * a.ldo + cc2) = a2;
+    }
+    copy_store();
   }
   wb_wait_all();                                       // no LDS-DMA in flight at exit
   WB_T(17);
@@ -947,9 +995,11 @@ __global__ void __launch_bounds__(512, 1) winproj_kernel(const WinBlock3Args a) 
   int r = blockIdx.x;
   int wg = r < nact ? a.alist[a.w0 + r] : 0;
   if (r < nact) dma_o(wg, 0);
+  const int rot = ((blockIdx.x >> 3) * 5) % WPF;       // per-workgroup start (see winblock_kernel)
 #pragma unroll
   for (int i = 0; i < 9; ++i) {
-    const int f = w + 8 * i;
+    int f = w + 8 * i + rot;
+    if (f >= WPF) f -= WPF;
     wb_dma16(a.wp + ((size_t)f * 64 + lane) * 8, lds0 + P_WP + f * 1024);
   }
   wb_dma16(a.bias + lane * 4, lds0 + P_BP);
@@ -1218,35 +1268,14 @@ extern "C" int rgbac_debug_wb_times(unsigned long long* host, int nblocks) {
 }
 #endif
 
-extern "C" int rgbac_winattn_block_v2(int batch, int h, int w, int shift, int masked, float scale,
-                                   const void* x, int64_t ldx, const float* alpha,
-                                   const void* wq_packed, const float* bqkv,
-                                   const void* wp_packed, const float* bproj, const float* table,
-                                   void* out, int64_t ldo, void* stream) {
-  RGBAC_REQUIRE(batch > 0 && h > 0 && w > 0 && h % 8 == 0 && w % 8 == 0,
-                "H and W must be positive multiples of the window size 8");
-  RGBAC_REQUIRE(shift >= 0 && shift < 8, "0 <= shift < 8");
-  RGBAC_REQUIRE(x && out && wq_packed && bqkv && wp_packed && bproj && table, "null pointer");
-  RGBAC_REQUIRE(!masked || alpha, "masked attention needs alpha");
-  RGBAC_REQUIRE(ldx >= 192 && ldo >= 192 && ldx % 8 == 0 && ldo % 8 == 0, "strides");
-  RGBAC_REQUIRE(x != out, "out must not alias x");
-  const long long windows = (long long)batch * (h / 8) * (w / 8);
-  RGBAC_REQUIRE(windows < (1LL << 30), "too many windows");
-  RGBAC_REQUIRE((long long)batch * h * w < (1LL << 31), "pixel index must fit in 31 bits");
-  WinBlockArgs d;
-  d.batch = batch; d.H = h; d.W = w; d.shift = shift; d.masked = masked; d.scale = scale;
-  d.x = reinterpret_cast<const bf16_t*>(x); d.ldx = ldx; d.alpha = alpha;
-  d.wq = reinterpret_cast<const bf16_t*>(wq_packed); d.bqkv = bqkv;
-  d.wp = reinterpret_cast<const bf16_t*>(wp_packed); d.bproj = bproj; d.table = table;
-  d.out = reinterpret_cast<bf16_t*>(out); d.ldo = ldo;
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(winblock_v2_kernel),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, wb::LDS);
-    attr = true;
-  }
-  const dim3 grid((int)((windows + 1) / 2));
-  hipLaunchKernelGGL(winblock_v2_kernel, grid, dim3(512), wb::LDS, reinterpret_cast<hipStream_t>(stream), d);
+
+// the round-3 single-kernel form (winblock_v2_kernel) over the same packs: one workgroup per
+// window pair streaming all four head pairs' weights; the faster form while one round of
+// workgroups covers the windows
+static int launch_winblock_v2(const WinBlockArgs& d, long long windows, hipStream_t st) {
+  static unsigned long long attr = 0;
+  lds_optin(reinterpret_cast<const void*>(winblock_v2_kernel), wb::LDS, &attr);
+  hipLaunchKernelGGL(winblock_v2_kernel, dim3((unsigned)((windows + 1) / 2)), dim3(512), wb::LDS, st, d);
   return check_launch("winblock_v2_kernel");
 }
 
@@ -1304,6 +1333,19 @@ extern "C" int rgbac_winattn_block(int batch, int h, int w, int shift, int maske
   d.alist = reinterpret_cast<int*>(wk + lay.alist);
   d.acount = reinterpret_cast<int*>(wk + lay.acount);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // form: the round-3 kernel below 2,048 windows (one round of workgroups, whose chain the
+  // persistent pair is not shorter than), the head-pair kernels above; RGBAC_WINBLOCK_FORM=2|3
+  // forces one (A/B and the bit-identity tests; read per call, host side only)
+  const char* fe = getenv("RGBAC_WINBLOCK_FORM");
+  const int form = (fe && fe[0] == '2') ? 2 : (fe && fe[0] == '3') ? 3 : (nwin < 2048 ? 2 : 3);
+  if (form == 2) {
+    RGBAC_REQUIRE(nwin < (1LL << 30), "too many windows");
+    WinBlockArgs v;
+    v.batch = batch; v.H = h; v.W = w; v.shift = shift; v.masked = masked; v.scale = scale;
+    v.x = d.x; v.ldx = ldx; v.alpha = alpha; v.wq = d.wq; v.bqkv = bias_pack;
+    v.wp = d.wp; v.bproj = bias_pack; v.table = table_pad; v.out = d.out; v.ldo = ldo;
+    return launch_winblock_v2(v, nwin, st);
+  }
   if (masked) {
     const long long blocks = (nwin + 3) / 4;
     RGBAC_REQUIRE(blocks < (1LL << 31), "too many windows");

@@ -493,27 +493,22 @@ int rgbac_gdn_reparam_bwd(int nb, int ng, const float* beta, const float* gamma,
  * [4][54][64][8]; wp [2][12][3][64][8] in the kernel's accumulator-operand k order: element e
  * of lane l in k-step s of pair-pair u is input channel 96u + 32s + 4(l >> 4) + (e & 3) +
  * 16(e >> 2)); bias_pack: fp32 [5][256] = bproj (192) | per head pair p: qkv.bias rows
- * 48p.., 192 + 48p.., 384 + 48p.. (48 each), zero padded; table_pad: relative_position_bias_table
- * [225][8] fp32 zero-padded to 2048 floats.  work: device workspace of at least
+ * 48p.., 192 + 48p.., 384 + 48p.. (48 each), zero padded; table_pad: fp32 [4][1024], per head
+ * pair p [var 2][head 2][225] = (relative_position_bias_table[:, 2p + head] (- 100 for var 1))
+ * * log2(e) in fp32, zero padded.  work: device workspace of at least
  * rgbac_winattn_block_workspace(batch, h, w) bytes, 256-byte aligned (no initial contents
- * needed).  Launches per 8,192 windows: one flag pass (masked only, once), the persistent
- * head-pair kernel (qkv + attention of one head pair over a share of the active windows, O
- * to the workspace, inactive windows copied) and the proj kernel over the compacted active
- * windows.  Replaces the qkv GEMM, rgbac_winattn_core_ex and the MASKSEL proj GEMM of one
- * WinBasedAttention call. */
+ * needed).  Two bit-identical forms, chosen by the window count: below 2,048 windows one
+ * launch of the round-3 kernel (one workgroup per window pair, all four head pairs' weights
+ * streamed through its LDS); from 2,048 on, per 8,192 windows: one flag pass (masked only),
+ * the persistent head-pair kernel (qkv + attention of one head pair over a share of the
+ * active windows, O to the workspace, inactive windows copied) and the proj kernel over the
+ * compacted active windows (env RGBAC_WINBLOCK_FORM=2|3 forces a form).  Replaces the qkv
+ * GEMM, rgbac_winattn_core_ex and the MASKSEL proj GEMM of one WinBasedAttention call. */
 int64_t rgbac_winattn_block_workspace(int batch, int h, int w);
 int rgbac_winattn_block(int batch, int h, int w, int shift, int masked, float scale,
                         const void* x, int64_t ldx, const float* alpha, const void* wq_packed,
                         const float* bias_pack, const void* wp_packed, const float* table_pad,
                         void* out, int64_t ldo, void* work, int64_t work_bytes, void* stream);
-
-/* The round-3 single-kernel form of the same block (winblock_v2_kernel: one workgroup per
- * window pair streaming all four head pairs' weights), kept for the A/B against
- * rgbac_winattn_block until it is measured out: bqkv [576], bproj [192], table [225][8]. */
-int rgbac_winattn_block_v2(int batch, int h, int w, int shift, int masked, float scale,
-                           const void* x, int64_t ldx, const float* alpha, const void* wq_packed,
-                           const float* bqkv, const void* wp_packed, const float* bproj,
-                           const float* table, void* out, int64_t ldo, void* stream);
 
 /* The same block at window 4, C = 80, 8 heads of 10 (the 1/16-resolution attention blocks,
  * layers/TransformRGB.py:63,80): one wave per window, every product after the qkv GEMM in

@@ -135,11 +135,12 @@ def test_winattn_block_fused_matches_unfused_and_oracle(device, C, ws, B, H, W, 
         assert torch.equal(got[:, :, ws:H // 2, ws:W // 2], xb[:, :, ws:H // 2, ws:W // 2])
 
 
-# The head-pair ws-8 block (round 6): per-window flags (winflag_kernel), device-side
-# compaction and one head pair per persistent workgroup (winblock_kernel), the proj over the
-# compacted list (winproj_kernel).  It keeps every product and rounding point of the round-3
-# kernel (winblock_v2_kernel), so the two are compared bit for bit, over repeated calls on one
-# workspace.  B 3 at 512^2 (12,288 windows) spans two launches of at most 8,192 windows.
+# The head-pair ws-8 block (round 6, rgbac_winattn_block's form for >= 2,048 windows): per-window
+# flags (winflag_kernel), device-side compaction and one head pair per persistent workgroup
+# (winblock_kernel), the proj over the compacted list (winproj_kernel).  It keeps every product
+# and rounding point of the round-3 kernel (winblock_v2_kernel, the form below 2,048 windows),
+# so the two forms (RGBAC_WINBLOCK_FORM=3 / 2) are compared bit for bit, over repeated calls on
+# one workspace.  B 3 at 512^2 (12,288 windows) spans two launches of at most 8,192 windows.
 @pytest.mark.parametrize("B,H,W,shift,alpha_kind", [
     (8, 64, 64, 0, "bench"), (2, 64, 64, 4, "quarter"), (1, 32, 48, 0, "ones"),
     (1, 24, 40, 4, "quarter"), (2, 16, 16, 0, "zeros"), (1, 8, 8, 0, "one_pixel"),
@@ -175,13 +176,14 @@ def test_winblock_head_pair_kernel_bit_identical(device, B, H, W, shift, alpha_k
     with torch.no_grad():
         f = rt.to_nhwc(xg, torch.bfloat16)
         outs = []
-        for _ in range(3):                            # repeated calls on one workspace
-            outs.append(rt.to_nchw(m.attn.run_block(f, ag, shift, m.masked)).float())
-        os.environ["RGBAC_WINBLOCK_V2"] = "1"
         try:
+            os.environ["RGBAC_WINBLOCK_FORM"] = "3"
+            for _ in range(3):                        # repeated calls on one workspace
+                outs.append(rt.to_nchw(m.attn.run_block(f, ag, shift, m.masked)).float())
+            os.environ["RGBAC_WINBLOCK_FORM"] = "2"
             ref_out = rt.to_nchw(m.attn.run_block(f, ag, shift, m.masked)).float()
         finally:
-            os.environ.pop("RGBAC_WINBLOCK_V2", None)
+            os.environ.pop("RGBAC_WINBLOCK_FORM", None)
     for o in outs:
         assert torch.equal(o, ref_out), (o - ref_out).abs().max().item()
     if alpha_kind == "zeros":

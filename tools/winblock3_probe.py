@@ -1,5 +1,5 @@
 """Time the ws-8 window-attention block: the head-pair kernel (winblock_kernel + winflag_kernel,
-round 6) against the round-3 kernel (RGBAC_WINBLOCK_V2=1), each as N calls captured in one HIP
+round 6, RGBAC_WINBLOCK_FORM=3) against the round-3 kernel (=2), each as N calls captured in one HIP
 graph and replayed, on the bench's alpha pyramid level at the block's resolution (config 2:
 B 8, 64^2; config 4: B 4, 256^2).  Prints us per call and TF/s on active-window FLOPs.
 python tools/winblock3_probe.py [--configs 2,4] [--calls 50] [--reps 5]"""
@@ -45,9 +45,9 @@ def main():
         fl = nact * 64 * FLOP_PER_TOKEN
         for var in args.variants.split(","):
             if var == "v2":
-                os.environ["RGBAC_WINBLOCK_V2"] = "1"
+                os.environ["RGBAC_WINBLOCK_FORM"] = "2"
             else:
-                os.environ.pop("RGBAC_WINBLOCK_V2", None)
+                os.environ["RGBAC_WINBLOCK_FORM"] = "3"
             with torch.no_grad():
                 for _ in range(3):
                     m.nhwc(x, alpha)
@@ -76,7 +76,7 @@ def main():
                   f"{fl / us / 1e6:7.1f} TF/s active-window ({fl / us / 1e6 / 25:.1f} % of 2.5 PF)",
                   flush=True)
             del g
-    os.environ.pop("RGBAC_WINBLOCK_V2", None)
+    os.environ.pop("RGBAC_WINBLOCK_FORM", None)
 
 
 if __name__ == "__main__":
