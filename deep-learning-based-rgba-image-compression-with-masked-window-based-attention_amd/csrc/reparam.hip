@@ -51,6 +51,84 @@ __global__ void __launch_bounds__(256) gdn_reparam_bwd_kernel(
   }
 }
 
+// EntropyBottleneck parameter block of the training step (compressai EntropyBottleneck,
+// filters (3, 3, 3, 3); rgbac.train_forward.eb_params_t): per channel c the 64-float row
+//   [softplus(_matrix0..4) 33 | _bias0..4 13 | tanh(_factor0..3) 12 | median 1 | 0 x 5]
+// that rgbac_eb_forward / rgbac_eb_bwd read, in one launch each way instead of the softplus /
+// tanh / cat / pad chain and its backward (+ one .grad accumulate per parameter).
+struct EbParamSet {
+  const float* p[15];          // _matrix0..4, _bias0..4, _factor0..3, quantiles
+  float* g[15];                // their gradients (backward)
+};
+__device__ __forceinline__ void eb_col(int j, int& k, int& cnt, int& off, int& op) {
+  // op 0 softplus, 1 identity, 2 tanh, 3 median (quantiles[c][0][1]), 4 zero pad
+  constexpr int CNT[15] = {3, 9, 9, 9, 3, 3, 3, 3, 3, 1, 3, 3, 3, 3, 1};
+  int start = 0;
+  k = 15; cnt = 1; off = 0; op = 4;
+#pragma unroll
+  for (int i = 0; i < 15; ++i) {
+    if (k == 15 && j < start + CNT[i]) {
+      k = i; cnt = CNT[i]; off = j - start;
+      op = i < 5 ? 0 : (i < 10 ? 1 : (i < 14 ? 2 : 3));
+    }
+    start += CNT[i];
+  }
+}
+
+__global__ void __launch_bounds__(256) eb_params_kernel(int C, EbParamSet s, float* out) {
+#pragma clang fp contract(off)
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= C * 64) return;
+  const int c = e >> 6, j = e & 63;
+  int k, cnt, off, op;
+  eb_col(j, k, cnt, off, op);
+  float v = 0.0f;
+  if (op == 3) v = s.p[14][c * 3 + 1];
+  else if (op != 4) {
+    const float x = s.p[k][c * cnt + off];
+    v = op == 0 ? (x > 20.0f ? x : log1pf(expf(x))) : (op == 2 ? tanhf(x) : x);
+  }
+  out[e] = v;
+}
+
+__global__ void __launch_bounds__(256) eb_params_bwd_kernel(int C, EbParamSet s, const float* dout,
+                                                            int accumulate) {
+#pragma clang fp contract(off)
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= C * 64) return;
+  const int c = e >> 6, j = e & 63;
+  int k, cnt, off, op;
+  eb_col(j, k, cnt, off, op);
+  if (op == 4) return;
+  const float g = dout[e];
+  int idx;
+  float gin;
+  if (op == 3) {
+    idx = c * 3 + 1;
+    gin = g;
+  } else {
+    idx = c * cnt + off;
+    const float x = s.p[k][idx];
+    if (op == 0) {                                     // softplus_backward (beta 1, threshold 20)
+      const float z = expf(x);
+      gin = x > 20.0f ? g : (g * z) / (z + 1.0f);
+    } else if (op == 2) {                              // tanh_backward on the output
+      const float y = tanhf(x);
+      const float yy = y * y;
+      gin = g * (1.0f - yy);
+    } else {
+      gin = g;
+    }
+  }
+  float* d = s.g[k];
+  if (accumulate) {
+    const float prev = d[idx];
+    d[idx] = prev + gin;
+  } else {
+    d[idx] = gin;
+  }
+}
+
 }  // namespace rgbac
 
 using namespace rgbac;
@@ -80,4 +158,31 @@ extern "C" int rgbac_gdn_reparam_bwd(int nb, int ng, const float* beta, const fl
                      reinterpret_cast<hipStream_t>(stream), nb, ng, beta, gamma, beta_bound,
                      gamma_bound, dbeta_out, dgamma_out, dbeta, dgamma, accumulate);
   return check_launch("gdn_reparam_bwd_kernel");
+}
+
+extern "C" int rgbac_eb_params(int channels, const float* const* params, float* out, void* stream) {
+  RGBAC_REQUIRE(channels > 0 && params && out, "args");
+  EbParamSet s;
+  for (int i = 0; i < 15; ++i) {
+    RGBAC_REQUIRE(params[i], "null parameter");
+    s.p[i] = params[i];
+    s.g[i] = nullptr;
+  }
+  hipLaunchKernelGGL(eb_params_kernel, dim3((channels * 64 + 255) / 256), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), channels, s, out);
+  return check_launch("eb_params_kernel");
+}
+
+extern "C" int rgbac_eb_params_bwd(int channels, const float* const* params, const float* dout,
+                                   float* const* grads, int accumulate, void* stream) {
+  RGBAC_REQUIRE(channels > 0 && params && dout && grads, "args");
+  EbParamSet s;
+  for (int i = 0; i < 15; ++i) {
+    RGBAC_REQUIRE(params[i] && grads[i], "null parameter or gradient");
+    s.p[i] = params[i];
+    s.g[i] = grads[i];
+  }
+  hipLaunchKernelGGL(eb_params_bwd_kernel, dim3((channels * 64 + 255) / 256), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), channels, s, dout, accumulate);
+  return check_launch("eb_params_bwd_kernel");
 }

@@ -125,6 +125,8 @@ SIGNATURES = {
     "rgbac_winattn_block_workspace": [_I32, _I32, _I32],
     "rgbac_gdn_reparam": [_I32, _I32, _VP, _VP, _F, _F, _F, _VP, _VP, _VP],
     "rgbac_gdn_reparam_bwd": [_I32, _I32, _VP, _VP, _F, _F, _VP, _VP, _VP, _VP, _I32, _VP],
+    "rgbac_eb_params": [_I32, _VP, _VP, _VP],
+    "rgbac_eb_params_bwd": [_I32, _VP, _VP, _VP, _I32, _VP],
     "rgbac_winattn_block_ws4": [_I32, _I32, _I32, _I32, _I32, _F, _VP, _I64, _VP, _VP, _VP, _VP,
                                 _VP, _VP, _VP, _I64, _VP],
     "rgbac_rgba_augment": [_I32, _VP, _I32, _I32, _I32, _VP, _VP, _VP, _VP, _VP],

@@ -634,6 +634,47 @@ class GdnReparamFn(torch.autograd.Function):
         return (db if need_b else None), (dg if need_g else None), None, None, None
 
 
+class EbParamsFn(torch.autograd.Function):
+    """The EntropyBottleneck parameter block of rgbac_eb_forward / rgbac_eb_bwd ([C][64]:
+    softplus(_matrix0..4) | _bias0..4 | tanh(_factor0..3) | median | 0 pad; compressai
+    EntropyBottleneck, filters (3, 3, 3, 3)) from the 15 raw parameters in one HIP launch
+    (rgbac_eb_params), and its backward in one (rgbac_eb_params_bwd: softplus / tanh
+    derivatives, added straight into attached fp32 .grad tensors as DIRECT_GRAD does)."""
+
+    @staticmethod
+    def forward(ctx, C, *params):
+        ps = [t.detach() for t in params]
+        assert len(ps) == 15 and all(t.dtype == _F32 and t.is_contiguous() for t in ps)
+        out = torch.empty((C, 64), dtype=_F32, device=ps[0].device)
+        arr = (ctypes.c_void_p * 15)(*[t.data_ptr() for t in ps])
+        _lib.call("rgbac_eb_params", C, ctypes.cast(arr, ctypes.c_void_p), out.data_ptr(),
+                  _lib.stream_ptr(out.device))
+        ctx.C = C
+        ctx.save_for_backward(*params)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        params = ctx.saved_tensors
+        if dout is None:
+            return (None,) * 16
+        accs = [_direct_grad(t) if ctx.needs_input_grad[1 + i] else None
+                for i, t in enumerate(params)]
+        direct = all(a is not None for a in accs)
+        if direct:
+            grads = accs
+        else:
+            grads = [torch.empty_like(t) for t in params[:14]] + [torch.zeros_like(params[14])]
+        dout = dout.contiguous()
+        pa = (ctypes.c_void_p * 15)(*[t.data_ptr() for t in params])
+        ga = (ctypes.c_void_p * 15)(*[g.data_ptr() for g in grads])
+        _lib.call("rgbac_eb_params_bwd", ctx.C, ctypes.cast(pa, ctypes.c_void_p), dout.data_ptr(),
+                  ctypes.cast(ga, ctypes.c_void_p), 1 if direct else 0, _lib.stream_ptr(dout.device))
+        if direct:
+            return (None,) * 16
+        return (None, *[g if ctx.needs_input_grad[1 + i] else None for i, g in enumerate(grads)])
+
+
 class Sink:
     """Gradient buffer of one autograd-tracked training activation (a ConvFn / CatFn output).
     Consumers that know the protocol (ConvFn sources and residual operands, CatFn parts) add
@@ -1221,8 +1262,10 @@ class GaussFn(Function):
         if direct and ysink.buf is None:
             ysink.buf, ysink.own, ysink.slices = torch.zeros_like(y_t), True, True
         dy = Feat(ysink.buf if direct else torch.zeros_like(y_t), Cy)
-        dmu = Feat(torch.zeros_like(mu_t), cs)
-        dsc = Feat(torch.zeros_like(sc_t), cs)
+        # rgbac_gaussian_bwd writes every (pixel, channel < cs) element: no zero fill unless
+        # the tensors carry pad channels
+        dmu = Feat(torch.empty_like(mu_t) if mu_t.shape[-1] == cs else torch.zeros_like(mu_t), cs)
+        dsc = Feat(torch.empty_like(sc_t) if sc_t.shape[-1] == cs else torch.zeros_like(sc_t), cs)
         gb = (dbits if dbits is not None else torch.zeros((), device=dev)).float().reshape(1)
         dh = None if dhat is None else Feat(dhat.contiguous(), cs)
         _lib.call("rgbac_gaussian_bwd", _lib.dtype_code(y_t.dtype), npix, cs, y.ptr(coff), y.ldc,

@@ -187,9 +187,16 @@ def mask_seq_t(seq, x):
 
 
 def eb_params_t(eb):
-    """The [C][64] param block of rgbac_eb_forward with autograd to the raw parameters
-    (softplus / tanh chained by torch on O(C) tensors)."""
+    """The [C][64] param block of rgbac_eb_forward with autograd to the raw parameters: one
+    HIP launch each way (rgbac.autograd.EbParamsFn) for compressai's filters (3, 3, 3, 3);
+    other filter sets chain softplus / tanh in torch."""
     C = eb.channels
+    if tuple(eb.filters) == (3, 3, 3, 3):
+        ps = ([getattr(eb, f"_matrix{i}") for i in range(5)] +
+              [getattr(eb, f"_bias{i}") for i in range(5)] +
+              [getattr(eb, f"_factor{i}") for i in range(4)] + [eb.quantiles])
+        if all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() for t in ps):
+            return ag.EbParamsFn.apply(C, *ps)
     parts = [F.softplus(getattr(eb, f"_matrix{i}")).reshape(C, -1) for i in range(5)]
     parts += [getattr(eb, f"_bias{i}").reshape(C, -1) for i in range(5)]
     parts += [torch.tanh(getattr(eb, f"_factor{i}")).reshape(C, -1) for i in range(4)]
@@ -207,12 +214,12 @@ def latent_t(model, y, training, noise_z=None, noise_y=None):
     nz = None
     if training:
         nz = (noise_z.contiguous().float() if noise_z is not None else
-              torch.rand((z.B, z.H, z.W, z.C), device=dev) - 0.5)
+              torch.empty((z.B, z.H, z.W, z.C), device=dev).uniform_(-0.5, 0.5))
     zh_t, zbits = ag.EBFn.apply(z.t, z.C, eb_params_t(model.entropy_bottleneck), nz)
     z_hat = Feat(zh_t, z.C)
     scales = _seq_t(model.h_scale_s, z_hat)
     means = _seq_t(model.h_mean_s, z_hat)
-    yh, ybits = [], None
+    yh, ybits = [], []
     for i in range(ns):
         sup = yh if msup < 0 else yh[:msup]
         ms = ag.cat_t([means] + sup)
@@ -222,15 +229,16 @@ def latent_t(model, y, training, noise_z=None, noise_y=None):
         nyi = None
         if training:
             nyi = (noise_y[..., i * cs:(i + 1) * cs].contiguous().float() if noise_y is not None
-                   else torch.rand((y.B, y.H, y.W, cs), device=dev) - 0.5)
+                   else torch.empty((y.B, y.H, y.W, cs), device=dev).uniform_(-0.5, 0.5))
         hat, bits = ag.gauss_t(y, i * cs, mu, sc, nyi)
         lrp = model.lrp_transforms[i]
         lsup = ag.cat_t([ms, hat])
         t = conv_t(lrp[0], [lsup], act="gelu", defer=True)
         t = conv_t(lrp[2], [t], act="gelu", defer=True)
         yh.append(conv_t(lrp[4], [t], act="tanh_half", res1=hat))
-        ybits = bits if ybits is None else ybits + bits
-    return ag.cat_t(yh), ybits, zbits
+        ybits.append(bits)
+    # the slices' bits summed in one reduction (torch.stack + sum) instead of nine adds
+    return ag.cat_t(yh), torch.stack(ybits).sum(), zbits
 
 
 def rgb_forward_train(model, input, mask, reconmask, me2, me3, noise_z=None, noise_y=None):

@@ -482,6 +482,16 @@ int rgbac_gdn_reparam_bwd(int nb, int ng, const float* beta, const float* gamma,
                           const float* dgamma_out, float* dbeta, float* dgamma, int accumulate,
                           void* stream);
 
+/* EntropyBottleneck parameter block (compressai EntropyBottleneck, filters (3, 3, 3, 3)):
+ * params = the 15 fp32 parameters _matrix0..4, _bias0..4, _factor0..3, quantiles ([C][1][3]);
+ * out [channels][64] = softplus(_matrix0..4) (33) | _bias0..4 (13) | tanh(_factor0..3) (12) |
+ * quantiles[c][0][1] | 0 x 5 -- the block rgbac_eb_forward / rgbac_eb_bwd read.  The
+ * backward maps dout to the 15 gradients (softplus / tanh derivatives; quantiles: the median
+ * entry only), stored (accumulate == 0; quantiles' other entries untouched) or added. */
+int rgbac_eb_params(int channels, const float* const* params, float* out, void* stream);
+int rgbac_eb_params_bwd(int channels, const float* const* params, const float* dout,
+                        float* const* grads, int accumulate, void* stream);
+
 /* Fused masked shifted-window attention block, bf16, window 8, C = 192, 8 heads
  * (reference: layers/masked_win_attention.py:96-131 WindowAttention.forward, :169-251
  * WinBasedAttention.forward).  out = x + proj(attn(x)) on windows whose alpha is non-zero

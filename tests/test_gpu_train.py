@@ -1102,3 +1102,43 @@ def test_gdn_reparam_fn_bit_identical_to_torch_lowerbound():
             res[name] = (b.detach(), gm.detach(), beta.grad.clone(), gamma.grad.clone())
         for t, h in zip(res["torch"], res["hip"]):
             assert torch.equal(t, h), (direct, (t - h).abs().max().item())
+
+
+def test_eb_params_fn_matches_torch_chain():
+    """rgbac.autograd.EbParamsFn (one HIP launch each way) against the torch chain it replaces
+    (softplus / tanh / cat / pad of the EntropyBottleneck parameters, compressai filters
+    (3, 3, 3, 3)): the [C][64] block bit-identical; the 15 parameter gradients within fp32
+    rounding of torch's (softplus / tanh backward), stored and added into an attached .grad."""
+    import torch.nn.functional as Fn
+    from rgbac.autograd import EbParamsFn
+    from rgbac.entropy import EntropyBottleneck
+    torch.manual_seed(6)
+    eb = EntropyBottleneck(192).cuda()
+    with torch.no_grad():
+        for p in eb.parameters():
+            p.add_(torch.randn_like(p) * 0.5)
+    names = ([f"_matrix{i}" for i in range(5)] + [f"_bias{i}" for i in range(5)] +
+             [f"_factor{i}" for i in range(4)] + ["quantiles"])
+    dout = torch.randn(192, 64, device="cuda")
+
+    def torch_chain(ps):
+        C = 192
+        parts = [Fn.softplus(ps[i]).reshape(C, -1) for i in range(5)]
+        parts += [ps[5 + i].reshape(C, -1) for i in range(5)]
+        parts += [torch.tanh(ps[10 + i]).reshape(C, -1) for i in range(4)]
+        parts.append(ps[14][:, :, 1:2].reshape(C, 1))
+        return Fn.pad(torch.cat(parts, dim=1), (0, 64 - 59)).contiguous()
+
+    for direct in (False, True):
+        res = {}
+        for name, fn in (("torch", torch_chain), ("hip", lambda ps: EbParamsFn.apply(192, *ps))):
+            ps = [getattr(eb, n).detach().clone().requires_grad_(True) for n in names]
+            if direct:
+                for p in ps:
+                    p.grad = torch.full_like(p, 0.125)
+            out = fn(ps)
+            out.backward(dout)
+            res[name] = (out.detach(), [p.grad.clone() for p in ps])
+        assert torch.equal(res["torch"][0], res["hip"][0])
+        for gt, gh in zip(res["torch"][1], res["hip"][1]):
+            assert torch.allclose(gt, gh, rtol=2e-6, atol=1e-7), (direct, (gt - gh).abs().max().item())
