@@ -1228,17 +1228,14 @@ __global__ void __launch_bounds__(256, 2) conv_smallk_kernel(const ConvArgsDev a
 
 template <int NT, int NKS>
 static void launch_smallk_nt(const ConvArgsDev& d, int ny, int nz, hipStream_t st) {
-  static int per_cu = -1, ncu = 0;
+  static int per_cu = -1;                            // a property of the kernel
   auto kern = conv_smallk_kernel<NT, NKS>;
   if (per_cu < 0) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess ||
         per_cu < 1)
       per_cu = 1;
-    if (ncu < 1) ncu = 256;
   }
+  const int ncu = device_cus();
   const int ntile = (d.s.M + 31) / 32;
   int gx = (ncu * per_cu + ny * nz - 1) / (ny * nz);
   const int need = (ntile + 3) / 4;
@@ -1632,7 +1629,7 @@ __global__ void __launch_bounds__(512, 2) conv_pw2_kernel(const ConvArgsDev args
         case RGBAC_ACT_DLRELU: PW2_EPI(RGBAC_ACT_DLRELU); break;
         default: PW2_EPI(-1); break;
       }
-#undef PW2_EPI      }
+#undef PW2_EPI
     }
     if (nt < ntile) wait_vm<0>();
   }
@@ -1646,18 +1643,9 @@ template <int NKS, bool DACT>
 static void launch_pw_k(const ConvArgsDev& d, hipStream_t st) {
   auto kern = conv_pw_kernel<NKS, DACT>;
   constexpr size_t lds = (size_t)192 * 4 * NKS * 16;
-  static bool attr = false;
-  static int ncu = 0;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu < 1) ncu = 256;
-    (void)hipGetLastError();
-    attr = true;
-  }
+  static unsigned long long attr = 0;                 // per device
+  lds_optin((const void*)kern, (int)lds, &attr);
+  const int ncu = device_cus();
   const int nz = d.s.ngroups;
   const int ntile = (d.s.M + 15) / 16;
   int gx = (2 * ncu + nz - 1) / nz;
@@ -1671,18 +1659,9 @@ template <int NKS>
 static void launch_pw2_k(const ConvArgsDev& d, hipStream_t st) {
   auto kern = conv_pw2_kernel<NKS>;
   constexpr size_t lds = ((size_t)192 * 4 * NKS + 8 * 16 * 24) * 16;
-  static bool attr = false;
-  static int ncu = 0;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu < 1) ncu = 256;
-    (void)hipGetLastError();
-    attr = true;
-  }
+  static unsigned long long attr = 0;                 // per device
+  lds_optin((const void*)kern, (int)lds, &attr);
+  const int ncu = device_cus();
   const int nz = d.s.ngroups;
   const int ntile = (d.s.M + 15) / 16;
   int gx = (ncu + nz - 1) / nz;
@@ -1957,17 +1936,10 @@ static void launch_npatch(const ConvArgsDev& d, int max_cout, hipStream_t st) {
   const size_t red = (size_t)8 * tn * 4 * 64 * 16;
   const size_t lds = ((patch > red ? patch : red) + 1023) & ~(size_t)1023;
   const dim3 grid((unsigned)((long long)d.s.batch * (d.s.Hm / 4) * (d.s.Wm / 16)), 1, d.s.ngroups);
-  static bool attr = false;
-  if (!attr) {
-    // (below 160 KiB: the kernel also holds a few static LDS words, and a rejected attribute
-    // call would leave its error for the launch check)
-    (void)hipFuncSetAttribute((const void*)conv_npatch_kernel<1>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
-    (void)hipFuncSetAttribute((const void*)conv_npatch_kernel<2>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
-    (void)hipGetLastError();
-    attr = true;
-  }
+  // (below 160 KiB: the kernel also holds a few static LDS words); per device
+  static unsigned long long attr1 = 0, attr2 = 0;
+  lds_optin((const void*)conv_npatch_kernel<1>, 128 * 1024, &attr1);
+  lds_optin((const void*)conv_npatch_kernel<2>, 128 * 1024, &attr2);
   if (tn == 2) hipLaunchKernelGGL(conv_npatch_kernel<2>, grid, dim3(512), lds, st, d);
   else hipLaunchKernelGGL(conv_npatch_kernel<1>, grid, dim3(512), lds, st, d);
 }
@@ -2151,17 +2123,14 @@ static void launch_wstream(const ConvArgsDev& d, hipStream_t st) {
 // cached per kernel), evened out so every block gets the same number of tiles (+-1).
 template <typename T, int BM, int BN, int WGM, int WGN, int NBUF>
 static void launch_pers(const ConvArgsDev& d, int ntile, int nz, hipStream_t st) {
-  static int per_cu = -1, ncu = 0;
+  static int per_cu = -1;                            // a property of the kernel
   auto kern = conv_pers_kernel<T, BM, BN, WGM, WGN, NBUF>;
   if (per_cu < 0) {
-    int dev = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 256, 0) != hipSuccess ||
         per_cu < 1)
       per_cu = 1;
-    if (ncu < 1) ncu = 256;
   }
+  const int ncu = device_cus();
   int cap = (ncu * per_cu + nz - 1) / nz;
   if (cap < 1) cap = 1;
   const int rounds = (ntile + cap - 1) / cap;
@@ -2945,23 +2914,15 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
 #define RGBAC_FP1(TH_, BN_, C_)                                                               \
   do {                                                                                        \
     auto k_ = conv_fpatch_kernel<TH_, BN_, 4, 4, C_>;                                         \
-    static bool attr_ = false;                                                                \
-    if (!attr_) {                                                                             \
-      (void)hipFuncSetAttribute((const void*)k_, hipFuncAttributeMaxDynamicSharedMemorySize,  \
-                                160 * 1024);                                                  \
-      attr_ = true;                                                                           \
-    }                                                                                         \
+    static unsigned long long attr_ = 0;                                                      \
+    lds_optin((const void*)k_, 160 * 1024, &attr_);                                          \
     hipLaunchKernelGGL(k_, grid, dim3(256), lds, st, d);                                      \
   } while (0)
 #define RGBAC_FPK(TH_, BN_, NW_, C_)                                                          \
   do {                                                                                        \
     auto k_ = conv_fpatch_kernel<TH_, BN_, NW_, 4, C_, 3>;                                    \
-    static bool attr_ = false;                                                                \
-    if (!attr_) {                                                                             \
-      (void)hipFuncSetAttribute((const void*)k_, hipFuncAttributeMaxDynamicSharedMemorySize,  \
-                                160 * 1024);                                                  \
-      attr_ = true;                                                                           \
-    }                                                                                         \
+    static unsigned long long attr_ = 0;                                                      \
+    lds_optin((const void*)k_, 160 * 1024, &attr_);                                          \
     hipLaunchKernelGGL(k_, grid, dim3(64 * NW_ * 3), lds, st, d);                             \
   } while (0)
 #define RGBAC_FPKS(TH_, BN_, NW_)                                                             \

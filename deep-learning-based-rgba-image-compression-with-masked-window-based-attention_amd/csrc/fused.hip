@@ -924,13 +924,7 @@ extern "C" int rgbac_residual_unit_ex(const rgbac_ru_args* args, int ngroups, in
     const long long tiles = (long long)a->batch * (a->h / 8) * (a->w / 8);
     RGBAC_REQUIRE(tiles < (1ll << 31), "too many tiles");
     // one workgroup per CU over all groups (a workgroup stages its group's weights once)
-    static int ncu = 0;
-    if (ncu == 0) {
-      int dev = 0;
-      (void)hipGetDevice(&dev);
-      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-      if (ncu < 1) ncu = 256;
-    }
+    const int ncu = device_cus();
     long long gx = ncu / ngroups;
     if (gx < 1) gx = 1;
     const char* dual_env = getenv("RGBAC_RU_SMALL_DUAL");

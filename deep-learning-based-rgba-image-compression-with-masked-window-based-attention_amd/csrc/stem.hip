@@ -279,13 +279,7 @@ extern "C" int rgbac_stem_gdn(int batch, int in_h, int in_w, const void* x, int6
                 "16-byte alignment");
   const long long M = (long long)batch * ((in_h + 1) / 2) * ((in_w + 1) / 2);
   RGBAC_REQUIRE(M < (1ll << 31), "too many output pixels");
-  static int ncu = 0;
-  if (ncu == 0) {
-    int dev = 0;
-    (void)hipGetDevice(&dev);
-    (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (ncu < 1) ncu = 256;
-  }
+  const int ncu = device_cus();
   const long long ntile = (M + 31) / 32;
   long long g = (ntile + kStemNW - 1) / kStemNW;
   if (g > ncu) g = ncu;

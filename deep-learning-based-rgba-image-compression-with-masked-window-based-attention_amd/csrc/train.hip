@@ -2591,12 +2591,8 @@ static void launch_attn_bwd_mfma(dim3 grid, hipStream_t st, int batch, int h, in
                                  const void* dout, int64_t ldo, void* dqkv, int64_t lddq,
                                  float* bias_partial, const float* amask, int amask_nw) {
   constexpr int bytes = wbwd::Lay<T, DH>::BYTES;
-  static const bool attr = [] {                   // > 64 KiB of dynamic LDS for f32
-    hipFuncSetAttribute(reinterpret_cast<const void*>(winattn_bwd_mfma_kernel<T, WS, DH>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-    return true;
-  }();
-  (void)attr;
+  static unsigned long long attr = 0;             // > 64 KiB of dynamic LDS for f32; per device
+  lds_optin(reinterpret_cast<const void*>(winattn_bwd_mfma_kernel<T, WS, DH>), bytes, &attr);
   hipLaunchKernelGGL((winattn_bwd_mfma_kernel<T, WS, DH>), grid, dim3(256), bytes, st, batch, h, w,
                      channels, heads, shift, masked, scale, (const T*)qkv, ldq, alpha, bias,
                      (const T*)dout, ldo, (T*)dqkv, lddq, bias_partial, amask, amask_nw);

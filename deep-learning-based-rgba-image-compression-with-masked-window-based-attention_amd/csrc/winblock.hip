@@ -1408,14 +1408,11 @@ extern "C" int rgbac_winattn_block_ws4(int batch, int h, int w, int shift, int m
   }();
   // enough workgroups for every CU before more windows per weight fetch
   const int nw = nw_env ? nw_env : (windows >= 2048 ? 4 : 2);
-  static bool attr = false;
-  if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(winblock4_kernel<1>), hipFuncAttributeMaxDynamicSharedMemorySize, wb4::LDS);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(winblock4_kernel<2>), hipFuncAttributeMaxDynamicSharedMemorySize, wb4::LDS);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(winblock4_kernel<4>), hipFuncAttributeMaxDynamicSharedMemorySize, wb4::LDS);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(winblock4_kernel<8>), hipFuncAttributeMaxDynamicSharedMemorySize, wb4::LDS);
-    attr = true;
-  }
+  static unsigned long long attr[4] = {0, 0, 0, 0};      // per device (lds_optin)
+  lds_optin(reinterpret_cast<const void*>(winblock4_kernel<1>), wb4::LDS, &attr[0]);
+  lds_optin(reinterpret_cast<const void*>(winblock4_kernel<2>), wb4::LDS, &attr[1]);
+  lds_optin(reinterpret_cast<const void*>(winblock4_kernel<4>), wb4::LDS, &attr[2]);
+  lds_optin(reinterpret_cast<const void*>(winblock4_kernel<8>), wb4::LDS, &attr[3]);
   const long long grid = (windows + nw - 1) / nw;
   RGBAC_REQUIRE(grid < (1LL << 31), "too many windows");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);

@@ -31,6 +31,7 @@ Steps from then on issue the same collectives in the same order on every rank,
 so a step can be captured in a HIP graph (RCCL collectives are stream-ordered).
 """
 import atexit
+import contextlib
 import ctypes
 import os
 import sys
@@ -41,6 +42,20 @@ import torch
 import torch.distributed as dist
 
 from . import _lib
+
+
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """Route file descriptor 1 to 2 while RCCL initialises: librccl prints its version banner
+    to stdout, where it would land in front of bench.py's one JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
 
 
 class RcclComm:
@@ -104,7 +119,8 @@ class RcclComm:
                                f"({err if err is not None else 'a peer failed to load it'})")
         uid = torch.zeros(128, dtype=torch.uint8)
         if rank == 0:
-            _lib.call("rgbac_comm_unique_id", ctypes.c_void_p(uid.data_ptr()))
+            with _stdout_to_stderr():
+                _lib.call("rgbac_comm_unique_id", ctypes.c_void_p(uid.data_ptr()))
         if self.world > 1:
             src = dist.get_global_rank(group, 0) if group is not None else 0
             u = uid.to(device) if dist.get_backend(group) == "nccl" else uid
@@ -113,8 +129,9 @@ class RcclComm:
         comm = ctypes.c_void_p()
         err = None
         try:
-            _lib.call("rgbac_comm_init", ctypes.c_void_p(uid.data_ptr()), self.world, rank,
-                      device.index, ctypes.byref(comm))
+            with _stdout_to_stderr():
+                _lib.call("rgbac_comm_init", ctypes.c_void_p(uid.data_ptr()), self.world, rank,
+                          device.index, ctypes.byref(comm))
         except RuntimeError as e:
             err = e
         # an init that returned an error on one rank: every rank gives the path up together

@@ -212,9 +212,16 @@ def latent_t(model, y, training, noise_z=None, noise_y=None):
     cs = y.C // ns
     z = _seq_t(model.h_a, y)
     nz = None
+    draw = None
+    if training and (noise_z is None or noise_y is None):
+        # every drawn noise tensor of the step (z, then the ns y slices) from ONE uniform_
+        # launch; each is a contiguous view of it
+        zn = z.B * z.H * z.W * z.C if noise_z is None else 0
+        sn = y.B * y.H * y.W * cs if noise_y is None else 0
+        draw = (torch.empty(zn + ns * sn, device=dev).uniform_(-0.5, 0.5), zn, sn)
     if training:
         nz = (noise_z.contiguous().float() if noise_z is not None else
-              torch.empty((z.B, z.H, z.W, z.C), device=dev).uniform_(-0.5, 0.5))
+              draw[0][:draw[1]].view(z.B, z.H, z.W, z.C))
     zh_t, zbits = ag.EBFn.apply(z.t, z.C, eb_params_t(model.entropy_bottleneck), nz)
     z_hat = Feat(zh_t, z.C)
     scales = _seq_t(model.h_scale_s, z_hat)
@@ -228,8 +235,9 @@ def latent_t(model, y, training, noise_z=None, noise_y=None):
         sc = _seq_t(model.cc_scale_transforms[i], ss)
         nyi = None
         if training:
+            o = draw[1] + i * draw[2] if noise_y is None else 0
             nyi = (noise_y[..., i * cs:(i + 1) * cs].contiguous().float() if noise_y is not None
-                   else torch.empty((y.B, y.H, y.W, cs), device=dev).uniform_(-0.5, 0.5))
+                   else draw[0][o:o + draw[2]].view(y.B, y.H, y.W, cs))
         hat, bits = ag.gauss_t(y, i * cs, mu, sc, nyi)
         lrp = model.lrp_transforms[i]
         lsup = ag.cat_t([ms, hat])
