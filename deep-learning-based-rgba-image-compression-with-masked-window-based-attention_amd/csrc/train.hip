@@ -2287,6 +2287,55 @@ gather_multi_kernel(int ntask, const long long* __restrict__ tasks,
   }
 }
 
+// The per-step repack of the bf16 training packs as strided 8-element chunks: every 16-byte
+// chunk of a pack is 1..8 consecutive elements of ONE run of the fp32 parameter with a fixed
+// per-pack stride (a tap's input channels of a conv row, a tap's output channels of an
+// input-gradient row, ...), so the map holds one int32 per chunk instead of one per element
+// (index traffic / 8), and the chunk also goes straight to its slot of the fragment-major copy
+// (no second launch re-reading the plain pack).  Task t = 8 int64 {src, cmap, dst, nchunk,
+// stride, fmap, fdst, 0}; cmap[c] < 0: a zero chunk, else base = bits 0..27, valid elements - 1
+// = bits 28..30; fmap[c] >= 0: the fragment-major chunk it also fills.  A block owns 256
+// chunks, one per thread: every chunk's map load -> gathers -> stores chain in its own lane
+// (eight chunks per thread in a loop serialised eight such chains: 1.5x slower).
+constexpr int kRepackChunks = 256;
+__global__ void __launch_bounds__(256)
+repack_multi_kernel(int ntask, const long long* __restrict__ tasks,
+                    const long long* __restrict__ blk0) {
+  const long long b = blockIdx.x;
+  int lo = 0, hi = ntask - 1;
+  while (lo < hi) {                       // last t with blk0[t] <= b
+    const int mid = (lo + hi + 1) >> 1;
+    if (blk0[mid] <= b) lo = mid; else hi = mid - 1;
+  }
+  const long long* tk = tasks + 8 * lo;
+  const float* src = reinterpret_cast<const float*>(tk[0]);
+  const int* cmap = reinterpret_cast<const int*>(tk[1]);
+  uint4* dst = reinterpret_cast<uint4*>(tk[2]);
+  const long long n = tk[3];
+  const long long stride = tk[4];
+  const int* fmap = reinterpret_cast<const int*>(tk[5]);
+  uint4* fdst = reinterpret_cast<uint4*>(tk[6]);
+  const long long c = (b - blk0[lo]) * kRepackChunks + threadIdx.x;
+  if (c < n) {
+    const int m = cmap[c];
+    const int f = fmap ? fmap[c] : -1;               // (issued with the map load)
+    float v[8];
+    if (m >= 0) {
+      const long long base = m & 0x0FFFFFFF;
+      const int nv = ((m >> 28) & 7) + 1;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = j < nv ? src[base + j * stride] : 0.0f;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = 0.0f;
+    }
+    const uint4 q = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                               pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+    dst[c] = q;
+    if (f >= 0) fdst[f] = q;
+  }
+}
+
 // partial[blk][c] = sum over the block's pixels of x[p][c]   (bias gradients)
 template <typename T>
 __global__ void __launch_bounds__(256)
@@ -2875,6 +2924,16 @@ extern "C" int rgbac_weight_gather_multi(int ntask, const int64_t* tasks, const 
                      reinterpret_cast<const long long*>(tasks),
                      reinterpret_cast<const long long*>(blk0));
   return check_launch("gather_multi_kernel");
+}
+
+extern "C" int rgbac_weight_repack_multi(int ntask, const int64_t* tasks, const int64_t* blk0,
+                                         int64_t nblk, void* stream) {
+  RGBAC_REQUIRE(ntask >= 1 && tasks && blk0, "tasks");
+  RGBAC_REQUIRE(nblk >= 1 && nblk < (1ll << 31), "block count");
+  hipLaunchKernelGGL(repack_multi_kernel, dim3((unsigned)nblk), dim3(256), 0,
+                     reinterpret_cast<hipStream_t>(stream), ntask,
+                     reinterpret_cast<const long long*>(tasks), reinterpret_cast<const long long*>(blk0));
+  return check_launch("repack_multi_kernel");
 }
 
 extern "C" int rgbac_colsum(int dtype, int64_t npix, int channels, const void* x, int64_t ldx,

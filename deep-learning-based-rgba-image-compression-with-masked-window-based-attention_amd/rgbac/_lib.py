@@ -157,6 +157,7 @@ SIGNATURES = {
     "rgbac_channel_copy_multi_ex": [_I32, _I64, _I32, _VP, _VP],
     "rgbac_weight_gather": [_I32, _I64, _VP, _VP, _VP, _VP],
     "rgbac_weight_gather_multi": [_I32, _VP, _VP, _I64, _VP],
+    "rgbac_weight_repack_multi": [_I32, _VP, _VP, _I64, _VP],
     "rgbac_colsum": [_I32, _I64, _I32, _VP, _I64, _I32, _VP, _VP],
     "rgbac_sum_partials": [_I32, _I32, _VP, _VP, _VP],
     # bitstream (GPU symbol/index work + host rANS coder)

@@ -77,6 +77,7 @@ class TPack:
         self.gen = -1                  # rt.PARAM_GEN at that prefetch (an optimizer step bumps it)
         self.frag = self.fidx = None   # fragment-major copy (runtime.frag_weights layout)
         self.fcmap = None              # frag 16-byte chunk -> plain-pack chunk (prefetch_packs)
+        self._chunks = False           # strided-chunk form of the map (chunk_form), once built
 
     def enable_frag(self):
         """Also gather the fragment-major copy the conv_fpatch / conv_npatch tiles read
@@ -104,6 +105,49 @@ class TPack:
         self.src = None                # gather both at the next refresh
         return self
 
+    def chunk_form(self):
+        """(cmap, stride, fmap) for rgbac_weight_repack_multi, or None when the map is not of
+        that form: every 8-element chunk of the bf16 pack is a prefix of 1..8 real elements
+        base + j * stride of the parameter (one stride per pack) followed by padding.  fmap:
+        plain chunk -> fragment-major chunk (the inverse of fcmap), or None without a frag
+        copy."""
+        if self._chunks is not False:
+            return self._chunks
+        self._chunks = None
+        if self.w.dtype != torch.bfloat16 or self.idx.numel() % 8:
+            return None
+        v = self.idx.reshape(-1, 8).to(torch.int64)
+        dev = v.device
+        valid = v >= 0
+        nv = valid.sum(1)
+        j = torch.arange(8, device=dev)
+        if not bool((valid == (j[None, :] < nv[:, None])).all()):
+            return None
+        first = v[:, 0]
+        multi = nv >= 2
+        stride = 1
+        if bool(multi.any()):
+            d = (v[:, 1] - v[:, 0])[multi]
+            stride = int(d[0])
+            if stride <= 0 or not bool((d == stride).all()):
+                return None
+        if not bool(torch.where(valid, v == first[:, None] + j[None, :] * stride, True).all()):
+            return None
+        if int(first.max()) >= (1 << 28):
+            return None
+        cmap = torch.where(nv > 0, first | ((nv - 1).clamp(min=0) << 28),
+                           torch.full_like(first, -1)).to(torch.int32).contiguous()
+        fmap = None
+        if self.frag is not None:
+            fc = self.fcmap.to(torch.int64)
+            sel = fc >= 0
+            if int(torch.unique(fc[sel]).numel()) != int(sel.sum()):
+                return None
+            fmap = torch.full((cmap.numel(),), -1, dtype=torch.int32, device=dev)
+            fmap[fc[sel]] = torch.arange(fc.numel(), device=dev, dtype=torch.int32)[sel]
+        self._chunks = (cmap, stride, fmap)
+        return self._chunks
+
     def refresh(self, weight, bias=None):
         # re-gathered every training step: the optimizer kernel updates parameters in
         # place through raw pointers (no autograd version bump).  prefetch_packs() does
@@ -130,6 +174,8 @@ class TPack:
 
 
 PREFETCH = os.environ.get("RGBAC_PACK_PREFETCH", "1") != "0"
+# RGBAC_REPACK_CHUNKS=0: the element gather + chunk copy pair for every pack (A/B switch)
+REPACK_CHUNKS = os.environ.get("RGBAC_REPACK_CHUNKS", "1") != "0"
 _GATHER_COPY16 = 16          # rgbac_weight_gather_multi task dtype: 16-byte chunk copy
 _PREFETCH = [1]              # current prefetch token (TPack.token == it: gathered this step)
 _TASKS = {}
@@ -161,34 +207,49 @@ def prefetch_packs(model):
     if ent is None or ent[0] != key:
         if torch.cuda.is_current_stream_capturing():
             return                     # no host->device table upload inside a graph capture
-        # launch 1: the plain packs and biases, gathered from the fp32 parameters; launch 2:
-        # the fragment-major copies as 16-byte chunk copies of the plain packs (bf16 rows
-        # just written) -- one element gather from the parameters per packed weight, not two
+        # the bf16 packs whose maps are strided 8-element chunks (all of the RGB model's): ONE
+        # rgbac_weight_repack_multi launch writes each plain pack and its fragment-major copy
+        # from one int32 per chunk.  The rest (biases, fp32 packs, other maps): element gathers
+        # from the fp32 parameters, then the fragment-major copies as 16-byte chunk copies of
+        # the plain packs just written.
+        rrows, rblk0 = [], [0]
         rows, blk0, crows, cblk0 = [], [0], [], [0]
+        keep = []
         for tp in packs:
-            for dst, idx, sp, dt in ((tp.w, tp.idx, tp.src[0], _lib.dtype_code(tp.w.dtype)),
+            cf = tp.chunk_form() if REPACK_CHUNKS else None
+            if cf is not None:
+                cmap, stride, fmap = cf
+                n = cmap.numel()
+                rrows.append([tp.src[0], cmap.data_ptr(), tp.w.data_ptr(), n, stride,
+                              0 if fmap is None else fmap.data_ptr(),
+                              0 if fmap is None else tp.frag.data_ptr(), 0])
+                rblk0.append(rblk0[-1] + -(-n // 256))          # 256 chunks per block
+                keep.append(cf)
+            for dst, idx, sp, dt in ((None if cf is not None else tp.w, tp.idx, tp.src[0],
+                                      _lib.dtype_code(tp.w.dtype)),
                                      (tp.bias, tp.bias_idx, tp.src[1], _lib.F32)):
                 if sp is None or idx is None or dst is None or dst.numel() == 0:
                     continue
                 n = dst.numel()
                 rows.append([sp, idx.data_ptr(), dst.data_ptr(), n, dt])
                 blk0.append(blk0[-1] + -(-n // 2048))
-            if tp.frag is not None and tp.frag.numel():
+            if cf is None and tp.frag is not None and tp.frag.numel():
                 n = tp.fcmap.numel()
                 crows.append([tp.w.data_ptr(), tp.fcmap.data_ptr(), tp.frag.data_ptr(), n,
                               _GATHER_COPY16])
                 cblk0.append(cblk0[-1] + -(-n // 2048))
         dev = packs[0].w.device
         launches = []
-        for rr, bb in ((rows, blk0), (crows, cblk0)):
+        for fn, rr, bb in (("rgbac_weight_repack_multi", rrows, rblk0),
+                           ("rgbac_weight_gather_multi", rows, blk0),
+                           ("rgbac_weight_gather_multi", crows, cblk0)):
             if rr:
-                launches.append((torch.tensor(rr, dtype=torch.int64, device=dev),
+                launches.append((fn, torch.tensor(rr, dtype=torch.int64, device=dev),
                                  torch.tensor(bb, dtype=torch.int64, device=dev), len(rr), bb[-1]))
-        ent = (key, launches)
+        ent = (key, launches, keep)
         _TASKS[id(model)] = ent
-    for tasks, b0, ntask, nblk in ent[1]:
-        _lib.call("rgbac_weight_gather_multi", ntask, tasks.data_ptr(), b0.data_ptr(), nblk,
-                  _lib.stream_ptr(tasks.device))
+    for fn, tasks, b0, ntask, nblk in ent[1]:
+        _lib.call(fn, ntask, tasks.data_ptr(), b0.data_ptr(), nblk, _lib.stream_ptr(tasks.device))
     for tp in packs:
         tp.token, tp.gen = _PREFETCH[0], rt.PARAM_GEN
 

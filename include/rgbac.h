@@ -439,6 +439,16 @@ int rgbac_weight_gather(int dtype, int64_t n, const float* src, const int32_t* i
  * the source chunk (< 0: zeros); a block owns 2048 chunks.                  */
 int rgbac_weight_gather_multi(int ntask, const int64_t* tasks, const int64_t* blk0, int64_t nblk,
                               void* stream);
+/* The bf16 training packs' per-step repack as strided 8-element chunks (replaces the
+ * element gather + 16-byte chunk copy pair of rgbac_weight_gather_multi for maps of that
+ * form): tasks[8*t ..] = {src (const float*), cmap (const int32_t*), dst (16-byte chunks),
+ * nchunk, stride, fmap (const int32_t* or 0), fdst (16-byte chunks or 0), 0} as int64 in
+ * DEVICE memory; cmap[c] < 0: dst[c] = 0, else with base = cmap[c] & 0x0FFFFFFF and
+ * nv = ((cmap[c] >> 28) & 7) + 1, element j of dst[c] = j < nv ? bf16(src[base + j*stride])
+ * : 0; fmap[c] >= 0: fdst[fmap[c]] = dst[c].  Task t owns blocks [blk0[t], blk0[t+1]) of 256
+ * chunks (blk0 as for rgbac_weight_gather_multi).                              */
+int rgbac_weight_repack_multi(int ntask, const int64_t* tasks, const int64_t* blk0, int64_t nblk,
+                              void* stream);
 /* Per-channel sums over pixels into partial[nsplit][channels] (bias grads). */
 int rgbac_colsum(int dtype, int64_t npix, int channels, const void* x, int64_t ldx, int nsplit,
                  float* partial, void* stream);

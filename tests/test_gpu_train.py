@@ -1029,14 +1029,18 @@ def test_reduce_batch_matches_immediate_reductions():
     assert torch.equal(grads[True][0], grads[False][0])
 
 
-def test_prefetch_frag_packs_equal_element_gather():
-    """prefetch_packs' two launches (plain packs + biases gathered from the fp32 parameters,
-    then the fragment-major copies as 16-byte chunk copies of the plain packs) give every
-    fragment-major training pack the same bits as a direct element gather through its own
-    index map (TPack.fidx), after a parameter update too."""
+@pytest.mark.parametrize("chunks", [True, False])
+def test_prefetch_frag_packs_equal_element_gather(chunks, monkeypatch):
+    """prefetch_packs -- the strided-chunk repack (one launch writing every bf16 plain pack and
+    its fragment-major copy, rgbac_weight_repack_multi) or, with RGBAC_REPACK_CHUNKS=0, the
+    element gather + 16-byte chunk copy pair -- gives every training pack (plain and
+    fragment-major) the same bits as a direct element gather through its own index map
+    (TPack.idx / TPack.fidx), after a parameter update too."""
     from rgbac import _lib
     from rgbac import autograd as ag
     from rgbac.models.AutoEncoderRGB_Journal import AutoEncoder
+    monkeypatch.setattr(ag, "REPACK_CHUNKS", chunks)
+    monkeypatch.setattr(ag, "_TASKS", {})
     g = _gen(72)
     B, H, W = 2, 64, 64
     x = (torch.randint(0, 256, (B, 3, H, W), generator=g).float() / 255).cuda()
@@ -1050,21 +1054,39 @@ def test_prefetch_frag_packs_equal_element_gather():
         with torch.no_grad():
             for p in net.parameters():
                 p.add_(torch.randn_like(p) * 1e-3)     # parameters move between steps
+    # scribble over every pack first: the checked bits must come from this prefetch
+    # (the packs prefetch_packs owns: those of the model's own parameters -- GDN's
+    # reparametrised weights are re-gathered by their layer in the forward)
+    pset = {p.data_ptr() for p in net.parameters()}
+    packs = [tp for m in net.modules() for tc in m.__dict__.get("_rgbac_train", {}).values()
+             for tp in list(tc._fw.values()) + list(tc._bw.values())
+             if tp.src is not None and tp.src[0] in pset and (tp.src[1] is None or tp.src[1] in pset)]
+    for tp in packs:
+        tp.w.fill_(7.0)
+        if tp.frag is not None:
+            tp.frag.view(-1).view(torch.int16).copy_(
+                torch.where(tp.fidx.view(-1) >= 0, 7, 0).to(torch.int16))
     ag.prefetch_packs(net)
     torch.cuda.synchronize()
-    n = 0
-    for m in net.modules():
-        for tc in m.__dict__.get("_rgbac_train", {}).values():
-            for tp in list(tc._fw.values()) + list(tc._bw.values()):
-                if tp.frag is None or tp.src is None:
-                    continue
-                want = torch.empty_like(tp.frag)
-                _lib.call("rgbac_weight_gather", _lib.dtype_code(want.dtype), want.numel(),
-                          tp.src[0], tp.fidx.data_ptr(), want.data_ptr(), _lib.stream_ptr())
-                torch.cuda.synchronize()
-                assert torch.equal(want.view(torch.int16), tp.frag.view(torch.int16))
-                n += 1
-    assert n > 10
+    n = nf = nc = 0
+    for tp in packs:
+        nc += int(tp._chunks not in (False, None))
+        want = torch.empty_like(tp.w)
+        _lib.call("rgbac_weight_gather", _lib.dtype_code(want.dtype), want.numel(),
+                  tp.src[0], tp.idx.data_ptr(), want.data_ptr(), _lib.stream_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(want.view(torch.int16), tp.w.view(torch.int16))
+        n += 1
+        if tp.frag is None:
+            continue
+        want = torch.empty_like(tp.frag)
+        _lib.call("rgbac_weight_gather", _lib.dtype_code(want.dtype), want.numel(),
+                  tp.src[0], tp.fidx.data_ptr(), want.data_ptr(), _lib.stream_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(want.view(torch.int16), tp.frag.view(torch.int16))
+        nf += 1
+    assert n > 40 and nf > 10
+    assert (nc == n) if chunks else (nc == 0)
 
 
 def test_gdn_reparam_fn_bit_identical_to_torch_lowerbound():

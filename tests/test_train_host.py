@@ -178,3 +178,55 @@ def test_oracle_lower_bound_gradient_rule():
     assert torch.equal(y.detach(), torch.tensor([0.11, 0.2, 0.11, 0.2]))
     y.backward(torch.tensor([1.0, 1.0, -1.0, -1.0]))
     assert torch.equal(x.grad, torch.tensor([0.0, 1.0, -1.0, -1.0]))
+
+
+# (kind, wshape, stride, segs): the RGB model's pack kinds, incl. the slice stacks' multi-source
+# 3x3 convs and unpadded / padded channel segments
+REPACK_CASES = [
+    ("conv", (24, 120, 3, 3), 1, [(80, 80), (8, 8), (8, 8), (8, 8), (8, 8), (8, 8)]),
+    ("conv", (16, 3, 5, 5), 2, [(3, 8)]),
+    ("conv", (16, 24, 3, 3), 2, [(24, 24)]),
+    ("conv", (12, 20, 1, 1), 1, [(20, 24)]),
+    ("convt", (16, 8, 5, 5), 2, [(16, 16)]),
+    ("convt", (8, 16, 1, 1), 1, [(8, 8)]),
+    ("subpel", (32, 8, 3, 3), 1, [(8, 8)]),
+    ("gdn", (24, 24, 1, 1), 1, [(24, 24)]),
+]
+
+
+@pytest.mark.parametrize("kind,wshape,stride,segs", REPACK_CASES)
+def test_repack_chunk_form_rebuilds_the_gathered_packs(kind, wshape, stride, segs):
+    """rgbac_weight_repack_multi's chunk maps (TPack.chunk_form), emulated: every plain pack
+    and fragment-major copy it writes equals the element gather + chunk copy it replaces."""
+    from rgbac import autograd as ag
+    tc = ag.TrainConv(kind, wshape, stride, segs, torch.device("cpu"))
+    numel = tc.numel
+    src = torch.randn(numel, generator=torch.Generator().manual_seed(numel))
+    metas = [tc.fwd] + list(tc.bwd)
+    for pk, idx in metas:
+        tp = ag.TPack(pk, idx, torch.bfloat16)
+        if ag._frag_eligible(tp):
+            tp.enable_frag()
+        cf = tp.chunk_form()
+        assert cf is not None, "every pack kind of the model has the strided-chunk form"
+        cmap, stride_, fmap = cf
+        want = _gather(src, idx.reshape(-1)).to(torch.bfloat16)
+        # the kernel's arithmetic: base | (nv - 1) << 28, element j < nv = src[base + j*stride]
+        m = cmap.to(torch.int64)
+        base, nv = m & 0x0FFFFFFF, ((m >> 28) & 7) + 1
+        j = torch.arange(8)
+        pos = base[:, None] + j[None, :] * stride_
+        ok = (m[:, None] >= 0) & (j[None, :] < nv[:, None])
+        got = torch.where(ok, src[pos.clamp(0, numel - 1)], torch.zeros(())).to(torch.bfloat16)
+        assert torch.equal(got.reshape(-1), want)
+        if tp.frag is not None:
+            assert fmap is not None
+            frag_want = torch.zeros(tp.frag.numel() // 8, 8, dtype=torch.bfloat16)
+            sel = tp.fcmap >= 0
+            frag_want[sel] = want.reshape(-1, 8)[tp.fcmap[sel].long()]
+            frag_got = torch.zeros_like(frag_want)
+            fs = fmap >= 0
+            frag_got[fmap[fs].long()] = got[fs]
+            assert torch.equal(frag_got, frag_want)
+        else:
+            assert fmap is None
