@@ -1004,8 +1004,10 @@ def conv_t(m, srcs, act="none", act_param=0.0, res0=None, res1=None, res2=None, 
         call.src_sinks = tuple(None if isinstance(f, ActFeat) else _sink(f.t) for f in srcs)
         call.res_sinks = tuple(None if r is None else _sink(r.t) for r in (res0, res1, res2))
         call.zsink = _sink(zsrc)
-    w4 = w if w.dim() == 4 else w.reshape(wshape)
-    out = ConvFn.apply(call, w4, b, None if res0 is None else res0.t,
+    # the weight goes in with its own shape (ConvFn reads it flat through the pack maps): a
+    # Linear's 2-D leaf then takes the DIRECT_GRAD path like a conv's, instead of its reshaped
+    # view's gradient reaching .grad through an autograd-engine add
+    out = ConvFn.apply(call, w, b, None if res0 is None else res0.t,
                        None if res1 is None else res1.t, None if res2 is None else res2.t,
                        sel, zsrc, *[f.t for f in srcs])
     C = tc.cout // 4 if kind == "subpel" else tc.cout

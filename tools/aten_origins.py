@@ -69,6 +69,9 @@ def main():
                     if ("rgbac" in f or "bench.py" in f) and "aten_origins" not in f:
                         site = f"{os.path.basename(f)}:{fr.lineno} {fr.name}"
                         break
+                if site == "?":              # the autograd engine's own ops: name the operand
+                    t0 = dev_args[0]
+                    site = f"? {tuple(t0.shape)} {str(t0.dtype).replace('torch.', '')}"
                 by_site[(name, site)] += 1
                 by_op[name] += 1
             return out
