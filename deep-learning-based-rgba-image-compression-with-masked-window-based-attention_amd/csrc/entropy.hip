@@ -131,13 +131,12 @@ eb_forward_kernel(long long n, int C, const T* __restrict__ z, long long ldz,
 //           cnt = 3 * #(mask > 0)
 //   mode 1: plain (AutoEncoderMask_Journal.py:309): se = sum (xh - x)^2, cnt = #elements
 template <typename T>
-__global__ void __launch_bounds__(256)
-mse_partial_kernel(int mode, int cx, int HW, const float* __restrict__ x, const T* __restrict__ xh,
-                   long long ldh, const float* __restrict__ mask, double* __restrict__ part,
-                   float* __restrict__ xo, int vec) {
+__device__ __forceinline__ void mse_block(int mode, int cx, int HW, const float* __restrict__ x,
+                                          const T* __restrict__ xh, long long ldh,
+                                          const float* __restrict__ mask, double* __restrict__ part,
+                                          float* __restrict__ xo, int vec, double* red) {
   // xo (or null): x_hat's fp32 NCHW copy, written from the same reads (rgbac_finalize_ex).
   // vec (cx <= 4, vector-aligned rows): the pixel's channels arrive in one vector load.
-  __shared__ double red[4];
   const int b = blockIdx.y;
   double se = 0.0, cnt = 0.0;
   for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += gridDim.x * 256) {
@@ -169,19 +168,30 @@ mse_partial_kernel(int mode, int cx, int HW, const float* __restrict__ x, const 
   }
 }
 
+template <typename T>
+__global__ void __launch_bounds__(256)
+mse_partial_kernel(int mode, int cx, int HW, const float* __restrict__ x, const T* __restrict__ xh,
+                   long long ldh, const float* __restrict__ mask, double* __restrict__ part,
+                   float* __restrict__ xo, int vec) {
+  __shared__ double red[4];
+  mse_block<T>(mode, cx, HW, x, xh, ldh, mask, part, xo, vec, red);
+}
+
 constexpr int kFinWaves = 16;   // finalize_kernel: one 1024-thread block
 
-__global__ void __launch_bounds__(64 * kFinWaves)
-finalize_kernel(int mode, int batch, int nblk, double npix, const double* __restrict__ part,
-                const double* __restrict__ yb, int ny, const double* __restrict__ zb, int nz,
-                float* __restrict__ out) {
-  // One block; every reduction is a wave reduction (shuffles, no barrier) and the waves'
-  // results meet once in LDS, combined in wave order (fixed order: deterministic).  Wave w owns
-  // images w, w + 16, ...  The bits partials are summed four independent chains per thread
-  // (their loads in flight together: a single dependent chain over the 1024^2 frame's 20k
-  // partials was 37 us of load latencies), the chains then added in a fixed order.
-  constexpr int NT = 64 * kFinWaves;
-  __shared__ double wred[kFinWaves][5];
+// The finalisation of one forward by the NW waves of one block: every reduction is a wave
+// reduction (shuffles, no barrier) and the waves' results meet once in LDS, combined in wave
+// order (fixed order: deterministic).  Wave w owns images w, w + NW, ...  The bits partials are
+// summed four independent chains per thread (their loads in flight together: a single dependent
+// chain over the 1024^2 frame's 20k partials was 37 us of load latencies), the chains then added
+// in a fixed order.
+template <int NW>
+__device__ __forceinline__ void finalize_body(int mode, int batch, int nblk, double npix,
+                                              const double* __restrict__ part,
+                                              const double* __restrict__ yb, int ny,
+                                              const double* __restrict__ zb, int nz,
+                                              float* __restrict__ out, double (*wred)[5]) {
+  constexpr int NT = 64 * NW;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   double ya[4] = {0.0, 0.0, 0.0, 0.0}, za[4] = {0.0, 0.0, 0.0, 0.0};
   for (int i0 = threadIdx.x; i0 < ny; i0 += 4 * NT) {
@@ -205,7 +215,7 @@ finalize_kernel(int mode, int batch, int nblk, double npix, const double* __rest
     zs += __shfl_xor(zs, o);
   }
   double mse_acc = 0.0, se_all = 0.0, cnt_all = 0.0;
-  for (int b = wave; b < batch; b += kFinWaves) {
+  for (int b = wave; b < batch; b += NW) {
     double se = 0.0, cnt = 0.0;
     for (int i = lane; i < nblk; i += 64) {
       se += part[((size_t)b * nblk + i) * 2 + 0];
@@ -231,7 +241,7 @@ finalize_kernel(int mode, int batch, int nblk, double npix, const double* __rest
 #pragma unroll
     for (int k = 0; k < 5; ++k) {
       t[k] = 0.0;
-      for (int w = 0; w < kFinWaves; ++w) t[k] += wred[w][k];
+      for (int w = 0; w < NW; ++w) t[k] += wred[w][k];
     }
     float mse;
     if (mode == 0)
@@ -245,6 +255,55 @@ finalize_kernel(int mode, int batch, int nblk, double npix, const double* __rest
     out[2] = yb_pp;
     out[3] = zb_pp;
   }
+}
+
+__global__ void __launch_bounds__(64 * kFinWaves)
+finalize_kernel(int mode, int batch, int nblk, double npix, const double* __restrict__ part,
+                const double* __restrict__ yb, int ny, const double* __restrict__ zb, int nz,
+                float* __restrict__ out) {
+  __shared__ double wred[kFinWaves][5];
+  finalize_body<kFinWaves>(mode, batch, nblk, npix, part, yb, ny, zb, nz, out, wred);
+}
+
+// MSE partials and the finalisation in ONE launch (rgbac_finalize_fused): every block writes
+// its (se, cnt) partial, then draws a ticket; the block that draws the last one finalises.
+// Hand-off per cdna_hip_programming.md "In-launch split-K reduction": plain partial stores ->
+// vmcnt(0) -> barrier -> agent-scope release -> vmcnt(0) -> relaxed agent-scope ticket add; the
+// last arriver takes an agent-scope acquire before its plain loads of the partials, so the
+// result is right for any placement of the blocks over XCDs.  The ticket must be zero at entry
+// (the forward prologue zeroes it) and the last arriver sets it back to zero.
+template <typename T>
+__global__ void __launch_bounds__(256)
+mse_finalize_kernel(int mode, int cx, int HW, const float* __restrict__ x, const T* __restrict__ xh,
+                    long long ldh, const float* __restrict__ mask, double* __restrict__ part,
+                    float* __restrict__ xo, int vec, int batch, double npix,
+                    const double* __restrict__ yb, int ny, const double* __restrict__ zb, int nz,
+                    unsigned* __restrict__ ticket, float* __restrict__ out) {
+  __shared__ double red[4 * 5];                     // block sums, then the waves' finals
+  mse_block<T>(mode, cx, HW, x, xh, ldh, mask, part, xo, vec, red);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  unsigned* flag = reinterpret_cast<unsigned*>(red);
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned nb = gridDim.x * gridDim.y;
+    const unsigned old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned last = old == nb - 1;
+    if (last) {
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    flag[0] = last;
+  }
+  __syncthreads();
+  const bool last = flag[0] != 0;
+  __syncthreads();                                  // flag read before red is reused
+  if (!last) return;
+  finalize_body<4>(mode, batch, (int)gridDim.x, npix, part, yb, ny, zb, nz, out,
+                   reinterpret_cast<double (*)[5]>(red));
 }
 
 __global__ void round255_kernel(long long n, const float* __restrict__ in, float* __restrict__ out) {
@@ -285,14 +344,13 @@ __global__ void avgpool3s2_kernel(int batch, int H, int W, int Ho, int Wo,
 struct PyrOuts { float* p[4]; };
 
 template <int L>
-__global__ void __launch_bounds__(256) pyramid_kernel(int batch, int H, int W,
-                                                      const float* __restrict__ alpha,
-                                                      int round255, float* __restrict__ rounded,
-                                                      PyrOuts outs) {
+__device__ __forceinline__ void pyramid_tile(int blk, int batch, int H, int W,
+                                             const float* __restrict__ alpha, int round255,
+                                             float* __restrict__ rounded, const PyrOuts& outs,
+                                             float* pyr) {
   constexpr int TP = 32 >> L;                          // last-level tile: 16 / 8 / 4 / 2
   constexpr int N0 = (TP + 1) * (1 << L) - 1;          // level-0 region side (33 .. 47)
   constexpr int NL0 = (N0 * N0 + 255) / 256;           // level-0 elements per thread
-  extern __shared__ float pyr[];
   float* bufA = pyr;
   float* bufB = pyr + N0 * N0;
   int sh[L + 1], sw[L + 1];
@@ -300,7 +358,7 @@ __global__ void __launch_bounds__(256) pyramid_kernel(int batch, int H, int W,
 #pragma unroll
   for (int l = 1; l <= L; ++l) { sh[l] = (sh[l - 1] - 1) / 2 + 1; sw[l] = (sw[l - 1] - 1) / 2 + 1; }
   const int ntx = (sw[L] + TP - 1) / TP, nty = (sh[L] + TP - 1) / TP;
-  int t = blockIdx.x;
+  int t = blk;
   const int tx = t % ntx; t /= ntx;
   const int ty = t % nty;
   const int b = t / nty;
@@ -364,6 +422,15 @@ __global__ void __launch_bounds__(256) pyramid_kernel(int batch, int H, int W,
   }
 }
 
+template <int L>
+__global__ void __launch_bounds__(256) pyramid_kernel(int batch, int H, int W,
+                                                      const float* __restrict__ alpha,
+                                                      int round255, float* __restrict__ rounded,
+                                                      PyrOuts outs) {
+  extern __shared__ float pyr[];
+  pyramid_tile<L>(blockIdx.x, batch, H, W, alpha, round255, rounded, outs, pyr);
+}
+
 template <typename T>
 __global__ void nchw_to_nhwc_kernel(int batch, int C, int HW, const float* __restrict__ src,
                                     T* __restrict__ dst, long long ldc) {
@@ -395,12 +462,10 @@ __global__ void nhwc_to_nchw_kernel(int batch, int C, int HW, const T* __restric
 // coalesced over consecutive pixels, the row chunk goes out as one 16-byte store, and the
 // indices are 32-bit (the grid-stride form above divides 64-bit indices per element).
 template <typename T>
-__global__ void __launch_bounds__(256) nchw_to_nhwc_chunk_kernel(int n, int nck, int C, int HW,
-                                                                 const float* __restrict__ src,
-                                                                 T* __restrict__ dst, int ldc) {
+__device__ __forceinline__ void nchw_chunk(int i, int nck, int C, int HW,
+                                           const float* __restrict__ src, T* __restrict__ dst,
+                                           int ldc) {
   constexpr int E = Elem<T>::EPV;
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
   const int pix = i / nck, ck = i - (i / nck) * nck;
   const int b = pix / HW, p = pix - (pix / HW) * HW;
   float v[E];
@@ -418,6 +483,40 @@ __global__ void __launch_bounds__(256) nchw_to_nhwc_chunk_kernel(int n, int nck,
   } else {
     *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
   }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) nchw_to_nhwc_chunk_kernel(int n, int nck, int C, int HW,
+                                                                 const float* __restrict__ src,
+                                                                 T* __restrict__ dst, int ldc) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) nchw_chunk<T>(i, nck, C, HW, src, dst, ldc);
+}
+
+// The forward's prologue in ONE launch (rgbac_forward_prologue): three independent jobs that
+// each took a launch of their own at the head of the forward graph --
+//   blocks [0, npyr):  the decoder's mask pyramid (pyramid_tile, round(255 a) / 255 first),
+//   blocks [npyr, ..): the input's NCHW -> NHWC conversion (one 16-byte row chunk per thread),
+//                      and, grid-strided over the same blocks, the zero fill of the forward's
+//                      bits partials and its finalize ticket.
+// Every job writes exactly what its own kernel writes: the outputs are bit-identical.
+template <int L, typename T>
+__global__ void __launch_bounds__(256) prologue_kernel(int npyr, int batch, int H, int W,
+                                                       const float* __restrict__ alpha,
+                                                       int round255, float* __restrict__ rounded,
+                                                       PyrOuts outs, int n, int nck, int C,
+                                                       const float* __restrict__ src,
+                                                       T* __restrict__ dst, int ldc,
+                                                       double* __restrict__ zero, int nzero) {
+  extern __shared__ float pyr[];
+  if ((int)blockIdx.x < npyr) {
+    pyramid_tile<L>(blockIdx.x, batch, H, W, alpha, round255, rounded, outs, pyr);
+    return;
+  }
+  const int bx = (int)blockIdx.x - npyr, ncv = (int)gridDim.x - npyr;
+  for (int e = bx * 256 + threadIdx.x; e < nzero; e += ncv * 256) zero[e] = 0.0;
+  const int i = bx * 256 + threadIdx.x;
+  if (i < n) nchw_chunk<T>(i, nck, C, H * W, src, dst, ldc);
 }
 
 // One thread per pixel: its NHWC row read in 16-byte chunks, each channel written to its plane
@@ -546,6 +645,86 @@ extern "C" int rgbac_finalize_ex(int dtype, int mode, int batch, int cx, int h, 
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64 * kFinWaves), 0, st, mode, batch, nblk,
                      (double)batch * HW, scratch, ybits, ny, zbits, nz, out);
   return check_launch("finalize_kernel");
+}
+
+extern "C" int rgbac_finalize_fused(int dtype, int mode, int batch, int cx, int h, int w,
+                                    const float* x, const void* x_hat, int64_t ldh,
+                                    const float* mask, const double* ybits, int ny,
+                                    const double* zbits, int nz, double* scratch,
+                                    uint32_t* ticket, float* out, float* x_hat_nchw,
+                                    void* stream) {
+  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(mode == 0 || mode == 1, "mode");
+  RGBAC_REQUIRE(batch > 0 && cx > 0 && h > 0 && w > 0, "shape");
+  RGBAC_REQUIRE(x && x_hat && scratch && out && ybits && zbits && ticket, "null pointer");
+  RGBAC_REQUIRE(((uintptr_t)ticket % 4) == 0, "ticket alignment");
+  RGBAC_REQUIRE(mode == 1 || mask, "masked mse needs the mask");
+  RGBAC_REQUIRE(ldh >= cx, "ldh");
+  const int vec = cx <= 4 && ldh % 4 == 0 &&
+                  ((uintptr_t)x_hat % (dtype == RGBAC_F32 ? 16 : 8)) == 0;
+  const int HW = h * w;
+  const int nblk = rgbac_finalize_blocks(h, w);
+  const double npix = (double)batch * HW;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (dtype == RGBAC_F32)
+    hipLaunchKernelGGL(mse_finalize_kernel<float>, dim3(nblk, batch), dim3(256), 0, st, mode, cx,
+                       HW, x, (const float*)x_hat, ldh, mask, scratch, x_hat_nchw, vec, batch,
+                       npix, ybits, ny, zbits, nz, ticket, out);
+  else
+    hipLaunchKernelGGL(mse_finalize_kernel<bf16_t>, dim3(nblk, batch), dim3(256), 0, st, mode, cx,
+                       HW, x, (const bf16_t*)x_hat, ldh, mask, scratch, x_hat_nchw, vec, batch,
+                       npix, ybits, ny, zbits, nz, ticket, out);
+  return check_launch("mse_finalize_kernel");
+}
+
+extern "C" int rgbac_forward_prologue(int dtype, int batch, int c, int h, int w, const float* x,
+                                      void* xf, int64_t ldc, const float* alpha, int round255,
+                                      float* rounded, int levels, float* const* outs,
+                                      double* zero, int64_t nzero, void* stream) {
+  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
+  RGBAC_REQUIRE(batch > 0 && c > 0 && h > 0 && w > 0 && ldc >= c && x && xf && alpha, "shape");
+  RGBAC_REQUIRE(levels >= 1 && levels <= 4, "levels: 1..4");
+  RGBAC_REQUIRE(!round255 || rounded, "round255 needs an output buffer");
+  RGBAC_REQUIRE(nzero >= 0 && (nzero == 0 || zero) && nzero < (1ll << 30), "zero range");
+  for (int l = 0; l < levels; ++l) RGBAC_REQUIRE(outs && outs[l], "null pyramid output");
+  const int E = dtype == RGBAC_F32 ? 4 : 8;
+  const long long n = (long long)batch * h * w * ldc;
+  RGBAC_REQUIRE(ldc % E == 0 && ((uintptr_t)xf & 15) == 0 && n / E < (1ll << 31) - 256,
+                "the fused prologue needs 16-byte NHWC row chunks (ldc % 8 bf16 / % 4 f32)");
+  PyrOuts po{};
+  for (int l = 0; l < levels; ++l) po.p[l] = outs[l];
+  int hl = h, wl = w;
+  for (int l = 0; l < levels; ++l) { hl = (hl - 1) / 2 + 1; wl = (wl - 1) / 2 + 1; }
+  const int tp = 32 >> levels;
+  const long long npyr = (long long)batch * ((hl + tp - 1) / tp) * ((wl + tp - 1) / tp);
+  const int nck = (int)(ldc / E), nn = (int)(n / E);
+  const long long ncv = (nn + 255) / 256;
+  RGBAC_REQUIRE(npyr + ncv < (1ll << 31), "too many prologue blocks");
+  const int n0 = (tp + 1) * (1 << levels) - 1;
+  const size_t lds = (size_t)2 * n0 * n0 * sizeof(float);
+  const dim3 grid((unsigned)(npyr + ncv));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define PRO_LAUNCH(L_, T_)                                                                      \
+  hipLaunchKernelGGL((prologue_kernel<L_, T_>), grid, dim3(256), lds, st, (int)npyr, batch, h, w, \
+                     alpha, round255, rounded, po, nn, nck, c, x, (T_*)xf, (int)ldc, zero,      \
+                     (int)nzero)
+  if (dtype == RGBAC_F32) {
+    switch (levels) {
+      case 1: PRO_LAUNCH(1, float); break;
+      case 2: PRO_LAUNCH(2, float); break;
+      case 3: PRO_LAUNCH(3, float); break;
+      default: PRO_LAUNCH(4, float); break;
+    }
+  } else {
+    switch (levels) {
+      case 1: PRO_LAUNCH(1, bf16_t); break;
+      case 2: PRO_LAUNCH(2, bf16_t); break;
+      case 3: PRO_LAUNCH(3, bf16_t); break;
+      default: PRO_LAUNCH(4, bf16_t); break;
+    }
+  }
+#undef PRO_LAUNCH
+  return check_launch("prologue_kernel");
 }
 
 extern "C" int rgbac_mask_pyramid(int batch, int h, int w, const float* alpha, int round255,

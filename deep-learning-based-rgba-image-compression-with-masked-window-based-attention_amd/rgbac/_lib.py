@@ -113,6 +113,10 @@ SIGNATURES = {
     "rgbac_finalize_blocks": [_I32, _I32],
     "rgbac_finalize_ex": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP, _VP, _I32,
                           _VP, _I32, _VP, _VP, _VP, _VP],
+    "rgbac_finalize_fused": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP, _VP, _I32,
+                             _VP, _I32, _VP, _VP, _VP, _VP, _VP],
+    "rgbac_forward_prologue": [_I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP, _I32, _VP,
+                               _I32, _VP, _VP, _I64, _VP],
     "rgbac_mask_pyramid": [_I32, _I32, _I32, _VP, _I32, _VP, _I32, _VP, _VP],
     "rgbac_nchw_to_nhwc": [_I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP],
     "rgbac_nhwc_to_nchw": [_I32, _I32, _I32, _I32, _I32, _VP, _I64, _VP, _VP],

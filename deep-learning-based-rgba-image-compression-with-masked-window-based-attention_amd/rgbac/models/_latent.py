@@ -110,8 +110,15 @@ def _part_prepare(m, srcs, c0, c1, bias, **kw):
     return rt.prepare(pk[1], srcs, **kw)
 
 
-def latent_path(model, y, training=False, noise_z=None, noise_y=None, debug=None):
-    """y: Feat (B,h,w,M) -> (YH Feat, ybits fp64 partials, zbits fp64 partials)."""
+def ypart_slots(model, B, h, w):
+    """(slices, slots per slice) of latent_path's fp64 bits partials for a B x h x w latent."""
+    return model.num_slices, -(-(B * h * w) // 32)
+
+
+def latent_path(model, y, training=False, noise_z=None, noise_y=None, debug=None, ypart=None):
+    """y: Feat (B,h,w,M) -> (YH Feat, ybits fp64 partials, zbits fp64 partials).
+    ``ypart``: a zeroed fp64 (slices, slots) buffer (ypart_slots) for the bits partials, e.g.
+    zero-filled by the forward's prologue launch; allocated and zeroed here when None."""
     dev, dt = y.t.device, y.t.dtype
     ns, msup = model.num_slices, model.max_support_slices
     M = y.C
@@ -134,7 +141,9 @@ def latent_path(model, y, training=False, noise_z=None, noise_y=None, debug=None
     YH = rt.new_feat(B, h, w, M, dt, dev)
     # one fp64 bits partial per M block of the GAUSS conv (64-pixel LDS-ring tiles or
     # 32-pixel wave tiles); unused slots stay zero
-    ypart = torch.zeros((ns, -(-npix // 32)), dtype=torch.float64, device=dev)
+    if ypart is None:
+        ypart = torch.zeros(ypart_slots(model, B, h, w), dtype=torch.float64, device=dev)
+    assert tuple(ypart.shape) == ypart_slots(model, B, h, w) and ypart.dtype == torch.float64
     liks = [None] * ns
     musig = [None] * ns
     waves = [[i] for i in range(min(msup, ns))]

@@ -242,6 +242,25 @@ int rgbac_finalize_ex(int dtype, int mode, int batch, int cx, int h, int w,
                       const float* mask, const double* ybits, int ny,
                       const double* zbits, int nz, double* scratch, float* out,
                       float* x_hat_nchw, void* stream);
+/* rgbac_finalize_ex in ONE launch: the MSE blocks draw a ticket and the last one finalises
+ * (agent-scope release / acquire hand-off).  *ticket (uint32) must be 0 on entry; the last
+ * block sets it back to 0.  Same outputs as rgbac_finalize_ex (the bits partials are summed
+ * by 4 waves instead of 16: same values up to fp64 summation order). */
+int rgbac_finalize_fused(int dtype, int mode, int batch, int cx, int h, int w,
+                         const float* x, const void* x_hat, int64_t ldh,
+                         const float* mask, const double* ybits, int ny,
+                         const double* zbits, int nz, double* scratch,
+                         uint32_t* ticket, float* out, float* x_hat_nchw, void* stream);
+
+/* The forward's prologue in ONE launch (AutoEncoderRGB_Journal.py:209-217): the decoder mask
+ * pyramid of rgbac_mask_pyramid (levels 1..4), the input's rgbac_nchw_to_nhwc (x fp32 NCHW
+ * [B,c,H,W] -> xf NHWC, ldc a multiple of 8 bf16 / 4 f32, xf 16-byte aligned; alpha is
+ * [B,H,W] of the same B, H, W) and a zero fill of zero[0 .. nzero) doubles (the forward's
+ * bits partials and its rgbac_finalize_fused ticket).  Outputs identical to the three calls. */
+int rgbac_forward_prologue(int dtype, int batch, int c, int h, int w, const float* x,
+                           void* xf, int64_t ldc, const float* alpha, int round255,
+                           float* rounded, int levels, float* const* outs,
+                           double* zero, int64_t nzero, void* stream);
 
 /* SupplyMaskToTransform (layers/SupplyMask.py:11-18): ``levels`` successive
  * AvgPool2d(3, s2, p1, count_include_pad) of fp32 [B,H,W]; if round255, the
