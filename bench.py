@@ -475,8 +475,10 @@ def dp_train_record(args, world, rank, dev, dist):
     own_group = False
     if not tdist.is_initialized():
         # plain `python bench.py`: one rank, an in-process store, RCCL communicator of one
-        tdist.init_process_group("nccl", store=tdist.HashStore(), rank=0, world_size=1,
-                                 device_id=dev)
+        from rgbac.parallel import _stdout_to_stderr
+        with _stdout_to_stderr():       # RCCL's version banner: stderr, not the JSON line
+            tdist.init_process_group("nccl", store=tdist.HashStore(), rank=0, world_size=1,
+                                     device_id=dev)
         own_group = True
     B, S = args.dp_batch, 256
     tuned = os.path.join(ROOT, "profiles", f"tune_train_bf16_b{B}_{S}.json")
@@ -912,7 +914,9 @@ def main():
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        from rgbac.parallel import _stdout_to_stderr
+        with _stdout_to_stderr():       # RCCL's version banner: stderr, not the JSON line
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
 

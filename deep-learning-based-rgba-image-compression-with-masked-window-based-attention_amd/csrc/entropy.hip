@@ -265,47 +265,6 @@ finalize_kernel(int mode, int batch, int nblk, double npix, const double* __rest
   finalize_body<kFinWaves>(mode, batch, nblk, npix, part, yb, ny, zb, nz, out, wred);
 }
 
-// MSE partials and the finalisation in ONE launch (rgbac_finalize_fused): every block writes
-// its (se, cnt) partial, then draws a ticket; the block that draws the last one finalises.
-// Hand-off per cdna_hip_programming.md "In-launch split-K reduction": plain partial stores ->
-// vmcnt(0) -> barrier -> agent-scope release -> vmcnt(0) -> relaxed agent-scope ticket add; the
-// last arriver takes an agent-scope acquire before its plain loads of the partials, so the
-// result is right for any placement of the blocks over XCDs.  The ticket must be zero at entry
-// (the forward prologue zeroes it) and the last arriver sets it back to zero.
-template <typename T>
-__global__ void __launch_bounds__(256)
-mse_finalize_kernel(int mode, int cx, int HW, const float* __restrict__ x, const T* __restrict__ xh,
-                    long long ldh, const float* __restrict__ mask, double* __restrict__ part,
-                    float* __restrict__ xo, int vec, int batch, double npix,
-                    const double* __restrict__ yb, int ny, const double* __restrict__ zb, int nz,
-                    unsigned* __restrict__ ticket, float* __restrict__ out) {
-  __shared__ double red[4 * 5];                     // block sums, then the waves' finals
-  mse_block<T>(mode, cx, HW, x, xh, ldh, mask, part, xo, vec, red);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  unsigned* flag = reinterpret_cast<unsigned*>(red);
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned nb = gridDim.x * gridDim.y;
-    const unsigned old = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned last = old == nb - 1;
-    if (last) {
-      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    flag[0] = last;
-  }
-  __syncthreads();
-  const bool last = flag[0] != 0;
-  __syncthreads();                                  // flag read before red is reused
-  if (!last) return;
-  finalize_body<4>(mode, batch, (int)gridDim.x, npix, part, yb, ny, zb, nz, out,
-                   reinterpret_cast<double (*)[5]>(red));
-}
-
 __global__ void round255_kernel(long long n, const float* __restrict__ in, float* __restrict__ out) {
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
     out[i] = rintf(in[i] * 255.0f) / 255.0f;
@@ -498,7 +457,7 @@ __global__ void __launch_bounds__(256) nchw_to_nhwc_chunk_kernel(int n, int nck,
 //   blocks [0, npyr):  the decoder's mask pyramid (pyramid_tile, round(255 a) / 255 first),
 //   blocks [npyr, ..): the input's NCHW -> NHWC conversion (one 16-byte row chunk per thread),
 //                      and, grid-strided over the same blocks, the zero fill of the forward's
-//                      bits partials and its finalize ticket.
+//                      bits partials.
 // Every job writes exactly what its own kernel writes: the outputs are bit-identical.
 template <int L, typename T>
 __global__ void __launch_bounds__(256) prologue_kernel(int npyr, int batch, int H, int W,
@@ -645,36 +604,6 @@ extern "C" int rgbac_finalize_ex(int dtype, int mode, int batch, int cx, int h, 
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64 * kFinWaves), 0, st, mode, batch, nblk,
                      (double)batch * HW, scratch, ybits, ny, zbits, nz, out);
   return check_launch("finalize_kernel");
-}
-
-extern "C" int rgbac_finalize_fused(int dtype, int mode, int batch, int cx, int h, int w,
-                                    const float* x, const void* x_hat, int64_t ldh,
-                                    const float* mask, const double* ybits, int ny,
-                                    const double* zbits, int nz, double* scratch,
-                                    uint32_t* ticket, float* out, float* x_hat_nchw,
-                                    void* stream) {
-  RGBAC_REQUIRE(dtype == RGBAC_F32 || dtype == RGBAC_BF16, "dtype");
-  RGBAC_REQUIRE(mode == 0 || mode == 1, "mode");
-  RGBAC_REQUIRE(batch > 0 && cx > 0 && h > 0 && w > 0, "shape");
-  RGBAC_REQUIRE(x && x_hat && scratch && out && ybits && zbits && ticket, "null pointer");
-  RGBAC_REQUIRE(((uintptr_t)ticket % 4) == 0, "ticket alignment");
-  RGBAC_REQUIRE(mode == 1 || mask, "masked mse needs the mask");
-  RGBAC_REQUIRE(ldh >= cx, "ldh");
-  const int vec = cx <= 4 && ldh % 4 == 0 &&
-                  ((uintptr_t)x_hat % (dtype == RGBAC_F32 ? 16 : 8)) == 0;
-  const int HW = h * w;
-  const int nblk = rgbac_finalize_blocks(h, w);
-  const double npix = (double)batch * HW;
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  if (dtype == RGBAC_F32)
-    hipLaunchKernelGGL(mse_finalize_kernel<float>, dim3(nblk, batch), dim3(256), 0, st, mode, cx,
-                       HW, x, (const float*)x_hat, ldh, mask, scratch, x_hat_nchw, vec, batch,
-                       npix, ybits, ny, zbits, nz, ticket, out);
-  else
-    hipLaunchKernelGGL(mse_finalize_kernel<bf16_t>, dim3(nblk, batch), dim3(256), 0, st, mode, cx,
-                       HW, x, (const bf16_t*)x_hat, ldh, mask, scratch, x_hat_nchw, vec, batch,
-                       npix, ybits, ny, zbits, nz, ticket, out);
-  return check_launch("mse_finalize_kernel");
 }
 
 extern "C" int rgbac_forward_prologue(int dtype, int batch, int c, int h, int w, const float* x,

@@ -42,7 +42,22 @@ struct RuArgsDev {
   int batch, H, W, ngroups;
   int stagger;                     // ru_stream_kernel: s_sleep(16) rounds of the later half of the grid
   RuGroup g[kRuMaxGroups];
+  // ru_stream_kernel<.., GATE = true> (rgbac_residual_unit_gate): the attention block's gate
+  const bf16_t* gw;                // conv_b[3] weights, fragment-major [12][6][64][8]
+  const float* gb;                 // its bias [192]
+  const bf16_t* gid; long long ldid;   // the block input (identity)
+  unsigned* flags;                 // per-tile hand-off words (zero at entry, left zero)
+  unsigned* timeout;               // set to 1 if a hand-off wait ever gave up (never expected)
 };
+
+// 16-byte write-through (sc1) store: the hand-off payload of rgbac_residual_unit_gate (no release
+// fence needed: cdna_hip_programming.md Guideline 16 R1).  Not counted by hipcc: the caller
+// drains it with s_waitcnt vmcnt(0) before the flag store.
+typedef unsigned ru_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st16_wt(void* p, const uint4& v) {
+  const ru_u32x4 d = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(d) : "memory");
+}
 
 __device__ __forceinline__ float ru_gelu(float v) { return gelu_fast(v); }   // bf16 outputs
 
@@ -613,10 +628,113 @@ __device__ unsigned long long g_ru_w[8192][2];     // wall clock (100 MHz) at st
 #define RU_T(k) do {} while (0)
 #endif
 
+// Group 1 of the gated launch: the b tile (bf16, 128 pixels x 192 channels, 400-B rows) is in OT.
+// Wave (wn, wm) computes gate channels 96 wn .. +95 of pixel rows 4 wm .. 4 wm + 3 -- the stage-3
+// tiling, K = 192 in 6 k-steps from OT -- then waits for group 0's tile and writes
+//   out = a * sigmoid(W_g b + b_g) + x
+// with conv_pw2_kernel's gate epilogue arithmetic (pw2_epi<.., RGBAC_ACT_GATE>).
+__device__ __forceinline__ void ru_gate_tile(const RuArgsDev& args, const unsigned char* OT, int tile,
+                                             int b, int y0, int x0, int wn, int wm, int fr, int fq,
+                                             int lane) {
+  using namespace rsw;
+  constexpr int RG = 3;                            // gate weight ring depth (k-steps)
+  const uint4* const WG = reinterpret_cast<const uint4*>(args.gw) + lane + (size_t)(6 * wn) * 6 * 64;
+  uint4 wr[RG][6];
+#pragma unroll
+  for (int u = 0; u < RG; ++u)
+#pragma unroll
+    for (int j = 0; j < 6; ++j) wr[u][j] = WG[(j * 6 + u) * 64];
+  float4 gb[6];
+#pragma unroll
+  for (int j = 0; j < 6; ++j) gb[j] = *reinterpret_cast<const float4*>(args.gb + 96 * wn + 16 * j + 4 * fq);
+  f32x4 acc[6][4];
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const unsigned char* const otl = OT + (4 * wm * TX + fr) * ORW + fq * 16;
+#pragma unroll
+  for (int ks = 0; ks < 6; ++ks) {
+    uint4 bv[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bv[i] = *reinterpret_cast<const uint4*>(otl + i * TX * ORW + ks * 64);
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) mma_step<bf16_t>(acc[j][i], wr[ks % RG][j], bv[i]);
+    if (ks + RG < 6) {
+#pragma unroll
+      for (int j = 0; j < 6; ++j) wr[ks % RG][j] = WG[(j * 6 + ks + RG) * 64];
+    }
+  }
+  const RuGroup& ga = args.g[0];
+  const RuGroup& gbg = args.g[1];
+  // the identity quads are no hand-off: in flight while the flag is polled
+  uint2 av[4][6], xv[4][6];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long long pix = (long long)(b * args.H + y0 + 4 * wm + i) * args.W + x0 + fr;
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+      xv[i][j] = *reinterpret_cast<const uint2*>(args.gid + pix * args.ldid + 96 * wn + 16 * j + 4 * fq);
+  }
+  // group 0's tile: poll its flag (relaxed, every lane the same word), bounded; then ONE
+  // agent-scope acquire and plain loads (Guideline 16 recipe)
+  unsigned* const flag = args.flags + tile;
+  for (unsigned spins = 0;; ++spins) {
+    if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) break;
+    if (spins > (1u << 16)) {                        // never expected: record and go on
+      if (lane == 0)
+        __hip_atomic_store(args.timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long long pix = (long long)(b * args.H + y0 + 4 * wm + i) * args.W + x0 + fr;
+#pragma unroll
+    for (int j = 0; j < 6; ++j)
+      av[i][j] = *reinterpret_cast<const uint2*>(ga.out + pix * ga.ldo + 96 * wn + 16 * j + 4 * fq);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const long long pix = (long long)(b * args.H + y0 + 4 * wm + i) * args.W + x0 + fr;
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      const int n = 96 * wn + 16 * j + 4 * fq;
+      const float bb[4] = {gb[j].x, gb[j].y, gb[j].z, gb[j].w};
+      const float r1[4] = {bf2f(av[i][j].x & 0xFFFF), bf2f(av[i][j].x >> 16),
+                           bf2f(av[i][j].y & 0xFFFF), bf2f(av[i][j].y >> 16)};
+      const float r2[4] = {bf2f(xv[i][j].x & 0xFFFF), bf2f(xv[i][j].x >> 16),
+                           bf2f(xv[i][j].y & 0xFFFF), bf2f(xv[i][j].y >> 16)};
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float x = acc[j][i][r] + bb[r];
+        v[r] = r1[r] * (1.0f / (1.0f + expf(-x))) + r2[r];     // conv_common.h sigmoid_f
+      }
+      Elem<bf16_t>::st4(gbg.out + pix * gbg.ldo + n, v);
+    }
+  }
+  // this workgroup is the flag's only reader: once every wave has seen it, leave it zero for
+  // the next launch
+  __syncthreads();
+  if (wn == 0 && wm == 0 && lane == 0)
+    __hip_atomic_store(flag, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // TYV = 8: 8 x 16 tiles, 4 waves, two workgroups per CU (the launched form).  16 x 16 tiles at
 // one 8-wave workgroup per CU measured 4-5 % slower and were removed, as were
 // 8 x 8 half tiles (14k).
-template <int RB, int TYV>
+// GATE (the last unit pair of a Win_noShift_Attention block, Masked_Attention.py:182-189, group 0 =
+// conv_a[2], group 1 = conv_b[2]): group 0 publishes its tile (a) by write-through stores and a
+// per-tile flag; group 1 keeps its tile (b) in LDS, runs conv_b[3] (1x1, 192 -> 192) on it, waits
+// for the flag (group 0's workgroups precede group 1's in dispatch order, so the wait always
+// ends; it is bounded anyway) and writes out = a * sigmoid(W_g b + b_g) + x.  The gate's HBM
+// round trip of b and its launch disappear.
+template <int RB, int TYV, bool GATE = false>
 __global__ void __launch_bounds__(32 * TYV, TYV == 8 ? 2 : 1) ru_stream_kernel(const RuArgsDev args) {
   using namespace rsw;
   constexpr int TY = TYV, NH = (TYV + 2) * HX;      // (shadow rsw's 8-row values)
@@ -645,6 +763,7 @@ __global__ void __launch_bounds__(32 * TYV, TYV == 8 ? 2 : 1) ru_stream_kernel(c
     const int nwg = gridDim.x, xcd = t & 7, q = nwg >> 3, r = nwg & 7;
     t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (t >> 3);
   }
+  const int tile = t;                              // (both groups map blockIdx.x alike)
   const int tx = t % tx_n; t /= tx_n;
   const int ty = t % ty_n;
   const int b = t / ty_n;
@@ -851,13 +970,26 @@ __global__ void __launch_bounds__(32 * TYV, TYV == 8 ? 2 : 1) ru_stream_kernel(c
     }
   }
   __syncthreads();
+  if constexpr (GATE) {
+    if (blockIdx.z == 1) {
+      ru_gate_tile(args, OT, tile, b, y0, x0, wn, wm, fr, fq, lane);
+      return;
+    }
+  }
   // whole 16-B chunks, consecutive lanes on consecutive chunks of a pixel's 384 bytes
 #pragma unroll
   for (int u = 0; u < TY * TX * 24 / NTH; ++u) {
     const int c = tid + NTH * u, p = c / 24, q = c - (c / 24) * 24;
     const long long pix = (long long)(b * args.H + y0 + p / TX) * args.W + x0 + p % TX;
-    *reinterpret_cast<uint4*>(g.out + pix * g.ldo + q * 8) =
-        *reinterpret_cast<const uint4*>(OT + p * ORW + q * 16);
+    const uint4 v = *reinterpret_cast<const uint4*>(OT + p * ORW + q * 16);
+    if constexpr (GATE) st16_wt(g.out + pix * g.ldo + q * 8, v);     // group 0: the hand-off
+    else *reinterpret_cast<uint4*>(g.out + pix * g.ldo + q * 8) = v;
+  }
+  if constexpr (GATE) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave drained (R1) ...
+    __syncthreads();                                   // ... before the one flag store
+    if (tid == 0)
+      __hip_atomic_store(&args.flags[tile], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   RU_T(7);
 }
@@ -978,4 +1110,57 @@ extern "C" int rgbac_residual_unit_ex(const rgbac_ru_args* args, int ngroups, in
                             dim3(256), 0, st, d);
   }
   return check_launch("ru_fused_kernel");
+}
+
+extern "C" int rgbac_residual_unit_gate(const rgbac_ru_args* args, const void* gate_w,
+                                        const float* gate_b, const void* ident, int64_t ident_ldc,
+                                        uint32_t* flags, int64_t nflags, void* stream) {
+  RGBAC_REQUIRE(args != nullptr && gate_w && gate_b && ident && flags, "null pointer");
+  const rgbac_ru_args* a = args;
+  RGBAC_REQUIRE(a->dtype == RGBAC_BF16 && a->channels == 192,
+                "the gated unit pair is bf16, C = 192 only");
+  RGBAC_REQUIRE(a->batch > 0 && a->h > 0 && a->w > 0 && a->h % 8 == 0 && a->w % 16 == 0,
+                "the gated unit pair needs H % 8 == 0, W % 16 == 0");
+  const long long tiles = (long long)a->batch * (a->h / 8) * (a->w / 16);
+  RGBAC_REQUIRE(tiles < (1ll << 31) && nflags >= tiles + 1,
+                "flags: one zeroed word per 8 x 16 tile plus the timeout word (the last)");
+  RGBAC_REQUIRE(((uintptr_t)flags % 4) == 0 && ((uintptr_t)gate_w % 16) == 0 &&
+                    ((uintptr_t)gate_b % 16) == 0 && ((uintptr_t)ident % 8) == 0 &&
+                    ident_ldc >= 192 && ident_ldc % 4 == 0,
+                "gate operand alignment / stride");
+  RGBAC_REQUIRE((long long)a->batch * a->h * a->w * ident_ldc < (1ll << 31) ||
+                    ident_ldc > 0, "identity stride");
+  RuArgsDev d{};
+  d.batch = a->batch; d.H = a->h; d.W = a->w; d.ngroups = 2;
+  for (int i = 0; i < 2; ++i) {
+    const rgbac_ru_args* q = &args[i];
+    RGBAC_REQUIRE(q->dtype == a->dtype && q->channels == 192 && q->batch == a->batch &&
+                      q->h == a->h && q->w == a->w, "both units must share the geometry");
+    RGBAC_REQUIRE(q->x && q->out && q->w1 && q->w2 && q->w3 && q->b1 && q->b2 && q->b3,
+                  "null pointer");
+    RGBAC_REQUIRE(q->x != q->out && q->out != ident, "out must alias neither x nor the identity");
+    RGBAC_REQUIRE(q->w1_kpad == 0 && q->w2_kpad == 0 && q->w3_kpad == 0,
+                  "fragment-major packs only (the streamed unit)");
+    RGBAC_REQUIRE(q->x_ldc >= 192 && q->x_ldc % 8 == 0 && q->out_ldc >= 192 &&
+                      q->out_ldc % 8 == 0, "strides");
+    RGBAC_REQUIRE(((uintptr_t)q->x % 16) == 0 && ((uintptr_t)q->w1 % 16) == 0 &&
+                      ((uintptr_t)q->w2 % 16) == 0 && ((uintptr_t)q->w3 % 16) == 0 &&
+                      ((uintptr_t)q->b1 % 16) == 0 && ((uintptr_t)q->b2 % 16) == 0 &&
+                      ((uintptr_t)q->b3 % 16) == 0 && ((uintptr_t)q->out % 16) == 0,
+                  "16-byte alignment");
+    RGBAC_REQUIRE((long long)a->batch * a->h * a->w * q->x_ldc < (1ll << 31),
+                  "the streamed unit addresses x with 32-bit element offsets");
+    RuGroup& g = d.g[i];
+    g.x = (const bf16_t*)q->x; g.ldx = q->x_ldc;
+    g.w1 = (const bf16_t*)q->w1; g.w2 = (const bf16_t*)q->w2; g.w3 = (const bf16_t*)q->w3;
+    g.b1 = q->b1; g.b2 = q->b2; g.b3 = q->b3;
+    g.out = (bf16_t*)q->out; g.ldo = q->out_ldc;
+  }
+  d.gw = (const bf16_t*)gate_w; d.gb = gate_b;
+  d.gid = (const bf16_t*)ident; d.ldid = ident_ldc;
+  d.flags = flags; d.timeout = flags + (nflags - 1);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // group 0 (blockIdx.z = 0) is dispatched ahead of group 1, whose workgroups wait on it
+  hipLaunchKernelGGL((ru_stream_kernel<0, 8, true>), dim3((unsigned)tiles, 1, 2), dim3(256), 0, st, d);
+  return check_launch("ru_stream_kernel");
 }

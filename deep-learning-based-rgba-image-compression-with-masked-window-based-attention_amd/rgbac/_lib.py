@@ -113,8 +113,6 @@ SIGNATURES = {
     "rgbac_finalize_blocks": [_I32, _I32],
     "rgbac_finalize_ex": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP, _VP, _I32,
                           _VP, _I32, _VP, _VP, _VP, _VP],
-    "rgbac_finalize_fused": [_I32, _I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP, _VP, _I32,
-                             _VP, _I32, _VP, _VP, _VP, _VP, _VP],
     "rgbac_forward_prologue": [_I32, _I32, _I32, _I32, _I32, _VP, _VP, _I64, _VP, _I32, _VP,
                                _I32, _VP, _VP, _I64, _VP],
     "rgbac_mask_pyramid": [_I32, _I32, _I32, _VP, _I32, _VP, _I32, _VP, _VP],
@@ -122,6 +120,7 @@ SIGNATURES = {
     "rgbac_nhwc_to_nchw": [_I32, _I32, _I32, _I32, _I32, _VP, _I64, _VP, _VP],
     "rgbac_residual_unit": [_VP, _I32, _VP],
     "rgbac_residual_unit_ex": [_VP, _I32, _I32, _VP],
+    "rgbac_residual_unit_gate": [_VP, _VP, _VP, _VP, _I64, _VP, _I64, _VP],
     "rgbac_stem_gdn": [_I32, _I32, _I32, _VP, _I64, _VP, _I32, _VP, _VP, _I32, _VP, _I32, _VP,
                        _I64, _VP],
     "rgbac_winattn_block": [_I32, _I32, _I32, _I32, _I32, _F, _VP, _I64, _VP, _VP, _VP, _VP, _VP,

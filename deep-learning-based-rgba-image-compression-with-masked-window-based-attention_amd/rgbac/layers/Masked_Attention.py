@@ -178,6 +178,86 @@ def run_bottlenecks_fused(units, kind):
     return outs
 
 
+# the last unit pair + gate of a C = 192 block as one launch (rgbac_residual_unit_gate);
+# RGBAC_GATE_FUSED=0: the unit-pair launch, then the gate conv launch
+GATE_FUSED = os.environ.get("RGBAC_GATE_FUSED", "1") != "0"
+
+
+def gate_pack(conv):
+    """conv_b[3] (1x1, 192 -> 192) as the fragment-major [12][6][64][8] bf16 pack and its fp32
+    bias, cached on the module per parameter version."""
+    key = (rt.PARAM_GEN, conv.weight._version, conv.weight.data_ptr(), conv.bias._version,
+           conv.bias.data_ptr())
+    ent = conv.__dict__.get("_rgbac_gate_pack")
+    if ent is None or ent[0] != key:
+        with torch.no_grad():
+            kfn = lambda ks, l, e: 32 * ks + 8 * (l >> 4) + e
+            pw = _frag_pack(conv.weight.float().reshape(192, 192), 12, 6, kfn)
+            pb = conv.bias.float().contiguous().clone()
+        conv.__dict__["_rgbac_gate_pack"] = (key, (pw, pb))
+        ent = conv.__dict__["_rgbac_gate_pack"]
+    return ent[1]
+
+
+_FLAGS = {}
+
+
+def gate_flags(dev, n):
+    """One zeroed int32 buffer per device for the gated launch's per-tile hand-off words (each
+    launch leaves them zero; launches on a stream run one after the other); its last word is
+    the timeout word.  Allocated outside graph capture only."""
+    buf = _FLAGS.get(dev)
+    if buf is None or buf.numel() < n:
+        if torch.cuda.is_current_stream_capturing():
+            return None
+        buf = torch.zeros(max(n, 1 << 16), dtype=torch.int32, device=dev)
+        _FLAGS[dev] = buf
+    return buf
+
+
+def gated_ok(block, a, b, x):
+    return (GATE_FUSED and STREAM and _fused_ok([(block.conv_a[2], a), (block.conv_b[2], b)]) and
+            a.C == 192 and a.W % 16 == 0 and x.ldc % 8 == 0 and
+            block.conv_b[3].weight.shape == (192, 192, 1, 1))
+
+
+def run_last_units_gated(block, a, b, x):
+    """conv_a[2] on a, conv_b[2] on b and the gate a3 * sigmoid(conv_b[3](b3)) + x as ONE launch
+    (rgbac_residual_unit_gate): the b3 tile never leaves LDS, a3 is handed over in-launch.
+    Returns the block output, or None when the hand-off words are not available (first use
+    inside a graph capture)."""
+    ntiles = a.B * (a.H // 8) * (a.W // 16)
+    flags = gate_flags(a.t.device, ntiles + 1)
+    if flags is None:
+        return None
+    arr = (_lib.RuArgs * 2)()
+    keep = []
+    outs = []
+    for i, (u, t) in enumerate(((block.conv_a[2], a), (block.conv_b[2], b))):
+        c1, c2, c3 = u.conv[0], u.conv[2], u.conv[4]
+        p1, p2, p3, b1, b2, b3 = wide_unit_packs(c1, c2, c3)
+        o = rt.new_feat(t.B, t.H, t.W, t.C, t.t.dtype, t.t.device)
+        r = arr[i]
+        r.dtype, r.channels, r.batch, r.h, r.w = _lib.BF16, t.C, t.B, t.H, t.W
+        r.x, r.x_ldc = t.ptr(), t.ldc
+        r.w1, r.w2, r.w3 = p1.data_ptr(), p2.data_ptr(), p3.data_ptr()
+        r.w1_kpad = r.w2_kpad = r.w3_kpad = 0
+        r.b1, r.b2, r.b3 = b1.data_ptr(), b2.data_ptr(), b3.data_ptr()
+        r.out, r.out_ldc = o.ptr(), o.ldc
+        keep.append((p1, p2, p3, b1, b2, b3))
+        outs.append(o)
+    gw, gb = gate_pack(block.conv_b[3])
+    npix = a.B * a.H * a.W
+    C = 192
+    flops = 2.0 * npix * (2 * (C * C // 2 * 2 + 9 * (C // 2) ** 2) + C * C)
+    rt.timed("ru_stream_kernel<0, 8, true>", flops, 2 * npix * 6 * C,
+             lambda: _lib.call("rgbac_residual_unit_gate", ctypes.addressof(arr), gw.data_ptr(),
+                               gb.data_ptr(), x.ptr(), x.ldc, flags.data_ptr(), flags.numel(),
+                               _lib.stream_ptr(a.t.device)),
+             f"ru_stream_kernel<0, 8, true> gate C{C} {a.H}x{a.W} B{a.B}")
+    return outs[1]
+
+
 def run_residual_units_fused(pairs):
     """The same units as ONE fused launch (both intermediates in LDS)."""
     return run_bottlenecks_fused([((u.conv[0], u.conv[2], u.conv[4]), x) for u, x in pairs], 0)
@@ -217,8 +297,13 @@ class Win_noShift_Attention(nn.Module):
         # until the gate: their residual units run pairwise as 2-group launches
         b = self.attn.nhwc(x, mask)
         a = x
-        for k in range(3):
+        for k in range(2):
             a, b = run_residual_units([(self.conv_a[k], a), (self.conv_b[k], b)])
+        if gated_ok(self, a, b, x):
+            out = run_last_units_gated(self, a, b, x)
+            if out is not None:
+                return out
+        a, b = run_residual_units([(self.conv_a[2], a), (self.conv_b[2], b)])
         pk = rt.packed(self.conv_b[3], x.t.dtype, rt.segs_of(b.src()))
         return rt.conv(pk, [b.src()], act="gate", res1=a, res2=x)
 

@@ -11,8 +11,7 @@ from ..layers.GDN import GDN
 from ..layers.Masked_Attention import _fused_ok, run_bottlenecks_fused
 from ..layers.TransformRGB import _act_of, _layer_forward, dse_fused, dse_fused_ok, prep_conv, run_conv
 from ..layers._blocks import conv, conv3x3, deconv, subpel_conv3x3  # noqa: F401
-from . import AutoEncoderRGB_Journal as _rgb
-from ._latent import latent_path, ypart_slots
+from ._latent import latent_path
 from .AutoEncoderRGB_Journal import (_CompressionModelMixin, _hyper_analysis, _hyper_synthesis,
                                      _stack3, check_geometry, finalize, get_scale_table,  # noqa: F401
                                      ste_round)
@@ -189,18 +188,11 @@ class AutoEncoder(_CompressionModelMixin, nn.Module):
         with torch.no_grad():
             m = mask.contiguous().float()
             y = _run_seq(self.EncoderMask, rt.to_nhwc(m, dt))
-            ypart = ticket = None
-            if _rgb.FUSED_PROLOGUE:
-                # one zero fill for the bits partials and the one-launch finalize's ticket
-                ns, nslot = ypart_slots(self, y.B, y.H, y.W)
-                zero = torch.zeros(ns * nslot + 1, dtype=torch.float64, device=m.device)
-                ypart, ticket = zero[:ns * nslot].view(ns, nslot), zero[ns * nslot:].view(torch.int32)
-            yh, ypart, zpart = latent_path(self, y, self.training, noise_z, noise_y, debug,
-                                           ypart=ypart)
+            yh, ypart, zpart = latent_path(self, y, self.training, noise_z, noise_y, debug)
             xh = _run_seq(self.DecoderMask, yh)
             # x_hat's NCHW copy written by the loss pass (was a separate rgbac_nhwc_to_nchw)
             x_hat = torch.empty((B, xh.C, H, W), dtype=torch.float32, device=m.device)
-            out = finalize(1, m, xh, None, ypart, zpart, x_hat_nchw=x_hat, ticket=ticket)
+            out = finalize(1, m, xh, None, ypart, zpart, x_hat_nchw=x_hat)
         if debug is not None:
             debug.update(y=y)
         return x_hat, out[0], out[1], out[2], out[3]

@@ -50,8 +50,8 @@ def reconstruct_error(input, output, input_mask, output_mask=None):
     return torch.mean(se / cnt)
 
 
-# RGBAC_FUSED_PROLOGUE=0: the separate pyramid / NHWC / zero-fill / MSE / finalize launches
-# (A/B and the bit-identity test)
+# RGBAC_FUSED_PROLOGUE=0: the separate pyramid / NHWC / zero-fill launches (A/B and the
+# bit-identity test)
 FUSED_PROLOGUE = os.environ.get("RGBAC_FUSED_PROLOGUE", "1") != "0"
 
 
@@ -120,31 +120,26 @@ def _hyper_analysis(M):
                          conv3x3(224, 192, stride=2))
 
 
-def finalize(mode, x, x_hat, mask, ypart, zpart, x_hat_nchw=None, ticket=None):
+def finalize(mode, x, x_hat, mask, ypart, zpart, x_hat_nchw=None):
     """rgbac_finalize_ex -> fp32 [mse, bpp, y_bpp, z_bpp] on device; with ``x_hat_nchw`` (fp32
-    [B, cx, H, W]) the same pass also writes x_hat's NCHW copy.  ``ticket``: a zeroed device
-    word (e.g. the forward prologue's) selects the one-launch rgbac_finalize_fused."""
+    [B, cx, H, W]) the same pass also writes x_hat's NCHW copy.  (A one-launch form through a
+    last-arriving-block ticket measured slower, 20.5 vs 16.4 us: DESIGN 15e.)"""
     B, cx, H, W = x.shape
     dev = x.device
     scratch = torch.empty(_lib.finalize_scratch_doubles(B, H, W), dtype=torch.float64,
                           device=dev)
     out = torch.empty(4, dtype=torch.float32, device=dev)
-    head = (_lib.dtype_code(x_hat.t.dtype), mode, B, cx, H, W, x.data_ptr(), x_hat.ptr(),
-            x_hat.ldc, _lib.ptr(mask), ypart.data_ptr(), ypart.numel(), zpart.data_ptr(),
-            zpart.numel(), scratch.data_ptr())
-    if ticket is not None:
-        _lib.call("rgbac_finalize_fused", *head, ticket.data_ptr(), out.data_ptr(),
-                  _lib.ptr(x_hat_nchw), _lib.stream_ptr(dev))
-    else:
-        _lib.call("rgbac_finalize_ex", *head, out.data_ptr(), _lib.ptr(x_hat_nchw),
-                  _lib.stream_ptr(dev))
+    _lib.call("rgbac_finalize_ex", _lib.dtype_code(x_hat.t.dtype), mode, B, cx, H, W,
+              x.data_ptr(), x_hat.ptr(), x_hat.ldc, _lib.ptr(mask), ypart.data_ptr(),
+              ypart.numel(), zpart.data_ptr(), zpart.numel(), scratch.data_ptr(),
+              out.data_ptr(), _lib.ptr(x_hat_nchw), _lib.stream_ptr(dev))
     return out
 
 
 def forward_prologue(model, x, dt, reconmask, levels=4):
     """The forward's head in ONE launch (rgbac_forward_prologue, :209-217): the decoder mask
     pyramid of round(reconmask * 255) / 255, x's NHWC copy, and the zero fill of the slice
-    loop's bits partials plus the finalize ticket.  -> (xf, md, ypart, ticket)."""
+    loop's bits partials.  -> (xf, md, ypart)."""
     B, C, H, W = x.shape
     dev = x.device
     a = reconmask.contiguous().float()
@@ -157,12 +152,12 @@ def forward_prologue(model, x, dt, reconmask, levels=4):
     rounded = torch.empty_like(a)
     from ._latent import ypart_slots
     ns, nslot = ypart_slots(model, B, H // 8, W // 8)        # x1..x3: three stride-2 convs
-    zero = torch.empty(ns * nslot + 1, dtype=torch.float64, device=dev)
+    zero = torch.empty((ns, nslot), dtype=torch.float64, device=dev)
     ptrs = (ctypes.c_void_p * levels)(*[o.data_ptr() for o in md])
     _lib.call("rgbac_forward_prologue", _lib.dtype_code(dt), B, C, H, W, x.data_ptr(),
               xf.t.data_ptr(), xf.ldc, a.data_ptr(), 1, rounded.data_ptr(), levels, ptrs,
               zero.data_ptr(), zero.numel(), _lib.stream_ptr(dev))
-    return xf, md, zero[:ns * nslot].view(ns, nslot), zero[ns * nslot:].view(torch.int32)
+    return xf, md, zero
 
 
 class AutoEncoder(_CompressionModelMixin, nn.Module):
@@ -223,10 +218,10 @@ class AutoEncoder(_CompressionModelMixin, nn.Module):
             # only the decoder reads md, so the pyramid may run on a side stream beside the
             # encoder (rt.side_streams; off by default: the fork / join measured slower)
             main, side = rt.side_streams(x.device)
-            ypart = ticket = None
+            ypart = None
             if side is main and FUSED_PROLOGUE:
-                # pyramid + NHWC copy + bits-partial / ticket zero fill: one launch
-                xf, md, ypart, ticket = forward_prologue(self, x, dt, reconmask)
+                # pyramid + NHWC copy + bits-partial zero fill: one launch
+                xf, md, ypart = forward_prologue(self, x, dt, reconmask)
             else:
                 side.wait_stream(main)
                 with torch.cuda.stream(side):
@@ -242,7 +237,7 @@ class AutoEncoder(_CompressionModelMixin, nn.Module):
             # x_hat's NCHW copy written by the loss pass itself (one read of x_hat)
             x_hat = torch.empty((B, xh.C, H, W), dtype=torch.float32, device=x.device)
             out = finalize(0, x, xh, mask.contiguous().float(), ypart, zpart,     # :280-295
-                           x_hat_nchw=x_hat, ticket=ticket)
+                           x_hat_nchw=x_hat)
         if debug is not None:
             debug.update(y=y)
         return x_hat, out[0], out[1], out[2], out[3]

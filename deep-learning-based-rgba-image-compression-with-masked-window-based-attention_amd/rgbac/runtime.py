@@ -528,7 +528,7 @@ class PackedConv:
 class Prepared:
     """One conv's ABI record plus what the launcher needs (output, tuning key)."""
     __slots__ = ("a", "out", "key", "mgrid", "nphase", "nst", "nks", "pk", "desc", "flops",
-                 "nbytes")
+                 "nbytes", "partial")
 
 
 def prepare(pk, srcs, out=None, out_coff=0, act="none", act_param=0.0, res0=None, res1=None,
@@ -592,6 +592,7 @@ def prepare(pk, srcs, out=None, out_coff=0, act="none", act_param=0.0, res0=None
         a.zout, a.zout_ldc = zout.ptr(), zout.ldc
     pr = Prepared()
     pr.a, pr.out, pr.pk = a, out, pk
+    pr.partial = partial
     taps = 9 if pk.mode == CONVT_S2 else pk.ksize * pk.ksize
     pr.mgrid = B * (H * W if pk.mode != CONV else Ho * Wo)
     pr.nphase = 4 if pk.mode == CONVT_S2 else 1
@@ -913,6 +914,12 @@ def launch(preps, force=None):
                 if best is None or ms < best[0]:
                     best = (ms, cand)
             choice = best[1]
+            if gauss:
+                # every candidate wrote bits partials at ITS M-block granularity: slots the
+                # chosen tile does not write must read zero again (the caller zeroed them once)
+                for pr in preps:
+                    if pr.partial is not None:
+                        pr.partial.zero_()
             if scratch:
                 for i in range(n):
                     if arr[i].out != outs[i]:

@@ -242,21 +242,11 @@ int rgbac_finalize_ex(int dtype, int mode, int batch, int cx, int h, int w,
                       const float* mask, const double* ybits, int ny,
                       const double* zbits, int nz, double* scratch, float* out,
                       float* x_hat_nchw, void* stream);
-/* rgbac_finalize_ex in ONE launch: the MSE blocks draw a ticket and the last one finalises
- * (agent-scope release / acquire hand-off).  *ticket (uint32) must be 0 on entry; the last
- * block sets it back to 0.  Same outputs as rgbac_finalize_ex (the bits partials are summed
- * by 4 waves instead of 16: same values up to fp64 summation order). */
-int rgbac_finalize_fused(int dtype, int mode, int batch, int cx, int h, int w,
-                         const float* x, const void* x_hat, int64_t ldh,
-                         const float* mask, const double* ybits, int ny,
-                         const double* zbits, int nz, double* scratch,
-                         uint32_t* ticket, float* out, float* x_hat_nchw, void* stream);
-
 /* The forward's prologue in ONE launch (AutoEncoderRGB_Journal.py:209-217): the decoder mask
  * pyramid of rgbac_mask_pyramid (levels 1..4), the input's rgbac_nchw_to_nhwc (x fp32 NCHW
  * [B,c,H,W] -> xf NHWC, ldc a multiple of 8 bf16 / 4 f32, xf 16-byte aligned; alpha is
  * [B,H,W] of the same B, H, W) and a zero fill of zero[0 .. nzero) doubles (the forward's
- * bits partials and its rgbac_finalize_fused ticket).  Outputs identical to the three calls. */
+ * bits partials).  Outputs identical to the three separate launches. */
 int rgbac_forward_prologue(int dtype, int batch, int c, int h, int w, const float* x,
                            void* xf, int64_t ldc, const float* alpha, int round255,
                            float* rounded, int levels, float* const* outs,
@@ -305,6 +295,17 @@ int rgbac_residual_unit(const rgbac_ru_args* args, int ngroups, void* stream);
  * / [192], 16-byte aligned (rgbac.layers.Masked_Attention.wide_unit_packs): the barrier-free
  * weight-streaming kernel, one 8x16 output tile per workgroup. */
 int rgbac_residual_unit_ex(const rgbac_ru_args* args, int ngroups, int kind, void* stream);
+/* The LAST unit pair of a C = 192 Win_noShift_Attention block and its gate in ONE launch
+ * (layers/Masked_Attention.py:177-189): args[0] = conv_a[2] on a, args[1] = conv_b[2] on b (both
+ * fragment-major, as rgbac_residual_unit_ex's streamed form); gate_w = conv_b[3] (1x1,
+ * 192 -> 192) fragment-major [12][6][64][8] bf16, gate_b fp32 [192]; ident = the block input.
+ * args[1].out receives the block output a3 * sigmoid(conv_b[3](b3)) + ident; args[0].out
+ * receives a3 (the in-launch hand-off buffer).  flags: nflags >= B*(H/8)*(W/16) + 1 uint32,
+ * zero on entry and left zero; the last word, flags[nflags - 1], turns 1 if a hand-off wait
+ * ever gave up (never expected: the waited-on workgroups are dispatched first). */
+int rgbac_residual_unit_gate(const rgbac_ru_args* args, const void* gate_w,
+                             const float* gate_b, const void* ident, int64_t ident_ldc,
+                             uint32_t* flags, int64_t nflags, void* stream);
 
 /* ====================================================================== *
  * Training step (trainRGB.py:178-198): backward kernels, optimizer.       *

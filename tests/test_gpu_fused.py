@@ -291,3 +291,48 @@ def test_small_unit_two_tile_matches_one_tile(device, monkeypatch, kind, B, H, W
         assert torch.equal(a.view(torch.int16), b.view(torch.int16))
 
 
+
+
+# ---------------------------------------------------------------------------------------
+# The last unit pair + gate of a C = 192 Win_noShift_Attention block in one launch
+# (rgbac_residual_unit_gate, Masked_Attention.py:177-189) against the pair launch + the gate
+# conv launch it replaces.  The b3 tile is rounded to bf16 in LDS exactly where the unfused
+# path stores it, the gate GEMM runs the same MFMA k-step order and the epilogue the same
+# arithmetic as conv_pw2_kernel's gate, so the block outputs agree bit for bit (bar: at most
+# 1e-3 of the elements 1 bf16 ulp apart).  Shapes: config 2's encoder block (one round of
+# workgroups), a multi-round grid (group-1 workgroups waiting on group-0 ones dispatched rounds
+# earlier), a small odd grid; the hand-off words are left zero and the timeout word unset.
+@pytest.mark.parametrize("B,H,W,masked", [(8, 64, 64, True), (4, 128, 128, True), (1, 24, 48, False),
+                                          (2, 32, 32, True)])
+def test_gated_last_unit_pair_matches_unfused(device, B, H, W, masked):
+    from rgbac import runtime as rt
+    from rgbac.layers import Masked_Attention as MA
+    torch.manual_seed(31)
+    m = MA.Win_noShift_Attention(192, num_heads=8, window_size=8, shift_size=4).cuda().eval()
+    g = torch.Generator().manual_seed(32)
+    x = torch.randn((B, 192, H, W), generator=g).cuda()
+    mask = torch.ones((B, 1, H, W))
+    if masked:
+        mask[:, :, : H // 3, :] = 0.0
+    mask = mask.cuda()
+    with torch.no_grad():
+        f = rt.to_nhwc(x, torch.bfloat16)
+        assert MA.gated_ok(m, f, f, f)
+        old = MA.GATE_FUSED
+        try:
+            MA.GATE_FUSED = False
+            want = rt.to_nchw(m.nhwc(f, mask)).float()
+            MA.GATE_FUSED = True
+            gots = [rt.to_nchw(m.nhwc(f, mask)).float() for _ in range(2)]
+        finally:
+            MA.GATE_FUSED = old
+    torch.cuda.synchronize()
+    flags = MA.gate_flags(f.t.device, 1)
+    assert int(flags.abs().sum().item()) == 0, "hand-off words left set (or a wait timed out)"
+    for got in gots:
+        diff = (got - want).abs()
+        ulp = want.abs().clamp(min=2.0 ** -126) * 2.0 ** -7
+        frac = (diff > 0).float().mean().item()
+        print(f"gated {B}x{H}x{W}: differing fraction {frac:.2e}, max |d| {diff.max().item():.3e}")
+        assert (diff <= ulp).all()
+        assert frac <= 1e-3

@@ -1,12 +1,9 @@
-"""GPU: the forward's one-launch head and tail against the launches they replace.
+"""GPU: the forward's one-launch head against the launches it replaces.
 
 rgbac_forward_prologue (AutoEncoderRGB_Journal.py:209-217) = rgbac_mask_pyramid(round255) +
-rgbac_nchw_to_nhwc + a zero fill, bit for bit.  rgbac_finalize_fused (:280-295) =
-rgbac_finalize_ex in one launch through a last-arriving-block ticket: same per-image MSE
-partials, the scalars equal up to fp64 summation order (4 combining waves instead of 16),
-x_hat's NCHW copy bit-identical, and the ticket is back at zero after every launch (graph
-replays reuse it).  The whole bf16 forward with both is bit-identical in x_hat to the separate
-launches."""
+rgbac_nchw_to_nhwc + a zero fill, bit for bit.  The whole bf16 forward with it is bit-identical
+in x_hat to the separate launches, and its scalars agree (the bits partials are the same
+values: only who zeroes them changed)."""
 import ctypes
 
 import pytest
@@ -67,49 +64,11 @@ def test_prologue_rejects_unchunked_rows(device):
                   6, a.data_ptr(), 0, None, 1, ptrs, None, 0, _lib.stream_ptr(x.device))
 
 
-@pytest.mark.parametrize("mode,B,H,W", [(0, 8, 256, 256), (0, 1, 64, 64), (1, 3, 128, 96),
-                                        (0, 2, 1024, 512)])
-def test_finalize_fused_equals_two_launches(device, mode, B, H, W):
-    from rgbac import _lib
-    from rgbac import runtime as rt
-    g = torch.Generator().manual_seed(11)
-    cx = 3 if mode == 0 else 1
-    x = torch.rand((B, cx, H, W), generator=g).cuda()
-    xh = rt.to_nhwc((x + 0.05 * torch.randn((B, cx, H, W), generator=g).cuda()).clamp(0, 1),
-                    torch.bfloat16)
-    mask = _alpha(B, H, W, 12)[:, 0].contiguous() if mode == 0 else None
-    yb = torch.rand(10 * 77, generator=g, dtype=torch.float64).cuda() * 100
-    zb = torch.rand(5, generator=g, dtype=torch.float64).cuda() * 10
-    nd = _lib.finalize_scratch_doubles(B, H, W)
-
-    def run(fused, ticket=None):
-        scratch = torch.empty(nd, dtype=torch.float64, device="cuda")
-        out = torch.empty(4, dtype=torch.float32, device="cuda")
-        xo = torch.full((B, cx, H, W), float("nan"), device="cuda")
-        head = (_lib.BF16, mode, B, cx, H, W, x.data_ptr(), xh.ptr(), xh.ldc, _lib.ptr(mask),
-                yb.data_ptr(), yb.numel(), zb.data_ptr(), zb.numel(), scratch.data_ptr())
-        if fused:
-            _lib.call("rgbac_finalize_fused", *head, ticket.data_ptr(), out.data_ptr(),
-                      xo.data_ptr(), _lib.stream_ptr(x.device))
-        else:
-            _lib.call("rgbac_finalize_ex", *head, out.data_ptr(), xo.data_ptr(),
-                      _lib.stream_ptr(x.device))
-        torch.cuda.synchronize()
-        return out.cpu(), xo
-
-    want, want_xo = run(False)
-    ticket = torch.zeros(1, dtype=torch.int32, device="cuda")
-    for _ in range(3):                             # the last arriver resets the ticket
-        got, got_xo = run(True, ticket)
-        assert ticket.item() == 0
-        # same partials; the 4-wave combine adds them in another fixed fp64 order
-        torch.testing.assert_close(got, want, rtol=2e-7, atol=0.0)
-        assert torch.equal(got_xo, want_xo)
-
-
-def test_rgb_forward_fused_head_and_tail_bit_identical(device):
-    """bf16 forward at the bench's config-2 shape with the one-launch prologue / finalize vs
-    the separate launches: x_hat identical, the scalars equal to fp64-order rounding."""
+def test_rgb_forward_fused_head_bit_identical(device):
+    """bf16 forward at the bench's config-2 shape with the one-launch prologue vs the separate
+    launches: x_hat and the four scalars identical.  (The first forward of a shape tunes its
+    tiles live: the GAUSS launches' candidates write bits partials at their own granularity, so
+    the tuner re-zeroes them -- rgbac/runtime.py launch -- or the first bpp over-counts.)"""
     from bench import rgb_net, synth_inputs
     from rgbac.layers.SupplyMask import mask_pyramid
     from rgbac.models import AutoEncoderRGB_Journal as M
@@ -130,4 +89,4 @@ def test_rgb_forward_fused_head_and_tail_bit_identical(device):
     a, b = outs[False], outs[True]
     assert torch.equal(a[0], b[0])
     for i in (1, 2, 3, 4):
-        assert abs(a[i].item() - b[i].item()) <= 1e-6 * abs(a[i].item()), (i, a[i], b[i])
+        assert a[i].item() == b[i].item(), (i, a[i], b[i])
