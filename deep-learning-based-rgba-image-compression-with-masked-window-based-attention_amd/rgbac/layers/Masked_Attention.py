@@ -168,7 +168,7 @@ def run_bottlenecks_fused(units, kind):
         dual = (tiles > max(1, ncu // len(units)) and dual_env != "0") or dual_env == "2"
         kname = f"ru_small_kernel<{kind}, {2 if dual else 1}>"
     elif stream:
-        kname = f"ru_stream_kernel<{kind}, 8>"
+        kname = f"ru_stream_kernel<{kind}, 8, false>"     # (rocprofv3 name)
     else:
         kname = f"ru_fused_kernel<{C}, {C // 2}>"
     rt.timed(kname, flops, 2 * npix * len(units) * 2 * C,
