@@ -640,10 +640,18 @@ __global__ void __launch_bounds__(256) conv_splitk_epilogue(const ConvArgsDev ar
     const int n = 4 * q;
     if (n >= g.cout) continue;
     float v[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int sp = 0; sp < s.ksplit; ++sp) {
-      const float4 t = *reinterpret_cast<const float4*>(
-          g.ws + (((size_t)sp * s.nphase + ph) * s.M + m) * g.cout16 + n);
-      v[0] += t.x; v[1] += t.y; v[2] += t.z; v[3] += t.w;
+    // up to 8 slabs' loads in flight before the first add (the adds keep slab order: the
+    // sums are the one-load-at-a-time loop's, bit for bit)
+    const size_t slab = (size_t)s.nphase * s.M * g.cout16;
+    const float* wp = g.ws + ((size_t)ph * s.M + m) * g.cout16 + n;
+    for (int sp0 = 0; sp0 < s.ksplit; sp0 += 8) {
+      float4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (sp0 + u < s.ksplit) t[u] = *reinterpret_cast<const float4*>(wp + (sp0 + u) * slab);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (sp0 + u < s.ksplit) { v[0] += t[u].x; v[1] += t[u].y; v[2] += t[u].z; v[3] += t[u].w; }
     }
     epilogue4<T>(s, g, ph, m, n, v);
   }
@@ -1090,6 +1098,9 @@ constexpr int kFirstFPatchKS = 51; // 51..53: conv_fpatch_kernel<4, 64|128|192, 
 constexpr int kTilePW = 54;        // conv_pw_kernel (bf16 1x1, one source, cin/cout <= 192)
 constexpr int kTileNPatch = 55;    // conv_npatch_kernel (bf16 3x3 s1, cout <= 32, fragment-major)
 constexpr int kFirstFPatchKS2 = 56; // 56..58: conv_fpatch_kernel<8,64|8,128|16,32, ..., KS = 3>
+__host__ __device__ constexpr bool patch_tile(int t) {   // conv_patch_kernel tiles
+  return (t >= 36 && t <= 41) || t == 48 || t == 49;
+}
 __host__ __device__ constexpr bool fpatch_tile(int t) {
   return (t >= 42 && t <= 47) || (t >= 50 && t <= 53) || (t >= 56 && t <= 58);
 }
@@ -2320,6 +2331,11 @@ __global__ void __launch_bounds__(512) conv_patch_kernel(const ConvArgsDev args)
   const bool convt = s.mode == RGBAC_CONVT_S2;
   const bool s2 = s.mode == RGBAC_CONV && s.sy == 2;     // polyphase 5x5 stride-2 conv
   const int nph = (convt || s2) ? 4 : 1;
+  // phase split (grid z = 4, ksplit 4): this workgroup runs phase blockIdx.z only -- a convT
+  // phase writes its own output pixels; a strided-conv phase writes its fp32 partial slab,
+  // summed in phase order by conv_splitk_epilogue
+  const int pz = gridDim.z > 1 ? (int)blockIdx.z : -1;
+  const int ph0 = pz >= 0 ? pz : 0;
   const int in_h = s.in_h, in_w = s.in_w, cin_pad = g.cin_pad;
   const int nck = (cin_pad + 63) >> 6;
   const int send0 = g.send0, send1 = g.send1, send2 = g.send2;
@@ -2328,8 +2344,9 @@ __global__ void __launch_bounds__(512) conv_patch_kernel(const ConvArgsDev args)
   const char* const sp2 = reinterpret_cast<const char*>(g.sp2);
   const int sld0 = (int)g.sld0, sld1 = (int)g.sld1, sld2 = (int)g.sld2;
   // groups (phase, chunk); group sizes 9 (conv) or 9, 6, 6, 4 (convT phases)
-  const int ngroups = nph * nck;
-  const int ns = nph == 4 ? nck * 25 : nck * 9;
+  const int ntap0 = (3 - (ph0 >> 1)) * (3 - (ph0 & 1));   // taps of phase ph0 (9 when nph 1)
+  const int ngroups = pz >= 0 ? nck : nph * nck;
+  const int ns = pz >= 0 ? nck * ntap0 : (nph == 4 ? nck * 25 : nck * 9);
 
   // ---- per-lane DMA geometry (constant through the K loop)
   const int lrow = lane >> 3;
@@ -2398,10 +2415,11 @@ _Pragma("unroll")                                                               
   } while (0)
 
   // issue-side state: stage weight address, tap / chunk / phase counters, group index
-  int itap = 0, intap = 9, ick = 0, iph = 0, igrp = 0, itx = 0, itw = 3;
-  const char* wph = wbase;                        // current phase's packed weights
-  const char* wst = wbase;                        // current stage's weight column
+  int itap = 0, intap = ntap0, ick = 0, iph = ph0, igrp = 0, itx = 0, itw = 3 - (ph0 & 1);
   const int tapstep = cin_pad * 2;                // bytes from one tap's column to the next
+  // current phase's packed weights / current stage's weight column
+  const char* wph = convt ? wbase + ph0 * phstride : wbase;
+  const char* wst = s2 ? wbase + ((ph0 >> 1) * 5 + (ph0 & 1)) * tapstep : wph;
 
   // s2: the group's taps (ty, tx) are kernel taps (2 ty + qy, 2 tx + qx) of the plain 5x5
   // packing: +2 taps along a row, +10 - 2 (tw - 1) taps to the next row's first
@@ -2433,7 +2451,7 @@ _Pragma("unroll")                                                               
     }                                                                                         \
   } while (0)
 
-  PATCH_ISSUE(0, 0, 0);
+  PATCH_ISSUE(0, 0, ph0);
 #pragma unroll
   for (int st = 0; st < NBUF - 1; ++st)
     if (st < ns) STAGE_ISSUE(st);
@@ -2452,7 +2470,7 @@ _Pragma("unroll")                                                               
 #pragma unroll
   for (int i = 0; i < TM; ++i) bbase[i] = ((wm * TM + i) * PW + fr) * RSC + fq;
   // compute-side state: tap within the group, tap offset (uint4), group parity, phase
-  int ctap = 0, cntap = 9, ctx = 0, ctw = 3, cck = 0, cph = 0, cgrp = 0;
+  int ctap = 0, cntap = ntap0, ctx = 0, ctw = 3 - (ph0 & 1), cck = 0, cph = ph0, cgrp = 0;
   int toff = convt ? (2 * PW + 2) * RSC : 0;      // (oy * PW + ox) * RSC of the group's tap 0
 
   for (int it = 0; it < ns; ++it) {
@@ -2502,11 +2520,23 @@ _Pragma("unroll")                                                               
       toff = convt ? (2 * PW + 2) * RSC : 0;
       if (++cck == nck) {                         // end of a phase: epilogue (s2: the last)
         cck = 0;
-        if (!s2 || cph == 3) {
+        if (!s2 || cph == 3 || pz >= 0) {
           int nn[TN];
 #pragma unroll
           for (int j = 0; j < TN; ++j) nn[j] = n0 + wn * TN * 16 + j * 16 + fq * 4;
-          patch_epilogue<TN, TM, DACT>(s, g, s2 ? 0 : cph, b, y0 + wm * TM, x0, fr, nn, acc);
+          if (s2 && pz >= 0) {                      // the phase's fp32 partial slab
+#pragma unroll
+            for (int i = 0; i < TM; ++i) {
+              const int m = (b * s.Hm + y0 + wm * TM + i) * s.Wm + x0 + fr;
+#pragma unroll
+              for (int j = 0; j < TN; ++j)
+                if (nn[j] < g.cout)
+                  *reinterpret_cast<float4*>(g.ws + ((size_t)pz * s.M + m) * g.cout16 + nn[j]) =
+                      make_float4(acc[j][i][0], acc[j][i][1], acc[j][i][2], acc[j][i][3]);
+            }
+          } else {
+            patch_epilogue<TN, TM, DACT>(s, g, s2 ? 0 : cph, b, y0 + wm * TM, x0, fr, nn, acc);
+          }
 #pragma unroll
           for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -2790,8 +2820,9 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
   const bool inlaunch = s.ksplit > 1 && d.g[0].cnt != nullptr &&
                         (tile < kFirstWres || (tile >= kFirstDeep && tile < kFirstPers));
   if (part == 2) {                         // split-K reduce + epilogue kernels only
+    const bool patch_slabs = patch_tile(tile) && s.mode == RGBAC_CONV;   // strided-conv split
     if (s.ksplit == 1 || inlaunch || tile == kTileSpatial || tile == kTileSmallK ||
-        tile == kTileWStream || tile >= kFirstPatch ||
+        tile == kTileWStream || (tile >= kFirstPatch && !patch_slabs) ||
         (tile >= kFirstWres && tile < kFirstDeep))
       return RGBAC_OK;
     goto splitk_epilogue;
@@ -2976,7 +3007,8 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
     if constexpr (sizeof(T) == 2) {
       const int th = tc.bm / 16;
       const long long nsp = (long long)s.batch * (s.Hm / th) * (s.Wm / 16) * s.ngroups;
-      dim3 grid((unsigned)nsp, (unsigned)((max_cout + tc.bn - 1) / tc.bn), 1);
+      // ksplit 4: the phase split (grid z = the 5x5/s2 conv's / convT's four phases)
+      dim3 grid((unsigned)nsp, (unsigned)((max_cout + tc.bn - 1) / tc.bn), s.ksplit > 1 ? 4 : 1);
       // the folded activation backward (training input gradients) in instances of their own:
       // the forward instances keep the register allocation they were tuned with (the shared
       // epilogue code cost the 5x5/s2 patch kernels 37 % when compiled into them)
@@ -2997,7 +3029,9 @@ static int launch_conv(const ConvArgsDev& d, int tile, int max_cout, hipStream_t
         PATCH_LAUNCH(false)
       }
 #undef PATCH_LAUNCH
-      return check_launch("conv_patch_kernel");
+      const int rc = check_launch("conv_patch_kernel");
+      if (rc || s.ksplit == 1 || s.mode != RGBAC_CONV || part == 1) return rc;
+      goto splitk_epilogue;
     } else {
       set_error("the patch tiles are bf16 only");
       return RGBAC_E_ARG;
@@ -3077,7 +3111,9 @@ splitk_epilogue:
 int fill_group(const rgbac_conv_args* a, int ntaps_max, ConvGroup& g) {
   RGBAC_REQUIRE(a->nsrc >= 1 && a->nsrc <= 3, "nsrc must be 1..3");
   RGBAC_REQUIRE(a->weight && a->out, "null weight/out");
-  RGBAC_REQUIRE(a->ksplit == 1 || a->workspace, "split-K needs a workspace");
+  RGBAC_REQUIRE(a->ksplit == 1 || a->workspace ||
+                    (patch_tile(a->tile) && a->mode == RGBAC_CONVT_S2),   // (phase split)
+                "split-K needs a workspace");
   RGBAC_REQUIRE(a->cout > 0 && a->cout_pad % 128 == 0 && a->cout_pad >= a->cout,
                 "cout_pad (packed weight rows) must be a multiple of 128 and >= cout");
   RGBAC_REQUIRE(a->cin_pad % 8 == 0 && a->cin_pad > 0, "cin_pad must be a multiple of 8");
@@ -3281,7 +3317,11 @@ extern "C" int rgbac_conv2d_grouped_part(const rgbac_conv_args* args, int ngroup
                     "the spatial 3x3 tile needs one 32-channel source and cout <= 32");
   } else if (a->tile >= kFirstPatch) {
     const int th = kTiles[a->tile].bm / 16;
-    RGBAC_REQUIRE(a->dtype == RGBAC_BF16 && a->ksplit == 1 && !a->square_input &&
+    // ksplit 4 on conv_patch_kernel tiles: the phase split of the 5x5/s2 conv / convT
+    const bool psplit = a->ksplit == 4 && patch_tile(a->tile) &&
+                        (a->mode == RGBAC_CONVT_S2 ||
+                         (a->mode == RGBAC_CONV && a->ksize == 5 && a->stride == 2));
+    RGBAC_REQUIRE(a->dtype == RGBAC_BF16 && (a->ksplit == 1 || psplit) && !a->square_input &&
                       a->act != RGBAC_ACT_GAUSS &&
                       (a->mode == RGBAC_CONVT_S2 ||
                        (a->ksize == 3 && a->stride == 1 &&

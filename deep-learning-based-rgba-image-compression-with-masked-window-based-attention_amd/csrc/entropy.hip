@@ -139,6 +139,44 @@ __device__ __forceinline__ void mse_block(int mode, int cx, int HW, const float*
   // vec (cx <= 4, vector-aligned rows): the pixel's channels arrive in one vector load.
   const int b = blockIdx.y;
   double se = 0.0, cnt = 0.0;
+  if (vec) {
+    // the thread's (<= 4, rgbac_finalize_blocks) pixels: every load issued before the first
+    // use, then the same per-pixel, per-channel order as the loop below (bit-identical sums;
+    // the loop's dependent load -> add chain was ~3x the HBM time of the pass)
+    constexpr int U = 4;
+    const int stride = gridDim.x * 256;
+    for (int p0 = blockIdx.x * 256 + threadIdx.x; p0 < HW; p0 += U * stride) {
+      float mv[U], hq[U][4], xv[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int p = p0 + u * stride;
+        mv[u] = 0.0f;
+        if (p < HW) {
+          const long long pix = (long long)b * HW + p;
+          mv[u] = mode == 0 ? (mask[pix] > 0.0f ? 1.0f : 0.0f) : 1.0f;
+          Elem<T>::ld4(xh + pix * ldh, hq[u]);
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            xv[u][c] = c < cx ? x[((long long)b * cx + c) * HW + p] : 0.0f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int p = p0 + u * stride;
+        if (p >= HW) break;
+        const float m = mv[u];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          if (c >= cx) break;
+          const float hv = hq[u][c], xc = xv[u][c];
+          if (xo) xo[((long long)b * cx + c) * HW + p] = hv;
+          const float dlt = mode == 0 ? (xc * m - hv * m) : (hv - xc);
+          se += (double)(dlt * dlt);
+        }
+        cnt += (double)(m * cx);
+      }
+    }
+  } else
   for (int p = blockIdx.x * 256 + threadIdx.x; p < HW; p += gridDim.x * 256) {
     const long long pix = (long long)b * HW + p;
     float m = 1.0f;

@@ -143,6 +143,15 @@ FIRST_PATCH = 36         # 36..41: conv_patch_kernel (TH x 16 M-grid tile, BN ch
 PATCH_SIG = {36: (8, 192, 2, 4, 3), 37: (8, 128, 2, 4, 3), 38: (8, 96, 4, 2, 3),
              39: (8, 256, 2, 4, 3), 40: (8, 192, 2, 4, 4), 41: (8, 64, 4, 2, 3),
              48: (8, 64, 4, 2, 4), 49: (8, 128, 2, 4, 4)}
+
+
+def _patch_split_ok(preps):
+    """The phase split (ksplit 4 on a conv_patch_kernel tile, csrc/conv.hip): one workgroup
+    per (tile, phase) of the 5x5/s2 conv (fp32 phase slabs summed by the split-K epilogue) or
+    of the convT (each phase writes its own output pixels; no workspace)."""
+    a = preps[0].a
+    return (a.mode == CONVT_S2 or (a.mode == CONV and a.ksize == 5 and a.stride == 2)) and \
+        a.act not in (ACT["dgelu"], ACT["dlrelu"])
 FIRST_FPATCH = 42        # 42..47: conv_fpatch_kernel (fragment-major weight copy, 4 waves)
 FPATCH_SIG = {42: (8, 192), 43: (4, 192), 44: (8, 128), 45: (4, 128), 46: (8, 256), 47: (8, 64),
               50: (4, 64), 51: (4, 64), 52: (4, 128), 53: (4, 192),
@@ -252,6 +261,16 @@ def _patch_tiles(preps):
             if all(p.pk.cout_pad >= -(-p.pk.cout // bn) * bn for p in preps):
                 out.append(t)
     return out
+def _patch_cands(preps):
+    """(tile, ksplit) candidates of the patch tiles: every applicable tile unsplit, and the
+    conv_patch_kernel tiles with the phase split where it applies."""
+    ts = _patch_tiles(preps)
+    out = [(t, 1) for t in ts]
+    if _patch_split_ok(preps):
+        out += [(t, 4) for t in ts if t in PATCH_SIG]
+    return out
+
+
 SMALLK_MAX = 256
 KSPLITS = (1, 2, 4, 8)
 TUNE = os.environ.get("RGBAC_TUNE", "1") != "0"
@@ -847,7 +866,7 @@ def launch(preps, force=None):
             # the fragment-streamed tiles read the fragment-major weight copy
             arr[i].weight = (frag_weights(pr.pk).data_ptr() if t in FRAG_TILES
                              else pr.pk.w.data_ptr())
-            if ks > 1:
+            if ks > 1 and not (t in PATCH_SIG and pr.a.mode == CONVT_S2):   # (phase split)
                 ws = torch.empty(ks * pr.nphase * pr.mgrid * round_up(pr.pk.cout, 16),
                                  dtype=torch.float32, device=dev)
                 keep.append(ws)
@@ -874,7 +893,7 @@ def launch(preps, force=None):
             cands = _candidates(mtot, cout, nst, max(pr.nks for pr in preps),
                                 p0.pk.mode == CONV, _spatial_ok(preps), _smallk_ok(preps),
                                 _wstream_ok(preps))
-            cands += [(t, 1) for t in _patch_tiles(preps)]
+            cands += _patch_cands(preps)
             if _pw_ok(preps):
                 cands.append((TILE_PW, 1))
             if _npatch_ok(preps):
@@ -936,7 +955,9 @@ def launch(preps, force=None):
             choice = _heuristic(mtot, cout, nst)
         if not fixed:
             _tune_cache[key] = choice
-    if not gauss and not _choice_valid(choice[0], preps):
+    if not gauss and (not _choice_valid(choice[0], preps) or (
+            choice[1] > 1 and choice[0] in PATCH_SIG and
+            (choice[1] != 4 or not _patch_split_ok(preps)))):
         # a cached / forced tile the C side would refuse for THESE convs: the cache key
         # (dtype / mode / ksize / stride / shape / cin_pad / cout) does not hold the source
         # count, the residual operands, the activation or the pack type, so the same key

@@ -768,7 +768,7 @@ PATCH_CASES = [
 
 @pytest.mark.parametrize("mode,cin,cout,H,W", PATCH_CASES)
 def test_conv_patch_tiles(device, mode, cin, cout, H, W):
-    """conv_patch_kernel (tiles 36..41, 48, 49, bf16): ConvTranspose 5x5/s2 (four phases from
+    """conv_patch_kernel (tiles 36..41, 48, 49, unsplit and phase-split, bf16): ConvTranspose 5x5/s2 (four phases from
     one staged patch), 3x3 convs (incl. three concatenated sources and a partial last
     64-channel chunk), subpel convs and the polyphase 5x5 stride-2 conv (four input phases
     accumulated into one tile), with GELU / residual epilogues, against PyTorch fp32 on the
@@ -810,7 +810,10 @@ def test_conv_patch_tiles(device, mode, cin, cout, H, W):
             srcs = [rt.to_nhwc(xd, dt).src()]
         fr = rt.to_nhwc(r.to(device), dt)
         tiles = None
-        for force in [None] + sorted(set(rt.PATCH_SIG) | set(rt.FPATCH_SIG) | {rt.TILE_NPATCH}):
+        forces = [None] + [(t, 1) for t in sorted(set(rt.PATCH_SIG) | set(rt.FPATCH_SIG) |
+                                                  {rt.TILE_NPATCH})]
+        forces += [(t, 4) for t in sorted(rt.PATCH_SIG)]      # the phase split
+        for force in forces:
             if mode == "subpel":
                 pr = prep_subpel(m, srcs, act="gelu")
             elif mode == "convt_small":
@@ -822,14 +825,24 @@ def test_conv_patch_tiles(device, mode, cin, cout, H, W):
                 ok = ok + [rt.TILE_NPATCH]
             if tiles is None:
                 tiles = ok
-            if force is not None and force not in ok:
+            if force is not None and (force[0] not in ok or
+                                      (force[1] > 1 and not rt._patch_split_ok([pr]))):
                 continue
-            o = rt.launch([pr], force=None if force is None else (force, 1))[0]
+            o = rt.launch([pr], force=force)[0]
+            assert force is None or rt.LAST_CHOICE[0] == force
             outs[force] = rt.to_nchw(o).cpu()
     assert tiles, "no patch tile applies"
     for t, got in outs.items():
         assert got.shape == want.shape
         assert rel(got, want) < 1e-2, (t, rel(got, want))
+    # the convT phase split runs each phase's unchanged K loop: bit-identical to the unsplit
+    # tile; the strided conv's split sums four fp32 phase slabs (one bf16 rounding apart)
+    for t, got in outs.items():
+        if t is not None and t[1] == 4:
+            if mode == "convt":
+                assert torch.equal(got, outs[(t[0], 1)]), t
+            else:
+                assert rel(got, outs[(t[0], 1)]) < 1e-2, t
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
